@@ -1,0 +1,120 @@
+#!/usr/bin/env python3
+"""Headline benchmark: GPT-2 "124M" (small preset, 151.9M LLaMA-style params),
+seq_len 1024, micro-batch 8 x grad-accum 4 per GPU (the reference DDP CLI default,
+``ddp_trainer.py:497,523-527``), bf16, DDP over RCCL -- tokens/sec for the WHOLE job.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; N>1 is
+launched by torch.distributed.run (one rank per GPU).  W untimed warmup steps, then
+exactly K optimizer steps between barrier+synchronize brackets; the max elapsed time
+over ranks is used; rank 0 prints ONE JSON line.
+
+A "step" is one full optimizer step exactly as the trainer runs it: 4 micro-steps of
+forward+backward (dropout 0.1 on, like the reference config), gradient all-reduce,
+clip-by-global-norm and AdamW -- nothing skipped.  Data: synthetic random token ids
+(no datasets offline); weights: random init of the real architecture.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+BASELINE_TPS = {1: 12500.0, 2: 24100.0, 4: 46800.0}  # BASELINE.md (README.md:191-197 of the reference)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--model_size", default="small")
+    ap.add_argument("--batch_size", type=int, default=8)
+    ap.add_argument("--grad_accum", type=int, default=4)
+    ap.add_argument("--seq_len", type=int, default=1024)
+    ap.add_argument("--mode", default="ddp", choices=["ddp", "fsdp"])
+    ap.add_argument("--sharding", default="FULL_SHARD")
+    ap.add_argument("--no_ac", action="store_true", help="FSDP: disable activation checkpointing")
+    args = ap.parse_args()
+
+    from distributed_llm_trainer_amd.models.config import GPTConfig
+    cfg = GPTConfig.from_preset(args.model_size)
+    cfg.max_seq_len = args.seq_len
+    if args.mode == "ddp":
+        from distributed_llm_trainer_amd.training.configs import TrainingConfig
+        from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
+        tc = TrainingConfig(batch_size=args.batch_size, gradient_accumulation_steps=args.grad_accum,
+                            max_steps=100000, mixed_precision="bf16")
+        trainer = DistributedTrainer(cfg, tc)
+    else:
+        from distributed_llm_trainer_amd.training.configs import FSDPConfig, FSDPTrainingConfig
+        from distributed_llm_trainer_amd.training.fsdp_trainer import FSDPTrainer
+        tc = FSDPTrainingConfig(batch_size=args.batch_size, gradient_accumulation_steps=args.grad_accum,
+                                max_steps=100000)
+        fc = FSDPConfig(sharding_strategy=args.sharding, activation_checkpointing=not args.no_ac)
+        trainer = FSDPTrainer(cfg, tc, fc)
+    dev = trainer.device
+    world = trainer.world_size
+    if world != args.gpus and trainer.is_main_process:
+        print(f"[bench] warning: --gpus {args.gpus} but world size {world}", file=sys.stderr)
+    g = torch.Generator(device="cpu").manual_seed(1234 + trainer.rank)
+    B = args.batch_size * args.grad_accum
+    batches = [torch.randint(0, cfg.vocab_size, (B, args.seq_len), generator=g).to(dev) for _ in range(4)]
+
+    for i in range(args.warmup):
+        trainer.train_step({"input_ids": batches[i % 4]}, sync_loss=False)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        if trainer.distributed:
+            dist.barrier()
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    if dev.type == "cuda":
+        torch.cuda.reset_peak_memory_stats(dev)
+    sync()
+    t0 = time.perf_counter()
+    last = None
+    for i in range(args.steps):
+        last = trainer.train_step({"input_ids": batches[i % 4]}, sync_loss=False)
+    sync()
+    elapsed = time.perf_counter() - t0
+    loss = float(last["loss"]) if last is not None else float("nan")
+    peak = torch.cuda.max_memory_allocated(dev) / 1e9 if dev.type == "cuda" else 0.0
+    t = torch.tensor([elapsed, peak], dtype=torch.float64, device=dev if dev.type == "cuda" else "cpu")
+    if trainer.distributed:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, peak = float(t[0]), float(t[1])
+    tokens = args.steps * B * args.seq_len * world
+    tps = tokens / elapsed
+    if trainer.is_main_process:
+        base = BASELINE_TPS.get(world)
+        out = {
+            "metric": "tokens/sec", "value": round(tps, 1), "unit": "tokens/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 3),
+            "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": round(tps / base, 3) if base else None, "dtype": "bf16", "data": "synthetic",
+            "config": {"model": f"GPT-2 124M (gpt2_{args.model_size} preset, {cfg.num_parameters():,} params, "
+                                "LLaMA-style as in the reference)" if args.model_size == "small" else args.model_size,
+                       "global_batch": B * world, "seq_len": args.seq_len,
+                       "parallelism": f"{args.mode}{world}", "micro_batch": args.batch_size,
+                       "grad_accum": args.grad_accum},
+            "peak_gb_per_gpu": round(peak, 3), "final_loss": round(loss, 4),
+            "vs_baseline_linear": round(tps / (12500.0 * world), 3),
+        }
+        print(json.dumps(out), flush=True)
+    if trainer.distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,360 @@
+"""Hand-scheduled forward/backward executor for the GPT block stack.
+
+The reference runs the model through PyTorch autograd with dozens of small ATen
+kernels per layer (``gpt.py:388-455``; op list in SURVEY §2.5).  This engine instead
+issues a fixed schedule of fused HIP kernels + hipBLASLt GEMMs per layer and writes
+weight gradients straight into fp32 flat gradient buffers ("main grads"), which is
+what lets the DDP/FSDP runtimes in ``parallel/`` overlap RCCL collectives with the
+remaining backward at layer granularity (hooks below) instead of relying on
+autograd-hook bucketing.
+
+Per layer (M = B*S rows, residual stream kept in fp32 like the reference's DDP
+autocast path):
+
+  fwd:  x,n1   = add_dropout_rmsnorm(r, d_prev)        [fused kernel]
+        qkv    = n1 @ Wqkv^T                             [GEMM, N = 3H]
+        q,k,v  = rope_split(qkv)                         [fused kernel]
+        o,lse  = flash_attention(q,k,v; causal, dropout) [MFMA kernel]
+        a      = o @ Wo^T                                [GEMM]
+        x2,n2  = add_dropout_rmsnorm(x, a)               [fused kernel]
+        gu     = n2 @ Wgu^T                              [GEMM, N = 2I]
+        s      = silu(g) * u                             [fused kernel]
+        d      = s @ Wdown^T                             [GEMM]  -> (x2, d) to next layer
+  head: xf,nf  = add_dropout_rmsnorm(x2, d); logits = nf @ E^T; CE + dlogits in place.
+
+Dropout masks are pure functions of (seed, micro-step, layer, site, index)
+(``ops/rng.py``), so activation checkpointing just re-runs the layer forward.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, List, Optional
+
+import torch
+
+from ..ops import rng
+
+
+@dataclass
+class LayerWeights:
+    wqkv: torch.Tensor   # [3H, H] compute dtype (rows: q | k | v)
+    wo: torch.Tensor     # [H, H]
+    wgu: torch.Tensor    # [2I, H] (rows: gate | up)
+    wdown: torch.Tensor  # [H, I]
+    ln1: torch.Tensor    # [H]
+    ln2: torch.Tensor    # [H]
+
+
+@dataclass
+class LayerGrads:
+    wqkv: torch.Tensor   # fp32, accumulated in place
+    wo: torch.Tensor
+    wgu: torch.Tensor
+    wdown: torch.Tensor
+    ln1: torch.Tensor
+    ln2: torch.Tensor
+
+
+@dataclass
+class HeadWeights:
+    embed: torch.Tensor      # [V or Vp, H] gather table (fp32 master or gathered bf16)
+    lm_head: torch.Tensor    # [Vp, H] compute dtype, rows >= V are zero
+    norm: torch.Tensor       # [H]
+
+
+@dataclass
+class HeadGrads:
+    embed: torch.Tensor      # [Vp, H] fp32 (tied: lm_head wgrad + embedding scatter-add)
+    norm: torch.Tensor       # [H] fp32
+
+
+class ParamProvider:
+    """Interface the engine uses to fetch weights / gradient sinks and fire hooks.
+
+    Implemented by ``parallel.flat.FlatParamStore`` (single GPU / DDP) and by
+    ``parallel.fsdp.FSDPRuntime`` (sharded units).  Unit ids: ``"head"`` for the
+    root unit (embedding, tied lm_head, final norm) and ``0..L-1`` for blocks.
+    """
+
+    def layer(self, i: int) -> LayerWeights: ...
+    def layer_grads(self, i: int) -> LayerGrads: ...
+    def head(self) -> HeadWeights: ...
+    def head_grads(self) -> HeadGrads: ...
+
+    # hooks -- default no-ops
+    def pre_forward(self, unit) -> None: pass
+    def post_forward(self, unit) -> None: pass
+    def pre_backward(self, unit) -> None: pass
+    def post_backward(self, unit) -> None: pass
+
+
+def shift_targets(labels: torch.Tensor) -> torch.Tensor:
+    """labels [B,S] -> per-row targets [B*S]: labels[b, s+1], IGNORE at s = S-1.
+
+    Equivalent to the reference's ``logits[:, :-1]`` / ``labels[:, 1:]`` shift
+    (``gpt.py:451-453``) without materialising shifted logits.
+    """
+    B, S = labels.shape
+    t = torch.full((B, S), -100, dtype=torch.int64, device=labels.device)
+    t[:, :-1] = labels[:, 1:]
+    return t.reshape(-1)
+
+
+@dataclass
+class _LayerCache:
+    x: torch.Tensor
+    rstd1: Any = None
+    n1: Any = None
+    q: Any = None
+    k: Any = None
+    v: Any = None
+    o: Any = None
+    lse: Any = None
+    x2: Any = None
+    rstd2: Any = None
+    n2: Any = None
+    gu: Any = None
+    s: Any = None
+
+
+@dataclass
+class _StepState:
+    ids: torch.Tensor
+    B: int
+    S: int
+    micro: int
+    train: bool
+    recompute: bool
+    caches: List[_LayerCache] = field(default_factory=list)
+    xf: Any = None
+    rstdf: Any = None
+    nf: Any = None
+    dlogits: Any = None
+    d_last: Any = None  # bf16 d of last layer (input of final norm)
+
+
+class GPTEngine:
+    def __init__(self, cfg, provider: ParamProvider, ops, act_dtype=torch.bfloat16,
+                 seed: int = 1234, eps: float = 1e-6, gemm=None):
+        self.cfg = cfg
+        self.provider = provider
+        self.ops = ops
+        self.act_dtype = act_dtype
+        self.seed = int(seed) & 0xFFFFFFFF
+        self.eps = eps
+        self.micro_counter = 0
+        self.gemm = gemm or _TorchGemm()
+        self._rope = {}
+        # dropout probabilities (zeroed in eval mode)
+        self.p_attn = float(cfg.attention_dropout)
+        self.p_hidden = float(cfg.dropout)
+
+    # ---------------------------------------------------------------- helpers
+    def rope(self, S: int, device):
+        key = (S, str(device))
+        if key not in self._rope:
+            self._rope[key] = self.ops.rope_tables(self.cfg.head_dim, max(S, self.cfg.max_seq_len), device=device)
+        return self._rope[key]
+
+    def _keys(self, micro: int, layer: int):
+        return (rng.site_key(self.seed, micro, layer, rng.SITE_ATTN),
+                rng.site_key(self.seed, micro, layer, rng.SITE_RESID),
+                rng.site_key(self.seed, micro, layer, rng.SITE_MLP))
+
+    # ---------------------------------------------------------------- forward
+    def _layer_forward(self, st: _StepState, i: int, r, d, key_d: int, p_d: float,
+                       save: bool):
+        ops, gm, cfg = self.ops, self.gemm, self.cfg
+        B, S = st.B, st.S
+        w = self.provider.layer(i)
+        pa = self.p_attn if st.train else 0.0
+        ph = self.p_hidden if st.train else 0.0
+        k_attn, k_resid, k_mlp = self._keys(st.micro, i)
+        cos, sin = self.rope(S, r.device)
+
+        x, n1, rstd1 = ops.add_dropout_rmsnorm_fwd(r, d, w.ln1, self.eps, p_d, key_d, self.act_dtype)
+        qkv = gm.linear(n1, w.wqkv)
+        q, k, v = ops.rope_qkv_fwd(qkv, B, S, cfg.num_heads, cos, sin)
+        del qkv
+        o, lse = ops.attention_fwd(q, k, v, pa, k_attn, True)
+        a = gm.linear(o, w.wo)
+        x2, n2, rstd2 = ops.add_dropout_rmsnorm_fwd(x, a, w.ln2, self.eps, ph, k_resid, self.act_dtype)
+        del a
+        gu = gm.linear(n2, w.wgu)
+        s = ops.swiglu_fwd(gu)
+        d_out = gm.linear(s, w.wdown)
+        if save:
+            c = _LayerCache(x=x, rstd1=rstd1, n1=n1, q=q, k=k, v=v, o=o, lse=lse,
+                            x2=x2, rstd2=rstd2, n2=n2, gu=gu, s=s)
+        else:
+            c = _LayerCache(x=x) if st.recompute else None
+        return x2, d_out, c
+
+    def forward(self, ids: torch.Tensor, targets: Optional[torch.Tensor], train: bool,
+                recompute: bool = False, return_logits: bool = False,
+                need_backward: Optional[bool] = None):
+        """Returns (loss or None, logits or None, state for backward or None)."""
+        B, S = ids.shape
+        if need_backward is None:
+            need_backward = torch.is_grad_enabled()
+        need_bwd = bool(need_backward) and train and targets is not None
+        if train:
+            micro = self.micro_counter
+            self.micro_counter += 1
+        else:
+            micro = 0
+        st = _StepState(ids=ids, B=B, S=S, micro=micro, train=train, recompute=recompute)
+        prov = self.provider
+        ph = self.p_hidden if train else 0.0
+
+        prov.pre_forward("head")
+        hw = prov.head()
+        r = self.ops.embedding_fwd(ids, hw.embed)
+        d, key_d, p_d = None, 0, 0.0
+        for i in range(self.cfg.num_layers):
+            prov.pre_forward(i)
+            save = need_bwd and not recompute
+            r_new, d_new, c = self._layer_forward(st, i, r, d, key_d, p_d, save)
+            if need_bwd:
+                st.caches.append(c)
+            prov.post_forward(i)
+            r, d = r_new, d_new
+            key_d, p_d = self._keys(micro, i)[2], ph
+        hw = prov.head()
+        xf, nf, rstdf = self.ops.add_dropout_rmsnorm_fwd(r, d, hw.norm, self.eps, p_d, key_d, self.act_dtype)
+        st.d_last = None
+        loss, logits = None, None
+        V, Vp = self.cfg.vocab_size, hw.lm_head.shape[0]
+        if targets is not None:
+            lg = self.gemm.linear(nf, hw.lm_head)           # [M, Vp]
+            n_valid = (targets != -100).sum()
+            row_loss = self.ops.cross_entropy_fwd_bwd(lg, targets, V, n_valid)
+            loss = row_loss.sum() / n_valid.clamp(min=1).float()
+            if need_bwd:
+                st.dlogits = lg  # now holds d(mean loss)/d(logits), unscaled
+                st.xf, st.rstdf, st.nf = xf, rstdf, nf
+        if return_logits or targets is None:
+            lg2 = self.gemm.linear(nf, hw.lm_head)
+            logits = lg2[:, :V].reshape(B, S, V)
+        prov.post_forward("head")
+        return loss, logits, (st if need_bwd else None)
+
+    # --------------------------------------------------------------- backward
+    def backward(self, st: _StepState, dloss: torch.Tensor) -> None:
+        ops, gm, cfg, prov = self.ops, self.gemm, self.cfg, self.provider
+        B, S = st.B, st.S
+        L = cfg.num_layers
+        ph = self.p_hidden if st.train else 0.0
+        pa = self.p_attn if st.train else 0.0
+        dloss = dloss.reshape(()).float()
+
+        prov.pre_backward("head")
+        hw, hg = prov.head(), prov.head_grads()
+        # lm_head: dnf = dlogits @ E ; dE += dlogits^T @ (nf * dloss)
+        dnf = gm.linear_dgrad(st.dlogits, hw.lm_head)
+        nf_scaled = (st.nf.float() * dloss).to(st.nf.dtype)
+        gm.wgrad_acc(hg.embed, st.dlogits, nf_scaled)
+        st.dlogits = None
+        key_last = self._keys(st.micro, L - 1)[2]
+        g_x2, g_d = ops.rmsnorm_bwd(dnf, st.xf, st.rstdf, hw.norm, None, hg.norm,
+                                    ph, key_last, dy_scale=dloss, want_ddelta=True)
+        del dnf
+        cos, sin = self.rope(S, g_x2.device)
+
+        for i in reversed(range(L)):
+            prov.pre_backward(i)
+            c = st.caches[i]
+            if st.recompute:
+                # Re-run the layer forward from its saved fp32 input; masks replay exactly.
+                _, _, c = self._layer_forward(st, i, c.x, None, 0, 0.0, save=True)
+            w, gr = prov.layer(i), prov.layer_grads(i)
+            k_attn, k_resid, k_mlp = self._keys(st.micro, i)
+            # MLP
+            ds = gm.linear_dgrad(g_d, w.wdown)
+            gm.wgrad_acc(gr.wdown, g_d, c.s)
+            dgu = ops.swiglu_bwd(c.gu, ds)
+            del ds
+            dn2 = gm.linear_dgrad(dgu, w.wgu)
+            gm.wgrad_acc(gr.wgu, dgu, c.n2)
+            del dgu
+            dx2, da = ops.rmsnorm_bwd(dn2, c.x2, c.rstd2, w.ln2, g_x2, gr.ln2, ph, k_resid)
+            del dn2
+            # attention
+            do = gm.linear_dgrad(da, w.wo)
+            gm.wgrad_acc(gr.wo, da, c.o)
+            del da
+            dq, dk, dv = ops.attention_bwd(c.q, c.k, c.v, c.o, do, c.lse, pa, k_attn, True)
+            del do
+            dqkv = ops.rope_qkv_bwd(dq, dk, dv, cos, sin)
+            del dq, dk, dv
+            dn1 = gm.linear_dgrad(dqkv, w.wqkv)
+            gm.wgrad_acc(gr.wqkv, dqkv, c.n1)
+            del dqkv
+            key_prev = self._keys(st.micro, i - 1)[2] if i > 0 else 0
+            p_prev = ph if i > 0 else 0.0
+            g_x2, g_d = ops.rmsnorm_bwd(dn1, c.x, c.rstd1, w.ln1, dx2, gr.ln1, p_prev, key_prev,
+                                        want_ddelta=(i > 0))
+            del dn1, dx2
+            st.caches[i] = None
+            prov.post_backward(i)
+        # embedding (tied with lm_head): scatter-add
+        ops.embedding_bwd(st.ids, g_x2, hg.embed)
+        prov.post_backward("head")
+
+
+class _TorchGemm:
+    """Plain library GEMMs (hipBLASLt on ROCm via torch.matmul).
+
+    ``wgrad_acc`` accumulates bf16 x bf16 products straight into the fp32 main-grad
+    buffer with ``addmm(..., out_dtype=float32)`` when available (no bf16 round trip,
+    no separate add kernel); otherwise falls back to matmul + add_.
+    """
+
+    def __init__(self):
+        self._fp32_out_ok = None
+
+    @staticmethod
+    def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+        return torch.matmul(x, w.t())
+
+    @staticmethod
+    def linear_dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+        return torch.matmul(dy, w)
+
+    def wgrad_acc(self, dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
+        dw2 = dw.view(dy.shape[1], x.shape[1])
+        if dy.dtype == torch.float32:
+            dw2.addmm_(dy.t(), x)
+            return
+        if self._fp32_out_ok is not False and dy.is_cuda:
+            try:
+                torch.addmm(dw2, dy.t(), x, out_dtype=torch.float32, out=dw2)
+                self._fp32_out_ok = True
+                return
+            except (RuntimeError, TypeError):
+                self._fp32_out_ok = False
+        dw2.add_(torch.matmul(dy.t(), x))
+
+
+class EngineFunction(torch.autograd.Function):
+    """Autograd bridge: ``loss.backward()`` runs ``GPTEngine.backward``.
+
+    Weight gradients are written into the provider's fp32 gradient buffers directly
+    (the ``param.grad`` views); autograd only sees a dummy anchor input.
+    """
+
+    @staticmethod
+    def forward(ctx, anchor, engine, ids, targets, recompute):
+        loss, _, st = engine.forward(ids, targets, train=True, recompute=recompute,
+                                    need_backward=True)
+        ctx.engine = engine
+        ctx.state = st
+        return loss
+
+    @staticmethod
+    def backward(ctx, dloss):
+        if ctx.state is not None:
+            ctx.engine.backward(ctx.state, dloss)
+            ctx.state = None
+        return None, None, None, None, None

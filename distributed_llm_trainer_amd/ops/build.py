@@ -1,0 +1,81 @@
+"""In-tree build of the gfx950 HIP kernel library (no hipify, no torch JIT cache).
+
+Every ``ops/csrc/*.hip`` file is compiled with ``hipcc --offload-arch=gfx950`` into an
+object file and linked into ``ops/_dlt_kernels.so``, a plain C-ABI shared library
+loaded with ctypes (``ops/hip.py``).  Incremental: a source is rebuilt only when it
+or a header is newer than its object.  ``python -m distributed_llm_trainer_amd.ops.build``.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+BUILD = os.path.join(HERE, "_build")
+LIB = os.path.join(HERE, "_dlt_kernels.so")
+ARCH = os.environ.get("DLT_OFFLOAD_ARCH", "gfx950")
+
+CXXFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (ROCm required to build the MI355X kernels)")
+
+
+def _needs(src: str, obj: str, headers) -> bool:
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return os.path.getmtime(src) > t or any(os.path.getmtime(hh) > t for hh in headers)
+
+
+def _compile(src: str, obj: str, extra):
+    cmd = [hipcc(), *CXXFLAGS, *extra, "-I", CSRC, "-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {os.path.basename(src)}:\n{r.stderr[-6000:]}")
+    return obj
+
+
+def build(verbose: bool = True, jobs: int = 0, extra=()) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    headers = glob.glob(os.path.join(CSRC, "*.h"))
+    objs, todo = [], []
+    for s in srcs:
+        o = os.path.join(BUILD, os.path.basename(s)[:-4] + ".o")
+        objs.append(o)
+        if _needs(s, o, headers):
+            todo.append((s, o))
+    if todo:
+        jobs = jobs or min(len(todo), max(1, min(8, (os.cpu_count() or 2))))
+        if verbose:
+            print(f"[dlt-build] compiling {len(todo)} HIP sources for {ARCH} (-j{jobs})", flush=True)
+        with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+            futs = [ex.submit(_compile, s, o, list(extra)) for s, o in todo]
+            for f in futs:
+                f.result()
+    relink = not os.path.exists(LIB) or any(os.path.getmtime(o) > os.path.getmtime(LIB) for o in objs)
+    if relink:
+        tmp = LIB + ".tmp"
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
+        os.replace(tmp, LIB)
+        if verbose:
+            print(f"[dlt-build] linked {LIB}", flush=True)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(verbose=True)
+    sys.exit(0)

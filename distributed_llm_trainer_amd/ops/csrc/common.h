@@ -1,0 +1,57 @@
+// Shared device helpers for the gfx950 (MI355X / CDNA4) kernels of this framework.
+//
+// Conventions
+//  * wave = 64 lanes; every block size is a multiple of 64.
+//  * bf16 tensors are handled as raw 16-bit words and moved in 16-byte vectors
+//    (8 x bf16 per lane) -- hipcc does not vectorise scalar bf16 loads.
+//  * f32 -> bf16 uses the compiler cast (v_cvt_pk_bf16_f32, RNE, NaN-preserving).
+//  * Dropout randomness: lowbias32 hash of (key ^ pair_index); one hash gives 16
+//    bits to each of two neighbouring elements (see ops/rng.py for the contract).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DLT_API extern "C" __attribute__((visibility("default")))
+
+typedef uint16_t bf16_t;
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float floatx4_t __attribute__((ext_vector_type(4)));
+typedef float floatx16_t __attribute__((ext_vector_type(16)));
+typedef short shortx4_t __attribute__((ext_vector_type(4)));
+
+struct alignas(16) u16x8 { uint16_t v[8]; };
+struct alignas(8) u16x4 { uint16_t v[4]; };
+
+__device__ __forceinline__ float bf2f(uint16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, b);
+}
+
+__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+// 16 random bits for flat element index `idx` under `key`.
+__device__ __forceinline__ uint32_t drop_bits(uint32_t key, uint64_t idx) {
+  uint32_t h = lowbias32(key ^ (uint32_t)(idx >> 1));
+  return (idx & 1) ? (h >> 16) : (h & 0xffffu);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+#define DLT_CHECK_LAUNCH() return (int)hipGetLastError()

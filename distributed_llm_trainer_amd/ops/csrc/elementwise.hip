@@ -1,0 +1,233 @@
+// Memory-bound fused elementwise kernels: embedding gather / scatter-add,
+// RoPE + QKV head split (fwd/bwd), SwiGLU (fwd/bwd).  All move 8-16 B per lane.
+//
+// Reference ops replaced: K1 embedding (gpt.py:438), K4 RoPE
+// (gpt.py:144-147,195-196) together with the view/transpose of gpt.py:190-192,
+// K8 silu*mul (gpt.py:280).
+#include "common.h"
+
+// ---------------------------------------------------------------- embedding
+// out[m, :] = float(W[ids[m], :]); W is fp32 (wdt=0) or bf16 (wdt=1).
+__global__ __launch_bounds__(256) void k_embedding_fwd(const int64_t* __restrict__ ids, const void* __restrict__ W,
+                                                       int wdt, float* __restrict__ out, int M, int H) {
+  const int q = H >> 2;  // float4 per row
+  const size_t total = (size_t)M * q;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int m = (int)(i / q);
+    const int c = (int)(i % q);
+    const int64_t id = ids[m];
+    float4 v;
+    if (wdt == 0) {
+      v = *(reinterpret_cast<const float4*>(W) + (size_t)id * q + c);
+    } else {
+      const u16x4 b = *(reinterpret_cast<const u16x4*>(W) + (size_t)id * q + c);
+      v = make_float4(bf2f(b.v[0]), bf2f(b.v[1]), bf2f(b.v[2]), bf2f(b.v[3]));
+    }
+    *(reinterpret_cast<float4*>(out) + i) = v;
+  }
+}
+
+// dW[ids[m], :] += dout[m, :]   (one 256-B contiguous atomic wave-instruction per 64 lanes)
+__global__ __launch_bounds__(256) void k_embedding_bwd(const int64_t* __restrict__ ids, const float* __restrict__ dout,
+                                                       float* __restrict__ dW, int M, int H) {
+  const size_t total = (size_t)M * H;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int m = (int)(i / H);
+    const int h = (int)(i % H);
+    unsafeAtomicAdd(dW + (size_t)ids[m] * H + h, dout[i]);
+  }
+}
+
+DLT_API int dlt_embedding_fwd(const int64_t* ids, const void* W, int wdt, float* out, int M, int H, hipStream_t s) {
+  if (H % 4) return -1;
+  const size_t total = (size_t)M * (H / 4);
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  k_embedding_fwd<<<blocks, 256, 0, s>>>(ids, W, wdt, out, M, H);
+  DLT_CHECK_LAUNCH();
+}
+
+DLT_API int dlt_embedding_bwd(const int64_t* ids, const float* dout, float* dW, int M, int H, hipStream_t s) {
+  const size_t total = (size_t)M * H;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  k_embedding_bwd<<<blocks, 256, 0, s>>>(ids, dout, dW, M, H);
+  DLT_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------- RoPE
+// qkv [B*S, 3, nh, hd] (bf16) -> q, k, v [B, nh, S, hd]; q, k rotated (NeoX half split)
+// in fp32 with cos/sin tables [S, hd/2].  One thread = 4 rotary pairs of one head.
+__global__ __launch_bounds__(256) void k_rope_qkv_fwd(const bf16_t* __restrict__ qkv, const float* __restrict__ cosT,
+                                                      const float* __restrict__ sinT, bf16_t* __restrict__ q,
+                                                      bf16_t* __restrict__ k, bf16_t* __restrict__ v,
+                                                      int B, int S, int nh, int hd) {
+  const int half = hd >> 1;
+  const int per_head = half >> 2;  // threads per head-section
+  const size_t total = (size_t)B * S * 3 * nh * per_head;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int j4 = (int)(i % per_head);
+    size_t r = i / per_head;
+    const int h = (int)(r % nh);
+    r /= nh;
+    const int sec = (int)(r % 3);
+    const size_t m = r / 3;
+    const int s = (int)(m % S);
+    const int b = (int)(m / S);
+    const int j = j4 * 4;
+    const bf16_t* src = qkv + m * (size_t)(3 * nh * hd) + (size_t)sec * nh * hd + (size_t)h * hd;
+    const u16x4 a = *reinterpret_cast<const u16x4*>(src + j);
+    const u16x4 c = *reinterpret_cast<const u16x4*>(src + half + j);
+    bf16_t* dstbase = (sec == 0 ? q : (sec == 1 ? k : v)) + (((size_t)b * nh + h) * S + s) * hd;
+    u16x4 o1, o2;
+    if (sec == 2) {
+      o1 = a; o2 = c;
+    } else {
+      const float4 cs = *reinterpret_cast<const float4*>(cosT + (size_t)s * half + j);
+      const float4 sn = *reinterpret_cast<const float4*>(sinT + (size_t)s * half + j);
+      const float cc[4] = {cs.x, cs.y, cs.z, cs.w};
+      const float ss[4] = {sn.x, sn.y, sn.z, sn.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float x1 = bf2f(a.v[e]), x2 = bf2f(c.v[e]);
+        o1.v[e] = f2bf(x1 * cc[e] - x2 * ss[e]);
+        o2.v[e] = f2bf(x2 * cc[e] + x1 * ss[e]);
+      }
+    }
+    *reinterpret_cast<u16x4*>(dstbase + j) = o1;
+    *reinterpret_cast<u16x4*>(dstbase + half + j) = o2;
+  }
+}
+
+// dq, dk, dv [B, nh, S, hd] -> dqkv [B*S, 3*nh*hd] (inverse rotation for dq, dk).
+// dq may be fp32 (dqf != nullptr, produced by the attention dQ kernel) or bf16.
+__global__ __launch_bounds__(256) void k_rope_qkv_bwd(const bf16_t* __restrict__ dq, const float* __restrict__ dqf,
+                                                      const bf16_t* __restrict__ dk, const bf16_t* __restrict__ dv,
+                                                      const float* __restrict__ cosT, const float* __restrict__ sinT,
+                                                      bf16_t* __restrict__ dqkv, int B, int S, int nh, int hd) {
+  const int half = hd >> 1;
+  const int per_head = half >> 2;
+  const size_t total = (size_t)B * S * 3 * nh * per_head;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int j4 = (int)(i % per_head);
+    size_t r = i / per_head;
+    const int h = (int)(r % nh);
+    r /= nh;
+    const int sec = (int)(r % 3);
+    const size_t m = r / 3;
+    const int s = (int)(m % S);
+    const int b = (int)(m / S);
+    const int j = j4 * 4;
+    const size_t soff = (((size_t)b * nh + h) * S + s) * hd;
+    float g1[4], g2[4];
+    if (sec == 0 && dqf) {
+      const float4 a = *reinterpret_cast<const float4*>(dqf + soff + j);
+      const float4 c = *reinterpret_cast<const float4*>(dqf + soff + half + j);
+      g1[0] = a.x; g1[1] = a.y; g1[2] = a.z; g1[3] = a.w;
+      g2[0] = c.x; g2[1] = c.y; g2[2] = c.z; g2[3] = c.w;
+    } else {
+      const bf16_t* src = (sec == 0 ? dq : (sec == 1 ? dk : dv)) + soff;
+      const u16x4 a = *reinterpret_cast<const u16x4*>(src + j);
+      const u16x4 c = *reinterpret_cast<const u16x4*>(src + half + j);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { g1[e] = bf2f(a.v[e]); g2[e] = bf2f(c.v[e]); }
+    }
+    u16x4 o1, o2;
+    if (sec == 2) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { o1.v[e] = f2bf(g1[e]); o2.v[e] = f2bf(g2[e]); }
+    } else {
+      const float4 cs = *reinterpret_cast<const float4*>(cosT + (size_t)s * half + j);
+      const float4 sn = *reinterpret_cast<const float4*>(sinT + (size_t)s * half + j);
+      const float cc[4] = {cs.x, cs.y, cs.z, cs.w};
+      const float ss[4] = {sn.x, sn.y, sn.z, sn.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o1.v[e] = f2bf(g1[e] * cc[e] + g2[e] * ss[e]);
+        o2.v[e] = f2bf(g2[e] * cc[e] - g1[e] * ss[e]);
+      }
+    }
+    bf16_t* dst = dqkv + m * (size_t)(3 * nh * hd) + (size_t)sec * nh * hd + (size_t)h * hd;
+    *reinterpret_cast<u16x4*>(dst + j) = o1;
+    *reinterpret_cast<u16x4*>(dst + half + j) = o2;
+  }
+}
+
+static inline int ew_blocks(size_t total) {
+  size_t b = (total + 255) / 256;
+  return (int)(b > 16384 ? 16384 : (b == 0 ? 1 : b));
+}
+
+DLT_API int dlt_rope_qkv_fwd(const bf16_t* qkv, const float* cosT, const float* sinT, bf16_t* q, bf16_t* k,
+                             bf16_t* v, int B, int S, int nh, int hd, hipStream_t st) {
+  if (hd % 8) return -1;
+  const size_t total = (size_t)B * S * 3 * nh * (hd / 8);
+  k_rope_qkv_fwd<<<ew_blocks(total), 256, 0, st>>>(qkv, cosT, sinT, q, k, v, B, S, nh, hd);
+  DLT_CHECK_LAUNCH();
+}
+
+DLT_API int dlt_rope_qkv_bwd(const bf16_t* dq, const float* dqf, const bf16_t* dk, const bf16_t* dv,
+                             const float* cosT, const float* sinT, bf16_t* dqkv, int B, int S, int nh, int hd,
+                             hipStream_t st) {
+  if (hd % 8) return -1;
+  const size_t total = (size_t)B * S * 3 * nh * (hd / 8);
+  k_rope_qkv_bwd<<<ew_blocks(total), 256, 0, st>>>(dq, dqf, dk, dv, cosT, sinT, dqkv, B, S, nh, hd);
+  DLT_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------- SwiGLU
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+
+// gu [M, 2I] = [gate | up] -> a [M, I] = silu(gate) * up
+__global__ __launch_bounds__(256) void k_swiglu_fwd(const bf16_t* __restrict__ gu, bf16_t* __restrict__ a, int M, int I) {
+  const int q = I >> 3;
+  const size_t total = (size_t)M * q;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t m = i / q;
+    const int c = (int)(i % q) * 8;
+    const u16x8 g = *reinterpret_cast<const u16x8*>(gu + m * 2 * I + c);
+    const u16x8 u = *reinterpret_cast<const u16x8*>(gu + m * 2 * I + I + c);
+    u16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float gv = bf2f(g.v[e]);
+      o.v[e] = f2bf(gv * sigmoidf_(gv) * bf2f(u.v[e]));
+    }
+    *reinterpret_cast<u16x8*>(a + m * I + c) = o;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_swiglu_bwd(const bf16_t* __restrict__ gu, const bf16_t* __restrict__ da,
+                                                    bf16_t* __restrict__ dgu, int M, int I) {
+  const int q = I >> 3;
+  const size_t total = (size_t)M * q;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t m = i / q;
+    const int c = (int)(i % q) * 8;
+    const u16x8 g = *reinterpret_cast<const u16x8*>(gu + m * 2 * I + c);
+    const u16x8 u = *reinterpret_cast<const u16x8*>(gu + m * 2 * I + I + c);
+    const u16x8 d = *reinterpret_cast<const u16x8*>(da + m * I + c);
+    u16x8 og, ou;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float gv = bf2f(g.v[e]), uv = bf2f(u.v[e]), dv = bf2f(d.v[e]);
+      const float sg = sigmoidf_(gv);
+      og.v[e] = f2bf(dv * uv * sg * (1.f + gv * (1.f - sg)));
+      ou.v[e] = f2bf(dv * gv * sg);
+    }
+    *reinterpret_cast<u16x8*>(dgu + m * 2 * I + c) = og;
+    *reinterpret_cast<u16x8*>(dgu + m * 2 * I + I + c) = ou;
+  }
+}
+
+DLT_API int dlt_swiglu_fwd(const bf16_t* gu, bf16_t* a, int M, int I, hipStream_t st) {
+  if (I % 8) return -1;
+  k_swiglu_fwd<<<ew_blocks((size_t)M * (I / 8)), 256, 0, st>>>(gu, a, M, I);
+  DLT_CHECK_LAUNCH();
+}
+
+DLT_API int dlt_swiglu_bwd(const bf16_t* gu, const bf16_t* da, bf16_t* dgu, int M, int I, hipStream_t st) {
+  if (I % 8) return -1;
+  k_swiglu_bwd<<<ew_blocks((size_t)M * (I / 8)), 256, 0, st>>>(gu, da, dgu, M, I);
+  DLT_CHECK_LAUNCH();
+}

@@ -1,0 +1,124 @@
+// Flat multi-tensor AdamW + global grad-norm for the fp32 master / bf16 shadow layout.
+//
+// Reference: torch.optim.AdamW(fused=True) over 110 tensors + clip_grad_norm_
+// (foreach norm, host-visible scalar) + autocast re-casting every weight to bf16 each
+// micro-step (ddp_trainer.py:229-234,347-356).  Here:
+//  * k_sumsq: one pass over the flat fp32 grad buffer -> device scalar (no host sync);
+//  * k_clip_coef: norm / clip coefficient computed ON DEVICE, folded with the DDP
+//    1/world averaging into a single grad scale read by the AdamW kernel;
+//  * k_adamw: decoupled weight decay + bias-corrected Adam on the flat buffer, also
+//    writing the bf16 shadow weights the GEMMs consume.
+#include "common.h"
+
+__global__ __launch_bounds__(256) void k_sumsq(const float* __restrict__ x, int64_t n, float* __restrict__ out) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  const int64_t n4 = n >> 2;
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 v = x4[i];
+    acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  if (blockIdx.x == 0) {
+    for (int64_t i = (n4 << 2) + threadIdx.x; i < n; i += blockDim.x) acc += x[i] * x[i];
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) unsafeAtomicAdd(out, red[0] + red[1] + red[2] + red[3]);
+}
+
+// norm = sqrt(sumsq) * norm_mul;  coef = min(1, max_norm / (norm + 1e-6))  (clip_grad_norm_ semantics)
+// out[0] = norm, out[1] = grad scale for AdamW = coef * scale_mul (max_norm <= 0 disables clipping)
+__global__ void k_clip_coef(const float* __restrict__ sumsq, float* __restrict__ out, float norm_mul, float max_norm,
+                            float scale_mul) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const float norm = sqrtf(*sumsq) * norm_mul;
+    float coef = 1.f;
+    if (max_norm > 0.f) {
+      coef = max_norm / (norm + 1e-6f);
+      coef = coef < 1.f ? coef : 1.f;
+    }
+    out[0] = norm;
+    out[1] = coef * scale_mul;
+  }
+}
+
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float lr, float b1, float b2, float eps,
+                                          float wd, float step_size, float inv_bc2_sqrt) {
+  p *= (1.f - lr * wd);
+  m = m + (1.f - b1) * (g - m);  // lerp, as torch
+  v = b2 * v + (1.f - b2) * g * g;
+  const float denom = sqrtf(v) * inv_bc2_sqrt + eps;
+  p -= step_size * m / denom;
+}
+
+__global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                               float* __restrict__ v, bf16_t* __restrict__ shadow, int64_t n, float lr,
+                                               float b1, float b2, float eps, float wd, float step_size,
+                                               float inv_bc2_sqrt, const float* __restrict__ gscale_ptr) {
+  const float gs = gscale_ptr ? gscale_ptr[1] : 1.f;
+  const int64_t n4 = n >> 2;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    float4 pp = reinterpret_cast<float4*>(p)[i];
+    const float4 gg = reinterpret_cast<const float4*>(g)[i];
+    float4 mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    adam_elem(pp.x, gg.x * gs, mm.x, vv.x, lr, b1, b2, eps, wd, step_size, inv_bc2_sqrt);
+    adam_elem(pp.y, gg.y * gs, mm.y, vv.y, lr, b1, b2, eps, wd, step_size, inv_bc2_sqrt);
+    adam_elem(pp.z, gg.z * gs, mm.z, vv.z, lr, b1, b2, eps, wd, step_size, inv_bc2_sqrt);
+    adam_elem(pp.w, gg.w * gs, mm.w, vv.w, lr, b1, b2, eps, wd, step_size, inv_bc2_sqrt);
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+    if (shadow) {
+      u16x4 s;
+      s.v[0] = f2bf(pp.x); s.v[1] = f2bf(pp.y); s.v[2] = f2bf(pp.z); s.v[3] = f2bf(pp.w);
+      reinterpret_cast<u16x4*>(shadow)[i] = s;
+    }
+  }
+  if (blockIdx.x == 0) {
+    for (int64_t i = (n4 << 2) + threadIdx.x; i < n; i += blockDim.x) {
+      float pp = p[i], mm = m[i], vv = v[i];
+      adam_elem(pp, g[i] * gs, mm, vv, lr, b1, b2, eps, wd, step_size, inv_bc2_sqrt);
+      p[i] = pp; m[i] = mm; v[i] = vv;
+      if (shadow) shadow[i] = f2bf(pp);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_cast_bf16(const float* __restrict__ x, bf16_t* __restrict__ y, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = f2bf(x[i]);
+}
+
+static inline int flat_blocks(int64_t n) {
+  int64_t b = (n / 4 + 255) / 256;
+  if (b > 4096) b = 4096;
+  return (int)(b < 1 ? 1 : b);
+}
+
+DLT_API int dlt_sumsq(const float* x, int64_t n, float* out, hipStream_t st) {
+  k_sumsq<<<flat_blocks(n), 256, 0, st>>>(x, n, out);
+  DLT_CHECK_LAUNCH();
+}
+
+DLT_API int dlt_clip_coef(const float* sumsq, float* out, float norm_mul, float max_norm, float scale_mul,
+                          hipStream_t st) {
+  k_clip_coef<<<1, 64, 0, st>>>(sumsq, out, norm_mul, max_norm, scale_mul);
+  DLT_CHECK_LAUNCH();
+}
+
+DLT_API int dlt_adamw(float* p, const float* g, float* m, float* v, bf16_t* shadow, int64_t n, float lr, float b1,
+                      float b2, float eps, float wd, float step_size, float inv_bc2_sqrt, const float* gscale,
+                      hipStream_t st) {
+  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return -1;
+  if (shadow && ((uintptr_t)shadow & 7)) return -1;
+  k_adamw<<<flat_blocks(n), 256, 0, st>>>(p, g, m, v, shadow, n, lr, b1, b2, eps, wd, step_size, inv_bc2_sqrt, gscale);
+  DLT_CHECK_LAUNCH();
+}
+
+DLT_API int dlt_cast_bf16(const float* x, bf16_t* y, int64_t n, hipStream_t st) {
+  k_cast_bf16<<<flat_blocks(n * 4), 256, 0, st>>>(x, y, n);
+  DLT_CHECK_LAUNCH();
+}

@@ -1,0 +1,303 @@
+"""ctypes bindings for the gfx950 kernel library (``ops/_dlt_kernels.so``).
+
+Every wrapper validates shapes/dtypes/contiguity on the host BEFORE launching (a
+mis-shaped launch of a hand-written kernel must never reach the GPU), allocates
+outputs with the torch caching allocator and launches on the current HIP stream, so
+the calls are graph-capturable and ordered with hipBLASLt GEMMs and RCCL.
+
+Import is loud: on a GPU box, a missing or stale library raises instead of silently
+falling back to PyTorch ops.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+from typing import Optional
+
+import torch
+
+from . import rng
+
+_LIB = None
+_LIBPATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_dlt_kernels.so")
+
+c_void_p, c_int, c_float, c_uint32, c_int64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_uint32, ctypes.c_int64
+
+_SIGS = {
+    "dlt_add_dropout_rmsnorm_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                    c_float, c_uint32, c_uint32, c_float, c_void_p],
+    "dlt_rmsnorm_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                        c_int, c_int, c_uint32, c_uint32, c_float, c_void_p],
+    "dlt_embedding_fwd": [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p],
+    "dlt_embedding_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "dlt_rope_qkv_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                         c_void_p],
+    "dlt_rope_qkv_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                         c_int, c_void_p],
+    "dlt_swiglu_fwd": [c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "dlt_swiglu_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "dlt_cross_entropy_fwd_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
+    "dlt_sumsq": [c_void_p, c_int64, c_void_p, c_void_p],
+    "dlt_clip_coef": [c_void_p, c_void_p, c_float, c_float, c_float, c_void_p],
+    "dlt_adamw": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float, c_float,
+                  c_float, c_float, c_float, c_void_p, c_void_p],
+    "dlt_cast_bf16": [c_void_p, c_void_p, c_int64, c_void_p],
+    "dlt_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_uint32,
+                     c_uint32, c_float, c_void_p],
+    "dlt_attn_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                     c_void_p, c_int, c_int, c_int, c_int, c_float, c_uint32, c_uint32, c_float, c_void_p],
+}
+
+
+def library_path() -> str:
+    return _LIBPATH
+
+
+def lib():
+    """Load (once) the kernel library; raises with a clear message if it is missing."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(_LIBPATH):
+            raise RuntimeError(
+                f"MI355X kernel library not built: {_LIBPATH} missing. Run "
+                "`python -m distributed_llm_trainer_amd.ops.build` (or __graft_entry__.build()).")
+        import torch  # noqa: F401  (load torch's HIP runtime first so the .so binds to it)
+        L = ctypes.CDLL(_LIBPATH)
+        for name, argt in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = argt
+            fn.restype = c_int
+        _LIB = L
+    return _LIB
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _chk(rc: int, name: str):
+    if rc != 0:
+        raise RuntimeError(f"{name} failed (code {rc})")
+
+
+def _req(t: torch.Tensor, dtype, name: str, numel: Optional[int] = None):
+    if not t.is_cuda:
+        raise ValueError(f"{name}: expected a GPU tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if numel is not None and t.numel() != numel:
+        raise ValueError(f"{name}: expected {numel} elements, got {t.numel()}")
+    if t.data_ptr() % 16:
+        raise ValueError(f"{name}: must be 16-byte aligned")
+
+
+# ------------------------------------------------------------------ tables
+def rope_tables(head_dim: int, seq_len: int, device=None):
+    from .reference import rope_tables as rt
+    c, s = rt(head_dim, seq_len, device=device)
+    return c.contiguous(), s.contiguous()
+
+
+# ---------------------------------------------------------------- embedding
+def embedding_fwd(ids: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    ids = ids.reshape(-1).contiguous()
+    if ids.dtype != torch.int64:
+        ids = ids.long()
+    M = ids.numel()
+    V, H = weight.shape
+    if weight.dtype not in (torch.float32, torch.bfloat16):
+        raise TypeError("embedding weight must be fp32 or bf16")
+    _req(weight, weight.dtype, "embedding.weight")
+    out = torch.empty(M, H, dtype=torch.float32, device=weight.device)
+    _chk(lib().dlt_embedding_fwd(_p(ids), _p(weight), 0 if weight.dtype == torch.float32 else 1, _p(out), M, H,
+                                 _stream()), "embedding_fwd")
+    return out
+
+
+def embedding_bwd(ids: torch.Tensor, dout: torch.Tensor, dweight: torch.Tensor) -> None:
+    ids = ids.reshape(-1).contiguous()
+    if ids.dtype != torch.int64:
+        ids = ids.long()
+    M = ids.numel()
+    H = dweight.shape[-1]
+    _req(dout, torch.float32, "embedding_bwd.dout", M * H)
+    _req(dweight, torch.float32, "embedding_bwd.dweight")
+    _chk(lib().dlt_embedding_bwd(_p(ids), _p(dout), _p(dweight), M, H, _stream()), "embedding_bwd")
+
+
+# ---------------------------------------------------------------- RMSNorm
+def add_dropout_rmsnorm_fwd(resid, delta, weight, eps, p, key, out_dtype=torch.bfloat16):
+    src = resid if resid is not None else delta
+    M, H = src.shape
+    if out_dtype != torch.bfloat16:
+        raise TypeError("HIP rmsnorm emits bf16")
+    if resid is not None:
+        _req(resid, torch.float32, "rmsnorm.resid", M * H)
+    if delta is not None:
+        _req(delta, torch.bfloat16, "rmsnorm.delta", M * H)
+    w = weight if weight.dtype == torch.float32 else weight.float()
+    w = w.contiguous()
+    _req(w, torch.float32, "rmsnorm.weight", H)
+    y = torch.empty(M, H, dtype=torch.bfloat16, device=src.device)
+    rstd = torch.empty(M, dtype=torch.float32, device=src.device)
+    if delta is None:
+        x, xo = resid, None       # x is just the residual: no copy
+    else:
+        x = torch.empty(M, H, dtype=torch.float32, device=src.device)
+        xo = x
+    thr = rng.keep_threshold(p)
+    dscale = 1.0 / (1.0 - p) if thr else 1.0
+    _chk(lib().dlt_add_dropout_rmsnorm_fwd(_p(resid), _p(delta), _p(w), _p(xo), _p(y), _p(rstd), M, H, float(eps),
+                                           key & 0xFFFFFFFF, thr, dscale, _stream()), "add_dropout_rmsnorm_fwd")
+    return x, y, rstd
+
+
+def rmsnorm_bwd(dy, x, rstd, weight, dres, dweight, p_prev, key_prev, dy_scale=None, want_ddelta=True):
+    M, H = x.shape
+    _req(dy, torch.bfloat16, "rmsnorm_bwd.dy", M * H)
+    _req(x, torch.float32, "rmsnorm_bwd.x", M * H)
+    _req(rstd, torch.float32, "rmsnorm_bwd.rstd", M)
+    if dres is not None:
+        _req(dres, torch.float32, "rmsnorm_bwd.dres", M * H)
+    _req(dweight, torch.float32, "rmsnorm_bwd.dweight", H)
+    w = (weight if weight.dtype == torch.float32 else weight.float()).contiguous()
+    scale_t = None
+    if dy_scale is not None:
+        scale_t = dy_scale.reshape(1).float().contiguous()
+    dx = torch.empty(M, H, dtype=torch.float32, device=x.device)
+    dd = torch.empty(M, H, dtype=torch.bfloat16, device=x.device) if want_ddelta else None
+    thr = rng.keep_threshold(p_prev)
+    dscale = 1.0 / (1.0 - p_prev) if thr else 1.0
+    _chk(lib().dlt_rmsnorm_bwd(_p(dy), _p(x), _p(rstd), _p(w), _p(dres), _p(dx), _p(dd), _p(dweight), _p(scale_t),
+                               M, H, key_prev & 0xFFFFFFFF, thr, dscale, _stream()), "rmsnorm_bwd")
+    return dx, dd
+
+
+# ------------------------------------------------------------------- RoPE
+def rope_qkv_fwd(qkv, B, S, nh, cos, sin):
+    M, threeH = qkv.shape
+    hd = threeH // (3 * nh)
+    if M != B * S or hd * 3 * nh != threeH:
+        raise ValueError("rope_qkv_fwd: bad shapes")
+    _req(qkv, torch.bfloat16, "rope.qkv")
+    if cos.shape[0] < S or cos.shape[1] != hd // 2:
+        raise ValueError("rope tables too short")
+    q = torch.empty(B, nh, S, hd, dtype=torch.bfloat16, device=qkv.device)
+    k = torch.empty_like(q)
+    v = torch.empty_like(q)
+    _chk(lib().dlt_rope_qkv_fwd(_p(qkv), _p(cos), _p(sin), _p(q), _p(k), _p(v), B, S, nh, hd, _stream()),
+         "rope_qkv_fwd")
+    return q, k, v
+
+
+def rope_qkv_bwd(dq, dk, dv, cos, sin):
+    B, nh, S, hd = dk.shape
+    for t, n in ((dk, "dk"), (dv, "dv")):
+        _req(t, torch.bfloat16, "rope_bwd." + n, B * nh * S * hd)
+    dqf = dq if dq.dtype == torch.float32 else None
+    dqb = dq if dq.dtype == torch.bfloat16 else None
+    _req(dq, dq.dtype, "rope_bwd.dq", B * nh * S * hd)
+    out = torch.empty(B * S, 3 * nh * hd, dtype=torch.bfloat16, device=dk.device)
+    _chk(lib().dlt_rope_qkv_bwd(_p(dqb), _p(dqf), _p(dk), _p(dv), _p(cos), _p(sin), _p(out), B, S, nh, hd, _stream()),
+         "rope_qkv_bwd")
+    return out
+
+
+# -------------------------------------------------------------- attention
+def attention_fwd(q, k, v, p, key, causal=True):
+    if not causal:
+        raise NotImplementedError("only causal attention is implemented (the model is a causal LM)")
+    B, nh, S, hd = q.shape
+    for t, n in ((q, "q"), (k, "k"), (v, "v")):
+        _req(t, torch.bfloat16, "attn." + n, B * nh * S * hd)
+    if hd != 64:
+        raise NotImplementedError(f"attention kernel is specialised for head_dim 64 (got {hd})")
+    o = torch.empty(B * S, nh * hd, dtype=torch.bfloat16, device=q.device)
+    lse = torch.empty(B, nh, S, dtype=torch.float32, device=q.device)
+    thr = rng.keep_threshold(p)
+    dscale = 1.0 / (1.0 - p) if thr else 1.0
+    _chk(lib().dlt_attn_fwd(_p(q), _p(k), _p(v), _p(o), _p(lse), B, nh, S, hd, 1.0 / math.sqrt(hd),
+                            key & 0xFFFFFFFF, thr, dscale, _stream()), "attn_fwd")
+    return o, lse
+
+
+def attention_bwd(q, k, v, o, do, lse, p, key, causal=True):
+    B, nh, S, hd = q.shape
+    n = B * nh * S * hd
+    for t, nm in ((q, "q"), (k, "k"), (v, "v"), (o, "o"), (do, "do")):
+        _req(t, torch.bfloat16, "attn_bwd." + nm, n)
+    _req(lse, torch.float32, "attn_bwd.lse", B * nh * S)
+    delta = torch.empty(B, nh, S, dtype=torch.float32, device=q.device)
+    dq = torch.empty_like(q)
+    dk = torch.empty_like(k)
+    dv = torch.empty_like(v)
+    thr = rng.keep_threshold(p)
+    dscale = 1.0 / (1.0 - p) if thr else 1.0
+    _chk(lib().dlt_attn_bwd(_p(q), _p(k), _p(v), _p(o), _p(do), _p(lse), _p(delta), _p(dq), _p(dk), _p(dv),
+                            B, nh, S, hd, 1.0 / math.sqrt(hd), key & 0xFFFFFFFF, thr, dscale, _stream()), "attn_bwd")
+    return dq, dk, dv
+
+
+# ----------------------------------------------------------------- SwiGLU
+def swiglu_fwd(gu):
+    M, twoI = gu.shape
+    _req(gu, torch.bfloat16, "swiglu.gu")
+    out = torch.empty(M, twoI // 2, dtype=torch.bfloat16, device=gu.device)
+    _chk(lib().dlt_swiglu_fwd(_p(gu), _p(out), M, twoI // 2, _stream()), "swiglu_fwd")
+    return out
+
+
+def swiglu_bwd(gu, da):
+    M, twoI = gu.shape
+    _req(gu, torch.bfloat16, "swiglu_bwd.gu")
+    _req(da, torch.bfloat16, "swiglu_bwd.da", M * twoI // 2)
+    out = torch.empty_like(gu)
+    _chk(lib().dlt_swiglu_bwd(_p(gu), _p(da), _p(out), M, twoI // 2, _stream()), "swiglu_bwd")
+    return out
+
+
+# ------------------------------------------------------------ cross-entropy
+def cross_entropy_fwd_bwd(logits, targets, vocab, n_valid):
+    M, Vp = logits.shape
+    _req(logits, torch.bfloat16, "ce.logits")
+    targets = targets.contiguous()
+    if targets.dtype != torch.int64 or targets.numel() != M:
+        raise ValueError("ce.targets must be int64 [M]")
+    nv = n_valid.reshape(1).to(torch.int64).contiguous()
+    loss = torch.empty(M, dtype=torch.float32, device=logits.device)
+    _chk(lib().dlt_cross_entropy_fwd_bwd(_p(logits), _p(targets), _p(nv), _p(loss), M, Vp, vocab, _stream()),
+         "cross_entropy")
+    return loss
+
+
+# --------------------------------------------------------------- optimizer
+def sumsq(x: torch.Tensor, out: torch.Tensor) -> None:
+    _req(x, torch.float32, "sumsq.x")
+    _chk(lib().dlt_sumsq(_p(x), x.numel(), _p(out), _stream()), "sumsq")
+
+
+def clip_coef(sumsq_t: torch.Tensor, out: torch.Tensor, norm_mul: float, max_norm: float, scale_mul: float) -> None:
+    _chk(lib().dlt_clip_coef(_p(sumsq_t), _p(out), norm_mul, max_norm, scale_mul, _stream()), "clip_coef")
+
+
+def adamw_flat(param, grad, exp_avg, exp_avg_sq, shadow, lr, beta1, beta2, eps, wd, step, gscale):
+    n = param.numel()
+    for t, nm in ((param, "param"), (grad, "grad"), (exp_avg, "exp_avg"), (exp_avg_sq, "exp_avg_sq")):
+        _req(t, torch.float32, "adamw." + nm, n)
+    if shadow is not None and (shadow.dtype != torch.bfloat16 or shadow.numel() != n):
+        raise ValueError("adamw.shadow must be bf16 of the same numel")
+    bc1 = 1.0 - beta1 ** step
+    bc2 = 1.0 - beta2 ** step
+    _chk(lib().dlt_adamw(_p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), _p(shadow), n, lr, beta1, beta2, eps, wd,
+                         lr / bc1, 1.0 / math.sqrt(bc2), _p(gscale), _stream()), "adamw")
+
+
+def cast_bf16(x: torch.Tensor, y: torch.Tensor) -> None:
+    _chk(lib().dlt_cast_bf16(_p(x), _p(y), x.numel(), _stream()), "cast_bf16")

@@ -1,0 +1,131 @@
+"""Data-parallel gradient reduction over RCCL (xGMI) with layer-granular overlap.
+
+Replaces ``torch.nn.parallel.DistributedDataParallel`` as used by the reference
+(``ddp_trainer.py:167-172,329-332``).  What it does
+differently, by design for an 8x MI355X xGMI full mesh:
+
+* **Zero-copy buckets.** Gradients already live in one flat fp32 buffer
+  (``parallel/flat.py``) whose layer regions are contiguous, so a bucket is a slice:
+  no flatten/unflatten copy kernels.
+* **Big buckets.** Default 64 MB (vs DDP's 25 MB / 1 MB first bucket).  A ring
+  all-reduce over xGMI is per-link bound and RCCL spreads a large message over
+  several channels/links; fewer, larger collectives amortise the ~10-20 us launch
+  and protocol cost.  (small: 607 MB of fp32 grads -> ~10 buckets.)
+* **Layer-granular overlap.** The fused executor calls ``post_backward(i)`` when
+  layer i's weight gradients are final; the bucket whose lowest layer is i is then
+  enqueued on RCCL's stream (async) while layer i-1's backward keeps computing.
+* **no_sync.** Only the micro-step that calls ``require_sync(True)`` reduces
+  (reference GA semantics, ``ddp_trainer.py:329-332``).
+* **No per-step buffer broadcast.** The reference's DDP rebroadcasts the RoPE
+  buffers every step (X3); they are deterministic, so we don't.
+* **Averaging folded into the optimizer.** All-reduce uses SUM; the 1/world factor
+  is applied inside the AdamW kernel together with the clip coefficient.
+* Optional ``reduce_dtype=torch.bfloat16`` halves the bytes on the wire (the fp32
+  accumulation buffer is kept; bf16 is only the transport).
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+class DDPRuntime:
+    def __init__(self, store, process_group=None, bucket_cap_mb: float = 64.0,
+                 reduce_dtype: torch.dtype = torch.float32, broadcast_init: bool = True):
+        self.store = store
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(process_group) if dist.is_initialized() else 0
+        self.reduce_dtype = reduce_dtype
+        self.sync = True
+        self.handles: List[Tuple[object, Optional[torch.Tensor], int, int]] = []
+        lay = store.layout
+        elem = store.grad.element_size()
+        cap = max(1, int(bucket_cap_mb * 1024 * 1024 / elem))
+        # buckets over layers, formed from the LAST layer downwards (backward order)
+        self.fire_at = {}  # unit -> list of (start, end)
+        L = len(lay.layer_bounds)
+        i = L - 1
+        while i >= 0:
+            j = i
+            end = lay.layer_bounds[i][1]
+            while j > 0 and end - lay.layer_bounds[j - 1][0] <= cap:
+                j -= 1
+            start = lay.layer_bounds[j][0]
+            self.fire_at.setdefault(j, []).append((start, end))
+            i = j - 1
+        # embedding (tied lm_head) + all norm weights: final after the embedding bwd
+        self.fire_at.setdefault("head", []).append((lay.embed_offset, lay.total))
+        self.buckets = [b for v in self.fire_at.values() for b in v]
+        if broadcast_init and self.world > 1:
+            self.broadcast_parameters()
+        store.hooks = self
+
+    # ------------------------------------------------------------------ init
+    @torch.no_grad()
+    def broadcast_parameters(self) -> None:
+        """Rank 0's weights win (one flat broadcast instead of DDP's per-bucket X2)."""
+        dist.broadcast(self.store.flat, src=0, group=self.pg)
+        self.store.refresh_shadow()
+
+    # ----------------------------------------------------------------- no_sync
+    def require_sync(self, flag: bool) -> None:
+        self.sync = bool(flag)
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        old = self.sync
+        self.sync = False
+        try:
+            yield
+        finally:
+            self.sync = old
+
+    # ------------------------------------------------------------------- hooks
+    def pre_forward(self, unit):
+        pass
+
+    def post_forward(self, unit):
+        pass
+
+    def pre_backward(self, unit):
+        pass
+
+    def post_backward(self, unit):
+        if not self.sync or self.world == 1:
+            return
+        for (a, b) in self.fire_at.get(unit, ()):
+            self._launch(a, b)
+
+    def _launch(self, a: int, b: int) -> None:
+        g = self.store.grad[a:b]
+        if self.reduce_dtype != g.dtype:
+            t = g.to(self.reduce_dtype)
+            h = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+            self.handles.append((h, t, a, b))
+        else:
+            h = dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+            self.handles.append((h, None, a, b))
+
+    def reduce_all_now(self) -> None:
+        """Synchronous fallback used by the eager (non-engine) path."""
+        if self.world == 1:
+            return
+        for (a, b) in self.buckets:
+            self._launch(a, b)
+        self.finish()
+
+    def finish(self) -> None:
+        """Wait for every outstanding bucket (makes the current stream wait on RCCL)."""
+        for (h, t, a, b) in self.handles:
+            h.wait()
+            if t is not None:
+                self.store.grad[a:b].copy_(t)
+        self.handles.clear()
+
+    @property
+    def grad_div(self) -> float:
+        return float(self.world)

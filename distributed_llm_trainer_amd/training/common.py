@@ -1,0 +1,81 @@
+"""Pieces shared by the DDP and FSDP trainers: process-group bootstrap, device
+selection, seeding, LR schedule, memory stats and the YAML/CLI config merge."""
+from __future__ import annotations
+
+import datetime
+import math
+import os
+import random
+from typing import Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def setup_distributed(require: bool = False, timeout_s: Optional[float] = None):
+    """Returns (distributed, rank, world_size, local_rank).
+
+    Backend: "nccl" (= RCCL on ROCm) when a GPU is present, else "gloo" (CPU tests /
+    the plumbing config).  ``DLT_PG_TIMEOUT`` (seconds) bounds every collective so a
+    dead rank surfaces as an error instead of a hang.
+    """
+    distributed = dist.is_initialized() or "RANK" in os.environ or require
+    if distributed and not dist.is_initialized():
+        backend = os.environ.get("DLT_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+        t = timeout_s or float(os.environ.get("DLT_PG_TIMEOUT", "1800"))
+        kw = dict(backend=backend, timeout=datetime.timedelta(seconds=t))
+        if backend == "nccl" and torch.cuda.is_available():
+            lr = int(os.environ.get("LOCAL_RANK", 0))
+            torch.cuda.set_device(lr)
+            kw["device_id"] = torch.device(f"cuda:{lr}")
+        dist.init_process_group(**kw)
+    if distributed:
+        return True, dist.get_rank(), dist.get_world_size(), int(os.environ.get("LOCAL_RANK", 0))
+    return False, 0, 1, 0
+
+
+def select_device(local_rank: int) -> torch.device:
+    if torch.cuda.is_available() and os.environ.get("DLT_FORCE_CPU") != "1":
+        d = torch.device(f"cuda:{local_rank}")
+        torch.cuda.set_device(d)
+        return d
+    return torch.device("cpu")
+
+
+def seed_all(seed: int) -> None:
+    random.seed(seed)
+    np.random.seed(seed % (2 ** 32))
+    torch.manual_seed(seed)
+
+
+def cosine_lr(step: int, lr: float, warmup: int, max_steps: int, clamp: bool = True) -> float:
+    """Linear warmup then cosine to 0.1*lr (``ddp_trainer.py:262-271``).  The DDP
+    reference does not clamp the decay ratio (LR rises again after max_steps, Q6);
+    ``clamp=True`` applies the FSDP trainer's clamp (``fsdp_trainer.py:354``)."""
+    if step < warmup:
+        return lr * (step / warmup)
+    denom = max(1, max_steps - warmup)
+    ratio = (step - warmup) / denom
+    if clamp:
+        ratio = min(ratio, 1.0)
+    coeff = 0.5 * (1.0 + math.cos(math.pi * ratio))
+    min_lr = 0.1 * lr
+    return min_lr + coeff * (lr - min_lr)
+
+
+def memory_stats(device) -> dict:
+    """GB (1e9), like ``fsdp_trainer.py:496-505``."""
+    if torch.device(device).type != "cuda":
+        return {"allocated_gb": 0.0, "reserved_gb": 0.0, "max_allocated_gb": 0.0}
+    return {"allocated_gb": torch.cuda.memory_allocated(device) / 1e9,
+            "reserved_gb": torch.cuda.memory_reserved(device) / 1e9,
+            "max_allocated_gb": torch.cuda.max_memory_allocated(device) / 1e9}
+
+
+def unwrap_batch(batch):
+    if isinstance(batch, dict):
+        return batch["input_ids"]
+    if isinstance(batch, (list, tuple)):
+        return batch[0]
+    return batch

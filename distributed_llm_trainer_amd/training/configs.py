@@ -1,0 +1,83 @@
+"""Training-side configuration dataclasses (field names/defaults = the reference).
+
+* ``TrainingConfig``      -- ``ddp_trainer.py:34-63``
+* ``FSDPTrainingConfig``  -- ``fsdp_trainer.py:78-93`` (exported as ``TrainingConfig``
+  from ``training.fsdp_trainer`` for API parity)
+* ``FSDPConfig``          -- ``fsdp_trainer.py:53-75``
+
+Additions are appended after the reference fields with defaults that reproduce the
+reference behaviour (e.g. ``seed``), or enable MI355X-specific knobs
+(``bucket_cap_mb``, ``reduce_dtype``, ``hip_graphs``).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Optional
+
+
+@dataclass
+class TrainingConfig:
+    # Data
+    batch_size: int = 8
+    max_seq_len: int = 1024
+    # Optimization
+    learning_rate: float = 6e-4
+    weight_decay: float = 0.1
+    beta1: float = 0.9
+    beta2: float = 0.95
+    grad_clip: float = 1.0
+    # Schedule
+    max_steps: int = 10000
+    warmup_steps: int = 1000
+    log_interval: int = 1
+    eval_interval: int = 500
+    save_interval: int = 1000
+    # Mixed precision
+    mixed_precision: str = "bf16"
+    # Gradient accumulation
+    gradient_accumulation_steps: int = 4
+    # Checkpointing
+    checkpoint_dir: str = "checkpoints"
+    resume_from: Optional[str] = None
+    # ---- additions (MI355X build)
+    seed: int = 1234
+    bucket_cap_mb: float = 64.0
+    reduce_dtype: str = "fp32"         # gradient all-reduce wire dtype: fp32 | bf16
+    lr_schedule_fix: bool = True       # set LR before the step + clamp cosine (Q5/Q6)
+    adam_eps: float = 1e-8
+
+
+@dataclass
+class FSDPTrainingConfig:
+    batch_size: int = 4
+    max_seq_len: int = 1024
+    learning_rate: float = 3e-4
+    weight_decay: float = 0.1
+    beta1: float = 0.9
+    beta2: float = 0.95
+    grad_clip: float = 1.0
+    max_steps: int = 10000
+    warmup_steps: int = 1000
+    log_interval: int = 10
+    save_interval: int = 1000
+    gradient_accumulation_steps: int = 8
+    checkpoint_dir: str = "checkpoints_fsdp"
+    # ---- additions
+    resume_from: Optional[str] = None
+    seed: int = 1234
+    lr_schedule_fix: bool = True
+    adam_eps: float = 1e-8
+    eval_interval: int = 500
+
+
+@dataclass
+class FSDPConfig:
+    sharding_strategy: str = "FULL_SHARD"     # FULL_SHARD | SHARD_GRAD_OP | NO_SHARD | HYBRID_SHARD
+    cpu_offload: bool = False
+    mixed_precision: str = "bf16"             # bf16 | fp16 | fp32
+    backward_prefetch: str = "BACKWARD_PRE"   # BACKWARD_PRE | BACKWARD_POST | NONE
+    activation_checkpointing: bool = True
+    limit_all_gathers: bool = True
+    # ---- additions
+    reduce_dtype: str = "bf16"                # reduce-scatter wire dtype (reference: bf16)
+    sync_every_micro_step: bool = True        # reference reduce-scatters every micro-step (Q15)

@@ -1,0 +1,346 @@
+"""Single-GPU / data-parallel trainer (CLI- and API-compatible with the reference's
+``src/training/ddp_trainer.py``).
+
+Reference call stack: torchrun -> main() -> DistributedTrainer ->
+DDP(GPT) + fused AdamW -> train_step (GA micro-loop, no_sync, autocast, clip, step).
+
+MI355X design:
+* bf16 (the default and the headline config) runs the fused executor
+  (``models/engine.py``) on the HIP kernels; weights are views into a flat fp32
+  master buffer with a bf16 shadow (``parallel/flat.py``).
+* Data parallelism is ``parallel/ddp.py``: zero-copy 64 MB buckets all-reduced over
+  RCCL as soon as each group of layers finishes its backward.
+* Loss is accumulated on the device; the only host sync per optimizer step is the
+  logged loss value (the reference syncs on every micro-step, Q10).
+* fp32 / fp16 run the eager module path (autocast + dynamic loss scaling for fp16);
+  on CPU the fused executor runs with the PyTorch reference ops in fp32.
+
+Intentional fixes (documented in README "Divergences"): LR is set before the
+optimizer step and the cosine is clamped (Q5/Q6, switch off with
+``lr_schedule_fix=False``), seeded init (Q13), working ``--resume_from`` (Q8) and
+``--config`` YAML (Q1).
+"""
+from __future__ import annotations
+
+import argparse
+import contextlib
+import json
+import os
+import sys
+import time
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from ..models.config import GPTConfig
+from ..models.gpt import GPT, count_parameters
+from ..parallel.ddp import DDPRuntime
+from ..parallel.flat import FlatParamStore
+from ..utils import checkpoint as ckpt
+from ..utils.profiling import Profiler, range_push, range_pop
+from .common import cosine_lr, memory_stats, seed_all, select_device, setup_distributed, unwrap_batch
+from .configs import TrainingConfig
+from .optim import flat_store_optimizer
+
+
+class DistributedTrainer:
+    """DDP trainer.  ``train_step(batch) -> {"loss", "lr", "tokens"}``."""
+
+    def __init__(self, model_config: GPTConfig, training_config: TrainingConfig, use_engine: Optional[bool] = None):
+        self.model_config = model_config
+        self.training_config = training_config
+        self._setup_distributed()
+        self._setup_device(use_engine)
+        self._setup_model()
+        self._setup_optimizer()
+        self.global_step = 0
+        self.tokens_seen = 0
+        self._last_norm = None
+
+    # ------------------------------------------------------------------ setup
+    def _setup_distributed(self):
+        self.distributed, self.rank, self.world_size, self.local_rank = setup_distributed()
+        self.is_main_process = self.rank == 0
+        if self.is_main_process:
+            print(f"Distributed training: {self.distributed}")
+            print(f"World size: {self.world_size}")
+
+    def _setup_device(self, use_engine):
+        self.device = select_device(self.local_rank)
+        mp = self.training_config.mixed_precision
+        cuda = self.device.type == "cuda"
+        if use_engine is None:
+            use_engine = (not cuda) or mp == "bf16"
+        self.use_engine = use_engine
+        self.autocast_ctx = contextlib.nullcontext()
+        self.loss_scale = None
+        if cuda and mp == "bf16":
+            self.dtype = torch.bfloat16
+        elif cuda and mp == "fp16":
+            self.dtype = torch.float16
+            self.autocast_ctx = torch.autocast(device_type="cuda", dtype=torch.float16)
+            self.loss_scale = 2.0 ** 16
+        else:
+            self.dtype = torch.float32
+        if self.is_main_process:
+            path = "fused HIP engine" if (use_engine and cuda) else ("fused engine (CPU reference ops)"
+                                                                    if use_engine else "eager")
+            print(f"Device: {self.device}")
+            print(f"Mixed precision: {mp} (dtype: {self.dtype}) | execution: {path}")
+
+    def _setup_model(self):
+        seed_all(self.training_config.seed)
+        model = GPT(self.model_config)
+        self.model = model.to(self.device)
+        if self.is_main_process:
+            print(f"Model parameters: {count_parameters(self.model):,}")
+        if self.use_engine:
+            eng = self.model.enable_engine(seed=self.training_config.seed + 1000003 * self.rank)
+            self.store = self.model.store
+        else:
+            self.store = FlatParamStore(self.model, self.device, compute_dtype=torch.float32)
+        self.ddp = None
+        if self.distributed:
+            rd = torch.bfloat16 if self.training_config.reduce_dtype == "bf16" else torch.float32
+            self.ddp = DDPRuntime(self.store, bucket_cap_mb=self.training_config.bucket_cap_mb, reduce_dtype=rd)
+
+    def _setup_optimizer(self):
+        c = self.training_config
+        self.optimizer = flat_store_optimizer(self.store, c.learning_rate, (c.beta1, c.beta2), c.adam_eps,
+                                              c.weight_decay, split_no_decay=True)
+
+    # --------------------------------------------------------------- schedule
+    def get_lr(self, step: int) -> float:
+        c = self.training_config
+        return cosine_lr(step, c.learning_rate, c.warmup_steps, c.max_steps, clamp=c.lr_schedule_fix)
+
+    # ------------------------------------------------------------------- step
+    def train_step(self, batch, sync_loss: bool = True) -> dict:
+        cfg = self.training_config
+        self.model.train()
+        if cfg.lr_schedule_fix:
+            lr = self.get_lr(self.global_step)
+            for g in self.optimizer.param_groups:
+                g["lr"] = lr
+        self.optimizer.zero_grad(set_to_none=True)
+        input_ids = unwrap_batch(batch).to(self.device, non_blocking=True)
+        GA = cfg.gradient_accumulation_steps
+        micro_bs = input_ids.shape[0] // GA
+        total = torch.zeros((), dtype=torch.float32, device=self.device)
+        for micro in range(GA):
+            ids = input_ids[micro * micro_bs:(micro + 1) * micro_bs]
+            if self.ddp is not None:
+                self.ddp.require_sync(micro == GA - 1)
+            range_push(f"micro{micro}")
+            with self.autocast_ctx:
+                _, loss = self.model(ids, labels=ids)
+                loss = loss / GA
+            if self.loss_scale is not None:
+                (loss * self.loss_scale).backward()
+            else:
+                loss.backward()
+            range_pop()
+            total += loss.detach().float()
+        if not self.use_engine:
+            self.store.sync_grads_from_params()
+            if self.ddp is not None:
+                self.ddp.reduce_all_now()
+        elif self.ddp is not None:
+            self.ddp.finish()
+        div = float(self.world_size) * (self.loss_scale or 1.0)
+        scale = self.optimizer.compute_scale(cfg.grad_clip, grad_div=div)
+        skip = False
+        if self.loss_scale is not None:  # fp16 dynamic loss scaling
+            if not torch.isfinite(scale[0]).item():
+                self.loss_scale /= 2.0
+                skip = True
+            elif (self.global_step + 1) % 2000 == 0:
+                self.loss_scale *= 2.0
+        if not skip:
+            self.optimizer.step(scale)
+            if not self.use_engine:
+                self.store.refresh_shadow()
+        self._last_norm = scale[0]
+        self.optimizer.zero_grad(set_to_none=True)
+        if not cfg.lr_schedule_fix:  # reference order: LR for the *next* step set after this one
+            lr = self.get_lr(self.global_step)
+            for g in self.optimizer.param_groups:
+                g["lr"] = lr
+        else:
+            lr = self.optimizer.param_groups[0]["lr"]
+        self.global_step += 1
+        self.tokens_seen += input_ids.numel() * self.world_size
+        out = {"loss": total.item() if sync_loss else total, "lr": lr, "tokens": self.tokens_seen}
+        return out
+
+    # ------------------------------------------------------------ checkpoints
+    def save_checkpoint(self, path: str):
+        if not self.is_main_process:
+            return
+        payload = {
+            "model": ckpt.model_state_dict_cpu(self.model),
+            "optimizer": self.optimizer.state_dict(),
+            "global_step": self.global_step,
+            "tokens_seen": self.tokens_seen,
+            "model_config": self.model_config,
+            "training_config": self.training_config,
+        }
+        ckpt.save_checkpoint(path, payload)
+
+    def load_checkpoint(self, path: str):
+        c = ckpt.load_checkpoint(path, map_location="cpu")
+        sd = c["model"]
+        with torch.no_grad():
+            self.model.load_state_dict(sd, strict=False)
+        self.store.refresh_shadow()
+        self.optimizer.load_state_dict(c["optimizer"])
+        self.global_step = int(c["global_step"])
+        self.tokens_seen = int(c["tokens_seen"])
+        if self.is_main_process:
+            print(f"Loaded Checkpoint from {path} (step {self.global_step})")
+
+    def get_memory_stats(self) -> dict:
+        return memory_stats(self.device)
+
+
+# --------------------------------------------------------------------------- CLI
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(description="MI355X DDP trainer (reference-compatible CLI)")
+    p.add_argument("--model_size", type=str, default="small", choices=["small", "medium", "large", "xl"])
+    p.add_argument("--batch_size", type=int, default=8)
+    p.add_argument("--max_steps", type=int, default=1000)
+    p.add_argument("--mixed_precision", type=str, default="bf16", choices=["fp32", "fp16", "bf16"])
+    p.add_argument("--gradient_checkpointing", action="store_true")
+    p.add_argument("--dataset", type=str, default="dummy", choices=["dummy", "tinystories", "openwebtext"])
+    p.add_argument("--data_path", type=str, default=None)
+    p.add_argument("--max_tokens", type=int, default=None)
+    p.add_argument("--streaming", action="store_true")
+    p.add_argument("--cache_max_tokens", type=int, default=None)
+    # additions
+    p.add_argument("--config", type=str, default=None, help="YAML config (configs/*.yaml); CLI flags override it")
+    p.add_argument("--resume_from", type=str, default=None)
+    p.add_argument("--checkpoint_dir", type=str, default=None)
+    p.add_argument("--save_interval", type=int, default=None)
+    p.add_argument("--log_interval", type=int, default=None)
+    p.add_argument("--learning_rate", type=float, default=None)
+    p.add_argument("--warmup_steps", type=int, default=None)
+    p.add_argument("--gradient_accumulation_steps", type=int, default=None)
+    p.add_argument("--seq_len", type=int, default=None)
+    p.add_argument("--seed", type=int, default=None)
+    p.add_argument("--tokenizer", type=str, default="gpt2")
+    p.add_argument("--profile", type=str, default=None, help="write a torch.profiler trace to this dir")
+    p.add_argument("--metrics_jsonl", type=str, default=None)
+    p.add_argument("--no_final_save", action="store_true")
+    return p
+
+
+def main(argv=None):
+    from ..utils.config_loader import explicit_args, load_yaml_config
+    parser = build_parser()
+    args = parser.parse_args(argv)
+    given = explicit_args(parser, argv)
+
+    model_config = GPTConfig.from_preset(args.model_size)
+    tc = TrainingConfig(batch_size=args.batch_size, max_steps=args.max_steps, mixed_precision=args.mixed_precision)
+    if args.config:
+        model_config, tc, _, data_cfg = load_yaml_config(args.config, model_config, tc, None,
+                                                         keep_model_preset="model_size" in given)
+        # CLI flags that were explicitly given still win
+        for k in ("batch_size", "max_steps", "mixed_precision"):
+            if k in given:
+                setattr(tc, k, getattr(args, k))
+        if "dataset" not in given and data_cfg.get("dataset") in ("dummy", "tinystories", "openwebtext"):
+            args.dataset = data_cfg["dataset"]
+    if args.gradient_checkpointing:
+        model_config.gradient_checkpointing = True
+    for k in ("resume_from", "checkpoint_dir", "save_interval", "log_interval", "learning_rate", "warmup_steps",
+              "gradient_accumulation_steps", "seed"):
+        v = getattr(args, k)
+        if v is not None:
+            setattr(tc, k, v)
+    if args.seq_len:
+        model_config.max_seq_len = args.seq_len
+
+    trainer = DistributedTrainer(model_config, tc)
+    if tc.resume_from:
+        trainer.load_checkpoint(tc.resume_from)
+
+    loader_bs = tc.batch_size * tc.gradient_accumulation_steps
+    seq_len = model_config.max_seq_len
+    if args.dataset in ("tinystories", "openwebtext"):
+        if args.data_path is None:
+            raise ValueError(f"{args.dataset} dataset requires --data_path")
+        from ..data import create_openwebtext_dataloader, create_tinystories_dataloader
+        fn = create_tinystories_dataloader if args.dataset == "tinystories" else create_openwebtext_dataloader
+        dataloader = fn(path=args.data_path, batch_size=loader_bs, seq_len=seq_len, distributed=trainer.distributed,
+                        rank=trainer.rank, world_size=trainer.world_size, tokenizer_name=args.tokenizer,
+                        max_tokens=args.max_tokens, streaming=args.streaming,
+                        cache_max_tokens=args.cache_max_tokens, num_workers=0 if args.streaming else 2)
+    else:
+        from ..data import create_dummy_dataloader
+        dataloader = create_dummy_dataloader(batch_size=loader_bs, seq_len=seq_len,
+                                             vocab_size=model_config.vocab_size, distributed=trainer.distributed,
+                                             rank=trainer.rank, world_size=trainer.world_size,
+                                             num_batches=int(os.environ.get("DLT_DUMMY_BATCHES", "64")),
+                                             seed=tc.seed)
+
+    if trainer.is_main_process:
+        print("\n" + "=" * 60)
+        print("Starting training...")
+        print("=" * 60 + "\n")
+    metrics_f = open(args.metrics_jsonl, "a") if (args.metrics_jsonl and trainer.is_main_process) else None
+    prof = Profiler(args.profile, enabled=bool(args.profile) and trainer.is_main_process)
+    data_iter = iter(dataloader)
+    start_time = time.time()
+    start_step = trainer.global_step
+    steady_t0, steady_tok0 = None, 0
+    for step in range(start_step, tc.max_steps):
+        try:
+            batch = next(data_iter)
+        except StopIteration:
+            if hasattr(dataloader.sampler, "set_epoch"):
+                dataloader.sampler.set_epoch(step)
+            data_iter = iter(dataloader)
+            batch = next(data_iter)
+        do_log = step % tc.log_interval == 0
+        metrics = trainer.train_step({"input_ids": unwrap_batch(batch)}, sync_loss=do_log)
+        prof.step()
+        if step - start_step == 10:
+            steady_t0, steady_tok0 = time.time(), trainer.tokens_seen
+        if do_log and trainer.is_main_process:
+            elapsed = time.time() - start_time
+            tps = (metrics["tokens"] - start_step * 0) / max(elapsed, 1e-9)
+            print(f"Step {step:6d} | Loss: {metrics['loss']:.4f} | LR: {metrics['lr']:.2e} | Tokens/sec: {tps:,.0f}",
+                  flush=True)
+            if metrics_f:
+                rec = {"step": step, "loss": metrics["loss"], "lr": metrics["lr"], "tokens": metrics["tokens"],
+                       "tokens_per_sec": tps, **trainer.get_memory_stats()}
+                if trainer._last_norm is not None:
+                    rec["grad_norm"] = float(trainer._last_norm)
+                metrics_f.write(json.dumps(rec) + "\n")
+                metrics_f.flush()
+        if step > 0 and step % tc.save_interval == 0:
+            trainer.save_checkpoint(f"{tc.checkpoint_dir}/step_{step}.pt")
+    prof.close()
+    if not args.no_final_save:
+        trainer.save_checkpoint(f"{tc.checkpoint_dir}/final.pt")
+    if trainer.distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+    if trainer.is_main_process:
+        total_time = time.time() - start_time
+        print(f"\nTraining complete! Total time: {total_time:.2f}s")
+        print(f"Total tokens processed: {trainer.tokens_seen:,}")
+        if steady_t0 is not None:
+            dt = time.time() - steady_t0
+            print(f"Steady-state tokens/sec (after step 10): {(trainer.tokens_seen - steady_tok0) / dt:,.0f}")
+        ms = trainer.get_memory_stats()
+        print(f"Peak memory: {ms['max_allocated_gb']:.2f} GB")
+    if metrics_f:
+        metrics_f.close()
+    return trainer
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,165 @@
+"""Fused AdamW over flat parameter buffers, plus on-device gradient clipping.
+
+Semantics follow ``torch.optim.AdamW`` (decoupled weight decay, bias correction,
+eps outside the sqrt) exactly as the reference configures it:
+
+* DDP trainer (``ddp_trainer.py:214-234``): two groups, weight decay on everything
+  except names containing "bias"/"norm" -> here the flat layout puts all norm weights
+  after ``decay_end`` so the two groups are two contiguous regions.
+* FSDP trainer (``fsdp_trainer.py:334-343``): one group, weight decay on everything.
+
+Differences by design: one kernel launch per region instead of
+a per-tensor loop; the clip coefficient and the DDP 1/world averaging are computed on
+the device and folded into the AdamW grad scale (no ``.item()`` host sync); the
+kernel also refreshes the bf16 shadow weights used by the GEMMs.
+
+``state_dict()`` emits the torch AdamW format (int param ids in param-group order,
+``{step, exp_avg, exp_avg_sq}``) so checkpoints are interchangeable with the
+reference's ``optimizer.state_dict()``.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from ..ops import reference as ref
+
+
+class FlatAdamW:
+    def __init__(self, flat: torch.Tensor, grad: torch.Tensor, shadow: Optional[torch.Tensor],
+                 regions: Sequence[Tuple[int, int, float]], lr: float, betas=(0.9, 0.95),
+                 eps: float = 1e-8, param_map: Optional[List[List[Tuple[str, int, int, tuple]]]] = None):
+        """``regions``: list of (start, end, weight_decay) -- one per param group.
+        ``param_map``: per group, the (name, offset, numel, shape) of each parameter, in
+        the reference's param order (used for state_dict compatibility)."""
+        self.flat, self.grad = flat, grad
+        self.shadow = shadow if (shadow is not None and shadow is not flat) else None
+        self.exp_avg = torch.zeros_like(flat)
+        self.exp_avg_sq = torch.zeros_like(flat)
+        self.regions = list(regions)
+        self.param_groups = [dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=wd, amsgrad=False,
+                                  maximize=False, foreach=None, capturable=False, differentiable=False,
+                                  fused=None, decoupled_weight_decay=True)
+                             for (_, _, wd) in self.regions]
+        self.param_map = param_map
+        self.step_count = 0
+        self.is_cuda = flat.is_cuda
+        self._scale_buf = torch.zeros(2, dtype=torch.float32, device=flat.device)
+        self._sumsq = torch.zeros(1, dtype=torch.float32, device=flat.device)
+        self._ones = torch.tensor([0.0, 1.0], dtype=torch.float32, device=flat.device)
+
+    # ----------------------------------------------------------- grad clipping
+    def local_sumsq(self) -> torch.Tensor:
+        self._sumsq.zero_()
+        if self.is_cuda:
+            from ..ops import hip
+            hip.sumsq(self.grad, self._sumsq)
+        else:
+            self._sumsq += self.grad.float().pow(2).sum()
+        return self._sumsq
+
+    def compute_scale(self, max_norm: float, grad_div: float = 1.0, sumsq: Optional[torch.Tensor] = None
+                      ) -> torch.Tensor:
+        """Returns a device tensor [total_norm, grad_scale].  The stored grads are
+        ``grad_div`` times the true gradient (e.g. a SUM all-reduce over ranks), the
+        norm reported is that of the true gradient, and grad_scale = clip_coef/grad_div."""
+        if sumsq is None:
+            sumsq = self.local_sumsq()
+        if self.is_cuda:
+            from ..ops import hip
+            hip.clip_coef(sumsq, self._scale_buf, 1.0 / grad_div, float(max_norm), 1.0 / grad_div)
+        else:
+            norm = torch.sqrt(sumsq.reshape(())) / grad_div
+            coef = torch.clamp(max_norm / (norm + 1e-6), max=1.0) if max_norm > 0 else torch.ones(())
+            self._scale_buf[0] = norm
+            self._scale_buf[1] = coef / grad_div
+        return self._scale_buf
+
+    # ------------------------------------------------------------------- step
+    @torch.no_grad()
+    def step(self, scale: Optional[torch.Tensor] = None) -> None:
+        self.step_count += 1
+        sc = scale if scale is not None else self._ones
+        for (a, b, _), g in zip(self.regions, self.param_groups):
+            if b <= a:
+                continue
+            lr, (b1, b2), eps, wd = g["lr"], g["betas"], g["eps"], g["weight_decay"]
+            if self.is_cuda:
+                from ..ops import hip
+                hip.adamw_flat(self.flat[a:b], self.grad[a:b], self.exp_avg[a:b], self.exp_avg_sq[a:b],
+                               None if self.shadow is None else self.shadow[a:b], lr, b1, b2, eps, wd,
+                               self.step_count, sc)
+            else:
+                ref.adamw_step(self.flat[a:b], self.grad[a:b], self.exp_avg[a:b], self.exp_avg_sq[a:b],
+                               None, lr, b1, b2, eps, wd, self.step_count, sc[1])
+
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        # grads are persistent flat views; "set_to_none" semantics = zero the buffer
+        self.grad.zero_()
+
+    # ------------------------------------------------------------- state dict
+    def state_dict(self) -> Dict:
+        state, groups, idx = {}, [], 0
+        pm = self.param_map or [[("flat", a, b - a, (b - a,))] for (a, b, _) in self.regions]
+        for g, plist in zip(self.param_groups, pm):
+            ids = []
+            for (_name, off, n, shape) in plist:
+                state[idx] = {"step": torch.tensor(float(self.step_count)),
+                              "exp_avg": self.exp_avg[off:off + n].view(shape).detach().cpu().clone(),
+                              "exp_avg_sq": self.exp_avg_sq[off:off + n].view(shape).detach().cpu().clone()}
+                ids.append(idx)
+                idx += 1
+            gg = {k: v for k, v in g.items()}
+            gg["params"] = ids
+            groups.append(gg)
+        return {"state": state, "param_groups": groups}
+
+    def load_state_dict(self, sd: Dict) -> None:
+        pm = self.param_map or [[("flat", a, b - a, (b - a,))] for (a, b, _) in self.regions]
+        st = sd["state"]
+        steps = []
+        with torch.no_grad():
+            for g, sg, plist in zip(self.param_groups, sd["param_groups"], pm):
+                for k in ("lr", "betas", "eps", "weight_decay"):
+                    if k in sg:
+                        g[k] = tuple(sg[k]) if k == "betas" else sg[k]
+                for pid, (_name, off, n, shape) in zip(sg["params"], plist):
+                    s = st.get(pid) if isinstance(st, dict) else None
+                    if s is None:
+                        s = st.get(str(pid)) if isinstance(st, dict) else None
+                    if s is None:
+                        continue
+                    self.exp_avg[off:off + n].copy_(s["exp_avg"].reshape(-1).to(self.exp_avg))
+                    self.exp_avg_sq[off:off + n].copy_(s["exp_avg_sq"].reshape(-1).to(self.exp_avg_sq))
+                    stp = s.get("step", 0)
+                    steps.append(int(stp.item() if torch.is_tensor(stp) else stp))
+        if steps:
+            self.step_count = max(steps)
+
+
+def flat_store_optimizer(store, lr: float, betas, eps: float, weight_decay: float,
+                         split_no_decay: bool = True) -> FlatAdamW:
+    """AdamW over a FlatParamStore; groups mirror the reference DDP (split) or FSDP (single)."""
+    lay = store.layout
+    model = store.model
+    names = [n for n, _ in model.named_parameters()]
+    by = lay.by_name
+
+    def pm(filter_fn):
+        out = []
+        for n in names:
+            if filter_fn(n):
+                s = by[n]
+                out.append((n, s.offset, s.numel, s.shape))
+        return out
+
+    if split_no_decay:
+        regions = [(0, lay.decay_end, weight_decay), (lay.decay_end, lay.total, 0.0)]
+        nd = lambda n: ("bias" in n) or ("norm" in n)  # noqa: E731 (reference rule)
+        param_map = [pm(lambda n: not nd(n)), pm(nd)]
+    else:
+        regions = [(0, lay.total, weight_decay)]
+        param_map = [pm(lambda n: True)]
+    return FlatAdamW(store.flat, store.grad, store.shadow, regions, lr, betas, eps, param_map)

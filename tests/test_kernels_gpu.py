@@ -1,0 +1,193 @@
+"""Numerics of every HIP kernel against the plain-PyTorch fp32 reference of the same op
+(ops/reference.py), on the MI355X.  Dropout is ON where the op has it: the counter-hash
+masks are bit-identical between kernel and reference (ops/rng.py)."""
+import math
+
+import pytest
+import torch
+
+from distributed_llm_trainer_amd.ops import hip, reference as ref, rng
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _close(a, b, atol, rtol=0.0, what=""):
+    a, b = a.float(), b.float()
+    err = (a - b).abs()
+    lim = atol + rtol * b.abs()
+    bad = (err > lim).sum().item()
+    assert bad == 0, f"{what}: {bad} elements out of tolerance, max err {err.max().item():.3e}"
+
+
+def test_library_loads():
+    L = hip.lib()
+    assert L is not None
+
+
+@pytest.mark.parametrize("H", [768, 1024, 1600])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_add_dropout_rmsnorm_fwd(H, p):
+    torch.manual_seed(0)
+    M = 515
+    r = torch.randn(M, H, device=DEV)
+    d = torch.randn(M, H, device=DEV).bfloat16()
+    w = torch.rand(H, device=DEV) + 0.5
+    key = rng.site_key(7, 3, 1, rng.SITE_RESID)
+    x, y, rs = hip.add_dropout_rmsnorm_fwd(r, d, w, 1e-6, p, key)
+    x2, y2, rs2 = ref.add_dropout_rmsnorm_fwd(r, d, w, 1e-6, p, key)
+    _close(x, x2, 1e-5, 1e-5, "x")
+    _close(rs, rs2, 1e-5, 1e-4, "rstd")
+    _close(y, y2.float(), 2e-2, 1e-2, "y")
+
+
+@pytest.mark.parametrize("H", [768, 1600])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_rmsnorm_bwd(H, p):
+    torch.manual_seed(1)
+    M = 1031
+    x = torch.randn(M, H, device=DEV)
+    rstd = torch.rsqrt(x.pow(2).mean(-1) + 1e-6)
+    w = torch.rand(H, device=DEV) + 0.5
+    dy = torch.randn(M, H, device=DEV).bfloat16()
+    dres = torch.randn(M, H, device=DEV)
+    key = rng.site_key(9, 0, 2, rng.SITE_MLP)
+    sc = torch.tensor(0.25, device=DEV)
+    dw1 = torch.zeros(H, device=DEV)
+    dw2 = torch.zeros(H, device=DEV)
+    dx, dd = hip.rmsnorm_bwd(dy, x, rstd, w, dres, dw1, p, key, dy_scale=sc)
+    dx2, dd2 = ref.rmsnorm_bwd(dy, x, rstd, w, dres, dw2, p, key, dy_scale=sc)
+    _close(dx, dx2, 1e-4, 1e-4, "dx")
+    _close(dd, dd2.float(), 2e-2, 1e-2, "ddelta")
+    _close(dw1, dw2, 1e-2, 1e-4, "dw")
+
+
+def test_embedding():
+    torch.manual_seed(2)
+    V, H, M = 1000, 768, 4096
+    W = torch.randn(V, H, device=DEV)
+    ids = torch.randint(0, V, (M,), device=DEV)
+    _close(hip.embedding_fwd(ids, W), ref.embedding_fwd(ids, W), 0.0, 0.0, "emb fwd fp32")
+    Wb = W.bfloat16()
+    _close(hip.embedding_fwd(ids, Wb), ref.embedding_fwd(ids, Wb), 0.0, 0.0, "emb fwd bf16")
+    dout = torch.randn(M, H, device=DEV)
+    g1 = torch.zeros(V, H, device=DEV)
+    g2 = torch.zeros(V, H, device=DEV)
+    hip.embedding_bwd(ids, dout, g1)
+    ref.embedding_bwd(ids, dout, g2)
+    _close(g1, g2, 1e-4, 1e-5, "emb bwd")
+
+
+def test_rope():
+    torch.manual_seed(3)
+    B, S, nh, hd = 2, 300, 12, 64
+    qkv = torch.randn(B * S, 3 * nh * hd, device=DEV).bfloat16()
+    cos, sin = hip.rope_tables(hd, 1024, device=DEV)
+    q, k, v = hip.rope_qkv_fwd(qkv, B, S, nh, cos, sin)
+    q2, k2, v2 = ref.rope_qkv_fwd(qkv, B, S, nh, cos, sin)
+    for a, b, n in ((q, q2, "q"), (k, k2, "k"), (v, v2, "v")):
+        _close(a, b, 2e-2, 1e-2, n)
+    dq, dk, dv = (torch.randn(B, nh, S, hd, device=DEV).bfloat16() for _ in range(3))
+    _close(hip.rope_qkv_bwd(dq, dk, dv, cos, sin), ref.rope_qkv_bwd(dq, dk, dv, cos, sin), 2e-2, 1e-2, "dqkv")
+    dqf = dq.float()
+    _close(hip.rope_qkv_bwd(dqf, dk, dv, cos, sin), ref.rope_qkv_bwd(dq, dk, dv, cos, sin), 2e-2, 1e-2, "dqkv f32")
+
+
+def test_swiglu():
+    torch.manual_seed(4)
+    M, I = 777, 3072
+    gu = (torch.randn(M, 2 * I, device=DEV) * 2).bfloat16()
+    _close(hip.swiglu_fwd(gu), ref.swiglu_fwd(gu), 3e-2, 1e-2, "swiglu fwd")
+    da = torch.randn(M, I, device=DEV).bfloat16()
+    _close(hip.swiglu_bwd(gu, da), ref.swiglu_bwd(gu, da), 3e-2, 1e-2, "swiglu bwd")
+
+
+def test_cross_entropy():
+    torch.manual_seed(5)
+    M, V, Vp = 1024, 50257, 50304
+    logits = (torch.randn(M, Vp, device=DEV) * 3).bfloat16()
+    tg = torch.randint(0, V, (M,), device=DEV)
+    tg[::7] = -100
+    nv = (tg != -100).sum()
+    l1 = logits.clone()
+    l2 = logits.clone()
+    loss1 = hip.cross_entropy_fwd_bwd(l1, tg, V, nv)
+    loss2 = ref.cross_entropy_fwd_bwd(l2, tg, V, nv)
+    _close(loss1, loss2, 2e-3, 1e-4, "ce loss")
+    _close(l1, l2, 1e-6, 2e-2, "ce grad")
+    assert l1[:, V:].abs().max().item() == 0.0
+
+
+def test_adamw_and_norm():
+    torch.manual_seed(6)
+    n = 100003
+    p = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV)
+    m = torch.randn(n, device=DEV) * 0.1
+    v = torch.rand(n, device=DEV) * 0.01
+    sh = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    p2, m2, v2 = p.clone(), m.clone(), v.clone()
+    ss = torch.zeros(1, device=DEV)
+    hip.sumsq(g, ss)
+    _close(ss, g.pow(2).sum().reshape(1), 1e-1, 1e-5, "sumsq")
+    scale = torch.zeros(2, device=DEV)
+    hip.clip_coef(ss, scale, 0.5, 1.0, 0.5)
+    norm = g.norm() * 0.5
+    _close(scale[0], norm, 1e-3, 1e-5, "norm")
+    _close(scale[1], torch.clamp(1.0 / (norm + 1e-6), max=1.0) * 0.5, 1e-6, 1e-5, "coef")
+    hip.adamw_flat(p, g, m, v, sh, 1e-3, 0.9, 0.95, 1e-8, 0.1, 5, scale)
+    ref.adamw_step(p2, g, m2, v2, None, 1e-3, 0.9, 0.95, 1e-8, 0.1, 5, scale[1])
+    _close(p, p2, 1e-6, 1e-5, "param")
+    _close(m, m2, 1e-6, 1e-5, "m")
+    _close(v, v2, 1e-7, 1e-5, "v")
+    _close(sh, p.bfloat16(), 0.0, 0.0, "shadow")
+
+
+def _attn_inputs(B, nh, S, seed):
+    torch.manual_seed(seed)
+    q = torch.randn(B, nh, S, 64, device=DEV).bfloat16()
+    k = torch.randn(B, nh, S, 64, device=DEV).bfloat16()
+    v = torch.randn(B, nh, S, 64, device=DEV).bfloat16()
+    return q, k, v
+
+
+@pytest.mark.parametrize("S", [64, 128, 200, 1024])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attention_fwd(S, p):
+    B, nh = 2, 3
+    q, k, v = _attn_inputs(B, nh, S, 10 + S)
+    key = rng.site_key(1, 2, 3, rng.SITE_ATTN)
+    o, lse = hip.attention_fwd(q, k, v, p, key)
+    o2, lse2 = ref.attention_fwd(q, k, v, p, key)
+    _close(lse, lse2, 2e-3, 1e-4, "lse")
+    _close(o, o2.float(), 2e-2, 2e-2, "o")
+
+
+def test_attention_fwd_identity_asymmetric():
+    """A = I-style check with asymmetric V: catches transposed C/D or operand maps."""
+    B, nh, S = 1, 1, 128
+    q = torch.zeros(B, nh, S, 64, device=DEV)
+    k = torch.zeros(B, nh, S, 64, device=DEV)
+    q[..., 0] = 40.0   # huge scores on the diagonal only via position-dependent k
+    for j in range(S):
+        k[0, 0, j, 0] = 1.0 if j % 2 == 0 else -1.0
+    v = torch.arange(S * 64, device=DEV, dtype=torch.float32).view(1, 1, S, 64) / (S * 64)
+    q, k, v = q.bfloat16(), k.bfloat16(), v.bfloat16()
+    o, lse = hip.attention_fwd(q, k, v, 0.0, 0)
+    o2, lse2 = ref.attention_fwd(q, k, v, 0.0, 0)
+    _close(o, o2.float(), 1e-2, 1e-2, "o(asym)")
+
+
+@pytest.mark.parametrize("S", [64, 192, 1024])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attention_bwd(S, p):
+    B, nh = 2, 3
+    q, k, v = _attn_inputs(B, nh, S, 20 + S)
+    key = rng.site_key(4, 5, 6, rng.SITE_ATTN)
+    o, lse = ref.attention_fwd(q, k, v, p, key)
+    do = torch.randn_like(o.float()).bfloat16()
+    dq, dk, dv = hip.attention_bwd(q, k, v, o, do, lse, p, key)
+    dq2, dk2, dv2 = ref.attention_bwd(q, k, v, o, do, lse, p, key)
+    for a, b, n in ((dq, dq2, "dq"), (dk, dk2, "dk"), (dv, dv2, "dv")):
+        scale = b.float().abs().max().item()
+        _close(a, b.float(), 2e-2 * max(1.0, scale), 2e-2, n)
