@@ -20,7 +20,10 @@ BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "_dlt_kernels.so")
 ARCH = os.environ.get("DLT_OFFLOAD_ARCH", "gfx950")
 
-CXXFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+# -amdgpu-mfma-vgpr-form: keep MFMA accumulators in arch VGPRs (gfx950 has a unified
+# VGPR/AGPR file) -- removes v_accvgpr_read/write copies around the attention softmax.
+CXXFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result",
+            "-mllvm", "-amdgpu-mfma-vgpr-form"]
 
 
 def hipcc() -> str:

@@ -5,21 +5,26 @@
 // the SDPA path (gpt.py:199-206).  SURVEY §2.5 K5/K6.
 //
 // Design (CDNA4-first, see docs/KERNELS.md):
-//  * v_mfma_f32_32x32x16_bf16 everywhere.  "Swapped" products put the softmax row
-//    on the lane: S^T = K.Q^T leaves one query per lane with its keys in 16
-//    accumulator registers, so row max / row sum are in-lane plus one xor-32 swap,
-//    and the accumulator IS the B operand of the next product (O^T = V^T.P^T) --
-//    P never touches LDS.
+//  * v_mfma_f32_32x32x16_bf16 everywhere, accumulators in arch VGPRs
+//    (-mllvm -amdgpu-mfma-vgpr-form: no v_accvgpr copies around the softmax).
+//  * "Swapped" products put the softmax row on the lane: S^T = K.Q^T leaves one
+//    query per lane with its keys in 16 accumulator registers, so row max / row sum
+//    are in-lane plus one xor-32 swap, and the accumulator IS the B operand of the
+//    next product (O^T = V^T.P^T) -- P never touches LDS.
 //  * V / dO / Q / K^T operands are read with ds_read_b64_tr_b16 (hardware transpose).
-//  * K/V (fwd, dQ) and Q/dO (dK/dV) tiles are register-staged into XOR-swizzled
-//    LDS, double buffered: the global loads of tile t+1 are issued before the MFMAs
-//    of tile t and written to LDS after them (issue-early / write-late).
-//  * Dropout masks are regenerated from a counter hash (common.h drop_bits), one
-//    hash per two keys; nothing but (o, lse) is stored for backward.
-//  * Backward = 3 kernels: delta = rowsum(dO*O); dK/dV (one workgroup per 128 keys,
-//    dK/dV accumulated in registers); dQ (one workgroup per 128 queries,
-//    recomputes S and dP) -- no fp32 atomics anywhere.
-//  * Causal tile skipping; the heaviest tiles are launched first.
+//  * K/V (fwd, dQ) and Q/dO (dK/dV) tiles are register-staged into XOR-swizzled LDS,
+//    double buffered: global loads of tile t+1 are issued before the MFMAs of tile t
+//    and written to LDS after them (issue-early / write-late), one barrier per tile.
+//  * Wave-uniform control: the wave index goes through readfirstlane, and each tile
+//    is dispatched to a MASKED (diagonal / ragged) or UNMASKED instantiation, so the
+//    hot loop has no exec-mask divergence and no per-element mask selects.
+//  * Dropout: the forward regenerates the keep decision from a counter hash (one
+//    lowbias32 per two keys) and ALSO stores it as a bitmask [bh][S][ceil(S/32)]
+//    (12.6 MB per layer at B8 S1024 nh12); the two backward kernels read bits
+//    instead of re-hashing (the hash is ~half the VALU work of a tile).
+//  * Backward = 3 kernels: delta = rowsum(dO*O); dK/dV (workgroup per 128 keys,
+//    accumulated in registers); dQ (workgroup per 128 queries, recomputes S, dP) --
+//    no fp32 atomics anywhere.  Causal tile skipping; heaviest tiles launch first.
 //
 // Layouts: q, k, v, dq, dk, dv: [B*nh, S, 64] bf16;  o, do: [B, S, nh, 64] bf16
 // (= the [M, H] GEMM layout);  lse, delta: [B*nh, S] fp32 (natural-log lse).
@@ -30,17 +35,17 @@
 #define QB 128     // queries per workgroup (fwd / dQ), 32 per wave
 #define KB 128     // keys per workgroup (dK/dV), 32 per wave
 #define QSTEP 64   // queries per staged tile (dK/dV)
+#define LOG2E 1.44269504088896340736f
 
 typedef __attribute__((address_space(3))) shortx4_t lds_shortx4_t;
+typedef short shortx8_t __attribute__((ext_vector_type(8)));
 
-// LDS tile: [64 rows][64 bf16] = 128-B rows, 16-B chunk c of row r stored at chunk
-// c ^ ((r >> 1) & 7): conflict-free ds_read_b128 row-fragment reads (see notes in
-// docs/KERNELS.md), 2-way on the transposed reads.
+// LDS tile: [64 rows][64 bf16] = 128-B rows; 16-B chunk c of row r is stored at
+// chunk c ^ ((r >> 1) & 7): conflict-free ds_read_b128 row-fragment reads.
 __device__ __forceinline__ int swz_off(int row, int col) {
   return row * HD + ((((col >> 3) ^ ((row >> 1) & 7))) << 3) + (col & 7);
 }
 
-// 32x32x16 operand: 8 consecutive d of one row (row-major A or B fragment)
 __device__ __forceinline__ bf16x8_t lds_row8(const bf16_t* T, int row, int col) {
   return *reinterpret_cast<const bf16x8_t*>(T + swz_off(row, col));
 }
@@ -49,21 +54,19 @@ __device__ __forceinline__ shortx4_t lds_tr4(const bf16_t* T, int row, int col) 
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_shortx4_t*)(T + swz_off(row, col)));
 }
 
-// A operand of  X^T-style products:  A[d][k] with k = rows of T (keys or queries),
-// permuted so that it matches accumulator registers 8s..8s+7 used as the B operand:
-// element j of lane-half h <-> row 16*kk + 8*(j>>2) + 4*h + (j&3).
+// A operand A[d][k] (k = rows of T) in the permuted k order that matches accumulator
+// registers 8s..8s+7 used as the B operand: element j of lane-half h <-> row
+// 16*kk + 8*(j>>2) + 4*h + (j&3)  (cdna_hip_programming.md §3).
 __device__ __forceinline__ bf16x8_t tr_frag(const bf16_t* T, int kk, int dt, int lane) {
   const int h = lane >> 5, i = lane & 15;
   const int col = 32 * dt + 16 * ((lane >> 4) & 1) + 4 * (i & 3);
   const int r1 = 16 * kk + 4 * h + (i >> 2);
   const shortx4_t a = lds_tr4(T, r1, col);
   const shortx4_t b = lds_tr4(T, r1 + 8, col);
-  typedef short shortx8_t __attribute__((ext_vector_type(8)));
   shortx8_t c = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
   return __builtin_bit_cast(bf16x8_t, c);
 }
 
-// accumulator registers 8s..8s+7 -> bf16 B fragment
 __device__ __forceinline__ bf16x8_t acc_frag(const floatx16_t& acc, int s) {
   bf16x8_t r;
 #pragma unroll
@@ -75,38 +78,34 @@ __device__ __forceinline__ floatx16_t mfma(const bf16x8_t& a, const bf16x8_t& b,
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
-// row offset (within a 32x32 tile) of accumulator register i for lane-half h
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// row (within a 32x32 tile) of accumulator register i for lane-half h
 __device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
-// Register-staged tile copy: 64 rows x 64 cols bf16 from a [*, S, 64] head (rows
-// row0.., zero-filled past S), 2 chunks of 16 B per thread of a 256-thread block.
-struct Stage2 { u16x8 c[2]; };
-__device__ __forceinline__ void stage_load(Stage2& st, const bf16_t* __restrict__ head, int row0, int S, int tid) {
+__device__ __forceinline__ floatx16_t zero16() {
+  floatx16_t z;
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int c = tid + 256 * u;
-    const int r = c >> 3, ch = c & 7;
-    if (row0 + r < S) {
-      st.c[u] = *reinterpret_cast<const u16x8*>(head + (size_t)(row0 + r) * HD + ch * 8);
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) st.c[u].v[e] = 0;
-    }
-  }
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
 }
-// same, for a [B, S, nh, 64] tensor (o / do layout): row stride nh*64
-__device__ __forceinline__ void stage_load_bsh(Stage2& st, const bf16_t* __restrict__ base, int row0, int S,
-                                               int rstride, int tid) {
+
+// Register-staged tile copy: 64 rows x 64 cols bf16, rows beyond S zero-filled;
+// 2 x 16 B per thread of a 256-thread block.  `rstride` = row stride in elements.
+struct Stage2 { u16x8 c[2]; };
+__device__ __forceinline__ void stage_load(Stage2& st, const bf16_t* __restrict__ base, int row0, int S,
+                                           int rstride, int tid) {
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int c = tid + 256 * u;
     const int r = c >> 3, ch = c & 7;
-    if (row0 + r < S) {
-      st.c[u] = *reinterpret_cast<const u16x8*>(base + (size_t)(row0 + r) * rstride + ch * 8);
-    } else {
+    const int row = min(row0 + r, S - 1);
+    u16x8 v = *reinterpret_cast<const u16x8*>(base + (size_t)row * rstride + ch * 8);
+    if (row0 + r >= S) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) st.c[u].v[e] = 0;
+      for (int e = 0; e < 8; ++e) v.v[e] = 0;
     }
+    st.c[u] = v;
   }
 }
 __device__ __forceinline__ void stage_store(const Stage2& st, bf16_t* T, int tid) {
@@ -119,48 +118,148 @@ __device__ __forceinline__ void stage_store(const Stage2& st, bf16_t* T, int tid
 }
 
 __device__ __forceinline__ bf16x8_t load_row8(const bf16_t* __restrict__ p, bool ok) {
-  if (ok) return *reinterpret_cast<const bf16x8_t*>(p);
-  bf16x8_t z;
+  bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(p);
+  if (!ok) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) z[j] = (__bf16)0.f;
-  return z;
+    for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
+  }
+  return v;
+}
+
+// ============================================================================ dropout bits
+// keep-bit words: mask[bh][q][w] bit j = keep(q, key = 32w + j), causal words only
+// (w*32 <= q).  Pure VALU at full occupancy (~3 us per layer at B8 nh12 S1024), so
+// the MFMA kernels only test bits instead of hashing at 2 waves/SIMD.
+__global__ __launch_bounds__(256) void k_dropout_bits(uint32_t* __restrict__ mask, int BH, int S, uint32_t key,
+                                                      uint32_t thr) {
+  // grid: (ceil(S*W/256), BH); 32-bit index math only (64-bit div/mod is emulated)
+  const int W = (S + 31) >> 5;
+  const int bh = blockIdx.y;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= S * W) return;
+  const int q = idx / W, w = idx - q * W;
+  if (w * 32 > q) return;  // above the causal diagonal: never read
+  const uint32_t kbh = lowbias32(key + (uint32_t)bh * 0x9E3779B9u);
+  const uint32_t base = (uint32_t)q * (uint32_t)S + (uint32_t)(w * 32);
+  const int nk = min(32, S - w * 32);
+  uint32_t word = 0;
+  if ((base & 1u) == 0 && nk == 32) {
+#pragma unroll
+    for (int j = 0; j < 32; j += 2) {
+      const uint32_t hsh = lowbias32(kbh ^ ((base + j) >> 1));
+      word |= ((uint32_t)((hsh & 0xffffu) >= thr) << j) | ((uint32_t)((hsh >> 16) >= thr) << (j + 1));
+    }
+  } else {
+    for (int j = 0; j < nk; ++j) {
+      const uint32_t flat = base + (uint32_t)j;
+      const uint32_t hsh = lowbias32(kbh ^ (flat >> 1));
+      const uint32_t bits = (flat & 1u) ? (hsh >> 16) : (hsh & 0xffffu);
+      word |= (uint32_t)(bits >= thr) << j;
+    }
+  }
+  mask[(size_t)bh * S * W + idx] = word;
 }
 
 // ============================================================================ forward
+struct FwdState {
+  floatx16_t o[2];
+  float m, l;  // running max (raw score units) and per-lane partial row sum
+};
+
+template <bool MASK, bool DROP>
+__device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const bf16_t* Vt, const bf16x8_t (&qf)[4],
+                                         int k0, int qa, int S, int lane, float c_log2,
+                                         const uint32_t* __restrict__ mrow) {
+  const int h = lane >> 5, ql = lane & 31;
+  uint32_t words[2] = {0u, 0u};
+  if (DROP) {  // issue the keep-bit loads first; they land under the QK^T MFMAs
+    words[0] = mrow[k0 >> 5];
+    words[1] = mrow[(k0 >> 5) + 1];
+  }
+  floatx16_t sacc[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    sacc[t] = zero16();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) sacc[t] = mfma(lds_row8(Kt, 32 * t + ql, 16 * s + 8 * h), qf[s], sacc[t]);
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      if (MASK) {
+        const int ka = k0 + 32 * t + acc_row(i, h);
+        sacc[t][i] = (ka > qa || ka >= S) ? -INFINITY : sacc[t][i];
+      }
+      mx = fmaxf(mx, sacc[t][i]);
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  // defer the O/l rescale while no lane's running max grows (T13 with THR = 0:
+  // exact -- the rescale factor would be 1.0)
+  if (__any(mx > fs.m)) {
+    const float m_new = fmaxf(fs.m, mx);
+    const float alpha = fast_exp2((fs.m - m_new) * c_log2);
+    fs.m = m_new;
+    fs.l *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) fs.o[dt][i] *= alpha;
+  }
+  const float nmc = -fs.m * c_log2;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float p = fast_exp2(fmaf(sacc[t][i], c_log2, nmc));
+      fs.l += p;
+      if (DROP) sacc[t][i] = ((words[t] >> acc_row(i, h)) & 1u) ? p : 0.f;  // 1/(1-p) applied at the end
+      else sacc[t][i] = p;
+    }
+  }
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    const bf16x8_t pb = acc_frag(sacc[kk >> 1], kk & 1);
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) fs.o[dt] = mfma(tr_frag(Vt, kk, dt, lane), pb, fs.o[dt]);
+  }
+}
+
 template <bool DROP>
-__global__ __launch_bounds__(256) void k_attn_fwd(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
-                                                  const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
-                                                  float* __restrict__ lse, int S, int nh, float c_log2,
-                                                  uint32_t key, uint32_t thr, float dscale) {
+__global__ __launch_bounds__(256, 2) void k_attn_fwd(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
+                                                     const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
+                                                     float* __restrict__ lse, const uint32_t* __restrict__ mask,
+                                                     int S, int nh, float c_log2, float dscale) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * 2 * KVB * HD];  // [buf][K|V][64][64]
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, ql = lane & 31;
   const int nqb = (S + QB - 1) / QB;
   const int qb = nqb - 1 - blockIdx.x;  // heaviest (last) query blocks first
   const int bh = blockIdx.y;
   const int b = bh / nh, head = bh % nh;
   const size_t hoff = (size_t)bh * S * HD;
-  const int q0 = qb * QB + wid * 32;  // this wave's first query
-  const int qa = q0 + ql;             // this lane's query
-  const uint32_t kbh = lowbias32(key + (uint32_t)bh * 0x9E3779B9u);
+  const int q0 = qb * QB + wid * 32;  // this wave's first query (wave-uniform)
+  const int qa = q0 + ql;
+  const int W = (S + 31) >> 5;
+  const uint32_t* mrow = mask ? mask + ((size_t)bh * S + min(qa, S - 1)) * W : nullptr;
 
-  // Q^T B-operand fragments, kept in registers for the whole KV sweep
   bf16x8_t qf[4];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) qf[s] = load_row8(q + hoff + (size_t)qa * HD + 16 * s + 8 * h, qa < S);
+  for (int s = 0; s < 4; ++s) qf[s] = load_row8(q + hoff + (size_t)min(qa, S - 1) * HD + 16 * s + 8 * h, qa < S);
 
-  floatx16_t oacc[2];
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) oacc[dt][i] = 0.f;
-  float m_run = -INFINITY, l_run = 0.f;
+  FwdState fs;
+  fs.o[0] = zero16();
+  fs.o[1] = zero16();
+  fs.m = -INFINITY;
+  fs.l = 0.f;
 
   const int kv_end = min(S, qb * QB + QB);
   const int nkv = (kv_end + KVB - 1) / KVB;
   Stage2 sk, sv;
-  stage_load(sk, k + hoff, 0, S, tid);
-  stage_load(sv, v + hoff, 0, S, tid);
+  stage_load(sk, k + hoff, 0, S, HD, tid);
+  stage_load(sv, v + hoff, 0, S, HD, tid);
   stage_store(sk, lds, tid);
   stage_store(sv, lds + KVB * HD, tid);
   __syncthreads();
@@ -169,71 +268,16 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const bf16_t* __restrict__ q, 
     const int cur = kb & 1;
     const bool more = kb + 1 < nkv;
     if (more) {
-      stage_load(sk, k + hoff, (kb + 1) * KVB, S, tid);
-      stage_load(sv, v + hoff, (kb + 1) * KVB, S, tid);
+      stage_load(sk, k + hoff, (kb + 1) * KVB, S, HD, tid);
+      stage_load(sv, v + hoff, (kb + 1) * KVB, S, HD, tid);
     }
     const bf16_t* Kt = lds + cur * 2 * KVB * HD;
     const bf16_t* Vt = Kt + KVB * HD;
     const int k0 = kb * KVB;
-    if (k0 <= q0 + 31) {  // wave-uniform causal skip
-      floatx16_t sacc[2];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sacc[t][i] = 0.f;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) sacc[t] = mfma(lds_row8(Kt, 32 * t + ql, 16 * s + 8 * h), qf[s], sacc[t]);
-      }
-      const bool need_mask = (k0 + KVB - 1 > q0) || (k0 + KVB > S);
-      float mx = -INFINITY;
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float sv2 = sacc[t][i] * c_log2;
-          if (need_mask) {
-            const int ka = k0 + 32 * t + acc_row(i, h);
-            if (ka > qa || ka >= S) sv2 = -INFINITY;
-          }
-          sacc[t][i] = sv2;
-          mx = fmaxf(mx, sv2);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m_run, mx);
-      const float alpha = exp2f(m_run - m_new);
-      m_run = m_new;
-      l_run *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
-      const uint32_t rowidx = (uint32_t)qa * (uint32_t)S;
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-#pragma unroll
-        for (int i = 0; i < 16; i += 2) {
-          const float p0 = exp2f(sacc[t][i] - m_new);
-          const float p1 = exp2f(sacc[t][i + 1] - m_new);
-          l_run += p0 + p1;
-          if (DROP) {
-            const uint32_t ka = (uint32_t)(k0 + 32 * t + acc_row(i, h));
-            const uint32_t hsh = lowbias32(kbh ^ ((rowidx + ka) >> 1));
-            sacc[t][i] = ((hsh & 0xffffu) >= thr) ? p0 * dscale : 0.f;
-            sacc[t][i + 1] = ((hsh >> 16) >= thr) ? p1 * dscale : 0.f;
-          } else {
-            sacc[t][i] = p0;
-            sacc[t][i + 1] = p1;
-          }
-        }
-      }
-      // O^T[d][q] += V^T[d][key] . P^T[key][q]
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const bf16x8_t pb = acc_frag(sacc[kk >> 1], kk & 1);
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) oacc[dt] = mfma(tr_frag(Vt, kk, dt, lane), pb, oacc[dt]);
-      }
-    }
+    if (k0 + KVB - 1 <= q0 && k0 + KVB <= S)
+      fwd_tile<false, DROP>(fs, Kt, Vt, qf, k0, qa, S, lane, c_log2, mrow);
+    else if (k0 <= q0 + 31)
+      fwd_tile<true, DROP>(fs, Kt, Vt, qf, k0, qa, S, lane, c_log2, mrow);
     if (more) {
       bf16_t* Kn = lds + (cur ^ 1) * 2 * KVB * HD;
       stage_store(sk, Kn, tid);
@@ -242,10 +286,10 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const bf16_t* __restrict__ q, 
     __syncthreads();
   }
 
-  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
-  const float inv_l = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  const float l_tot = fs.l + __shfl_xor(fs.l, 32, 64);
+  const float inv_l = (DROP ? dscale : 1.f) / l_tot;
   if (qa < S) {
-    if (h == 0) lse[(size_t)bh * S + qa] = (m_run + log2f(l_tot)) * 0.69314718055994530942f;
+    if (h == 0) lse[(size_t)bh * S + qa] = fs.m * (c_log2 / LOG2E) + __logf(l_tot);
     bf16_t* orow = o + (((size_t)b * S + qa) * nh + head) * HD;
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt)
@@ -253,7 +297,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const bf16_t* __restrict__ q, 
       for (int g = 0; g < 4; ++g) {
         u16x4 w;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) w.v[e] = f2bf(oacc[dt][4 * g + e] * inv_l);
+        for (int e = 0; e < 4; ++e) w.v[e] = f2bf(fs.o[dt][4 * g + e] * inv_l);
         *reinterpret_cast<u16x4*>(orow + 32 * dt + 8 * g + 4 * h) = w;
       }
   }
@@ -282,57 +326,123 @@ __global__ __launch_bounds__(256) void k_attn_bwd_delta(const bf16_t* __restrict
   delta[((size_t)b * nh + head) * S + s] = acc;
 }
 
-// dK, dV: one workgroup per 128 keys (32 per wave), sweep query tiles of 64.
-template <bool DROP>
-__global__ __launch_bounds__(256) void k_attn_bwd_dkdv(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
-                                                       const bf16_t* __restrict__ v, const bf16_t* __restrict__ dout,
-                                                       const float* __restrict__ lse, const float* __restrict__ delta,
-                                                       bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, int S, int nh,
-                                                       float c_log2, float scale, uint32_t key, uint32_t thr,
-                                                       float dscale) {
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * 2 * QSTEP * HD];  // [buf][Q|dO][64][64]
-  __shared__ __attribute__((aligned(16))) float rowc[2][2][QSTEP];          // [buf][lse2|delta][64]
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+// ---------------------------------------------------------------- dK / dV
+// One workgroup per 128 keys (32 per wave); sweep query tiles of 64 (two 32-row
+// sub-tiles).  Accumulators: S and dP with queries in registers, keys on lanes.
+template <bool MASK, bool DROP>
+__device__ __forceinline__ void dkdv_subtile(floatx16_t (&dka)[2], floatx16_t (&dva)[2], const bf16_t* Qt,
+                                             const bf16_t* Dt, const float* rl, const float* rd,
+                                             const uint32_t* mw, const bf16x8_t (&kf)[4], const bf16x8_t (&vf)[4],
+                                             int qs, int ka, int S, int lane, int wid, float c_log2, float dscale) {
   const int h = lane >> 5, kl = lane & 31;
-  const int kblk = blockIdx.x;  // early key blocks are the heaviest; they launch first
+  floatx16_t sacc = zero16(), pacc = zero16();
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    sacc = mfma(lds_row8(Qt, kl, 16 * s + 8 * h), kf[s], sacc);
+    pacc = mfma(lds_row8(Dt, kl, 16 * s + 8 * h), vf[s], pacc);
+  }
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const float4 l4 = *reinterpret_cast<const float4*>(rl + 8 * g + 4 * h);
+    const float4 d4 = *reinterpret_cast<const float4*>(rd + 8 * g + 4 * h);
+    const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
+    const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int i = 4 * g + e;
+      const int r = 8 * g + 4 * h + e;  // query row within the sub-tile
+      float p = fast_exp2(fmaf(sacc[i], c_log2, -lv[e]));
+      if (MASK) {
+        const int qa = qs + r;
+        p = (ka > qa || qa >= S || ka >= S) ? 0.f : p;
+      }
+      float dp = pacc[i];
+      float pd = p;
+      if (DROP) {
+        const bool keep = (mw[r * 4 + wid] >> kl) & 1u;
+        pd = keep ? p : 0.f;  // 1/(1-p) folded into the dV epilogue
+        dp = keep ? dp * dscale : 0.f;
+      }
+      sacc[i] = pd;               // dropped P  -> dV
+      pacc[i] = p * (dp - dv[e]); // dS         -> dK
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const bf16x8_t pb = acc_frag(sacc, s);
+    const bf16x8_t sb = acc_frag(pacc, s);
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      dva[dt] = mfma(tr_frag(Dt, s, dt, lane), pb, dva[dt]);
+      dka[dt] = mfma(tr_frag(Qt, s, dt, lane), sb, dka[dt]);
+    }
+  }
+}
+
+template <bool DROP>
+__global__ __launch_bounds__(256, 2) void k_attn_bwd_dkdv(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
+                                                          const bf16_t* __restrict__ v,
+                                                          const bf16_t* __restrict__ dout,
+                                                          const float* __restrict__ lse,
+                                                          const float* __restrict__ delta,
+                                                          const uint32_t* __restrict__ mask, bf16_t* __restrict__ dk,
+                                                          bf16_t* __restrict__ dv, int S, int nh, float c_log2,
+                                                          float scale, float dscale) {
+  // one LDS object (avoids hipcc's extra vmcnt waits with several __shared__ arrays)
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * QSTEP * HD * 2 + 2 * 2 * QSTEP * 4 + 2 * QSTEP * 4 * 4];
+  bf16_t* lds = reinterpret_cast<bf16_t*>(smem);                              // [buf][Q|dO][64][64]
+  float* rowc = reinterpret_cast<float*>(smem + 2 * 2 * QSTEP * HD * 2);      // [buf][lse2|delta][64]
+  uint32_t* mws = reinterpret_cast<uint32_t*>(smem + 2 * 2 * QSTEP * HD * 2 + 2 * 2 * QSTEP * 4);  // [buf][64][4]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, kl = lane & 31;
+  const int kblk = blockIdx.x;  // early key blocks are the heaviest and launch first
   const int bh = blockIdx.y;
   const int b = bh / nh, head = bh % nh;
   const size_t hoff = (size_t)bh * S * HD;
-  const int k0 = kblk * KB + wid * 32;
+  const int k0 = kblk * KB + wid * 32;  // wave-uniform
   const int ka = k0 + kl;
-  const uint32_t kbh = lowbias32(key + (uint32_t)bh * 0x9E3779B9u);
   const int rstride = nh * HD;
-  const bf16_t* dob = dout + ((size_t)b * S * nh + head) * HD;  // row s at dob + s*rstride
+  const int W = (S + 31) >> 5;
+  const bf16_t* dob = dout + ((size_t)b * S * nh + head) * HD;
 
   bf16x8_t kf[4], vf[4];
+  const int kc = min(ka, S - 1);
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    kf[s] = load_row8(k + hoff + (size_t)ka * HD + 16 * s + 8 * h, ka < S);
-    vf[s] = load_row8(v + hoff + (size_t)ka * HD + 16 * s + 8 * h, ka < S);
+    kf[s] = load_row8(k + hoff + (size_t)kc * HD + 16 * s + 8 * h, ka < S);
+    vf[s] = load_row8(v + hoff + (size_t)kc * HD + 16 * s + 8 * h, ka < S);
   }
-  floatx16_t dka[2], dva[2];
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) { dka[dt][i] = 0.f; dva[dt][i] = 0.f; }
+  floatx16_t dka[2] = {zero16(), zero16()}, dva[2] = {zero16(), zero16()};
 
   const int qt_begin = (kblk * KB) / QSTEP;
   const int nqt = (S + QSTEP - 1) / QSTEP;
   Stage2 sq, sd;
   float rl = 0.f, rd = 0.f;
+  uint32_t mwv = 0;
   auto load_rows = [&](int t) {
-    stage_load(sq, q + hoff, t * QSTEP, S, tid);
-    stage_load_bsh(sd, dob, t * QSTEP, S, rstride, tid);
+    stage_load(sq, q + hoff, t * QSTEP, S, HD, tid);
+    stage_load(sd, dob, t * QSTEP, S, rstride, tid);
     if (tid < QSTEP) {
-      const int qq = t * QSTEP + tid;
-      rl = qq < S ? lse[(size_t)bh * S + qq] * 1.44269504088896340736f : 0.f;
-      rd = qq < S ? delta[(size_t)bh * S + qq] : 0.f;
+      const int qq = min(t * QSTEP + tid, S - 1);
+      const bool ok = t * QSTEP + tid < S;
+      rl = ok ? lse[(size_t)bh * S + qq] * LOG2E : 0.f;
+      rd = ok ? delta[(size_t)bh * S + qq] : 0.f;
+    }
+    if (DROP) {
+      const int qq = t * QSTEP + (tid >> 2);
+      const int wi = kblk * 4 + (tid & 3);
+      mwv = (qq < S && wi < W) ? mask[((size_t)bh * S + qq) * W + wi] : 0u;
     }
   };
   auto store_rows = [&](int buf) {
     stage_store(sq, lds + buf * 2 * QSTEP * HD, tid);
     stage_store(sd, lds + buf * 2 * QSTEP * HD + QSTEP * HD, tid);
-    if (tid < QSTEP) { rowc[buf][0][tid] = rl; rowc[buf][1][tid] = rd; }
+    if (tid < QSTEP) {
+      rowc[buf * 2 * QSTEP + tid] = rl;
+      rowc[buf * 2 * QSTEP + QSTEP + tid] = rd;
+    }
+    if (DROP) mws[buf * QSTEP * 4 + tid] = mwv;
   };
   if (qt_begin < nqt) {
     load_rows(qt_begin);
@@ -346,56 +456,20 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(const bf16_t* __restrict_
     if (more) load_rows(t + 1);
     const bf16_t* Qt = lds + cur * 2 * QSTEP * HD;
     const bf16_t* Dt = Qt + QSTEP * HD;
+    const float* rlp = rowc + cur * 2 * QSTEP;
+    const float* rdp = rlp + QSTEP;
+    const uint32_t* mwp = mws + cur * QSTEP * 4;
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
       const int qs = t * QSTEP + 32 * qt;
-      if (qs + 31 < k0) continue;  // fully masked (wave-uniform)
-      floatx16_t sacc, pacc;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) { sacc[i] = 0.f; pacc[i] = 0.f; }
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        sacc = mfma(lds_row8(Qt, 32 * qt + kl, 16 * s + 8 * h), kf[s], sacc);
-        pacc = mfma(lds_row8(Dt, 32 * qt + kl, 16 * s + 8 * h), vf[s], pacc);
-      }
-      // rows of the accumulators are queries qs + acc_row(i,h); lanes are keys
-      const bool need_mask = (qs < k0 + 31) || (qs + 32 > S) || (k0 + 32 > S);
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 l4 = *reinterpret_cast<const float4*>(&rowc[cur][0][32 * qt + 8 * g + 4 * h]);
-        const float4 d4 = *reinterpret_cast<const float4*>(&rowc[cur][1][32 * qt + 8 * g + 4 * h]);
-        const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
-        const float dvv[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int i = 4 * g + e;
-          const int qa = qs + 8 * g + 4 * h + e;
-          float p = exp2f(sacc[i] * c_log2 - lv[e]);
-          if (need_mask && (ka > qa || qa >= S || ka >= S)) p = 0.f;
-          float dp = pacc[i];
-          float pd = p;
-          if (DROP) {
-            const uint32_t idx = (uint32_t)qa * (uint32_t)S + (uint32_t)ka;
-            const uint32_t hsh = lowbias32(kbh ^ (idx >> 1));
-            const uint32_t bits = (idx & 1) ? (hsh >> 16) : (hsh & 0xffffu);
-            const bool keep = bits >= thr;
-            pd = keep ? p * dscale : 0.f;
-            dp = keep ? dp * dscale : 0.f;
-          }
-          sacc[i] = pd;                   // P (dropped) for dV
-          pacc[i] = p * (dp - dvv[e]);    // dS
-        }
-      }
-      // dV^T += dO^T . Pd ;  dK^T += Q^T . dS   (sum over the 32 queries of this sub-tile)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8_t pb = acc_frag(sacc, s);
-        const bf16x8_t sb = acc_frag(pacc, s);
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-          dva[dt] = mfma(tr_frag(Dt + 32 * qt * HD, s, dt, lane), pb, dva[dt]);
-          dka[dt] = mfma(tr_frag(Qt + 32 * qt * HD, s, dt, lane), sb, dka[dt]);
-        }
+      const bf16_t* Qs = Qt + 32 * qt * HD;
+      const bf16_t* Ds = Dt + 32 * qt * HD;
+      if (qs >= k0 + 31 && qs + 32 <= S && k0 + 32 <= S) {
+        dkdv_subtile<false, DROP>(dka, dva, Qs, Ds, rlp + 32 * qt, rdp + 32 * qt, mwp + 32 * qt * 4, kf, vf, qs, ka,
+                                  S, lane, wid, c_log2, dscale);
+      } else if (qs + 31 >= k0) {
+        dkdv_subtile<true, DROP>(dka, dva, Qs, Ds, rlp + 32 * qt, rdp + 32 * qt, mwp + 32 * qt * 4, kf, vf, qs, ka,
+                                 S, lane, wid, c_log2, dscale);
       }
     }
     if (more) store_rows(cur ^ 1);
@@ -413,7 +487,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(const bf16_t* __restrict_
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           wk.v[e] = f2bf(dka[dt][4 * g + e] * scale);
-          wv.v[e] = f2bf(dva[dt][4 * g + e]);
+          wv.v[e] = f2bf(dva[dt][4 * g + e] * (DROP ? dscale : 1.f));
         }
         *reinterpret_cast<u16x4*>(dkr + 32 * dt + 8 * g + 4 * h) = wk;
         *reinterpret_cast<u16x4*>(dvr + 32 * dt + 8 * g + 4 * h) = wv;
@@ -421,15 +495,59 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(const bf16_t* __restrict_
   }
 }
 
-// dQ: one workgroup per 128 queries (32 per wave), sweep key tiles of 64; recomputes S, dP.
+// ---------------------------------------------------------------------- dQ
+template <bool MASK, bool DROP>
+__device__ __forceinline__ void dq_tile(floatx16_t (&dqa)[2], const bf16_t* Kt, const bf16_t* Vt,
+                                        const bf16x8_t (&qf)[4], const bf16x8_t (&df)[4], int k0, int qa, int S,
+                                        int lane, float c_log2, float nl2, float dl, float dscale,
+                                        const uint32_t* __restrict__ mrow) {
+  const int h = lane >> 5, ql = lane & 31;
+  floatx16_t sacc[2], pacc[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    sacc[t] = zero16();
+    pacc[t] = zero16();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      sacc[t] = mfma(lds_row8(Kt, 32 * t + ql, 16 * s + 8 * h), qf[s], sacc[t]);
+      pacc[t] = mfma(lds_row8(Vt, 32 * t + ql, 16 * s + 8 * h), df[s], pacc[t]);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    uint32_t word = 0;
+    if (DROP) word = mrow[(k0 + 32 * t) >> 5];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int kr = acc_row(i, h);
+      float p = fast_exp2(fmaf(sacc[t][i], c_log2, nl2));
+      if (MASK) {
+        const int kA = k0 + 32 * t + kr;
+        p = (kA > qa || kA >= S) ? 0.f : p;
+      }
+      float dp = pacc[t][i];
+      if (DROP) dp = ((word >> kr) & 1u) ? dp * dscale : 0.f;
+      pacc[t][i] = p * (dp - dl);
+    }
+  }
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    const bf16x8_t sb = acc_frag(pacc[kk >> 1], kk & 1);
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) dqa[dt] = mfma(tr_frag(Kt, kk, dt, lane), sb, dqa[dt]);
+  }
+}
+
 template <bool DROP>
-__global__ __launch_bounds__(256) void k_attn_bwd_dq(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
-                                                     const bf16_t* __restrict__ v, const bf16_t* __restrict__ dout,
-                                                     const float* __restrict__ lse, const float* __restrict__ delta,
-                                                     bf16_t* __restrict__ dq, int S, int nh, float c_log2, float scale,
-                                                     uint32_t key, uint32_t thr, float dscale) {
+__global__ __launch_bounds__(256, 2) void k_attn_bwd_dq(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
+                                                        const bf16_t* __restrict__ v, const bf16_t* __restrict__ dout,
+                                                        const float* __restrict__ lse,
+                                                        const float* __restrict__ delta,
+                                                        const uint32_t* __restrict__ mask, bf16_t* __restrict__ dq,
+                                                        int S, int nh, float c_log2, float scale, float dscale) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * 2 * KVB * HD];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, ql = lane & 31;
   const int nqb = (S + QB - 1) / QB;
   const int qb = nqb - 1 - blockIdx.x;
@@ -439,85 +557,44 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(const bf16_t* __restrict__ 
   const int q0 = qb * QB + wid * 32;
   const int qa = q0 + ql;
   const bool qok = qa < S;
-  const uint32_t kbh = lowbias32(key + (uint32_t)bh * 0x9E3779B9u);
+  const int qc = min(qa, S - 1);
+  const int W = (S + 31) >> 5;
+  const uint32_t* mrow = mask ? mask + ((size_t)bh * S + qc) * W : nullptr;
 
   bf16x8_t qf[4], df[4];
-  const bf16_t* dorow = dout + (((size_t)b * S + (qok ? qa : 0)) * nh + head) * HD;
+  const bf16_t* dorow = dout + (((size_t)b * S + qc) * nh + head) * HD;
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    qf[s] = load_row8(q + hoff + (size_t)qa * HD + 16 * s + 8 * h, qok);
+    qf[s] = load_row8(q + hoff + (size_t)qc * HD + 16 * s + 8 * h, qok);
     df[s] = load_row8(dorow + 16 * s + 8 * h, qok);
   }
-  const float l2 = qok ? lse[(size_t)bh * S + qa] * 1.44269504088896340736f : 0.f;
-  const float dl = qok ? delta[(size_t)bh * S + qa] : 0.f;
-  floatx16_t dqa[2];
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) dqa[dt][i] = 0.f;
+  const float nl2 = qok ? -lse[(size_t)bh * S + qc] * LOG2E : 0.f;
+  const float dl = qok ? delta[(size_t)bh * S + qc] : 0.f;
+  floatx16_t dqa[2] = {zero16(), zero16()};
 
   const int kv_end = min(S, qb * QB + QB);
   const int nkv = (kv_end + KVB - 1) / KVB;
   Stage2 sk, sv;
-  stage_load(sk, k + hoff, 0, S, tid);
-  stage_load(sv, v + hoff, 0, S, tid);
+  stage_load(sk, k + hoff, 0, S, HD, tid);
+  stage_load(sv, v + hoff, 0, S, HD, tid);
   stage_store(sk, lds, tid);
   stage_store(sv, lds + KVB * HD, tid);
   __syncthreads();
-  const uint32_t rowidx = (uint32_t)qa * (uint32_t)S;
 
   for (int kb = 0; kb < nkv; ++kb) {
     const int cur = kb & 1;
     const bool more = kb + 1 < nkv;
     if (more) {
-      stage_load(sk, k + hoff, (kb + 1) * KVB, S, tid);
-      stage_load(sv, v + hoff, (kb + 1) * KVB, S, tid);
+      stage_load(sk, k + hoff, (kb + 1) * KVB, S, HD, tid);
+      stage_load(sv, v + hoff, (kb + 1) * KVB, S, HD, tid);
     }
     const bf16_t* Kt = lds + cur * 2 * KVB * HD;
     const bf16_t* Vt = Kt + KVB * HD;
     const int k0 = kb * KVB;
-    if (k0 <= q0 + 31) {
-      floatx16_t sacc[2], pacc[2];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) { sacc[t][i] = 0.f; pacc[t][i] = 0.f; }
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          sacc[t] = mfma(lds_row8(Kt, 32 * t + ql, 16 * s + 8 * h), qf[s], sacc[t]);
-          pacc[t] = mfma(lds_row8(Vt, 32 * t + ql, 16 * s + 8 * h), df[s], pacc[t]);
-        }
-      }
-      const bool need_mask = (k0 + KVB - 1 > q0) || (k0 + KVB > S);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-#pragma unroll
-        for (int i = 0; i < 16; i += 2) {
-          const int kA = k0 + 32 * t + acc_row(i, h);
-          float p0 = exp2f(sacc[t][i] * c_log2 - l2);
-          float p1 = exp2f(sacc[t][i + 1] * c_log2 - l2);
-          if (need_mask) {
-            if (kA > qa || kA >= S) p0 = 0.f;
-            if (kA + 1 > qa || kA + 1 >= S) p1 = 0.f;
-          }
-          float dp0 = pacc[t][i], dp1 = pacc[t][i + 1];
-          if (DROP) {
-            const uint32_t hsh = lowbias32(kbh ^ ((rowidx + (uint32_t)kA) >> 1));
-            dp0 = ((hsh & 0xffffu) >= thr) ? dp0 * dscale : 0.f;
-            dp1 = ((hsh >> 16) >= thr) ? dp1 * dscale : 0.f;
-          }
-          pacc[t][i] = p0 * (dp0 - dl);
-          pacc[t][i + 1] = p1 * (dp1 - dl);
-        }
-      }
-      // dQ^T[d][q] += K^T[d][key] . dS^T[key][q]
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const bf16x8_t sb = acc_frag(pacc[kk >> 1], kk & 1);
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) dqa[dt] = mfma(tr_frag(Kt, kk, dt, lane), sb, dqa[dt]);
-      }
-    }
+    if (k0 + KVB - 1 <= q0 && k0 + KVB <= S)
+      dq_tile<false, DROP>(dqa, Kt, Vt, qf, df, k0, qa, S, lane, c_log2, nl2, dl, dscale, mrow);
+    else if (k0 <= q0 + 31)
+      dq_tile<true, DROP>(dqa, Kt, Vt, qf, df, k0, qa, S, lane, c_log2, nl2, dl, dscale, mrow);
     if (more) {
       bf16_t* Kn = lds + (cur ^ 1) * 2 * KVB * HD;
       stage_store(sk, Kn, tid);
@@ -540,33 +617,40 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(const bf16_t* __restrict__ 
 }
 
 // ============================================================================ launchers
-DLT_API int dlt_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int nh,
-                         int S, int hd, float scale, uint32_t key, uint32_t thr, float dscale, hipStream_t st) {
+// mask: uint32 [B*nh, S, ceil(S/32)] keep-bits written by the forward when dropout is
+// on (may be null: then the forward only regenerates masks on the fly).
+DLT_API int dlt_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, uint32_t* mask,
+                         int B, int nh, int S, int hd, float scale, uint32_t key, uint32_t thr, float dscale,
+                         hipStream_t st) {
   if (hd != HD || S <= 0) return -1;
+  if (thr && !mask) return -2;  // dropout needs the keep-bit buffer
   const dim3 grid((S + QB - 1) / QB, B * nh);
-  const float c_log2 = scale * 1.44269504088896340736f;
-  if (thr)
-    k_attn_fwd<true><<<grid, 256, 0, st>>>(q, k, v, o, lse, S, nh, c_log2, key, thr, dscale);
-  else
-    k_attn_fwd<false><<<grid, 256, 0, st>>>(q, k, v, o, lse, S, nh, c_log2, key, thr, dscale);
+  const float c_log2 = scale * LOG2E;
+  if (thr) {
+    const int words = S * ((S + 31) / 32);
+    k_dropout_bits<<<dim3((words + 255) / 256, B * nh), 256, 0, st>>>(mask, B * nh, S, key, thr);
+    k_attn_fwd<true><<<grid, 256, 0, st>>>(q, k, v, o, lse, mask, S, nh, c_log2, dscale);
+  } else {
+    k_attn_fwd<false><<<grid, 256, 0, st>>>(q, k, v, o, lse, nullptr, S, nh, c_log2, dscale);
+  }
   DLT_CHECK_LAUNCH();
 }
 
 DLT_API int dlt_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,
-                         const float* lse, float* delta_ws, bf16_t* dq, bf16_t* dk, bf16_t* dv, int B, int nh, int S,
-                         int hd, float scale, uint32_t key, uint32_t thr, float dscale, hipStream_t st) {
+                         const float* lse, const uint32_t* mask, float* delta_ws, bf16_t* dq, bf16_t* dk, bf16_t* dv,
+                         int B, int nh, int S, int hd, float scale, float dscale, hipStream_t st) {
   if (hd != HD || S <= 0) return -1;
   const int rows = B * S * nh;
   k_attn_bwd_delta<<<(rows + 255) / 256, 256, 0, st>>>(o, dout, delta_ws, B, S, nh);
-  const float c_log2 = scale * 1.44269504088896340736f;
+  const float c_log2 = scale * LOG2E;
   const dim3 gk((S + KB - 1) / KB, B * nh);
   const dim3 gq((S + QB - 1) / QB, B * nh);
-  if (thr) {
-    k_attn_bwd_dkdv<true><<<gk, 256, 0, st>>>(q, k, v, dout, lse, delta_ws, dk, dv, S, nh, c_log2, scale, key, thr, dscale);
-    k_attn_bwd_dq<true><<<gq, 256, 0, st>>>(q, k, v, dout, lse, delta_ws, dq, S, nh, c_log2, scale, key, thr, dscale);
+  if (mask) {
+    k_attn_bwd_dkdv<true><<<gk, 256, 0, st>>>(q, k, v, dout, lse, delta_ws, mask, dk, dv, S, nh, c_log2, scale, dscale);
+    k_attn_bwd_dq<true><<<gq, 256, 0, st>>>(q, k, v, dout, lse, delta_ws, mask, dq, S, nh, c_log2, scale, dscale);
   } else {
-    k_attn_bwd_dkdv<false><<<gk, 256, 0, st>>>(q, k, v, dout, lse, delta_ws, dk, dv, S, nh, c_log2, scale, key, thr, dscale);
-    k_attn_bwd_dq<false><<<gq, 256, 0, st>>>(q, k, v, dout, lse, delta_ws, dq, S, nh, c_log2, scale, key, thr, dscale);
+    k_attn_bwd_dkdv<false><<<gk, 256, 0, st>>>(q, k, v, dout, lse, delta_ws, mask, dk, dv, S, nh, c_log2, scale, dscale);
+    k_attn_bwd_dq<false><<<gq, 256, 0, st>>>(q, k, v, dout, lse, delta_ws, mask, dq, S, nh, c_log2, scale, dscale);
   }
   DLT_CHECK_LAUNCH();
 }

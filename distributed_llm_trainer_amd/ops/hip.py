@@ -43,10 +43,10 @@ _SIGS = {
     "dlt_adamw": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float, c_float,
                   c_float, c_float, c_float, c_void_p, c_void_p],
     "dlt_cast_bf16": [c_void_p, c_void_p, c_int64, c_void_p],
-    "dlt_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_uint32,
-                     c_uint32, c_float, c_void_p],
+    "dlt_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
+                     c_uint32, c_uint32, c_float, c_void_p],
     "dlt_attn_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                     c_void_p, c_int, c_int, c_int, c_int, c_float, c_uint32, c_uint32, c_float, c_void_p],
+                     c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_float, c_void_p],
 }
 
 
@@ -211,7 +211,13 @@ def rope_qkv_bwd(dq, dk, dv, cos, sin):
 
 
 # -------------------------------------------------------------- attention
-def attention_fwd(q, k, v, p, key, causal=True):
+class AttnAux(tuple):
+    """(lse [B,nh,S] fp32, keep-bit mask [B*nh, S, ceil(S/32)] uint32 or None)."""
+
+
+def attention_fwd(q, k, v, p, key, causal=True, store_mask=True):
+    """Returns (o [B*S, nh*hd] bf16, aux).  With dropout on, the keep bits are written
+    to a bitmask consumed by attention_bwd (no re-hashing in the backward)."""
     if not causal:
         raise NotImplementedError("only causal attention is implemented (the model is a causal LM)")
     B, nh, S, hd = q.shape
@@ -223,25 +229,38 @@ def attention_fwd(q, k, v, p, key, causal=True):
     lse = torch.empty(B, nh, S, dtype=torch.float32, device=q.device)
     thr = rng.keep_threshold(p)
     dscale = 1.0 / (1.0 - p) if thr else 1.0
-    _chk(lib().dlt_attn_fwd(_p(q), _p(k), _p(v), _p(o), _p(lse), B, nh, S, hd, 1.0 / math.sqrt(hd),
+    mask = None
+    if thr and store_mask:
+        mask = torch.empty(B * nh, S, (S + 31) // 32, dtype=torch.int32, device=q.device)
+    _chk(lib().dlt_attn_fwd(_p(q), _p(k), _p(v), _p(o), _p(lse), _p(mask), B, nh, S, hd, 1.0 / math.sqrt(hd),
                             key & 0xFFFFFFFF, thr, dscale, _stream()), "attn_fwd")
-    return o, lse
+    return o, AttnAux((lse, mask))
 
 
-def attention_bwd(q, k, v, o, do, lse, p, key, causal=True):
+def attention_bwd(q, k, v, o, do, aux, p, key, causal=True):
     B, nh, S, hd = q.shape
     n = B * nh * S * hd
     for t, nm in ((q, "q"), (k, "k"), (v, "v"), (o, "o"), (do, "do")):
         _req(t, torch.bfloat16, "attn_bwd." + nm, n)
+    if isinstance(aux, tuple):
+        lse, mask = aux
+    else:
+        lse, mask = aux, None
     _req(lse, torch.float32, "attn_bwd.lse", B * nh * S)
+    thr = rng.keep_threshold(p)
+    if thr and mask is None:
+        # regenerate the keep bits (e.g. forward ran with store_mask=False)
+        _, aux2 = attention_fwd(q, k, v, p, key, causal, store_mask=True)
+        mask = aux2[1]
+    if not thr:
+        mask = None
     delta = torch.empty(B, nh, S, dtype=torch.float32, device=q.device)
     dq = torch.empty_like(q)
     dk = torch.empty_like(k)
     dv = torch.empty_like(v)
-    thr = rng.keep_threshold(p)
     dscale = 1.0 / (1.0 - p) if thr else 1.0
-    _chk(lib().dlt_attn_bwd(_p(q), _p(k), _p(v), _p(o), _p(do), _p(lse), _p(delta), _p(dq), _p(dk), _p(dv),
-                            B, nh, S, hd, 1.0 / math.sqrt(hd), key & 0xFFFFFFFF, thr, dscale, _stream()), "attn_bwd")
+    _chk(lib().dlt_attn_bwd(_p(q), _p(k), _p(v), _p(o), _p(do), _p(lse), _p(mask), _p(delta), _p(dq), _p(dk), _p(dv),
+                            B, nh, S, hd, 1.0 / math.sqrt(hd), dscale, _stream()), "attn_bwd")
     return dq, dk, dv
 
 

@@ -157,9 +157,18 @@ def test_attention_fwd(S, p):
     B, nh = 2, 3
     q, k, v = _attn_inputs(B, nh, S, 10 + S)
     key = rng.site_key(1, 2, 3, rng.SITE_ATTN)
-    o, lse = hip.attention_fwd(q, k, v, p, key)
+    o, aux = hip.attention_fwd(q, k, v, p, key)
+    lse = aux[0]
     o2, lse2 = ref.attention_fwd(q, k, v, p, key)
     _close(lse, lse2, 2e-3, 1e-4, "lse")
+    if p > 0:
+        keep = rng.attn_keep_mask(B * nh, S, S, key, p, device=DEV)
+        W = (S + 31) // 32
+        bits = aux[1].view(B * nh, S, W)
+        kk = torch.arange(S, device=DEV)
+        got = ((bits[:, :, kk // 32].long() >> (kk % 32)) & 1).bool()
+        causal = torch.tril(torch.ones(S, S, dtype=torch.bool, device=DEV))
+        assert torch.equal(got & causal, keep & causal), "stored dropout bitmask differs from the hash"
     _close(o, o2.float(), 2e-2, 2e-2, "o")
 
 
@@ -173,8 +182,8 @@ def test_attention_fwd_identity_asymmetric():
         k[0, 0, j, 0] = 1.0 if j % 2 == 0 else -1.0
     v = torch.arange(S * 64, device=DEV, dtype=torch.float32).view(1, 1, S, 64) / (S * 64)
     q, k, v = q.bfloat16(), k.bfloat16(), v.bfloat16()
-    o, lse = hip.attention_fwd(q, k, v, 0.0, 0)
-    o2, lse2 = ref.attention_fwd(q, k, v, 0.0, 0)
+    o, _ = hip.attention_fwd(q, k, v, 0.0, 0)
+    o2, _ = ref.attention_fwd(q, k, v, 0.0, 0)
     _close(o, o2.float(), 1e-2, 1e-2, "o(asym)")
 
 
@@ -186,7 +195,10 @@ def test_attention_bwd(S, p):
     key = rng.site_key(4, 5, 6, rng.SITE_ATTN)
     o, lse = ref.attention_fwd(q, k, v, p, key)
     do = torch.randn_like(o.float()).bfloat16()
-    dq, dk, dv = hip.attention_bwd(q, k, v, o, do, lse, p, key)
+    dq, dk, dv = hip.attention_bwd(q, k, v, o, do, lse, p, key)  # regenerates the bitmask
+    _, aux = hip.attention_fwd(q, k, v, p, key)
+    dq3, dk3, dv3 = hip.attention_bwd(q, k, v, o, do, (lse, aux[1]), p, key)
+    assert torch.equal(dq, dq3) and torch.equal(dk, dk3) and torch.equal(dv, dv3)
     dq2, dk2, dv2 = ref.attention_bwd(q, k, v, o, do, lse, p, key)
     for a, b, n in ((dq, dq2, "dq"), (dk, dk2, "dk"), (dv, dv2, "dv")):
         scale = b.float().abs().max().item()

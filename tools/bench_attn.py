@@ -1,0 +1,45 @@
+"""Micro-benchmark of the attention kernels at the headline shape (B8 nh12 S1024 hd64)."""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from distributed_llm_trainer_amd.ops import hip, rng  # noqa: E402
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--B", type=int, default=8)
+    ap.add_argument("--nh", type=int, default=12)
+    ap.add_argument("--S", type=int, default=1024)
+    ap.add_argument("--p", type=float, default=0.1)
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    torch.manual_seed(0)
+    q, k, v = (torch.randn(a.B, a.nh, a.S, 64, device="cuda").bfloat16() for _ in range(3))
+    key = rng.site_key(1, 2, 3, rng.SITE_ATTN)
+    o, aux = hip.attention_fwd(q, k, v, a.p, key)
+    do = torch.randn_like(o)
+    t_f = timeit(lambda: hip.attention_fwd(q, k, v, a.p, key), a.iters)
+    t_b = timeit(lambda: hip.attention_bwd(q, k, v, o, do, aux, a.p, key), a.iters)
+    fl = 4 * a.B * a.nh * a.S * a.S / 2 * 64
+    print(f"fwd {t_f:.1f} us ({fl / t_f / 1e6:.1f} TF/s)  bwd {t_b:.1f} us ({2.5 * fl / t_b / 1e6:.1f} TF/s)")
+
+
+if __name__ == "__main__":
+    main()
