@@ -1,0 +1,121 @@
+"""KV-cached autoregressive decoding for ``GPT.generate`` on the engine path.
+
+The reference's ``generate`` (``gpt.py:457-484``) re-runs the full forward over the
+whole context for every new token (O(T^2) work).  Here the prompt is
+prefilled once, per-layer K/V (already RoPE-rotated) are cached in preallocated
+``[B, nh, max_seq_len, hd]`` buffers, and each new token costs one token's worth of
+GEMV + attention.  Sampling semantics are the reference's: temperature, top-k
+filtering (``logits < kth`` -> -inf), softmax, ``torch.multinomial``; contexts longer
+than ``max_seq_len`` are cropped to the last ``max_seq_len`` tokens (the cache is then
+re-prefilled on the cropped window so RoPE positions match the reference exactly).
+
+Weights are read from the engine's provider (bf16 shadows on GPU / FSDP gathered
+units), so generation works the same for single-GPU, DDP and FSDP-trained models.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+
+class KVCache:
+    def __init__(self, cfg, B: int, device, dtype):
+        self.k = [torch.zeros(B, cfg.num_heads, cfg.max_seq_len, cfg.head_dim, device=device, dtype=dtype)
+                  for _ in range(cfg.num_layers)]
+        self.v = [torch.zeros_like(t) for t in self.k]
+        self.len = 0
+
+
+def _rms(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    xf = x.float()
+    return xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+
+
+def _rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    # x [B, T, nh, hd] fp32; cos/sin [T, hd/2]
+    half = x.shape[-1] // 2
+    c, s = cos[None, :, None, :], sin[None, :, None, :]
+    x1, x2 = x[..., :half], x[..., half:]
+    return torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1)
+
+
+@torch.no_grad()
+def forward_cached(model, ids: torch.Tensor, cache: KVCache) -> torch.Tensor:
+    """Append ``ids`` [B, T] at positions cache.len.. ; returns last-position logits [B, V]."""
+    eng = model.engine
+    cfg = model.config
+    prov = eng.provider
+    dt = eng.act_dtype
+    B, T = ids.shape
+    p0 = cache.len
+    nh, hd = cfg.num_heads, cfg.head_dim
+    cos_t, sin_t = eng.rope(max(cfg.max_seq_len, p0 + T), ids.device)
+    cos, sin = cos_t[p0:p0 + T].float(), sin_t[p0:p0 + T].float()
+    prov.pre_forward("head")
+    hw = prov.head()
+    h = hw.embed.index_select(0, ids.reshape(-1)).float().view(B, T, -1)
+    scale = 1.0 / math.sqrt(hd)
+    for i in range(cfg.num_layers):
+        prov.pre_forward(i)
+        w = prov.layer(i)
+        n1 = _rms(h, w.ln1, eng.eps).to(dt)
+        qkv = torch.matmul(n1, w.wqkv.t()).float().view(B, T, 3, nh, hd)
+        q = _rope(qkv[:, :, 0], cos, sin)
+        k = _rope(qkv[:, :, 1], cos, sin)
+        v = qkv[:, :, 2]
+        cache.k[i][:, :, p0:p0 + T] = k.transpose(1, 2).to(dt)
+        cache.v[i][:, :, p0:p0 + T] = v.transpose(1, 2).to(dt)
+        K = cache.k[i][:, :, :p0 + T].float()
+        Vv = cache.v[i][:, :, :p0 + T].float()
+        qh = q.to(dt).float().transpose(1, 2)  # [B, nh, T, hd]
+        s = torch.matmul(qh, K.transpose(-2, -1)) * scale
+        if T > 1:
+            qpos = torch.arange(p0, p0 + T, device=ids.device)[:, None]
+            kpos = torch.arange(0, p0 + T, device=ids.device)[None, :]
+            s = s.masked_fill(kpos > qpos, float("-inf"))
+        pr = torch.softmax(s, dim=-1)
+        o = torch.matmul(pr, Vv).transpose(1, 2).reshape(B, T, nh * hd).to(dt)
+        h = h + torch.matmul(o, w.wo.t()).float()
+        n2 = _rms(h, w.ln2, eng.eps).to(dt)
+        gu = torch.matmul(n2, w.wgu.t()).float()
+        I = cfg.intermediate_size
+        a = (F.silu(gu[..., :I]) * gu[..., I:]).to(dt)
+        h = h + torch.matmul(a, w.wdown.t()).float()
+        prov.post_forward(i)
+    hw = prov.head()
+    nf = _rms(h[:, -1], hw.norm, eng.eps).to(dt)
+    logits = torch.matmul(nf, hw.lm_head.t())[:, :cfg.vocab_size].float()
+    prov.post_forward("head")
+    cache.len = p0 + T
+    return logits
+
+
+@torch.no_grad()
+def kv_cached_generate(model, input_ids: torch.Tensor, max_new_tokens: int = 100, temperature: float = 1.0,
+                       top_k: int = 50) -> torch.Tensor:
+    cfg = model.config
+    eng = model.engine
+    B = input_ids.shape[0]
+    cache = KVCache(cfg, B, input_ids.device, eng.act_dtype)
+    ctx = input_ids[:, -cfg.max_seq_len:]
+    logits = forward_cached(model, ctx, cache)
+    out = input_ids
+    for step in range(max_new_tokens):
+        lg = logits / temperature
+        if top_k > 0:
+            v, _ = torch.topk(lg, min(top_k, lg.size(-1)))
+            lg = lg.masked_fill(lg < v[:, [-1]], float("-inf"))
+        probs = F.softmax(lg, dim=-1)
+        nxt = torch.multinomial(probs, num_samples=1)
+        out = torch.cat([out, nxt], dim=1)
+        if step == max_new_tokens - 1:
+            break
+        if cache.len + 1 <= cfg.max_seq_len:
+            logits = forward_cached(model, nxt, cache)
+        else:  # context window full: re-prefill the cropped window (reference cropping semantics)
+            cache.len = 0
+            logits = forward_cached(model, out[:, -cfg.max_seq_len:], cache)
+    return out

@@ -93,7 +93,8 @@ class FlatAdamW:
                                self.step_count, sc)
             else:
                 ref.adamw_step(self.flat[a:b], self.grad[a:b], self.exp_avg[a:b], self.exp_avg_sq[a:b],
-                               None, lr, b1, b2, eps, wd, self.step_count, sc[1])
+                               None if self.shadow is None else self.shadow[a:b], lr, b1, b2, eps, wd,
+                               self.step_count, sc[1])
 
     def zero_grad(self, set_to_none: bool = True) -> None:
         # grads are persistent flat views; "set_to_none" semantics = zero the buffer

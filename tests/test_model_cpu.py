@@ -1,0 +1,161 @@
+"""CPU checks of the model and the fused executor (reference ops, fp32)."""
+import copy
+import math
+
+import pytest
+import torch
+
+from distributed_llm_trainer_amd.models import GPT, GPTConfig, count_parameters
+from distributed_llm_trainer_amd.models.engine import shift_targets
+
+
+def tiny(**kw):
+    d = dict(vocab_size=256, hidden_size=64, num_layers=2, num_heads=4, max_seq_len=32, dropout=0.0,
+             attention_dropout=0.0)
+    d.update(kw)
+    return GPTConfig(**d)
+
+
+@pytest.mark.parametrize("preset,expected", [("small", 151_862_784), ("medium", 454_166_528),
+                                             ("large", 1_008_140_800), ("xl", 2_046_646_400)])
+def test_param_counts(preset, expected):
+    cfg = GPTConfig.from_preset(preset)
+    assert cfg.num_parameters() == expected
+    if preset == "small":
+        assert count_parameters(GPT(cfg)) == expected
+        assert cfg.num_parameters_legacy() == 124_356_864
+
+
+def test_state_dict_keys_match_reference_schema():
+    m = GPT(GPTConfig.gpt2_small())
+    sd = m.state_dict()
+    assert len(sd) == 147
+    assert list(sd)[0] == "embed_tokens.weight" and list(sd)[-1] == "lm_head.weight"
+    assert sd["layers.0.attention.rotary_emb.cos_cached"].shape == (1024, 64)
+    assert sd["layers.0.attention.rotary_emb.inv_freq"].shape == (32,)
+    assert m.lm_head.weight.data_ptr() == m.embed_tokens.weight.data_ptr()
+
+
+def test_initial_loss_is_ln_vocab():
+    torch.manual_seed(0)
+    m = GPT(GPTConfig.gpt2_small())
+    ids = torch.randint(0, 50257, (2, 128))
+    _, loss = m(ids, labels=ids)
+    assert abs(loss.item() - math.log(50257)) < 0.15
+
+
+def test_rotate_half_example():
+    from distributed_llm_trainer_amd.models.gpt import rotate_half
+    assert rotate_half(torch.tensor([1.0, 2.0, 3.0, 4.0])).tolist() == [-3.0, -4.0, 1.0, 2.0]
+
+
+def _grads(m):
+    return {n: p.grad.clone() for n, p in m.named_parameters()}
+
+
+@pytest.mark.parametrize("recompute", [False, True])
+def test_engine_matches_eager_autograd(recompute):
+    torch.manual_seed(0)
+    m1 = GPT(tiny())
+    m2 = copy.deepcopy(m1)
+    ids = torch.randint(0, 256, (3, 32))
+    _, l1 = m1(ids, labels=ids)
+    (l1 * 0.5).backward()
+    m2.enable_engine()
+    m2.gradient_checkpointing = recompute
+    _, l2 = m2(ids, labels=ids)
+    assert l2.requires_grad
+    (l2 * 0.5).backward()
+    assert abs(l1.item() - l2.item()) < 1e-5
+    g1, g2 = _grads(m1), _grads(m2)
+    for n in g1:
+        assert torch.allclose(g1[n], g2[n], atol=1e-6, rtol=1e-4), n
+
+
+def test_ignore_index_labels():
+    torch.manual_seed(1)
+    m1 = GPT(tiny())
+    m2 = copy.deepcopy(m1)
+    ids = torch.randint(0, 256, (2, 32))
+    labels = ids.clone()
+    labels[:, 10:20] = -100
+    _, l1 = m1(ids, labels=labels)
+    m2.enable_engine()
+    _, l2 = m2(ids, labels=labels)
+    assert abs(l1.item() - l2.item()) < 1e-5
+
+
+def test_dropout_recompute_replays_masks():
+    """Activation checkpointing must reproduce identical dropout masks."""
+    torch.manual_seed(2)
+    cfg = tiny(dropout=0.1, attention_dropout=0.1)
+    m1 = GPT(cfg)
+    m2 = copy.deepcopy(m1)
+    m1.enable_engine(seed=11)
+    m2.enable_engine(seed=11)
+    m2.gradient_checkpointing = True
+    ids = torch.randint(0, 256, (2, 32))
+    _, l1 = m1(ids, labels=ids)
+    l1.backward()
+    _, l2 = m2(ids, labels=ids)
+    l2.backward()
+    assert l1.item() == l2.item()
+    for (n, p1), (_, p2) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert torch.allclose(p1.grad, p2.grad, atol=1e-7, rtol=1e-5), n
+
+
+def test_dropout_gradient_finite_difference():
+    """With deterministic counter-RNG masks the loss is a smooth function of the
+    weights; the engine's hand-written backward must match finite differences."""
+    torch.manual_seed(3)
+    cfg = tiny(dropout=0.1, attention_dropout=0.1, num_layers=1)
+    m = GPT(cfg).double() if False else GPT(cfg)
+    eng = m.enable_engine(seed=5)
+    ids = torch.randint(0, 256, (2, 32))
+    eng.micro_counter = 0
+    _, loss = m(ids, labels=ids)
+    loss.backward()
+    w = m.layers[0].mlp.up_proj.weight
+    g = w.grad.clone()
+    idx = [(3, 7), (10, 1), (100, 50)]
+    for (i, j) in idx:
+        old = w.data[i, j].item()
+        eps = 1e-3
+        w.data[i, j] = old + eps
+        eng.micro_counter = 0
+        with torch.no_grad():
+            lp = eng.forward(ids, shift_targets(ids), train=True, need_backward=False)[0].item()
+        w.data[i, j] = old - eps
+        eng.micro_counter = 0
+        with torch.no_grad():
+            lm = eng.forward(ids, shift_targets(ids), train=True, need_backward=False)[0].item()
+        w.data[i, j] = old
+        fd = (lp - lm) / (2 * eps)
+        assert abs(fd - g[i, j].item()) < 2e-3 + 2e-2 * abs(fd), (i, j, fd, g[i, j].item())
+
+
+def test_eval_logits_match_eager():
+    torch.manual_seed(4)
+    m1 = GPT(tiny())
+    m2 = copy.deepcopy(m1)
+    m2.enable_engine()
+    m1.eval(); m2.eval()
+    ids = torch.randint(0, 256, (2, 20))
+    with torch.no_grad():
+        a, _ = m1(ids)
+        b, _ = m2(ids)
+    assert torch.allclose(a, b, atol=1e-5)
+
+
+def test_generate_topk_shapes_and_kv_cache_parity():
+    torch.manual_seed(5)
+    m1 = GPT(tiny())
+    m2 = copy.deepcopy(m1)
+    m2.enable_engine()
+    ids = torch.randint(0, 256, (1, 5))
+    torch.manual_seed(9)
+    o1 = m1.generate(ids, max_new_tokens=8, temperature=1.0, top_k=1)  # greedy
+    torch.manual_seed(9)
+    o2 = m2.generate(ids, max_new_tokens=8, temperature=1.0, top_k=1)
+    assert o1.shape == (1, 13)
+    assert torch.equal(o1, o2)
