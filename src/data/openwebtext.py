@@ -1,0 +1,6 @@
+"""Reference-path shim for ``data.openwebtext``."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+from distributed_llm_trainer_amd.data.openwebtext import *  # noqa: E402,F401,F403
