@@ -184,7 +184,13 @@ class GPT(nn.Module):
             self.store = provider
         if ops is None:
             ops = ops_mod.for_device(dev)
-        self.engine = GPTEngine(self.config, provider, ops, act_dtype=act_dtype, seed=seed)
+        gemm = None
+        if dev.type == "cuda" and ops.backend == "hip":
+            import os
+            from ..ops import gemm as gemm_mod
+            if os.environ.get("DLT_GEMM", "planner") == "planner" and gemm_mod.available():
+                gemm = gemm_mod.HipGemm()
+        self.engine = GPTEngine(self.config, provider, ops, act_dtype=act_dtype, seed=seed, gemm=gemm)
         self._anchor = torch.zeros((), device=dev, requires_grad=True)
         return self.engine
 

@@ -18,6 +18,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "_dlt_kernels.so")
+GEMM_SRC = os.path.join(HERE, "csrc_gemm", "gemm_planner.cpp")
+GEMM_LIB = os.path.join(HERE, "_dlt_gemm.so")
 ARCH = os.environ.get("DLT_OFFLOAD_ARCH", "gfx950")
 
 # -amdgpu-mfma-vgpr-form: keep MFMA accumulators in arch VGPRs (gfx950 has a unified
@@ -76,7 +78,25 @@ def build(verbose: bool = True, jobs: int = 0, extra=()) -> str:
         os.replace(tmp, LIB)
         if verbose:
             print(f"[dlt-build] linked {LIB}", flush=True)
+    build_gemm(verbose)
     return LIB
+
+
+def build_gemm(verbose: bool = True) -> str:
+    """Host-side hipBLASLt planner library (links libhipblaslt.so.1; at run time it binds
+    to the copy already loaded by torch -- same SONAME)."""
+    if os.path.exists(GEMM_LIB) and os.path.getmtime(GEMM_LIB) >= os.path.getmtime(GEMM_SRC):
+        return GEMM_LIB
+    tmp = GEMM_LIB + ".tmp"
+    cmd = [hipcc(), "-O2", "-fPIC", "-shared", "-std=c++17", "-Wno-unused-result", GEMM_SRC, "-o", tmp,
+           "-L/opt/rocm/lib", "-lhipblaslt"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"gemm planner build failed:\n{r.stderr[-4000:]}")
+    os.replace(tmp, GEMM_LIB)
+    if verbose:
+        print(f"[dlt-build] linked {GEMM_LIB}", flush=True)
+    return GEMM_LIB
 
 
 if __name__ == "__main__":

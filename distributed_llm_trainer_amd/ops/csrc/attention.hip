@@ -36,6 +36,9 @@
 #define KB 128     // keys per workgroup (dK/dV), 32 per wave
 #define QSTEP 64   // queries per staged tile (dK/dV)
 #define LOG2E 1.44269504088896340736f
+#ifndef ATTN_EXP
+#define ATTN_EXP 0  // profiling experiments only (tools/cpp/attn_bench.cpp): 1 = no softmax VALU, 2 = no K/V reloads
+#endif
 
 typedef __attribute__((address_space(3))) shortx4_t lds_shortx4_t;
 typedef short shortx8_t __attribute__((ext_vector_type(8)));
@@ -183,6 +186,17 @@ __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const b
 #pragma unroll
     for (int s = 0; s < 4; ++s) sacc[t] = mfma(lds_row8(Kt, 32 * t + ql, 16 * s + 8 * h), qf[s], sacc[t]);
   }
+#if ATTN_EXP == 1
+  if (true) {
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const bf16x8_t pb = acc_frag(sacc[kk >> 1], kk & 1);
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) fs.o[dt] = mfma(tr_frag(Vt, kk, dt, lane), pb, fs.o[dt]);
+    }
+    return;
+  }
+#endif
   float mx = -INFINITY;
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -266,12 +280,12 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd(const bf16_t* __restrict__ 
 
   for (int kb = 0; kb < nkv; ++kb) {
     const int cur = kb & 1;
-    const bool more = kb + 1 < nkv;
+    const bool more = ATTN_EXP != 2 && kb + 1 < nkv;
     if (more) {
       stage_load(sk, k + hoff, (kb + 1) * KVB, S, HD, tid);
       stage_load(sv, v + hoff, (kb + 1) * KVB, S, HD, tid);
     }
-    const bf16_t* Kt = lds + cur * 2 * KVB * HD;
+    const bf16_t* Kt = lds + (ATTN_EXP == 2 ? 0 : cur) * 2 * KVB * HD;
     const bf16_t* Vt = Kt + KVB * HD;
     const int k0 = kb * KVB;
     if (k0 + KVB - 1 <= q0 && k0 + KVB <= S)

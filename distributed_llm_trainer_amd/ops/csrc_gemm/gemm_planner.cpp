@@ -1,0 +1,203 @@
+// Native GEMM planner: hipBLASLt with per-shape autotuned algorithm selection.
+//
+// The engine's projection GEMMs are plain library GEMMs (bf16 x bf16 -> bf16, and
+// bf16 x bf16 -> fp32 accumulated into the fp32 main-grad buffer for weight
+// gradients).  Measured on MI355X (tools/cpp/hipblaslt_sweep.cpp, random data), the
+// solution the framework's default path picks for the weight-gradient GEMMs
+// (dW[N,K] += dY^T X with K_red = B*S = 8192) runs at 180-620 TF/s, while the best
+// hipBLASLt solution for the same problem runs 1.3-2x faster.  This planner:
+//   * maps row-major PyTorch tensors onto column-major hipBLASLt descriptors,
+//   * keys a plan cache on (opA, opB, m, n, k, lds, dtypes, beta != 0),
+//   * on the first call of a key, times up to DLT_GEMM_CANDIDATES heuristic
+//     solutions on the caller's stream and keeps the fastest (a key first seen
+//     inside a HIP-graph capture takes heuristic #0 without timing),
+//   * owns one device workspace (DLT_GEMM_WORKSPACE_MB, default 64).
+// C ABI, loaded by ctypes from ops/gemm.py.
+#include <hip/hip_runtime.h>
+#include <hipblaslt/hipblaslt.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#define DLT_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+struct Key {
+  int ta, tb, m, n, k, lda, ldb, ldc, dta, dtb, dtc, accumulate;
+  bool operator<(const Key& o) const {
+    return std::tie(ta, tb, m, n, k, lda, ldb, ldc, dta, dtb, dtc, accumulate) <
+           std::tie(o.ta, o.tb, o.m, o.n, o.k, o.lda, o.ldb, o.ldc, o.dta, o.dtb, o.dtc, o.accumulate);
+  }
+};
+
+struct Plan {
+  hipblasLtMatmulDesc_t desc = nullptr;
+  hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr;
+  hipblasLtMatmulAlgo_t algo;
+  size_t ws = 0;
+  float us = -1.f;
+  int chosen = 0, candidates = 0;
+};
+
+struct Planner {
+  hipblasLtHandle_t h = nullptr;
+  void* ws = nullptr;
+  size_t wsz = 0;
+  std::map<Key, Plan> plans;
+  std::mutex mu;
+  int max_cand = 24;
+  bool tune = true;
+  bool verbose = false;
+};
+
+Planner* g = nullptr;
+
+hipDataType dt_of(int code) { return code == 0 ? HIP_R_32F : (code == 1 ? HIP_R_16BF : HIP_R_16F); }
+
+int init() {
+  if (g) return 0;
+  Planner* p = new Planner();
+  if (hipblasLtCreate(&p->h) != HIPBLAS_STATUS_SUCCESS) return -10;
+  const char* e = getenv("DLT_GEMM_WORKSPACE_MB");
+  p->wsz = (size_t)(e ? atoi(e) : 64) << 20;
+  if (hipMalloc(&p->ws, p->wsz) != hipSuccess) return -11;
+  e = getenv("DLT_GEMM_CANDIDATES");
+  if (e) p->max_cand = atoi(e);
+  e = getenv("DLT_GEMM_TUNE");
+  if (e && atoi(e) == 0) p->tune = false;
+  e = getenv("DLT_GEMM_VERBOSE");
+  p->verbose = e && atoi(e) != 0;
+  g = p;
+  return 0;
+}
+
+bool capturing(hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) != hipSuccess) return false;
+  return st != hipStreamCaptureStatusNone;
+}
+
+int build_plan(const Key& k, Plan& p, const void* A, const void* B, void* C, hipStream_t s) {
+  if (hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS) return -20;
+  hipblasOperation_t ta = k.ta ? HIPBLAS_OP_T : HIPBLAS_OP_N, tb = k.tb ? HIPBLAS_OP_T : HIPBLAS_OP_N;
+  hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta));
+  hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb));
+  const int ar = k.ta ? k.k : k.m, ac = k.ta ? k.m : k.k;  // stored (rows, cols) of A in col-major
+  const int br = k.tb ? k.n : k.k, bc = k.tb ? k.k : k.n;
+  if (hipblasLtMatrixLayoutCreate(&p.la, dt_of(k.dta), ar, ac, k.lda) != HIPBLAS_STATUS_SUCCESS) return -21;
+  if (hipblasLtMatrixLayoutCreate(&p.lb, dt_of(k.dtb), br, bc, k.ldb) != HIPBLAS_STATUS_SUCCESS) return -22;
+  if (hipblasLtMatrixLayoutCreate(&p.lc, dt_of(k.dtc), k.m, k.n, k.ldc) != HIPBLAS_STATUS_SUCCESS) return -23;
+  hipblasLtMatmulPreference_t pref;
+  hipblasLtMatmulPreferenceCreate(&pref);
+  hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &g->wsz, sizeof(g->wsz));
+  std::vector<hipblasLtMatmulHeuristicResult_t> res(std::max(1, g->max_cand));
+  int n = 0;
+  hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(g->h, p.desc, p.la, p.lb, p.lc, p.lc, pref,
+                                                       (int)res.size(), res.data(), &n);
+  hipblasLtMatmulPreferenceDestroy(pref);
+  if (st != HIPBLAS_STATUS_SUCCESS || n == 0) return -24;
+  p.algo = res[0].algo;
+  p.ws = res[0].workspaceSize;
+  p.candidates = n;
+  if (!g->tune || n == 1 || capturing(s)) return 0;
+  // Autotune on the caller's stream.  Timing needs a host sync; this runs once per
+  // shape (warmup step).  beta = 0 while timing so an accumulating GEMM does not
+  // disturb C (its real call comes right after with the requested beta).
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  float alpha = 1.f, beta0 = 0.f;
+  std::vector<char> scratch;  // keep C intact for accumulate=1: save + restore
+  size_t csize = (size_t)k.ldc * k.n * (k.dtc == 0 ? 4 : 2);
+  void* cbak = nullptr;
+  if (k.accumulate && hipMalloc(&cbak, csize) == hipSuccess)
+    hipMemcpyAsync(cbak, C, csize, hipMemcpyDeviceToDevice, s);
+  float best = 1e30f;
+  int bi = 0;
+  for (int i = 0; i < n; ++i) {
+    if (res[i].workspaceSize > g->wsz) continue;
+    bool ok = true;
+    for (int w = 0; w < 2 && ok; ++w)
+      ok = hipblasLtMatmul(g->h, p.desc, &alpha, A, p.la, B, p.lb, &beta0, C, p.lc, C, p.lc, &res[i].algo, g->ws,
+                           g->wsz, s) == HIPBLAS_STATUS_SUCCESS;
+    if (!ok) continue;
+    hipEventRecord(e0, s);
+    const int iters = 5;
+    for (int it = 0; it < iters; ++it)
+      hipblasLtMatmul(g->h, p.desc, &alpha, A, p.la, B, p.lb, &beta0, C, p.lc, C, p.lc, &res[i].algo, g->ws, g->wsz,
+                      s);
+    hipEventRecord(e1, s);
+    hipEventSynchronize(e1);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, e0, e1);
+    const float us = ms * 1000.f / iters;
+    if (us < best) { best = us; bi = i; }
+  }
+  if (cbak) {
+    hipMemcpyAsync(C, cbak, csize, hipMemcpyDeviceToDevice, s);
+    hipStreamSynchronize(s);
+    hipFree(cbak);
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  p.algo = res[bi].algo;
+  p.ws = res[bi].workspaceSize;
+  p.us = best;
+  p.chosen = bi;
+  if (g->verbose)
+    fprintf(stderr, "[dlt-gemm] ta=%d tb=%d m=%d n=%d k=%d acc=%d: %d candidates, chose #%d (%.1f us, %.0f TF/s)\n", k.ta,
+            k.tb, k.m, k.n, k.k, k.accumulate, n, bi, best, 2.0 * k.m * k.n * k.k / best / 1e6);
+  return 0;
+}
+
+}  // namespace
+
+// C[m,n] (col-major, ldc) = alpha * op(A) * op(B) + beta * C ; dtype codes: 0 fp32, 1 bf16, 2 fp16
+DLT_API int dlt_gemm(int ta, int tb, int m, int n, int k, const void* A, int lda, int dta, const void* B, int ldb,
+                     int dtb, void* C, int ldc, int dtc, float alpha, float beta, hipStream_t s) {
+  if (int rc = init()) return rc;
+  Key key{ta, tb, m, n, k, lda, ldb, ldc, dta, dtb, dtc, beta != 0.f ? 1 : 0};
+  Plan* p;
+  {
+    std::lock_guard<std::mutex> lk(g->mu);
+    auto it = g->plans.find(key);
+    if (it == g->plans.end()) {
+      Plan np;
+      int rc = build_plan(key, np, A, B, C, s);
+      if (rc) return rc;
+      it = g->plans.emplace(key, np).first;
+    }
+    p = &it->second;
+  }
+  hipblasStatus_t st = hipblasLtMatmul(g->h, p->desc, &alpha, A, p->la, B, p->lb, &beta, C, p->lc, C, p->lc, &p->algo,
+                                       g->ws, g->wsz, s);
+  return st == HIPBLAS_STATUS_SUCCESS ? 0 : -30 - (int)st;
+}
+
+DLT_API int dlt_gemm_num_plans() { return g ? (int)g->plans.size() : 0; }
+
+// Dump the plan table (shape, chosen candidate, measured us) for profiles/ and logs.
+DLT_API int dlt_gemm_report(char* buf, int len) {
+  if (!g || len <= 0) return 0;
+  std::string out;
+  for (auto& kv : g->plans) {
+    const Key& k = kv.first;
+    const Plan& p = kv.second;
+    char line[256];
+    snprintf(line, sizeof(line), "ta=%d tb=%d m=%d n=%d k=%d acc=%d dtc=%d cand=%d chosen=%d us=%.1f\n", k.ta, k.tb,
+             k.m, k.n, k.k, k.accumulate, k.dtc, p.candidates, p.chosen, p.us);
+    out += line;
+  }
+  int n = (int)std::min<size_t>(out.size(), (size_t)len - 1);
+  memcpy(buf, out.data(), n);
+  buf[n] = 0;
+  return n;
+}

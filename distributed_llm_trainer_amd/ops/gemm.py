@@ -1,0 +1,101 @@
+"""GEMMs of the fused executor through the native hipBLASLt planner (``_dlt_gemm.so``).
+
+Row-major PyTorch operands are mapped onto column-major BLAS calls (a row-major
+[r, c] matrix is a column-major [c, r] matrix with ld = c):
+
+  linear       Y[M,N]  = X[M,K] . W[N,K]^T   ->  Y^T = op_T(W_c) . X_c        (m=N, n=M, k=K)
+  linear_dgrad dX[M,K] = dY[M,N] . W[N,K]    ->  dX^T = W_c . dY_c            (m=K, n=M, k=N)
+  wgrad_acc    dW[N,K] += dY^T . X           ->  dW^T += X_c . op_T(dY_c)     (m=K, n=N, k=M), fp32 C
+
+Each distinct shape is autotuned once on first use (see ``csrc_gemm/gemm_planner.cpp``).
+If the planner library cannot be loaded, the engine uses torch.matmul (also hipBLASLt,
+default heuristics) and logs why.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import warnings
+
+import torch
+
+_LIB = None
+_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_dlt_gemm.so")
+_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        import torch  # noqa: F401  (torch's HIP runtime + hipBLASLt must be loaded first)
+        L = ctypes.CDLL(_PATH)
+        c = ctypes
+        L.dlt_gemm.argtypes = [c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, c.c_void_p, c.c_int, c.c_int, c.c_void_p,
+                               c.c_int, c.c_int, c.c_void_p, c.c_int, c.c_int, c.c_float, c.c_float, c.c_void_p]
+        L.dlt_gemm.restype = c.c_int
+        L.dlt_gemm_report.argtypes = [c.c_char_p, c.c_int]
+        L.dlt_gemm_report.restype = c.c_int
+        _LIB = L
+    return _LIB
+
+
+def available() -> bool:
+    if not os.path.exists(_PATH):
+        return False
+    try:
+        lib()
+        return True
+    except OSError as e:  # pragma: no cover
+        warnings.warn(f"GEMM planner unavailable ({e}); using torch.matmul")
+        return False
+
+
+def report() -> str:
+    buf = ctypes.create_string_buffer(1 << 16)
+    n = lib().dlt_gemm_report(buf, len(buf))
+    return buf.value[:n].decode()
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _gemm(ta, tb, m, n, k, A, lda, B, ldb, C, ldc, alpha=1.0, beta=0.0):
+    rc = lib().dlt_gemm(ta, tb, m, n, k, ctypes.c_void_p(A.data_ptr()), lda, _DT[A.dtype],
+                        ctypes.c_void_p(B.data_ptr()), ldb, _DT[B.dtype], ctypes.c_void_p(C.data_ptr()), ldc,
+                        _DT[C.dtype], alpha, beta, _stream())
+    if rc != 0:
+        raise RuntimeError(f"dlt_gemm failed ({rc}) for ta={ta} tb={tb} m={m} n={n} k={k}")
+
+
+def _rowmajor(t: torch.Tensor) -> int:
+    """Leading dimension of a row-major 2-D tensor (must be unit-stride in dim 1)."""
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError("GEMM operand must be 2-D with unit inner stride")
+    return t.stride(0)
+
+
+class HipGemm:
+    """The engine's GEMM interface on the autotuned hipBLASLt planner."""
+
+    def linear(self, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+        M, K = x.shape
+        N = w.shape[0]
+        y = torch.empty(M, N, dtype=x.dtype, device=x.device)
+        _gemm(1, 0, N, M, K, w, _rowmajor(w), x, _rowmajor(x), y, N)
+        return y
+
+    def linear_dgrad(self, dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+        M, N = dy.shape
+        K = w.shape[1]
+        dx = torch.empty(M, K, dtype=dy.dtype, device=dy.device)
+        _gemm(0, 0, K, M, N, w, _rowmajor(w), dy, _rowmajor(dy), dx, K)
+        return dx
+
+    def wgrad_acc(self, dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
+        M, N = dy.shape
+        K = x.shape[1]
+        dw2 = dw.view(N, K)
+        if dw2.dtype != torch.float32 or not dw2.is_contiguous():
+            raise ValueError("wgrad accumulator must be contiguous fp32")
+        _gemm(0, 1, K, N, M, x, _rowmajor(x), dy, _rowmajor(dy), dw2, K, 1.0, 1.0)

@@ -43,6 +43,7 @@ _SIGS = {
     "dlt_adamw": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float, c_float,
                   c_float, c_float, c_float, c_void_p, c_void_p],
     "dlt_cast_bf16": [c_void_p, c_void_p, c_int64, c_void_p],
+    "dlt_wgrad_gemm": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
     "dlt_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                      c_uint32, c_uint32, c_float, c_void_p],
     "dlt_attn_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -320,3 +321,18 @@ def adamw_flat(param, grad, exp_avg, exp_avg_sq, shadow, lr, beta1, beta2, eps, 
 
 def cast_bf16(x: torch.Tensor, y: torch.Tensor) -> None:
     _chk(lib().dlt_cast_bf16(_p(x), _p(y), x.numel(), _stream()), "cast_bf16")
+
+
+# ---------------------------------------------------------------- wgrad GEMM
+def wgrad_gemm(dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, splits: int = 0) -> bool:
+    """dw[N,K] (fp32) += dy[M,N]^T @ x[M,K] with the hand-written MFMA kernel.
+    Returns False (nothing launched) when the shape is outside the kernel's tiling."""
+    M, N = dy.shape
+    K = x.shape[1]
+    if M % 64 or N % 128 or K % 128:
+        return False
+    _req(dy, torch.bfloat16, "wgrad.dy")
+    _req(x, torch.bfloat16, "wgrad.x", M * K)
+    _req(dw, torch.float32, "wgrad.dw", N * K)
+    _chk(lib().dlt_wgrad_gemm(_p(dy), _p(x), _p(dw), M, N, K, splits, _stream()), "wgrad_gemm")
+    return True

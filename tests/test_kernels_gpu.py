@@ -203,3 +203,36 @@ def test_attention_bwd(S, p):
     for a, b, n in ((dq, dq2, "dq"), (dk, dk2, "dk"), (dv, dv2, "dv")):
         scale = b.float().abs().max().item()
         _close(a, b.float(), 2e-2 * max(1.0, scale), 2e-2, n)
+
+
+@pytest.mark.parametrize("M,N,K", [(8192, 2304, 768), (8192, 768, 3072), (1000, 300, 200), (256, 50304, 768)])
+def test_gemm_planner(M, N, K):
+    from distributed_llm_trainer_amd.ops import gemm
+    assert gemm.available()
+    g = gemm.HipGemm()
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = torch.randn(N, K, device=DEV).bfloat16()
+    dy = torch.randn(M, N, device=DEV).bfloat16()
+    y = g.linear(x, w)
+    _close(y, (x.float() @ w.float().t()), 0.05 * K ** 0.5, 2e-2, "linear")
+    dx = g.linear_dgrad(dy, w)
+    _close(dx, dy.float() @ w.float(), 0.05 * N ** 0.5, 2e-2, "dgrad")
+    dw = torch.randn(N, K, device=DEV)
+    ref = dw + dy.float().t() @ x.float()
+    g.wgrad_acc(dw, dy, x)
+    _close(dw, ref, 1e-2 * M ** 0.5, 1e-3, "wgrad acc")
+    g.wgrad_acc(dw, dy, x)  # second call uses the cached (tuned) plan, accumulates again
+    _close(dw, ref + dy.float().t() @ x.float(), 2e-2 * M ** 0.5, 1e-3, "wgrad acc 2")
+
+
+@pytest.mark.parametrize("M,N,K", [(1024, 256, 128), (2048, 768, 384)])
+def test_wgrad_gemm_kernel(M, N, K):
+    torch.manual_seed(0)
+    dy = torch.randn(M, N, device=DEV).bfloat16()
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    for splits in (1, 2, 0):
+        dw = torch.randn(N, K, device=DEV)
+        ref = dw + dy.float().t() @ x.float()
+        assert hip.wgrad_gemm(dw, dy, x, splits)
+        _close(dw, ref, 1e-3 * M ** 0.5, 1e-4, f"wgrad splits={splits}")
