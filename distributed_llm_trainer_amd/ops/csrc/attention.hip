@@ -135,13 +135,22 @@ __device__ __forceinline__ bf16x8_t load_row8(const bf16_t* __restrict__ p, bool
 // the MFMA kernels only test bits instead of hashing at 2 waves/SIMD.
 __global__ __launch_bounds__(256) void k_dropout_bits(uint32_t* __restrict__ mask, int BH, int S, uint32_t key,
                                                       uint32_t thr) {
-  // grid: (ceil(S*W/256), BH); 32-bit index math only (64-bit div/mod is emulated)
+  // grid: (ceil(n_causal_words / 256), BH).  Thread t enumerates only the causal words
+  // (w*32 <= q): rows of 32-row band r have r+1 words, band r starts at word
+  // 32*r*(r+1)/2 -- no idle lanes above the diagonal.  32-bit index math only.
   const int W = (S + 31) >> 5;
   const int bh = blockIdx.y;
-  const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx >= S * W) return;
-  const int q = idx / W, w = idx - q * W;
-  if (w * 32 > q) return;  // above the causal diagonal: never read
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int nb = W;  // number of 32-row bands
+  const int total = 16 * nb * (nb + 1);  // 32 * sum_{r<nb} (r+1)
+  if (t >= total) return;
+  int r = (int)((sqrtf(1.f + (float)t / 4.f) - 1.f) * 0.5f);  // approx band, then fix up
+  while (16 * (r + 1) * (r + 2) <= t) ++r;
+  while (r > 0 && 16 * r * (r + 1) > t) --r;
+  const int rem = t - 16 * r * (r + 1);  // index within band r: (row-in-band, word)
+  const int q = r * 32 + rem / (r + 1);
+  const int w = rem % (r + 1);
+  if (q >= S) return;
   const uint32_t kbh = lowbias32(key + (uint32_t)bh * 0x9E3779B9u);
   const uint32_t base = (uint32_t)q * (uint32_t)S + (uint32_t)(w * 32);
   const int nk = min(32, S - w * 32);
@@ -160,7 +169,7 @@ __global__ __launch_bounds__(256) void k_dropout_bits(uint32_t* __restrict__ mas
       word |= (uint32_t)(bits >= thr) << j;
     }
   }
-  mask[(size_t)bh * S * W + idx] = word;
+  mask[((size_t)bh * S + q) * W + w] = word;
 }
 
 // ============================================================================ forward
@@ -173,70 +182,74 @@ template <bool MASK, bool DROP>
 __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const bf16_t* Vt, const bf16x8_t (&qf)[4],
                                          int k0, int qa, int S, int lane, float c_log2,
                                          const uint32_t* __restrict__ mrow) {
+  // Two 32-key halves, each a complete online-softmax step, with the LDS reads for
+  // the half's PV product (V^T via tr-reads) issued BEFORE its softmax VALU so their
+  // latency hides under the exp/max work; ~half the live registers of a 64-key step.
   const int h = lane >> 5, ql = lane & 31;
   uint32_t words[2] = {0u, 0u};
-  if (DROP) {  // issue the keep-bit loads first; they land under the QK^T MFMAs
+  if (DROP) {
     words[0] = mrow[k0 >> 5];
     words[1] = mrow[(k0 >> 5) + 1];
   }
-  floatx16_t sacc[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    sacc[t] = zero16();
+    bf16x8_t kf[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) sacc[t] = mfma(lds_row8(Kt, 32 * t + ql, 16 * s + 8 * h), qf[s], sacc[t]);
-  }
+    for (int s = 0; s < 4; ++s) kf[s] = lds_row8(Kt, 32 * t + ql, 16 * s + 8 * h);
+    bf16x8_t vf[2][2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) vf[kk][dt] = tr_frag(Vt, 2 * t + kk, dt, lane);
+    floatx16_t sacc = zero16();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) sacc = mfma(kf[s], qf[s], sacc);
 #if ATTN_EXP == 1
-  if (true) {
+    {
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const bf16x8_t pb = acc_frag(sacc[kk >> 1], kk & 1);
+      for (int kk = 0; kk < 2; ++kk) {
+        const bf16x8_t pb = acc_frag(sacc, kk);
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt) fs.o[dt] = mfma(tr_frag(Vt, kk, dt, lane), pb, fs.o[dt]);
+        for (int dt = 0; dt < 2; ++dt) fs.o[dt] = mfma(vf[kk][dt], pb, fs.o[dt]);
+      }
+      continue;
     }
-    return;
-  }
 #endif
-  float mx = -INFINITY;
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
+    float mx = -INFINITY;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       if (MASK) {
         const int ka = k0 + 32 * t + acc_row(i, h);
-        sacc[t][i] = (ka > qa || ka >= S) ? -INFINITY : sacc[t][i];
+        sacc[i] = (ka > qa || ka >= S) ? -INFINITY : sacc[i];
       }
-      mx = fmaxf(mx, sacc[t][i]);
+      mx = fmaxf(mx, sacc[i]);
     }
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-  // defer the O/l rescale while no lane's running max grows (T13 with THR = 0:
-  // exact -- the rescale factor would be 1.0)
-  if (__any(mx > fs.m)) {
-    const float m_new = fmaxf(fs.m, mx);
-    const float alpha = fast_exp2((fs.m - m_new) * c_log2);
-    fs.m = m_new;
-    fs.l *= alpha;
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    // exact deferred rescale: skip while no lane's running max grows
+    if (__any(mx > fs.m)) {
+      const float m_new = fmaxf(fs.m, mx);
+      const float alpha = fast_exp2((fs.m - m_new) * c_log2);
+      fs.m = m_new;
+      fs.l *= alpha;
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
+      for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) fs.o[dt][i] *= alpha;
-  }
-  const float nmc = -fs.m * c_log2;
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
+        for (int i = 0; i < 16; ++i) fs.o[dt][i] *= alpha;
+    }
+    const float nmc = -fs.m * c_log2;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const float p = fast_exp2(fmaf(sacc[t][i], c_log2, nmc));
+      const float p = fast_exp2(fmaf(sacc[i], c_log2, nmc));
       fs.l += p;
-      if (DROP) sacc[t][i] = ((words[t] >> acc_row(i, h)) & 1u) ? p : 0.f;  // 1/(1-p) applied at the end
-      else sacc[t][i] = p;
+      if (DROP) sacc[i] = ((words[t] >> acc_row(i, h)) & 1u) ? p : 0.f;  // 1/(1-p) applied at the end
+      else sacc[i] = p;
     }
-  }
 #pragma unroll
-  for (int kk = 0; kk < 4; ++kk) {
-    const bf16x8_t pb = acc_frag(sacc[kk >> 1], kk & 1);
+    for (int kk = 0; kk < 2; ++kk) {
+      const bf16x8_t pb = acc_frag(sacc, kk);
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt) fs.o[dt] = mfma(tr_frag(Vt, kk, dt, lane), pb, fs.o[dt]);
+      for (int dt = 0; dt < 2; ++dt) fs.o[dt] = mfma(vf[kk][dt], pb, fs.o[dt]);
+    }
   }
 }
 
@@ -280,12 +293,12 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd(const bf16_t* __restrict__ 
 
   for (int kb = 0; kb < nkv; ++kb) {
     const int cur = kb & 1;
-    const bool more = ATTN_EXP != 2 && kb + 1 < nkv;
+    const bool more = ATTN_EXP != 2 && ATTN_EXP != 4 && kb + 1 < nkv;
     if (more) {
       stage_load(sk, k + hoff, (kb + 1) * KVB, S, HD, tid);
       stage_load(sv, v + hoff, (kb + 1) * KVB, S, HD, tid);
     }
-    const bf16_t* Kt = lds + (ATTN_EXP == 2 ? 0 : cur) * 2 * KVB * HD;
+    const bf16_t* Kt = lds + ((ATTN_EXP == 2 || ATTN_EXP == 4) ? 0 : cur) * 2 * KVB * HD;
     const bf16_t* Vt = Kt + KVB * HD;
     const int k0 = kb * KVB;
     if (k0 + KVB - 1 <= q0 && k0 + KVB <= S)
@@ -297,7 +310,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd(const bf16_t* __restrict__ 
       stage_store(sk, Kn, tid);
       stage_store(sv, Kn + KVB * HD, tid);
     }
-    __syncthreads();
+    if (ATTN_EXP < 4) __syncthreads();
   }
 
   const float l_tot = fs.l + __shfl_xor(fs.l, 32, 64);
@@ -641,7 +654,8 @@ DLT_API int dlt_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16
   const dim3 grid((S + QB - 1) / QB, B * nh);
   const float c_log2 = scale * LOG2E;
   if (thr) {
-    const int words = S * ((S + 31) / 32);
+    const int nbands = (S + 31) / 32;
+    const int words = 16 * nbands * (nbands + 1);
     k_dropout_bits<<<dim3((words + 255) / 256, B * nh), 256, 0, st>>>(mask, B * nh, S, key, thr);
     k_attn_fwd<true><<<grid, 256, 0, st>>>(q, k, v, o, lse, mask, S, nh, c_log2, dscale);
   } else {

@@ -134,7 +134,7 @@ def embedding_bwd(ids: torch.Tensor, dout: torch.Tensor, dweight: torch.Tensor) 
 
 
 # ---------------------------------------------------------------- RMSNorm
-def add_dropout_rmsnorm_fwd(resid, delta, weight, eps, p, key, out_dtype=torch.bfloat16):
+def add_dropout_rmsnorm_fwd(resid, delta, weight, eps, p, key, out_dtype=torch.bfloat16, y_out=None):
     src = resid if resid is not None else delta
     M, H = src.shape
     if out_dtype != torch.bfloat16:
@@ -146,7 +146,8 @@ def add_dropout_rmsnorm_fwd(resid, delta, weight, eps, p, key, out_dtype=torch.b
     w = weight if weight.dtype == torch.float32 else weight.float()
     w = w.contiguous()
     _req(w, torch.float32, "rmsnorm.weight", H)
-    y = torch.empty(M, H, dtype=torch.bfloat16, device=src.device)
+    y = torch.empty(M, H, dtype=torch.bfloat16, device=src.device) if y_out is None else y_out
+    _req(y, torch.bfloat16, "rmsnorm.y", M * H)
     rstd = torch.empty(M, dtype=torch.float32, device=src.device)
     if delta is None:
         x, xo = resid, None       # x is just the residual: no copy
@@ -160,7 +161,8 @@ def add_dropout_rmsnorm_fwd(resid, delta, weight, eps, p, key, out_dtype=torch.b
     return x, y, rstd
 
 
-def rmsnorm_bwd(dy, x, rstd, weight, dres, dweight, p_prev, key_prev, dy_scale=None, want_ddelta=True):
+def rmsnorm_bwd(dy, x, rstd, weight, dres, dweight, p_prev, key_prev, dy_scale=None, want_ddelta=True,
+                ddelta_out=None):
     M, H = x.shape
     _req(dy, torch.bfloat16, "rmsnorm_bwd.dy", M * H)
     _req(x, torch.float32, "rmsnorm_bwd.x", M * H)
@@ -173,7 +175,10 @@ def rmsnorm_bwd(dy, x, rstd, weight, dres, dweight, p_prev, key_prev, dy_scale=N
     if dy_scale is not None:
         scale_t = dy_scale.reshape(1).float().contiguous()
     dx = torch.empty(M, H, dtype=torch.float32, device=x.device)
-    dd = torch.empty(M, H, dtype=torch.bfloat16, device=x.device) if want_ddelta else None
+    dd = None
+    if want_ddelta:
+        dd = torch.empty(M, H, dtype=torch.bfloat16, device=x.device) if ddelta_out is None else ddelta_out
+        _req(dd, torch.bfloat16, "rmsnorm_bwd.ddelta", M * H)
     thr = rng.keep_threshold(p_prev)
     dscale = 1.0 / (1.0 - p_prev) if thr else 1.0
     _chk(lib().dlt_rmsnorm_bwd(_p(dy), _p(x), _p(rstd), _p(w), _p(dres), _p(dx), _p(dd), _p(dweight), _p(scale_t),
@@ -198,14 +203,16 @@ def rope_qkv_fwd(qkv, B, S, nh, cos, sin):
     return q, k, v
 
 
-def rope_qkv_bwd(dq, dk, dv, cos, sin):
+def rope_qkv_bwd(dq, dk, dv, cos, sin, out=None):
     B, nh, S, hd = dk.shape
     for t, n in ((dk, "dk"), (dv, "dv")):
         _req(t, torch.bfloat16, "rope_bwd." + n, B * nh * S * hd)
     dqf = dq if dq.dtype == torch.float32 else None
     dqb = dq if dq.dtype == torch.bfloat16 else None
     _req(dq, dq.dtype, "rope_bwd.dq", B * nh * S * hd)
-    out = torch.empty(B * S, 3 * nh * hd, dtype=torch.bfloat16, device=dk.device)
+    if out is None:
+        out = torch.empty(B * S, 3 * nh * hd, dtype=torch.bfloat16, device=dk.device)
+    _req(out, torch.bfloat16, "rope_bwd.out", B * S * 3 * nh * hd)
     _chk(lib().dlt_rope_qkv_bwd(_p(dqb), _p(dqf), _p(dk), _p(dv), _p(cos), _p(sin), _p(out), B, S, nh, hd, _stream()),
          "rope_qkv_bwd")
     return out
@@ -216,7 +223,7 @@ class AttnAux(tuple):
     """(lse [B,nh,S] fp32, keep-bit mask [B*nh, S, ceil(S/32)] uint32 or None)."""
 
 
-def attention_fwd(q, k, v, p, key, causal=True, store_mask=True):
+def attention_fwd(q, k, v, p, key, causal=True, store_mask=True, out=None):
     """Returns (o [B*S, nh*hd] bf16, aux).  With dropout on, the keep bits are written
     to a bitmask consumed by attention_bwd (no re-hashing in the backward)."""
     if not causal:
@@ -226,7 +233,8 @@ def attention_fwd(q, k, v, p, key, causal=True, store_mask=True):
         _req(t, torch.bfloat16, "attn." + n, B * nh * S * hd)
     if hd != 64:
         raise NotImplementedError(f"attention kernel is specialised for head_dim 64 (got {hd})")
-    o = torch.empty(B * S, nh * hd, dtype=torch.bfloat16, device=q.device)
+    o = torch.empty(B * S, nh * hd, dtype=torch.bfloat16, device=q.device) if out is None else out
+    _req(o, torch.bfloat16, "attn.o", B * S * nh * hd)
     lse = torch.empty(B, nh, S, dtype=torch.float32, device=q.device)
     thr = rng.keep_threshold(p)
     dscale = 1.0 / (1.0 - p) if thr else 1.0
@@ -266,19 +274,23 @@ def attention_bwd(q, k, v, o, do, aux, p, key, causal=True):
 
 
 # ----------------------------------------------------------------- SwiGLU
-def swiglu_fwd(gu):
+def swiglu_fwd(gu, out=None):
     M, twoI = gu.shape
     _req(gu, torch.bfloat16, "swiglu.gu")
-    out = torch.empty(M, twoI // 2, dtype=torch.bfloat16, device=gu.device)
+    if out is None:
+        out = torch.empty(M, twoI // 2, dtype=torch.bfloat16, device=gu.device)
+    _req(out, torch.bfloat16, "swiglu.out", M * twoI // 2)
     _chk(lib().dlt_swiglu_fwd(_p(gu), _p(out), M, twoI // 2, _stream()), "swiglu_fwd")
     return out
 
 
-def swiglu_bwd(gu, da):
+def swiglu_bwd(gu, da, out=None):
     M, twoI = gu.shape
     _req(gu, torch.bfloat16, "swiglu_bwd.gu")
     _req(da, torch.bfloat16, "swiglu_bwd.da", M * twoI // 2)
-    out = torch.empty_like(gu)
+    if out is None:
+        out = torch.empty_like(gu)
+    _req(out, torch.bfloat16, "swiglu_bwd.out", M * twoI)
     _chk(lib().dlt_swiglu_bwd(_p(gu), _p(da), _p(out), M, twoI // 2, _stream()), "swiglu_bwd")
     return out
 

@@ -41,7 +41,7 @@ def dropout_apply(x: torch.Tensor, key: int, p: float) -> torch.Tensor:
 
 def add_dropout_rmsnorm_fwd(resid: Optional[torch.Tensor], delta: Optional[torch.Tensor],
                             weight: torch.Tensor, eps: float, p: float, key: int,
-                            out_dtype=torch.bfloat16) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+                            out_dtype=torch.bfloat16, y_out=None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """x = resid + dropout(delta);  y = x * rsqrt(mean(x^2)+eps) * w.
 
     Returns (x fp32, y out_dtype, rstd fp32[M]).  ``resid``/``delta`` may be None.
@@ -54,13 +54,16 @@ def add_dropout_rmsnorm_fwd(resid: Optional[torch.Tensor], delta: Optional[torch
         x = resid.float() + dropout_apply(delta.float(), key, p)
     rstd = torch.rsqrt(x.pow(2).mean(dim=-1, keepdim=True) + eps)
     y = (x * rstd * weight.float()).to(out_dtype)
+    if y_out is not None:
+        y_out.copy_(y)
+        y = y_out
     return x, y, rstd.squeeze(-1)
 
 
 def rmsnorm_bwd(dy: torch.Tensor, x: torch.Tensor, rstd: torch.Tensor, weight: torch.Tensor,
                 dres: Optional[torch.Tensor], dweight: torch.Tensor, p_prev: float, key_prev: int,
                 dy_scale: Optional[torch.Tensor] = None,
-                want_ddelta: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+                want_ddelta: bool = True, ddelta_out=None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     """Backward of add_dropout_rmsnorm.
 
     dx = dres + J_rmsnorm^T dy ; ddelta = dropout_bwd(dx) (grad for the delta that was
@@ -83,6 +86,9 @@ def rmsnorm_bwd(dy: torch.Tensor, x: torch.Tensor, rstd: torch.Tensor, weight: t
     ddelta = None
     if want_ddelta:
         ddelta = dropout_apply(dx, key_prev, p_prev).to(out_dt)
+        if ddelta_out is not None:
+            ddelta_out.copy_(ddelta)
+            ddelta = ddelta_out
     return dx, ddelta
 
 
@@ -115,21 +121,23 @@ def rope_qkv_fwd(qkv: torch.Tensor, B: int, S: int, nh: int, cos: torch.Tensor, 
 
 
 def rope_qkv_bwd(dq: torch.Tensor, dk: torch.Tensor, dv: torch.Tensor,
-                 cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+                 cos: torch.Tensor, sin: torch.Tensor, out=None) -> torch.Tensor:
     """Inverse rotation; returns dqkv [B*S, 3H] in dq's dtype."""
     B, nh, S, hd = dq.shape
     c = cos[:S].view(1, 1, S, hd // 2)
     s = sin[:S].view(1, 1, S, hd // 2)
     gq = _rot(dq.float(), c, -s)
     gk = _rot(dk.float(), c, -s)
-    out = torch.stack([gq, gk, dv.float()], dim=0)  # [3, B, nh, S, hd]
-    out = out.permute(1, 3, 0, 2, 4).reshape(B * S, 3 * nh * hd)
-    return out.to(dq.dtype)
+    res = torch.stack([gq, gk, dv.float()], dim=0).permute(1, 3, 0, 2, 4).reshape(B * S, 3 * nh * hd).to(dq.dtype)
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res
 
 
 # -------------------------------------------------------------- attention
 def attention_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, p: float, key: int,
-                  causal: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
+                  causal: bool = True, out=None) -> Tuple[torch.Tensor, torch.Tensor]:
     """q,k,v [B, nh, S, hd] -> o [B*S, nh*hd] (q dtype), lse [B, nh, S] fp32."""
     B, nh, S, hd = q.shape
     scale = 1.0 / math.sqrt(hd)
@@ -144,6 +152,9 @@ def attention_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, p: float, k
         prob = torch.where(keep, prob / (1.0 - p), torch.zeros((), device=q.device))
     o = torch.matmul(prob, v.float())
     o = o.transpose(1, 2).reshape(B * S, nh * hd).to(q.dtype)
+    if out is not None:
+        out.copy_(o)
+        o = out
     return o, lse
 
 
@@ -176,14 +187,18 @@ def attention_bwd(q, k, v, o, do, lse, p: float, key: int, causal: bool = True):
 
 
 # ----------------------------------------------------------------- SwiGLU
-def swiglu_fwd(gu: torch.Tensor) -> torch.Tensor:
+def swiglu_fwd(gu: torch.Tensor, out=None) -> torch.Tensor:
     """gu [M, 2I] (gate | up) -> silu(gate) * up [M, I]."""
     i = gu.shape[-1] // 2
     g, u = gu[:, :i].float(), gu[:, i:].float()
-    return (g * torch.sigmoid(g) * u).to(gu.dtype)
+    r = (g * torch.sigmoid(g) * u).to(gu.dtype)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
 
 
-def swiglu_bwd(gu: torch.Tensor, da: torch.Tensor) -> torch.Tensor:
+def swiglu_bwd(gu: torch.Tensor, da: torch.Tensor, out=None) -> torch.Tensor:
     i = gu.shape[-1] // 2
     g, u = gu[:, :i].float(), gu[:, i:].float()
     d = da.float()
@@ -191,7 +206,11 @@ def swiglu_bwd(gu: torch.Tensor, da: torch.Tensor) -> torch.Tensor:
     silu = g * sg
     dg = d * u * sg * (1.0 + g * (1.0 - sg))
     du = d * silu
-    return torch.cat([dg, du], dim=-1).to(gu.dtype)
+    r = torch.cat([dg, du], dim=-1).to(gu.dtype)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
 
 
 # ------------------------------------------------------ cross-entropy (fused with grad)

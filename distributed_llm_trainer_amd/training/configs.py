@@ -45,6 +45,7 @@ class TrainingConfig:
     reduce_dtype: str = "fp32"         # gradient all-reduce wire dtype: fp32 | bf16
     lr_schedule_fix: bool = True       # set LR before the step + clamp cosine (Q5/Q6)
     adam_eps: float = 1e-8
+    defer_wgrad: bool = True           # one weight-grad GEMM per layer per optimizer step
 
 
 @dataclass

@@ -132,6 +132,8 @@ class DistributedTrainer:
             ids = input_ids[micro * micro_bs:(micro + 1) * micro_bs]
             if self.ddp is not None:
                 self.ddp.require_sync(micro == GA - 1)
+            if self.use_engine:
+                self.model.engine.set_accumulation(micro, GA, defer=cfg.defer_wgrad)
             range_push(f"micro{micro}")
             with self.autocast_ctx:
                 _, loss = self.model(ids, labels=ids)

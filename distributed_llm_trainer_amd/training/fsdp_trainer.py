@@ -115,6 +115,7 @@ class FSDPTrainer:
         for micro in range(GA):
             ids = input_ids[micro * micro_bs:(micro + 1) * micro_bs]
             rt.require_sync(micro == GA - 1)
+            self.model.engine.set_accumulation(micro, GA, defer=not self.fsdp_config.sync_every_micro_step)
             _, loss = self.model(ids, labels=ids)
             loss = loss / GA
             loss.backward()

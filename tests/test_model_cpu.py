@@ -159,3 +159,25 @@ def test_generate_topk_shapes_and_kv_cache_parity():
     o2 = m2.generate(ids, max_new_tokens=8, temperature=1.0, top_k=1)
     assert o1.shape == (1, 13)
     assert torch.equal(o1, o2)
+
+
+@pytest.mark.parametrize("recompute", [False, True])
+def test_deferred_wgrad_matches_per_micro_step(recompute):
+    """One weight-grad GEMM over the whole accumulation window == per-micro-step sums."""
+    torch.manual_seed(6)
+    cfg = tiny(dropout=0.1, attention_dropout=0.1)
+    m1 = GPT(cfg)
+    m2 = copy.deepcopy(m1)
+    e1 = m1.enable_engine(seed=3)
+    e2 = m2.enable_engine(seed=3)
+    m1.gradient_checkpointing = m2.gradient_checkpointing = recompute
+    data = torch.randint(0, 256, (3, 2, 32))
+    for j in range(3):
+        e1.set_accumulation(j, 3, defer=False)
+        e2.set_accumulation(j, 3, defer=True)
+        _, l1 = m1(data[j], labels=data[j])
+        (l1 / 3).backward()
+        _, l2 = m2(data[j], labels=data[j])
+        (l2 / 3).backward()
+    for (n, p1), (_, p2) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert torch.allclose(p1.grad, p2.grad, atol=1e-6, rtol=1e-4), n

@@ -116,3 +116,23 @@ def test_generate_kv_cache_gpu():
             lg, _ = m(g[:, :17 + t])
         assert lg[0, -1].argmax().item() == g[0, 17 + t].item() or \
             (lg[0, -1].max() - lg[0, -1][g[0, 17 + t]]).abs().item() < 0.05
+
+
+def test_deferred_wgrad_gpu():
+    """hipBLASLt wgrad over the whole accumulation window == per-micro-step wgrads."""
+    torch.manual_seed(2)
+    base = GPT(_cfg(0.1)).to(DEV)
+    m1, m2 = copy.deepcopy(base), copy.deepcopy(base)
+    e1, e2 = m1.enable_engine(seed=9), m2.enable_engine(seed=9)
+    data = torch.randint(0, 1000, (4, 2, 256), device=DEV)
+    for j in range(4):
+        e1.set_accumulation(j, 4, defer=False)
+        e2.set_accumulation(j, 4, defer=True)
+        for m in (m1, m2):
+            _, loss = m(data[j], labels=data[j])
+            (loss / 4).backward()
+    g1, g2 = _grads(m1), _grads(m2)
+    for n in g1:
+        assert _cos(g1[n], g2[n]) > 0.999, n
+        r = g1[n].norm() / g2[n].norm()
+        assert 0.99 < r.item() < 1.01, (n, r.item())
