@@ -33,7 +33,7 @@ def create_openwebtext_dataloader(path: str, batch_size: int, seq_len: int, dist
                                   rank: int = 0, world_size: int = 1, tokenizer_name: str = "gpt2",
                                   max_tokens: Optional[int] = None, streaming: bool = False,
                                   cache_max_tokens: Optional[int] = None, num_workers: int = 2,
-                                  tokenizer=None) -> DataLoader:
+                                  tokenizer=None, **kw):
     path = resolve_path(path)
     return create_text_dataloader(path, batch_size, seq_len, distributed, rank, world_size, tokenizer_name,
-                                  max_tokens, streaming, cache_max_tokens, num_workers, tokenizer)
+                                  max_tokens, streaming, cache_max_tokens, num_workers, tokenizer, **kw)

@@ -135,7 +135,14 @@ class StreamingTextDataset(IterableDataset):
 def create_text_dataloader(path: str, batch_size: int, seq_len: int, distributed: bool = False, rank: int = 0,
                            world_size: int = 1, tokenizer_name: str = "gpt2", max_tokens: Optional[int] = None,
                            streaming: bool = False, cache_max_tokens: Optional[int] = None,
-                           num_workers: int = 2, tokenizer=None) -> DataLoader:
+                           num_workers: int = 2, tokenizer=None, seed: int = 0, device=None):
+    if path.endswith(".bin") and os.environ.get("DLT_NATIVE_DATA", "1") != "0":
+        from ..runtime import loader as nl
+        if nl.available():
+            tb = 4 if os.environ.get("DLT_TOKEN_DTYPE", "uint16") == "uint32" else 2
+            return nl.NativeTokenLoader(path, seq_len, batch_size, token_bytes=tb, max_tokens=max_tokens,
+                                        rank=rank if distributed else 0, world_size=world_size if distributed else 1,
+                                        seed=seed, device=device)
     cfg = TextDataConfig(path=path, seq_len=seq_len, tokenizer_name=tokenizer_name, max_tokens=max_tokens,
                          streaming=streaming, cache_max_tokens=cache_max_tokens)
     if path.endswith(".bin"):

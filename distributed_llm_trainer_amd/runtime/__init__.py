@@ -1,0 +1,1 @@
+"""Native (C++) host runtime: the input pipeline (``loader``)."""

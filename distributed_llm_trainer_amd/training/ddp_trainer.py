@@ -278,14 +278,17 @@ def main(argv=None):
         dataloader = fn(path=args.data_path, batch_size=loader_bs, seq_len=seq_len, distributed=trainer.distributed,
                         rank=trainer.rank, world_size=trainer.world_size, tokenizer_name=args.tokenizer,
                         max_tokens=args.max_tokens, streaming=args.streaming,
-                        cache_max_tokens=args.cache_max_tokens, num_workers=0 if args.streaming else 2)
+                        cache_max_tokens=args.cache_max_tokens, num_workers=0 if args.streaming else 2,
+                        seed=tc.seed, device=trainer.device)
     else:
         from ..data import create_dummy_dataloader
         dataloader = create_dummy_dataloader(batch_size=loader_bs, seq_len=seq_len,
                                              vocab_size=model_config.vocab_size, distributed=trainer.distributed,
                                              rank=trainer.rank, world_size=trainer.world_size,
                                              num_batches=int(os.environ.get("DLT_DUMMY_BATCHES", "64")),
-                                             seed=tc.seed)
+                                             seed=tc.seed, device=trainer.device)
+    if hasattr(dataloader, "seek") and trainer.global_step:
+        dataloader.seek(trainer.global_step)  # native loader: resume the exact batch stream
 
     if trainer.is_main_process:
         print("\n" + "=" * 60)

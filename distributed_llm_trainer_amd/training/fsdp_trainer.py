@@ -290,7 +290,10 @@ def main(argv=None):
     dataloader = create_dummy_dataloader(batch_size=total_batch, seq_len=model_config.max_seq_len,
                                          vocab_size=model_config.vocab_size, distributed=trainer.distributed,
                                          rank=trainer.rank, world_size=trainer.world_size,
-                                         num_batches=int(os.environ.get("DLT_DUMMY_BATCHES", "64")), seed=tc.seed)
+                                         num_batches=int(os.environ.get("DLT_DUMMY_BATCHES", "64")), seed=tc.seed,
+                                         device=trainer.device)
+    if hasattr(dataloader, "seek") and trainer.global_step:
+        dataloader.seek(trainer.global_step)
     if trainer.is_main_process:
         print("\n" + "=" * 60)
         print("Starting FSDP training...")

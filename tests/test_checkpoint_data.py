@@ -111,8 +111,8 @@ def test_token_file_dataset(tmp_path):
 
 
 def test_dummy_loader_seeded_drop_last():
-    a = next(iter(create_dummy_dataloader(4, 16, 100, num_batches=3, seed=1)))[0]
-    b = next(iter(create_dummy_dataloader(4, 16, 100, num_batches=3, seed=1)))[0]
+    a = next(iter(create_dummy_dataloader(4, 16, 100, num_batches=3, seed=1, native=False)))[0]
+    b = next(iter(create_dummy_dataloader(4, 16, 100, num_batches=3, seed=1, native=False)))[0]
     assert a.shape == (4, 16)
-    dl = create_dummy_dataloader(3, 16, 100, num_batches=2, seed=1)
+    dl = create_dummy_dataloader(3, 16, 100, num_batches=2, seed=1, native=False)
     assert all(x[0].shape[0] == 3 for x in dl)
