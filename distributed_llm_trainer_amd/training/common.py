@@ -26,7 +26,7 @@ def setup_distributed(require: bool = False, timeout_s: Optional[float] = None):
         t = timeout_s or float(os.environ.get("DLT_PG_TIMEOUT", "1800"))
         kw = dict(backend=backend, timeout=datetime.timedelta(seconds=t))
         if backend == "nccl" and torch.cuda.is_available():
-            lr = int(os.environ.get("LOCAL_RANK", 0))
+            lr = _device_index(int(os.environ.get("LOCAL_RANK", 0)))
             torch.cuda.set_device(lr)
             kw["device_id"] = torch.device(f"cuda:{lr}")
         dist.init_process_group(**kw)
@@ -35,9 +35,18 @@ def setup_distributed(require: bool = False, timeout_s: Optional[float] = None):
     return False, 0, 1, 0
 
 
+def _device_index(local_rank: int) -> int:
+    """GPU of a local rank.  One rank per GPU; ``DLT_SHARE_GPU=1`` folds ranks onto the
+    visible GPUs (local_rank mod count) -- only for rehearsing multi-rank code paths
+    with the gloo backend on a 1-GPU box (RCCL itself rejects two ranks per GPU)."""
+    if os.environ.get("DLT_SHARE_GPU") == "1":
+        return local_rank % max(1, torch.cuda.device_count())
+    return local_rank
+
+
 def select_device(local_rank: int) -> torch.device:
     if torch.cuda.is_available() and os.environ.get("DLT_FORCE_CPU") != "1":
-        d = torch.device(f"cuda:{local_rank}")
+        d = torch.device(f"cuda:{_device_index(local_rank)}")
         torch.cuda.set_device(d)
         return d
     return torch.device("cpu")
