@@ -44,6 +44,9 @@ from .configs import TrainingConfig
 from .optim import flat_store_optimizer
 
 
+PEAK_BF16_FLOPS = 2.5e15  # MI355X dense bf16 MFMA peak (no sparsity), for MFU reporting
+
+
 class DistributedTrainer:
     """DDP trainer.  ``train_step(batch) -> {"loss", "lr", "tokens"}``."""
 
@@ -339,7 +342,15 @@ def main(argv=None):
         print(f"Total tokens processed: {trainer.tokens_seen:,}")
         if steady_t0 is not None:
             dt = time.time() - steady_t0
-            print(f"Steady-state tokens/sec (after step 10): {(trainer.tokens_seen - steady_tok0) / dt:,.0f}")
+            sps = (trainer.tokens_seen - steady_tok0) / dt
+            fpt = model_config.flops_per_token(seq_len, recompute=bool(model_config.gradient_checkpointing))
+            mfu = sps / trainer.world_size * fpt / PEAK_BF16_FLOPS
+            print(f"Steady-state tokens/sec (after step 10): {sps:,.0f} "
+                  f"({sps / trainer.world_size:,.0f}/GPU, MFU {100 * mfu:.1f}% of {PEAK_BF16_FLOPS / 1e15:.1f} PF dense bf16)")
+            if metrics_f:
+                metrics_f.write(json.dumps({"summary": True, "steady_tokens_per_sec": sps,
+                                            "tokens_per_sec_per_gpu": sps / trainer.world_size, "mfu": mfu,
+                                            **trainer.get_memory_stats()}) + "\n")
         ms = trainer.get_memory_stats()
         print(f"Peak memory: {ms['max_allocated_gb']:.2f} GB")
     if metrics_f:
