@@ -28,6 +28,7 @@ Dropout masks are pure functions of (seed, micro-step, layer, site, index)
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional
 
@@ -155,6 +156,7 @@ class GPTEngine:
         # deferred weight gradients (see set_accumulation)
         self.acc_slot, self.acc_slots, self.defer = 0, 1, False
         self._slots = {}
+        self._side = None  # weight-gradient side stream (lazily created)
 
     # ------------------------------------------------------- grad accumulation
     def set_accumulation(self, slot: int, n_slots: int, defer: bool = True) -> None:
@@ -280,6 +282,19 @@ class GPTEngine:
         return loss, logits, (st if need_bwd else None)
 
     # --------------------------------------------------------------- backward
+    def _wgrad_stream(self, dev):
+        """Side HIP stream for the deferred weight-gradient GEMMs (None = run inline).
+
+        Only with a provider whose gradient hooks are stream-safe (the flat store /
+        DDP runtime) and a GEMM backend with per-stream workspaces."""
+        if dev.type != "cuda" or os.environ.get("DLT_WGRAD_STREAM", "1") == "0":
+            return None
+        if not getattr(self.provider, "side_stream_hooks", False) or not getattr(self.gemm, "stream_safe", False):
+            return None
+        if self._side is None:
+            self._side = torch.cuda.Stream(dev)
+        return self._side
+
     def backward(self, st: _StepState, dloss: torch.Tensor) -> None:
         ops, gm, cfg, prov = self.ops, self.gemm, self.cfg, self.provider
         B, S = st.B, st.S
@@ -310,6 +325,7 @@ class GPTEngine:
         del dnf
         cos, sin = self.rope(S, g_x2.device)
         do_wgrad = (not st.defer) or st.last
+        side = self._wgrad_stream(dev) if (do_wgrad and st.defer) else None
 
         for i in reversed(range(L)):
             prov.pre_backward(i)
@@ -340,8 +356,20 @@ class GPTEngine:
                                           want_ddelta=(i > 0), ddelta_out=sb(i - 1, "dd", H) if i > 0 else None)
             del dn1, dx2
             # weight gradients (fp32 accumulate into the main-grad buffers)
+            side_ctx = None
             if do_wgrad:
                 if st.defer:
+                    # One GEMM per weight over the whole accumulation window.  The
+                    # slot buffers are persistent, so these can run on a side stream
+                    # concurrently with the next layer's dgrad chain (the small-output
+                    # wgrads leave most CUs idle); the layer's gradient hook (DDP
+                    # bucket all-reduce) is issued from the same stream.
+                    if side is not None:
+                        ev = torch.cuda.Event()
+                        ev.record()
+                        side.wait_event(ev)
+                        side_ctx = torch.cuda.stream(side)
+                        side_ctx.__enter__()
                     gm.wgrad_acc(gr.wdown, full(i, "dd", H), full(i, "s", I))
                     gm.wgrad_acc(gr.wgu, full(i, "dgu", 2 * I), full(i, "n2", H))
                     gm.wgrad_acc(gr.wo, full(i, "da", H), full(i, "o", H))
@@ -354,19 +382,29 @@ class GPTEngine:
             del dgu, da, dqkv
             g_x2, g_d = g_x2n, g_dn
             st.caches[i] = None
-            prov.post_backward(i)
+            try:
+                prov.post_backward(i)
+            finally:
+                if side_ctx is not None:
+                    side_ctx.__exit__(None, None, None)
         # embedding (tied with lm_head): scatter-add
         ops.embedding_bwd(st.ids, g_x2, hg.embed)
         prov.post_backward("head")
+        if side is not None and do_wgrad and st.defer:
+            torch.cuda.current_stream().wait_stream(side)
 
 
 class _TorchGemm:
     """Plain library GEMMs (hipBLASLt on ROCm via torch.matmul).
 
+    Stream-safe: torch keeps one BLAS workspace per stream.
+
     ``wgrad_acc`` accumulates bf16 x bf16 products straight into the fp32 main-grad
     buffer with ``addmm(..., out_dtype=float32)`` when available (no bf16 round trip,
     no separate add kernel); otherwise falls back to matmul + add_.
     """
+
+    stream_safe = True
 
     def __init__(self):
         self._fp32_out_ok = None

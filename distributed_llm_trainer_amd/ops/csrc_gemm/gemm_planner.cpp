@@ -11,7 +11,8 @@
 //   * on the first call of a key, times up to DLT_GEMM_CANDIDATES heuristic
 //     solutions on the caller's stream and keeps the fastest (a key first seen
 //     inside a HIP-graph capture takes heuristic #0 without timing),
-//   * owns one device workspace (DLT_GEMM_WORKSPACE_MB, default 64).
+//   * owns one device workspace per stream (DLT_GEMM_WORKSPACE_MB, default 64), so
+//     GEMMs on the compute and weight-gradient streams can run concurrently.
 // C ABI, loaded by ctypes from ops/gemm.py.
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt.h>
@@ -49,7 +50,7 @@ struct Plan {
 
 struct Planner {
   hipblasLtHandle_t h = nullptr;
-  void* ws = nullptr;
+  std::map<hipStream_t, void*> ws;  // one workspace per stream (concurrent GEMMs)
   size_t wsz = 0;
   std::map<Key, Plan> plans;
   std::mutex mu;
@@ -68,7 +69,6 @@ int init() {
   if (hipblasLtCreate(&p->h) != HIPBLAS_STATUS_SUCCESS) return -10;
   const char* e = getenv("DLT_GEMM_WORKSPACE_MB");
   p->wsz = (size_t)(e ? atoi(e) : 64) << 20;
-  if (hipMalloc(&p->ws, p->wsz) != hipSuccess) return -11;
   e = getenv("DLT_GEMM_CANDIDATES");
   if (e) p->max_cand = atoi(e);
   e = getenv("DLT_GEMM_TUNE");
@@ -79,13 +79,23 @@ int init() {
   return 0;
 }
 
+// caller holds g->mu
+void* workspace(hipStream_t s) {
+  auto it = g->ws.find(s);
+  if (it != g->ws.end()) return it->second;
+  void* w = nullptr;
+  if (hipMalloc(&w, g->wsz) != hipSuccess) return nullptr;
+  g->ws.emplace(s, w);
+  return w;
+}
+
 bool capturing(hipStream_t s) {
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(s, &st) != hipSuccess) return false;
   return st != hipStreamCaptureStatusNone;
 }
 
-int build_plan(const Key& k, Plan& p, const void* A, const void* B, void* C, hipStream_t s) {
+int build_plan(const Key& k, Plan& p, const void* A, const void* B, void* C, hipStream_t s, void* ws) {
   if (hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS) return -20;
   hipblasOperation_t ta = k.ta ? HIPBLAS_OP_T : HIPBLAS_OP_N, tb = k.tb ? HIPBLAS_OP_T : HIPBLAS_OP_N;
   hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta));
@@ -126,13 +136,13 @@ int build_plan(const Key& k, Plan& p, const void* A, const void* B, void* C, hip
     if (res[i].workspaceSize > g->wsz) continue;
     bool ok = true;
     for (int w = 0; w < 2 && ok; ++w)
-      ok = hipblasLtMatmul(g->h, p.desc, &alpha, A, p.la, B, p.lb, &beta0, C, p.lc, C, p.lc, &res[i].algo, g->ws,
+      ok = hipblasLtMatmul(g->h, p.desc, &alpha, A, p.la, B, p.lb, &beta0, C, p.lc, C, p.lc, &res[i].algo, ws,
                            g->wsz, s) == HIPBLAS_STATUS_SUCCESS;
     if (!ok) continue;
     hipEventRecord(e0, s);
     const int iters = 5;
     for (int it = 0; it < iters; ++it)
-      hipblasLtMatmul(g->h, p.desc, &alpha, A, p.la, B, p.lb, &beta0, C, p.lc, C, p.lc, &res[i].algo, g->ws, g->wsz,
+      hipblasLtMatmul(g->h, p.desc, &alpha, A, p.la, B, p.lb, &beta0, C, p.lc, C, p.lc, &res[i].algo, ws, g->wsz,
                       s);
     hipEventRecord(e1, s);
     hipEventSynchronize(e1);
@@ -166,19 +176,22 @@ DLT_API int dlt_gemm(int ta, int tb, int m, int n, int k, const void* A, int lda
   if (int rc = init()) return rc;
   Key key{ta, tb, m, n, k, lda, ldb, ldc, dta, dtb, dtc, beta != 0.f ? 1 : 0};
   Plan* p;
+  void* ws;
   {
     std::lock_guard<std::mutex> lk(g->mu);
+    ws = workspace(s);
+    if (!ws) return -11;
     auto it = g->plans.find(key);
     if (it == g->plans.end()) {
       Plan np;
-      int rc = build_plan(key, np, A, B, C, s);
+      int rc = build_plan(key, np, A, B, C, s, ws);
       if (rc) return rc;
       it = g->plans.emplace(key, np).first;
     }
     p = &it->second;
   }
   hipblasStatus_t st = hipblasLtMatmul(g->h, p->desc, &alpha, A, p->la, B, p->lb, &beta, C, p->lc, C, p->lc, &p->algo,
-                                       g->ws, g->wsz, s);
+                                       ws, g->wsz, s);
   return st == HIPBLAS_STATUS_SUCCESS ? 0 : -30 - (int)st;
 }
 

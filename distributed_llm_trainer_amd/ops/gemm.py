@@ -76,7 +76,10 @@ def _rowmajor(t: torch.Tensor) -> int:
 
 
 class HipGemm:
-    """The engine's GEMM interface on the autotuned hipBLASLt planner."""
+    """The engine's GEMM interface on the autotuned hipBLASLt planner (one workspace
+    per stream, so GEMMs on the compute and weight-gradient streams may overlap)."""
+
+    stream_safe = True
 
     def linear(self, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         M, K = x.shape

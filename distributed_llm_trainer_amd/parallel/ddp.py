@@ -123,6 +123,8 @@ class DDPRuntime:
         for (h, t, a, b) in self.handles:
             h.wait()
             if t is not None:
+                if t.is_cuda:  # may have been allocated on the weight-gradient stream
+                    t.record_stream(torch.cuda.current_stream(t.device))
                 self.store.grad[a:b].copy_(t)
         self.handles.clear()
 

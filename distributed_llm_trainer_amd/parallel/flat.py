@@ -78,6 +78,10 @@ class FlatLayout:
 
 
 class FlatParamStore(ParamProvider):
+    # gradient hooks (DDP bucket launches) may be issued from the engine's
+    # weight-gradient stream: they only enqueue collectives on the current stream
+    side_stream_hooks = True
+
     def __init__(self, model, device, compute_dtype=torch.bfloat16, grad_dtype=torch.float32):
         self.model = model
         self.cfg = model.config
