@@ -3,10 +3,15 @@
 // Reference: F.cross_entropy on shifted [B*(S-1), V] logits, fp32 under autocast
 // (gpt.py:449-453; SURVEY §2.5 K11/K12: the fp32 log_softmax alone is 1.65 GB for
 // small at B=8).  Here the bf16 logits buffer [M, Vp] from the lm_head GEMM is
-// read twice (online max/sum pass, then grad pass) and overwritten by
+// overwritten by
 //   dlogits = (softmax(l) - onehot(target)) / n_valid       (0 for padded columns
 // and for rows whose target is ignore_index), so no fp32 logits or separate
-// softmax-backward kernel ever exist.  One 256-thread block per row; loads are 16 B.
+// softmax-backward kernel ever exist.
+//
+// k_ce_row: one 512-thread block per row holds the whole row in registers (CPT
+// 16-byte chunks per thread: 13 for Vp = 50304, i.e. 52 VGPRs), so HBM sees exactly
+// one read and one write of the logits (the memory-bound minimum).  Rows too long for
+// that fall back to k_ce_fwd_bwd (online max/sum pass + gradient pass).
 #include "common.h"
 
 __global__ __launch_bounds__(256) void k_ce_fwd_bwd(bf16_t* __restrict__ logits, const int64_t* __restrict__ targets,
@@ -73,9 +78,127 @@ __global__ __launch_bounds__(256) void k_ce_fwd_bwd(bf16_t* __restrict__ logits,
   }
 }
 
+template <int CPT>
+__global__ __launch_bounds__(512) void k_ce_row(bf16_t* __restrict__ logits, const int64_t* __restrict__ targets,
+                                                const int64_t* __restrict__ n_valid, float* __restrict__ loss_rows,
+                                                int M, int Vp, int V) {
+  // Per element only: max, one exp2 for the sum, one exp2 + scale for the gradient.
+  // Column bounds are tested per 8-wide chunk (only the last chunk straddles V), and
+  // the target column is patched by its owning thread per chunk, not per element.
+  __shared__ float red[8];
+  const int row = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  bf16_t* lrow = logits + (size_t)row * Vp;
+  const int64_t tgt = targets[row];
+  const bool valid = tgt >= 0 && tgt < V;
+  const int tchunk = valid ? (int)(tgt >> 3) : -1;
+  const int nchunk = Vp >> 3;
+  const float L2E = 1.44269504088896340736f;
+  uint4 x[CPT];  // 8 bf16 per chunk as 4 packed words
+#pragma unroll
+  for (int t = 0; t < CPT; ++t) {
+    const int c = tid + 512 * t;
+    if (c < nchunk) x[t] = *reinterpret_cast<const uint4*>(lrow + c * 8);
+  }
+  auto el = [&](int t, int e) -> float {
+    const uint32_t w = e < 2 ? (e == 0 ? x[t].x : x[t].x) : e < 4 ? x[t].y : e < 6 ? x[t].z : x[t].w;
+    return __uint_as_float((e & 1) ? (w & 0xffff0000u) : (w << 16));
+  };
+  // Keep only the raw bf16 words live across the passes (52 VGPRs at CPT 13): the
+  // empty asm makes the compiler re-convert per pass instead of holding 104 floats.
+  auto pin = [&]() {
+#pragma unroll
+    for (int t = 0; t < CPT; ++t) {
+      asm volatile("" : "+v"(x[t].x), "+v"(x[t].y), "+v"(x[t].z), "+v"(x[t].w));
+    }
+  };
+  float mx = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < CPT; ++t) {
+    const int c = tid + 512 * t;
+    if (c * 8 + 8 <= V) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) mx = fmaxf(mx, el(t, e));
+    } else if (c < nchunk) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (c * 8 + e < V) mx = fmaxf(mx, el(t, e));
+    }
+  }
+  pin();
+  mx = wave_max(mx);
+  if (lane == 0) red[wid] = mx;
+  __syncthreads();
+  float gm = red[0];
+#pragma unroll
+  for (int w = 1; w < 8; ++w) gm = fmaxf(gm, red[w]);
+  __syncthreads();
+  const float nm2 = -gm * L2E;
+  float sm = 0.f;
+#pragma unroll
+  for (int t = 0; t < CPT; ++t) {
+    const int c = tid + 512 * t;
+    if (c * 8 + 8 <= V) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sm += __builtin_amdgcn_exp2f(fmaf(el(t, e), L2E, nm2));
+    } else if (c < nchunk) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (c * 8 + e < V) sm += __builtin_amdgcn_exp2f(fmaf(el(t, e), L2E, nm2));
+    }
+  }
+  pin();
+  sm = wave_sum(sm);
+  if (lane == 0) red[wid] = sm;
+  __syncthreads();
+  float gs = 0.f;
+#pragma unroll
+  for (int w = 0; w < 8; ++w) gs += red[w];
+  const float lse = gm + __logf(gs);
+  const int64_t nv = *n_valid;
+  const float inv_n = valid ? 1.f / (float)(nv > 0 ? nv : 1) : 0.f;
+  const float nl2 = -lse * L2E;
+#pragma unroll
+  for (int t = 0; t < CPT; ++t) {
+    const int c = tid + 512 * t;
+    if (c < nchunk) {
+      u16x8 o;
+      if (c * 8 + 8 <= V) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o.v[e] = f2bf(__builtin_amdgcn_exp2f(fmaf(el(t, e), L2E, nl2)) * inv_n);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          o.v[e] = f2bf(c * 8 + e < V ? __builtin_amdgcn_exp2f(fmaf(el(t, e), L2E, nl2)) * inv_n : 0.f);
+      }
+      if (c == tchunk) {
+        const int e = (int)(tgt & 7);
+        float l = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) l = (j == e) ? el(t, j) : l;
+        loss_rows[row] = lse - l;
+        const uint16_t gt = f2bf((__builtin_amdgcn_exp2f(fmaf(l, L2E, nl2)) - 1.f) * inv_n);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o.v[j] = (j == e) ? gt : o.v[j];
+      }
+      *reinterpret_cast<u16x8*>(lrow + c * 8) = o;
+    }
+  }
+  if (!valid && tid == 0) loss_rows[row] = 0.f;
+}
+
 DLT_API int dlt_cross_entropy_fwd_bwd(bf16_t* logits, const int64_t* targets, const int64_t* n_valid,
                                       float* loss_rows, int M, int Vp, int V, hipStream_t st) {
   if (Vp % 8 || V > Vp) return -1;
-  k_ce_fwd_bwd<<<M, 256, 0, st>>>(logits, targets, n_valid, loss_rows, M, Vp, V);
+  const int cpt = (Vp / 8 + 511) / 512;
+#define CE_ARGS logits, targets, n_valid, loss_rows, M, Vp, V
+  if (cpt <= 1) k_ce_row<1><<<M, 512, 0, st>>>(CE_ARGS);
+  else if (cpt <= 2) k_ce_row<2><<<M, 512, 0, st>>>(CE_ARGS);
+  else if (cpt <= 4) k_ce_row<4><<<M, 512, 0, st>>>(CE_ARGS);
+  else if (cpt <= 8) k_ce_row<8><<<M, 512, 0, st>>>(CE_ARGS);
+  else if (cpt <= 13) k_ce_row<13><<<M, 512, 0, st>>>(CE_ARGS);
+  else if (cpt <= 16) k_ce_row<16><<<M, 512, 0, st>>>(CE_ARGS);
+  else k_ce_fwd_bwd<<<M, 256, 0, st>>>(CE_ARGS);
+#undef CE_ARGS
   DLT_CHECK_LAUNCH();
 }

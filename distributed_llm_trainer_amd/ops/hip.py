@@ -28,7 +28,7 @@ _SIGS = {
     "dlt_add_dropout_rmsnorm_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                                     c_float, c_uint32, c_uint32, c_float, c_void_p],
     "dlt_rmsnorm_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                        c_int, c_int, c_uint32, c_uint32, c_float, c_void_p],
+                        c_void_p, c_int, c_int, c_uint32, c_uint32, c_float, c_void_p],
     "dlt_embedding_fwd": [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p],
     "dlt_embedding_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "dlt_rope_qkv_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
@@ -181,8 +181,10 @@ def rmsnorm_bwd(dy, x, rstd, weight, dres, dweight, p_prev, key_prev, dy_scale=N
         _req(dd, torch.bfloat16, "rmsnorm_bwd.ddelta", M * H)
     thr = rng.keep_threshold(p_prev)
     dscale = 1.0 / (1.0 - p_prev) if thr else 1.0
-    _chk(lib().dlt_rmsnorm_bwd(_p(dy), _p(x), _p(rstd), _p(w), _p(dres), _p(dx), _p(dd), _p(dweight), _p(scale_t),
-                               M, H, key_prev & 0xFFFFFFFF, thr, dscale, _stream()), "rmsnorm_bwd")
+    # per-block dw partials (two-stage column reduction instead of same-address atomics)
+    ws = torch.empty(min((M + 3) // 4, 1024) * H, dtype=torch.float32, device=x.device)
+    _chk(lib().dlt_rmsnorm_bwd(_p(dy), _p(x), _p(rstd), _p(w), _p(dres), _p(dx), _p(dd), _p(dweight), _p(ws),
+                               _p(scale_t), M, H, key_prev & 0xFFFFFFFF, thr, dscale, _stream()), "rmsnorm_bwd")
     return dx, dd
 
 
