@@ -38,6 +38,7 @@ from ..models.gpt import GPT, count_parameters
 from ..parallel.ddp import DDPRuntime
 from ..parallel.flat import FlatParamStore
 from ..utils import checkpoint as ckpt
+from ..utils import debug as dbg
 from ..utils.profiling import Profiler, range_push, range_pop
 from .common import cosine_lr, memory_stats, seed_all, select_device, setup_distributed, unwrap_batch
 from .configs import TrainingConfig
@@ -202,6 +203,8 @@ class DistributedTrainer:
         self.optimizer.load_state_dict(c["optimizer"])
         self.global_step = int(c["global_step"])
         self.tokens_seen = int(c["tokens_seen"])
+        if self.use_engine:  # dropout streams continue exactly where the saved run was
+            self.model.engine.micro_counter = self.global_step * self.training_config.gradient_accumulation_steps
         if self.is_main_process:
             print(f"Loaded Checkpoint from {path} (step {self.global_step})")
 
@@ -300,10 +303,14 @@ def main(argv=None):
     metrics_f = open(args.metrics_jsonl, "a") if (args.metrics_jsonl and trainer.is_main_process) else None
     prof = Profiler(args.profile, enabled=bool(args.profile) and trainer.is_main_process)
     data_iter = iter(dataloader)
+    check_every = dbg.replica_check_interval()
+    if check_every:
+        dbg.check_replicas(trainer.store.flat)
     start_time = time.time()
     start_step = trainer.global_step
     steady_t0, steady_tok0 = None, 0
     for step in range(start_step, tc.max_steps):
+        dbg.maybe_inject_fault(step, trainer.rank)
         try:
             batch = next(data_iter)
         except StopIteration:
@@ -328,6 +335,8 @@ def main(argv=None):
                     rec["grad_norm"] = float(trainer._last_norm)
                 metrics_f.write(json.dumps(rec) + "\n")
                 metrics_f.flush()
+        if check_every and (step + 1) % check_every == 0:
+            dbg.check_replicas(trainer.store.flat)
         if step > 0 and step % tc.save_interval == 0:
             trainer.save_checkpoint(f"{tc.checkpoint_dir}/step_{step}.pt")
     prof.close()

@@ -28,6 +28,7 @@ from ..models.config import GPTConfig
 from ..models.gpt import GPT, count_parameters
 from ..parallel.fsdp import FSDPRuntime
 from ..utils import checkpoint as ckpt
+from ..utils import debug as dbg
 from .common import cosine_lr, memory_stats, seed_all, select_device, setup_distributed, unwrap_batch
 from .configs import FSDPConfig, FSDPTrainingConfig
 from .optim import FlatAdamW
@@ -222,6 +223,7 @@ class FSDPTrainer:
             opt.exp_avg[a:b].copy_(fm[la:lb].to(opt.exp_avg.device))
             opt.exp_avg_sq[a:b].copy_(fv[la:lb].to(opt.exp_avg_sq.device))
         self.global_step, self.tokens_seen, opt.step_count = meta[0]
+        self.model.engine.micro_counter = self.global_step * self.training_config.gradient_accumulation_steps
         if self.is_main_process:
             print(f"Loaded Checkpoint from {path} (step {self.global_step})")
 
@@ -303,6 +305,7 @@ def main(argv=None):
     data_iter = iter(dataloader)
     start_time = time.time()
     for step in range(trainer.global_step, tc.max_steps):
+        dbg.maybe_inject_fault(step, trainer.rank)
         try:
             batch = next(data_iter)
         except StopIteration:

@@ -65,3 +65,35 @@ def test_fsdp_cli_single_process(tmp_path, capsys):
     assert c["global_step"] == 6 and "fsdp_config" in c
     assert all(isinstance(k, str) for k in c["optimizer"]["state"])
     assert torch.isfinite(torch.stack([v.float().norm() for v in c["model"].values()])).all()
+
+
+def _run_cli(args, env_extra):
+    import subprocess
+    import sys
+    env = dict(os.environ, **env_extra)
+    env.pop("RANK", None)
+    return subprocess.run([sys.executable, "-m", "distributed_llm_trainer_amd.training.ddp_trainer", *args],
+                          env=env, capture_output=True, text=True, timeout=600)
+
+
+def test_fault_injection_then_resume_matches_uninterrupted(tmp_path):
+    """Kill the run at step 8 (DLT_FAULT_INJECT), resume from step_5.pt, and land on the
+    same final weights and optimizer state as a run that never stopped (data stream,
+    dropout streams, LR schedule and AdamW state all resume exactly)."""
+    cfg = _yaml(tmp_path)
+    full, part = str(tmp_path / "full"), str(tmp_path / "part")
+    r = _run_cli(["--config", cfg, "--max_steps", "12", "--checkpoint_dir", full], {})
+    assert r.returncode == 0, r.stderr[-2000:]
+    r = _run_cli(["--config", cfg, "--max_steps", "12", "--checkpoint_dir", part], {"DLT_FAULT_INJECT": "8"})
+    assert r.returncode == 17 and "injected fault at step 8" in r.stderr
+    assert not os.path.exists(os.path.join(part, "final.pt"))
+    r = _run_cli(["--config", cfg, "--max_steps", "12", "--checkpoint_dir", part,
+                  "--resume_from", os.path.join(part, "step_5.pt")], {})
+    assert r.returncode == 0, r.stderr[-2000:]
+    a = load_checkpoint(os.path.join(full, "final.pt"))
+    b = load_checkpoint(os.path.join(part, "final.pt"))
+    assert a["global_step"] == b["global_step"] == 12
+    for k in a["model"]:
+        assert torch.equal(a["model"][k], b["model"][k]), k
+    for i, st in a["optimizer"]["state"].items():
+        assert torch.equal(st["exp_avg"], b["optimizer"]["state"][i]["exp_avg"])

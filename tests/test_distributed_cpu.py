@@ -156,3 +156,24 @@ def test_fsdp_single_matches_ddp_engine():
     fsdp_sd = _fsdp_single(3, 2)
     for k in fsdp_sd:
         assert torch.allclose(fsdp_sd[k], ddp_sd[k], atol=3e-5, rtol=1e-4), k
+
+
+def _replica_worker(rank, world):
+    import torch
+    from distributed_llm_trainer_amd.training.common import setup_distributed
+    from distributed_llm_trainer_amd.utils import debug
+    setup_distributed()
+    flat = torch.arange(1000, dtype=torch.float32) * 0.01
+    debug.check_replicas(flat)  # identical replicas pass
+    if rank == 1:
+        flat[123] += 1e-6  # one ulp-scale divergence on one rank
+    try:
+        debug.check_replicas(flat)
+        return "no error"
+    except RuntimeError as e:
+        return str(e)
+
+
+def test_replica_divergence_detected():
+    out = run_multiprocess(_replica_worker, world=2)
+    assert all("ranks [1]" in o for o in out), out
