@@ -18,10 +18,11 @@
 //  * Wave-uniform control: the wave index goes through readfirstlane, and each tile
 //    is dispatched to a MASKED (diagonal / ragged) or UNMASKED instantiation, so the
 //    hot loop has no exec-mask divergence and no per-element mask selects.
-//  * Dropout: the forward regenerates the keep decision from a counter hash (one
-//    lowbias32 per two keys) and ALSO stores it as a bitmask [bh][S][ceil(S/32)]
-//    (12.6 MB per layer at B8 S1024 nh12); the two backward kernels read bits
-//    instead of re-hashing (the hash is ~half the VALU work of a tile).
+//  * Dropout: a VALU kernel hashes the keep decisions once (one lowbias32 per two
+//    keys) into bitmasks in two layouts, row-major [bh][q][S/32] for the kernels
+//    whose lanes are queries (fwd, dQ) and transposed [bh][k][S/32] for dK/dV whose
+//    lanes are keys -- every MFMA kernel fetches ONE 32-bit word per lane per 32x32
+//    sub-tile (2 x 12.6 MB per layer at B8 S1024 nh12).
 //  * Backward = 3 kernels: delta = rowsum(dO*O); dK/dV (workgroup per 128 keys,
 //    accumulated in registers); dQ (workgroup per 128 queries, recomputes S, dP) --
 //    no fp32 atomics anywhere.  Causal tile skipping; heaviest tiles launch first.
@@ -130,46 +131,61 @@ __device__ __forceinline__ bf16x8_t load_row8(const bf16_t* __restrict__ p, bool
 }
 
 // ============================================================================ dropout bits
-// keep-bit words: mask[bh][q][w] bit j = keep(q, key = 32w + j), causal words only
-// (w*32 <= q).  Pure VALU at full occupancy (~3 us per layer at B8 nh12 S1024), so
-// the MFMA kernels only test bits instead of hashing at 2 waves/SIMD.
-__global__ __launch_bounds__(256) void k_dropout_bits(uint32_t* __restrict__ mask, int BH, int S, uint32_t key,
-                                                      uint32_t thr) {
-  // grid: (ceil(n_causal_words / 256), BH).  Thread t enumerates only the causal words
-  // (w*32 <= q): rows of 32-row band r have r+1 words, band r starts at word
-  // 32*r*(r+1)/2 -- no idle lanes above the diagonal.  32-bit index math only.
-  const int W = (S + 31) >> 5;
+// Keep-bit words in two layouts (one hash per element pair, computed once):
+//   mask [bh][q][w]  bit j = keep(q, key = 32w + j)   -- lane = query (fwd, dQ)
+//   maskT[bh][k][w]  bit j = keep(q = 32w + j, key k) -- lane = key   (dK/dV)
+// Only causal 32x32 tiles (key word <= query band) exist.  One half-wave per tile:
+// lane l hashes row q = 32r + l (16 hashes -> its row word), then 32 wave ballots
+// transpose the tile's bits so lane j holds the column word of key 32w + j.
+// Pure VALU at full occupancy (~3-4 us per layer at B8 nh12 S1024), so the MFMA
+// kernels only test bits instead of hashing at 2 waves/SIMD.
+__global__ __launch_bounds__(256) void k_dropout_bits(uint32_t* __restrict__ mask, uint32_t* __restrict__ maskT,
+                                                      int BH, int S, uint32_t key, uint32_t thr) {
+  const int W = (S + 31) >> 5;  // words per row == number of 32-row bands
   const int bh = blockIdx.y;
-  const int t = blockIdx.x * 256 + threadIdx.x;
-  const int nb = W;  // number of 32-row bands
-  const int total = 16 * nb * (nb + 1);  // 32 * sum_{r<nb} (r+1)
-  if (t >= total) return;
-  int r = (int)((sqrtf(1.f + (float)t / 4.f) - 1.f) * 0.5f);  // approx band, then fix up
-  while (16 * (r + 1) * (r + 2) <= t) ++r;
-  while (r > 0 && 16 * r * (r + 1) > t) --r;
-  const int rem = t - 16 * r * (r + 1);  // index within band r: (row-in-band, word)
-  const int q = r * 32 + rem / (r + 1);
-  const int w = rem % (r + 1);
-  if (q >= S) return;
-  const uint32_t kbh = lowbias32(key + (uint32_t)bh * 0x9E3779B9u);
-  const uint32_t base = (uint32_t)q * (uint32_t)S + (uint32_t)(w * 32);
-  const int nk = min(32, S - w * 32);
-  uint32_t word = 0;
-  if ((base & 1u) == 0 && nk == 32) {
-#pragma unroll
-    for (int j = 0; j < 32; j += 2) {
-      const uint32_t hsh = lowbias32(kbh ^ ((base + j) >> 1));
-      word |= ((uint32_t)((hsh & 0xffffu) >= thr) << j) | ((uint32_t)((hsh >> 16) >= thr) << (j + 1));
-    }
-  } else {
-    for (int j = 0; j < nk; ++j) {
-      const uint32_t flat = base + (uint32_t)j;
-      const uint32_t hsh = lowbias32(kbh ^ (flat >> 1));
-      const uint32_t bits = (flat & 1u) ? (hsh >> 16) : (hsh & 0xffffu);
-      word |= (uint32_t)(bits >= thr) << j;
-    }
+  const int lane = threadIdx.x & 63, l = lane & 31, half = lane >> 5;
+  const int tile = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + half;  // one tile per half-wave
+  const int ntiles = W * (W + 1) / 2;
+  const bool active = tile < ntiles;
+  // tile -> (band r, word w <= r): band r starts at tile r(r+1)/2
+  int r = active ? (int)((sqrtf(8.f * (float)tile + 1.f) - 1.f) * 0.5f) : 0;
+  if (active) {
+    while ((r + 1) * (r + 2) / 2 <= tile) ++r;
+    while (r > 0 && r * (r + 1) / 2 > tile) --r;
   }
-  mask[((size_t)bh * S + q) * W + w] = word;
+  const int w = active ? tile - r * (r + 1) / 2 : 0;
+  const int q = r * 32 + l;
+  const uint32_t kbh = lowbias32(key + (uint32_t)bh * 0x9E3779B9u);
+  uint32_t word = 0;
+  if (active && q < S) {
+    const uint32_t base = (uint32_t)q * (uint32_t)S + (uint32_t)(w * 32);
+    const int nk = min(32, S - w * 32);
+    if ((base & 1u) == 0 && nk == 32) {
+#pragma unroll
+      for (int j = 0; j < 32; j += 2) {
+        const uint32_t hsh = lowbias32(kbh ^ ((base + j) >> 1));
+        word |= ((uint32_t)((hsh & 0xffffu) >= thr) << j) | ((uint32_t)((hsh >> 16) >= thr) << (j + 1));
+      }
+    } else {
+      for (int j = 0; j < nk; ++j) {
+        const uint32_t flat = base + (uint32_t)j;
+        const uint32_t hsh = lowbias32(kbh ^ (flat >> 1));
+        const uint32_t bits = (flat & 1u) ? (hsh >> 16) : (hsh & 0xffffu);
+        word |= (uint32_t)(bits >= thr) << j;
+      }
+    }
+    mask[((size_t)bh * S + q) * W + w] = word;
+  }
+  // transpose within each half-wave: bit (row l, key j) -> column word j, bit l
+  uint32_t col = 0;
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    const uint64_t bal = __ballot((word >> j) & 1u);
+    const uint32_t mine = half ? (uint32_t)(bal >> 32) : (uint32_t)bal;
+    col = (l == j) ? mine : col;
+  }
+  const int kk = w * 32 + l;
+  if (active && kk < S) maskT[((size_t)bh * S + kk) * W + r] = col;
 }
 
 // ============================================================================ forward
@@ -359,8 +375,8 @@ __global__ __launch_bounds__(256) void k_attn_bwd_delta(const bf16_t* __restrict
 template <bool MASK, bool DROP>
 __device__ __forceinline__ void dkdv_subtile(floatx16_t (&dka)[2], floatx16_t (&dva)[2], const bf16_t* Qt,
                                              const bf16_t* Dt, const float* rl, const float* rd,
-                                             const uint32_t* mw, const bf16x8_t (&kf)[4], const bf16x8_t (&vf)[4],
-                                             int qs, int ka, int S, int lane, int wid, float c_log2, float dscale) {
+                                             uint32_t mw, const bf16x8_t (&kf)[4], const bf16x8_t (&vf)[4],
+                                             int qs, int ka, int S, int lane, float c_log2, float dscale) {
   const int h = lane >> 5, kl = lane & 31;
   floatx16_t sacc = zero16(), pacc = zero16();
 #pragma unroll
@@ -386,7 +402,7 @@ __device__ __forceinline__ void dkdv_subtile(floatx16_t (&dka)[2], floatx16_t (&
       float dp = pacc[i];
       float pd = p;
       if (DROP) {
-        const bool keep = (mw[r * 4 + wid] >> kl) & 1u;
+        const bool keep = (mw >> r) & 1u;  // maskT word: bit r = query qs + r
         pd = keep ? p : 0.f;  // 1/(1-p) folded into the dV epilogue
         dp = keep ? dp * dscale : 0.f;
       }
@@ -412,14 +428,13 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dkdv(const bf16_t* __restri
                                                           const bf16_t* __restrict__ dout,
                                                           const float* __restrict__ lse,
                                                           const float* __restrict__ delta,
-                                                          const uint32_t* __restrict__ mask, bf16_t* __restrict__ dk,
+                                                          const uint32_t* __restrict__ maskT, bf16_t* __restrict__ dk,
                                                           bf16_t* __restrict__ dv, int S, int nh, float c_log2,
                                                           float scale, float dscale) {
   // one LDS object (avoids hipcc's extra vmcnt waits with several __shared__ arrays)
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * QSTEP * HD * 2 + 2 * 2 * QSTEP * 4 + 2 * QSTEP * 4 * 4];
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * QSTEP * HD * 2 + 2 * 2 * QSTEP * 4];
   bf16_t* lds = reinterpret_cast<bf16_t*>(smem);                              // [buf][Q|dO][64][64]
   float* rowc = reinterpret_cast<float*>(smem + 2 * 2 * QSTEP * HD * 2);      // [buf][lse2|delta][64]
-  uint32_t* mws = reinterpret_cast<uint32_t*>(smem + 2 * 2 * QSTEP * HD * 2 + 2 * 2 * QSTEP * 4);  // [buf][64][4]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, kl = lane & 31;
@@ -432,6 +447,8 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dkdv(const bf16_t* __restri
   const int rstride = nh * HD;
   const int W = (S + 31) >> 5;
   const bf16_t* dob = dout + ((size_t)b * S * nh + head) * HD;
+  // this lane's key column of the transposed keep-bit mask: one word per 32 queries
+  const uint32_t* mcol = DROP ? maskT + ((size_t)bh * S + min(ka, S - 1)) * W : nullptr;
 
   bf16x8_t kf[4], vf[4];
   const int kc = min(ka, S - 1);
@@ -446,7 +463,6 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dkdv(const bf16_t* __restri
   const int nqt = (S + QSTEP - 1) / QSTEP;
   Stage2 sq, sd;
   float rl = 0.f, rd = 0.f;
-  uint32_t mwv = 0;
   auto load_rows = [&](int t) {
     stage_load(sq, q + hoff, t * QSTEP, S, HD, tid);
     stage_load(sd, dob, t * QSTEP, S, rstride, tid);
@@ -456,11 +472,6 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dkdv(const bf16_t* __restri
       rl = ok ? lse[(size_t)bh * S + qq] * LOG2E : 0.f;
       rd = ok ? delta[(size_t)bh * S + qq] : 0.f;
     }
-    if (DROP) {
-      const int qq = t * QSTEP + (tid >> 2);
-      const int wi = kblk * 4 + (tid & 3);
-      mwv = (qq < S && wi < W) ? mask[((size_t)bh * S + qq) * W + wi] : 0u;
-    }
   };
   auto store_rows = [&](int buf) {
     stage_store(sq, lds + buf * 2 * QSTEP * HD, tid);
@@ -469,7 +480,6 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dkdv(const bf16_t* __restri
       rowc[buf * 2 * QSTEP + tid] = rl;
       rowc[buf * 2 * QSTEP + QSTEP + tid] = rd;
     }
-    if (DROP) mws[buf * QSTEP * 4 + tid] = mwv;
   };
   if (qt_begin < nqt) {
     load_rows(qt_begin);
@@ -480,23 +490,29 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dkdv(const bf16_t* __restri
   for (int t = qt_begin; t < nqt; ++t) {
     const int cur = (t - qt_begin) & 1;
     const bool more = t + 1 < nqt;
+    uint32_t mw0 = 0, mw1 = 0;
+    if (DROP) {  // the two 32-query words of this tile (issued before the staging loads)
+      const int w0 = (t * QSTEP) >> 5;
+      mw0 = mcol[w0];
+      mw1 = (w0 + 1 < W) ? mcol[w0 + 1] : 0u;
+    }
     if (more) load_rows(t + 1);
     const bf16_t* Qt = lds + cur * 2 * QSTEP * HD;
     const bf16_t* Dt = Qt + QSTEP * HD;
     const float* rlp = rowc + cur * 2 * QSTEP;
     const float* rdp = rlp + QSTEP;
-    const uint32_t* mwp = mws + cur * QSTEP * 4;
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
       const int qs = t * QSTEP + 32 * qt;
       const bf16_t* Qs = Qt + 32 * qt * HD;
       const bf16_t* Ds = Dt + 32 * qt * HD;
+      const uint32_t mw = qt ? mw1 : mw0;
       if (qs >= k0 + 31 && qs + 32 <= S && k0 + 32 <= S) {
-        dkdv_subtile<false, DROP>(dka, dva, Qs, Ds, rlp + 32 * qt, rdp + 32 * qt, mwp + 32 * qt * 4, kf, vf, qs, ka,
-                                  S, lane, wid, c_log2, dscale);
+        dkdv_subtile<false, DROP>(dka, dva, Qs, Ds, rlp + 32 * qt, rdp + 32 * qt, mw, kf, vf, qs, ka, S, lane,
+                                  c_log2, dscale);
       } else if (qs + 31 >= k0) {
-        dkdv_subtile<true, DROP>(dka, dva, Qs, Ds, rlp + 32 * qt, rdp + 32 * qt, mwp + 32 * qt * 4, kf, vf, qs, ka,
-                                 S, lane, wid, c_log2, dscale);
+        dkdv_subtile<true, DROP>(dka, dva, Qs, Ds, rlp + 32 * qt, rdp + 32 * qt, mw, kf, vf, qs, ka, S, lane,
+                                 c_log2, dscale);
       }
     }
     if (more) store_rows(cur ^ 1);
@@ -644,8 +660,9 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dq(const bf16_t* __restrict
 }
 
 // ============================================================================ launchers
-// mask: uint32 [B*nh, S, ceil(S/32)] keep-bits written by the forward when dropout is
-// on (may be null: then the forward only regenerates masks on the fly).
+// mask: uint32 [2][B*nh, S, ceil(S/32)] keep-bits written by the forward when dropout
+// is on -- [0] row layout (lane = query), [1] transposed (lane = key), see
+// k_dropout_bits.
 DLT_API int dlt_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, uint32_t* mask,
                          int B, int nh, int S, int hd, float scale, uint32_t key, uint32_t thr, float dscale,
                          hipStream_t st) {
@@ -654,9 +671,10 @@ DLT_API int dlt_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16
   const dim3 grid((S + QB - 1) / QB, B * nh);
   const float c_log2 = scale * LOG2E;
   if (thr) {
-    const int nbands = (S + 31) / 32;
-    const int words = 16 * nbands * (nbands + 1);
-    k_dropout_bits<<<dim3((words + 255) / 256, B * nh), 256, 0, st>>>(mask, B * nh, S, key, thr);
+    const int W = (S + 31) / 32;
+    const int ntiles = W * (W + 1) / 2;  // 8 tiles (2 per wave) per block
+    uint32_t* maskT = mask + (size_t)B * nh * S * W;
+    k_dropout_bits<<<dim3((ntiles + 7) / 8, B * nh), 256, 0, st>>>(mask, maskT, B * nh, S, key, thr);
     k_attn_fwd<true><<<grid, 256, 0, st>>>(q, k, v, o, lse, mask, S, nh, c_log2, dscale);
   } else {
     k_attn_fwd<false><<<grid, 256, 0, st>>>(q, k, v, o, lse, nullptr, S, nh, c_log2, dscale);
@@ -674,7 +692,9 @@ DLT_API int dlt_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, cons
   const dim3 gk((S + KB - 1) / KB, B * nh);
   const dim3 gq((S + QB - 1) / QB, B * nh);
   if (mask) {
-    k_attn_bwd_dkdv<true><<<gk, 256, 0, st>>>(q, k, v, dout, lse, delta_ws, mask, dk, dv, S, nh, c_log2, scale, dscale);
+    const uint32_t* maskT = mask + (size_t)B * nh * S * ((S + 31) / 32);
+    k_attn_bwd_dkdv<true><<<gk, 256, 0, st>>>(q, k, v, dout, lse, delta_ws, maskT, dk, dv, S, nh, c_log2, scale,
+                                              dscale);
     k_attn_bwd_dq<true><<<gq, 256, 0, st>>>(q, k, v, dout, lse, delta_ws, mask, dq, S, nh, c_log2, scale, dscale);
   } else {
     k_attn_bwd_dkdv<false><<<gk, 256, 0, st>>>(q, k, v, dout, lse, delta_ws, mask, dk, dv, S, nh, c_log2, scale, dscale);

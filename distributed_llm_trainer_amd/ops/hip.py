@@ -222,7 +222,8 @@ def rope_qkv_bwd(dq, dk, dv, cos, sin, out=None):
 
 # -------------------------------------------------------------- attention
 class AttnAux(tuple):
-    """(lse [B,nh,S] fp32, keep-bit mask [B*nh, S, ceil(S/32)] uint32 or None)."""
+    """(lse [B,nh,S] fp32, keep-bit masks [2, B*nh, S, ceil(S/32)] int32 or None:
+    [0] = bits by (query, key word), [1] = bits by (key, query word))."""
 
 
 def attention_fwd(q, k, v, p, key, causal=True, store_mask=True, out=None):
@@ -242,7 +243,8 @@ def attention_fwd(q, k, v, p, key, causal=True, store_mask=True, out=None):
     dscale = 1.0 / (1.0 - p) if thr else 1.0
     mask = None
     if thr and store_mask:
-        mask = torch.empty(B * nh, S, (S + 31) // 32, dtype=torch.int32, device=q.device)
+        # [0] row layout (lane = query), [1] transposed (lane = key) -- see attention.hip
+        mask = torch.empty(2, B * nh, S, (S + 31) // 32, dtype=torch.int32, device=q.device)
     _chk(lib().dlt_attn_fwd(_p(q), _p(k), _p(v), _p(o), _p(lse), _p(mask), B, nh, S, hd, 1.0 / math.sqrt(hd),
                             key & 0xFFFFFFFF, thr, dscale, _stream()), "attn_fwd")
     return o, AttnAux((lse, mask))
