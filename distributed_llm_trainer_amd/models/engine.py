@@ -157,6 +157,7 @@ class GPTEngine:
         self.acc_slot, self.acc_slots, self.defer = 0, 1, False
         self._slots = {}
         self._side = None  # weight-gradient side stream (lazily created)
+        self._mask_side = None  # attention keep-bit side stream
 
     # ------------------------------------------------------- grad accumulation
     def set_accumulation(self, slot: int, n_slots: int, defer: bool = True) -> None:
@@ -197,6 +198,25 @@ class GPTEngine:
                 rng.site_key(self.seed, micro, layer, rng.SITE_MLP))
 
     # ---------------------------------------------------------------- forward
+    def _attn_mask_async(self, B, S, p, key, dev):
+        """(mask, ready-event) built on a side stream (opt-in, ``DLT_MASK_STREAM=1``), or
+        (None, None) to let the attention launch build it inline.  Measured neutral on
+        the headline config (the GPU is saturated either way), so off by default."""
+        if (p <= 0.0 or dev.type != "cuda" or not hasattr(self.ops, "attention_dropout_mask")
+                or os.environ.get("DLT_MASK_STREAM", "0") != "1"):
+            return None, None
+        if self._mask_side is None:
+            self._mask_side = torch.cuda.Stream(dev)
+        main = torch.cuda.current_stream()
+        # allocated from the side stream's own pool: no wait on main needed, so the
+        # masks of later layers can be produced while earlier layers still compute
+        with torch.cuda.stream(self._mask_side):
+            mask = self.ops.attention_dropout_mask(B, self.cfg.num_heads, S, p, key, device=dev)
+            ev = torch.cuda.Event()
+            ev.record()
+        mask.record_stream(main)
+        return mask, ev
+
     def _layer_forward(self, st: _StepState, i: int, r, d, key_d: int, p_d: float,
                        save: bool):
         ops, gm, cfg = self.ops, self.gemm, self.cfg
@@ -210,12 +230,19 @@ class GPTEngine:
         M, H, I = B * S, cfg.hidden_size, cfg.intermediate_size
         dv = r.device
         sb = (lambda name, n: self._slot_buf(st, i, name, M, n, dv)[0]) if st.defer else (lambda name, n: None)
+        # attention keep-bits depend only on the RNG key: build them on a side stream
+        # so the VALU-only hashing overlaps the norm + QKV GEMM + RoPE below
+        mask, mask_ev = self._attn_mask_async(B, S, pa, k_attn, dv)
         x, n1, rstd1 = ops.add_dropout_rmsnorm_fwd(r, d, w.ln1, self.eps, p_d, key_d, self.act_dtype,
                                                    y_out=sb("n1", H))
         qkv = gm.linear(n1, w.wqkv)
         q, k, v = ops.rope_qkv_fwd(qkv, B, S, cfg.num_heads, cos, sin)
         del qkv
-        o, lse = ops.attention_fwd(q, k, v, pa, k_attn, True, out=sb("o", H))
+        if mask is not None:
+            torch.cuda.current_stream().wait_event(mask_ev)
+            o, lse = ops.attention_fwd(q, k, v, pa, k_attn, True, out=sb("o", H), mask=mask)
+        else:
+            o, lse = ops.attention_fwd(q, k, v, pa, k_attn, True, out=sb("o", H))
         a = gm.linear(o, w.wo)
         x2, n2, rstd2 = ops.add_dropout_rmsnorm_fwd(x, a, w.ln2, self.eps, ph, k_resid, self.act_dtype,
                                                     y_out=sb("n2", H))

@@ -31,15 +31,14 @@
 // (= the [M, H] GEMM layout);  lse, delta: [B*nh, S] fp32 (natural-log lse).
 #include "common.h"
 
+#include <type_traits>
+
 #define HD 64
 #define KVB 64     // keys per staged tile (fwd / dQ)
 #define QB 128     // queries per workgroup (fwd / dQ), 32 per wave
 #define KB 128     // keys per workgroup (dK/dV), 32 per wave
 #define QSTEP 64   // queries per staged tile (dK/dV)
 #define LOG2E 1.44269504088896340736f
-#ifndef ATTN_EXP
-#define ATTN_EXP 0  // profiling experiments only (tools/cpp/attn_bench.cpp): 1 = no softmax VALU, 2 = no K/V reloads
-#endif
 
 typedef __attribute__((address_space(3))) shortx4_t lds_shortx4_t;
 typedef short shortx8_t __attribute__((ext_vector_type(8)));
@@ -189,6 +188,24 @@ __global__ __launch_bounds__(256) void k_dropout_bits(uint32_t* __restrict__ mas
 }
 
 // ============================================================================ forward
+// Cross-half (lane i <-> i^32) exchange without LDS: v_permlane32_swap (CDNA4).
+__device__ __forceinline__ float xhalf_max(float x) {
+  const uint32_t u = __float_as_uint(x);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xhalf_sum(float x) {
+  const uint32_t u = __float_as_uint(x);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// Rescale threshold (log2 units): the running max is only moved when some row's max
+// grew by more than 2^RESCALE_LOG2 (P is then bounded by 2^8 = 256 instead of 1,
+// exact in fp32 l/O and the same relative bf16 precision for P).  Almost every
+// rescale after a row's first tile is skipped.
+#define RESCALE_LOG2 8.0f
+
 struct FwdState {
   floatx16_t o[2];
   float m, l;  // running max (raw score units) and per-lane partial row sum
@@ -198,14 +215,13 @@ template <bool MASK, bool DROP>
 __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const bf16_t* Vt, const bf16x8_t (&qf)[4],
                                          int k0, int qa, int S, int lane, float c_log2,
                                          const uint32_t* __restrict__ mrow) {
-  // Two 32-key halves, each a complete online-softmax step, with the LDS reads for
-  // the half's PV product (V^T via tr-reads) issued BEFORE its softmax VALU so their
-  // latency hides under the exp/max work; ~half the live registers of a 64-key step.
+  // Two 32-key halves, each a complete online-softmax step; the V^T tr-reads of a
+  // half are issued before its softmax VALU so their latency hides under it.
   const int h = lane >> 5, ql = lane & 31;
   uint32_t words[2] = {0u, 0u};
-  if (DROP) {
-    words[0] = mrow[k0 >> 5];
-    words[1] = mrow[(k0 >> 5) + 1];
+  if (DROP) {  // this lane-half's 16 keep bits per half-tile sit at (i&3) + 8(i>>2)
+    words[0] = mrow[k0 >> 5] >> (4 * h);
+    words[1] = mrow[(k0 >> 5) + 1] >> (4 * h);
   }
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -220,17 +236,6 @@ __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const b
     floatx16_t sacc = zero16();
 #pragma unroll
     for (int s = 0; s < 4; ++s) sacc = mfma(kf[s], qf[s], sacc);
-#if ATTN_EXP == 1
-    {
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const bf16x8_t pb = acc_frag(sacc, kk);
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) fs.o[dt] = mfma(vf[kk][dt], pb, fs.o[dt]);
-      }
-      continue;
-    }
-#endif
     float mx = -INFINITY;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -240,9 +245,8 @@ __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const b
       }
       mx = fmaxf(mx, sacc[i]);
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    // exact deferred rescale: skip while no lane's running max grows
-    if (__any(mx > fs.m)) {
+    mx = xhalf_max(mx);
+    if (!__all((mx - fs.m) * c_log2 <= RESCALE_LOG2)) {
       const float m_new = fmaxf(fs.m, mx);
       const float alpha = fast_exp2((fs.m - m_new) * c_log2);
       fs.m = m_new;
@@ -257,7 +261,7 @@ __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const b
     for (int i = 0; i < 16; ++i) {
       const float p = fast_exp2(fmaf(sacc[i], c_log2, nmc));
       fs.l += p;
-      if (DROP) sacc[i] = ((words[t] >> acc_row(i, h)) & 1u) ? p : 0.f;  // 1/(1-p) applied at the end
+      if (DROP) sacc[i] = (words[t] & (1u << ((i & 3) + 8 * (i >> 2)))) ? p : 0.f;  // 1/(1-p) at the end
       else sacc[i] = p;
     }
 #pragma unroll
@@ -307,14 +311,16 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd(const bf16_t* __restrict__ 
   stage_store(sv, lds + KVB * HD, tid);
   __syncthreads();
 
-  for (int kb = 0; kb < nkv; ++kb) {
-    const int cur = kb & 1;
-    const bool more = ATTN_EXP != 2 && ATTN_EXP != 4 && kb + 1 < nkv;
+  // One K/V tile per step; BUF is a compile-time LDS buffer index (the loop is
+  // unrolled by two), so every LDS address is lane-base + immediate offset.
+  auto step = [&](auto bufc, int kb) {
+    constexpr int BUF = decltype(bufc)::value;
+    const bool more = kb + 1 < nkv;
     if (more) {
       stage_load(sk, k + hoff, (kb + 1) * KVB, S, HD, tid);
       stage_load(sv, v + hoff, (kb + 1) * KVB, S, HD, tid);
     }
-    const bf16_t* Kt = lds + ((ATTN_EXP == 2 || ATTN_EXP == 4) ? 0 : cur) * 2 * KVB * HD;
+    const bf16_t* Kt = lds + BUF * 2 * KVB * HD;
     const bf16_t* Vt = Kt + KVB * HD;
     const int k0 = kb * KVB;
     if (k0 + KVB - 1 <= q0 && k0 + KVB <= S)
@@ -322,14 +328,18 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd(const bf16_t* __restrict__ 
     else if (k0 <= q0 + 31)
       fwd_tile<true, DROP>(fs, Kt, Vt, qf, k0, qa, S, lane, c_log2, mrow);
     if (more) {
-      bf16_t* Kn = lds + (cur ^ 1) * 2 * KVB * HD;
+      bf16_t* Kn = lds + (BUF ^ 1) * 2 * KVB * HD;
       stage_store(sk, Kn, tid);
       stage_store(sv, Kn + KVB * HD, tid);
     }
-    if (ATTN_EXP < 4) __syncthreads();
+    __syncthreads();
+  };
+  for (int kb = 0; kb < nkv; kb += 2) {
+    step(std::integral_constant<int, 0>{}, kb);
+    if (kb + 1 < nkv) step(std::integral_constant<int, 1>{}, kb + 1);
   }
 
-  const float l_tot = fs.l + __shfl_xor(fs.l, 32, 64);
+  const float l_tot = xhalf_sum(fs.l);
   const float inv_l = (DROP ? dscale : 1.f) / l_tot;
   if (qa < S) {
     if (h == 0) lse[(size_t)bh * S + qa] = fs.m * (c_log2 / LOG2E) + __logf(l_tot);
@@ -402,7 +412,7 @@ __device__ __forceinline__ void dkdv_subtile(floatx16_t (&dka)[2], floatx16_t (&
       float dp = pacc[i];
       float pd = p;
       if (DROP) {
-        const bool keep = (mw >> r) & 1u;  // maskT word: bit r = query qs + r
+        const bool keep = mw & (1u << (8 * g + e));  // maskT word >> 4h: query qs + r
         pd = keep ? p : 0.f;  // 1/(1-p) folded into the dV epilogue
         dp = keep ? dp * dscale : 0.f;
       }
@@ -506,7 +516,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dkdv(const bf16_t* __restri
       const int qs = t * QSTEP + 32 * qt;
       const bf16_t* Qs = Qt + 32 * qt * HD;
       const bf16_t* Ds = Dt + 32 * qt * HD;
-      const uint32_t mw = qt ? mw1 : mw0;
+      const uint32_t mw = (qt ? mw1 : mw0) >> (4 * h);
       if (qs >= k0 + 31 && qs + 32 <= S && k0 + 32 <= S) {
         dkdv_subtile<false, DROP>(dka, dva, Qs, Ds, rlp + 32 * qt, rdp + 32 * qt, mw, kf, vf, qs, ka, S, lane,
                                   c_log2, dscale);
@@ -559,7 +569,7 @@ __device__ __forceinline__ void dq_tile(floatx16_t (&dqa)[2], const bf16_t* Kt, 
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     uint32_t word = 0;
-    if (DROP) word = mrow[(k0 + 32 * t) >> 5];
+    if (DROP) word = mrow[(k0 + 32 * t) >> 5] >> (4 * h);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int kr = acc_row(i, h);
@@ -569,7 +579,7 @@ __device__ __forceinline__ void dq_tile(floatx16_t (&dqa)[2], const bf16_t* Kt, 
         p = (kA > qa || kA >= S) ? 0.f : p;
       }
       float dp = pacc[t][i];
-      if (DROP) dp = ((word >> kr) & 1u) ? dp * dscale : 0.f;
+      if (DROP) dp = (word & (1u << ((i & 3) + 8 * (i >> 2)))) ? dp * dscale : 0.f;
       pacc[t][i] = p * (dp - dl);
     }
   }
@@ -663,18 +673,31 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dq(const bf16_t* __restrict
 // mask: uint32 [2][B*nh, S, ceil(S/32)] keep-bits written by the forward when dropout
 // is on -- [0] row layout (lane = query), [1] transposed (lane = key), see
 // k_dropout_bits.
+// Keep-bit masks only (they depend on the key, not on the data): lets the engine
+// produce them on a side stream ahead of the layer's GEMMs.
+DLT_API int dlt_attn_dropout_mask(uint32_t* mask, int B, int nh, int S, uint32_t key, uint32_t thr,
+                                  hipStream_t st) {
+  if (S <= 0 || !mask || !thr) return -1;
+  const int W = (S + 31) / 32;
+  const int ntiles = W * (W + 1) / 2;  // 8 tiles (2 per wave) per block
+  uint32_t* maskT = mask + (size_t)B * nh * S * W;
+  k_dropout_bits<<<dim3((ntiles + 7) / 8, B * nh), 256, 0, st>>>(mask, maskT, B * nh, S, key, thr);
+  DLT_CHECK_LAUNCH();
+}
+
+// gen_mask = 0: the keep bits are already in `mask` (dlt_attn_dropout_mask).
 DLT_API int dlt_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, uint32_t* mask,
                          int B, int nh, int S, int hd, float scale, uint32_t key, uint32_t thr, float dscale,
-                         hipStream_t st) {
+                         int gen_mask, hipStream_t st) {
   if (hd != HD || S <= 0) return -1;
   if (thr && !mask) return -2;  // dropout needs the keep-bit buffer
   const dim3 grid((S + QB - 1) / QB, B * nh);
   const float c_log2 = scale * LOG2E;
   if (thr) {
-    const int W = (S + 31) / 32;
-    const int ntiles = W * (W + 1) / 2;  // 8 tiles (2 per wave) per block
-    uint32_t* maskT = mask + (size_t)B * nh * S * W;
-    k_dropout_bits<<<dim3((ntiles + 7) / 8, B * nh), 256, 0, st>>>(mask, maskT, B * nh, S, key, thr);
+    if (gen_mask) {
+      const int rc = dlt_attn_dropout_mask(mask, B, nh, S, key, thr, st);
+      if (rc) return rc;
+    }
     k_attn_fwd<true><<<grid, 256, 0, st>>>(q, k, v, o, lse, mask, S, nh, c_log2, dscale);
   } else {
     k_attn_fwd<false><<<grid, 256, 0, st>>>(q, k, v, o, lse, nullptr, S, nh, c_log2, dscale);

@@ -45,7 +45,8 @@ _SIGS = {
     "dlt_cast_bf16": [c_void_p, c_void_p, c_int64, c_void_p],
     "dlt_wgrad_gemm": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
     "dlt_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
-                     c_uint32, c_uint32, c_float, c_void_p],
+                     c_uint32, c_uint32, c_float, c_int, c_void_p],
+    "dlt_attn_dropout_mask": [c_void_p, c_int, c_int, c_int, c_uint32, c_uint32, c_void_p],
     "dlt_attn_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                      c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_float, c_void_p],
 }
@@ -226,9 +227,21 @@ class AttnAux(tuple):
     [0] = bits by (query, key word), [1] = bits by (key, query word))."""
 
 
-def attention_fwd(q, k, v, p, key, causal=True, store_mask=True, out=None):
+def attention_dropout_mask(B, nh, S, p, key, device=None):
+    """Keep-bit masks [2, B*nh, S, ceil(S/32)] for attention dropout (None if p == 0).
+    Data-independent, so the engine builds them on a side stream ahead of time."""
+    thr = rng.keep_threshold(p)
+    if not thr:
+        return None
+    mask = torch.empty(2, B * nh, S, (S + 31) // 32, dtype=torch.int32, device=device)
+    _chk(lib().dlt_attn_dropout_mask(_p(mask), B, nh, S, key & 0xFFFFFFFF, thr, _stream()), "attn_dropout_mask")
+    return mask
+
+
+def attention_fwd(q, k, v, p, key, causal=True, store_mask=True, out=None, mask=None):
     """Returns (o [B*S, nh*hd] bf16, aux).  With dropout on, the keep bits are written
-    to a bitmask consumed by attention_bwd (no re-hashing in the backward)."""
+    to a bitmask consumed by attention_bwd (no re-hashing in the backward); pass
+    ``mask`` from ``attention_dropout_mask`` to skip generating it here."""
     if not causal:
         raise NotImplementedError("only causal attention is implemented (the model is a causal LM)")
     B, nh, S, hd = q.shape
@@ -241,12 +254,17 @@ def attention_fwd(q, k, v, p, key, causal=True, store_mask=True, out=None):
     lse = torch.empty(B, nh, S, dtype=torch.float32, device=q.device)
     thr = rng.keep_threshold(p)
     dscale = 1.0 / (1.0 - p) if thr else 1.0
-    mask = None
-    if thr and store_mask:
+    gen = 1
+    if not thr:
+        mask = None
+    elif mask is not None:
+        _req(mask, torch.int32, "attn.mask", 2 * B * nh * S * ((S + 31) // 32))
+        gen = 0
+    elif store_mask:
         # [0] row layout (lane = query), [1] transposed (lane = key) -- see attention.hip
         mask = torch.empty(2, B * nh, S, (S + 31) // 32, dtype=torch.int32, device=q.device)
     _chk(lib().dlt_attn_fwd(_p(q), _p(k), _p(v), _p(o), _p(lse), _p(mask), B, nh, S, hd, 1.0 / math.sqrt(hd),
-                            key & 0xFFFFFFFF, thr, dscale, _stream()), "attn_fwd")
+                            key & 0xFFFFFFFF, thr, dscale, gen, _stream()), "attn_fwd")
     return o, AttnAux((lse, mask))
 
 
