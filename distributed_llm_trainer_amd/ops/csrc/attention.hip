@@ -246,7 +246,7 @@ __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const b
       mx = fmaxf(mx, sacc[i]);
     }
     mx = xhalf_max(mx);
-    if (!__all((mx - fs.m) * c_log2 <= RESCALE_LOG2)) {
+    if (!__all((mx - fs.m) * c_log2 <= RESCALE_LOG2)) {  // rare: a row's max grew by > 2^8
       const float m_new = fmaxf(fs.m, mx);
       const float alpha = fast_exp2((fs.m - m_new) * c_log2);
       fs.m = m_new;
@@ -274,7 +274,7 @@ __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const b
 }
 
 template <bool DROP>
-__global__ __launch_bounds__(256, 2) void k_attn_fwd(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
+__global__ __launch_bounds__(256, 3) void k_attn_fwd(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
                                                      const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
                                                      float* __restrict__ lse, const uint32_t* __restrict__ mask,
                                                      int S, int nh, float c_log2, float dscale) {
@@ -311,10 +311,13 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd(const bf16_t* __restrict__ 
   stage_store(sv, lds + KVB * HD, tid);
   __syncthreads();
 
-  // One K/V tile per step; BUF is a compile-time LDS buffer index (the loop is
-  // unrolled by two), so every LDS address is lane-base + immediate offset.
-  auto step = [&](auto bufc, int kb) {
+  // One K/V tile per step.  BUF is a compile-time LDS buffer index and MASKED a
+  // compile-time tile kind: tiles kb < 2*qb lie entirely below every query of the
+  // block (one straight-line unmasked loop, unrolled by two so every LDS address is
+  // lane-base + immediate); only the last one or two tiles hold the diagonal.
+  auto step = [&](auto bufc, auto maskc, int kb) {
     constexpr int BUF = decltype(bufc)::value;
+    constexpr bool MASKED = decltype(maskc)::value;
     const bool more = kb + 1 < nkv;
     if (more) {
       stage_load(sk, k + hoff, (kb + 1) * KVB, S, HD, tid);
@@ -323,7 +326,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd(const bf16_t* __restrict__ 
     const bf16_t* Kt = lds + BUF * 2 * KVB * HD;
     const bf16_t* Vt = Kt + KVB * HD;
     const int k0 = kb * KVB;
-    if (k0 + KVB - 1 <= q0 && k0 + KVB <= S)
+    if (!MASKED)
       fwd_tile<false, DROP>(fs, Kt, Vt, qf, k0, qa, S, lane, c_log2, mrow);
     else if (k0 <= q0 + 31)
       fwd_tile<true, DROP>(fs, Kt, Vt, qf, k0, qa, S, lane, c_log2, mrow);
@@ -334,10 +337,17 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd(const bf16_t* __restrict__ 
     }
     __syncthreads();
   };
-  for (int kb = 0; kb < nkv; kb += 2) {
-    step(std::integral_constant<int, 0>{}, kb);
-    if (kb + 1 < nkv) step(std::integral_constant<int, 1>{}, kb + 1);
+  using B0 = std::integral_constant<int, 0>;
+  using B1 = std::integral_constant<int, 1>;
+  using UNM = std::integral_constant<bool, false>;
+  using MSK = std::integral_constant<bool, true>;
+  const int nfull = 2 * qb;  // even
+  for (int kb = 0; kb < nfull; kb += 2) {
+    step(B0{}, UNM{}, kb);
+    step(B1{}, UNM{}, kb + 1);
   }
+  if (nfull < nkv) step(B0{}, MSK{}, nfull);
+  if (nfull + 1 < nkv) step(B1{}, MSK{}, nfull + 1);
 
   const float l_tot = xhalf_sum(fs.l);
   const float inv_l = (DROP ? dscale : 1.f) / l_tot;
@@ -467,6 +477,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dkdv(const bf16_t* __restri
     kf[s] = load_row8(k + hoff + (size_t)kc * HD + 16 * s + 8 * h, ka < S);
     vf[s] = load_row8(v + hoff + (size_t)kc * HD + 16 * s + 8 * h, ka < S);
   }
+
   floatx16_t dka[2] = {zero16(), zero16()}, dva[2] = {zero16(), zero16()};
 
   const int qt_begin = (kblk * KB) / QSTEP;
@@ -497,7 +508,11 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dkdv(const bf16_t* __restri
   }
   __syncthreads();
 
-  for (int t = qt_begin; t < nqt; ++t) {
+  // Tiles qt_begin, qt_begin+1 hold every diagonal sub-tile of the block (masked
+  // kind, fully-masked sub-tiles skipped); later full tiles are straight-line
+  // unmasked; a ragged last tile (S % 64) is masked again.
+  auto step = [&](auto maskc, int t) {
+    constexpr bool MASKED = decltype(maskc)::value;
     const int cur = (t - qt_begin) & 1;
     const bool more = t + 1 < nqt;
     uint32_t mw0 = 0, mw1 = 0;
@@ -517,17 +532,23 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dkdv(const bf16_t* __restri
       const bf16_t* Qs = Qt + 32 * qt * HD;
       const bf16_t* Ds = Dt + 32 * qt * HD;
       const uint32_t mw = (qt ? mw1 : mw0) >> (4 * h);
-      if (qs >= k0 + 31 && qs + 32 <= S && k0 + 32 <= S) {
+      if (!MASKED)
         dkdv_subtile<false, DROP>(dka, dva, Qs, Ds, rlp + 32 * qt, rdp + 32 * qt, mw, kf, vf, qs, ka, S, lane,
                                   c_log2, dscale);
-      } else if (qs + 31 >= k0) {
+      else if (qs + 31 >= k0)
         dkdv_subtile<true, DROP>(dka, dva, Qs, Ds, rlp + 32 * qt, rdp + 32 * qt, mw, kf, vf, qs, ka, S, lane,
                                  c_log2, dscale);
-      }
     }
     if (more) store_rows(cur ^ 1);
     __syncthreads();
-  }
+  };
+  using UNM = std::integral_constant<bool, false>;
+  using MSK = std::integral_constant<bool, true>;
+  int t = qt_begin;
+  const int t_diag = min(nqt, qt_begin + 2), t_full = S / QSTEP;
+  for (; t < t_diag; ++t) step(MSK{}, t);
+  for (; t < t_full; ++t) step(UNM{}, t);
+  for (; t < nqt; ++t) step(MSK{}, t);
 
   if (ka < S) {
     bf16_t* dkr = dk + hoff + (size_t)ka * HD;
@@ -621,6 +642,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dq(const bf16_t* __restrict
     qf[s] = load_row8(q + hoff + (size_t)qc * HD + 16 * s + 8 * h, qok);
     df[s] = load_row8(dorow + 16 * s + 8 * h, qok);
   }
+
   const float nl2 = qok ? -lse[(size_t)bh * S + qc] * LOG2E : 0.f;
   const float dl = qok ? delta[(size_t)bh * S + qc] : 0.f;
   floatx16_t dqa[2] = {zero16(), zero16()};
@@ -634,27 +656,41 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dq(const bf16_t* __restrict
   stage_store(sv, lds + KVB * HD, tid);
   __syncthreads();
 
-  for (int kb = 0; kb < nkv; ++kb) {
-    const int cur = kb & 1;
+  // Same loop structure as the forward: straight-line unmasked tiles (static LDS
+  // buffers, unrolled by two), then the one or two diagonal tiles.
+  auto step = [&](auto bufc, auto maskc, int kb) {
+    constexpr int BUF = decltype(bufc)::value;
+    constexpr bool MASKED = decltype(maskc)::value;
     const bool more = kb + 1 < nkv;
     if (more) {
       stage_load(sk, k + hoff, (kb + 1) * KVB, S, HD, tid);
       stage_load(sv, v + hoff, (kb + 1) * KVB, S, HD, tid);
     }
-    const bf16_t* Kt = lds + cur * 2 * KVB * HD;
+    const bf16_t* Kt = lds + BUF * 2 * KVB * HD;
     const bf16_t* Vt = Kt + KVB * HD;
     const int k0 = kb * KVB;
-    if (k0 + KVB - 1 <= q0 && k0 + KVB <= S)
+    if (!MASKED)
       dq_tile<false, DROP>(dqa, Kt, Vt, qf, df, k0, qa, S, lane, c_log2, nl2, dl, dscale, mrow);
     else if (k0 <= q0 + 31)
       dq_tile<true, DROP>(dqa, Kt, Vt, qf, df, k0, qa, S, lane, c_log2, nl2, dl, dscale, mrow);
     if (more) {
-      bf16_t* Kn = lds + (cur ^ 1) * 2 * KVB * HD;
+      bf16_t* Kn = lds + (BUF ^ 1) * 2 * KVB * HD;
       stage_store(sk, Kn, tid);
       stage_store(sv, Kn + KVB * HD, tid);
     }
     __syncthreads();
+  };
+  using B0 = std::integral_constant<int, 0>;
+  using B1 = std::integral_constant<int, 1>;
+  using UNM = std::integral_constant<bool, false>;
+  using MSK = std::integral_constant<bool, true>;
+  const int nfull = 2 * qb;
+  for (int kb = 0; kb < nfull; kb += 2) {
+    step(B0{}, UNM{}, kb);
+    step(B1{}, UNM{}, kb + 1);
   }
+  if (nfull < nkv) step(B0{}, MSK{}, nfull);
+  if (nfull + 1 < nkv) step(B1{}, MSK{}, nfull + 1);
   if (qok) {
     bf16_t* dqr = dq + hoff + (size_t)qa * HD;
 #pragma unroll
