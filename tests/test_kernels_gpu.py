@@ -240,3 +240,24 @@ def test_wgrad_gemm_kernel(M, N, K):
         ref = dw + dy.float().t() @ x.float()
         assert hip.wgrad_gemm(dw, dy, x, splits)
         _close(dw, ref, 1e-3 * M ** 0.5, 1e-4, f"wgrad splits={splits}")
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attention_fwd_growing_max_rescales(p):
+    """Scores rise steeply along the keys, so the running row max grows by far more
+    than the 2^8 rescale threshold in many tiles: exercises the deferred-rescale path
+    (random data almost never takes it)."""
+    B, nh, S = 1, 2, 512
+    q = torch.zeros(B, nh, S, 64, device=DEV)
+    k = torch.zeros(B, nh, S, 64, device=DEV)
+    q[..., 0] = 8.0
+    k[..., 0] = torch.arange(S, device=DEV, dtype=torch.float32) * 0.05  # score slope 0.05 per key
+    k[..., 1] = torch.randn(S, device=DEV)
+    q[..., 1] = torch.randn(S, device=DEV)
+    v = torch.randn(B, nh, S, 64, device=DEV)
+    q, k, v = q.bfloat16(), k.bfloat16(), v.bfloat16()
+    key = rng.site_key(7, 8, 9, rng.SITE_ATTN)
+    o, aux = hip.attention_fwd(q, k, v, p, key)
+    o2, lse2 = ref.attention_fwd(q, k, v, p, key)
+    _close(aux[0], lse2, 2e-3, 1e-3, "lse(growing)")
+    _close(o, o2.float(), 2e-2, 2e-2, "o(growing)")
