@@ -93,31 +93,24 @@ __device__ __forceinline__ floatx16_t zero16() {
   return z;
 }
 
-// Register-staged tile copy: 64 rows x 64 cols bf16, rows beyond S zero-filled;
-// 2 x 16 B per thread of a 256-thread block.  `rstride` = row stride in elements.
-struct Stage2 { u16x8 c[2]; };
+// Register-staged tile copy: 64 rows x 64 cols bf16; 2 x 16 B per thread of a
+// 256-thread block.  Rows beyond S are CLAMPED to row S-1, not zero-filled: a
+// zero-fill select right after the load would force an immediate vmcnt wait and
+// serialise the prefetch with the tile compute.  Every tile that can reach past S
+// runs the masked tile kind, which zeroes those rows' probabilities, and the clamped
+// data is finite, so it never contributes.  `rstride` = row stride in elements.
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+struct Stage2 { u32x4_t c0, c1; };  // vector members: stays in VGPRs (no scratch alloca)
 __device__ __forceinline__ void stage_load(Stage2& st, const bf16_t* __restrict__ base, int row0, int S,
                                            int rstride, int tid) {
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int c = tid + 256 * u;
-    const int r = c >> 3, ch = c & 7;
-    const int row = min(row0 + r, S - 1);
-    u16x8 v = *reinterpret_cast<const u16x8*>(base + (size_t)row * rstride + ch * 8);
-    if (row0 + r >= S) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v.v[e] = 0;
-    }
-    st.c[u] = v;
-  }
+  const int r = tid >> 3, ch = tid & 7;  // chunk u = tid + 256u -> row r + 32u
+  st.c0 = *reinterpret_cast<const u32x4_t*>(base + (size_t)min(row0 + r, S - 1) * rstride + ch * 8);
+  st.c1 = *reinterpret_cast<const u32x4_t*>(base + (size_t)min(row0 + r + 32, S - 1) * rstride + ch * 8);
 }
 __device__ __forceinline__ void stage_store(const Stage2& st, bf16_t* T, int tid) {
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int c = tid + 256 * u;
-    const int r = c >> 3, ch = c & 7;
-    *reinterpret_cast<u16x8*>(T + swz_off(r, ch * 8)) = st.c[u];
-  }
+  const int r = tid >> 3, ch = tid & 7;
+  *reinterpret_cast<u32x4_t*>(T + swz_off(r, ch * 8)) = st.c0;
+  *reinterpret_cast<u32x4_t*>(T + swz_off(r + 32, ch * 8)) = st.c1;
 }
 
 __device__ __forceinline__ bf16x8_t load_row8(const bf16_t* __restrict__ p, bool ok) {
@@ -134,8 +127,8 @@ __device__ __forceinline__ bf16x8_t load_row8(const bf16_t* __restrict__ p, bool
 //   mask [bh][q][w]  bit j = keep(q, key = 32w + j)   -- lane = query (fwd, dQ)
 //   maskT[bh][k][w]  bit j = keep(q = 32w + j, key k) -- lane = key   (dK/dV)
 // Only causal 32x32 tiles (key word <= query band) exist.  One half-wave per tile:
-// lane l hashes row q = 32r + l (16 hashes -> its row word), then 32 wave ballots
-// transpose the tile's bits so lane j holds the column word of key 32w + j.
+// lane l hashes row q = 32r + l (16 hashes -> its row word), then a 5-stage butterfly
+// bit transpose gives lane j the column word of key 32w + j.
 // Pure VALU at full occupancy (~3-4 us per layer at B8 nh12 S1024), so the MFMA
 // kernels only test bits instead of hashing at 2 waves/SIMD.
 __global__ __launch_bounds__(256) void k_dropout_bits(uint32_t* __restrict__ mask, uint32_t* __restrict__ maskT,
@@ -175,13 +168,15 @@ __global__ __launch_bounds__(256) void k_dropout_bits(uint32_t* __restrict__ mas
     }
     mask[((size_t)bh * S + q) * W + w] = word;
   }
-  // transpose within each half-wave: bit (row l, key j) -> column word j, bit l
-  uint32_t col = 0;
+  // 32x32 bit transpose within each half-wave (lane l holds row l; afterwards lane j
+  // holds column j): 5 butterfly stages, each one lane^d exchange + 4 bit ops.
+  uint32_t col = word;
 #pragma unroll
-  for (int j = 0; j < 32; ++j) {
-    const uint64_t bal = __ballot((word >> j) & 1u);
-    const uint32_t mine = half ? (uint32_t)(bal >> 32) : (uint32_t)bal;
-    col = (l == j) ? mine : col;
+  for (int d = 16; d >= 1; d >>= 1) {
+    const uint32_t m = d == 16 ? 0x0000FFFFu : d == 8 ? 0x00FF00FFu : d == 4 ? 0x0F0F0F0Fu : d == 2 ? 0x33333333u
+                                                                                                   : 0x55555555u;
+    const uint32_t y = (uint32_t)__shfl_xor((int)col, d, 64);
+    col = (l & d) ? ((col & ~m) | ((y >> d) & m)) : ((col & m) | ((y & m) << d));
   }
   const int kk = w * 32 + l;
   if (active && kk < S) maskT[((size_t)bh * S + kk) * W + r] = col;
@@ -213,16 +208,14 @@ struct FwdState {
 
 template <bool MASK, bool DROP>
 __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const bf16_t* Vt, const bf16x8_t (&qf)[4],
-                                         int k0, int qa, int S, int lane, float c_log2,
-                                         const uint32_t* __restrict__ mrow) {
+                                         int k0, int qa, int S, int lane, float c_log2, uint2 mw) {
   // Two 32-key halves, each a complete online-softmax step; the V^T tr-reads of a
   // half are issued before its softmax VALU so their latency hides under it.
   const int h = lane >> 5, ql = lane & 31;
-  uint32_t words[2] = {0u, 0u};
-  if (DROP) {  // this lane-half's 16 keep bits per half-tile sit at (i&3) + 8(i>>2)
-    words[0] = mrow[k0 >> 5] >> (4 * h);
-    words[1] = mrow[(k0 >> 5) + 1] >> (4 * h);
-  }
+  // keep-bit words of this tile (prefetched with the previous tile's staging loads,
+  // so no vmcnt wait lands inside the tile); this lane-half's 16 bits per half-tile
+  // sit at (i&3) + 8(i>>2)
+  const uint32_t words[2] = {mw.x >> (4 * h), mw.y >> (4 * h)};
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     bf16x8_t kf[4];
@@ -315,6 +308,8 @@ __global__ __launch_bounds__(256, 3) void k_attn_fwd(const bf16_t* __restrict__ 
   // compile-time tile kind: tiles kb < 2*qb lie entirely below every query of the
   // block (one straight-line unmasked loop, unrolled by two so every LDS address is
   // lane-base + immediate); only the last one or two tiles hold the diagonal.
+  uint2 mw_cur = make_uint2(0u, 0u), mw_next = make_uint2(0u, 0u);
+  if (DROP) mw_cur = make_uint2(mrow[0], W > 1 ? mrow[1] : 0u);  // words of tile 0
   auto step = [&](auto bufc, auto maskc, int kb) {
     constexpr int BUF = decltype(bufc)::value;
     constexpr bool MASKED = decltype(maskc)::value;
@@ -322,14 +317,16 @@ __global__ __launch_bounds__(256, 3) void k_attn_fwd(const bf16_t* __restrict__ 
     if (more) {
       stage_load(sk, k + hoff, (kb + 1) * KVB, S, HD, tid);
       stage_load(sv, v + hoff, (kb + 1) * KVB, S, HD, tid);
+      if (DROP) mw_next = make_uint2(mrow[2 * (kb + 1)], 2 * (kb + 1) + 1 < W ? mrow[2 * (kb + 1) + 1] : 0u);
     }
     const bf16_t* Kt = lds + BUF * 2 * KVB * HD;
     const bf16_t* Vt = Kt + KVB * HD;
     const int k0 = kb * KVB;
     if (!MASKED)
-      fwd_tile<false, DROP>(fs, Kt, Vt, qf, k0, qa, S, lane, c_log2, mrow);
+      fwd_tile<false, DROP>(fs, Kt, Vt, qf, k0, qa, S, lane, c_log2, mw_cur);
     else if (k0 <= q0 + 31)
-      fwd_tile<true, DROP>(fs, Kt, Vt, qf, k0, qa, S, lane, c_log2, mrow);
+      fwd_tile<true, DROP>(fs, Kt, Vt, qf, k0, qa, S, lane, c_log2, mw_cur);
+    mw_cur = mw_next;
     if (more) {
       bf16_t* Kn = lds + (BUF ^ 1) * 2 * KVB * HD;
       stage_store(sk, Kn, tid);
@@ -484,9 +481,14 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dkdv(const bf16_t* __restri
   const int nqt = (S + QSTEP - 1) / QSTEP;
   Stage2 sq, sd;
   float rl = 0.f, rd = 0.f;
+  uint2 mw_cur = make_uint2(0u, 0u), mw_next = make_uint2(0u, 0u);
   auto load_rows = [&](int t) {
     stage_load(sq, q + hoff, t * QSTEP, S, HD, tid);
     stage_load(sd, dob, t * QSTEP, S, rstride, tid);
+    if (DROP) {  // this lane's two 32-query keep words of tile t (consumed one tile later)
+      const int w0 = (t * QSTEP) >> 5;
+      mw_next = make_uint2(mcol[w0], (w0 + 1 < W) ? mcol[w0 + 1] : 0u);
+    }
     if (tid < QSTEP) {
       const int qq = min(t * QSTEP + tid, S - 1);
       const bool ok = t * QSTEP + tid < S;
@@ -505,6 +507,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dkdv(const bf16_t* __restri
   if (qt_begin < nqt) {
     load_rows(qt_begin);
     store_rows(0);
+    mw_cur = mw_next;
   }
   __syncthreads();
 
@@ -515,12 +518,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dkdv(const bf16_t* __restri
     constexpr bool MASKED = decltype(maskc)::value;
     const int cur = (t - qt_begin) & 1;
     const bool more = t + 1 < nqt;
-    uint32_t mw0 = 0, mw1 = 0;
-    if (DROP) {  // the two 32-query words of this tile (issued before the staging loads)
-      const int w0 = (t * QSTEP) >> 5;
-      mw0 = mcol[w0];
-      mw1 = (w0 + 1 < W) ? mcol[w0 + 1] : 0u;
-    }
+    const uint32_t mw0 = mw_cur.x, mw1 = mw_cur.y;
     if (more) load_rows(t + 1);
     const bf16_t* Qt = lds + cur * 2 * QSTEP * HD;
     const bf16_t* Dt = Qt + QSTEP * HD;
@@ -540,6 +538,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dkdv(const bf16_t* __restri
                                  c_log2, dscale);
     }
     if (more) store_rows(cur ^ 1);
+    mw_cur = mw_next;
     __syncthreads();
   };
   using UNM = std::integral_constant<bool, false>;
@@ -573,8 +572,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dkdv(const bf16_t* __restri
 template <bool MASK, bool DROP>
 __device__ __forceinline__ void dq_tile(floatx16_t (&dqa)[2], const bf16_t* Kt, const bf16_t* Vt,
                                         const bf16x8_t (&qf)[4], const bf16x8_t (&df)[4], int k0, int qa, int S,
-                                        int lane, float c_log2, float nl2, float dl, float dscale,
-                                        const uint32_t* __restrict__ mrow) {
+                                        int lane, float c_log2, float nl2, float dl, float dscale, uint2 mw) {
   const int h = lane >> 5, ql = lane & 31;
   floatx16_t sacc[2], pacc[2];
 #pragma unroll
@@ -589,8 +587,7 @@ __device__ __forceinline__ void dq_tile(floatx16_t (&dqa)[2], const bf16_t* Kt, 
   }
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    uint32_t word = 0;
-    if (DROP) word = mrow[(k0 + 32 * t) >> 5] >> (4 * h);
+    const uint32_t word = DROP ? ((t ? mw.y : mw.x) >> (4 * h)) : 0u;  // prefetched a tile ahead
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int kr = acc_row(i, h);
@@ -658,6 +655,8 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dq(const bf16_t* __restrict
 
   // Same loop structure as the forward: straight-line unmasked tiles (static LDS
   // buffers, unrolled by two), then the one or two diagonal tiles.
+  uint2 mw_cur = make_uint2(0u, 0u), mw_next = make_uint2(0u, 0u);
+  if (DROP) mw_cur = make_uint2(mrow[0], W > 1 ? mrow[1] : 0u);
   auto step = [&](auto bufc, auto maskc, int kb) {
     constexpr int BUF = decltype(bufc)::value;
     constexpr bool MASKED = decltype(maskc)::value;
@@ -665,14 +664,16 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dq(const bf16_t* __restrict
     if (more) {
       stage_load(sk, k + hoff, (kb + 1) * KVB, S, HD, tid);
       stage_load(sv, v + hoff, (kb + 1) * KVB, S, HD, tid);
+      if (DROP) mw_next = make_uint2(mrow[2 * (kb + 1)], 2 * (kb + 1) + 1 < W ? mrow[2 * (kb + 1) + 1] : 0u);
     }
     const bf16_t* Kt = lds + BUF * 2 * KVB * HD;
     const bf16_t* Vt = Kt + KVB * HD;
     const int k0 = kb * KVB;
     if (!MASKED)
-      dq_tile<false, DROP>(dqa, Kt, Vt, qf, df, k0, qa, S, lane, c_log2, nl2, dl, dscale, mrow);
+      dq_tile<false, DROP>(dqa, Kt, Vt, qf, df, k0, qa, S, lane, c_log2, nl2, dl, dscale, mw_cur);
     else if (k0 <= q0 + 31)
-      dq_tile<true, DROP>(dqa, Kt, Vt, qf, df, k0, qa, S, lane, c_log2, nl2, dl, dscale, mrow);
+      dq_tile<true, DROP>(dqa, Kt, Vt, qf, df, k0, qa, S, lane, c_log2, nl2, dl, dscale, mw_cur);
+    mw_cur = mw_next;
     if (more) {
       bf16_t* Kn = lds + (BUF ^ 1) * 2 * KVB * HD;
       stage_store(sk, Kn, tid);
