@@ -35,9 +35,9 @@
 
 #define HD 64
 #define KVB 64     // keys per staged tile (fwd / dQ)
-#define QB 128     // queries per workgroup (fwd / dQ), 32 per wave
-#define KB 128     // keys per workgroup (dK/dV), 32 per wave
+#define RB 64      // rows (queries for fwd / dQ, keys for dK/dV) per work item: 2 waves x 32
 #define QSTEP 64   // queries per staged tile (dK/dV)
+#define NT 128     // threads per workgroup
 #define LOG2E 1.44269504088896340736f
 
 typedef __attribute__((address_space(3))) shortx4_t lds_shortx4_t;
@@ -93,24 +93,50 @@ __device__ __forceinline__ floatx16_t zero16() {
   return z;
 }
 
-// Register-staged tile copy: 64 rows x 64 cols bf16; 2 x 16 B per thread of a
-// 256-thread block.  Rows beyond S are CLAMPED to row S-1, not zero-filled: a
+// Register-staged tile copy: 64 rows x 64 cols bf16; 4 x 16 B per thread of a
+// 128-thread block.  Rows beyond S are CLAMPED to row S-1, not zero-filled: a
 // zero-fill select right after the load would force an immediate vmcnt wait and
 // serialise the prefetch with the tile compute.  Every tile that can reach past S
 // runs the masked tile kind, which zeroes those rows' probabilities, and the clamped
 // data is finite, so it never contributes.  `rstride` = row stride in elements.
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-struct Stage2 { u32x4_t c0, c1; };  // vector members: stays in VGPRs (no scratch alloca)
-__device__ __forceinline__ void stage_load(Stage2& st, const bf16_t* __restrict__ base, int row0, int S,
+struct Stage4 { u32x4_t c0, c1, c2, c3; };  // vector members: stays in VGPRs (no scratch alloca)
+// 128 threads: thread t moves 16-B chunk (t & 7) of rows (t >> 3) + {0, 16, 32, 48}.
+__device__ __forceinline__ void stage_load(Stage4& st, const bf16_t* __restrict__ base, int row0, int S,
                                            int rstride, int tid) {
-  const int r = tid >> 3, ch = tid & 7;  // chunk u = tid + 256u -> row r + 32u
-  st.c0 = *reinterpret_cast<const u32x4_t*>(base + (size_t)min(row0 + r, S - 1) * rstride + ch * 8);
-  st.c1 = *reinterpret_cast<const u32x4_t*>(base + (size_t)min(row0 + r + 32, S - 1) * rstride + ch * 8);
+  const int r = tid >> 3, ch = tid & 7;
+  const bf16_t* p = base + ch * 8;
+  st.c0 = *reinterpret_cast<const u32x4_t*>(p + (size_t)min(row0 + r, S - 1) * rstride);
+  st.c1 = *reinterpret_cast<const u32x4_t*>(p + (size_t)min(row0 + r + 16, S - 1) * rstride);
+  st.c2 = *reinterpret_cast<const u32x4_t*>(p + (size_t)min(row0 + r + 32, S - 1) * rstride);
+  st.c3 = *reinterpret_cast<const u32x4_t*>(p + (size_t)min(row0 + r + 48, S - 1) * rstride);
 }
-__device__ __forceinline__ void stage_store(const Stage2& st, bf16_t* T, int tid) {
+__device__ __forceinline__ void stage_store(const Stage4& st, bf16_t* T, int tid) {
   const int r = tid >> 3, ch = tid & 7;
   *reinterpret_cast<u32x4_t*>(T + swz_off(r, ch * 8)) = st.c0;
-  *reinterpret_cast<u32x4_t*>(T + swz_off(r + 32, ch * 8)) = st.c1;
+  *reinterpret_cast<u32x4_t*>(T + swz_off(r + 16, ch * 8)) = st.c1;
+  *reinterpret_cast<u32x4_t*>(T + swz_off(r + 32, ch * 8)) = st.c2;
+  *reinterpret_cast<u32x4_t*>(T + swz_off(r + 48, ch * 8)) = st.c3;
+}
+
+// Direct global->LDS tile copy (global_load_lds_dwordx4, no staging registers): one
+// wave-instruction writes 1 KiB = 8 rows contiguously (lane l -> row l/8, 16-B slot
+// l%8), so the XOR swizzle is applied on the SOURCE address: slot s of row r holds
+// global chunk s ^ ((r >> 1) & 7), exactly the image swz_off() reads.  64 rows =
+// 8 instructions, 4 per wave of the 2-wave workgroup.  Completion is tracked by
+// vmcnt; the __syncthreads() that ends every tile step waits for it.
+typedef __attribute__((address_space(3))) void* lds_vptr_t;
+typedef const __attribute__((address_space(1))) void* gbl_cvptr_t;
+__device__ __forceinline__ void glds_tile(const bf16_t* __restrict__ base, int row0, int S, int rstride, bf16_t* T,
+                                          int wid, int lane) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int rr = (wid * 4 + j) * 8;  // first row of this 1 KiB piece (wave-uniform)
+    const int row = rr + (lane >> 3);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    const bf16_t* g = base + (size_t)min(row0 + row, S - 1) * rstride + c * 8;
+    __builtin_amdgcn_global_load_lds((gbl_cvptr_t)g, (lds_vptr_t)(T + rr * HD), 16, 0, 0);
+  }
 }
 
 __device__ __forceinline__ bf16x8_t load_row8(const bf16_t* __restrict__ p, bool ok) {
@@ -266,100 +292,107 @@ __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const b
   }
 }
 
+// Work decomposition (causal balance): a workgroup = 2 waves = one 64-query item,
+// and each workgroup processes the PAIR of items (nrb-1-p, p) one after the other,
+// so every workgroup does the same amount of work ((nrb+1) key tiles).  With one
+// item per workgroup the per-CU load would follow the round-robin dispatch, which
+// stacks items of equal length on a CU (measured 1.8x slower than balanced).
 template <bool DROP>
-__global__ __launch_bounds__(256, 3) void k_attn_fwd(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
-                                                     const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
-                                                     float* __restrict__ lse, const uint32_t* __restrict__ mask,
-                                                     int S, int nh, float c_log2, float dscale) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_attn_fwd(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
+                                                    const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
+                                                    float* __restrict__ lse, const uint32_t* __restrict__ mask,
+                                                    int S, int nh, float c_log2, float dscale) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * 2 * KVB * HD];  // [buf][K|V][64][64]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, ql = lane & 31;
-  const int nqb = (S + QB - 1) / QB;
-  const int qb = nqb - 1 - blockIdx.x;  // heaviest (last) query blocks first
+  const int nrb = (S + RB - 1) / RB;
   const int bh = blockIdx.y;
   const int b = bh / nh, head = bh % nh;
   const size_t hoff = (size_t)bh * S * HD;
-  const int q0 = qb * QB + wid * 32;  // this wave's first query (wave-uniform)
-  const int qa = q0 + ql;
   const int W = (S + 31) >> 5;
-  const uint32_t* mrow = mask ? mask + ((size_t)bh * S + min(qa, S - 1)) * W : nullptr;
-
-  bf16x8_t qf[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) qf[s] = load_row8(q + hoff + (size_t)min(qa, S - 1) * HD + 16 * s + 8 * h, qa < S);
-
-  FwdState fs;
-  fs.o[0] = zero16();
-  fs.o[1] = zero16();
-  fs.m = -INFINITY;
-  fs.l = 0.f;
-
-  const int kv_end = min(S, qb * QB + QB);
-  const int nkv = (kv_end + KVB - 1) / KVB;
-  Stage2 sk, sv;
-  stage_load(sk, k + hoff, 0, S, HD, tid);
-  stage_load(sv, v + hoff, 0, S, HD, tid);
-  stage_store(sk, lds, tid);
-  stage_store(sv, lds + KVB * HD, tid);
-  __syncthreads();
-
-  // One K/V tile per step.  BUF is a compile-time LDS buffer index and MASKED a
-  // compile-time tile kind: tiles kb < 2*qb lie entirely below every query of the
-  // block (one straight-line unmasked loop, unrolled by two so every LDS address is
-  // lane-base + immediate); only the last one or two tiles hold the diagonal.
-  uint2 mw_cur = make_uint2(0u, 0u), mw_next = make_uint2(0u, 0u);
-  if (DROP) mw_cur = make_uint2(mrow[0], W > 1 ? mrow[1] : 0u);  // words of tile 0
-  auto step = [&](auto bufc, auto maskc, int kb) {
-    constexpr int BUF = decltype(bufc)::value;
-    constexpr bool MASKED = decltype(maskc)::value;
-    const bool more = kb + 1 < nkv;
-    if (more) {
-      stage_load(sk, k + hoff, (kb + 1) * KVB, S, HD, tid);
-      stage_load(sv, v + hoff, (kb + 1) * KVB, S, HD, tid);
-      if (DROP) mw_next = make_uint2(mrow[2 * (kb + 1)], 2 * (kb + 1) + 1 < W ? mrow[2 * (kb + 1) + 1] : 0u);
-    }
-    const bf16_t* Kt = lds + BUF * 2 * KVB * HD;
-    const bf16_t* Vt = Kt + KVB * HD;
-    const int k0 = kb * KVB;
-    if (!MASKED)
-      fwd_tile<false, DROP>(fs, Kt, Vt, qf, k0, qa, S, lane, c_log2, mw_cur);
-    else if (k0 <= q0 + 31)
-      fwd_tile<true, DROP>(fs, Kt, Vt, qf, k0, qa, S, lane, c_log2, mw_cur);
-    mw_cur = mw_next;
-    if (more) {
-      bf16_t* Kn = lds + (BUF ^ 1) * 2 * KVB * HD;
-      stage_store(sk, Kn, tid);
-      stage_store(sv, Kn + KVB * HD, tid);
-    }
-    __syncthreads();
-  };
   using B0 = std::integral_constant<int, 0>;
   using B1 = std::integral_constant<int, 1>;
   using UNM = std::integral_constant<bool, false>;
   using MSK = std::integral_constant<bool, true>;
-  const int nfull = 2 * qb;  // even
-  for (int kb = 0; kb < nfull; kb += 2) {
-    step(B0{}, UNM{}, kb);
-    step(B1{}, UNM{}, kb + 1);
-  }
-  if (nfull < nkv) step(B0{}, MSK{}, nfull);
-  if (nfull + 1 < nkv) step(B1{}, MSK{}, nfull + 1);
 
-  const float l_tot = xhalf_sum(fs.l);
-  const float inv_l = (DROP ? dscale : 1.f) / l_tot;
-  if (qa < S) {
-    if (h == 0) lse[(size_t)bh * S + qa] = fs.m * (c_log2 / LOG2E) + __logf(l_tot);
-    bf16_t* orow = o + (((size_t)b * S + qa) * nh + head) * HD;
+#pragma unroll 1
+  for (int it = 0; it < 2; ++it) {
+    const int qb = it == 0 ? nrb - 1 - (int)blockIdx.x : (int)blockIdx.x;  // long item first
+    if (it == 1 && qb >= nrb - 1 - (int)blockIdx.x) break;                 // odd nrb: middle item once
+    const int q0 = qb * RB + wid * 32;  // this wave's first query (wave-uniform)
+    const int qa = q0 + ql;
+    const uint32_t* mrow = mask ? mask + ((size_t)bh * S + min(qa, S - 1)) * W : nullptr;
+
+    bf16x8_t qf[4];
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        u16x4 w;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) w.v[e] = f2bf(fs.o[dt][4 * g + e] * inv_l);
-        *reinterpret_cast<u16x4*>(orow + 32 * dt + 8 * g + 4 * h) = w;
+    for (int s = 0; s < 4; ++s) qf[s] = load_row8(q + hoff + (size_t)min(qa, S - 1) * HD + 16 * s + 8 * h, qa < S);
+
+    FwdState fs;
+    fs.o[0] = zero16();
+    fs.o[1] = zero16();
+    fs.m = -INFINITY;
+    fs.l = 0.f;
+
+    const int nkv = (min(S, qb * RB + RB) + KVB - 1) / KVB;  // = qb + 1 except at a ragged end
+    glds_tile(k + hoff, 0, S, HD, lds, wid, lane);
+    glds_tile(v + hoff, 0, S, HD, lds + KVB * HD, wid, lane);
+    __syncthreads();
+
+    // One K/V tile per step.  BUF is a compile-time LDS buffer index and MASKED a
+    // compile-time tile kind: tiles kb < qb lie entirely below every query of the
+    // item (straight-line unmasked loop, unrolled by two so every LDS address is
+    // lane-base + immediate); tile qb holds the diagonal.
+    uint2 mw_cur = make_uint2(0u, 0u), mw_next = make_uint2(0u, 0u);
+    if (DROP) mw_cur = make_uint2(mrow[0], W > 1 ? mrow[1] : 0u);  // words of tile 0
+    auto step = [&](auto bufc, auto maskc, int kb) {
+      constexpr int BUF = decltype(bufc)::value;
+      constexpr bool MASKED = decltype(maskc)::value;
+      const bool more = kb + 1 < nkv;
+      if (more) {  // next tile straight into the other buffer (read by nobody since the last barrier)
+        bf16_t* Kn = lds + (BUF ^ 1) * 2 * KVB * HD;
+        glds_tile(k + hoff, (kb + 1) * KVB, S, HD, Kn, wid, lane);
+        glds_tile(v + hoff, (kb + 1) * KVB, S, HD, Kn + KVB * HD, wid, lane);
+        if (DROP) mw_next = make_uint2(mrow[2 * (kb + 1)], 2 * (kb + 1) + 1 < W ? mrow[2 * (kb + 1) + 1] : 0u);
       }
+      const bf16_t* Kt = lds + BUF * 2 * KVB * HD;
+      const bf16_t* Vt = Kt + KVB * HD;
+      const int k0 = kb * KVB;
+      if (!MASKED)
+        fwd_tile<false, DROP>(fs, Kt, Vt, qf, k0, qa, S, lane, c_log2, mw_cur);
+      else if (k0 <= q0 + 31)
+        fwd_tile<true, DROP>(fs, Kt, Vt, qf, k0, qa, S, lane, c_log2, mw_cur);
+      mw_cur = mw_next;
+      __syncthreads();
+    };
+    const int nfull = min(qb, nkv);
+    int kb = 0;
+    for (; kb + 1 < nfull; kb += 2) {
+      step(B0{}, UNM{}, kb);
+      step(B1{}, UNM{}, kb + 1);
+    }
+    if (kb < nfull) {  // odd count: last unmasked tile in buffer 0, diagonal in buffer 1
+      step(B0{}, UNM{}, kb);
+      if (kb + 1 < nkv) step(B1{}, MSK{}, kb + 1);
+    } else if (kb < nkv) {
+      step(B0{}, MSK{}, kb);
+    }
+
+    const float l_tot = xhalf_sum(fs.l);
+    const float inv_l = (DROP ? dscale : 1.f) / l_tot;
+    if (qa < S) {
+      if (h == 0) lse[(size_t)bh * S + qa] = fs.m * (c_log2 / LOG2E) + __logf(l_tot);
+      bf16_t* orow = o + (((size_t)b * S + qa) * nh + head) * HD;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          u16x4 w;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w.v[e] = f2bf(fs.o[dt][4 * g + e] * inv_l);
+          *reinterpret_cast<u16x4*>(orow + 32 * dt + 8 * g + 4 * h) = w;
+        }
+    }
   }
 }
 
@@ -439,15 +472,17 @@ __device__ __forceinline__ void dkdv_subtile(floatx16_t (&dka)[2], floatx16_t (&
   }
 }
 
+// Work items: 64 keys (2 waves x 32); a workgroup processes the pair of key blocks
+// (p, nrb-1-p) -- equal work per workgroup (see the forward).
 template <bool DROP>
-__global__ __launch_bounds__(256, 2) void k_attn_bwd_dkdv(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
-                                                          const bf16_t* __restrict__ v,
-                                                          const bf16_t* __restrict__ dout,
-                                                          const float* __restrict__ lse,
-                                                          const float* __restrict__ delta,
-                                                          const uint32_t* __restrict__ maskT, bf16_t* __restrict__ dk,
-                                                          bf16_t* __restrict__ dv, int S, int nh, float c_log2,
-                                                          float scale, float dscale) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_attn_bwd_dkdv(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
+                                                         const bf16_t* __restrict__ v,
+                                                         const bf16_t* __restrict__ dout,
+                                                         const float* __restrict__ lse,
+                                                         const float* __restrict__ delta,
+                                                         const uint32_t* __restrict__ maskT, bf16_t* __restrict__ dk,
+                                                         bf16_t* __restrict__ dv, int S, int nh, float c_log2,
+                                                         float scale, float dscale) {
   // one LDS object (avoids hipcc's extra vmcnt waits with several __shared__ arrays)
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * QSTEP * HD * 2 + 2 * 2 * QSTEP * 4];
   bf16_t* lds = reinterpret_cast<bf16_t*>(smem);                              // [buf][Q|dO][64][64]
@@ -455,116 +490,116 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_dkdv(const bf16_t* __restri
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, kl = lane & 31;
-  const int kblk = blockIdx.x;  // early key blocks are the heaviest and launch first
+  const int nrb = (S + RB - 1) / RB;
   const int bh = blockIdx.y;
   const int b = bh / nh, head = bh % nh;
   const size_t hoff = (size_t)bh * S * HD;
-  const int k0 = kblk * KB + wid * 32;  // wave-uniform
-  const int ka = k0 + kl;
   const int rstride = nh * HD;
   const int W = (S + 31) >> 5;
-  const bf16_t* dob = dout + ((size_t)b * S * nh + head) * HD;
-  // this lane's key column of the transposed keep-bit mask: one word per 32 queries
-  const uint32_t* mcol = DROP ? maskT + ((size_t)bh * S + min(ka, S - 1)) * W : nullptr;
-
-  bf16x8_t kf[4], vf[4];
-  const int kc = min(ka, S - 1);
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    kf[s] = load_row8(k + hoff + (size_t)kc * HD + 16 * s + 8 * h, ka < S);
-    vf[s] = load_row8(v + hoff + (size_t)kc * HD + 16 * s + 8 * h, ka < S);
-  }
-
-  floatx16_t dka[2] = {zero16(), zero16()}, dva[2] = {zero16(), zero16()};
-
-  const int qt_begin = (kblk * KB) / QSTEP;
   const int nqt = (S + QSTEP - 1) / QSTEP;
-  Stage2 sq, sd;
-  float rl = 0.f, rd = 0.f;
-  uint2 mw_cur = make_uint2(0u, 0u), mw_next = make_uint2(0u, 0u);
-  auto load_rows = [&](int t) {
-    stage_load(sq, q + hoff, t * QSTEP, S, HD, tid);
-    stage_load(sd, dob, t * QSTEP, S, rstride, tid);
-    if (DROP) {  // this lane's two 32-query keep words of tile t (consumed one tile later)
-      const int w0 = (t * QSTEP) >> 5;
-      mw_next = make_uint2(mcol[w0], (w0 + 1 < W) ? mcol[w0 + 1] : 0u);
-    }
-    if (tid < QSTEP) {
-      const int qq = min(t * QSTEP + tid, S - 1);
-      const bool ok = t * QSTEP + tid < S;
-      rl = ok ? lse[(size_t)bh * S + qq] * LOG2E : 0.f;
-      rd = ok ? delta[(size_t)bh * S + qq] : 0.f;
-    }
-  };
-  auto store_rows = [&](int buf) {
-    stage_store(sq, lds + buf * 2 * QSTEP * HD, tid);
-    stage_store(sd, lds + buf * 2 * QSTEP * HD + QSTEP * HD, tid);
-    if (tid < QSTEP) {
-      rowc[buf * 2 * QSTEP + tid] = rl;
-      rowc[buf * 2 * QSTEP + QSTEP + tid] = rd;
-    }
-  };
-  if (qt_begin < nqt) {
-    load_rows(qt_begin);
-    store_rows(0);
-    mw_cur = mw_next;
-  }
-  __syncthreads();
-
-  // Tiles qt_begin, qt_begin+1 hold every diagonal sub-tile of the block (masked
-  // kind, fully-masked sub-tiles skipped); later full tiles are straight-line
-  // unmasked; a ragged last tile (S % 64) is masked again.
-  auto step = [&](auto maskc, int t) {
-    constexpr bool MASKED = decltype(maskc)::value;
-    const int cur = (t - qt_begin) & 1;
-    const bool more = t + 1 < nqt;
-    const uint32_t mw0 = mw_cur.x, mw1 = mw_cur.y;
-    if (more) load_rows(t + 1);
-    const bf16_t* Qt = lds + cur * 2 * QSTEP * HD;
-    const bf16_t* Dt = Qt + QSTEP * HD;
-    const float* rlp = rowc + cur * 2 * QSTEP;
-    const float* rdp = rlp + QSTEP;
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      const int qs = t * QSTEP + 32 * qt;
-      const bf16_t* Qs = Qt + 32 * qt * HD;
-      const bf16_t* Ds = Dt + 32 * qt * HD;
-      const uint32_t mw = (qt ? mw1 : mw0) >> (4 * h);
-      if (!MASKED)
-        dkdv_subtile<false, DROP>(dka, dva, Qs, Ds, rlp + 32 * qt, rdp + 32 * qt, mw, kf, vf, qs, ka, S, lane,
-                                  c_log2, dscale);
-      else if (qs + 31 >= k0)
-        dkdv_subtile<true, DROP>(dka, dva, Qs, Ds, rlp + 32 * qt, rdp + 32 * qt, mw, kf, vf, qs, ka, S, lane,
-                                 c_log2, dscale);
-    }
-    if (more) store_rows(cur ^ 1);
-    mw_cur = mw_next;
-    __syncthreads();
-  };
+  const bf16_t* dob = dout + ((size_t)b * S * nh + head) * HD;
   using UNM = std::integral_constant<bool, false>;
   using MSK = std::integral_constant<bool, true>;
-  int t = qt_begin;
-  const int t_diag = min(nqt, qt_begin + 2), t_full = S / QSTEP;
-  for (; t < t_diag; ++t) step(MSK{}, t);
-  for (; t < t_full; ++t) step(UNM{}, t);
-  for (; t < nqt; ++t) step(MSK{}, t);
 
-  if (ka < S) {
-    bf16_t* dkr = dk + hoff + (size_t)ka * HD;
-    bf16_t* dvr = dv + hoff + (size_t)ka * HD;
+#pragma unroll 1
+  for (int it = 0; it < 2; ++it) {
+    const int kblk = it == 0 ? (int)blockIdx.x : nrb - 1 - (int)blockIdx.x;  // long item (early keys) first
+    if (it == 1 && kblk <= (int)blockIdx.x) break;                           // odd nrb: middle item once
+    const int k0 = kblk * RB + wid * 32;  // wave-uniform
+    const int ka = k0 + kl;
+    // this lane's key column of the transposed keep-bit mask: one word per 32 queries
+    const uint32_t* mcol = DROP ? maskT + ((size_t)bh * S + min(ka, S - 1)) * W : nullptr;
+
+    bf16x8_t kf[4], vf[4];
+    const int kc = min(ka, S - 1);
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        u16x4 wk, wv;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          wk.v[e] = f2bf(dka[dt][4 * g + e] * scale);
-          wv.v[e] = f2bf(dva[dt][4 * g + e] * (DROP ? dscale : 1.f));
-        }
-        *reinterpret_cast<u16x4*>(dkr + 32 * dt + 8 * g + 4 * h) = wk;
-        *reinterpret_cast<u16x4*>(dvr + 32 * dt + 8 * g + 4 * h) = wv;
+    for (int s = 0; s < 4; ++s) {
+      kf[s] = load_row8(k + hoff + (size_t)kc * HD + 16 * s + 8 * h, ka < S);
+      vf[s] = load_row8(v + hoff + (size_t)kc * HD + 16 * s + 8 * h, ka < S);
+    }
+    floatx16_t dka[2] = {zero16(), zero16()}, dva[2] = {zero16(), zero16()};
+
+    const int qt_begin = kblk;  // the 64-query tile holding this item's diagonal
+    float rl = 0.f, rd = 0.f;
+    uint2 mw_cur = make_uint2(0u, 0u), mw_next = make_uint2(0u, 0u);
+    auto load_rows = [&](int t, int buf) {  // Q / dO tiles by LDS-DMA, row stats via registers
+      glds_tile(q + hoff, t * QSTEP, S, HD, lds + buf * 2 * QSTEP * HD, wid, lane);
+      glds_tile(dob, t * QSTEP, S, rstride, lds + buf * 2 * QSTEP * HD + QSTEP * HD, wid, lane);
+      if (DROP) {  // this lane's two 32-query keep words of tile t (consumed one tile later)
+        const int w0 = (t * QSTEP) >> 5;
+        mw_next = make_uint2(mcol[w0], (w0 + 1 < W) ? mcol[w0 + 1] : 0u);
       }
+      if (tid < QSTEP) {
+        const int qq = min(t * QSTEP + tid, S - 1);
+        const bool ok = t * QSTEP + tid < S;
+        rl = ok ? lse[(size_t)bh * S + qq] * LOG2E : 0.f;
+        rd = ok ? delta[(size_t)bh * S + qq] : 0.f;
+      }
+    };
+    auto store_rows = [&](int buf) {
+      if (tid < QSTEP) {
+        rowc[buf * 2 * QSTEP + tid] = rl;
+        rowc[buf * 2 * QSTEP + QSTEP + tid] = rd;
+      }
+    };
+    load_rows(qt_begin, 0);
+    store_rows(0);
+    mw_cur = mw_next;
+    __syncthreads();
+
+    // Tile qt_begin holds every diagonal sub-tile of the item (masked kind, fully
+    // masked sub-tiles skipped); later full tiles are straight-line unmasked; a ragged
+    // last tile (S % 64) is masked again.
+    auto step = [&](auto maskc, int t) {
+      constexpr bool MASKED = decltype(maskc)::value;
+      const int cur = (t - qt_begin) & 1;
+      const bool more = t + 1 < nqt;
+      const uint32_t mw0 = mw_cur.x, mw1 = mw_cur.y;
+      if (more) load_rows(t + 1, cur ^ 1);
+      const bf16_t* Qt = lds + cur * 2 * QSTEP * HD;
+      const bf16_t* Dt = Qt + QSTEP * HD;
+      const float* rlp = rowc + cur * 2 * QSTEP;
+      const float* rdp = rlp + QSTEP;
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        const int qs = t * QSTEP + 32 * qt;
+        const bf16_t* Qs = Qt + 32 * qt * HD;
+        const bf16_t* Ds = Dt + 32 * qt * HD;
+        const uint32_t mw = (qt ? mw1 : mw0) >> (4 * h);
+        if (!MASKED)
+          dkdv_subtile<false, DROP>(dka, dva, Qs, Ds, rlp + 32 * qt, rdp + 32 * qt, mw, kf, vf, qs, ka, S, lane,
+                                    c_log2, dscale);
+        else if (qs + 31 >= k0)
+          dkdv_subtile<true, DROP>(dka, dva, Qs, Ds, rlp + 32 * qt, rdp + 32 * qt, mw, kf, vf, qs, ka, S, lane,
+                                   c_log2, dscale);
+      }
+      if (more) store_rows(cur ^ 1);
+      mw_cur = mw_next;
+      __syncthreads();
+    };
+    int t = qt_begin;
+    const int t_full = S / QSTEP;
+    if (t < nqt) step(MSK{}, t++);
+    for (; t < t_full; ++t) step(UNM{}, t);
+    for (; t < nqt; ++t) step(MSK{}, t);
+
+    if (ka < S) {
+      bf16_t* dkr = dk + hoff + (size_t)ka * HD;
+      bf16_t* dvr = dv + hoff + (size_t)ka * HD;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          u16x4 wk, wv;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            wk.v[e] = f2bf(dka[dt][4 * g + e] * scale);
+            wv.v[e] = f2bf(dva[dt][4 * g + e] * (DROP ? dscale : 1.f));
+          }
+          *reinterpret_cast<u16x4*>(dkr + 32 * dt + 8 * g + 4 * h) = wk;
+          *reinterpret_cast<u16x4*>(dvr + 32 * dt + 8 * g + 4 * h) = wv;
+        }
+    }
   }
 }
 
@@ -610,99 +645,100 @@ __device__ __forceinline__ void dq_tile(floatx16_t (&dqa)[2], const bf16_t* Kt, 
 }
 
 template <bool DROP>
-__global__ __launch_bounds__(256, 2) void k_attn_bwd_dq(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
-                                                        const bf16_t* __restrict__ v, const bf16_t* __restrict__ dout,
-                                                        const float* __restrict__ lse,
-                                                        const float* __restrict__ delta,
-                                                        const uint32_t* __restrict__ mask, bf16_t* __restrict__ dq,
-                                                        int S, int nh, float c_log2, float scale, float dscale) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_attn_bwd_dq(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
+                                                       const bf16_t* __restrict__ v, const bf16_t* __restrict__ dout,
+                                                       const float* __restrict__ lse,
+                                                       const float* __restrict__ delta,
+                                                       const uint32_t* __restrict__ mask, bf16_t* __restrict__ dq,
+                                                       int S, int nh, float c_log2, float scale, float dscale) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * 2 * KVB * HD];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, ql = lane & 31;
-  const int nqb = (S + QB - 1) / QB;
-  const int qb = nqb - 1 - blockIdx.x;
+  const int nrb = (S + RB - 1) / RB;
   const int bh = blockIdx.y;
   const int b = bh / nh, head = bh % nh;
   const size_t hoff = (size_t)bh * S * HD;
-  const int q0 = qb * QB + wid * 32;
-  const int qa = q0 + ql;
-  const bool qok = qa < S;
-  const int qc = min(qa, S - 1);
   const int W = (S + 31) >> 5;
-  const uint32_t* mrow = mask ? mask + ((size_t)bh * S + qc) * W : nullptr;
-
-  bf16x8_t qf[4], df[4];
-  const bf16_t* dorow = dout + (((size_t)b * S + qc) * nh + head) * HD;
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    qf[s] = load_row8(q + hoff + (size_t)qc * HD + 16 * s + 8 * h, qok);
-    df[s] = load_row8(dorow + 16 * s + 8 * h, qok);
-  }
-
-  const float nl2 = qok ? -lse[(size_t)bh * S + qc] * LOG2E : 0.f;
-  const float dl = qok ? delta[(size_t)bh * S + qc] : 0.f;
-  floatx16_t dqa[2] = {zero16(), zero16()};
-
-  const int kv_end = min(S, qb * QB + QB);
-  const int nkv = (kv_end + KVB - 1) / KVB;
-  Stage2 sk, sv;
-  stage_load(sk, k + hoff, 0, S, HD, tid);
-  stage_load(sv, v + hoff, 0, S, HD, tid);
-  stage_store(sk, lds, tid);
-  stage_store(sv, lds + KVB * HD, tid);
-  __syncthreads();
-
-  // Same loop structure as the forward: straight-line unmasked tiles (static LDS
-  // buffers, unrolled by two), then the one or two diagonal tiles.
-  uint2 mw_cur = make_uint2(0u, 0u), mw_next = make_uint2(0u, 0u);
-  if (DROP) mw_cur = make_uint2(mrow[0], W > 1 ? mrow[1] : 0u);
-  auto step = [&](auto bufc, auto maskc, int kb) {
-    constexpr int BUF = decltype(bufc)::value;
-    constexpr bool MASKED = decltype(maskc)::value;
-    const bool more = kb + 1 < nkv;
-    if (more) {
-      stage_load(sk, k + hoff, (kb + 1) * KVB, S, HD, tid);
-      stage_load(sv, v + hoff, (kb + 1) * KVB, S, HD, tid);
-      if (DROP) mw_next = make_uint2(mrow[2 * (kb + 1)], 2 * (kb + 1) + 1 < W ? mrow[2 * (kb + 1) + 1] : 0u);
-    }
-    const bf16_t* Kt = lds + BUF * 2 * KVB * HD;
-    const bf16_t* Vt = Kt + KVB * HD;
-    const int k0 = kb * KVB;
-    if (!MASKED)
-      dq_tile<false, DROP>(dqa, Kt, Vt, qf, df, k0, qa, S, lane, c_log2, nl2, dl, dscale, mw_cur);
-    else if (k0 <= q0 + 31)
-      dq_tile<true, DROP>(dqa, Kt, Vt, qf, df, k0, qa, S, lane, c_log2, nl2, dl, dscale, mw_cur);
-    mw_cur = mw_next;
-    if (more) {
-      bf16_t* Kn = lds + (BUF ^ 1) * 2 * KVB * HD;
-      stage_store(sk, Kn, tid);
-      stage_store(sv, Kn + KVB * HD, tid);
-    }
-    __syncthreads();
-  };
   using B0 = std::integral_constant<int, 0>;
   using B1 = std::integral_constant<int, 1>;
   using UNM = std::integral_constant<bool, false>;
   using MSK = std::integral_constant<bool, true>;
-  const int nfull = 2 * qb;
-  for (int kb = 0; kb < nfull; kb += 2) {
-    step(B0{}, UNM{}, kb);
-    step(B1{}, UNM{}, kb + 1);
-  }
-  if (nfull < nkv) step(B0{}, MSK{}, nfull);
-  if (nfull + 1 < nkv) step(B1{}, MSK{}, nfull + 1);
-  if (qok) {
-    bf16_t* dqr = dq + hoff + (size_t)qa * HD;
+
+#pragma unroll 1
+  for (int it = 0; it < 2; ++it) {
+    const int qb = it == 0 ? nrb - 1 - (int)blockIdx.x : (int)blockIdx.x;  // long item first
+    if (it == 1 && qb >= nrb - 1 - (int)blockIdx.x) break;
+    const int q0 = qb * RB + wid * 32;
+    const int qa = q0 + ql;
+    const bool qok = qa < S;
+    const int qc = min(qa, S - 1);
+    const uint32_t* mrow = mask ? mask + ((size_t)bh * S + qc) * W : nullptr;
+
+    bf16x8_t qf[4], df[4];
+    const bf16_t* dorow = dout + (((size_t)b * S + qc) * nh + head) * HD;
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        u16x4 w;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) w.v[e] = f2bf(dqa[dt][4 * g + e] * scale);
-        *reinterpret_cast<u16x4*>(dqr + 32 * dt + 8 * g + 4 * h) = w;
+    for (int s = 0; s < 4; ++s) {
+      qf[s] = load_row8(q + hoff + (size_t)qc * HD + 16 * s + 8 * h, qok);
+      df[s] = load_row8(dorow + 16 * s + 8 * h, qok);
+    }
+    const float nl2 = qok ? -lse[(size_t)bh * S + qc] * LOG2E : 0.f;
+    const float dl = qok ? delta[(size_t)bh * S + qc] : 0.f;
+    floatx16_t dqa[2] = {zero16(), zero16()};
+
+    const int nkv = (min(S, qb * RB + RB) + KVB - 1) / KVB;
+    glds_tile(k + hoff, 0, S, HD, lds, wid, lane);
+    glds_tile(v + hoff, 0, S, HD, lds + KVB * HD, wid, lane);
+    __syncthreads();
+
+    // Same loop structure as the forward: straight-line unmasked tiles (static LDS
+    // buffers, unrolled by two), then the diagonal tile.
+    uint2 mw_cur = make_uint2(0u, 0u), mw_next = make_uint2(0u, 0u);
+    if (DROP) mw_cur = make_uint2(mrow[0], W > 1 ? mrow[1] : 0u);
+    auto step = [&](auto bufc, auto maskc, int kb) {
+      constexpr int BUF = decltype(bufc)::value;
+      constexpr bool MASKED = decltype(maskc)::value;
+      const bool more = kb + 1 < nkv;
+      if (more) {  // next tile straight into the other buffer (read by nobody since the last barrier)
+        bf16_t* Kn = lds + (BUF ^ 1) * 2 * KVB * HD;
+        glds_tile(k + hoff, (kb + 1) * KVB, S, HD, Kn, wid, lane);
+        glds_tile(v + hoff, (kb + 1) * KVB, S, HD, Kn + KVB * HD, wid, lane);
+        if (DROP) mw_next = make_uint2(mrow[2 * (kb + 1)], 2 * (kb + 1) + 1 < W ? mrow[2 * (kb + 1) + 1] : 0u);
       }
+      const bf16_t* Kt = lds + BUF * 2 * KVB * HD;
+      const bf16_t* Vt = Kt + KVB * HD;
+      const int k0 = kb * KVB;
+      if (!MASKED)
+        dq_tile<false, DROP>(dqa, Kt, Vt, qf, df, k0, qa, S, lane, c_log2, nl2, dl, dscale, mw_cur);
+      else if (k0 <= q0 + 31)
+        dq_tile<true, DROP>(dqa, Kt, Vt, qf, df, k0, qa, S, lane, c_log2, nl2, dl, dscale, mw_cur);
+      mw_cur = mw_next;
+      __syncthreads();
+    };
+    const int nfull = min(qb, nkv);
+    int kb = 0;
+    for (; kb + 1 < nfull; kb += 2) {
+      step(B0{}, UNM{}, kb);
+      step(B1{}, UNM{}, kb + 1);
+    }
+    if (kb < nfull) {
+      step(B0{}, UNM{}, kb);
+      if (kb + 1 < nkv) step(B1{}, MSK{}, kb + 1);
+    } else if (kb < nkv) {
+      step(B0{}, MSK{}, kb);
+    }
+    if (qok) {
+      bf16_t* dqr = dq + hoff + (size_t)qa * HD;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          u16x4 w;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w.v[e] = f2bf(dqa[dt][4 * g + e] * scale);
+          *reinterpret_cast<u16x4*>(dqr + 32 * dt + 8 * g + 4 * h) = w;
+        }
+    }
   }
 }
 
@@ -728,16 +764,17 @@ DLT_API int dlt_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16
                          int gen_mask, hipStream_t st) {
   if (hd != HD || S <= 0) return -1;
   if (thr && !mask) return -2;  // dropout needs the keep-bit buffer
-  const dim3 grid((S + QB - 1) / QB, B * nh);
+  const int nrb = (S + RB - 1) / RB;
+  const dim3 grid((nrb + 1) / 2, B * nh);  // item pairs
   const float c_log2 = scale * LOG2E;
   if (thr) {
     if (gen_mask) {
       const int rc = dlt_attn_dropout_mask(mask, B, nh, S, key, thr, st);
       if (rc) return rc;
     }
-    k_attn_fwd<true><<<grid, 256, 0, st>>>(q, k, v, o, lse, mask, S, nh, c_log2, dscale);
+    k_attn_fwd<true><<<grid, NT, 0, st>>>(q, k, v, o, lse, mask, S, nh, c_log2, dscale);
   } else {
-    k_attn_fwd<false><<<grid, 256, 0, st>>>(q, k, v, o, lse, nullptr, S, nh, c_log2, dscale);
+    k_attn_fwd<false><<<grid, NT, 0, st>>>(q, k, v, o, lse, nullptr, S, nh, c_log2, dscale);
   }
   DLT_CHECK_LAUNCH();
 }
@@ -749,16 +786,16 @@ DLT_API int dlt_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, cons
   const int rows = B * S * nh;
   k_attn_bwd_delta<<<(rows + 255) / 256, 256, 0, st>>>(o, dout, delta_ws, B, S, nh);
   const float c_log2 = scale * LOG2E;
-  const dim3 gk((S + KB - 1) / KB, B * nh);
-  const dim3 gq((S + QB - 1) / QB, B * nh);
+  const int nrb = (S + RB - 1) / RB;
+  const dim3 gk((nrb + 1) / 2, B * nh), gq((nrb + 1) / 2, B * nh);  // item pairs
   if (mask) {
     const uint32_t* maskT = mask + (size_t)B * nh * S * ((S + 31) / 32);
-    k_attn_bwd_dkdv<true><<<gk, 256, 0, st>>>(q, k, v, dout, lse, delta_ws, maskT, dk, dv, S, nh, c_log2, scale,
+    k_attn_bwd_dkdv<true><<<gk, NT, 0, st>>>(q, k, v, dout, lse, delta_ws, maskT, dk, dv, S, nh, c_log2, scale,
                                               dscale);
-    k_attn_bwd_dq<true><<<gq, 256, 0, st>>>(q, k, v, dout, lse, delta_ws, mask, dq, S, nh, c_log2, scale, dscale);
+    k_attn_bwd_dq<true><<<gq, NT, 0, st>>>(q, k, v, dout, lse, delta_ws, mask, dq, S, nh, c_log2, scale, dscale);
   } else {
-    k_attn_bwd_dkdv<false><<<gk, 256, 0, st>>>(q, k, v, dout, lse, delta_ws, mask, dk, dv, S, nh, c_log2, scale, dscale);
-    k_attn_bwd_dq<false><<<gq, 256, 0, st>>>(q, k, v, dout, lse, delta_ws, mask, dq, S, nh, c_log2, scale, dscale);
+    k_attn_bwd_dkdv<false><<<gk, NT, 0, st>>>(q, k, v, dout, lse, delta_ws, mask, dk, dv, S, nh, c_log2, scale, dscale);
+    k_attn_bwd_dq<false><<<gq, NT, 0, st>>>(q, k, v, dout, lse, delta_ws, mask, dq, S, nh, c_log2, scale, dscale);
   }
   DLT_CHECK_LAUNCH();
 }
