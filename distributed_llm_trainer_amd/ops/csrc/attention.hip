@@ -70,6 +70,39 @@ __device__ __forceinline__ bf16x8_t tr_frag(const bf16_t* T, int kk, int dt, int
   return __builtin_bit_cast(bf16x8_t, c);
 }
 
+// The same fragment read through inline asm.  hipcc conservatively drains vmcnt(0)
+// before any ds_read_b64_tr_b16 *intrinsic* while a global_load_lds is in flight
+// (it cannot prove the DMA target and the read disjoint), which serialises the next
+// tile's LDS-DMA with this tile's compute.  Asm reads are invisible to that alias
+// check; the protocol that makes them safe is explicit: every tile step ends with
+// `s_waitcnt vmcnt(0)` + barrier (tile_barrier), so a tile is complete before any
+// wave reads it, and tr_wait() retires the reads before their registers are used.
+__device__ __forceinline__ shortx4_t lds_tr4_asm(const bf16_t* T, int row, int col) {
+  shortx4_t r;
+  const uint32_t addr = (uint32_t)(uintptr_t)(T + swz_off(row, col));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr));
+  return r;
+}
+__device__ __forceinline__ bf16x8_t tr_frag_asm(const bf16_t* T, int kk, int dt, int lane) {
+  const int h = lane >> 5, i = lane & 15;
+  const int col = 32 * dt + 16 * ((lane >> 4) & 1) + 4 * (i & 3);
+  const int r1 = 16 * kk + 4 * h + (i >> 2);
+  const shortx4_t a = lds_tr4_asm(T, r1, col);
+  const shortx4_t b = lds_tr4_asm(T, r1 + 8, col);
+  shortx8_t c = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8_t, c);
+}
+// Retire outstanding LDS reads; the fragments are in/out operands so no consumer can
+// be scheduled above the wait.
+__device__ __forceinline__ void tr_wait(bf16x8_t& a, bf16x8_t& b, bf16x8_t& c, bf16x8_t& d) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d)::"memory");
+}
+// End of a tile step: this wave's LDS-DMA writes have landed, then the workgroup syncs.
+__device__ __forceinline__ void tile_barrier() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
 __device__ __forceinline__ bf16x8_t acc_frag(const floatx16_t& acc, int s) {
   bf16x8_t r;
 #pragma unroll
@@ -251,7 +284,7 @@ __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const b
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt) vf[kk][dt] = tr_frag(Vt, 2 * t + kk, dt, lane);
+      for (int dt = 0; dt < 2; ++dt) vf[kk][dt] = tr_frag_asm(Vt, 2 * t + kk, dt, lane);
     floatx16_t sacc = zero16();
 #pragma unroll
     for (int s = 0; s < 4; ++s) sacc = mfma(kf[s], qf[s], sacc);
@@ -283,6 +316,7 @@ __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const b
       if (DROP) sacc[i] = (words[t] & (1u << ((i & 3) + 8 * (i >> 2)))) ? p : 0.f;  // 1/(1-p) at the end
       else sacc[i] = p;
     }
+    tr_wait(vf[0][0], vf[0][1], vf[1][0], vf[1][1]);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const bf16x8_t pb = acc_frag(sacc, kk);
@@ -363,7 +397,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       else if (k0 <= q0 + 31)
         fwd_tile<true, DROP>(fs, Kt, Vt, qf, k0, qa, S, lane, c_log2, mw_cur);
       mw_cur = mw_next;
-      __syncthreads();
+      tile_barrier();
     };
     const int nfull = min(qb, nkv);
     int kb = 0;
@@ -575,7 +609,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       }
       if (more) store_rows(cur ^ 1);
       mw_cur = mw_next;
-      __syncthreads();
+      tile_barrier();
     };
     int t = qt_begin;
     const int t_full = S / QSTEP;
@@ -713,7 +747,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       else if (k0 <= q0 + 31)
         dq_tile<true, DROP>(dqa, Kt, Vt, qf, df, k0, qa, S, lane, c_log2, nl2, dl, dscale, mw_cur);
       mw_cur = mw_next;
-      __syncthreads();
+      tile_barrier();
     };
     const int nfull = min(qb, nkv);
     int kb = 0;
