@@ -23,9 +23,9 @@
 //    whose lanes are queries (fwd, dQ) and transposed [bh][k][S/32] for dK/dV whose
 //    lanes are keys -- every MFMA kernel fetches ONE 32-bit word per lane per 32x32
 //    sub-tile (2 x 12.6 MB per layer at B8 S1024 nh12).
-//  * Backward = 3 kernels: delta = rowsum(dO*O); dK/dV (workgroup per 128 keys,
-//    accumulated in registers); dQ (workgroup per 128 queries, recomputes S, dP) --
-//    no fp32 atomics anywhere.  Causal tile skipping; heaviest tiles launch first.
+//  * Backward = 2 kernels: dQ (recomputes S, dP; also emits Delta = rowsum(dO*O)),
+//    then dK/dV (accumulated in registers) -- no fp32 atomics anywhere.  Causal
+//    tile skipping; workgroups process paired items of equal total length.
 //
 // Layouts: q, k, v, dq, dk, dv: [B*nh, S, 64] bf16;  o, do: [B, S, nh, 64] bf16
 // (= the [M, H] GEMM layout);  lse, delta: [B*nh, S] fp32 (natural-log lse).
@@ -431,28 +431,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 }
 
 // ============================================================================ backward
-// delta[bh, q] = sum_d dO[b,q,head,d] * O[b,q,head,d]
-__global__ __launch_bounds__(256) void k_attn_bwd_delta(const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout,
-                                                        float* __restrict__ delta, int B, int S, int nh) {
-  const int rows = B * S * nh;
-  const int r = blockIdx.x * 256 + threadIdx.x;
-  if (r >= rows) return;
-  const int head = r % nh;
-  const int s = (r / nh) % S;
-  const int b = r / (nh * S);
-  const bf16_t* po = o + (size_t)r * HD;
-  const bf16_t* pd = dout + (size_t)r * HD;
-  float acc = 0.f;
-#pragma unroll
-  for (int c = 0; c < HD / 8; ++c) {
-    const u16x8 a = *reinterpret_cast<const u16x8*>(po + 8 * c);
-    const u16x8 d = *reinterpret_cast<const u16x8*>(pd + 8 * c);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) acc += bf2f(a.v[e]) * bf2f(d.v[e]);
-  }
-  delta[((size_t)b * nh + head) * S + s] = acc;
-}
-
 // ---------------------------------------------------------------- dK / dV
 // One workgroup per 128 keys (32 per wave); sweep query tiles of 64 (two 32-row
 // sub-tiles).  Accumulators: S and dP with queries in registers, keys on lanes.
@@ -681,8 +659,9 @@ __device__ __forceinline__ void dq_tile(floatx16_t (&dqa)[2], const bf16_t* Kt, 
 template <bool DROP>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_attn_bwd_dq(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
                                                        const bf16_t* __restrict__ v, const bf16_t* __restrict__ dout,
+                                                       const bf16_t* __restrict__ o,
                                                        const float* __restrict__ lse,
-                                                       const float* __restrict__ delta,
+                                                       float* __restrict__ delta,
                                                        const uint32_t* __restrict__ mask, bf16_t* __restrict__ dq,
                                                        int S, int nh, float c_log2, float scale, float dscale) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * 2 * KVB * HD];
@@ -710,14 +689,19 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     const uint32_t* mrow = mask ? mask + ((size_t)bh * S + qc) * W : nullptr;
 
     bf16x8_t qf[4], df[4];
-    const bf16_t* dorow = dout + (((size_t)b * S + qc) * nh + head) * HD;
+    const size_t orow = (((size_t)b * S + qc) * nh + head) * HD;
+    float dsum = 0.f;  // Delta = rowsum(dO * O), computed here (this kernel runs before dK/dV)
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       qf[s] = load_row8(q + hoff + (size_t)qc * HD + 16 * s + 8 * h, qok);
-      df[s] = load_row8(dorow + 16 * s + 8 * h, qok);
+      df[s] = load_row8(dout + orow + 16 * s + 8 * h, qok);
+      const bf16x8_t of = load_row8(o + orow + 16 * s + 8 * h, qok);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dsum += (float)df[s][j] * (float)of[j];
     }
     const float nl2 = qok ? -lse[(size_t)bh * S + qc] * LOG2E : 0.f;
-    const float dl = qok ? delta[(size_t)bh * S + qc] : 0.f;
+    const float dl = xhalf_sum(dsum);
+    if (qok && h == 0) delta[(size_t)bh * S + qa] = dl;
     floatx16_t dqa[2] = {zero16(), zero16()};
 
     const int nkv = (min(S, qb * RB + RB) + KVB - 1) / KVB;
@@ -817,19 +801,20 @@ DLT_API int dlt_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, cons
                          const float* lse, const uint32_t* mask, float* delta_ws, bf16_t* dq, bf16_t* dk, bf16_t* dv,
                          int B, int nh, int S, int hd, float scale, float dscale, hipStream_t st) {
   if (hd != HD || S <= 0) return -1;
-  const int rows = B * S * nh;
-  k_attn_bwd_delta<<<(rows + 255) / 256, 256, 0, st>>>(o, dout, delta_ws, B, S, nh);
   const float c_log2 = scale * LOG2E;
   const int nrb = (S + RB - 1) / RB;
   const dim3 gk((nrb + 1) / 2, B * nh), gq((nrb + 1) / 2, B * nh);  // item pairs
+  // dQ first: it also produces Delta = rowsum(dO * O) (no separate kernel), which
+  // dK/dV then reads.
   if (mask) {
     const uint32_t* maskT = mask + (size_t)B * nh * S * ((S + 31) / 32);
+    k_attn_bwd_dq<true><<<gq, NT, 0, st>>>(q, k, v, dout, o, lse, delta_ws, mask, dq, S, nh, c_log2, scale, dscale);
     k_attn_bwd_dkdv<true><<<gk, NT, 0, st>>>(q, k, v, dout, lse, delta_ws, maskT, dk, dv, S, nh, c_log2, scale,
-                                              dscale);
-    k_attn_bwd_dq<true><<<gq, NT, 0, st>>>(q, k, v, dout, lse, delta_ws, mask, dq, S, nh, c_log2, scale, dscale);
+                                             dscale);
   } else {
-    k_attn_bwd_dkdv<false><<<gk, NT, 0, st>>>(q, k, v, dout, lse, delta_ws, mask, dk, dv, S, nh, c_log2, scale, dscale);
-    k_attn_bwd_dq<false><<<gq, NT, 0, st>>>(q, k, v, dout, lse, delta_ws, mask, dq, S, nh, c_log2, scale, dscale);
+    k_attn_bwd_dq<false><<<gq, NT, 0, st>>>(q, k, v, dout, o, lse, delta_ws, mask, dq, S, nh, c_log2, scale, dscale);
+    k_attn_bwd_dkdv<false><<<gk, NT, 0, st>>>(q, k, v, dout, lse, delta_ws, mask, dk, dv, S, nh, c_log2, scale,
+                                              dscale);
   }
   DLT_CHECK_LAUNCH();
 }
