@@ -44,6 +44,7 @@ _SIGS = {
                   c_float, c_float, c_float, c_void_p, c_void_p],
     "dlt_cast_bf16": [c_void_p, c_void_p, c_int64, c_void_p],
     "dlt_wgrad_gemm": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
+    "dlt_gemm_tn": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "dlt_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                      c_uint32, c_uint32, c_float, c_int, c_void_p],
     "dlt_attn_dropout_mask": [c_void_p, c_int, c_int, c_int, c_uint32, c_uint32, c_void_p],
@@ -370,3 +371,24 @@ def wgrad_gemm(dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, splits: int 
     _req(dw, torch.float32, "wgrad.dw", N * K)
     _chk(lib().dlt_wgrad_gemm(_p(dy), _p(x), _p(dw), M, N, K, splits, _stream()), "wgrad_gemm")
     return True
+
+
+# ------------------------------------------------------------------ TN GEMM
+GEMM_TN_TILES = {0: (256, 256), 1: (256, 128), 2: (128, 128), 3: (128, 64), 4: (64, 128)}
+
+
+def gemm_tn(a: torch.Tensor, b: torch.Tensor, cfg: int, out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """C[M,N] = A[M,K] @ B[N,K]^T (bf16, fp32 accumulate) with the hand-written MFMA
+    kernel (``csrc/gemm_tn.hip``) in tile configuration ``cfg``.  Returns None (nothing
+    launched) when the shape does not tile for that configuration."""
+    M, K = a.shape
+    N = b.shape[0]
+    bm, bn = GEMM_TN_TILES[cfg]
+    if M % bm or N % bn or K % 64 or b.shape[1] != K:
+        return None
+    _req(a, torch.bfloat16, "gemm_tn.a")
+    _req(b, torch.bfloat16, "gemm_tn.b")
+    c = torch.empty(M, N, dtype=torch.bfloat16, device=a.device) if out is None else out
+    _req(c, torch.bfloat16, "gemm_tn.c", M * N)
+    _chk(lib().dlt_gemm_tn(_p(a), _p(b), _p(c), M, N, K, K, K, N, cfg, _stream()), "gemm_tn")
+    return c

@@ -261,3 +261,20 @@ def test_attention_fwd_growing_max_rescales(p):
     o2, lse2 = ref.attention_fwd(q, k, v, p, key)
     _close(aux[0], lse2, 2e-3, 1e-3, "lse(growing)")
     _close(o, o2.float(), 2e-2, 2e-2, "o(growing)")
+
+
+@pytest.mark.parametrize("cfg", sorted(hip.GEMM_TN_TILES))
+@pytest.mark.parametrize("shape", [(512, 768, 768), (256, 2304, 768), (256, 768, 3072)])
+def test_gemm_tn(cfg, shape):
+    """Hand-written MFMA GEMM C = A B^T against an fp32 torch reference."""
+    M, N, K = shape
+    torch.manual_seed(cfg)
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = torch.randn(N, K, device=DEV).bfloat16()
+    c = hip.gemm_tn(a, b, cfg)
+    bm, bn = hip.GEMM_TN_TILES[cfg]
+    if M % bm or N % bn:
+        assert c is None
+        return
+    ref = a.float() @ b.float().t()
+    _close(c, ref, 2e-2 * ref.abs().max().item(), 1e-2, f"gemm_tn cfg{cfg}")
