@@ -177,3 +177,31 @@ def _replica_worker(rank, world):
 def test_replica_divergence_detected():
     out = run_multiprocess(_replica_worker, world=2)
     assert all("ranks [1]" in o for o in out), out
+
+
+def _fsdp_reshard_load_worker(rank, world, path):
+    """Load a checkpoint written by a 2-rank FSDP job into a job of a different size."""
+    from distributed_llm_trainer_amd.models.config import GPTConfig
+    from distributed_llm_trainer_amd.training.configs import FSDPConfig, FSDPTrainingConfig
+    from distributed_llm_trainer_amd.training.fsdp_trainer import FSDPTrainer
+    cfg = GPTConfig(**TINY)
+    tc = FSDPTrainingConfig(batch_size=2, gradient_accumulation_steps=2, warmup_steps=1, learning_rate=1e-2)
+    tr = FSDPTrainer(cfg, tc, FSDPConfig(reduce_dtype="fp32"))
+    tr.load_checkpoint(path)
+    sd = tr._full_state()
+    return {k: v.clone() for k, v in sd.items()}, tr.global_step
+
+
+def test_fsdp_checkpoint_loads_at_other_world_size(tmp_path):
+    """FULL_STATE_DICT checkpoints are world-size independent: written by 2 ranks, read
+    back by 1 and by 3 ranks with identical full parameters."""
+    path = str(tmp_path / "fsdp2.pt")
+    run_multiprocess(_fsdp_ckpt_worker, world=2, args=(path,))
+    from distributed_llm_trainer_amd.utils.checkpoint import load_checkpoint
+    ref = load_checkpoint(path)["model"]
+    for world in (1, 3):
+        outs = run_multiprocess(_fsdp_reshard_load_worker, world=world, args=(path,))
+        for sd, step in outs:
+            assert step == 2
+            for k, v in ref.items():
+                assert torch.equal(sd[k].float(), v.float()), (world, k)
