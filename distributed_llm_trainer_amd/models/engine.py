@@ -334,7 +334,7 @@ class GPTEngine:
         hw, hg = prov.head(), prov.head_grads()
         # lm_head: dnf = dlogits @ E ; dE += dlogits^T @ (nf * dloss)
         dnf = gm.linear_dgrad(st.dlogits, hw.lm_head)
-        nf_scaled = (st.nf.float() * dloss).to(st.nf.dtype)
+        nf_scaled = ops.scale_bf16(st.nf, dloss) if st.nf.dtype == torch.bfloat16 else st.nf * dloss
         gm.wgrad_acc(hg.embed, st.dlogits, nf_scaled)
         st.dlogits = None
         key_last = self._keys(st.micro, L - 1)[2]

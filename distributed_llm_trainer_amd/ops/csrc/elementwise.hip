@@ -220,6 +220,27 @@ __global__ __launch_bounds__(256) void k_swiglu_bwd(const bf16_t* __restrict__ g
   }
 }
 
+// y = x * (*scale) for a bf16 tensor and a device fp32 scalar (the autograd output
+// gradient), one pass -- replaces an upcast + multiply + downcast kernel chain.
+__global__ __launch_bounds__(256) void k_scale_bf16(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                    long n8, const float* __restrict__ scale) {
+  const float sc = *scale;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    u16x8 v = reinterpret_cast<const u16x8*>(x)[i];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v.v[e] = f2bf(bf2f(v.v[e]) * sc);
+    reinterpret_cast<u16x8*>(y)[i] = v;
+  }
+}
+
+DLT_API int dlt_scale_bf16(const bf16_t* x, bf16_t* y, long n, const float* scale, hipStream_t st) {
+  if (n % 8) return -1;
+  const long n8 = n / 8;
+  const int blocks = (int)((n8 + 255) / 256 < 4096 ? (n8 + 255) / 256 : 4096);
+  k_scale_bf16<<<blocks, 256, 0, st>>>(x, y, n8, scale);
+  DLT_CHECK_LAUNCH();
+}
+
 DLT_API int dlt_swiglu_fwd(const bf16_t* gu, bf16_t* a, int M, int I, hipStream_t st) {
   if (I % 8) return -1;
   k_swiglu_fwd<<<ew_blocks((size_t)M * (I / 8)), 256, 0, st>>>(gu, a, M, I);

@@ -198,7 +198,8 @@ __global__ __launch_bounds__(256) void k_rmsnorm_bwd(
   }
 }
 
-// dw[j] += sum over the partial rows; grid (ceil(H/256), 32): 32 atomics per column.
+// dw[j] += sum over the partial rows; grid (ceil(H/256), 128): 128 atomics per column,
+// 8 rows per thread (latency-bound otherwise).
 __global__ __launch_bounds__(256) void k_colsum_acc(const float* __restrict__ part, float* __restrict__ dw, int rows,
                                                     int H) {
   const int j = blockIdx.x * 256 + threadIdx.x;
@@ -274,6 +275,6 @@ DLT_API int dlt_rmsnorm_bwd(const bf16_t* dy, const float* x, const float* rstd,
     default: k_rmsnorm_bwd<16><<<grid, block, shm, stream>>>(ARGS); break;
   }
 #undef ARGS
-  if (dw_ws) k_colsum_acc<<<dim3((H + 255) / 256, 32), 256, 0, stream>>>(dw_ws, dw, blocks, H);
+  if (dw_ws) k_colsum_acc<<<dim3((H + 255) / 256, 128), 256, 0, stream>>>(dw_ws, dw, blocks, H);
   DLT_CHECK_LAUNCH();
 }

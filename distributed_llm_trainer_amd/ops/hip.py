@@ -44,6 +44,7 @@ _SIGS = {
                   c_float, c_float, c_float, c_void_p, c_void_p],
     "dlt_cast_bf16": [c_void_p, c_void_p, c_int64, c_void_p],
     "dlt_wgrad_gemm": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
+    "dlt_scale_bf16": [c_void_p, c_void_p, ctypes.c_long, c_void_p, c_void_p],
     "dlt_gemm_tn": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "dlt_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                      c_uint32, c_uint32, c_float, c_int, c_void_p],
@@ -392,3 +393,14 @@ def gemm_tn(a: torch.Tensor, b: torch.Tensor, cfg: int, out: Optional[torch.Tens
     _req(c, torch.bfloat16, "gemm_tn.c", M * N)
     _chk(lib().dlt_gemm_tn(_p(a), _p(b), _p(c), M, N, K, K, K, N, cfg, _stream()), "gemm_tn")
     return c
+
+
+def scale_bf16(x: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
+    """y = x * scale with a device scalar (no host sync); falls back for odd sizes."""
+    _req(x, torch.bfloat16, "scale_bf16.x")
+    s = scale.reshape(1).float().contiguous()
+    if x.numel() % 8:
+        return (x.float() * s).to(torch.bfloat16)
+    y = torch.empty_like(x)
+    _chk(lib().dlt_scale_bf16(_p(x), _p(y), x.numel(), _p(s), _stream()), "scale_bf16")
+    return y

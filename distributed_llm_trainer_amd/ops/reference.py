@@ -254,3 +254,8 @@ def adamw_step(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, e
 
 def sumsq(x: torch.Tensor, out: torch.Tensor) -> None:
     out += x.float().pow(2).sum()
+
+
+def scale_bf16(x: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
+    """y = x * scale (scale: 0-d/1-element device tensor), result in x's dtype."""
+    return (x.float() * scale.reshape(()).float()).to(x.dtype)

@@ -61,6 +61,7 @@ class DistributedTrainer:
         self.global_step = 0
         self.tokens_seen = 0
         self._last_norm = None
+        self._grads_zeroed = False
 
     # ------------------------------------------------------------------ setup
     def _setup_distributed(self):
@@ -127,7 +128,9 @@ class DistributedTrainer:
             lr = self.get_lr(self.global_step)
             for g in self.optimizer.param_groups:
                 g["lr"] = lr
-        self.optimizer.zero_grad(set_to_none=True)
+        if not self._grads_zeroed:  # the previous step already zeroed them (saves a 600 MB memset)
+            self.optimizer.zero_grad(set_to_none=True)
+        self._grads_zeroed = False
         input_ids = unwrap_batch(batch).to(self.device, non_blocking=True)
         GA = cfg.gradient_accumulation_steps
         micro_bs = input_ids.shape[0] // GA
@@ -169,6 +172,7 @@ class DistributedTrainer:
                 self.store.refresh_shadow()
         self._last_norm = scale[0]
         self.optimizer.zero_grad(set_to_none=True)
+        self._grads_zeroed = True
         if not cfg.lr_schedule_fix:  # reference order: LR for the *next* step set after this one
             lr = self.get_lr(self.global_step)
             for g in self.optimizer.param_groups:

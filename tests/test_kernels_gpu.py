@@ -278,3 +278,9 @@ def test_gemm_tn(cfg, shape):
         return
     ref = a.float() @ b.float().t()
     _close(c, ref, 2e-2 * ref.abs().max().item(), 1e-2, f"gemm_tn cfg{cfg}")
+
+
+def test_scale_bf16():
+    x = torch.randn(64, 768, device=DEV).bfloat16()
+    s = torch.tensor(0.25, device=DEV)
+    _close(hip.scale_bf16(x, s), ref.scale_bf16(x, s), 1e-6, 0.0, "scale_bf16")
