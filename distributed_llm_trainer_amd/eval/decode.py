@@ -93,6 +93,86 @@ def forward_cached(model, ids: torch.Tensor, cache: KVCache) -> torch.Tensor:
     return logits
 
 
+class DecodeGraph:
+    """The one-token decode step captured once as a HIP graph and replayed per token.
+
+    Decode is launch-bound (~200 small kernels per token for GPT-2 small); a graph
+    replay issues them with one call.  Everything inside has a fixed shape: the token
+    ids and the position are device tensors, the new K/V row is written with
+    ``index_copy_`` at the position, and attention runs over the whole preallocated
+    cache with a ``key_pos > pos`` mask (a few extra MB per layer per token, far cheaper
+    than the launches it saves).  Used by ``kv_cached_generate`` on a GPU with a
+    single-process parameter store (FSDP gathers are collectives: not captured).
+    """
+
+    def __init__(self, model, cache: KVCache, pos: int):
+        self.model, self.cache = model, cache
+        cfg = model.config
+        dev = cache.k[0].device
+        B = cache.k[0].shape[0]
+        self.ids = torch.zeros(B, 1, dtype=torch.long, device=dev)
+        self.pos = torch.full((1,), pos, dtype=torch.long, device=dev)
+        self.kpos = torch.arange(cfg.max_seq_len, device=dev)
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):  # warm up allocations / library plans outside the capture
+            for _ in range(2):
+                self._step()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.logits = self._step()
+
+    def _step(self) -> torch.Tensor:
+        model, cache = self.model, self.cache
+        eng, cfg = model.engine, model.config
+        prov, dt = eng.provider, eng.act_dtype
+        B = self.ids.shape[0]
+        nh, hd = cfg.num_heads, cfg.head_dim
+        cos_t, sin_t = eng.rope(cfg.max_seq_len, self.ids.device)
+        cos = cos_t.index_select(0, self.pos).float()
+        sin = sin_t.index_select(0, self.pos).float()
+        hw = prov.head()
+        h = hw.embed.index_select(0, self.ids.view(-1)).float().view(B, 1, -1)
+        scale = 1.0 / math.sqrt(hd)
+        masked = (self.kpos > self.pos)[None, None, None, :]
+        for i in range(cfg.num_layers):
+            w = prov.layer(i)
+            n1 = _rms(h, w.ln1, eng.eps).to(dt)
+            qkv = torch.matmul(n1, w.wqkv.t()).float().view(B, 1, 3, nh, hd)
+            q = _rope(qkv[:, :, 0], cos, sin)
+            k = _rope(qkv[:, :, 1], cos, sin)
+            cache.k[i].index_copy_(2, self.pos, k.transpose(1, 2).to(dt))
+            cache.v[i].index_copy_(2, self.pos, qkv[:, :, 2].transpose(1, 2).to(dt))
+            qh = q.to(dt).transpose(1, 2)  # [B, nh, 1, hd]; bf16 GEMVs straight on the bf16 cache
+            s_ = torch.matmul(qh, cache.k[i].transpose(-2, -1)).float() * scale
+            pr = torch.softmax(s_.masked_fill(masked, float("-inf")), dim=-1)
+            o = torch.matmul(pr.to(dt), cache.v[i]).transpose(1, 2).reshape(B, 1, nh * hd)
+            h = h + torch.matmul(o, w.wo.t()).float()
+            n2 = _rms(h, w.ln2, eng.eps).to(dt)
+            gu = torch.matmul(n2, w.wgu.t()).float()
+            I = cfg.intermediate_size
+            h = h + torch.matmul((F.silu(gu[..., :I]) * gu[..., I:]).to(dt), w.wdown.t()).float()
+        nf = _rms(h[:, -1], hw.norm, eng.eps).to(dt)
+        return torch.matmul(nf, hw.lm_head.t())[:, :cfg.vocab_size].float()
+
+    def __call__(self, ids: torch.Tensor) -> torch.Tensor:
+        """Append ``ids`` [B, 1] at position cache.len; returns logits [B, V] (graph-owned:
+        consume before the next call)."""
+        self.ids.copy_(ids)
+        self.pos.fill_(self.cache.len)
+        self.graph.replay()
+        self.cache.len += 1
+        return self.logits
+
+
+def _graph_ok(model, device) -> bool:
+    import os
+    from ..parallel.flat import FlatParamStore
+    return (device.type == "cuda" and os.environ.get("DLT_DECODE_GRAPH", "1") != "0"
+            and isinstance(model.engine.provider, FlatParamStore))
+
+
 @torch.no_grad()
 def kv_cached_generate(model, input_ids: torch.Tensor, max_new_tokens: int = 100, temperature: float = 1.0,
                        top_k: int = 50) -> torch.Tensor:
@@ -102,6 +182,8 @@ def kv_cached_generate(model, input_ids: torch.Tensor, max_new_tokens: int = 100
     cache = KVCache(cfg, B, input_ids.device, eng.act_dtype)
     ctx = input_ids[:, -cfg.max_seq_len:]
     logits = forward_cached(model, ctx, cache)
+    graph = DecodeGraph(model, cache, cache.len) if (_graph_ok(model, input_ids.device)
+                                                    and cache.len < cfg.max_seq_len and max_new_tokens > 1) else None
     out = input_ids
     for step in range(max_new_tokens):
         lg = logits / temperature
@@ -114,7 +196,7 @@ def kv_cached_generate(model, input_ids: torch.Tensor, max_new_tokens: int = 100
         if step == max_new_tokens - 1:
             break
         if cache.len + 1 <= cfg.max_seq_len:
-            logits = forward_cached(model, nxt, cache)
+            logits = graph(nxt) if graph is not None else forward_cached(model, nxt, cache)
         else:  # context window full: re-prefill the cropped window (reference cropping semantics)
             cache.len = 0
             logits = forward_cached(model, out[:, -cfg.max_seq_len:], cache)
