@@ -58,98 +58,103 @@ DLT_API int dlt_embedding_bwd(const int64_t* ids, const float* dout, float* dW, 
 // ---------------------------------------------------------------- RoPE
 // qkv [B*S, 3, nh, hd] (bf16) -> q, k, v [B, nh, S, hd]; q, k rotated (NeoX half split)
 // in fp32 with cos/sin tables [S, hd/2].  One thread = 4 rotary pairs of one head.
+// One thread = one 8-wide chunk of each rotation half (16-B vectors; the partner
+// element of column j is j + hd/2 in NeoX rotate_half).  32-bit index math only
+// (64-bit div/mod is emulated on the GPU and cost ~30 % of this kernel).
 __global__ __launch_bounds__(256) void k_rope_qkv_fwd(const bf16_t* __restrict__ qkv, const float* __restrict__ cosT,
                                                       const float* __restrict__ sinT, bf16_t* __restrict__ q,
                                                       bf16_t* __restrict__ k, bf16_t* __restrict__ v,
                                                       int B, int S, int nh, int hd) {
   const int half = hd >> 1;
-  const int per_head = half >> 2;  // threads per head-section
-  const size_t total = (size_t)B * S * 3 * nh * per_head;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    const int j4 = (int)(i % per_head);
-    size_t r = i / per_head;
-    const int h = (int)(r % nh);
+  const int cpr = half >> 3;  // 8-wide chunks per rotation half
+  const int total = B * S * 3 * nh * cpr;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int j = (i % cpr) * 8;
+    int r = i / cpr;
+    const int h = r % nh;
     r /= nh;
-    const int sec = (int)(r % 3);
-    const size_t m = r / 3;
-    const int s = (int)(m % S);
-    const int b = (int)(m / S);
-    const int j = j4 * 4;
-    const bf16_t* src = qkv + m * (size_t)(3 * nh * hd) + (size_t)sec * nh * hd + (size_t)h * hd;
-    const u16x4 a = *reinterpret_cast<const u16x4*>(src + j);
-    const u16x4 c = *reinterpret_cast<const u16x4*>(src + half + j);
-    bf16_t* dstbase = (sec == 0 ? q : (sec == 1 ? k : v)) + (((size_t)b * nh + h) * S + s) * hd;
-    u16x4 o1, o2;
-    if (sec == 2) {
-      o1 = a; o2 = c;
-    } else {
-      const float4 cs = *reinterpret_cast<const float4*>(cosT + (size_t)s * half + j);
-      const float4 sn = *reinterpret_cast<const float4*>(sinT + (size_t)s * half + j);
-      const float cc[4] = {cs.x, cs.y, cs.z, cs.w};
-      const float ss[4] = {sn.x, sn.y, sn.z, sn.w};
+    const int sec = r % 3;
+    const int m = r / 3;
+    const int s = m % S, b = m / S;
+    const bf16_t* src = qkv + (size_t)m * (3 * nh * hd) + (sec * nh + h) * hd;
+    const u16x8 a = *reinterpret_cast<const u16x8*>(src + j);
+    const u16x8 c = *reinterpret_cast<const u16x8*>(src + half + j);
+    bf16_t* dst = (sec == 0 ? q : (sec == 1 ? k : v)) + ((size_t)(b * nh + h) * S + s) * hd;
+    u16x8 o1 = a, o2 = c;
+    if (sec != 2) {
+      const float* cp = cosT + s * half + j;
+      const float* sp = sinT + s * half + j;
+      const float4 c0 = *reinterpret_cast<const float4*>(cp), c1 = *reinterpret_cast<const float4*>(cp + 4);
+      const float4 s0 = *reinterpret_cast<const float4*>(sp), s1 = *reinterpret_cast<const float4*>(sp + 4);
+      const float cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      const float ss[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
+      for (int e = 0; e < 8; ++e) {
         const float x1 = bf2f(a.v[e]), x2 = bf2f(c.v[e]);
         o1.v[e] = f2bf(x1 * cc[e] - x2 * ss[e]);
         o2.v[e] = f2bf(x2 * cc[e] + x1 * ss[e]);
       }
     }
-    *reinterpret_cast<u16x4*>(dstbase + j) = o1;
-    *reinterpret_cast<u16x4*>(dstbase + half + j) = o2;
+    *reinterpret_cast<u16x8*>(dst + j) = o1;
+    *reinterpret_cast<u16x8*>(dst + half + j) = o2;
   }
 }
 
 // dq, dk, dv [B, nh, S, hd] -> dqkv [B*S, 3*nh*hd] (inverse rotation for dq, dk).
-// dq may be fp32 (dqf != nullptr, produced by the attention dQ kernel) or bf16.
+// dq may be fp32 (dqf != nullptr) or bf16.
 __global__ __launch_bounds__(256) void k_rope_qkv_bwd(const bf16_t* __restrict__ dq, const float* __restrict__ dqf,
                                                       const bf16_t* __restrict__ dk, const bf16_t* __restrict__ dv,
                                                       const float* __restrict__ cosT, const float* __restrict__ sinT,
                                                       bf16_t* __restrict__ dqkv, int B, int S, int nh, int hd) {
   const int half = hd >> 1;
-  const int per_head = half >> 2;
-  const size_t total = (size_t)B * S * 3 * nh * per_head;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    const int j4 = (int)(i % per_head);
-    size_t r = i / per_head;
-    const int h = (int)(r % nh);
+  const int cpr = half >> 3;
+  const int total = B * S * 3 * nh * cpr;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int j = (i % cpr) * 8;
+    int r = i / cpr;
+    const int h = r % nh;
     r /= nh;
-    const int sec = (int)(r % 3);
-    const size_t m = r / 3;
-    const int s = (int)(m % S);
-    const int b = (int)(m / S);
-    const int j = j4 * 4;
-    const size_t soff = (((size_t)b * nh + h) * S + s) * hd;
-    float g1[4], g2[4];
+    const int sec = r % 3;
+    const int m = r / 3;
+    const int s = m % S, b = m / S;
+    const size_t soff = ((size_t)(b * nh + h) * S + s) * hd;
+    float g1[8], g2[8];
     if (sec == 0 && dqf) {
-      const float4 a = *reinterpret_cast<const float4*>(dqf + soff + j);
-      const float4 c = *reinterpret_cast<const float4*>(dqf + soff + half + j);
-      g1[0] = a.x; g1[1] = a.y; g1[2] = a.z; g1[3] = a.w;
-      g2[0] = c.x; g2[1] = c.y; g2[2] = c.z; g2[3] = c.w;
+      const float* p = dqf + soff;
+#pragma unroll
+      for (int e = 0; e < 8; e += 4) {
+        const float4 a = *reinterpret_cast<const float4*>(p + j + e);
+        const float4 c = *reinterpret_cast<const float4*>(p + half + j + e);
+        g1[e] = a.x; g1[e + 1] = a.y; g1[e + 2] = a.z; g1[e + 3] = a.w;
+        g2[e] = c.x; g2[e + 1] = c.y; g2[e + 2] = c.z; g2[e + 3] = c.w;
+      }
     } else {
       const bf16_t* src = (sec == 0 ? dq : (sec == 1 ? dk : dv)) + soff;
-      const u16x4 a = *reinterpret_cast<const u16x4*>(src + j);
-      const u16x4 c = *reinterpret_cast<const u16x4*>(src + half + j);
+      const u16x8 a = *reinterpret_cast<const u16x8*>(src + j);
+      const u16x8 c = *reinterpret_cast<const u16x8*>(src + half + j);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) { g1[e] = bf2f(a.v[e]); g2[e] = bf2f(c.v[e]); }
+      for (int e = 0; e < 8; ++e) { g1[e] = bf2f(a.v[e]); g2[e] = bf2f(c.v[e]); }
     }
-    u16x4 o1, o2;
+    u16x8 o1, o2;
     if (sec == 2) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) { o1.v[e] = f2bf(g1[e]); o2.v[e] = f2bf(g2[e]); }
+      for (int e = 0; e < 8; ++e) { o1.v[e] = f2bf(g1[e]); o2.v[e] = f2bf(g2[e]); }
     } else {
-      const float4 cs = *reinterpret_cast<const float4*>(cosT + (size_t)s * half + j);
-      const float4 sn = *reinterpret_cast<const float4*>(sinT + (size_t)s * half + j);
-      const float cc[4] = {cs.x, cs.y, cs.z, cs.w};
-      const float ss[4] = {sn.x, sn.y, sn.z, sn.w};
+      const float* cp = cosT + s * half + j;
+      const float* sp = sinT + s * half + j;
+      const float4 c0 = *reinterpret_cast<const float4*>(cp), c1 = *reinterpret_cast<const float4*>(cp + 4);
+      const float4 s0 = *reinterpret_cast<const float4*>(sp), s1 = *reinterpret_cast<const float4*>(sp + 4);
+      const float cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      const float ss[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
+      for (int e = 0; e < 8; ++e) {
         o1.v[e] = f2bf(g1[e] * cc[e] + g2[e] * ss[e]);
         o2.v[e] = f2bf(g2[e] * cc[e] - g1[e] * ss[e]);
       }
     }
-    bf16_t* dst = dqkv + m * (size_t)(3 * nh * hd) + (size_t)sec * nh * hd + (size_t)h * hd;
-    *reinterpret_cast<u16x4*>(dst + j) = o1;
-    *reinterpret_cast<u16x4*>(dst + half + j) = o2;
+    bf16_t* dst = dqkv + (size_t)m * (3 * nh * hd) + (sec * nh + h) * hd;
+    *reinterpret_cast<u16x8*>(dst + j) = o1;
+    *reinterpret_cast<u16x8*>(dst + half + j) = o2;
   }
 }
 
@@ -160,8 +165,8 @@ static inline int ew_blocks(size_t total) {
 
 DLT_API int dlt_rope_qkv_fwd(const bf16_t* qkv, const float* cosT, const float* sinT, bf16_t* q, bf16_t* k,
                              bf16_t* v, int B, int S, int nh, int hd, hipStream_t st) {
-  if (hd % 8) return -1;
-  const size_t total = (size_t)B * S * 3 * nh * (hd / 8);
+  if (hd % 16 || (long)B * S * 3 * nh * hd >= (1L << 31)) return -1;
+  const size_t total = (size_t)B * S * 3 * nh * (hd / 16);
   k_rope_qkv_fwd<<<ew_blocks(total), 256, 0, st>>>(qkv, cosT, sinT, q, k, v, B, S, nh, hd);
   DLT_CHECK_LAUNCH();
 }
@@ -169,8 +174,8 @@ DLT_API int dlt_rope_qkv_fwd(const bf16_t* qkv, const float* cosT, const float* 
 DLT_API int dlt_rope_qkv_bwd(const bf16_t* dq, const float* dqf, const bf16_t* dk, const bf16_t* dv,
                              const float* cosT, const float* sinT, bf16_t* dqkv, int B, int S, int nh, int hd,
                              hipStream_t st) {
-  if (hd % 8) return -1;
-  const size_t total = (size_t)B * S * 3 * nh * (hd / 8);
+  if (hd % 16 || (long)B * S * 3 * nh * hd >= (1L << 31)) return -1;
+  const size_t total = (size_t)B * S * 3 * nh * (hd / 16);
   k_rope_qkv_bwd<<<ew_blocks(total), 256, 0, st>>>(dq, dqf, dk, dv, cosT, sinT, dqkv, B, S, nh, hd);
   DLT_CHECK_LAUNCH();
 }
