@@ -59,11 +59,8 @@ __global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, const floa
                                                float inv_bc2_sqrt, const float* __restrict__ gscale_ptr) {
   const float gs = gscale_ptr ? gscale_ptr[1] : 1.f;
   const int64_t n4 = n >> 2;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-    float4 pp = reinterpret_cast<float4*>(p)[i];
-    const float4 gg = reinterpret_cast<const float4*>(g)[i];
-    float4 mm = reinterpret_cast<float4*>(m)[i];
-    float4 vv = reinterpret_cast<float4*>(v)[i];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  auto upd = [&](int64_t i, float4 pp, float4 gg, float4 mm, float4 vv) {
     adam_elem(pp.x, gg.x * gs, mm.x, vv.x, lr, b1, b2, eps, wd, step_size, inv_bc2_sqrt);
     adam_elem(pp.y, gg.y * gs, mm.y, vv.y, lr, b1, b2, eps, wd, step_size, inv_bc2_sqrt);
     adam_elem(pp.z, gg.z * gs, mm.z, vv.z, lr, b1, b2, eps, wd, step_size, inv_bc2_sqrt);
@@ -76,7 +73,21 @@ __global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, const floa
       s.v[0] = f2bf(pp.x); s.v[1] = f2bf(pp.y); s.v[2] = f2bf(pp.z); s.v[3] = f2bf(pp.w);
       reinterpret_cast<u16x4*>(shadow)[i] = s;
     }
+  };
+  // two independent float4 groups per iteration: 8 loads in flight per thread
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  for (; i + stride < n4; i += 2 * stride) {
+    const int64_t j = i + stride;
+    const float4 p0 = reinterpret_cast<const float4*>(p)[i], p1 = reinterpret_cast<const float4*>(p)[j];
+    const float4 g0 = reinterpret_cast<const float4*>(g)[i], g1 = reinterpret_cast<const float4*>(g)[j];
+    const float4 m0 = reinterpret_cast<const float4*>(m)[i], m1 = reinterpret_cast<const float4*>(m)[j];
+    const float4 v0 = reinterpret_cast<const float4*>(v)[i], v1 = reinterpret_cast<const float4*>(v)[j];
+    upd(i, p0, g0, m0, v0);
+    upd(j, p1, g1, m1, v1);
   }
+  if (i < n4)
+    upd(i, reinterpret_cast<const float4*>(p)[i], reinterpret_cast<const float4*>(g)[i],
+        reinterpret_cast<const float4*>(m)[i], reinterpret_cast<const float4*>(v)[i]);
   if (blockIdx.x == 0) {
     for (int64_t i = (n4 << 2) + threadIdx.x; i < n; i += blockDim.x) {
       float pp = p[i], mm = m[i], vv = v[i];
