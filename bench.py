@@ -41,11 +41,15 @@ def main():
     ap.add_argument("--mode", default="ddp", choices=["ddp", "fsdp"])
     ap.add_argument("--sharding", default="FULL_SHARD")
     ap.add_argument("--no_ac", action="store_true", help="FSDP: disable activation checkpointing")
+    ap.add_argument("--dropout", type=float, default=None,
+                    help="ablation only: override dropout/attention_dropout (reference config: 0.1)")
     args = ap.parse_args()
 
     from distributed_llm_trainer_amd.models.config import GPTConfig
     cfg = GPTConfig.from_preset(args.model_size)
     cfg.max_seq_len = args.seq_len
+    if args.dropout is not None:
+        cfg.dropout = cfg.attention_dropout = args.dropout
     if args.mode == "ddp":
         from distributed_llm_trainer_amd.training.configs import TrainingConfig
         from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer

@@ -295,7 +295,10 @@ class GPTEngine:
         loss, logits = None, None
         V, Vp = self.cfg.vocab_size, hw.lm_head.shape[0]
         if targets is not None:
-            lg = self.gemm.linear(nf, hw.lm_head)           # [M, Vp]
+            # [M, Vp]; with deferred weight gradients the logits (-> dlogits) of every
+            # micro-step of the window stay resident for ONE lm_head wgrad GEMM
+            lg_out = self._slot_buf(st, "head", "lg", B * S, Vp, nf.device)[0] if st.defer else None
+            lg = self.gemm.linear(nf, hw.lm_head, out=lg_out)
             n_valid = (targets != -100).sum()
             row_loss = self.ops.cross_entropy_fwd_bwd(lg, targets, V, n_valid)
             loss = row_loss.sum() / n_valid.clamp(min=1).float()
@@ -332,14 +335,40 @@ class GPTEngine:
 
         prov.pre_backward("head")
         hw, hg = prov.head(), prov.head_grads()
+        M, H, I = B * S, cfg.hidden_size, cfg.intermediate_size
+        dev = st.dlogits.device
+        do_wgrad = (not st.defer) or st.last
+        side = self._wgrad_stream(dev) if (do_wgrad and st.defer) else None
         # lm_head: dnf = dlogits @ E ; dE += dlogits^T @ (nf * dloss)
         dnf = gm.linear_dgrad(st.dlogits, hw.lm_head)
-        nf_scaled = ops.scale_bf16(st.nf, dloss) if st.nf.dtype == torch.bfloat16 else st.nf * dloss
-        gm.wgrad_acc(hg.embed, st.dlogits, nf_scaled)
+        nf_out = self._slot_buf(st, "head", "nf", M, H, dev)[0] if st.defer else None
+        if st.nf.dtype == torch.bfloat16:
+            nf_scaled = ops.scale_bf16(st.nf, dloss, out=nf_out)
+        else:
+            nf_scaled = st.nf * dloss
+            if nf_out is not None:
+                nf_scaled = nf_out.copy_(nf_scaled)
+        head_ev = None
+        if not st.defer:
+            gm.wgrad_acc(hg.embed, st.dlogits, nf_scaled)
+        elif st.last:
+            # ONE [Vp, H] wgrad GEMM over all GA*M rows of the window (K = 32768 instead
+            # of 4 x 8192), on the weight-gradient stream so it overlaps the layer
+            # backward; the embedding scatter-add below (same buffer) waits for it.
+            lg_all = self._slot_buf(st, "head", "lg", M, hw.lm_head.shape[0], dev)[1]
+            nf_all = self._slot_buf(st, "head", "nf", M, H, dev)[1]
+            if side is not None:
+                ev = torch.cuda.Event()
+                ev.record()
+                side.wait_event(ev)
+                with torch.cuda.stream(side):
+                    gm.wgrad_acc(hg.embed, lg_all, nf_all)
+                    head_ev = torch.cuda.Event()
+                    head_ev.record()
+            else:
+                gm.wgrad_acc(hg.embed, lg_all, nf_all)
         st.dlogits = None
         key_last = self._keys(st.micro, L - 1)[2]
-        M, H, I = B * S, cfg.hidden_size, cfg.intermediate_size
-        dev = dnf.device
 
         def sb(layer, name, n):
             return self._slot_buf(st, layer, name, M, n, dev)[0] if st.defer else None
@@ -351,8 +380,6 @@ class GPTEngine:
                                     ph, key_last, dy_scale=dloss, want_ddelta=True, ddelta_out=sb(L - 1, "dd", H))
         del dnf
         cos, sin = self.rope(S, g_x2.device)
-        do_wgrad = (not st.defer) or st.last
-        side = self._wgrad_stream(dev) if (do_wgrad and st.defer) else None
 
         for i in reversed(range(L)):
             prov.pre_backward(i)
@@ -415,6 +442,8 @@ class GPTEngine:
                 if side_ctx is not None:
                     side_ctx.__exit__(None, None, None)
         # embedding (tied with lm_head): scatter-add
+        if head_ev is not None:
+            torch.cuda.current_stream().wait_event(head_ev)
         ops.embedding_bwd(st.ids, g_x2, hg.embed)
         prov.post_backward("head")
         if side is not None and do_wgrad and st.defer:
@@ -437,7 +466,9 @@ class _TorchGemm:
         self._fp32_out_ok = None
 
     @staticmethod
-    def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
+        if out is not None:
+            return torch.matmul(x, w.t(), out=out)
         return torch.matmul(x, w.t())
 
     @staticmethod

@@ -127,10 +127,12 @@ class HipGemm:
         self._choice[key] = choice
         return choice
 
-    def linear(self, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    def linear(self, x: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
         M, K = x.shape
         N = w.shape[0]
-        y = torch.empty(M, N, dtype=x.dtype, device=x.device)
+        if out is not None and (out.shape != (M, N) or not out.is_contiguous() or out.dtype != x.dtype):
+            raise ValueError("linear: out must be a contiguous [M, N] tensor of the input dtype")
+        y = torch.empty(M, N, dtype=x.dtype, device=x.device) if out is None else out
         cfg = self._pick(x, w, y)
         if cfg is not None:
             from . import hip

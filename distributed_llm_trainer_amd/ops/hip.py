@@ -46,6 +46,7 @@ _SIGS = {
     "dlt_wgrad_gemm": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
     "dlt_scale_bf16": [c_void_p, c_void_p, ctypes.c_long, c_void_p, c_void_p],
     "dlt_gemm_tn": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "dlt_gemm_tn8": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "dlt_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                      c_uint32, c_uint32, c_float, c_int, c_void_p],
     "dlt_attn_dropout_mask": [c_void_p, c_int, c_int, c_int, c_uint32, c_uint32, c_void_p],
@@ -375,32 +376,39 @@ def wgrad_gemm(dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, splits: int 
 
 
 # ------------------------------------------------------------------ TN GEMM
-GEMM_TN_TILES = {0: (256, 256), 1: (256, 128), 2: (128, 128), 3: (128, 64), 4: (64, 128)}
+GEMM_TN_TILES = {0: (256, 256), 1: (256, 128), 2: (128, 128), 3: (128, 64), 4: (64, 128),
+                 5: (256, 256)}  # 5 = the 8-phase pipelined kernel (csrc/gemm_tn8.hip), K % 128
 
 
 def gemm_tn(a: torch.Tensor, b: torch.Tensor, cfg: int, out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
     """C[M,N] = A[M,K] @ B[N,K]^T (bf16, fp32 accumulate) with the hand-written MFMA
-    kernel (``csrc/gemm_tn.hip``) in tile configuration ``cfg``.  Returns None (nothing
-    launched) when the shape does not tile for that configuration."""
+    kernel (``csrc/gemm_tn.hip``, or ``csrc/gemm_tn8.hip`` for cfg 5) in tile
+    configuration ``cfg``.  Returns None (nothing launched) when the shape does not tile
+    for that configuration."""
     M, K = a.shape
     N = b.shape[0]
     bm, bn = GEMM_TN_TILES[cfg]
-    if M % bm or N % bn or K % 64 or b.shape[1] != K:
+    if M % bm or N % bn or K % (128 if cfg == 5 else 64) or b.shape[1] != K:
         return None
     _req(a, torch.bfloat16, "gemm_tn.a")
     _req(b, torch.bfloat16, "gemm_tn.b")
     c = torch.empty(M, N, dtype=torch.bfloat16, device=a.device) if out is None else out
     _req(c, torch.bfloat16, "gemm_tn.c", M * N)
-    _chk(lib().dlt_gemm_tn(_p(a), _p(b), _p(c), M, N, K, K, K, N, cfg, _stream()), "gemm_tn")
+    if cfg == 5:
+        _chk(lib().dlt_gemm_tn8(_p(a), _p(b), _p(c), M, N, K, K, K, N, _stream()), "gemm_tn8")
+    else:
+        _chk(lib().dlt_gemm_tn(_p(a), _p(b), _p(c), M, N, K, K, K, N, cfg, _stream()), "gemm_tn")
     return c
 
 
-def scale_bf16(x: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
+def scale_bf16(x: torch.Tensor, scale: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = x * scale with a device scalar (no host sync); falls back for odd sizes."""
     _req(x, torch.bfloat16, "scale_bf16.x")
     s = scale.reshape(1).float().contiguous()
     if x.numel() % 8:
-        return (x.float() * s).to(torch.bfloat16)
-    y = torch.empty_like(x)
+        y = (x.float() * s).to(torch.bfloat16)
+        return y if out is None else out.copy_(y)
+    y = torch.empty_like(x) if out is None else out
+    _req(y, torch.bfloat16, "scale_bf16.out", x.numel())
     _chk(lib().dlt_scale_bf16(_p(x), _p(y), x.numel(), _p(s), _stream()), "scale_bf16")
     return y

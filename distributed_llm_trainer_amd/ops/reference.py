@@ -256,6 +256,7 @@ def sumsq(x: torch.Tensor, out: torch.Tensor) -> None:
     out += x.float().pow(2).sum()
 
 
-def scale_bf16(x: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
+def scale_bf16(x: torch.Tensor, scale: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
     """y = x * scale (scale: 0-d/1-element device tensor), result in x's dtype."""
-    return (x.float() * scale.reshape(()).float()).to(x.dtype)
+    y = (x.float() * scale.reshape(()).float()).to(x.dtype)
+    return y if out is None else out.copy_(y)

@@ -62,8 +62,20 @@ def main(path, micro=4):
         names[n[:90]][0] += d
         names[n[:90]][1] += 1
     span = (t1 - t0) / 1e3
+    # union of kernel intervals: time with >= 1 kernel running (rest = GPU idle)
+    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in step)
+    union, cs, ce = 0, iv[0][0], iv[0][1]
+    for a, b in iv[1:]:
+        if a > ce:
+            union += ce - cs
+            cs, ce = a, b
+        else:
+            ce = max(ce, b)
+    union += ce - cs
     print(f"Last optimizer step: span {span / 1e3:.2f} ms, kernel-busy {busy / 1e3:.2f} ms "
           f"({100 * busy / span:.1f}% busy), {len(step)} kernels; per micro-step ({micro}): {busy / 1e3 / micro:.2f} ms")
+    print(f"GPU occupied (>=1 kernel running) {union / 1e6:.2f} ms = {100 * union / 1e3 / span:.1f}% of the span; "
+          f"idle {span / 1e3 - union / 1e6:.2f} ms")
     print()
     print("| category | ms/step | % | launches |")
     print("|---|---:|---:|---:|")
