@@ -13,8 +13,9 @@ autocast path):
 
   fwd:  x,n1   = add_dropout_rmsnorm(r, d_prev)        [fused kernel]
         qkv    = n1 @ Wqkv^T                             [GEMM, N = 3H]
-        q,k,v  = rope_split(qkv)                         [fused kernel]
-        o,lse  = flash_attention(q,k,v; causal, dropout) [MFMA kernel]
+        qkv    = rope_qk(qkv)  (q, k rotated in place)   [fused kernel]
+        o,lse  = flash_attention(qkv; causal, dropout)   [MFMA kernel, reads the packed
+                                                          [M, 3H] GEMM output directly]
         a      = o @ Wo^T                                [GEMM]
         x2,n2  = add_dropout_rmsnorm(x, a)               [fused kernel]
         gu     = n2 @ Wgu^T                              [GEMM, N = 2I]
@@ -22,11 +23,23 @@ autocast path):
         d      = s @ Wdown^T                             [GEMM]  -> (x2, d) to next layer
   head: xf,nf  = add_dropout_rmsnorm(x2, d); logits = nf @ E^T; CE + dlogits in place.
 
+  The attention backward writes dq/dk/dv straight into the packed [M, 3H] gradient
+  with the inverse RoPE rotation applied in its epilogue (no repack kernel).
+
 Dropout masks are pure functions of (seed, micro-step, layer, site, index)
 (``ops/rng.py``), so activation checkpointing just re-runs the layer forward.
+
+Micro-step pipelining (:meth:`GPTEngine.train_window`): within a gradient-accumulation
+window the forward of micro-step k+1 does not depend on the backward of micro-step k
+(weights only change at the optimizer step), so the two are issued block by block on
+two HIP streams and the GPU overlaps them -- the small-N GEMMs, the 1.5-waves/SIMD
+attention grid and the memory-bound norm/SwiGLU kernels of one chain fill the CUs the
+other leaves idle.  The reference runs the micro-steps strictly one after the other
+(``ddp_trainer.py:322-345``).
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 from dataclasses import dataclass, field
@@ -35,6 +48,15 @@ from typing import Any, Callable, Dict, List, Optional
 import torch
 
 from ..ops import rng
+
+
+def _drain(gen):
+    """Run a generator to completion and return its return value."""
+    while True:
+        try:
+            next(gen)
+        except StopIteration as stop:
+            return stop.value
 
 
 @dataclass
@@ -107,7 +129,7 @@ class _LayerCache:
     x: torch.Tensor
     rstd1: Any = None
     n1: Any = None
-    q: Any = None
+    q: Any = None      # packed path: the roped [M, 3H] qkv (k, v = None)
     k: Any = None
     v: Any = None
     o: Any = None
@@ -158,6 +180,11 @@ class GPTEngine:
         self._slots = {}
         self._side = None  # weight-gradient side stream (lazily created)
         self._mask_side = None  # attention keep-bit side stream
+        self._pipe = None  # second compute stream of train_window
+        # attention straight on the packed [M, 3H] QKV GEMM output (RoPE in place,
+        # inverse RoPE in the backward epilogue); DLT_PACKED_QKV=0 -> split q/k/v copies
+        self.packed_qkv = (hasattr(ops, "attention_fwd_packed")
+                           and os.environ.get("DLT_PACKED_QKV", "1") != "0")
 
     # ------------------------------------------------------- grad accumulation
     def set_accumulation(self, slot: int, n_slots: int, defer: bool = True) -> None:
@@ -178,11 +205,17 @@ class GPTEngine:
         key = (layer, name)
         buf = self._slots.get(key)
         if buf is None or buf.shape != (self.acc_slots * M, N) or buf.device != device:
+            if buf is not None and buf.is_cuda:
+                # slot buffers are shared by the compute, pipeline and weight-gradient
+                # streams without record_stream: retire every user before reuse
+                torch.cuda.synchronize(buf.device)
             buf = torch.empty(self.acc_slots * M, N, dtype=self.act_dtype, device=device)
             self._slots[key] = buf
         return buf[st.slot * M:(st.slot + 1) * M], buf
 
     def release_slots(self) -> None:
+        if any(b.is_cuda for b in self._slots.values()):
+            torch.cuda.synchronize()
         self._slots.clear()
 
     # ---------------------------------------------------------------- helpers
@@ -236,13 +269,17 @@ class GPTEngine:
         x, n1, rstd1 = ops.add_dropout_rmsnorm_fwd(r, d, w.ln1, self.eps, p_d, key_d, self.act_dtype,
                                                    y_out=sb("n1", H))
         qkv = gm.linear(n1, w.wqkv)
-        q, k, v = ops.rope_qkv_fwd(qkv, B, S, cfg.num_heads, cos, sin)
-        del qkv
         if mask is not None:
             torch.cuda.current_stream().wait_event(mask_ev)
-            o, lse = ops.attention_fwd(q, k, v, pa, k_attn, True, out=sb("o", H), mask=mask)
+        if self.packed_qkv:
+            ops.rope_qk_inplace(qkv, B, S, cfg.num_heads, cos, sin)
+            o, lse = ops.attention_fwd_packed(qkv, B, S, cfg.num_heads, pa, k_attn, out=sb("o", H), mask=mask)
+            q, k, v = qkv, None, None
         else:
-            o, lse = ops.attention_fwd(q, k, v, pa, k_attn, True, out=sb("o", H))
+            q, k, v = ops.rope_qkv_fwd(qkv, B, S, cfg.num_heads, cos, sin)
+            kw = {"mask": mask} if mask is not None else {}
+            o, lse = ops.attention_fwd(q, k, v, pa, k_attn, True, out=sb("o", H), **kw)
+        del qkv
         a = gm.linear(o, w.wo)
         x2, n2, rstd2 = ops.add_dropout_rmsnorm_fwd(x, a, w.ln2, self.eps, ph, k_resid, self.act_dtype,
                                                     y_out=sb("n2", H))
@@ -261,6 +298,14 @@ class GPTEngine:
                 recompute: bool = False, return_logits: bool = False,
                 need_backward: Optional[bool] = None):
         """Returns (loss or None, logits or None, state for backward or None)."""
+        return _drain(self._forward_gen(ids, targets, train, recompute, return_logits, need_backward))
+
+    def _forward_gen(self, ids, targets, train, recompute=False, return_logits=False, need_backward=None,
+                     acc=None):
+        """Generator form of :meth:`forward`: yields after every block so the window
+        scheduler (:meth:`train_window`) can interleave it with another micro-step's
+        backward; the return value is forward's tuple.  ``acc`` = (slot, n_slots,
+        defer) overrides the engine-global accumulation state."""
         B, S = ids.shape
         if need_backward is None:
             need_backward = torch.is_grad_enabled()
@@ -271,8 +316,9 @@ class GPTEngine:
         else:
             micro = 0
         st = _StepState(ids=ids, B=B, S=S, micro=micro, train=train, recompute=recompute)
-        if need_bwd and self.defer:
-            st.slot, st.defer, st.last = self.acc_slot, True, self.acc_slot == self.acc_slots - 1
+        slot, n_slots, defer = acc if acc is not None else (self.acc_slot, self.acc_slots, self.defer)
+        if need_bwd and defer and n_slots > 1:
+            st.slot, st.defer, st.last = slot, True, slot == n_slots - 1
         prov = self.provider
         ph = self.p_hidden if train else 0.0
 
@@ -289,6 +335,7 @@ class GPTEngine:
             prov.post_forward(i)
             r, d = r_new, d_new
             key_d, p_d = self._keys(micro, i)[2], ph
+            yield
         hw = prov.head()
         xf, nf, rstdf = self.ops.add_dropout_rmsnorm_fwd(r, d, hw.norm, self.eps, p_d, key_d, self.act_dtype)
         st.d_last = None
@@ -326,6 +373,10 @@ class GPTEngine:
         return self._side
 
     def backward(self, st: _StepState, dloss: torch.Tensor) -> None:
+        _drain(self._backward_gen(st, dloss))
+
+    def _backward_gen(self, st: _StepState, dloss: torch.Tensor):
+        """Generator form of :meth:`backward` (yields after every block)."""
         ops, gm, cfg, prov = self.ops, self.gemm, self.cfg, self.provider
         B, S = st.B, st.S
         L = cfg.num_layers
@@ -399,10 +450,15 @@ class GPTEngine:
             del dn2
             # attention
             do = gm.linear_dgrad(da, w.wo)
-            dq, dk, dv = ops.attention_bwd(c.q, c.k, c.v, c.o, do, c.lse, pa, k_attn, True)
-            del do
-            dqkv = ops.rope_qkv_bwd(dq, dk, dv, cos, sin, out=sb(i, "dqkv", 3 * H))
-            del dq, dk, dv
+            if c.k is None:  # packed: dq/dk/dv land in [M, 3H] with the inverse RoPE applied
+                dqkv = ops.attention_bwd_packed(c.q, c.o, do, c.lse, pa, k_attn, B, S, cfg.num_heads, cos, sin,
+                                                out=sb(i, "dqkv", 3 * H))
+                del do
+            else:
+                dq, dk, dv = ops.attention_bwd(c.q, c.k, c.v, c.o, do, c.lse, pa, k_attn, True)
+                del do
+                dqkv = ops.rope_qkv_bwd(dq, dk, dv, cos, sin, out=sb(i, "dqkv", 3 * H))
+                del dq, dk, dv
             dn1 = gm.linear_dgrad(dqkv, w.wqkv)
             key_prev = self._keys(st.micro, i - 1)[2] if i > 0 else 0
             p_prev = ph if i > 0 else 0.0
@@ -441,6 +497,7 @@ class GPTEngine:
             finally:
                 if side_ctx is not None:
                     side_ctx.__exit__(None, None, None)
+            yield
         # embedding (tied with lm_head): scatter-add
         if head_ev is not None:
             torch.cuda.current_stream().wait_event(head_ev)
@@ -448,6 +505,77 @@ class GPTEngine:
         prov.post_backward("head")
         if side is not None and do_wgrad and st.defer:
             torch.cuda.current_stream().wait_stream(side)
+
+    # ------------------------------------------------------ pipelined window
+    def train_window(self, micro_ids: List[torch.Tensor], micro_targets: List[torch.Tensor],
+                     dloss: torch.Tensor, recompute: bool = False,
+                     before_last: Optional[Callable[[], None]] = None) -> List[torch.Tensor]:
+        """Forward + backward of a whole gradient-accumulation window.
+
+        Schedule (GA = 4):  F0 | B0+F1 | B1+F2 | B2+F3 | B3, where "Bk+Fk+1" issues the
+        blocks of the two chains alternately, micro-step k on stream ``k % 2`` (the
+        current stream and one pipeline stream).  A micro-step's forward and backward
+        run on the same stream, so its activations never cross streams; what is shared
+        (weights, slot buffers, RoPE tables, the ids) is read-only until the window
+        ends or is produced before the fork.  The last backward first joins the other
+        stream: its lm_head weight-gradient GEMM (beta = 1) and the DDP bucket
+        all-reduces must see every micro-step's gradient.  Weight gradients are
+        deferred (one GEMM per weight over the window), so before that point the
+        chains only add into gradients with atomics (norm weights, embedding rows).
+
+        ``dloss`` is d(total)/d(micro-step loss) (1/GA), ``before_last`` runs before
+        the last backward is issued (the DDP runtime switches its sync on there).
+        Returns the GA micro-step losses (device scalars, unscaled).  Dropout streams,
+        numerics and gradients are identical to running the micro-steps one by one.
+        """
+        GA = len(micro_ids)
+        dev = micro_ids[0].device
+        cuda = dev.type == "cuda"
+        self.set_accumulation(0, GA, defer=True)
+        streams = [None, None]
+        main = None
+        if cuda:
+            main = torch.cuda.current_stream(dev)
+            if self._pipe is None:
+                self._pipe = torch.cuda.Stream(dev)
+            streams = [main, self._pipe]
+            self.rope(micro_ids[0].shape[1], dev)  # lazily-built shared state: before the fork
+            self._pipe.wait_stream(main)
+
+        def on(k):
+            return torch.cuda.stream(streams[k % 2]) if cuda else contextlib.nullcontext()
+
+        def fwd(k):
+            return self._forward_gen(micro_ids[k], micro_targets[k], True, recompute, need_backward=True,
+                                     acc=(k, GA, True))
+
+        losses: List[Any] = [None] * GA
+        states: List[Any] = [None] * GA
+        with on(0):
+            losses[0], _, states[0] = _drain(fwd(0))
+        for k in range(GA):
+            if k == GA - 1:
+                if cuda and GA > 1:
+                    streams[k % 2].wait_stream(streams[(k + 1) % 2])
+                if before_last is not None:
+                    before_last()
+            running = [(k, self._backward_gen(states[k], dloss), False)]
+            states[k] = None
+            if k + 1 < GA:
+                running.append((k + 1, fwd(k + 1), True))
+            while running:
+                for item in list(running):
+                    j, gen, is_fwd = item
+                    with on(j):
+                        try:
+                            next(gen)
+                        except StopIteration as stop:
+                            running.remove(item)
+                            if is_fwd:
+                                losses[j], _, states[j] = stop.value
+        if cuda and GA > 1:
+            main.wait_stream(self._pipe)
+        return losses
 
 
 class _TorchGemm:

@@ -15,7 +15,8 @@ from . import reference, rng
 
 _FUNCS = ("rope_tables", "embedding_fwd", "embedding_bwd", "add_dropout_rmsnorm_fwd", "rmsnorm_bwd",
           "rope_qkv_fwd", "rope_qkv_bwd", "attention_fwd", "attention_bwd", "swiglu_fwd", "swiglu_bwd",
-          "cross_entropy_fwd_bwd", "scale_bf16")
+          "cross_entropy_fwd_bwd", "scale_bf16", "rope_qk_inplace", "attention_fwd_packed",
+          "attention_bwd_packed")
 
 
 def _namespace(mod, name):

@@ -27,8 +27,9 @@
 //    then dK/dV (accumulated in registers) -- no fp32 atomics anywhere.  Causal
 //    tile skipping; workgroups process paired items of equal total length.
 //
-// Layouts: q, k, v, dq, dk, dv: [B*nh, S, 64] bf16;  o, do: [B, S, nh, 64] bf16
-// (= the [M, H] GEMM layout);  lse, delta: [B*nh, S] fp32 (natural-log lse).
+// Layouts: q, k, v, dq, dk, dv: strided views -- head-major [B*nh, S, 64] or the
+// packed [B*S, 3, nh, 64] QKV GEMM output (see dlt_attn_fwd_ex); o, do: [B, S, nh, 64]
+// bf16 (= the [M, H] GEMM layout);  lse, delta: [B*nh, S] fp32 (natural-log lse).
 #include "common.h"
 
 #include <type_traits>
@@ -335,7 +336,8 @@ template <bool DROP>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_attn_fwd(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
                                                     const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
                                                     float* __restrict__ lse, const uint32_t* __restrict__ mask,
-                                                    int S, int nh, float c_log2, float dscale) {
+                                                    int S, int nh, float c_log2, float dscale, long in_bs,
+                                                    int in_hs, int in_rs) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * 2 * KVB * HD];  // [buf][K|V][64][64]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -343,7 +345,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const int nrb = (S + RB - 1) / RB;
   const int bh = blockIdx.y;
   const int b = bh / nh, head = bh % nh;
-  const size_t hoff = (size_t)bh * S * HD;
+  const size_t hin = (size_t)b * in_bs + (size_t)head * in_hs;  // (b, head) base of q / k / v
   const int W = (S + 31) >> 5;
   using B0 = std::integral_constant<int, 0>;
   using B1 = std::integral_constant<int, 1>;
@@ -360,7 +362,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 
     bf16x8_t qf[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) qf[s] = load_row8(q + hoff + (size_t)min(qa, S - 1) * HD + 16 * s + 8 * h, qa < S);
+    for (int s = 0; s < 4; ++s) qf[s] = load_row8(q + hin + (size_t)min(qa, S - 1) * in_rs + 16 * s + 8 * h, qa < S);
 
     FwdState fs;
     fs.o[0] = zero16();
@@ -369,8 +371,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     fs.l = 0.f;
 
     const int nkv = (min(S, qb * RB + RB) + KVB - 1) / KVB;  // = qb + 1 except at a ragged end
-    glds_tile(k + hoff, 0, S, HD, lds, wid, lane);
-    glds_tile(v + hoff, 0, S, HD, lds + KVB * HD, wid, lane);
+    glds_tile(k + hin, 0, S, in_rs, lds, wid, lane);
+    glds_tile(v + hin, 0, S, in_rs, lds + KVB * HD, wid, lane);
     __syncthreads();
 
     // One K/V tile per step.  BUF is a compile-time LDS buffer index and MASKED a
@@ -385,8 +387,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       const bool more = kb + 1 < nkv;
       if (more) {  // next tile straight into the other buffer (read by nobody since the last barrier)
         bf16_t* Kn = lds + (BUF ^ 1) * 2 * KVB * HD;
-        glds_tile(k + hoff, (kb + 1) * KVB, S, HD, Kn, wid, lane);
-        glds_tile(v + hoff, (kb + 1) * KVB, S, HD, Kn + KVB * HD, wid, lane);
+        glds_tile(k + hin, (kb + 1) * KVB, S, in_rs, Kn, wid, lane);
+        glds_tile(v + hin, (kb + 1) * KVB, S, in_rs, Kn + KVB * HD, wid, lane);
         if (DROP) mw_next = make_uint2(mrow[2 * (kb + 1)], 2 * (kb + 1) + 1 < W ? mrow[2 * (kb + 1) + 1] : 0u);
       }
       const bf16_t* Kt = lds + BUF * 2 * KVB * HD;
@@ -431,6 +433,39 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 }
 
 // ============================================================================ backward
+// Store one head row held in accumulators (element 4g+e of acc[dt] is dim
+// 32*dt + 8*g + 4*h + e) times `sc`.  With RoPE tables the inverse NeoX rotation of
+// position `pos` is applied first: the partner of dim j < 32 is j + 32, i.e. the same
+// register of the other dt -- the rotation needs no data exchange.  (Replaces the
+// separate repack kernel that read dq/dk back and wrote the packed [M, 3H] gradient.)
+__device__ __forceinline__ void store_head_row(bf16_t* __restrict__ dst, const floatx16_t (&a)[2], float sc, int h,
+                                               const float* __restrict__ cosT, const float* __restrict__ sinT,
+                                               int pos) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    u16x4 w0, w1;
+    if (cosT) {
+      const float4 c4 = *reinterpret_cast<const float4*>(cosT + pos * (HD / 2) + 8 * g + 4 * h);
+      const float4 s4 = *reinterpret_cast<const float4*>(sinT + pos * (HD / 2) + 8 * g + 4 * h);
+      const float cc[4] = {c4.x, c4.y, c4.z, c4.w}, ss[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float x1 = a[0][4 * g + e] * sc, x2 = a[1][4 * g + e] * sc;
+        w0.v[e] = f2bf(fmaf(x1, cc[e], x2 * ss[e]));
+        w1.v[e] = f2bf(fmaf(x2, cc[e], -x1 * ss[e]));
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        w0.v[e] = f2bf(a[0][4 * g + e] * sc);
+        w1.v[e] = f2bf(a[1][4 * g + e] * sc);
+      }
+    }
+    *reinterpret_cast<u16x4*>(dst + 8 * g + 4 * h) = w0;
+    *reinterpret_cast<u16x4*>(dst + 32 + 8 * g + 4 * h) = w1;
+  }
+}
+
 // ---------------------------------------------------------------- dK / dV
 // One workgroup per 128 keys (32 per wave); sweep query tiles of 64 (two 32-row
 // sub-tiles).  Accumulators: S and dP with queries in registers, keys on lanes.
@@ -494,7 +529,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
                                                          const float* __restrict__ delta,
                                                          const uint32_t* __restrict__ maskT, bf16_t* __restrict__ dk,
                                                          bf16_t* __restrict__ dv, int S, int nh, float c_log2,
-                                                         float scale, float dscale) {
+                                                         float scale, float dscale, long in_bs, int in_hs, int in_rs,
+                                                         long out_bs, int out_hs, int out_rs,
+                                                         const float* __restrict__ cosT,
+                                                         const float* __restrict__ sinT) {
   // one LDS object (avoids hipcc's extra vmcnt waits with several __shared__ arrays)
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * QSTEP * HD * 2 + 2 * 2 * QSTEP * 4];
   bf16_t* lds = reinterpret_cast<bf16_t*>(smem);                              // [buf][Q|dO][64][64]
@@ -505,7 +543,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const int nrb = (S + RB - 1) / RB;
   const int bh = blockIdx.y;
   const int b = bh / nh, head = bh % nh;
-  const size_t hoff = (size_t)bh * S * HD;
+  const size_t hin = (size_t)b * in_bs + (size_t)head * in_hs;     // q / k / v
+  const size_t hout = (size_t)b * out_bs + (size_t)head * out_hs;  // dk / dv
   const int rstride = nh * HD;
   const int W = (S + 31) >> 5;
   const int nqt = (S + QSTEP - 1) / QSTEP;
@@ -526,8 +565,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     const int kc = min(ka, S - 1);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      kf[s] = load_row8(k + hoff + (size_t)kc * HD + 16 * s + 8 * h, ka < S);
-      vf[s] = load_row8(v + hoff + (size_t)kc * HD + 16 * s + 8 * h, ka < S);
+      kf[s] = load_row8(k + hin + (size_t)kc * in_rs + 16 * s + 8 * h, ka < S);
+      vf[s] = load_row8(v + hin + (size_t)kc * in_rs + 16 * s + 8 * h, ka < S);
     }
     floatx16_t dka[2] = {zero16(), zero16()}, dva[2] = {zero16(), zero16()};
 
@@ -535,7 +574,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     float rl = 0.f, rd = 0.f;
     uint2 mw_cur = make_uint2(0u, 0u), mw_next = make_uint2(0u, 0u);
     auto load_rows = [&](int t, int buf) {  // Q / dO tiles by LDS-DMA, row stats via registers
-      glds_tile(q + hoff, t * QSTEP, S, HD, lds + buf * 2 * QSTEP * HD, wid, lane);
+      glds_tile(q + hin, t * QSTEP, S, in_rs, lds + buf * 2 * QSTEP * HD, wid, lane);
       glds_tile(dob, t * QSTEP, S, rstride, lds + buf * 2 * QSTEP * HD + QSTEP * HD, wid, lane);
       if (DROP) {  // this lane's two 32-query keep words of tile t (consumed one tile later)
         const int w0 = (t * QSTEP) >> 5;
@@ -596,21 +635,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     for (; t < nqt; ++t) step(MSK{}, t);
 
     if (ka < S) {
-      bf16_t* dkr = dk + hoff + (size_t)ka * HD;
-      bf16_t* dvr = dv + hoff + (size_t)ka * HD;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          u16x4 wk, wv;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            wk.v[e] = f2bf(dka[dt][4 * g + e] * scale);
-            wv.v[e] = f2bf(dva[dt][4 * g + e] * (DROP ? dscale : 1.f));
-          }
-          *reinterpret_cast<u16x4*>(dkr + 32 * dt + 8 * g + 4 * h) = wk;
-          *reinterpret_cast<u16x4*>(dvr + 32 * dt + 8 * g + 4 * h) = wv;
-        }
+      store_head_row(dk + hout + (size_t)ka * out_rs, dka, scale, h, cosT, sinT, ka);
+      store_head_row(dv + hout + (size_t)ka * out_rs, dva, DROP ? dscale : 1.f, h, nullptr, nullptr, 0);
     }
   }
 }
@@ -663,7 +689,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
                                                        const float* __restrict__ lse,
                                                        float* __restrict__ delta,
                                                        const uint32_t* __restrict__ mask, bf16_t* __restrict__ dq,
-                                                       int S, int nh, float c_log2, float scale, float dscale) {
+                                                       int S, int nh, float c_log2, float scale, float dscale,
+                                                       long in_bs, int in_hs, int in_rs, long out_bs, int out_hs,
+                                                       int out_rs, const float* __restrict__ cosT,
+                                                       const float* __restrict__ sinT) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * 2 * KVB * HD];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -671,7 +700,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const int nrb = (S + RB - 1) / RB;
   const int bh = blockIdx.y;
   const int b = bh / nh, head = bh % nh;
-  const size_t hoff = (size_t)bh * S * HD;
+  const size_t hin = (size_t)b * in_bs + (size_t)head * in_hs;     // q / k / v
+  const size_t hout = (size_t)b * out_bs + (size_t)head * out_hs;  // dq
   const int W = (S + 31) >> 5;
   using B0 = std::integral_constant<int, 0>;
   using B1 = std::integral_constant<int, 1>;
@@ -693,7 +723,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     float dsum = 0.f;  // Delta = rowsum(dO * O), computed here (this kernel runs before dK/dV)
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      qf[s] = load_row8(q + hoff + (size_t)qc * HD + 16 * s + 8 * h, qok);
+      qf[s] = load_row8(q + hin + (size_t)qc * in_rs + 16 * s + 8 * h, qok);
       df[s] = load_row8(dout + orow + 16 * s + 8 * h, qok);
       const bf16x8_t of = load_row8(o + orow + 16 * s + 8 * h, qok);
 #pragma unroll
@@ -705,8 +735,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     floatx16_t dqa[2] = {zero16(), zero16()};
 
     const int nkv = (min(S, qb * RB + RB) + KVB - 1) / KVB;
-    glds_tile(k + hoff, 0, S, HD, lds, wid, lane);
-    glds_tile(v + hoff, 0, S, HD, lds + KVB * HD, wid, lane);
+    glds_tile(k + hin, 0, S, in_rs, lds, wid, lane);
+    glds_tile(v + hin, 0, S, in_rs, lds + KVB * HD, wid, lane);
     __syncthreads();
 
     // Same loop structure as the forward: straight-line unmasked tiles (static LDS
@@ -719,8 +749,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       const bool more = kb + 1 < nkv;
       if (more) {  // next tile straight into the other buffer (read by nobody since the last barrier)
         bf16_t* Kn = lds + (BUF ^ 1) * 2 * KVB * HD;
-        glds_tile(k + hoff, (kb + 1) * KVB, S, HD, Kn, wid, lane);
-        glds_tile(v + hoff, (kb + 1) * KVB, S, HD, Kn + KVB * HD, wid, lane);
+        glds_tile(k + hin, (kb + 1) * KVB, S, in_rs, Kn, wid, lane);
+        glds_tile(v + hin, (kb + 1) * KVB, S, in_rs, Kn + KVB * HD, wid, lane);
         if (DROP) mw_next = make_uint2(mrow[2 * (kb + 1)], 2 * (kb + 1) + 1 < W ? mrow[2 * (kb + 1) + 1] : 0u);
       }
       const bf16_t* Kt = lds + BUF * 2 * KVB * HD;
@@ -745,18 +775,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     } else if (kb < nkv) {
       step(B0{}, MSK{}, kb);
     }
-    if (qok) {
-      bf16_t* dqr = dq + hoff + (size_t)qa * HD;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          u16x4 w;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) w.v[e] = f2bf(dqa[dt][4 * g + e] * scale);
-          *reinterpret_cast<u16x4*>(dqr + 32 * dt + 8 * g + 4 * h) = w;
-        }
-    }
+    if (qok) store_head_row(dq + hout + (size_t)qa * out_rs, dqa, scale, h, cosT, sinT, qa);
   }
 }
 
@@ -777,10 +796,13 @@ DLT_API int dlt_attn_dropout_mask(uint32_t* mask, int B, int nh, int S, uint32_t
 }
 
 // gen_mask = 0: the keep bits are already in `mask` (dlt_attn_dropout_mask).
-DLT_API int dlt_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, uint32_t* mask,
-                         int B, int nh, int S, int hd, float scale, uint32_t key, uint32_t thr, float dscale,
-                         int gen_mask, hipStream_t st) {
-  if (hd != HD || S <= 0) return -1;
+// q/k/v element (b, head, row, d) lives at base + b*in_bs + head*in_hs + row*in_rs + d:
+// head-major [B*nh, S, 64] (bs = nh*S*64, hs = S*64, rs = 64) or straight inside the
+// packed [B*S, 3H] QKV GEMM output (bs = S*3H, hs = 64, rs = 3H; k, v = q + H, q + 2H).
+DLT_API int dlt_attn_fwd_ex(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, uint32_t* mask,
+                            int B, int nh, int S, int hd, float scale, uint32_t key, uint32_t thr, float dscale,
+                            int gen_mask, long in_bs, int in_hs, int in_rs, hipStream_t st) {
+  if (hd != HD || S <= 0 || in_rs % 8 || in_hs % 8 || in_bs % 8) return -1;
   if (thr && !mask) return -2;  // dropout needs the keep-bit buffer
   const int nrb = (S + RB - 1) / RB;
   const dim3 grid((nrb + 1) / 2, B * nh);  // item pairs
@@ -790,17 +812,30 @@ DLT_API int dlt_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16
       const int rc = dlt_attn_dropout_mask(mask, B, nh, S, key, thr, st);
       if (rc) return rc;
     }
-    k_attn_fwd<true><<<grid, NT, 0, st>>>(q, k, v, o, lse, mask, S, nh, c_log2, dscale);
+    k_attn_fwd<true><<<grid, NT, 0, st>>>(q, k, v, o, lse, mask, S, nh, c_log2, dscale, in_bs, in_hs, in_rs);
   } else {
-    k_attn_fwd<false><<<grid, NT, 0, st>>>(q, k, v, o, lse, nullptr, S, nh, c_log2, dscale);
+    k_attn_fwd<false><<<grid, NT, 0, st>>>(q, k, v, o, lse, nullptr, S, nh, c_log2, dscale, in_bs, in_hs, in_rs);
   }
   DLT_CHECK_LAUNCH();
 }
 
-DLT_API int dlt_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,
-                         const float* lse, const uint32_t* mask, float* delta_ws, bf16_t* dq, bf16_t* dk, bf16_t* dv,
-                         int B, int nh, int S, int hd, float scale, float dscale, hipStream_t st) {
-  if (hd != HD || S <= 0) return -1;
+DLT_API int dlt_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, uint32_t* mask,
+                         int B, int nh, int S, int hd, float scale, uint32_t key, uint32_t thr, float dscale,
+                         int gen_mask, hipStream_t st) {
+  return dlt_attn_fwd_ex(q, k, v, o, lse, mask, B, nh, S, hd, scale, key, thr, dscale, gen_mask,
+                         (long)nh * S * HD, S * HD, HD, st);
+}
+
+// dq/dk/dv use the (out_bs, out_hs, out_rs) layout; with cosT/sinT ([>= S, 32] fp32)
+// the inverse RoPE rotation is applied to dq and dk in the store (the gradient w.r.t.
+// the pre-rotation q/k of the packed QKV).
+DLT_API int dlt_attn_bwd_ex(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,
+                            const float* lse, const uint32_t* mask, float* delta_ws, bf16_t* dq, bf16_t* dk,
+                            bf16_t* dv, int B, int nh, int S, int hd, float scale, float dscale, long in_bs,
+                            int in_hs, int in_rs, long out_bs, int out_hs, int out_rs, const float* cosT,
+                            const float* sinT, hipStream_t st) {
+  if (hd != HD || S <= 0 || in_rs % 8 || in_hs % 8 || in_bs % 8 || out_rs % 4 || out_hs % 4 || out_bs % 4) return -1;
+  if ((cosT == nullptr) != (sinT == nullptr)) return -3;
   const float c_log2 = scale * LOG2E;
   const int nrb = (S + RB - 1) / RB;
   const dim3 gk((nrb + 1) / 2, B * nh), gq((nrb + 1) / 2, B * nh);  // item pairs
@@ -808,13 +843,23 @@ DLT_API int dlt_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, cons
   // dK/dV then reads.
   if (mask) {
     const uint32_t* maskT = mask + (size_t)B * nh * S * ((S + 31) / 32);
-    k_attn_bwd_dq<true><<<gq, NT, 0, st>>>(q, k, v, dout, o, lse, delta_ws, mask, dq, S, nh, c_log2, scale, dscale);
+    k_attn_bwd_dq<true><<<gq, NT, 0, st>>>(q, k, v, dout, o, lse, delta_ws, mask, dq, S, nh, c_log2, scale, dscale,
+                                           in_bs, in_hs, in_rs, out_bs, out_hs, out_rs, cosT, sinT);
     k_attn_bwd_dkdv<true><<<gk, NT, 0, st>>>(q, k, v, dout, lse, delta_ws, maskT, dk, dv, S, nh, c_log2, scale,
-                                             dscale);
+                                             dscale, in_bs, in_hs, in_rs, out_bs, out_hs, out_rs, cosT, sinT);
   } else {
-    k_attn_bwd_dq<false><<<gq, NT, 0, st>>>(q, k, v, dout, o, lse, delta_ws, mask, dq, S, nh, c_log2, scale, dscale);
+    k_attn_bwd_dq<false><<<gq, NT, 0, st>>>(q, k, v, dout, o, lse, delta_ws, mask, dq, S, nh, c_log2, scale, dscale,
+                                            in_bs, in_hs, in_rs, out_bs, out_hs, out_rs, cosT, sinT);
     k_attn_bwd_dkdv<false><<<gk, NT, 0, st>>>(q, k, v, dout, lse, delta_ws, mask, dk, dv, S, nh, c_log2, scale,
-                                              dscale);
+                                              dscale, in_bs, in_hs, in_rs, out_bs, out_hs, out_rs, cosT, sinT);
   }
   DLT_CHECK_LAUNCH();
+}
+
+DLT_API int dlt_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,
+                         const float* lse, const uint32_t* mask, float* delta_ws, bf16_t* dq, bf16_t* dk, bf16_t* dv,
+                         int B, int nh, int S, int hd, float scale, float dscale, hipStream_t st) {
+  const long bs = (long)nh * S * HD;
+  return dlt_attn_bwd_ex(q, k, v, o, dout, lse, mask, delta_ws, dq, dk, dv, B, nh, S, hd, scale, dscale, bs, S * HD,
+                         HD, bs, S * HD, HD, nullptr, nullptr, st);
 }

@@ -158,6 +158,45 @@ __global__ __launch_bounds__(256) void k_rope_qkv_bwd(const bf16_t* __restrict__
   }
 }
 
+// In-place RoPE of the packed [B*S, 3, nh, hd] QKV GEMM output: the q and k column
+// blocks (2*nh contiguous heads per row) are rotated, v is untouched.  The attention
+// kernels then read q/k/v straight from this buffer (dlt_attn_fwd_ex), so no head-major
+// copies are written (2/3 of the traffic of k_rope_qkv_fwd, and its backward
+// disappears into the attention epilogue).
+__global__ __launch_bounds__(256) void k_rope_qk_inplace(bf16_t* __restrict__ qkv, const float* __restrict__ cosT,
+                                                         const float* __restrict__ sinT, int M, int S, int nh,
+                                                         int hd) {
+  const int half = hd >> 1;
+  const int cpr = half >> 3;  // 8-wide chunks per rotation half
+  const int hq = 2 * nh;      // rotated heads per row (q then k)
+  const int total = M * hq * cpr;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int j = (i % cpr) * 8;
+    const int r = i / cpr;
+    const int hh = r % hq;
+    const int m = r / hq;
+    const int s = m % S;
+    bf16_t* p = qkv + (size_t)m * (3 * nh * hd) + hh * hd;
+    const u16x8 a = *reinterpret_cast<const u16x8*>(p + j);
+    const u16x8 c = *reinterpret_cast<const u16x8*>(p + half + j);
+    const float* cp = cosT + s * half + j;
+    const float* sp = sinT + s * half + j;
+    const float4 c0 = *reinterpret_cast<const float4*>(cp), c1 = *reinterpret_cast<const float4*>(cp + 4);
+    const float4 s0 = *reinterpret_cast<const float4*>(sp), s1 = *reinterpret_cast<const float4*>(sp + 4);
+    const float cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    const float ss[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    u16x8 o1, o2;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float x1 = bf2f(a.v[e]), x2 = bf2f(c.v[e]);
+      o1.v[e] = f2bf(x1 * cc[e] - x2 * ss[e]);
+      o2.v[e] = f2bf(x2 * cc[e] + x1 * ss[e]);
+    }
+    *reinterpret_cast<u16x8*>(p + j) = o1;
+    *reinterpret_cast<u16x8*>(p + half + j) = o2;
+  }
+}
+
 static inline int ew_blocks(size_t total) {
   size_t b = (total + 255) / 256;
   return (int)(b > 16384 ? 16384 : (b == 0 ? 1 : b));
@@ -168,6 +207,14 @@ DLT_API int dlt_rope_qkv_fwd(const bf16_t* qkv, const float* cosT, const float* 
   if (hd % 16 || (long)B * S * 3 * nh * hd >= (1L << 31)) return -1;
   const size_t total = (size_t)B * S * 3 * nh * (hd / 16);
   k_rope_qkv_fwd<<<ew_blocks(total), 256, 0, st>>>(qkv, cosT, sinT, q, k, v, B, S, nh, hd);
+  DLT_CHECK_LAUNCH();
+}
+
+DLT_API int dlt_rope_qk_inplace(bf16_t* qkv, const float* cosT, const float* sinT, int M, int S, int nh, int hd,
+                                hipStream_t st) {
+  if (hd % 16 || S <= 0 || M % S || (long)M * 3 * nh * hd >= (1L << 31)) return -1;
+  const size_t total = (size_t)M * 2 * nh * (hd / 16);
+  k_rope_qk_inplace<<<ew_blocks(total), 256, 0, st>>>(qkv, cosT, sinT, M, S, nh, hd);
   DLT_CHECK_LAUNCH();
 }
 

@@ -52,6 +52,12 @@ _SIGS = {
     "dlt_attn_dropout_mask": [c_void_p, c_int, c_int, c_int, c_uint32, c_uint32, c_void_p],
     "dlt_attn_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                      c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_float, c_void_p],
+    "dlt_attn_fwd_ex": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                        c_float, c_uint32, c_uint32, c_float, c_int, ctypes.c_long, c_int, c_int, c_void_p],
+    "dlt_attn_bwd_ex": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                        c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_float, ctypes.c_long, c_int, c_int,
+                        ctypes.c_long, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "dlt_rope_qk_inplace": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
 }
 
 
@@ -224,6 +230,25 @@ def rope_qkv_bwd(dq, dk, dv, cos, sin, out=None):
     return out
 
 
+def rope_qk_inplace(qkv, B, S, nh, cos, sin):
+    """Rotate the q and k column blocks of the packed [B*S, 3H] QKV in place."""
+    M, threeH = qkv.shape
+    hd = threeH // (3 * nh)
+    if M != B * S or hd * 3 * nh != threeH or hd % 16:
+        raise ValueError("rope_qk_inplace: bad shapes")
+    _req(qkv, torch.bfloat16, "rope_qk.qkv")
+    if cos.shape[0] < S or cos.shape[1] != hd // 2 or sin.shape != cos.shape:
+        raise ValueError("rope tables too short")
+    _req(cos, torch.float32, "rope_qk.cos")
+    _req(sin, torch.float32, "rope_qk.sin")
+    _chk(lib().dlt_rope_qk_inplace(_p(qkv), _p(cos), _p(sin), M, S, nh, hd, _stream()), "rope_qk_inplace")
+    return qkv
+
+
+def _off(t: torch.Tensor, elems: int):
+    return ctypes.c_void_p(t.data_ptr() + elems * t.element_size())
+
+
 # -------------------------------------------------------------- attention
 class AttnAux(tuple):
     """(lse [B,nh,S] fp32, keep-bit masks [2, B*nh, S, ceil(S/32)] int32 or None:
@@ -269,6 +294,70 @@ def attention_fwd(q, k, v, p, key, causal=True, store_mask=True, out=None, mask=
     _chk(lib().dlt_attn_fwd(_p(q), _p(k), _p(v), _p(o), _p(lse), _p(mask), B, nh, S, hd, 1.0 / math.sqrt(hd),
                             key & 0xFFFFFFFF, thr, dscale, gen, _stream()), "attn_fwd")
     return o, AttnAux((lse, mask))
+
+
+def _packed_dims(qkv, B, S, nh):
+    M, threeH = qkv.shape
+    hd = threeH // (3 * nh)
+    if M != B * S or hd * 3 * nh != threeH:
+        raise ValueError("packed attention: qkv must be [B*S, 3*nh*hd]")
+    if hd != 64:
+        raise NotImplementedError(f"attention kernel is specialised for head_dim 64 (got {hd})")
+    _req(qkv, torch.bfloat16, "attn.qkv")
+    return M, nh * hd, hd
+
+
+def attention_fwd_packed(qkv, B, S, nh, p, key, out=None, mask=None, store_mask=True):
+    """Causal attention reading q/k/v straight from the packed (roped) [B*S, 3H] QKV.
+    Returns (o [B*S, H] bf16, aux) like :func:`attention_fwd`."""
+    M, H, hd = _packed_dims(qkv, B, S, nh)
+    o = torch.empty(M, H, dtype=torch.bfloat16, device=qkv.device) if out is None else out
+    _req(o, torch.bfloat16, "attn.o", M * H)
+    lse = torch.empty(B, nh, S, dtype=torch.float32, device=qkv.device)
+    thr = rng.keep_threshold(p)
+    dscale = 1.0 / (1.0 - p) if thr else 1.0
+    gen = 1
+    if not thr:
+        mask = None
+    elif mask is not None:
+        _req(mask, torch.int32, "attn.mask", 2 * B * nh * S * ((S + 31) // 32))
+        gen = 0
+    elif store_mask:
+        mask = torch.empty(2, B * nh, S, (S + 31) // 32, dtype=torch.int32, device=qkv.device)
+    _chk(lib().dlt_attn_fwd_ex(_p(qkv), _off(qkv, H), _off(qkv, 2 * H), _p(o), _p(lse), _p(mask), B, nh, S, hd,
+                               1.0 / math.sqrt(hd), key & 0xFFFFFFFF, thr, dscale, gen, S * 3 * H, hd, 3 * H,
+                               _stream()), "attn_fwd_packed")
+    return o, AttnAux((lse, mask))
+
+
+def attention_bwd_packed(qkv, o, do, aux, p, key, B, S, nh, cos, sin, out=None):
+    """Backward of :func:`attention_fwd_packed` + the in-place RoPE: returns dqkv
+    [B*S, 3H] (gradient w.r.t. the pre-rotation QKV GEMM output); dq/dk/dv are written
+    into it by the attention kernels with the inverse rotation in their epilogue."""
+    M, H, hd = _packed_dims(qkv, B, S, nh)
+    for t, nm in ((o, "o"), (do, "do")):
+        _req(t, torch.bfloat16, "attn_bwd." + nm, M * H)
+    lse, mask = aux if isinstance(aux, tuple) else (aux, None)
+    _req(lse, torch.float32, "attn_bwd.lse", B * nh * S)
+    if cos.shape[0] < S or cos.shape[1] != hd // 2 or sin.shape != cos.shape:
+        raise ValueError("rope tables too short")
+    _req(cos, torch.float32, "attn_bwd.cos")
+    _req(sin, torch.float32, "attn_bwd.sin")
+    thr = rng.keep_threshold(p)
+    if thr and mask is None:
+        _, aux2 = attention_fwd_packed(qkv, B, S, nh, p, key)
+        mask = aux2[1]
+    if not thr:
+        mask = None
+    dqkv = torch.empty(M, 3 * H, dtype=torch.bfloat16, device=qkv.device) if out is None else out
+    _req(dqkv, torch.bfloat16, "attn_bwd.dqkv", M * 3 * H)
+    delta = torch.empty(B, nh, S, dtype=torch.float32, device=qkv.device)
+    dscale = 1.0 / (1.0 - p) if thr else 1.0
+    st = S * 3 * H
+    _chk(lib().dlt_attn_bwd_ex(_p(qkv), _off(qkv, H), _off(qkv, 2 * H), _p(o), _p(do), _p(lse), _p(mask), _p(delta),
+                               _p(dqkv), _off(dqkv, H), _off(dqkv, 2 * H), B, nh, S, hd, 1.0 / math.sqrt(hd), dscale,
+                               st, hd, 3 * H, st, hd, 3 * H, _p(cos), _p(sin), _stream()), "attn_bwd_packed")
+    return dqkv
 
 
 def attention_bwd(q, k, v, o, do, aux, p, key, causal=True):

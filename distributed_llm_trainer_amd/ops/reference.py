@@ -135,6 +135,45 @@ def rope_qkv_bwd(dq: torch.Tensor, dk: torch.Tensor, dv: torch.Tensor,
     return res
 
 
+def _qkv_views(qkv: torch.Tensor, B: int, S: int, nh: int):
+    hd = qkv.shape[-1] // (3 * nh)
+    t = qkv.view(B, S, 3, nh, hd)
+    return t, hd
+
+
+def rope_qk_inplace(qkv: torch.Tensor, B: int, S: int, nh: int, cos: torch.Tensor, sin: torch.Tensor):
+    """Rotate the q and k column blocks of the packed [B*S, 3H] QKV in place."""
+    t, hd = _qkv_views(qkv, B, S, nh)
+    c = cos[:S].view(1, S, 1, hd // 2)
+    s = sin[:S].view(1, S, 1, hd // 2)
+    for j in (0, 1):
+        t[:, :, j] = _rot(t[:, :, j].float(), c, s).to(qkv.dtype)
+    return qkv
+
+
+def _split_packed(qkv, B, S, nh):
+    t, _ = _qkv_views(qkv, B, S, nh)
+    return tuple(t[:, :, j].transpose(1, 2).contiguous() for j in range(3))
+
+
+def attention_fwd_packed(qkv: torch.Tensor, B: int, S: int, nh: int, p: float, key: int, out=None, mask=None):
+    """Causal attention straight on the (already roped) packed [B*S, 3H] QKV."""
+    q, k, v = _split_packed(qkv, B, S, nh)
+    return attention_fwd(q, k, v, p, key, True, out=out)
+
+
+def attention_bwd_packed(qkv, o, do, lse, p: float, key: int, B: int, S: int, nh: int,
+                         cos: torch.Tensor, sin: torch.Tensor, out=None) -> torch.Tensor:
+    """Backward of attention_fwd_packed + the in-place RoPE: dqkv [B*S, 3H] (pre-RoPE)."""
+    q, k, v = _split_packed(qkv, B, S, nh)
+    dq, dk, dv = attention_bwd(q, k, v, o, do, lse, p, key, True)
+    res = rope_qkv_bwd(dq.float(), dk.float(), dv.float(), cos, sin).to(qkv.dtype)
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res
+
+
 # -------------------------------------------------------------- attention
 def attention_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, p: float, key: int,
                   causal: bool = True, out=None) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -46,6 +46,7 @@ class TrainingConfig:
     lr_schedule_fix: bool = True       # set LR before the step + clamp cosine (Q5/Q6)
     adam_eps: float = 1e-8
     defer_wgrad: bool = True           # one weight-grad GEMM per layer per optimizer step
+    pipeline_micro_steps: bool = True  # overlap fwd(k+1) with bwd(k) on two HIP streams (engine path)
 
 
 @dataclass

@@ -62,6 +62,7 @@ class DistributedTrainer:
         self.tokens_seen = 0
         self._last_norm = None
         self._grads_zeroed = False
+        self._engine_warm = False
 
     # ------------------------------------------------------------------ setup
     def _setup_distributed(self):
@@ -135,7 +136,26 @@ class DistributedTrainer:
         GA = cfg.gradient_accumulation_steps
         micro_bs = input_ids.shape[0] // GA
         total = torch.zeros((), dtype=torch.float32, device=self.device)
-        for micro in range(GA):
+        # micro-step pipelining (engine.train_window): from the second step on, so the
+        # first one runs the GEMM autotuning on a quiet GPU
+        pipelined = (self.use_engine and GA > 1 and cfg.defer_wgrad and cfg.pipeline_micro_steps
+                     and self.loss_scale is None and self._engine_warm
+                     and os.environ.get("DLT_PIPELINE", "1") != "0")
+        if pipelined:
+            ids_l = [input_ids[m * micro_bs:(m + 1) * micro_bs] for m in range(GA)]
+            from ..models.engine import shift_targets
+            tg_l = [shift_targets(x) for x in ids_l]
+            if self.ddp is not None:
+                self.ddp.require_sync(False)
+            dloss = torch.full((), 1.0 / GA, dtype=torch.float32, device=self.device)
+            range_push("window")
+            losses = self.model.engine.train_window(
+                ids_l, tg_l, dloss, recompute=bool(self.model.gradient_checkpointing),
+                before_last=(lambda: self.ddp.require_sync(True)) if self.ddp is not None else None)
+            range_pop()
+            for loss in losses:
+                total += (loss / GA).detach().float()
+        for micro in range(0 if not pipelined else GA, GA):
             ids = input_ids[micro * micro_bs:(micro + 1) * micro_bs]
             if self.ddp is not None:
                 self.ddp.require_sync(micro == GA - 1)
@@ -151,6 +171,7 @@ class DistributedTrainer:
                 loss.backward()
             range_pop()
             total += loss.detach().float()
+        self._engine_warm = self.use_engine
         if not self.use_engine:
             self.store.sync_grads_from_params()
             if self.ddp is not None:

@@ -209,6 +209,47 @@ def test_attention_bwd(S, p):
         _close(a, b.float(), 2e-2 * max(1.0, scale), 2e-2, n)
 
 
+def test_rope_qk_inplace():
+    torch.manual_seed(31)
+    B, S, nh, hd = 2, 300, 12, 64
+    qkv = torch.randn(B * S, 3 * nh * hd, device=DEV).bfloat16()
+    cos, sin = hip.rope_tables(hd, 1024, device=DEV)
+    got = hip.rope_qk_inplace(qkv.clone(), B, S, nh, cos, sin)
+    want = ref.rope_qk_inplace(qkv.float().clone(), B, S, nh, cos, sin)
+    _close(got, want, 2e-2, 1e-2, "rope in place")
+    H = nh * hd
+    assert torch.equal(got[:, 2 * H:], qkv[:, 2 * H:]), "v block must be untouched"
+
+
+@pytest.mark.parametrize("S", [64, 200, 1024])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attention_packed_fwd_bwd(S, p):
+    """Attention straight on the packed QKV (strided q/k/v) with the inverse RoPE in the
+    backward epilogue == the split path (RoPE copy kernel, head-major attention, repack)."""
+    torch.manual_seed(32 + S)
+    B, nh, hd = 2, 3, 64
+    H = nh * hd
+    raw = torch.randn(B * S, 3 * H, device=DEV).bfloat16()
+    cos, sin = hip.rope_tables(hd, 1024, device=DEV)
+    key = rng.site_key(7, 8, 9, rng.SITE_ATTN)
+    q, k, v = hip.rope_qkv_fwd(raw, B, S, nh, cos, sin)
+    o1, aux1 = hip.attention_fwd(q, k, v, p, key)
+    packed = hip.rope_qk_inplace(raw.clone(), B, S, nh, cos, sin)
+    o2, aux2 = hip.attention_fwd_packed(packed, B, S, nh, p, key)
+    assert torch.equal(o1, o2) and torch.equal(aux1[0], aux2[0])
+    do = torch.randn(B * S, H, device=DEV).bfloat16()
+    dq, dk, dv = hip.attention_bwd(q, k, v, o1, do, aux1, p, key)
+    assert torch.equal(dv.transpose(1, 2).reshape(B * S, H),
+                       hip.attention_bwd_packed(packed, o2, do, aux2, p, key, B, S, nh, cos, sin)[:, 2 * H:])
+    want = ref.rope_qkv_bwd(dq.float(), dk.float(), dv.float(), cos, sin)
+    got = hip.attention_bwd_packed(packed, o2, do, aux2, p, key, B, S, nh, cos, sin)
+    scale = want.abs().max().item()
+    _close(got, want, 1e-2 * max(1.0, scale), 1e-2, "dqkv packed")
+    # against the fp32 reference of the whole chain
+    want2 = ref.attention_bwd_packed(packed.float(), o2.float(), do.float(), aux2[0], p, key, B, S, nh, cos, sin)
+    _close(got, want2, 2e-2 * max(1.0, scale), 2e-2, "dqkv packed vs fp32 ref")
+
+
 @pytest.mark.parametrize("M,N,K", [(8192, 2304, 768), (8192, 768, 3072), (1000, 300, 200), (256, 50304, 768)])
 def test_gemm_planner(M, N, K):
     from distributed_llm_trainer_amd.ops import gemm

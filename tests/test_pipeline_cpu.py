@@ -1,0 +1,113 @@
+"""Micro-step pipelining (``GPTEngine.train_window``): the forward of micro-step k+1
+interleaved block by block with the backward of micro-step k must give exactly the
+gradients, losses and dropout masks of the sequential schedule.  Also covers the
+packed-QKV attention path of the CPU reference ops against the split q/k/v path."""
+import copy
+import os
+
+import pytest
+import torch
+
+from distributed_llm_trainer_amd.models import GPT, GPTConfig
+from distributed_llm_trainer_amd.models.engine import shift_targets
+from distributed_llm_trainer_amd.ops import reference as ref
+
+
+def tiny(**kw):
+    d = dict(vocab_size=256, hidden_size=64, num_layers=3, num_heads=4, max_seq_len=32, dropout=0.1,
+             attention_dropout=0.1)
+    d.update(kw)
+    return GPTConfig(**d)
+
+
+@pytest.mark.parametrize("GA,recompute", [(2, False), (3, False), (4, True)])
+def test_train_window_matches_sequential(GA, recompute):
+    torch.manual_seed(11)
+    m1 = GPT(tiny())
+    m2 = copy.deepcopy(m1)
+    e1 = m1.enable_engine(seed=5)
+    e2 = m2.enable_engine(seed=5)
+    m1.gradient_checkpointing = m2.gradient_checkpointing = recompute
+    m1.train()
+    m2.train()
+    data = torch.randint(0, 256, (GA, 2, 32))
+    seq = []
+    for j in range(GA):
+        e1.set_accumulation(j, GA, defer=True)
+        _, loss = m1(data[j], labels=data[j])
+        (loss / GA).backward()
+        seq.append(loss.detach())
+    dloss = torch.full((), 1.0 / GA)
+    win = e2.train_window([data[j] for j in range(GA)], [shift_targets(data[j]) for j in range(GA)], dloss,
+                          recompute=recompute)
+    assert e1.micro_counter == e2.micro_counter == GA
+    for a, b in zip(seq, win):
+        assert torch.equal(a, b)
+    for (n, p1), (_, p2) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert torch.allclose(p1.grad, p2.grad, atol=1e-7, rtol=1e-6), n
+
+
+def test_train_window_single_micro_step_is_plain_step():
+    torch.manual_seed(12)
+    m1 = GPT(tiny(dropout=0.0, attention_dropout=0.0))
+    m2 = copy.deepcopy(m1)
+    e1 = m1.enable_engine(seed=1)
+    e2 = m2.enable_engine(seed=1)
+    ids = torch.randint(0, 256, (2, 32))
+    e1.set_accumulation(0, 1)
+    _, loss = m1(ids, labels=ids)
+    loss.backward()
+    (l2,) = e2.train_window([ids], [shift_targets(ids)], torch.ones(()))
+    assert torch.equal(loss.detach(), l2)
+    for (n, p1), (_, p2) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert torch.allclose(p1.grad, p2.grad, atol=1e-7, rtol=1e-6), n
+
+
+def test_trainer_pipelined_step_matches_sequential():
+    from distributed_llm_trainer_amd.training.configs import TrainingConfig
+    from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
+    torch.manual_seed(13)
+    data = torch.randint(0, 256, (8, 32))
+    res = []
+    for pipe in (False, True):
+        tc = TrainingConfig(batch_size=2, gradient_accumulation_steps=4, warmup_steps=2, max_steps=10,
+                            pipeline_micro_steps=pipe)
+        tr = DistributedTrainer(tiny(), tc)
+        losses = [tr.train_step({"input_ids": data})["loss"] for _ in range(3)]
+        res.append((losses, tr.store.flat.clone()))
+    assert res[0][0] == res[1][0]
+    assert torch.allclose(res[0][1], res[1][1], atol=1e-7, rtol=1e-6)
+
+
+def test_packed_qkv_reference_matches_split():
+    torch.manual_seed(14)
+    B, S, nh, hd = 2, 24, 3, 16
+    qkv = torch.randn(B * S, 3 * nh * hd, dtype=torch.float64).float()
+    cos, sin = ref.rope_tables(hd, 32)
+    q, k, v = ref.rope_qkv_fwd(qkv, B, S, nh, cos, sin)
+    o1, l1 = ref.attention_fwd(q, k, v, 0.1, 77)
+    packed = ref.rope_qk_inplace(qkv.clone(), B, S, nh, cos, sin)
+    o2, l2 = ref.attention_fwd_packed(packed, B, S, nh, 0.1, 77)
+    assert torch.allclose(o1, o2, atol=1e-6) and torch.allclose(l1, l2, atol=1e-6)
+    do = torch.randn_like(o1)
+    dq, dk, dv = ref.attention_bwd(q, k, v, o1, do, l1, 0.1, 77)
+    d1 = ref.rope_qkv_bwd(dq, dk, dv, cos, sin)
+    d2 = ref.attention_bwd_packed(packed, o2, do, l2, 0.1, 77, B, S, nh, cos, sin)
+    assert torch.allclose(d1, d2, atol=1e-6)
+
+
+def test_engine_packed_matches_split_path(monkeypatch):
+    torch.manual_seed(15)
+    base = GPT(tiny())
+    grads = []
+    for packed in ("1", "0"):
+        monkeypatch.setenv("DLT_PACKED_QKV", packed)
+        m = copy.deepcopy(base)
+        e = m.enable_engine(seed=2)
+        assert e.packed_qkv == (packed == "1")
+        ids = torch.randint(0, 256, (2, 32), generator=torch.Generator().manual_seed(3))
+        _, loss = m(ids, labels=ids)
+        loss.backward()
+        grads.append([p.grad.clone() for p in m.parameters()])
+    for a, b in zip(*grads):
+        assert torch.allclose(a, b, atol=1e-6, rtol=1e-5)
