@@ -44,6 +44,9 @@ def main():
     ap.add_argument("--dropout", type=float, default=None,
                     help="ablation only: override dropout/attention_dropout (reference config: 0.1)")
     args = ap.parse_args()
+    if os.environ.get("DLT_HANG_DUMP"):  # debugging aid: periodic Python stack dumps
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["DLT_HANG_DUMP"]), repeat=True, file=sys.stderr)
 
     from distributed_llm_trainer_amd.models.config import GPTConfig
     cfg = GPTConfig.from_preset(args.model_size)
@@ -115,6 +118,10 @@ def main():
             "vs_baseline_linear": round(tps / (12500.0 * world), 3),
         }
         print(json.dumps(out), flush=True)
+        if os.environ.get("DLT_GEMM_REPORT"):
+            from distributed_llm_trainer_amd.ops import gemm as gemm_mod
+            if gemm_mod.available():
+                print(gemm_mod.report(), file=sys.stderr)
     if trainer.distributed:
         dist.barrier()
         dist.destroy_process_group()

@@ -513,8 +513,8 @@ class GPTEngine:
         """Forward + backward of a whole gradient-accumulation window.
 
         Schedule (GA = 4):  F0 | B0+F1 | B1+F2 | B2+F3 | B3, where "Bk+Fk+1" issues the
-        blocks of the two chains alternately, micro-step k on stream ``k % 2`` (the
-        current stream and one pipeline stream).  A micro-step's forward and backward
+        blocks of the two chains alternately; micro-steps alternate between the current
+        stream and the weight-gradient side stream, the last one on the current stream.  A micro-step's forward and backward
         run on the same stream, so its activations never cross streams; what is shared
         (weights, slot buffers, RoPE tables, the ids) is read-only until the window
         ends or is produced before the fork.  The last backward first joins the other
@@ -532,18 +532,26 @@ class GPTEngine:
         dev = micro_ids[0].device
         cuda = dev.type == "cuda"
         self.set_accumulation(0, GA, defer=True)
-        streams = [None, None]
-        main = None
+        main = pipe = None
         if cuda:
             main = torch.cuda.current_stream(dev)
-            if self._pipe is None:
-                self._pipe = torch.cuda.Stream(dev)
-            streams = [main, self._pipe]
+            # The second chain runs on the weight-gradient side stream: the last
+            # micro-step (the only one with weight-gradient GEMMs) is placed on the
+            # current stream and joins the other chain before it starts, so the side
+            # stream is idle by then.  Two streams in flight at any time, never three.
+            pipe = self._wgrad_stream(dev)
+            if pipe is None:
+                if self._pipe is None:
+                    self._pipe = torch.cuda.Stream(dev)
+                pipe = self._pipe
             self.rope(micro_ids[0].shape[1], dev)  # lazily-built shared state: before the fork
-            self._pipe.wait_stream(main)
+            pipe.wait_stream(main)
+
+        def stream_of(k):  # the last micro-step on the current stream, alternating backwards
+            return main if (GA - 1 - k) % 2 == 0 else pipe
 
         def on(k):
-            return torch.cuda.stream(streams[k % 2]) if cuda else contextlib.nullcontext()
+            return torch.cuda.stream(stream_of(k)) if cuda else contextlib.nullcontext()
 
         def fwd(k):
             return self._forward_gen(micro_ids[k], micro_targets[k], True, recompute, need_backward=True,
@@ -556,7 +564,7 @@ class GPTEngine:
         for k in range(GA):
             if k == GA - 1:
                 if cuda and GA > 1:
-                    streams[k % 2].wait_stream(streams[(k + 1) % 2])
+                    main.wait_stream(pipe)
                 if before_last is not None:
                     before_last()
             running = [(k, self._backward_gen(states[k], dloss), False)]
@@ -573,22 +581,23 @@ class GPTEngine:
                             running.remove(item)
                             if is_fwd:
                                 losses[j], _, states[j] = stop.value
-        if cuda and GA > 1:
-            main.wait_stream(self._pipe)
         return losses
 
 
 class _TorchGemm:
     """Plain library GEMMs (hipBLASLt on ROCm via torch.matmul).
 
-    Stream-safe: torch keeps one BLAS workspace per stream.
+    NOT stream-safe on the GPU: torch keeps one hipBLASLt handle per thread, and
+    hipBLASLt GEMMs in flight concurrently on two streams through one handle can
+    deadlock the gfx950 stream-K kernels (see ops/csrc_gemm/gemm_planner.cpp), so with
+    this backend the engine runs no side-stream GEMMs and no micro-step pipelining.
 
     ``wgrad_acc`` accumulates bf16 x bf16 products straight into the fp32 main-grad
     buffer with ``addmm(..., out_dtype=float32)`` when available (no bf16 round trip,
     no separate add kernel); otherwise falls back to matmul + add_.
     """
 
-    stream_safe = True
+    stream_safe = False
 
     def __init__(self):
         self._fp32_out_ok = None

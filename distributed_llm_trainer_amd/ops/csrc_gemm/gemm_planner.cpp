@@ -11,11 +11,14 @@
 //   * on the first call of a key, times up to DLT_GEMM_CANDIDATES heuristic
 //     solutions on the caller's stream and keeps the fastest (a key first seen
 //     inside a HIP-graph capture takes heuristic #0 without timing),
-//   * owns one device workspace per stream (DLT_GEMM_WORKSPACE_MB, default 64), so
-//     GEMMs on the compute and weight-gradient streams can run concurrently.
+//   * owns one hipBLASLt handle and one device workspace per stream
+//     (DLT_GEMM_WORKSPACE_MB, default 64), so GEMMs on the compute and side streams
+//     can run concurrently (see StreamCtx),
+//   * records the chosen kernel's name for the plan report.
 // C ABI, loaded by ctypes from ops/gemm.py.
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt.h>
+#include <hipblaslt/hipblaslt-ext.hpp>
 
 #include <algorithm>
 #include <cstdio>
@@ -46,11 +49,22 @@ struct Plan {
   size_t ws = 0;
   float us = -1.f;
   int chosen = 0, candidates = 0;
+  std::string kernel;
+};
+
+// Per-stream execution context: a hipBLASLt handle of its own plus a workspace.  A
+// handle is not safe for GEMMs in flight concurrently on two streams: the gfx950
+// kernels are stream-K "UserArgs" kernels and sharing one handle between the compute
+// and side streams deadlocked the GPU (100 % busy, spinning workgroups) within a few
+// pipelined training steps; one handle per stream does not.
+struct StreamCtx {
+  hipblasLtHandle_t h = nullptr;
+  void* ws = nullptr;
 };
 
 struct Planner {
-  hipblasLtHandle_t h = nullptr;
-  std::map<hipStream_t, void*> ws;  // one workspace per stream (concurrent GEMMs)
+  hipblasLtHandle_t h = nullptr;    // heuristics / autotune / kernel-name queries
+  std::map<hipStream_t, StreamCtx> ctx;  // one handle + workspace per stream
   size_t wsz = 0;
   std::map<Key, Plan> plans;
   std::mutex mu;
@@ -80,13 +94,13 @@ int init() {
 }
 
 // caller holds g->mu
-void* workspace(hipStream_t s) {
-  auto it = g->ws.find(s);
-  if (it != g->ws.end()) return it->second;
-  void* w = nullptr;
-  if (hipMalloc(&w, g->wsz) != hipSuccess) return nullptr;
-  g->ws.emplace(s, w);
-  return w;
+const StreamCtx* stream_ctx(hipStream_t s) {
+  auto it = g->ctx.find(s);
+  if (it != g->ctx.end()) return &it->second;
+  StreamCtx c;
+  if (hipblasLtCreate(&c.h) != HIPBLAS_STATUS_SUCCESS) return nullptr;
+  if (hipMalloc(&c.ws, g->wsz) != hipSuccess) return nullptr;
+  return &g->ctx.emplace(s, c).first->second;
 }
 
 bool capturing(hipStream_t s) {
@@ -95,7 +109,8 @@ bool capturing(hipStream_t s) {
   return st != hipStreamCaptureStatusNone;
 }
 
-int build_plan(const Key& k, Plan& p, const void* A, const void* B, void* C, hipStream_t s, void* ws) {
+int build_plan(const Key& k, Plan& p, const void* A, const void* B, void* C, hipStream_t s, const StreamCtx* sc) {
+  void* ws = sc->ws;
   if (hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS) return -20;
   hipblasOperation_t ta = k.ta ? HIPBLAS_OP_T : HIPBLAS_OP_N, tb = k.tb ? HIPBLAS_OP_T : HIPBLAS_OP_N;
   hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta));
@@ -136,13 +151,13 @@ int build_plan(const Key& k, Plan& p, const void* A, const void* B, void* C, hip
     if (res[i].workspaceSize > g->wsz) continue;
     bool ok = true;
     for (int w = 0; w < 2 && ok; ++w)
-      ok = hipblasLtMatmul(g->h, p.desc, &alpha, A, p.la, B, p.lb, &beta0, C, p.lc, C, p.lc, &res[i].algo, ws,
+      ok = hipblasLtMatmul(sc->h, p.desc, &alpha, A, p.la, B, p.lb, &beta0, C, p.lc, C, p.lc, &res[i].algo, ws,
                            g->wsz, s) == HIPBLAS_STATUS_SUCCESS;
     if (!ok) continue;
     hipEventRecord(e0, s);
     const int iters = 5;
     for (int it = 0; it < iters; ++it)
-      hipblasLtMatmul(g->h, p.desc, &alpha, A, p.la, B, p.lb, &beta0, C, p.lc, C, p.lc, &res[i].algo, ws, g->wsz,
+      hipblasLtMatmul(sc->h, p.desc, &alpha, A, p.la, B, p.lb, &beta0, C, p.lc, C, p.lc, &res[i].algo, ws, g->wsz,
                       s);
     hipEventRecord(e1, s);
     hipEventSynchronize(e1);
@@ -162,6 +177,7 @@ int build_plan(const Key& k, Plan& p, const void* A, const void* B, void* C, hip
   p.ws = res[bi].workspaceSize;
   p.us = best;
   p.chosen = bi;
+  p.kernel = hipblaslt_ext::getKernelNameFromAlgo(g->h, p.algo);
   if (g->verbose)
     fprintf(stderr, "[dlt-gemm] ta=%d tb=%d m=%d n=%d k=%d acc=%d: %d candidates, chose #%d (%.1f us, %.0f TF/s)\n", k.ta,
             k.tb, k.m, k.n, k.k, k.accumulate, n, bi, best, 2.0 * k.m * k.n * k.k / best / 1e6);
@@ -176,22 +192,22 @@ DLT_API int dlt_gemm(int ta, int tb, int m, int n, int k, const void* A, int lda
   if (int rc = init()) return rc;
   Key key{ta, tb, m, n, k, lda, ldb, ldc, dta, dtb, dtc, beta != 0.f ? 1 : 0};
   Plan* p;
-  void* ws;
+  const StreamCtx* sc;
   {
     std::lock_guard<std::mutex> lk(g->mu);
-    ws = workspace(s);
-    if (!ws) return -11;
+    sc = stream_ctx(s);
+    if (!sc) return -11;
     auto it = g->plans.find(key);
     if (it == g->plans.end()) {
       Plan np;
-      int rc = build_plan(key, np, A, B, C, s, ws);
+      int rc = build_plan(key, np, A, B, C, s, sc);
       if (rc) return rc;
       it = g->plans.emplace(key, np).first;
     }
     p = &it->second;
   }
-  hipblasStatus_t st = hipblasLtMatmul(g->h, p->desc, &alpha, A, p->la, B, p->lb, &beta, C, p->lc, C, p->lc, &p->algo,
-                                       ws, g->wsz, s);
+  hipblasStatus_t st = hipblasLtMatmul(sc->h, p->desc, &alpha, A, p->la, B, p->lb, &beta, C, p->lc, C, p->lc,
+                                       &p->algo, sc->ws, g->wsz, s);
   return st == HIPBLAS_STATUS_SUCCESS ? 0 : -30 - (int)st;
 }
 
@@ -204,9 +220,9 @@ DLT_API int dlt_gemm_report(char* buf, int len) {
   for (auto& kv : g->plans) {
     const Key& k = kv.first;
     const Plan& p = kv.second;
-    char line[256];
-    snprintf(line, sizeof(line), "ta=%d tb=%d m=%d n=%d k=%d acc=%d dtc=%d cand=%d chosen=%d us=%.1f\n", k.ta, k.tb,
-             k.m, k.n, k.k, k.accumulate, k.dtc, p.candidates, p.chosen, p.us);
+    char line[512];
+    snprintf(line, sizeof(line), "ta=%d tb=%d m=%d n=%d k=%d acc=%d dtc=%d cand=%d chosen=%d us=%.1f %.80s\n", k.ta,
+             k.tb, k.m, k.n, k.k, k.accumulate, k.dtc, p.candidates, p.chosen, p.us, p.kernel.c_str());
     out += line;
   }
   int n = (int)std::min<size_t>(out.size(), (size_t)len - 1);

@@ -76,8 +76,8 @@ def _rowmajor(t: torch.Tensor) -> int:
 
 
 class HipGemm:
-    """The engine's GEMM interface on the autotuned hipBLASLt planner (one workspace
-    per stream, so GEMMs on the compute and weight-gradient streams may overlap).
+    """The engine's GEMM interface on the autotuned hipBLASLt planner (one hipBLASLt
+    handle + workspace per stream, so GEMMs on the compute and side streams may overlap).
 
     Forward projections (y = x W^T, both operands K-contiguous) additionally race the
     hand-written MFMA kernel (``csrc/gemm_tn.hip``, several tile shapes) against the

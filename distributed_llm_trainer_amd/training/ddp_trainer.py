@@ -140,6 +140,7 @@ class DistributedTrainer:
         # first one runs the GEMM autotuning on a quiet GPU
         pipelined = (self.use_engine and GA > 1 and cfg.defer_wgrad and cfg.pipeline_micro_steps
                      and self.loss_scale is None and self._engine_warm
+                     and (self.device.type != "cuda" or getattr(self.model.engine.gemm, "stream_safe", False))
                      and os.environ.get("DLT_PIPELINE", "1") != "0")
         if pipelined:
             ids_l = [input_ids[m * micro_bs:(m + 1) * micro_bs] for m in range(GA)]
