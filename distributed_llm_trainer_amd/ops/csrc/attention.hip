@@ -242,6 +242,25 @@ __global__ __launch_bounds__(256) void k_dropout_bits(uint32_t* __restrict__ mas
   if (active && kk < S) maskT[((size_t)bh * S + kk) * W + r] = col;
 }
 
+// ============================================================================ work map
+// The MFMA kernels run a 1-D grid of (head, item-pair) work items.  The dispatcher deals
+// consecutive workgroup ids round-robin to the 8 XCDs, each with its own 4 MB L2; with
+// the natural order (pair fastest) XCD x would get pair x of EVERY head, so no two
+// workgroups on an XCD share a K/V (fwd, dQ) or Q/dO (dK/dV) stream and every tile is
+// fetched once per pair from the fabric.  The XCD-aware map gives each XCD a contiguous
+// range of items instead -- all pairs of a head on one XCD, reading the head's tiles
+// through the same L2 (bijective for any grid size, like the GEMM's tile map).
+__device__ __forceinline__ void work_item(int npairs, int xcd_map, int& bh, int& pair) {
+  const int bid = blockIdx.x;
+  int wg = bid;
+  if (xcd_map) {
+    const int nwg = gridDim.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  }
+  bh = wg / npairs;
+  pair = wg - bh * npairs;
+}
+
 // ============================================================================ forward
 // Cross-half (lane i <-> i^32) exchange without LDS: v_permlane32_swap (CDNA4).
 __device__ __forceinline__ float xhalf_max(float x) {
@@ -337,13 +356,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
                                                     const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
                                                     float* __restrict__ lse, const uint32_t* __restrict__ mask,
                                                     int S, int nh, float c_log2, float dscale, long in_bs,
-                                                    int in_hs, int in_rs) {
+                                                    int in_hs, int in_rs, int xcd_map) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * 2 * KVB * HD];  // [buf][K|V][64][64]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, ql = lane & 31;
   const int nrb = (S + RB - 1) / RB;
-  const int bh = blockIdx.y;
+  int bh, pair;
+  work_item((nrb + 1) / 2, xcd_map, bh, pair);
   const int b = bh / nh, head = bh % nh;
   const size_t hin = (size_t)b * in_bs + (size_t)head * in_hs;  // (b, head) base of q / k / v
   const int W = (S + 31) >> 5;
@@ -354,8 +374,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 
 #pragma unroll 1
   for (int it = 0; it < 2; ++it) {
-    const int qb = it == 0 ? nrb - 1 - (int)blockIdx.x : (int)blockIdx.x;  // long item first
-    if (it == 1 && qb >= nrb - 1 - (int)blockIdx.x) break;                 // odd nrb: middle item once
+    const int qb = it == 0 ? nrb - 1 - pair : pair;  // long item first
+    if (it == 1 && qb >= nrb - 1 - pair) break;      // odd nrb: middle item once
     const int q0 = qb * RB + wid * 32;  // this wave's first query (wave-uniform)
     const int qa = q0 + ql;
     const uint32_t* mrow = mask ? mask + ((size_t)bh * S + min(qa, S - 1)) * W : nullptr;
@@ -532,7 +552,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
                                                          float scale, float dscale, long in_bs, int in_hs, int in_rs,
                                                          long out_bs, int out_hs, int out_rs,
                                                          const float* __restrict__ cosT,
-                                                         const float* __restrict__ sinT) {
+                                                         const float* __restrict__ sinT, int xcd_map) {
   // one LDS object (avoids hipcc's extra vmcnt waits with several __shared__ arrays)
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * QSTEP * HD * 2 + 2 * 2 * QSTEP * 4];
   bf16_t* lds = reinterpret_cast<bf16_t*>(smem);                              // [buf][Q|dO][64][64]
@@ -541,7 +561,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, kl = lane & 31;
   const int nrb = (S + RB - 1) / RB;
-  const int bh = blockIdx.y;
+  int bh, pair;
+  work_item((nrb + 1) / 2, xcd_map, bh, pair);
   const int b = bh / nh, head = bh % nh;
   const size_t hin = (size_t)b * in_bs + (size_t)head * in_hs;     // q / k / v
   const size_t hout = (size_t)b * out_bs + (size_t)head * out_hs;  // dk / dv
@@ -554,8 +575,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 
 #pragma unroll 1
   for (int it = 0; it < 2; ++it) {
-    const int kblk = it == 0 ? (int)blockIdx.x : nrb - 1 - (int)blockIdx.x;  // long item (early keys) first
-    if (it == 1 && kblk <= (int)blockIdx.x) break;                           // odd nrb: middle item once
+    const int kblk = it == 0 ? pair : nrb - 1 - pair;  // long item (early keys) first
+    if (it == 1 && kblk <= pair) break;                 // odd nrb: middle item once
     const int k0 = kblk * RB + wid * 32;  // wave-uniform
     const int ka = k0 + kl;
     // this lane's key column of the transposed keep-bit mask: one word per 32 queries
@@ -692,13 +713,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
                                                        int S, int nh, float c_log2, float scale, float dscale,
                                                        long in_bs, int in_hs, int in_rs, long out_bs, int out_hs,
                                                        int out_rs, const float* __restrict__ cosT,
-                                                       const float* __restrict__ sinT) {
+                                                       const float* __restrict__ sinT, int xcd_map) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * 2 * KVB * HD];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, ql = lane & 31;
   const int nrb = (S + RB - 1) / RB;
-  const int bh = blockIdx.y;
+  int bh, pair;
+  work_item((nrb + 1) / 2, xcd_map, bh, pair);
   const int b = bh / nh, head = bh % nh;
   const size_t hin = (size_t)b * in_bs + (size_t)head * in_hs;     // q / k / v
   const size_t hout = (size_t)b * out_bs + (size_t)head * out_hs;  // dq
@@ -710,8 +732,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 
 #pragma unroll 1
   for (int it = 0; it < 2; ++it) {
-    const int qb = it == 0 ? nrb - 1 - (int)blockIdx.x : (int)blockIdx.x;  // long item first
-    if (it == 1 && qb >= nrb - 1 - (int)blockIdx.x) break;
+    const int qb = it == 0 ? nrb - 1 - pair : pair;  // long item first
+    if (it == 1 && qb >= nrb - 1 - pair) break;
     const int q0 = qb * RB + wid * 32;
     const int qa = q0 + ql;
     const bool qok = qa < S;
@@ -780,6 +802,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 }
 
 // ============================================================================ launchers
+#include <cstdlib>
+// XCD-aware work map on by default; DLT_ATTN_XCD=0 restores the natural order (A/B).
+static int xcd_map_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DLT_ATTN_XCD");
+    v = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  return v;
+}
 // mask: uint32 [2][B*nh, S, ceil(S/32)] keep-bits written by the forward when dropout
 // is on -- [0] row layout (lane = query), [1] transposed (lane = key), see
 // k_dropout_bits.
@@ -805,16 +837,17 @@ DLT_API int dlt_attn_fwd_ex(const bf16_t* q, const bf16_t* k, const bf16_t* v, b
   if (hd != HD || S <= 0 || in_rs % 8 || in_hs % 8 || in_bs % 8) return -1;
   if (thr && !mask) return -2;  // dropout needs the keep-bit buffer
   const int nrb = (S + RB - 1) / RB;
-  const dim3 grid((nrb + 1) / 2, B * nh);  // item pairs
+  const dim3 grid(((nrb + 1) / 2) * B * nh);  // (head, item pair) work items, see work_item()
+  const int xm = xcd_map_enabled();
   const float c_log2 = scale * LOG2E;
   if (thr) {
     if (gen_mask) {
       const int rc = dlt_attn_dropout_mask(mask, B, nh, S, key, thr, st);
       if (rc) return rc;
     }
-    k_attn_fwd<true><<<grid, NT, 0, st>>>(q, k, v, o, lse, mask, S, nh, c_log2, dscale, in_bs, in_hs, in_rs);
+    k_attn_fwd<true><<<grid, NT, 0, st>>>(q, k, v, o, lse, mask, S, nh, c_log2, dscale, in_bs, in_hs, in_rs, xm);
   } else {
-    k_attn_fwd<false><<<grid, NT, 0, st>>>(q, k, v, o, lse, nullptr, S, nh, c_log2, dscale, in_bs, in_hs, in_rs);
+    k_attn_fwd<false><<<grid, NT, 0, st>>>(q, k, v, o, lse, nullptr, S, nh, c_log2, dscale, in_bs, in_hs, in_rs, xm);
   }
   DLT_CHECK_LAUNCH();
 }
@@ -838,20 +871,21 @@ DLT_API int dlt_attn_bwd_ex(const bf16_t* q, const bf16_t* k, const bf16_t* v, c
   if ((cosT == nullptr) != (sinT == nullptr)) return -3;
   const float c_log2 = scale * LOG2E;
   const int nrb = (S + RB - 1) / RB;
-  const dim3 gk((nrb + 1) / 2, B * nh), gq((nrb + 1) / 2, B * nh);  // item pairs
+  const dim3 gk(((nrb + 1) / 2) * B * nh), gq(((nrb + 1) / 2) * B * nh);  // (head, item pair) work items
+  const int xm = xcd_map_enabled();
   // dQ first: it also produces Delta = rowsum(dO * O) (no separate kernel), which
   // dK/dV then reads.
   if (mask) {
     const uint32_t* maskT = mask + (size_t)B * nh * S * ((S + 31) / 32);
     k_attn_bwd_dq<true><<<gq, NT, 0, st>>>(q, k, v, dout, o, lse, delta_ws, mask, dq, S, nh, c_log2, scale, dscale,
-                                           in_bs, in_hs, in_rs, out_bs, out_hs, out_rs, cosT, sinT);
+                                           in_bs, in_hs, in_rs, out_bs, out_hs, out_rs, cosT, sinT, xm);
     k_attn_bwd_dkdv<true><<<gk, NT, 0, st>>>(q, k, v, dout, lse, delta_ws, maskT, dk, dv, S, nh, c_log2, scale,
-                                             dscale, in_bs, in_hs, in_rs, out_bs, out_hs, out_rs, cosT, sinT);
+                                             dscale, in_bs, in_hs, in_rs, out_bs, out_hs, out_rs, cosT, sinT, xm);
   } else {
     k_attn_bwd_dq<false><<<gq, NT, 0, st>>>(q, k, v, dout, o, lse, delta_ws, mask, dq, S, nh, c_log2, scale, dscale,
-                                            in_bs, in_hs, in_rs, out_bs, out_hs, out_rs, cosT, sinT);
+                                            in_bs, in_hs, in_rs, out_bs, out_hs, out_rs, cosT, sinT, xm);
     k_attn_bwd_dkdv<false><<<gk, NT, 0, st>>>(q, k, v, dout, lse, delta_ws, mask, dk, dv, S, nh, c_log2, scale,
-                                              dscale, in_bs, in_hs, in_rs, out_bs, out_hs, out_rs, cosT, sinT);
+                                              dscale, in_bs, in_hs, in_rs, out_bs, out_hs, out_rs, cosT, sinT, xm);
   }
   DLT_CHECK_LAUNCH();
 }

@@ -29,14 +29,23 @@ def main():
     ap.add_argument("--S", type=int, default=1024)
     ap.add_argument("--p", type=float, default=0.1)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--packed", action="store_true", help="attention on the packed [B*S, 3H] QKV (engine default)")
     a = ap.parse_args()
     torch.manual_seed(0)
     q, k, v = (torch.randn(a.B, a.nh, a.S, 64, device="cuda").bfloat16() for _ in range(3))
     key = rng.site_key(1, 2, 3, rng.SITE_ATTN)
-    o, aux = hip.attention_fwd(q, k, v, a.p, key)
-    do = torch.randn_like(o)
-    t_f = timeit(lambda: hip.attention_fwd(q, k, v, a.p, key), a.iters)
-    t_b = timeit(lambda: hip.attention_bwd(q, k, v, o, do, aux, a.p, key), a.iters)
+    if a.packed:
+        qkv = torch.randn(a.B * a.S, 3 * a.nh * 64, device="cuda").bfloat16()
+        cos, sin = hip.rope_tables(64, a.S, device="cuda")
+        o, aux = hip.attention_fwd_packed(qkv, a.B, a.S, a.nh, a.p, key)
+        do = torch.randn_like(o)
+        t_f = timeit(lambda: hip.attention_fwd_packed(qkv, a.B, a.S, a.nh, a.p, key), a.iters)
+        t_b = timeit(lambda: hip.attention_bwd_packed(qkv, o, do, aux, a.p, key, a.B, a.S, a.nh, cos, sin), a.iters)
+    else:
+        o, aux = hip.attention_fwd(q, k, v, a.p, key)
+        do = torch.randn_like(o)
+        t_f = timeit(lambda: hip.attention_fwd(q, k, v, a.p, key), a.iters)
+        t_b = timeit(lambda: hip.attention_bwd(q, k, v, o, do, aux, a.p, key), a.iters)
     fl = 4 * a.B * a.nh * a.S * a.S / 2 * 64
     print(f"fwd {t_f:.1f} us ({fl / t_f / 1e6:.1f} TF/s)  bwd {t_b:.1f} us ({2.5 * fl / t_b / 1e6:.1f} TF/s)")
 
