@@ -18,6 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "_dlt_kernels.so")
+DEBUG_LIB = os.path.join(HERE, "_dlt_kernels_debug.so")  # DLT_DEBUG bounds checks (DLT_KERNEL_DEBUG=1)
 GEMM_SRC = os.path.join(HERE, "csrc_gemm", "gemm_planner.cpp")
 GEMM_LIB = os.path.join(HERE, "_dlt_gemm.so")
 ARCH = os.environ.get("DLT_OFFLOAD_ARCH", "gfx950")
@@ -50,13 +51,18 @@ def _compile(src: str, obj: str, extra):
     return obj
 
 
-def build(verbose: bool = True, jobs: int = 0, extra=()) -> str:
+def build(verbose: bool = True, jobs: int = 0, extra=(), debug: bool = False) -> str:
+    """Compile every ``csrc/*.hip`` for gfx950 and link ``_dlt_kernels.so`` (or, with
+    ``debug``, ``_dlt_kernels_debug.so``: -DDLT_DEBUG device bounds checks, -g)."""
     os.makedirs(BUILD, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     headers = glob.glob(os.path.join(CSRC, "*.h"))
+    lib_path = DEBUG_LIB if debug else LIB
+    if debug:
+        extra = (*extra, "-DDLT_DEBUG", "-g")
     objs, todo = [], []
     for s in srcs:
-        o = os.path.join(BUILD, os.path.basename(s)[:-4] + ".o")
+        o = os.path.join(BUILD, os.path.basename(s)[:-4] + (".dbg.o" if debug else ".o"))
         objs.append(o)
         if _needs(s, o, headers):
             todo.append((s, o))
@@ -68,18 +74,18 @@ def build(verbose: bool = True, jobs: int = 0, extra=()) -> str:
             futs = [ex.submit(_compile, s, o, list(extra)) for s, o in todo]
             for f in futs:
                 f.result()
-    relink = not os.path.exists(LIB) or any(os.path.getmtime(o) > os.path.getmtime(LIB) for o in objs)
+    relink = not os.path.exists(lib_path) or any(os.path.getmtime(o) > os.path.getmtime(lib_path) for o in objs)
     if relink:
-        tmp = LIB + ".tmp"
+        tmp = lib_path + ".tmp"
         cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
-        os.replace(tmp, LIB)
+        os.replace(tmp, lib_path)
         if verbose:
-            print(f"[dlt-build] linked {LIB}", flush=True)
+            print(f"[dlt-build] linked {lib_path}", flush=True)
     build_gemm(verbose)
-    return LIB
+    return lib_path
 
 
 def build_gemm(verbose: bool = True) -> str:
@@ -100,5 +106,5 @@ def build_gemm(verbose: bool = True) -> str:
 
 
 if __name__ == "__main__":
-    build(verbose=True)
+    build(verbose=True, debug="--debug" in sys.argv)
     sys.exit(0)

@@ -55,3 +55,21 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 #define DLT_CHECK_LAUNCH() return (int)hipGetLastError()
+
+// Device-side bounds checks, compiled in only for the debug library
+// (`python -m distributed_llm_trainer_amd.ops.build --debug` -> _dlt_kernels_debug.so,
+// selected at run time with DLT_KERNEL_DEBUG=1): a failed check prints the condition
+// and traps the wave, so a bad token id or target stops at the faulting kernel instead
+// of silently reading another row (XNACK is off: out-of-range reads inside the
+// allocation do not fault).
+#ifdef DLT_DEBUG
+#define DLT_DASSERT(cond)                                                        \
+  do {                                                                           \
+    if (!(cond)) {                                                               \
+      printf("DLT_DASSERT failed %s:%d: %s\n", __FILE__, __LINE__, #cond);       \
+      __builtin_trap();                                                          \
+    }                                                                            \
+  } while (0)
+#else
+#define DLT_DASSERT(cond) ((void)0)
+#endif

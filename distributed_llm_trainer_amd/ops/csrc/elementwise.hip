@@ -9,13 +9,14 @@
 // ---------------------------------------------------------------- embedding
 // out[m, :] = float(W[ids[m], :]); W is fp32 (wdt=0) or bf16 (wdt=1).
 __global__ __launch_bounds__(256) void k_embedding_fwd(const int64_t* __restrict__ ids, const void* __restrict__ W,
-                                                       int wdt, float* __restrict__ out, int M, int H) {
+                                                       int wdt, float* __restrict__ out, int M, int H, int V) {
   const int q = H >> 2;  // float4 per row
   const size_t total = (size_t)M * q;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
     const int m = (int)(i / q);
     const int c = (int)(i % q);
     const int64_t id = ids[m];
+    DLT_DASSERT(id >= 0 && id < V);
     float4 v;
     if (wdt == 0) {
       v = *(reinterpret_cast<const float4*>(W) + (size_t)id * q + c);
@@ -29,29 +30,31 @@ __global__ __launch_bounds__(256) void k_embedding_fwd(const int64_t* __restrict
 
 // dW[ids[m], :] += dout[m, :]   (one 256-B contiguous atomic wave-instruction per 64 lanes)
 __global__ __launch_bounds__(256) void k_embedding_bwd(const int64_t* __restrict__ ids, const float* __restrict__ dout,
-                                                       float* __restrict__ dW, int M, int H) {
+                                                       float* __restrict__ dW, int M, int H, int V) {
   const size_t total = (size_t)M * H;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
     const int m = (int)(i / H);
     const int h = (int)(i % H);
+    DLT_DASSERT(ids[m] >= 0 && ids[m] < V);
     unsafeAtomicAdd(dW + (size_t)ids[m] * H + h, dout[i]);
   }
 }
 
-DLT_API int dlt_embedding_fwd(const int64_t* ids, const void* W, int wdt, float* out, int M, int H, hipStream_t s) {
+DLT_API int dlt_embedding_fwd(const int64_t* ids, const void* W, int wdt, float* out, int M, int H, int V,
+                              hipStream_t s) {
   if (H % 4) return -1;
   const size_t total = (size_t)M * (H / 4);
   int blocks = (int)((total + 255) / 256);
   if (blocks > 8192) blocks = 8192;
-  k_embedding_fwd<<<blocks, 256, 0, s>>>(ids, W, wdt, out, M, H);
+  k_embedding_fwd<<<blocks, 256, 0, s>>>(ids, W, wdt, out, M, H, V);
   DLT_CHECK_LAUNCH();
 }
 
-DLT_API int dlt_embedding_bwd(const int64_t* ids, const float* dout, float* dW, int M, int H, hipStream_t s) {
+DLT_API int dlt_embedding_bwd(const int64_t* ids, const float* dout, float* dW, int M, int H, int V, hipStream_t s) {
   const size_t total = (size_t)M * H;
   int blocks = (int)((total + 255) / 256);
   if (blocks > 8192) blocks = 8192;
-  k_embedding_bwd<<<blocks, 256, 0, s>>>(ids, dout, dW, M, H);
+  k_embedding_bwd<<<blocks, 256, 0, s>>>(ids, dout, dW, M, H, V);
   DLT_CHECK_LAUNCH();
 }
 

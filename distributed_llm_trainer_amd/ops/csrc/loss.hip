@@ -22,6 +22,7 @@ __global__ __launch_bounds__(256) void k_ce_fwd_bwd(bf16_t* __restrict__ logits,
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   bf16_t* lrow = logits + (size_t)row * Vp;
   const int64_t tgt = targets[row];
+  DLT_DASSERT(tgt == -100 || (tgt >= 0 && tgt < V));  // ignore_index or a real token
   const bool valid = tgt >= 0 && tgt < V;
   const int nchunk = Vp >> 3;
   // pass 1: online max / sum-exp
@@ -90,6 +91,7 @@ __global__ __launch_bounds__(512) void k_ce_row(bf16_t* __restrict__ logits, con
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   bf16_t* lrow = logits + (size_t)row * Vp;
   const int64_t tgt = targets[row];
+  DLT_DASSERT(tgt == -100 || (tgt >= 0 && tgt < V));  // ignore_index or a real token
   const bool valid = tgt >= 0 && tgt < V;
   const int tchunk = valid ? (int)(tgt >> 3) : -1;
   const int nchunk = Vp >> 3;

@@ -20,7 +20,9 @@ import torch
 from . import rng
 
 _LIB = None
-_LIBPATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_dlt_kernels.so")
+# DLT_KERNEL_DEBUG=1 loads the bounds-checked build (ops/build.py --debug)
+_LIBPATH = os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                        "_dlt_kernels_debug.so" if os.environ.get("DLT_KERNEL_DEBUG") == "1" else "_dlt_kernels.so")
 
 c_void_p, c_int, c_float, c_uint32, c_int64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_uint32, ctypes.c_int64
 
@@ -29,8 +31,8 @@ _SIGS = {
                                     c_float, c_uint32, c_uint32, c_float, c_void_p],
     "dlt_rmsnorm_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                         c_void_p, c_int, c_int, c_uint32, c_uint32, c_float, c_void_p],
-    "dlt_embedding_fwd": [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p],
-    "dlt_embedding_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "dlt_embedding_fwd": [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p],
+    "dlt_embedding_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "dlt_rope_qkv_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                          c_void_p],
     "dlt_rope_qkv_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
@@ -128,7 +130,7 @@ def embedding_fwd(ids: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     _req(weight, weight.dtype, "embedding.weight")
     out = torch.empty(M, H, dtype=torch.float32, device=weight.device)
     _chk(lib().dlt_embedding_fwd(_p(ids), _p(weight), 0 if weight.dtype == torch.float32 else 1, _p(out), M, H,
-                                 _stream()), "embedding_fwd")
+                                 V, _stream()), "embedding_fwd")
     return out
 
 
@@ -140,7 +142,8 @@ def embedding_bwd(ids: torch.Tensor, dout: torch.Tensor, dweight: torch.Tensor) 
     H = dweight.shape[-1]
     _req(dout, torch.float32, "embedding_bwd.dout", M * H)
     _req(dweight, torch.float32, "embedding_bwd.dweight")
-    _chk(lib().dlt_embedding_bwd(_p(ids), _p(dout), _p(dweight), M, H, _stream()), "embedding_bwd")
+    _chk(lib().dlt_embedding_bwd(_p(ids), _p(dout), _p(dweight), M, H, dweight.shape[0], _stream()),
+         "embedding_bwd")
 
 
 # ---------------------------------------------------------------- RMSNorm
