@@ -184,8 +184,11 @@ __device__ __forceinline__ bf16x8_t load_row8(const bf16_t* __restrict__ p, bool
 
 // ============================================================================ dropout bits
 // Keep-bit words in two layouts (one hash per element pair, computed once):
-//   mask [bh][q][w]  bit j = keep(q, key = 32w + j)   -- lane = query (fwd, dQ)
-//   maskT[bh][k][w]  bit j = keep(q = 32w + j, key k) -- lane = key   (dK/dV)
+//   mask [bh][w][q]  bit j = keep(q, key = 32w + j)   -- lane = query (fwd, dQ)
+//   maskT[bh][w][k]  bit j = keep(q = 32w + j, key k) -- lane = key   (dK/dV)
+// Word-major: the 32 lanes that write (here) or read (MFMA kernels: lane = row) one
+// word index touch 128 contiguous bytes; the row-major [bh][q][w] layout made every
+// lane's 4-byte access its own cache line (the store side cost ~3x the hashing).
 // Only causal 32x32 tiles (key word <= query band) exist.  One half-wave per tile:
 // lane l hashes row q = 32r + l (16 hashes -> its row word), then a 5-stage butterfly
 // bit transpose gives lane j the column word of key 32w + j.
@@ -226,7 +229,7 @@ __global__ __launch_bounds__(256) void k_dropout_bits(uint32_t* __restrict__ mas
         word |= (uint32_t)(bits >= thr) << j;
       }
     }
-    mask[((size_t)bh * S + q) * W + w] = word;
+    mask[((size_t)bh * W + w) * S + q] = word;  // word-major: the half-wave's 32 rows are contiguous
   }
   // 32x32 bit transpose within each half-wave (lane l holds row l; afterwards lane j
   // holds column j): 5 butterfly stages, each one lane^d exchange + 4 bit ops.
@@ -239,7 +242,7 @@ __global__ __launch_bounds__(256) void k_dropout_bits(uint32_t* __restrict__ mas
     col = (l & d) ? ((col & ~m) | ((y >> d) & m)) : ((col & m) | ((y & m) << d));
   }
   const int kk = w * 32 + l;
-  if (active && kk < S) maskT[((size_t)bh * S + kk) * W + r] = col;
+  if (active && kk < S) maskT[((size_t)bh * W + r) * S + kk] = col;
 }
 
 // ============================================================================ work map
@@ -378,7 +381,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     if (it == 1 && qb >= nrb - 1 - pair) break;      // odd nrb: middle item once
     const int q0 = qb * RB + wid * 32;  // this wave's first query (wave-uniform)
     const int qa = q0 + ql;
-    const uint32_t* mrow = mask ? mask + ((size_t)bh * S + min(qa, S - 1)) * W : nullptr;
+    const uint32_t* mrow = mask ? mask + (size_t)bh * W * S + min(qa, S - 1) : nullptr;  // word j at mrow[j*S]
 
     bf16x8_t qf[4];
 #pragma unroll
@@ -400,7 +403,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     // item (straight-line unmasked loop, unrolled by two so every LDS address is
     // lane-base + immediate); tile qb holds the diagonal.
     uint2 mw_cur = make_uint2(0u, 0u), mw_next = make_uint2(0u, 0u);
-    if (DROP) mw_cur = make_uint2(mrow[0], W > 1 ? mrow[1] : 0u);  // words of tile 0
+    if (DROP) mw_cur = make_uint2(mrow[0], W > 1 ? mrow[S] : 0u);  // words of tile 0
     auto step = [&](auto bufc, auto maskc, int kb) {
       constexpr int BUF = decltype(bufc)::value;
       constexpr bool MASKED = decltype(maskc)::value;
@@ -409,7 +412,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         bf16_t* Kn = lds + (BUF ^ 1) * 2 * KVB * HD;
         glds_tile(k + hin, (kb + 1) * KVB, S, in_rs, Kn, wid, lane);
         glds_tile(v + hin, (kb + 1) * KVB, S, in_rs, Kn + KVB * HD, wid, lane);
-        if (DROP) mw_next = make_uint2(mrow[2 * (kb + 1)], 2 * (kb + 1) + 1 < W ? mrow[2 * (kb + 1) + 1] : 0u);
+        if (DROP) mw_next = make_uint2(mrow[(size_t)(2 * (kb + 1)) * S], 2 * (kb + 1) + 1 < W ? mrow[(size_t)(2 * (kb + 1) + 1) * S] : 0u);
       }
       const bf16_t* Kt = lds + BUF * 2 * KVB * HD;
       const bf16_t* Vt = Kt + KVB * HD;
@@ -580,7 +583,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     const int k0 = kblk * RB + wid * 32;  // wave-uniform
     const int ka = k0 + kl;
     // this lane's key column of the transposed keep-bit mask: one word per 32 queries
-    const uint32_t* mcol = DROP ? maskT + ((size_t)bh * S + min(ka, S - 1)) * W : nullptr;
+    const uint32_t* mcol = DROP ? maskT + (size_t)bh * W * S + min(ka, S - 1) : nullptr;  // word j at mcol[j*S]
 
     bf16x8_t kf[4], vf[4];
     const int kc = min(ka, S - 1);
@@ -599,7 +602,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       glds_tile(dob, t * QSTEP, S, rstride, lds + buf * 2 * QSTEP * HD + QSTEP * HD, wid, lane);
       if (DROP) {  // this lane's two 32-query keep words of tile t (consumed one tile later)
         const int w0 = (t * QSTEP) >> 5;
-        mw_next = make_uint2(mcol[w0], (w0 + 1 < W) ? mcol[w0 + 1] : 0u);
+        mw_next = make_uint2(mcol[(size_t)w0 * S], (w0 + 1 < W) ? mcol[(size_t)(w0 + 1) * S] : 0u);
       }
       if (tid < QSTEP) {
         const int qq = min(t * QSTEP + tid, S - 1);
@@ -738,7 +741,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     const int qa = q0 + ql;
     const bool qok = qa < S;
     const int qc = min(qa, S - 1);
-    const uint32_t* mrow = mask ? mask + ((size_t)bh * S + qc) * W : nullptr;
+    const uint32_t* mrow = mask ? mask + (size_t)bh * W * S + qc : nullptr;  // word j at mrow[j*S]
 
     bf16x8_t qf[4], df[4];
     const size_t orow = (((size_t)b * S + qc) * nh + head) * HD;
@@ -764,7 +767,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     // Same loop structure as the forward: straight-line unmasked tiles (static LDS
     // buffers, unrolled by two), then the diagonal tile.
     uint2 mw_cur = make_uint2(0u, 0u), mw_next = make_uint2(0u, 0u);
-    if (DROP) mw_cur = make_uint2(mrow[0], W > 1 ? mrow[1] : 0u);
+    if (DROP) mw_cur = make_uint2(mrow[0], W > 1 ? mrow[S] : 0u);
     auto step = [&](auto bufc, auto maskc, int kb) {
       constexpr int BUF = decltype(bufc)::value;
       constexpr bool MASKED = decltype(maskc)::value;
@@ -773,7 +776,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         bf16_t* Kn = lds + (BUF ^ 1) * 2 * KVB * HD;
         glds_tile(k + hin, (kb + 1) * KVB, S, in_rs, Kn, wid, lane);
         glds_tile(v + hin, (kb + 1) * KVB, S, in_rs, Kn + KVB * HD, wid, lane);
-        if (DROP) mw_next = make_uint2(mrow[2 * (kb + 1)], 2 * (kb + 1) + 1 < W ? mrow[2 * (kb + 1) + 1] : 0u);
+        if (DROP) mw_next = make_uint2(mrow[(size_t)(2 * (kb + 1)) * S], 2 * (kb + 1) + 1 < W ? mrow[(size_t)(2 * (kb + 1) + 1) * S] : 0u);
       }
       const bf16_t* Kt = lds + BUF * 2 * KVB * HD;
       const bf16_t* Vt = Kt + KVB * HD;
@@ -812,7 +815,7 @@ static int xcd_map_enabled() {
   }
   return v;
 }
-// mask: uint32 [2][B*nh, S, ceil(S/32)] keep-bits written by the forward when dropout
+// mask: uint32 [2][B*nh, ceil(S/32), S] keep-bits written by the forward when dropout
 // is on -- [0] row layout (lane = query), [1] transposed (lane = key), see
 // k_dropout_bits.
 // Keep-bit masks only (they depend on the key, not on the data): lets the engine

@@ -254,17 +254,17 @@ def _off(t: torch.Tensor, elems: int):
 
 # -------------------------------------------------------------- attention
 class AttnAux(tuple):
-    """(lse [B,nh,S] fp32, keep-bit masks [2, B*nh, S, ceil(S/32)] int32 or None:
-    [0] = bits by (query, key word), [1] = bits by (key, query word))."""
+    """(lse [B,nh,S] fp32, keep-bit masks [2, B*nh, ceil(S/32), S] int32 or None:
+    [0] = bits by (key word, query), [1] = bits by (query word, key); word-major)."""
 
 
 def attention_dropout_mask(B, nh, S, p, key, device=None):
-    """Keep-bit masks [2, B*nh, S, ceil(S/32)] for attention dropout (None if p == 0).
+    """Keep-bit masks [2, B*nh, ceil(S/32), S] for attention dropout (None if p == 0).
     Data-independent, so the engine builds them on a side stream ahead of time."""
     thr = rng.keep_threshold(p)
     if not thr:
         return None
-    mask = torch.empty(2, B * nh, S, (S + 31) // 32, dtype=torch.int32, device=device)
+    mask = torch.empty(2, B * nh, (S + 31) // 32, S, dtype=torch.int32, device=device)
     _chk(lib().dlt_attn_dropout_mask(_p(mask), B, nh, S, key & 0xFFFFFFFF, thr, _stream()), "attn_dropout_mask")
     return mask
 
@@ -293,7 +293,7 @@ def attention_fwd(q, k, v, p, key, causal=True, store_mask=True, out=None, mask=
         gen = 0
     elif store_mask:
         # [0] row layout (lane = query), [1] transposed (lane = key) -- see attention.hip
-        mask = torch.empty(2, B * nh, S, (S + 31) // 32, dtype=torch.int32, device=q.device)
+        mask = torch.empty(2, B * nh, (S + 31) // 32, S, dtype=torch.int32, device=q.device)
     _chk(lib().dlt_attn_fwd(_p(q), _p(k), _p(v), _p(o), _p(lse), _p(mask), B, nh, S, hd, 1.0 / math.sqrt(hd),
                             key & 0xFFFFFFFF, thr, dscale, gen, _stream()), "attn_fwd")
     return o, AttnAux((lse, mask))
@@ -326,7 +326,7 @@ def attention_fwd_packed(qkv, B, S, nh, p, key, out=None, mask=None, store_mask=
         _req(mask, torch.int32, "attn.mask", 2 * B * nh * S * ((S + 31) // 32))
         gen = 0
     elif store_mask:
-        mask = torch.empty(2, B * nh, S, (S + 31) // 32, dtype=torch.int32, device=qkv.device)
+        mask = torch.empty(2, B * nh, (S + 31) // 32, S, dtype=torch.int32, device=qkv.device)
     _chk(lib().dlt_attn_fwd_ex(_p(qkv), _off(qkv, H), _off(qkv, 2 * H), _p(o), _p(lse), _p(mask), B, nh, S, hd,
                                1.0 / math.sqrt(hd), key & 0xFFFFFFFF, thr, dscale, gen, S * 3 * H, hd, 3 * H,
                                _stream()), "attn_fwd_packed")

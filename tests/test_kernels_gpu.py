@@ -164,12 +164,12 @@ def test_attention_fwd(S, p):
     if p > 0:
         keep = rng.attn_keep_mask(B * nh, S, S, key, p, device=DEV)
         W = (S + 31) // 32
-        bits = aux[1][0].view(B * nh, S, W)
+        bits = aux[1][0].view(B * nh, W, S).transpose(1, 2)  # word-major [bh][word][query]
         kk = torch.arange(S, device=DEV)
         got = ((bits[:, :, kk // 32].long() >> (kk % 32)) & 1).bool()
         causal = torch.tril(torch.ones(S, S, dtype=torch.bool, device=DEV))
         assert torch.equal(got & causal, keep & causal), "stored dropout bitmask differs from the hash"
-        bitsT = aux[1][1].view(B * nh, S, W)  # [bh][key][query word]
+        bitsT = aux[1][1].view(B * nh, W, S).transpose(1, 2)  # [bh][key][query word]
         qq = torch.arange(S, device=DEV)
         gotT = ((bitsT[:, :, qq // 32].long() >> (qq % 32)) & 1).bool()  # [bh][key][query]
         assert torch.equal(gotT.transpose(1, 2) & causal, keep & causal), "transposed bitmask differs"
