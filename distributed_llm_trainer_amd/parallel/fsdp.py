@@ -242,10 +242,11 @@ class FSDPRuntime(ParamProvider):
                 dist.all_reduce(out, group=self.rep_pg)
             if out.numel() != u.shard:  # NO_SHARD: full buffer == shard
                 out = out[:u.shard]
+            # add_ promotes the bf16 wire tensor inside the kernel: no separate cast pass
             if self.cpu_offload:
-                u.grad.add_(out.float().cpu())
+                u.grad.add_(out.cpu())
             else:
-                u.grad.add_(out.float())
+                u.grad.add_(out)
         u.rs_pending.clear()
 
     def finish(self):
