@@ -334,7 +334,7 @@ def main(argv=None):
         dbg.check_replicas(trainer.store.flat)
     start_time = time.time()
     start_step = trainer.global_step
-    steady_t0, steady_tok0 = None, 0
+    steady_t0, steady_tok0, steady_ckpt = None, 0, 0.0
     for step in range(start_step, tc.max_steps):
         dbg.maybe_inject_fault(step, trainer.rank)
         try:
@@ -364,7 +364,13 @@ def main(argv=None):
         if check_every and (step + 1) % check_every == 0:
             dbg.check_replicas(trainer.store.flat)
         if step > 0 and step % tc.save_interval == 0:
+            t_ck = time.time()
             trainer.save_checkpoint(f"{tc.checkpoint_dir}/step_{step}.pt")
+            if steady_t0 is not None:  # checkpoint I/O is not training throughput
+                steady_ckpt += time.time() - t_ck
+    if trainer.device.type == "cuda":
+        torch.cuda.synchronize(trainer.device)
+    steady_t1 = time.time()
     prof.close()
     if not args.no_final_save:
         trainer.save_checkpoint(f"{tc.checkpoint_dir}/final.pt")
@@ -376,7 +382,7 @@ def main(argv=None):
         print(f"\nTraining complete! Total time: {total_time:.2f}s")
         print(f"Total tokens processed: {trainer.tokens_seen:,}")
         if steady_t0 is not None:
-            dt = time.time() - steady_t0
+            dt = max(steady_t1 - steady_t0 - steady_ckpt, 1e-9)
             sps = (trainer.tokens_seen - steady_tok0) / dt
             fpt = model_config.flops_per_token(seq_len, recompute=bool(model_config.gradient_checkpointing))
             mfu = sps / trainer.world_size * fpt / PEAK_BF16_FLOPS
