@@ -162,7 +162,8 @@ def test_decode_graph_matches_eager():
             assert torch.allclose(a, b, atol=2e-2, rtol=2e-2), (t, (a - b).abs().max().item())
 
 
-def test_pipelined_window_matches_sequential_gpu():
+@pytest.mark.parametrize("recompute", [False, True])
+def test_pipelined_window_matches_sequential_gpu(recompute):
     """Two-stream micro-step pipelining (fwd k+1 || bwd k) == the sequential schedule:
     same losses and dropout masks; gradients equal up to fp32 atomic-add order."""
     from distributed_llm_trainer_amd.models.engine import shift_targets
@@ -170,6 +171,7 @@ def test_pipelined_window_matches_sequential_gpu():
     base = GPT(_cfg(0.1)).to(DEV)
     m1, m2 = copy.deepcopy(base), copy.deepcopy(base)
     e1, e2 = m1.enable_engine(seed=9), m2.enable_engine(seed=9)
+    m1.gradient_checkpointing = m2.gradient_checkpointing = recompute
     GA = 4
     data = torch.randint(0, 1000, (GA, 2, 256), device=DEV)
     seq = []
@@ -179,7 +181,7 @@ def test_pipelined_window_matches_sequential_gpu():
         (loss / GA).backward()
         seq.append(loss.item())
     win = e2.train_window([data[j] for j in range(GA)], [shift_targets(data[j]) for j in range(GA)],
-                          torch.full((), 1.0 / GA, device=DEV))
+                          torch.full((), 1.0 / GA, device=DEV), recompute=recompute)
     torch.cuda.synchronize()
     for a, b in zip(seq, win):
         assert abs(a - b.item()) < 1e-5 * abs(a), (seq, [w.item() for w in win])
