@@ -509,7 +509,7 @@ class GPTEngine:
     # ------------------------------------------------------ pipelined window
     def train_window(self, micro_ids: List[torch.Tensor], micro_targets: List[torch.Tensor],
                      dloss: torch.Tensor, recompute: bool = False,
-                     before_last: Optional[Callable[[], None]] = None) -> List[torch.Tensor]:
+                     before_last: Optional[Callable[[], None]] = None, defer: bool = True) -> List[torch.Tensor]:
         """Forward + backward of a whole gradient-accumulation window.
 
         Schedule (GA = 4):  F0 | B0+F1 | B1+F2 | B2+F3 | B3, where "Bk+Fk+1" issues the
@@ -525,13 +525,17 @@ class GPTEngine:
 
         ``dloss`` is d(total)/d(micro-step loss) (1/GA), ``before_last`` runs before
         the last backward is issued (the DDP runtime switches its sync on there).
+        ``defer=False`` (the FSDP runtime, which reduce-scatters every micro-step) runs
+        each micro-step's weight gradients in its own backward; the provider must then
+        give every micro-step fresh gradient buffers (FSDP's per-micro-step full_grad),
+        since two backwards may overlap on the GPU.
         Returns the GA micro-step losses (device scalars, unscaled).  Dropout streams,
         numerics and gradients are identical to running the micro-steps one by one.
         """
         GA = len(micro_ids)
         dev = micro_ids[0].device
         cuda = dev.type == "cuda"
-        self.set_accumulation(0, GA, defer=True)
+        self.set_accumulation(0, GA, defer=defer)
         main = pipe = None
         if cuda:
             main = torch.cuda.current_stream(dev)
@@ -555,7 +559,7 @@ class GPTEngine:
 
         def fwd(k):
             return self._forward_gen(micro_ids[k], micro_targets[k], True, recompute, need_backward=True,
-                                     acc=(k, GA, True))
+                                     acc=(k, GA, defer))
 
         losses: List[Any] = [None] * GA
         states: List[Any] = [None] * GA

@@ -79,6 +79,8 @@ class FlatUnit:
         self.full_grad: Optional[torch.Tensor] = None   # full fp32 grads during backward
         self.ag_work = None
         self.rs_pending = []
+        self.refs = 0            # chains (forward / backward of a micro-step) using `full`
+        self.ready_ev = None     # HIP event: `full` is complete (recorded after the gather wait)
 
     def local_slice(self) -> Tuple[int, int]:
         return self.rank * self.shard, (self.rank + 1) * self.shard
@@ -206,17 +208,44 @@ class FSDPRuntime(ParamProvider):
                 u.ag_work = None
 
     def _wait_gather(self, u: FlatUnit):
+        waited = False
         if u.full is None:
             self._gather(u, async_op=False)
+            waited = True
         if u.ag_work is not None:
             u.ag_work.wait()
             u.ag_work = None
+            waited = True
+        if waited and u.full is not None and u.full.is_cuda:
+            u.ready_ev = torch.cuda.Event()
+            u.ready_ev.record()
+
+    # Residency is reference-counted so that two chains (the forward of micro-step k+1
+    # and the backward of micro-step k, interleaved on two HIP streams by
+    # GPTEngine.train_window) can share a gathered unit: the buffer is resharded only
+    # when the last user releases it, every user's stream waits for the gather's
+    # completion event, and the buffer is recorded on every stream that read it.
+    def _acquire(self, u: FlatUnit):
+        self._wait_gather(u)
+        if u.full is not None and u.full.is_cuda:
+            cur = torch.cuda.current_stream(self.device)
+            if u.ready_ev is not None:
+                cur.wait_event(u.ready_ev)
+            if u.full is not u.shard_c:
+                u.full.record_stream(cur)
+        u.refs += 1
+
+    def _release(self, u: FlatUnit, reshard: bool):
+        u.refs = max(0, u.refs - 1)
+        if reshard and u.refs == 0:
+            self._reshard(u)
 
     def _reshard(self, u: FlatUnit):
         if u.ag_work is not None:
             u.ag_work.wait()
             u.ag_work = None
         u.full = None
+        u.ready_ev = None
 
     def _reduce(self, u: FlatUnit):
         """Sum full-size grads over ranks into this rank's fp32 shard grad (async)."""
@@ -242,6 +271,8 @@ class FSDPRuntime(ParamProvider):
                 dist.all_reduce(out, group=self.rep_pg)
             if out.numel() != u.shard:  # NO_SHARD: full buffer == shard
                 out = out[:u.shard]
+            if out.is_cuda:  # produced on the backward's stream (maybe the pipeline stream)
+                out.record_stream(torch.cuda.current_stream(out.device))
             # add_ promotes the bf16 wire tensor inside the kernel: no separate cast pass
             if self.cpu_offload:
                 u.grad.add_(out.cpu())
@@ -316,22 +347,18 @@ class FSDPRuntime(ParamProvider):
 
     def pre_forward(self, uid):
         u = self.units[uid]
-        if u.full is None:
-            self._gather(u, async_op=False)
+        self._acquire(u)
         nxt = self._next(uid, True)
         if nxt is not None:  # forward prefetch of the next unit
             self._gather(self.units[nxt], async_op=True)
 
     def post_forward(self, uid):
-        if uid == "head":
-            return  # the root stays gathered for the whole step (like FSDP's root)
-        if self.strategy in ("FULL_SHARD", "HYBRID_SHARD"):
-            self._reshard(self.units[uid])
+        # the root stays gathered until its backward (like FSDP's root unit)
+        self._release(self.units[uid], reshard=uid != "head" and self.strategy in ("FULL_SHARD", "HYBRID_SHARD"))
 
     def pre_backward(self, uid):
         u = self.units[uid]
-        if u.full is None:
-            self._gather(u, async_op=False)
+        self._acquire(u)
         if self.prefetch == "BACKWARD_PRE":
             nxt = self._next(uid, False)
             if nxt is not None and nxt != "head":
@@ -342,16 +369,11 @@ class FSDPRuntime(ParamProvider):
         do_reduce = self.sync or self.sync_every_micro_step
         if do_reduce:
             self._reduce(u)
-        if uid != "head":
-            if self.strategy != "NO_SHARD":
-                self._reshard(u)
-            if self.prefetch == "BACKWARD_POST":
-                nxt = self._next(uid, False)
-                if nxt is not None and nxt != "head":
-                    self._gather(self.units[nxt], async_op=True)
-        else:
-            if self.strategy != "NO_SHARD":
-                self._reshard(u)
+        self._release(u, reshard=self.strategy != "NO_SHARD")
+        if uid != "head" and self.prefetch == "BACKWARD_POST":
+            nxt = self._next(uid, False)
+            if nxt is not None and nxt != "head":
+                self._gather(self.units[nxt], async_op=True)
 
     def require_sync(self, flag: bool):
         self.sync = bool(flag)

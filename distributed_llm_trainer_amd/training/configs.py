@@ -70,6 +70,7 @@ class FSDPTrainingConfig:
     lr_schedule_fix: bool = True
     adam_eps: float = 1e-8
     eval_interval: int = 500
+    pipeline_micro_steps: bool = True  # overlap fwd(k+1) with bwd(k) on two HIP streams
 
 
 @dataclass

@@ -113,14 +113,33 @@ class FSDPTrainer:
         micro_bs = input_ids.shape[0] // GA
         total = torch.zeros((), dtype=torch.float32, device=self.device)
         rt.zero_grad()
-        for micro in range(GA):
+        defer = not self.fsdp_config.sync_every_micro_step
+        eng = self.model.engine
+        # micro-step pipelining (GPTEngine.train_window) from the second step on (the
+        # first runs the GEMM autotuning); units are shared by the two chains through
+        # the runtime's reference-counted residency
+        pipelined = (GA > 1 and getattr(tc, "pipeline_micro_steps", True) and getattr(self, "_engine_warm", False)
+                     and (self.device.type != "cuda" or getattr(eng.gemm, "stream_safe", False))
+                     and os.environ.get("DLT_PIPELINE", "1") != "0")
+        if pipelined:
+            from ..models.engine import shift_targets
+            ids_l = [input_ids[m * micro_bs:(m + 1) * micro_bs] for m in range(GA)]
+            rt.require_sync(False)
+            losses = eng.train_window(ids_l, [shift_targets(x) for x in ids_l],
+                                      torch.full((), 1.0 / GA, dtype=torch.float32, device=self.device),
+                                      recompute=bool(self.model.gradient_checkpointing),
+                                      before_last=lambda: rt.require_sync(True), defer=defer)
+            for loss in losses:
+                total += (loss / GA).detach().float()
+        for micro in range(GA if pipelined else 0, GA):
             ids = input_ids[micro * micro_bs:(micro + 1) * micro_bs]
             rt.require_sync(micro == GA - 1)
-            self.model.engine.set_accumulation(micro, GA, defer=not self.fsdp_config.sync_every_micro_step)
+            eng.set_accumulation(micro, GA, defer=defer)
             _, loss = self.model(ids, labels=ids)
             loss = loss / GA
             loss.backward()
             total += loss.detach().float()
+        self._engine_warm = True
         rt.finish()
         # global grad norm: local shard sumsq -> scalar all-reduce (reference X8)
         ss = self.optimizer.local_sumsq()

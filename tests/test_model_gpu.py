@@ -189,3 +189,24 @@ def test_pipelined_window_matches_sequential_gpu(recompute):
     for n in g1:
         err = (g1[n] - g2[n]).abs().max().item()
         assert err <= 1e-5 * max(1e-3, g1[n].abs().max().item()) + 1e-7, (n, err)
+
+
+@pytest.mark.parametrize("ac", [True, False])
+def test_fsdp_pipelined_matches_sequential_gpu(ac):
+    """FSDP trainer on one GPU: pipelined micro-steps (two HIP streams sharing gathered
+    units through the runtime's reference counts) == the sequential schedule."""
+    from distributed_llm_trainer_amd.training.configs import FSDPConfig, FSDPTrainingConfig
+    from distributed_llm_trainer_amd.training.fsdp_trainer import FSDPTrainer
+    data = torch.randint(0, 1000, (8, 256), device=DEV, generator=torch.Generator(DEV).manual_seed(8))
+    res = []
+    for pipe in (False, True):
+        torch.manual_seed(8)
+        tc = FSDPTrainingConfig(batch_size=2, gradient_accumulation_steps=4, warmup_steps=1, learning_rate=1e-5,
+                                pipeline_micro_steps=pipe)
+        tr = FSDPTrainer(_cfg(0.1), tc, FSDPConfig(activation_checkpointing=ac))
+        losses = [tr.train_step({"input_ids": data})["loss"] for _ in range(4)]
+        res.append((losses, {k: v.float().clone() for k, v in tr.runtime.state_dict_full().items()}))
+    for a, b in zip(res[0][0], res[1][0]):
+        assert abs(a - b) < 1e-4 * abs(a), (res[0][0], res[1][0])
+    for k in res[0][1]:
+        assert (res[0][1][k] - res[1][1][k]).abs().max().item() < 2e-4, k

@@ -111,3 +111,25 @@ def test_engine_packed_matches_split_path(monkeypatch):
         grads.append([p.grad.clone() for p in m.parameters()])
     for a, b in zip(*grads):
         assert torch.allclose(a, b, atol=1e-6, rtol=1e-5)
+
+
+@pytest.mark.parametrize("sync_every", [True, False])
+@pytest.mark.parametrize("strategy", ["FULL_SHARD", "SHARD_GRAD_OP"])
+def test_fsdp_trainer_pipelined_matches_sequential(strategy, sync_every):
+    """The FSDP runtime under the pipelined window (reference-counted unit residency,
+    per-micro-step or deferred reduce) == its sequential schedule."""
+    from distributed_llm_trainer_amd.training.configs import FSDPConfig, FSDPTrainingConfig
+    from distributed_llm_trainer_amd.training.fsdp_trainer import FSDPTrainer
+    torch.manual_seed(16)
+    data = torch.randint(0, 256, (8, 32))
+    res = []
+    for pipe in (False, True):
+        tc = FSDPTrainingConfig(batch_size=2, gradient_accumulation_steps=4, warmup_steps=2, max_steps=10,
+                                pipeline_micro_steps=pipe)
+        fc = FSDPConfig(sharding_strategy=strategy, sync_every_micro_step=sync_every)
+        tr = FSDPTrainer(tiny(), tc, fc)
+        losses = [tr.train_step({"input_ids": data})["loss"] for _ in range(3)]
+        res.append((losses, tr.runtime.state_dict_full()))
+    assert res[0][0] == res[1][0]
+    for k in res[0][1]:
+        assert torch.allclose(res[0][1][k], res[1][1][k], atol=1e-7, rtol=1e-6), k
