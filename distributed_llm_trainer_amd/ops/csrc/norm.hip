@@ -31,9 +31,20 @@ __device__ __forceinline__ void ld_bf4(const bf16_t* p, float (&v)[4]) {
   for (int e = 0; e < 4; ++e) v[e] = bf2f(d.v[e]);
 }
 
+// Norm weight: fp32 (flat master, DDP path) or bf16 (the gathered FSDP unit) -- read in
+// place, so the FSDP path needs no per-call weight upcast kernel.
+__device__ __forceinline__ f4 ld_w4(const void* w, int wbf16, int off) {
+  if (wbf16) {
+    f4 r;
+    ld_bf4(reinterpret_cast<const bf16_t*>(w) + off, r.v);
+    return r;
+  }
+  return ld_f4(reinterpret_cast<const float*>(w) + off);
+}
+
 template <int NCH>
 __global__ __launch_bounds__(256) void k_add_dropout_rmsnorm_fwd(
-    const float* __restrict__ resid, const bf16_t* __restrict__ delta, const float* __restrict__ w,
+    const float* __restrict__ resid, const bf16_t* __restrict__ delta, const void* __restrict__ w, int wbf16,
     float* __restrict__ x_out, bf16_t* __restrict__ y_out, float* __restrict__ rstd_out,
     int M, int H, float eps, uint32_t key, uint32_t thr, float dscale) {
   const int lane = threadIdx.x & 63;
@@ -83,7 +94,7 @@ __global__ __launch_bounds__(256) void k_add_dropout_rmsnorm_fwd(
     if (c < nc) {
       const size_t off = rbase + (size_t)c * 4;
       if (x_out) st_f4(x_out + off, xv[t]);
-      const f4 ww = ld_f4(w + c * 4);
+      const f4 ww = ld_w4(w, wbf16, c * 4);
       u16x4 y;
 #pragma unroll
       for (int e = 0; e < 4; ++e) y.v[e] = f2bf(xv[t][e] * rstd * ww.v[e]);
@@ -95,7 +106,7 @@ __global__ __launch_bounds__(256) void k_add_dropout_rmsnorm_fwd(
 template <int NCH>
 __global__ __launch_bounds__(256) void k_rmsnorm_bwd(
     const bf16_t* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ rstd_in,
-    const float* __restrict__ w, const float* dres, float* dx_out,
+    const void* __restrict__ w, int wbf16, const float* dres, float* dx_out,
     bf16_t* __restrict__ ddelta, float* __restrict__ dw, float* __restrict__ dw_part,
     const float* __restrict__ dy_scale, int M, int H, uint32_t key, uint32_t thr, float dscale) {
   extern __shared__ __attribute__((aligned(16))) float smem[];  // [4][H]
@@ -112,7 +123,7 @@ __global__ __launch_bounds__(256) void k_rmsnorm_bwd(
 #pragma unroll
     for (int e = 0; e < 4; ++e) { dwacc[t][e] = 0.f; wv[t][e] = 0.f; }
     if (c < nc) {
-      const f4 a = ld_f4(w + c * 4);
+      const f4 a = ld_w4(w, wbf16, c * 4);
 #pragma unroll
       for (int e = 0; e < 4; ++e) wv[t][e] = a.v[e];
     }
@@ -225,14 +236,14 @@ static inline int nch_of(int H) {
   return n;
 }
 
-DLT_API int dlt_add_dropout_rmsnorm_fwd(const float* resid, const bf16_t* delta, const float* w,
+DLT_API int dlt_add_dropout_rmsnorm_fwd(const float* resid, const bf16_t* delta, const void* w, int wbf16,
                                         float* x_out, bf16_t* y_out, float* rstd_out, int M, int H,
                                         float eps, uint32_t key, uint32_t thr, float dscale,
                                         hipStream_t stream) {
   if (H % 4 != 0 || H > 4096) return -1;
   const dim3 grid((M + 3) / 4), block(256);
   const int nch = nch_of(H);
-#define ARGS resid, delta, w, x_out, y_out, rstd_out, M, H, eps, key, thr, dscale
+#define ARGS resid, delta, w, wbf16, x_out, y_out, rstd_out, M, H, eps, key, thr, dscale
   switch (nch) {
     case 1: k_add_dropout_rmsnorm_fwd<1><<<grid, block, 0, stream>>>(ARGS); break;
     case 2: k_add_dropout_rmsnorm_fwd<2><<<grid, block, 0, stream>>>(ARGS); break;
@@ -249,7 +260,7 @@ DLT_API int dlt_add_dropout_rmsnorm_fwd(const float* resid, const bf16_t* delta,
   DLT_CHECK_LAUNCH();
 }
 
-DLT_API int dlt_rmsnorm_bwd(const bf16_t* dy, const float* x, const float* rstd, const float* w,
+DLT_API int dlt_rmsnorm_bwd(const bf16_t* dy, const float* x, const float* rstd, const void* w, int wbf16,
                             const float* dres, float* dx_out, bf16_t* ddelta, float* dw, float* dw_ws,
                             const float* dy_scale, int M, int H, uint32_t key, uint32_t thr,
                             float dscale, hipStream_t stream) {
@@ -261,7 +272,7 @@ DLT_API int dlt_rmsnorm_bwd(const bf16_t* dy, const float* x, const float* rstd,
   const dim3 grid(blocks), block(256);
   const size_t shm = (size_t)4 * H * sizeof(float);
   const int nch = nch_of(H);
-#define ARGS dy, x, rstd, w, dres, dx_out, ddelta, dw, dw_ws, dy_scale, M, H, key, thr, dscale
+#define ARGS dy, x, rstd, w, wbf16, dres, dx_out, ddelta, dw, dw_ws, dy_scale, M, H, key, thr, dscale
   switch (nch) {
     case 1: k_rmsnorm_bwd<1><<<grid, block, shm, stream>>>(ARGS); break;
     case 2: k_rmsnorm_bwd<2><<<grid, block, shm, stream>>>(ARGS); break;

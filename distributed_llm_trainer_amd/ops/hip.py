@@ -27,10 +27,10 @@ _LIBPATH = os.path.join(os.path.dirname(os.path.abspath(__file__)),
 c_void_p, c_int, c_float, c_uint32, c_int64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_uint32, ctypes.c_int64
 
 _SIGS = {
-    "dlt_add_dropout_rmsnorm_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
-                                    c_float, c_uint32, c_uint32, c_float, c_void_p],
-    "dlt_rmsnorm_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                        c_void_p, c_int, c_int, c_uint32, c_uint32, c_float, c_void_p],
+    "dlt_add_dropout_rmsnorm_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                                    c_int, c_float, c_uint32, c_uint32, c_float, c_void_p],
+    "dlt_rmsnorm_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                        c_void_p, c_void_p, c_int, c_int, c_uint32, c_uint32, c_float, c_void_p],
     "dlt_embedding_fwd": [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p],
     "dlt_embedding_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "dlt_rope_qkv_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
@@ -147,6 +147,19 @@ def embedding_bwd(ids: torch.Tensor, dout: torch.Tensor, dweight: torch.Tensor) 
 
 
 # ---------------------------------------------------------------- RMSNorm
+def _norm_weight(weight: torch.Tensor, H: int, name: str):
+    """(tensor, is_bf16): fp32 and bf16 norm weights are read in place by the kernels
+    (bf16 = the gathered FSDP unit); other dtypes are upcast once."""
+    if weight.dtype not in (torch.float32, torch.bfloat16):
+        weight = weight.float()
+    align = 8 if weight.dtype == torch.bfloat16 else 16  # u16x4 / float4 loads
+    if not weight.is_contiguous() or weight.data_ptr() % align:
+        weight = weight.contiguous().clone()
+    if not weight.is_cuda or weight.numel() != H:
+        raise ValueError(f"{name}: expected a GPU tensor of {H} elements")
+    return weight, int(weight.dtype == torch.bfloat16)
+
+
 def add_dropout_rmsnorm_fwd(resid, delta, weight, eps, p, key, out_dtype=torch.bfloat16, y_out=None):
     src = resid if resid is not None else delta
     M, H = src.shape
@@ -156,9 +169,7 @@ def add_dropout_rmsnorm_fwd(resid, delta, weight, eps, p, key, out_dtype=torch.b
         _req(resid, torch.float32, "rmsnorm.resid", M * H)
     if delta is not None:
         _req(delta, torch.bfloat16, "rmsnorm.delta", M * H)
-    w = weight if weight.dtype == torch.float32 else weight.float()
-    w = w.contiguous()
-    _req(w, torch.float32, "rmsnorm.weight", H)
+    w, wbf16 = _norm_weight(weight, H, "rmsnorm.weight")
     y = torch.empty(M, H, dtype=torch.bfloat16, device=src.device) if y_out is None else y_out
     _req(y, torch.bfloat16, "rmsnorm.y", M * H)
     rstd = torch.empty(M, dtype=torch.float32, device=src.device)
@@ -169,7 +180,8 @@ def add_dropout_rmsnorm_fwd(resid, delta, weight, eps, p, key, out_dtype=torch.b
         xo = x
     thr = rng.keep_threshold(p)
     dscale = 1.0 / (1.0 - p) if thr else 1.0
-    _chk(lib().dlt_add_dropout_rmsnorm_fwd(_p(resid), _p(delta), _p(w), _p(xo), _p(y), _p(rstd), M, H, float(eps),
+    _chk(lib().dlt_add_dropout_rmsnorm_fwd(_p(resid), _p(delta), _p(w), wbf16, _p(xo), _p(y), _p(rstd), M, H,
+                                           float(eps),
                                            key & 0xFFFFFFFF, thr, dscale, _stream()), "add_dropout_rmsnorm_fwd")
     return x, y, rstd
 
@@ -183,7 +195,7 @@ def rmsnorm_bwd(dy, x, rstd, weight, dres, dweight, p_prev, key_prev, dy_scale=N
     if dres is not None:
         _req(dres, torch.float32, "rmsnorm_bwd.dres", M * H)
     _req(dweight, torch.float32, "rmsnorm_bwd.dweight", H)
-    w = (weight if weight.dtype == torch.float32 else weight.float()).contiguous()
+    w, wbf16 = _norm_weight(weight, H, "rmsnorm_bwd.weight")
     scale_t = None
     if dy_scale is not None:
         scale_t = dy_scale.reshape(1).float().contiguous()
@@ -196,7 +208,7 @@ def rmsnorm_bwd(dy, x, rstd, weight, dres, dweight, p_prev, key_prev, dy_scale=N
     dscale = 1.0 / (1.0 - p_prev) if thr else 1.0
     # per-block dw partials (two-stage column reduction instead of same-address atomics)
     ws = torch.empty(min((M + 3) // 4, 1024) * H, dtype=torch.float32, device=x.device)
-    _chk(lib().dlt_rmsnorm_bwd(_p(dy), _p(x), _p(rstd), _p(w), _p(dres), _p(dx), _p(dd), _p(dweight), _p(ws),
+    _chk(lib().dlt_rmsnorm_bwd(_p(dy), _p(x), _p(rstd), _p(w), wbf16, _p(dres), _p(dx), _p(dd), _p(dweight), _p(ws),
                                _p(scale_t), M, H, key_prev & 0xFFFFFFFF, thr, dscale, _stream()), "rmsnorm_bwd")
     return dx, dd
 

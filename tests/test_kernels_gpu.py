@@ -325,3 +325,23 @@ def test_scale_bf16():
     x = torch.randn(64, 768, device=DEV).bfloat16()
     s = torch.tensor(0.25, device=DEV)
     _close(hip.scale_bf16(x, s), ref.scale_bf16(x, s), 1e-6, 0.0, "scale_bf16")
+
+
+def test_rmsnorm_bf16_weight_in_place():
+    """bf16 norm weights (the gathered FSDP unit) are read in place and give the same
+    result as the same values in fp32."""
+    torch.manual_seed(40)
+    M, H = 300, 768
+    r = torch.randn(M, H, device=DEV)
+    d = torch.randn(M, H, device=DEV).bfloat16()
+    wb = (torch.rand(H, device=DEV) + 0.5).bfloat16()
+    wf = wb.float()
+    x1, y1, s1 = hip.add_dropout_rmsnorm_fwd(r, d, wf, 1e-6, 0.1, 123)
+    x2, y2, s2 = hip.add_dropout_rmsnorm_fwd(r, d, wb, 1e-6, 0.1, 123)
+    assert torch.equal(y1, y2) and torch.equal(x1, x2)
+    dy = torch.randn(M, H, device=DEV).bfloat16()
+    dw1, dw2 = torch.zeros(H, device=DEV), torch.zeros(H, device=DEV)
+    g1 = hip.rmsnorm_bwd(dy, x1, s1, wf, None, dw1, 0.1, 77)
+    g2 = hip.rmsnorm_bwd(dy, x1, s1, wb, None, dw2, 0.1, 77)
+    assert torch.equal(g1[0], g2[0]) and torch.equal(g1[1], g2[1])
+    _close(dw1, dw2, 1e-4, 1e-5, "dw")
