@@ -45,6 +45,7 @@ _SIGS = {
     "dlt_adamw": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float, c_float,
                   c_float, c_float, c_float, c_void_p, c_void_p],
     "dlt_cast_bf16": [c_void_p, c_void_p, c_int64, c_void_p],
+    "dlt_add_bf16_f32": [c_void_p, c_void_p, c_int64, c_void_p],
     "dlt_wgrad_gemm": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
     "dlt_scale_bf16": [c_void_p, c_void_p, ctypes.c_long, c_void_p, c_void_p],
     "dlt_gemm_tn": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
@@ -458,6 +459,17 @@ def adamw_flat(param, grad, exp_avg, exp_avg_sq, shadow, lr, beta1, beta2, eps, 
     bc2 = 1.0 - beta2 ** step
     _chk(lib().dlt_adamw(_p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), _p(shadow), n, lr, beta1, beta2, eps, wd,
                          lr / bc1, 1.0 / math.sqrt(bc2), _p(gscale), _stream()), "adamw")
+
+
+def add_bf16_into_f32(dst: torch.Tensor, src: torch.Tensor) -> bool:
+    """dst (fp32) += src (bf16) in one kernel; False (nothing launched) if the shapes or
+    alignment do not fit the 8-wide vector path."""
+    n = dst.numel()
+    if (src.numel() != n or n % 8 or not dst.is_contiguous() or not src.is_contiguous()
+            or dst.dtype != torch.float32 or src.dtype != torch.bfloat16 or dst.data_ptr() % 16 or src.data_ptr() % 16):
+        return False
+    _chk(lib().dlt_add_bf16_f32(_p(dst), _p(src), n, _stream()), "add_bf16_f32")
+    return True
 
 
 def cast_bf16(x: torch.Tensor, y: torch.Tensor) -> None:

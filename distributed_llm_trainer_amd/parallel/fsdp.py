@@ -48,6 +48,12 @@ from ..models.engine import HeadGrads, HeadWeights, LayerGrads, LayerWeights, Pa
 STRATEGIES = ("FULL_SHARD", "SHARD_GRAD_OP", "NO_SHARD", "HYBRID_SHARD")
 
 
+def _add_bf16(dst: torch.Tensor, src: torch.Tensor) -> bool:
+    """fp32 dst += bf16 src with the fused HIP kernel (ops/csrc/optim.hip)."""
+    from ..ops import hip
+    return hip.add_bf16_into_f32(dst, src)
+
+
 @dataclass
 class _Seg:
     name: str
@@ -251,10 +257,12 @@ class FSDPRuntime(ParamProvider):
         """Sum full-size grads over ranks into this rank's fp32 shard grad (async)."""
         g = u.full_grad
         if self.shard_world == 1:
-            t = g if self.reduce_dtype == torch.float32 else g.to(self.reduce_dtype)
             work = None
             if self.dist and self.world > 1:
+                t = g if self.reduce_dtype == torch.float32 else g.to(self.reduce_dtype)
                 work = dist.all_reduce(t, group=self.pg if self.strategy != "NO_SHARD" else None, async_op=True)
+            else:  # nothing on the wire (one rank): no bf16 round trip, the fp32 grad is added directly
+                t = g
             u.rs_pending.append((work, t, None))
         else:
             src = g if self.reduce_dtype == torch.float32 else g.to(self.reduce_dtype)
@@ -273,11 +281,10 @@ class FSDPRuntime(ParamProvider):
                 out = out[:u.shard]
             if out.is_cuda:  # produced on the backward's stream (maybe the pipeline stream)
                 out.record_stream(torch.cuda.current_stream(out.device))
-            # add_ promotes the bf16 wire tensor inside the kernel: no separate cast pass
             if self.cpu_offload:
                 u.grad.add_(out.cpu())
-            else:
-                u.grad.add_(out)
+            elif not (out.is_cuda and out.dtype == torch.bfloat16 and _add_bf16(u.grad, out)):
+                u.grad.add_(out)  # add_ promotes the wire dtype inside the kernel
         u.rs_pending.clear()
 
     def finish(self):

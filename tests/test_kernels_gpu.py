@@ -345,3 +345,14 @@ def test_rmsnorm_bf16_weight_in_place():
     g2 = hip.rmsnorm_bwd(dy, x1, s1, wb, None, dw2, 0.1, 77)
     assert torch.equal(g1[0], g2[0]) and torch.equal(g1[1], g2[1])
     _close(dw1, dw2, 1e-4, 1e-5, "dw")
+
+
+def test_add_bf16_into_f32():
+    torch.manual_seed(41)
+    n = 7 * 1024 * 8 + 8
+    dst = torch.randn(n, device=DEV)
+    src = torch.randn(n, device=DEV).bfloat16()
+    want = dst + src.float()
+    assert hip.add_bf16_into_f32(dst, src)
+    assert torch.equal(dst, want)
+    assert not hip.add_bf16_into_f32(dst[:13], src[:13])  # outside the vector path: caller falls back
