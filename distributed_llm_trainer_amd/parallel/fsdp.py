@@ -257,12 +257,12 @@ class FSDPRuntime(ParamProvider):
         """Sum full-size grads over ranks into this rank's fp32 shard grad (async)."""
         g = u.full_grad
         if self.shard_world == 1:
+            # the reduce-dtype copy also on one rank: it is what stays pending until
+            # finish() (half the bytes of the fp32 full grad, which is freed here)
+            t = g if self.reduce_dtype == torch.float32 else g.to(self.reduce_dtype)
             work = None
             if self.dist and self.world > 1:
-                t = g if self.reduce_dtype == torch.float32 else g.to(self.reduce_dtype)
                 work = dist.all_reduce(t, group=self.pg if self.strategy != "NO_SHARD" else None, async_op=True)
-            else:  # nothing on the wire (one rank): no bf16 round trip, the fp32 grad is added directly
-                t = g
             u.rs_pending.append((work, t, None))
         else:
             src = g if self.reduce_dtype == torch.float32 else g.to(self.reduce_dtype)
