@@ -514,8 +514,9 @@ class GPTEngine:
 
         Schedule (GA = 4):  F0 | B0+F1 | B1+F2 | B2+F3 | B3, where "Bk+Fk+1" issues the
         blocks of the two chains alternately; micro-steps alternate between the current
-        stream and the weight-gradient side stream, the last one on the current stream.  A micro-step's forward and backward
-        run on the same stream, so its activations never cross streams; what is shared
+        stream and the weight-gradient side stream, the last one on the current stream.
+        A micro-step's forward and backward run on the same stream, so its activations
+        never cross streams; what is shared
         (weights, slot buffers, RoPE tables, the ids) is read-only until the window
         ends or is produced before the fork.  The last backward first joins the other
         stream: its lm_head weight-gradient GEMM (beta = 1) and the DDP bucket
