@@ -3,14 +3,21 @@
 // Reference: torch.optim.AdamW(fused=True) over 110 tensors + clip_grad_norm_
 // (foreach norm, host-visible scalar) + autocast re-casting every weight to bf16 each
 // micro-step (ddp_trainer.py:229-234,347-356).  Here:
-//  * k_sumsq: one pass over the flat fp32 grad buffer -> device scalar (no host sync);
+//  * k_sumsq + k_sum_partials: one pass over the flat fp32 grad buffer -> device
+//    scalar (no host sync), bitwise reproducible;
 //  * k_clip_coef: norm / clip coefficient computed ON DEVICE, folded with the DDP
 //    1/world averaging into a single grad scale read by the AdamW kernel;
 //  * k_adamw: decoupled weight decay + bias-corrected Adam on the flat buffer, also
 //    writing the bf16 shadow weights the GEMMs consume.
 #include "common.h"
 
-__global__ __launch_bounds__(256) void k_sumsq(const float* __restrict__ x, int64_t n, float* __restrict__ out) {
+// Deterministic two-stage sum of squares: every block writes its partial, one block
+// adds the partials in a fixed order.  (A float atomicAdd per block made the sum --
+// and so the clip coefficient -- depend on block completion order: DDP replicas
+// drifted apart in the last bit, tests/test_distributed_gpu.py.)
+constexpr int kSumsqMaxBlocks = 1024;
+
+__global__ __launch_bounds__(256) void k_sumsq(const float* __restrict__ x, int64_t n, float* __restrict__ part) {
   __shared__ float red[4];
   float acc = 0.f;
   const int64_t n4 = n >> 2;
@@ -25,7 +32,18 @@ __global__ __launch_bounds__(256) void k_sumsq(const float* __restrict__ x, int6
   acc = wave_sum(acc);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) unsafeAtomicAdd(out, red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// *out += sum(part[0:nb]) in a fixed order (one block)
+__global__ __launch_bounds__(256) void k_sum_partials(const float* __restrict__ part, int nb, float* __restrict__ out) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) acc += part[i];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) *out += (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // norm = sqrt(sumsq) * norm_mul;  coef = min(1, max_norm / (norm + 1e-6))  (clip_grad_norm_ semantics)
@@ -109,8 +127,12 @@ static inline int flat_blocks(int64_t n) {
   return (int)(b < 1 ? 1 : b);
 }
 
-DLT_API int dlt_sumsq(const float* x, int64_t n, float* out, hipStream_t st) {
-  k_sumsq<<<flat_blocks(n), 256, 0, st>>>(x, n, out);
+// part: device workspace of kSumsqMaxBlocks floats
+DLT_API int dlt_sumsq(const float* x, int64_t n, float* part, float* out, hipStream_t st) {
+  int nb = flat_blocks(n);
+  if (nb > kSumsqMaxBlocks) nb = kSumsqMaxBlocks;
+  k_sumsq<<<nb, 256, 0, st>>>(x, n, part);
+  k_sum_partials<<<1, 256, 0, st>>>(part, nb, out);
   DLT_CHECK_LAUNCH();
 }
 

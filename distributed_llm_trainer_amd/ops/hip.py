@@ -40,7 +40,7 @@ _SIGS = {
     "dlt_swiglu_fwd": [c_void_p, c_void_p, c_int, c_int, c_void_p],
     "dlt_swiglu_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "dlt_cross_entropy_fwd_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
-    "dlt_sumsq": [c_void_p, c_int64, c_void_p, c_void_p],
+    "dlt_sumsq": [c_void_p, c_int64, c_void_p, c_void_p, c_void_p],
     "dlt_clip_coef": [c_void_p, c_void_p, c_float, c_float, c_float, c_void_p],
     "dlt_adamw": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float, c_float,
                   c_float, c_float, c_float, c_void_p, c_void_p],
@@ -440,9 +440,17 @@ def cross_entropy_fwd_bwd(logits, targets, vocab, n_valid):
 
 
 # --------------------------------------------------------------- optimizer
+_SUMSQ_PARTS = {}  # device -> 1024-float workspace of the two-stage (deterministic) reduction
+
+
 def sumsq(x: torch.Tensor, out: torch.Tensor) -> None:
+    """out[0] += sum(x**2), bitwise reproducible (fixed-order partials, no atomics)."""
     _req(x, torch.float32, "sumsq.x")
-    _chk(lib().dlt_sumsq(_p(x), x.numel(), _p(out), _stream()), "sumsq")
+    _req(out, torch.float32, "sumsq.out")
+    part = _SUMSQ_PARTS.get(x.device)
+    if part is None:
+        part = _SUMSQ_PARTS[x.device] = torch.empty(1024, dtype=torch.float32, device=x.device)
+    _chk(lib().dlt_sumsq(_p(x), x.numel(), _p(part), _p(out), _stream()), "sumsq")
 
 
 def clip_coef(sumsq_t: torch.Tensor, out: torch.Tensor, norm_mul: float, max_norm: float, scale_mul: float) -> None:

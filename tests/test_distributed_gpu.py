@@ -1,0 +1,103 @@
+"""Multi-rank DDP / FSDP on the GPU: two ranks share the one MI355X of the test box
+(gloo carries the collectives -- RCCL itself needs one GPU per rank), running the fused
+HIP engine with micro-step pipelining, side-stream gradient buckets and FSDP unit
+residency exactly as on a multi-GPU node.  Each run is compared with one process that
+consumes every rank's micro-batches (GA = 2 x world):
+
+* ranks hold bit-identical parameters after every step (the all-reduce / gather worked),
+* the global gradient norm of every step matches the single process (gradients were
+  averaged over the right set, once),
+* the parameter updates point the same way (cosine of the deltas).
+
+bf16 GEMMs over a different micro-batch split change the fp32 accumulation order, so
+the comparisons are relative, not bitwise (the CPU versions in
+``test_distributed_cpu.py`` are bitwise-tight)."""
+import os
+
+import pytest
+import torch
+
+from tests.dist_utils import run_multiprocess
+
+pytestmark = pytest.mark.gpu
+
+TINY = dict(vocab_size=1000, hidden_size=256, num_layers=3, num_heads=4, max_seq_len=256, dropout=0.0,
+            attention_dropout=0.0)
+GPU_ENV = {"DLT_FORCE_CPU": None, "DLT_SHARE_GPU": "1"}
+STEPS = 3
+
+
+def _cpu_dry_run():
+    """DLT_FORCE_CPU=1 with GPU_ENV emptied runs the same logic on the CPU."""
+    return os.environ.get("DLT_FORCE_CPU") == "1"
+
+
+def _data(step, rank):
+    g = torch.Generator().manual_seed(1000 * step + rank)
+    return torch.randint(0, TINY["vocab_size"], (4, TINY["max_seq_len"]), generator=g)
+
+
+def _ddp(rank, world, single):
+    from distributed_llm_trainer_amd.models.config import GPTConfig
+    from distributed_llm_trainer_amd.training.configs import TrainingConfig
+    from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
+    tc = TrainingConfig(batch_size=2, gradient_accumulation_steps=2 * (world if single else 1), warmup_steps=1,
+                        max_steps=100, learning_rate=1e-3, bucket_cap_mb=1.0)
+    tr = DistributedTrainer(GPTConfig(**TINY), tc)
+    assert tr.use_engine and (tr.device.type == "cuda" or _cpu_dry_run())
+    init = tr.store.flat.detach().float().cpu().clone()
+    norms = []
+    for s in range(STEPS):
+        batch = torch.cat([_data(s, r) for r in range(world)]) if single else _data(s, rank)
+        tr.train_step({"input_ids": batch})
+        norms.append(float(tr._last_norm))
+    nb = len(tr.ddp.buckets) if tr.ddp is not None else 0
+    return init, tr.store.flat.detach().float().cpu().clone(), norms, nb
+
+
+def _fsdp(rank, world, single, strategy):
+    from distributed_llm_trainer_amd.models.config import GPTConfig
+    from distributed_llm_trainer_amd.training.configs import FSDPConfig, FSDPTrainingConfig
+    from distributed_llm_trainer_amd.training.fsdp_trainer import FSDPTrainer
+    tc = FSDPTrainingConfig(batch_size=2, gradient_accumulation_steps=2 * (world if single else 1),
+                            warmup_steps=1, max_steps=100, learning_rate=1e-3)
+    fc = FSDPConfig(sharding_strategy=strategy)
+    tr = FSDPTrainer(GPTConfig(**TINY), tc, fc)
+    assert tr.device.type == "cuda" or _cpu_dry_run()
+
+    def full():
+        sd = tr._full_state()
+        return torch.cat([v.detach().float().cpu().flatten() for k, v in sorted(sd.items()) if "rotary" not in k])
+
+    init = full()
+    norms = []
+    for s in range(STEPS):
+        batch = torch.cat([_data(s, r) for r in range(world)]) if single else _data(s, rank)
+        tr.train_step({"input_ids": batch})
+        norms.append(float(tr._last_norm))
+    return init, full(), norms, 0
+
+
+def _check(outs, ref):
+    (i0, p0, n0, _), (i1, p1, n1, _) = outs
+    ri, rp, rn, _ = ref
+    assert torch.equal(i0, i1) and torch.equal(i0, ri), "initialisation differs"
+    assert torch.equal(p0, p1), f"ranks diverged: {(p0 - p1).abs().max()}"
+    for a, b in zip(n0, rn):
+        assert abs(a - b) <= 2e-3 * abs(b), (n0, rn)
+    assert n0 == n1
+    d, dr = p0 - i0, rp - ri
+    cos = torch.nn.functional.cosine_similarity(d, dr, dim=0).item()
+    assert cos > 0.99, cos
+
+
+def test_ddp_two_ranks_on_gpu_match_single_process():
+    outs = run_multiprocess(_ddp, world=2, args=(False,), env=GPU_ENV, timeout=240)
+    assert outs[0][3] > 2  # several gradient buckets were all-reduced from the side stream
+    _check(outs, _ddp(0, 2, True))
+
+
+@pytest.mark.parametrize("strategy", ["FULL_SHARD", "SHARD_GRAD_OP"])
+def test_fsdp_two_ranks_on_gpu_match_single_process(strategy):
+    outs = run_multiprocess(_fsdp, world=2, args=(False, strategy), env=GPU_ENV, timeout=240)
+    _check(outs, _fsdp(0, 2, True, strategy))

@@ -130,6 +130,14 @@ def test_adamw_and_norm():
     ss = torch.zeros(1, device=DEV)
     hip.sumsq(g, ss)
     _close(ss, g.pow(2).sum().reshape(1), 1e-1, 1e-5, "sumsq")
+    big = torch.randn(50_000_003, device=DEV)  # 4096 blocks' worth: the capped grid
+    sums = []
+    for _ in range(4):  # bitwise reproducible: replicas must compute the same clip coefficient
+        t = torch.zeros(1, device=DEV)
+        hip.sumsq(big, t)
+        sums.append(t.item())
+    assert len(set(sums)) == 1, sums
+    assert abs(sums[0] - big.double().pow(2).sum().item()) < 1e-4 * sums[0]
     scale = torch.zeros(2, device=DEV)
     hip.clip_coef(ss, scale, 0.5, 1.0, 0.5)
     norm = g.norm() * 0.5
