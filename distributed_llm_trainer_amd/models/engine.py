@@ -185,6 +185,9 @@ class GPTEngine:
         # inverse RoPE in the backward epilogue); DLT_PACKED_QKV=0 -> split q/k/v copies
         self.packed_qkv = (hasattr(ops, "attention_fwd_packed")
                            and os.environ.get("DLT_PACKED_QKV", "1") != "0")
+        # last layers of the deferred-wgrad backward whose weight gradients run on the
+        # current stream instead of the side stream (see _backward_gen)
+        self.main_wgrad_layers = int(os.environ.get("DLT_MAIN_WGRAD_LAYERS", "1"))
 
     # ------------------------------------------------------- grad accumulation
     def set_accumulation(self, slot: int, n_slots: int, defer: bool = True) -> None:
@@ -420,6 +423,14 @@ class GPTEngine:
                 gm.wgrad_acc(hg.embed, lg_all, nf_all)
         st.dlogits = None
         key_last = self._keys(st.micro, L - 1)[2]
+        # The side stream lags the dgrad chain by a few layers' worth of weight-gradient
+        # GEMMs; the last ``n_main`` layers' wgrads run on the current stream instead, so
+        # the two queues drain together once the dgrad chain is done.  Their gradient
+        # hooks (DDP bucket launches) are issued at the end, after joining the side
+        # stream, so a bucket never reads a gradient still being written on another
+        # stream.  Only for providers whose hooks can be delayed (the flat DDP store).
+        n_main = self.main_wgrad_layers if (side is not None and getattr(prov, "late_post_backward_ok", False)) else 0
+        late = []
 
         def sb(layer, name, n):
             return self._slot_buf(st, layer, name, M, n, dev)[0] if st.defer else None
@@ -474,7 +485,7 @@ class GPTEngine:
                     # concurrently with the next layer's dgrad chain (the small-output
                     # wgrads leave most CUs idle); the layer's gradient hook (DDP
                     # bucket all-reduce) is issued from the same stream.
-                    if side is not None:
+                    if side is not None and i >= n_main:
                         ev = torch.cuda.Event()
                         ev.record()
                         side.wait_event(ev)
@@ -493,7 +504,10 @@ class GPTEngine:
             g_x2, g_d = g_x2n, g_dn
             st.caches[i] = None
             try:
-                prov.post_backward(i)
+                if i < n_main:
+                    late.append(i)
+                else:
+                    prov.post_backward(i)
             finally:
                 if side_ctx is not None:
                     side_ctx.__exit__(None, None, None)
@@ -502,6 +516,10 @@ class GPTEngine:
         if head_ev is not None:
             torch.cuda.current_stream().wait_event(head_ev)
         ops.embedding_bwd(st.ids, g_x2, hg.embed)
+        if late:
+            torch.cuda.current_stream().wait_stream(side)
+            for i in late:
+                prov.post_backward(i)
         prov.post_backward("head")
         if side is not None and do_wgrad and st.defer:
             torch.cuda.current_stream().wait_stream(side)

@@ -81,6 +81,8 @@ class FlatParamStore(ParamProvider):
     # gradient hooks (DDP bucket launches) may be issued from the engine's
     # weight-gradient stream: they only enqueue collectives on the current stream
     side_stream_hooks = True
+    # ... and may be delayed to the end of the backward (engine ``main_wgrad_layers``)
+    late_post_backward_ok = True
 
     def __init__(self, model, device, compute_dtype=torch.bfloat16, grad_dtype=torch.float32):
         self.model = model
