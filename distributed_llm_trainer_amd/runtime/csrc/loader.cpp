@@ -29,6 +29,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -77,29 +78,35 @@ struct Loader {
   int64_t next_take = 0;     // next step the consumer wants
   bool stop = false;
   std::vector<std::thread> workers;
-  // epoch permutations (cached: the current and the next epoch)
+  // epoch permutations, cached for two epochs.  Handed out as shared_ptr: a producer
+  // filling epoch e keeps its permutation alive while another producer replaces the
+  // cache entry with epoch e+2 (tiny corpora have ring-many epochs in flight; a plain
+  // vector reference here was a data race, found by tests/native/loader_stress.cpp
+  // under ThreadSanitizer).
   std::mutex perm_mu;
   int64_t perm_epoch[2] = {-1, -1};
-  std::vector<int64_t> perm[2];
+  std::shared_ptr<const std::vector<int64_t>> perm[2];
   std::atomic<int64_t> produced{0};
 
-  const std::vector<int64_t>& epoch_perm(int64_t epoch) {
-    std::lock_guard<std::mutex> g(perm_mu);
+  std::shared_ptr<const std::vector<int64_t>> epoch_perm(int64_t epoch) {
     const int k = (int)(epoch & 1);
-    if (perm_epoch[k] != epoch) {
-      auto& p = perm[k];
-      p.resize(windows);
-      for (int64_t i = 0; i < windows; ++i) p[i] = i;
-      if (shuffle) {
-        uint64_t s = seed ^ (0x5851F42D4C957F2Dull * (uint64_t)(epoch + 1));
-        for (int64_t i = windows - 1; i > 0; --i) {
-          const int64_t j = (int64_t)(splitmix64(s) % (uint64_t)(i + 1));
-          std::swap(p[i], p[j]);
-        }
-      }
-      perm_epoch[k] = epoch;
+    {
+      std::lock_guard<std::mutex> g(perm_mu);
+      if (perm_epoch[k] == epoch) return perm[k];
     }
-    return perm[k];
+    auto p = std::make_shared<std::vector<int64_t>>(windows);  // built outside the lock
+    for (int64_t i = 0; i < windows; ++i) (*p)[i] = i;
+    if (shuffle) {
+      uint64_t s = seed ^ (0x5851F42D4C957F2Dull * (uint64_t)(epoch + 1));
+      for (int64_t i = windows - 1; i > 0; --i) {
+        const int64_t j = (int64_t)(splitmix64(s) % (uint64_t)(i + 1));
+        std::swap((*p)[i], (*p)[j]);
+      }
+    }
+    std::lock_guard<std::mutex> g(perm_mu);
+    perm[k] = p;
+    perm_epoch[k] = epoch;
+    return p;
   }
 
   int64_t load_token(int64_t idx) const {
@@ -122,7 +129,8 @@ struct Loader {
     }
     const int64_t epoch = step / steps_per_epoch;
     const int64_t within = step % steps_per_epoch;
-    const auto& p = epoch_perm(epoch);
+    const auto perm_ref = epoch_perm(epoch);
+    const std::vector<int64_t>& p = *perm_ref;
     for (int64_t b = 0; b < batch; ++b) {
       // DistributedSampler layout: rank r takes positions r, r+W, r+2W, ...
       const int64_t pos = (within * batch + b) * world + rank;
