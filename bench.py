@@ -41,6 +41,9 @@ def main():
     ap.add_argument("--mode", default="ddp", choices=["ddp", "fsdp"])
     ap.add_argument("--sharding", default="FULL_SHARD")
     ap.add_argument("--no_ac", action="store_true", help="FSDP: disable activation checkpointing")
+    ap.add_argument("--model_override", default="",
+                    help="rehearsal only: comma-separated GPTConfig overrides (e.g. hidden_size=64,num_layers=2); "
+                         "the JSON line then names a custom model and vs_baseline is null")
     ap.add_argument("--dropout", type=float, default=None,
                     help="ablation only: override dropout/attention_dropout (reference config: 0.1)")
     args = ap.parse_args()
@@ -51,6 +54,16 @@ def main():
     from distributed_llm_trainer_amd.models.config import GPTConfig
     cfg = GPTConfig.from_preset(args.model_size)
     cfg.max_seq_len = args.seq_len
+    overrides = {}
+    for kv in filter(None, args.model_override.split(",")):
+        k, v = kv.split("=", 1)
+        if not hasattr(cfg, k):
+            raise SystemExit(f"unknown GPTConfig field {k!r}")
+        overrides[k] = type(getattr(cfg, k))(v) if getattr(cfg, k) is not None else int(v)
+    if overrides:
+        if "hidden_size" in overrides and "intermediate_size" not in overrides:
+            overrides["intermediate_size"] = 4 * overrides["hidden_size"]
+        cfg = GPTConfig(**{**cfg.to_dict(), **overrides})
     if args.dropout is not None:
         cfg.dropout = cfg.attention_dropout = args.dropout
     if args.mode == "ddp":
@@ -103,19 +116,20 @@ def main():
     tokens = args.steps * B * args.seq_len * world
     tps = tokens / elapsed
     if trainer.is_main_process:
-        base = BASELINE_TPS.get(world)
+        base = None if overrides else BASELINE_TPS.get(world)
         out = {
             "metric": "tokens/sec", "value": round(tps, 1), "unit": "tokens/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 3),
             "higher_is_better": True, "scaling": "weak",
             "vs_baseline": round(tps / base, 3) if base else None, "dtype": "bf16", "data": "synthetic",
             "config": {"model": f"GPT-2 124M (gpt2_{args.model_size} preset, {cfg.num_parameters():,} params, "
-                                "LLaMA-style as in the reference)" if args.model_size == "small" else args.model_size,
+                                "LLaMA-style as in the reference)" if args.model_size == "small" and not overrides
+                                else f"{args.model_size}+{args.model_override}" if overrides else args.model_size,
                        "global_batch": B * world, "seq_len": args.seq_len,
                        "parallelism": f"{args.mode}{world}", "micro_batch": args.batch_size,
                        "grad_accum": args.grad_accum},
             "peak_gb_per_gpu": round(peak, 3), "final_loss": round(loss, 4),
-            "vs_baseline_linear": round(tps / (12500.0 * world), 3),
+            "vs_baseline_linear": None if overrides else round(tps / (12500.0 * world), 3),
         }
         print(json.dumps(out), flush=True)
         if os.environ.get("DLT_GEMM_REPORT"):
