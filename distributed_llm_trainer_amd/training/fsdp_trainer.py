@@ -14,6 +14,8 @@ Differences from the reference by design:
 * Checkpoints: FULL_STATE_DICT format of the reference (fp32 params with the same
   keys + FQN-keyed, unflattened optimizer state, one param group); loading reads
   the file on rank 0 and broadcasts flat units (no pickled broadcast, X11).
+  ``--state_dict_type sharded`` adds SHARDED_STATE_DICT (per-rank shard files, no
+  gather; the reference only discusses it at ``fsdp_trainer.py:416-418``).
 """
 from __future__ import annotations
 
@@ -211,8 +213,81 @@ class FSDPTrainer:
         if self.distributed:
             dist.barrier()
 
+    # ------------------------------------------------------- SHARDED_STATE_DICT
+    @torch.no_grad()
+    def save_sharded_checkpoint(self, path: str):
+        """SHARDED_STATE_DICT (the reference only discusses it, ``fsdp_trainer.py:416-418``):
+        every rank writes its own fp32 master / exp_avg / exp_avg_sq shards into the
+        directory ``path`` -- no all-gather, no rank-0 host copy of the full model, so a
+        save costs one local write per rank regardless of model size.  Rank 0 adds
+        ``meta.json`` (counters, configs, unit layout) and ``extra.pt`` (RoPE buffers and
+        the state-dict key order) so ``utils.checkpoint.consolidate_sharded`` can rebuild
+        the reference FULL_STATE_DICT file offline."""
+        rt, opt = self.runtime, self.optimizer
+        os.makedirs(path, exist_ok=True)
+        units = {}
+        for uid, u in rt.units.items():
+            a, b = rt.unit_offsets[uid]
+            units[str(uid)] = {"param": u.master.detach().to("cpu", copy=True),
+                               "exp_avg": opt.exp_avg[a:b].to("cpu", copy=True),
+                               "exp_avg_sq": opt.exp_avg_sq[a:b].to("cpu", copy=True)}
+        ckpt.save_checkpoint(os.path.join(path, f"shard_{self.rank:05d}.pt"), {
+            "rank": self.rank, "shard_rank": rt.shard_rank, "shard_world": rt.shard_world, "units": units})
+        if self.is_main_process:
+            sd_keys = list(self.model.state_dict().keys())
+            params = {n for n, _ in self.model.named_parameters()}
+            extra = {k: v.detach().to("cpu", copy=True) for k, v in self.model.state_dict().items()
+                     if k not in params and k != "lm_head.weight"}
+            ckpt.save_checkpoint(os.path.join(path, "extra.pt"), {"buffers": extra})
+            g = {k: v for k, v in opt.param_groups[0].items() if k != "params"}
+            meta = {
+                "format": ckpt.SHARDED_FORMAT, "world_size": self.world_size, "shard_world": rt.shard_world,
+                "strategy": rt.strategy, "global_step": self.global_step, "tokens_seen": self.tokens_seen,
+                "optimizer_step": opt.step_count, "param_group": g,
+                "state_dict_keys": sd_keys, "param_order": [n for n, _ in self.model.named_parameters()],
+                "model_config": ckpt.config_to_dict(self.model_config),
+                "training_config": ckpt.config_to_dict(self.training_config),
+                "fsdp_config": ckpt.config_to_dict(self.fsdp_config),
+                "units": {str(uid): {"numel": u.numel, "padded": u.padded, "shard": u.shard,
+                                     "segs": [[s.name, s.offset, s.numel, list(s.shape)] for s in u.segs]}
+                          for uid, u in rt.units.items()},
+            }
+            ckpt.write_json_atomic(os.path.join(path, "meta.json"), meta)
+        if self.distributed:
+            dist.barrier()
+
+    @torch.no_grad()
+    def load_sharded_checkpoint(self, path: str):
+        """Load a SHARDED_STATE_DICT directory written at the same shard layout; for a
+        different world size, consolidate it to a full checkpoint first."""
+        rt, opt = self.runtime, self.optimizer
+        meta = ckpt.read_sharded_meta(path)
+        if meta["world_size"] != self.world_size or meta["shard_world"] != rt.shard_world:
+            raise ValueError(f"sharded checkpoint was written by {meta['world_size']} ranks "
+                             f"(shard world {meta['shard_world']}); this job has {self.world_size} "
+                             f"(shard world {rt.shard_world}). Run utils.checkpoint.consolidate_sharded first.")
+        c = ckpt.load_checkpoint(os.path.join(path, f"shard_{self.rank:05d}.pt"))
+        if c["shard_rank"] != rt.shard_rank:
+            raise ValueError(f"shard file of rank {self.rank} holds shard {c['shard_rank']}, expected {rt.shard_rank}")
+        for uid, u in rt.units.items():
+            e = c["units"][str(uid)]
+            if e["param"].numel() != u.shard:
+                raise ValueError(f"unit {uid}: shard has {e['param'].numel()} elements, expected {u.shard}")
+            a, b = rt.unit_offsets[uid]
+            u.master.copy_(e["param"].to(u.master.device))
+            opt.exp_avg[a:b].copy_(e["exp_avg"].to(opt.exp_avg.device))
+            opt.exp_avg_sq[a:b].copy_(e["exp_avg_sq"].to(opt.exp_avg_sq.device))
+        rt.refresh_shadow()
+        self.global_step, self.tokens_seen = int(meta["global_step"]), int(meta["tokens_seen"])
+        opt.step_count = int(meta["optimizer_step"])
+        self.model.engine.micro_counter = self.global_step * self.training_config.gradient_accumulation_steps
+        if self.is_main_process:
+            print(f"Loaded sharded checkpoint from {path} (step {self.global_step})")
+
     @torch.no_grad()
     def load_checkpoint(self, path: str):
+        if os.path.isdir(path):
+            return self.load_sharded_checkpoint(path)
         rt, opt = self.runtime, self.optimizer
         c = ckpt.load_checkpoint(path, map_location="cpu") if (self.is_main_process or not self.distributed) else None
         meta = [None]
@@ -269,6 +344,9 @@ def build_parser():
     p.add_argument("--gradient_accumulation_steps", type=int, default=None)
     p.add_argument("--reduce_dtype", choices=["bf16", "fp32"], default=None)
     p.add_argument("--no_final_save", action="store_true")
+    p.add_argument("--state_dict_type", choices=["full", "sharded"], default="full",
+                   help="full: reference FULL_STATE_DICT file (rank-0 gather); sharded: per-rank shard "
+                        "directory, no gather (resume with --resume_from DIR)")
     return p
 
 
@@ -321,6 +399,12 @@ def main(argv=None):
         print("=" * 60 + "\n")
         mem = trainer.get_memory_stats()
         print(f"Initial memory: {mem['allocated_gb']:.2f} GB allocated")
+    def save(stem):
+        if args.state_dict_type == "sharded":
+            trainer.save_sharded_checkpoint(stem)
+        else:
+            trainer.save_checkpoint(stem + ".pt")
+
     data_iter = iter(dataloader)
     start_time = time.time()
     for step in range(trainer.global_step, tc.max_steps):
@@ -339,9 +423,9 @@ def main(argv=None):
             print(f"Step {step:6d} | Loss: {metrics['loss']:.4f} | LR: {metrics['lr']:.2e} | "
                   f"Tokens/s: {tps:,.0f} | Mem: {mem['allocated_gb']:.1f}GB", flush=True)
         if step > 0 and step % tc.save_interval == 0:
-            trainer.save_checkpoint(f"{tc.checkpoint_dir}/step_{step}.pt")
+            save(f"{tc.checkpoint_dir}/step_{step}")
     if not args.no_final_save:
-        trainer.save_checkpoint(f"{tc.checkpoint_dir}/final.pt")
+        save(f"{tc.checkpoint_dir}/final")
     if trainer.is_main_process:
         total_time = time.time() - start_time
         print(f"\nTraining complete! Total time: {total_time:.2f}s")

@@ -15,12 +15,16 @@ Fixes vs the reference:
   names (``models.config.GPTConfig``, ``__main__.TrainingConfig``,
   ``training.{ddp,fsdp}_trainer.*``) -- so both our checkpoints and the reference's
   load with ``weights_only=True``: nothing in the file is executed.
+* FSDP SHARDED_STATE_DICT (discussed, not implemented, in the reference): per-rank
+  shard files + ``meta.json``; ``consolidate_sharded`` turns one into the full format
+  (``python -m distributed_llm_trainer_amd.utils.checkpoint consolidate DIR OUT``).
 * Writes are atomic (tmp file + rename), so a crash mid-save never leaves a
   truncated ``final.pt`` behind for ``--resume_from``.
 """
 from __future__ import annotations
 
 import dataclasses
+import json
 import os
 from typing import Any, Dict, Optional
 
@@ -79,6 +83,79 @@ def load_checkpoint(path: str, map_location="cpu") -> Dict[str, Any]:
     return torch.load(path, map_location=map_location, weights_only=True)
 
 
+SHARDED_FORMAT = "dlt-fsdp-sharded-v1"
+
+
+def write_json_atomic(path: str, obj: Dict[str, Any]) -> None:
+    tmp = f"{path}.tmp.{os.getpid()}"
+    with open(tmp, "w") as f:
+        json.dump(obj, f, indent=1)
+    os.replace(tmp, path)
+
+
+def read_sharded_meta(path: str) -> Dict[str, Any]:
+    with open(os.path.join(path, "meta.json")) as f:
+        meta = json.load(f)
+    if meta.get("format") != SHARDED_FORMAT:
+        raise ValueError(f"{path}: not a sharded checkpoint ({meta.get('format')!r})")
+    return meta
+
+
+@torch.no_grad()
+def consolidate_sharded(path: str, out: Optional[str] = None) -> Dict[str, Any]:
+    """Rebuild the reference FULL_STATE_DICT payload (fp32 ``model`` with
+    the reference keys incl. RoPE buffers and the tied ``lm_head.weight``; FQN-keyed
+    ``optimizer``; counters; config objects) from a SHARDED_STATE_DICT directory written
+    by ``FSDPTrainer.save_sharded_checkpoint``.  Runs offline on CPU, one unit at a
+    time; writes it to ``out`` if given.  Any world size can then load the result."""
+    from ..training.configs import FSDPConfig, FSDPTrainingConfig
+    meta = read_sharded_meta(path)
+    W = meta["shard_world"]
+    # one file per shard index (HYBRID_SHARD replicas hold identical shards)
+    by_shard: Dict[int, Dict[str, Any]] = {}
+    for fn in sorted(os.listdir(path)):
+        if fn.startswith("shard_") and fn.endswith(".pt") and len(by_shard) < W:
+            c = torch.load(os.path.join(path, fn), map_location="cpu", weights_only=True, mmap=True)
+            by_shard.setdefault(int(c["shard_rank"]), c["units"])
+    missing = [i for i in range(W) if i not in by_shard]
+    if missing:
+        raise FileNotFoundError(f"{path}: missing shard files for shard ranks {missing}")
+    shards = [by_shard[i] for i in range(W)]
+    params, mom, var = {}, {}, {}
+    for uid, lay in meta["units"].items():
+        full = {k: torch.cat([shards[i][uid][k] for i in range(W)]) for k in ("param", "exp_avg", "exp_avg_sq")}
+        if full["param"].numel() != lay["padded"]:
+            raise ValueError(f"unit {uid}: {full['param'].numel()} elements, layout says {lay['padded']}")
+        for name, off, n, shape in lay["segs"]:
+            params[name] = full["param"][off:off + n].view(shape).clone()
+            mom[name] = full["exp_avg"][off:off + n].view(shape).clone()
+            var[name] = full["exp_avg_sq"][off:off + n].view(shape).clone()
+    buffers = load_checkpoint(os.path.join(path, "extra.pt"))["buffers"]
+    model = {}
+    for k in meta["state_dict_keys"]:
+        if k in params:
+            model[k] = params[k]
+        elif k == "lm_head.weight":
+            model[k] = params["embed_tokens.weight"]
+        else:
+            model[k] = buffers[k]
+    step = torch.tensor(float(meta["optimizer_step"]))
+    names = [n for n in meta["param_order"] if n in params]
+    group = dict(meta["param_group"])
+    if isinstance(group.get("betas"), list):
+        group["betas"] = tuple(group["betas"])
+    group["params"] = names
+    optim = {"state": {n: {"step": step.clone(), "exp_avg": mom[n], "exp_avg_sq": var[n]} for n in names},
+             "param_groups": [group]}
+    payload = {"model": model, "optimizer": optim, "global_step": meta["global_step"],
+               "tokens_seen": meta["tokens_seen"], "model_config": GPTConfig.from_dict(meta["model_config"]),
+               "training_config": FSDPTrainingConfig(**meta["training_config"]),
+               "fsdp_config": FSDPConfig(**meta["fsdp_config"])}
+    if out:
+        save_checkpoint(out, payload)
+    return payload
+
+
 def config_to_dict(cfg) -> Dict[str, Any]:
     if dataclasses.is_dataclass(cfg):
         return dataclasses.asdict(cfg)
@@ -91,3 +168,20 @@ def model_state_dict_cpu(model: torch.nn.Module) -> Dict[str, torch.Tensor]:
     for k, v in model.state_dict().items():
         out[k] = v.detach().to("cpu", copy=True).clone()
     return out
+
+
+def _main(argv=None):
+    import argparse
+    ap = argparse.ArgumentParser(description="checkpoint tools")
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    c = sub.add_parser("consolidate", help="sharded FSDP checkpoint dir -> reference full checkpoint file")
+    c.add_argument("src")
+    c.add_argument("out")
+    args = ap.parse_args(argv)
+    if args.cmd == "consolidate":
+        p = consolidate_sharded(args.src, args.out)
+        print(f"wrote {args.out}: {len(p['model'])} tensors, step {p['global_step']}")
+
+
+if __name__ == "__main__":
+    _main()

@@ -97,3 +97,19 @@ def test_fault_injection_then_resume_matches_uninterrupted(tmp_path):
         assert torch.equal(a["model"][k], b["model"][k]), k
     for i, st in a["optimizer"]["state"].items():
         assert torch.equal(st["exp_avg"], b["optimizer"]["state"][i]["exp_avg"])
+
+
+def test_fsdp_cli_sharded_save_resume_consolidate(tmp_path, capsys):
+    cfg = _yaml(tmp_path)
+    ck = str(tmp_path / "cks")
+    fsdp_trainer.main(["--config", cfg, "--max_steps", "4", "--checkpoint_dir", ck, "--state_dict_type", "sharded"])
+    final = os.path.join(ck, "final")
+    assert os.path.isfile(os.path.join(final, "meta.json"))
+    tr = fsdp_trainer.main(["--config", cfg, "--max_steps", "6", "--checkpoint_dir", ck, "--resume_from", final,
+                            "--state_dict_type", "sharded"])
+    assert tr.global_step == 6 and "Loaded sharded checkpoint" in capsys.readouterr().out
+    from distributed_llm_trainer_amd.utils.checkpoint import _main as ckpt_main
+    out = str(tmp_path / "full.pt")
+    ckpt_main(["consolidate", final, out])
+    c = load_checkpoint(out)
+    assert c["global_step"] == 6 and "fsdp_config" in c

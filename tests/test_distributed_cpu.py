@@ -205,3 +205,64 @@ def test_fsdp_checkpoint_loads_at_other_world_size(tmp_path):
             assert step == 2
             for k, v in ref.items():
                 assert torch.equal(sd[k].float(), v.float()), (world, k)
+
+
+def _fsdp_sharded_ckpt_worker(rank, world, path, full_path, strategy):
+    from distributed_llm_trainer_amd.models.config import GPTConfig
+    from distributed_llm_trainer_amd.training.configs import FSDPConfig, FSDPTrainingConfig
+    from distributed_llm_trainer_amd.training.fsdp_trainer import FSDPTrainer
+    cfg = GPTConfig(**TINY)
+    tc = FSDPTrainingConfig(batch_size=2, gradient_accumulation_steps=2, warmup_steps=1, learning_rate=1e-2)
+    fc = FSDPConfig(sharding_strategy=strategy, reduce_dtype="fp32")
+    tr = FSDPTrainer(cfg, tc, fc)
+    for s in range(2):
+        tr.train_step({"input_ids": _data(s, rank, n=4)})
+    tr.save_sharded_checkpoint(path)
+    tr.save_checkpoint(full_path)   # the same state through the FULL_STATE_DICT path
+    tr2 = FSDPTrainer(cfg, tc, fc)
+    tr2.load_checkpoint(path)       # a directory -> sharded load
+    same = torch.equal(tr.runtime.master_flat, tr2.runtime.master_flat) and \
+        torch.equal(tr.optimizer.exp_avg_sq, tr2.optimizer.exp_avg_sq) and tr2.global_step == 2 and \
+        tr2.optimizer.step_count == tr.optimizer.step_count
+    b = _data(5, rank, n=4)
+    tr.train_step({"input_ids": b})
+    tr2.train_step({"input_ids": b})
+    return same, torch.equal(tr.runtime.master_flat, tr2.runtime.master_flat)
+
+
+@pytest.mark.parametrize("strategy", ["FULL_SHARD", "HYBRID_SHARD"])
+def test_fsdp_sharded_checkpoint_roundtrip_and_consolidate(tmp_path, strategy):
+    """SHARDED_STATE_DICT: per-rank save/load resumes bit-exactly, and the offline
+    consolidation reproduces the FULL_STATE_DICT file of the same state."""
+    path, full_path = str(tmp_path / "sharded"), str(tmp_path / "full.pt")
+    outs = run_multiprocess(_fsdp_sharded_ckpt_worker, world=2, args=(path, full_path, strategy))
+    for same, same_after in outs:
+        assert same and same_after
+    assert sorted(os.listdir(path)) == ["extra.pt", "meta.json", "shard_00000.pt", "shard_00001.pt"]
+    from distributed_llm_trainer_amd.utils.checkpoint import consolidate_sharded, load_checkpoint
+    cons = consolidate_sharded(path, str(tmp_path / "cons.pt"))
+    full = load_checkpoint(full_path)
+    again = load_checkpoint(str(tmp_path / "cons.pt"))
+    assert set(again) == set(full)
+    assert list(again["model"]) == list(full["model"])
+    for k, v in full["model"].items():
+        assert torch.equal(cons["model"][k], v), k
+    assert list(full["optimizer"]["state"]) == list(cons["optimizer"]["state"])
+    for n, st in full["optimizer"]["state"].items():
+        for f in ("exp_avg", "exp_avg_sq", "step"):
+            assert torch.equal(cons["optimizer"]["state"][n][f], st[f]), (n, f)
+    assert cons["optimizer"]["param_groups"] == full["optimizer"]["param_groups"]
+    assert (cons["global_step"], cons["tokens_seen"]) == (full["global_step"], full["tokens_seen"])
+    assert cons["model_config"] == full["model_config"] and cons["fsdp_config"] == full["fsdp_config"]
+
+
+def test_fsdp_sharded_checkpoint_rejects_other_world_size(tmp_path):
+    path = str(tmp_path / "sharded")
+    run_multiprocess(_fsdp_sharded_ckpt_worker, world=2, args=(path, str(tmp_path / "f.pt"), "FULL_SHARD"))
+    from distributed_llm_trainer_amd.models.config import GPTConfig
+    from distributed_llm_trainer_amd.training.configs import FSDPConfig, FSDPTrainingConfig
+    from distributed_llm_trainer_amd.training.fsdp_trainer import FSDPTrainer
+    tr = FSDPTrainer(GPTConfig(**TINY), FSDPTrainingConfig(batch_size=2, gradient_accumulation_steps=2),
+                     FSDPConfig(reduce_dtype="fp32"))
+    with pytest.raises(ValueError, match="consolidate_sharded"):
+        tr.load_checkpoint(path)
