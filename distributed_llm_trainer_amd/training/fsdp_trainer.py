@@ -20,6 +20,7 @@ Differences from the reference by design:
 from __future__ import annotations
 
 import argparse
+import json
 import os
 import time
 
@@ -31,6 +32,7 @@ from ..models.gpt import GPT, count_parameters
 from ..parallel.fsdp import FSDPRuntime
 from ..utils import checkpoint as ckpt
 from ..utils import debug as dbg
+from ..utils.profiling import Profiler
 from .common import cosine_lr, memory_stats, seed_all, select_device, setup_distributed, unwrap_batch
 from .configs import FSDPConfig, FSDPTrainingConfig
 from .optim import FlatAdamW
@@ -344,6 +346,9 @@ def build_parser():
     p.add_argument("--gradient_accumulation_steps", type=int, default=None)
     p.add_argument("--reduce_dtype", choices=["bf16", "fp32"], default=None)
     p.add_argument("--no_final_save", action="store_true")
+    p.add_argument("--seed", type=int, default=None)
+    p.add_argument("--profile", type=str, default=None, help="write a torch.profiler trace to this dir")
+    p.add_argument("--metrics_jsonl", type=str, default=None)
     p.add_argument("--state_dict_type", choices=["full", "sharded"], default="full",
                    help="full: reference FULL_STATE_DICT file (rank-0 gather); sharded: per-rank shard "
                         "directory, no gather (resume with --resume_from DIR)")
@@ -373,7 +378,8 @@ def main(argv=None):
             fc.cpu_offload = True
         if "no_activation_checkpointing" in given:
             fc.activation_checkpointing = False
-    for k in ("resume_from", "checkpoint_dir", "save_interval", "log_interval", "gradient_accumulation_steps"):
+    for k in ("resume_from", "checkpoint_dir", "save_interval", "log_interval", "gradient_accumulation_steps",
+              "seed"):
         v = getattr(args, k)
         if v is not None:
             setattr(tc, k, v)
@@ -405,9 +411,13 @@ def main(argv=None):
         else:
             trainer.save_checkpoint(stem + ".pt")
 
+    metrics_f = open(args.metrics_jsonl, "a") if (args.metrics_jsonl and trainer.is_main_process) else None
+    prof = Profiler(args.profile, enabled=bool(args.profile) and trainer.is_main_process)
     data_iter = iter(dataloader)
     start_time = time.time()
-    for step in range(trainer.global_step, tc.max_steps):
+    start_step = trainer.global_step
+    steady_t0, steady_tok0, steady_ckpt = None, 0, 0.0
+    for step in range(start_step, tc.max_steps):
         dbg.maybe_inject_fault(step, trainer.rank)
         try:
             batch = next(data_iter)
@@ -416,14 +426,31 @@ def main(argv=None):
             batch = next(data_iter)
         do_log = step % tc.log_interval == 0
         metrics = trainer.train_step({"input_ids": unwrap_batch(batch)}, sync_loss=do_log)
+        prof.step()
+        if step - start_step == 10:
+            steady_t0, steady_tok0 = time.time(), trainer.tokens_seen
         if do_log and trainer.is_main_process:
             elapsed = time.time() - start_time
             tps = metrics["tokens"] / max(elapsed, 1e-9)
             mem = trainer.get_memory_stats()
             print(f"Step {step:6d} | Loss: {metrics['loss']:.4f} | LR: {metrics['lr']:.2e} | "
                   f"Tokens/s: {tps:,.0f} | Mem: {mem['allocated_gb']:.1f}GB", flush=True)
+            if metrics_f:
+                rec = {"step": step, "loss": metrics["loss"], "lr": metrics["lr"], "tokens": metrics["tokens"],
+                       "tokens_per_sec": tps, **mem}
+                if trainer._last_norm is not None:
+                    rec["grad_norm"] = float(trainer._last_norm)
+                metrics_f.write(json.dumps(rec) + "\n")
+                metrics_f.flush()
         if step > 0 and step % tc.save_interval == 0:
+            t_ck = time.time()
             save(f"{tc.checkpoint_dir}/step_{step}")
+            if steady_t0 is not None:  # checkpoint I/O is not training throughput
+                steady_ckpt += time.time() - t_ck
+    if trainer.device.type == "cuda":
+        torch.cuda.synchronize(trainer.device)
+    steady_t1 = time.time()
+    prof.close()
     if not args.no_final_save:
         save(f"{tc.checkpoint_dir}/final")
     if trainer.is_main_process:
@@ -431,6 +458,20 @@ def main(argv=None):
         print(f"\nTraining complete! Total time: {total_time:.2f}s")
         print(f"Tokens processed: {trainer.tokens_seen:,}")
         print(f"Peak memory: {trainer.get_memory_stats()['max_allocated_gb']:.2f} GB")
+        if steady_t0 is not None:
+            from .ddp_trainer import PEAK_BF16_FLOPS
+            dt = max(steady_t1 - steady_t0 - steady_ckpt, 1e-9)
+            sps = (trainer.tokens_seen - steady_tok0) / dt
+            fpt = model_config.flops_per_token(model_config.max_seq_len, recompute=fc.activation_checkpointing)
+            mfu = sps / trainer.world_size * fpt / PEAK_BF16_FLOPS
+            print(f"Steady-state tokens/s (after step 10): {sps:,.0f} "
+                  f"({sps / trainer.world_size:,.0f}/GPU, MFU {100 * mfu:.1f}% of {PEAK_BF16_FLOPS / 1e15:.1f} PF dense bf16)")
+            if metrics_f:
+                metrics_f.write(json.dumps({"summary": True, "steady_tokens_per_sec": sps,
+                                            "tokens_per_sec_per_gpu": sps / trainer.world_size, "mfu": mfu,
+                                            **trainer.get_memory_stats()}) + "\n")
+    if metrics_f:
+        metrics_f.close()
     if trainer.distributed:
         dist.destroy_process_group()
     return trainer

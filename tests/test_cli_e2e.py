@@ -113,3 +113,16 @@ def test_fsdp_cli_sharded_save_resume_consolidate(tmp_path, capsys):
     ckpt_main(["consolidate", final, out])
     c = load_checkpoint(out)
     assert c["global_step"] == 6 and "fsdp_config" in c
+
+
+def test_fsdp_cli_metrics_jsonl_and_steady_state(tmp_path, capsys):
+    cfg = _yaml(tmp_path)
+    mj = str(tmp_path / "m.jsonl")
+    fsdp_trainer.main(["--config", cfg, "--max_steps", "13", "--checkpoint_dir", str(tmp_path / "c"),
+                       "--metrics_jsonl", mj, "--no_final_save", "--seed", "7"])
+    out = capsys.readouterr().out
+    assert "Steady-state tokens/s (after step 10)" in out and "MFU" in out
+    import json
+    recs = [json.loads(x) for x in open(mj)]
+    assert recs[-1]["summary"] and recs[-1]["steady_tokens_per_sec"] > 0
+    assert all("loss" in r and "grad_norm" in r for r in recs[:-1])
