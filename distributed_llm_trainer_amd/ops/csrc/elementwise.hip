@@ -307,3 +307,31 @@ DLT_API int dlt_swiglu_bwd(const bf16_t* gu, const bf16_t* da, bf16_t* dgu, int 
   k_swiglu_bwd<<<ew_blocks((size_t)M * (I / 8)), 256, 0, st>>>(gu, da, dgu, M, I);
   DLT_CHECK_LAUNCH();
 }
+
+// ---------------------------------------------------------------- split-K sum
+// dw[i] += sum_{s < splits} part[s * n + i], summed in fixed order (deterministic, no
+// atomics: DDP replicas must stay bit-identical).  float4 per lane; part comes from the
+// strided-batched split-K weight-gradient GEMM (ops/gemm.py wgrad_acc).  n % 4 == 0.
+__global__ __launch_bounds__(256) void k_splitk_acc(const float4* __restrict__ part, float4* __restrict__ dw,
+                                                    long n4, int splits) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    float4 a = dw[i];
+    for (int s = 0; s < splits; ++s) {
+      const float4 p = part[(long)s * n4 + i];
+      a.x += p.x;
+      a.y += p.y;
+      a.z += p.z;
+      a.w += p.w;
+    }
+    dw[i] = a;
+  }
+}
+
+DLT_API int dlt_splitk_acc(const float* part, float* dw, long n, int splits, hipStream_t s) {
+  if (n <= 0 || (n & 3) || splits < 1) return -1;
+  const long n4 = n / 4;
+  const int blocks = (int)std::min<long>((n4 + 255) / 256, 2048);
+  hipLaunchKernelGGL(k_splitk_acc, dim3(blocks), dim3(256), 0, s, reinterpret_cast<const float4*>(part),
+                     reinterpret_cast<float4*>(dw), n4, splits);
+  return (int)hipGetLastError();
+}

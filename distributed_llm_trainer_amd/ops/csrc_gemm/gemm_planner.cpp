@@ -36,9 +36,12 @@ namespace {
 
 struct Key {
   int ta, tb, m, n, k, lda, ldb, ldc, dta, dtb, dtc, accumulate;
+  int batch = 1;  // strided-batched (split-K wgrad): element strides of A, B, C
+  long long sa = 0, sb = 0, sc = 0;
   bool operator<(const Key& o) const {
-    return std::tie(ta, tb, m, n, k, lda, ldb, ldc, dta, dtb, dtc, accumulate) <
-           std::tie(o.ta, o.tb, o.m, o.n, o.k, o.lda, o.ldb, o.ldc, o.dta, o.dtb, o.dtc, o.accumulate);
+    return std::tie(ta, tb, m, n, k, lda, ldb, ldc, dta, dtb, dtc, accumulate, batch, sa, sb, sc) <
+           std::tie(o.ta, o.tb, o.m, o.n, o.k, o.lda, o.ldb, o.ldc, o.dta, o.dtb, o.dtc, o.accumulate, o.batch, o.sa,
+                    o.sb, o.sc);
   }
 };
 
@@ -120,6 +123,15 @@ int build_plan(const Key& k, Plan& p, const void* A, const void* B, void* C, hip
   if (hipblasLtMatrixLayoutCreate(&p.la, dt_of(k.dta), ar, ac, k.lda) != HIPBLAS_STATUS_SUCCESS) return -21;
   if (hipblasLtMatrixLayoutCreate(&p.lb, dt_of(k.dtb), br, bc, k.ldb) != HIPBLAS_STATUS_SUCCESS) return -22;
   if (hipblasLtMatrixLayoutCreate(&p.lc, dt_of(k.dtc), k.m, k.n, k.ldc) != HIPBLAS_STATUS_SUCCESS) return -23;
+  if (k.batch > 1) {
+    const int32_t bc32 = k.batch;
+    const int64_t st[3] = {k.sa, k.sb, k.sc};
+    hipblasLtMatrixLayout_t ls[3] = {p.la, p.lb, p.lc};
+    for (int i = 0; i < 3; ++i) {
+      hipblasLtMatrixLayoutSetAttribute(ls[i], HIPBLASLT_MATRIX_LAYOUT_BATCH_COUNT, &bc32, sizeof(bc32));
+      hipblasLtMatrixLayoutSetAttribute(ls[i], HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &st[i], sizeof(st[i]));
+    }
+  }
   hipblasLtMatmulPreference_t pref;
   hipblasLtMatmulPreferenceCreate(&pref);
   hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &g->wsz, sizeof(g->wsz));
@@ -141,7 +153,8 @@ int build_plan(const Key& k, Plan& p, const void* A, const void* B, void* C, hip
   hipEventCreate(&e1);
   float alpha = 1.f, beta0 = 0.f;
   std::vector<char> scratch;  // keep C intact for accumulate=1: save + restore
-  size_t csize = (size_t)k.ldc * k.n * (k.dtc == 0 ? 4 : 2);
+  size_t csize = (k.batch > 1 ? (size_t)k.sc * (k.batch - 1) : 0) + (size_t)k.ldc * k.n;
+  csize *= (k.dtc == 0 ? 4 : 2);
   void* cbak = nullptr;
   if (k.accumulate && hipMalloc(&cbak, csize) == hipSuccess)
     hipMemcpyAsync(cbak, C, csize, hipMemcpyDeviceToDevice, s);
@@ -187,10 +200,8 @@ int build_plan(const Key& k, Plan& p, const void* A, const void* B, void* C, hip
 }  // namespace
 
 // C[m,n] (col-major, ldc) = alpha * op(A) * op(B) + beta * C ; dtype codes: 0 fp32, 1 bf16, 2 fp16
-DLT_API int dlt_gemm(int ta, int tb, int m, int n, int k, const void* A, int lda, int dta, const void* B, int ldb,
-                     int dtb, void* C, int ldc, int dtc, float alpha, float beta, hipStream_t s) {
+static int gemm_impl(Key key, const void* A, const void* B, void* C, float alpha, float beta, hipStream_t s) {
   if (int rc = init()) return rc;
-  Key key{ta, tb, m, n, k, lda, ldb, ldc, dta, dtb, dtc, beta != 0.f ? 1 : 0};
   Plan* p;
   const StreamCtx* sc;
   {
@@ -209,6 +220,29 @@ DLT_API int dlt_gemm(int ta, int tb, int m, int n, int k, const void* A, int lda
   hipblasStatus_t st = hipblasLtMatmul(sc->h, p->desc, &alpha, A, p->la, B, p->lb, &beta, C, p->lc, C, p->lc,
                                        &p->algo, sc->ws, g->wsz, s);
   return st == HIPBLAS_STATUS_SUCCESS ? 0 : -30 - (int)st;
+}
+
+DLT_API int dlt_gemm(int ta, int tb, int m, int n, int k, const void* A, int lda, int dta, const void* B, int ldb,
+                     int dtb, void* C, int ldc, int dtc, float alpha, float beta, hipStream_t s) {
+  Key key{ta, tb, m, n, k, lda, ldb, ldc, dta, dtb, dtc, beta != 0.f ? 1 : 0};
+  return gemm_impl(key, A, B, C, alpha, beta, s);
+}
+
+// Strided-batched GEMM: `batch` independent problems, operand i at A + i*sa etc.
+// (element strides).  Used for split-K weight gradients: the token dimension is cut
+// into `batch` slices whose partial dW land in a [batch, n, ldc] fp32 scratch that is
+// then summed into the accumulator -- the skinny 768x768 / 768x2304 wgrads have too
+// few output tiles to fill 256 CUs with K = 32768 on one tile per CU.
+DLT_API int dlt_gemm_batched(int ta, int tb, int m, int n, int k, const void* A, int lda, int dta, long long sa,
+                             const void* B, int ldb, int dtb, long long sb, void* C, int ldc, int dtc, long long sc,
+                             int batch, float alpha, float beta, hipStream_t s) {
+  if (batch < 1) return -5;
+  Key key{ta, tb, m, n, k, lda, ldb, ldc, dta, dtb, dtc, beta != 0.f ? 1 : 0};
+  key.batch = batch;
+  key.sa = sa;
+  key.sb = sb;
+  key.sc = sc;
+  return gemm_impl(key, A, B, C, alpha, beta, s);
 }
 
 DLT_API int dlt_gemm_num_plans() { return g ? (int)g->plans.size() : 0; }

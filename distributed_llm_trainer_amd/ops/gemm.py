@@ -33,6 +33,10 @@ def lib():
         L.dlt_gemm.argtypes = [c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, c.c_void_p, c.c_int, c.c_int, c.c_void_p,
                                c.c_int, c.c_int, c.c_void_p, c.c_int, c.c_int, c.c_float, c.c_float, c.c_void_p]
         L.dlt_gemm.restype = c.c_int
+        L.dlt_gemm_batched.argtypes = [c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, c.c_void_p, c.c_int, c.c_int,
+                                       c.c_longlong, c.c_void_p, c.c_int, c.c_int, c.c_longlong, c.c_void_p, c.c_int,
+                                       c.c_int, c.c_longlong, c.c_int, c.c_float, c.c_float, c.c_void_p]
+        L.dlt_gemm_batched.restype = c.c_int
         L.dlt_gemm_report.argtypes = [c.c_char_p, c.c_int]
         L.dlt_gemm_report.restype = c.c_int
         _LIB = L
@@ -68,6 +72,14 @@ def _gemm(ta, tb, m, n, k, A, lda, B, ldb, C, ldc, alpha=1.0, beta=0.0):
         raise RuntimeError(f"dlt_gemm failed ({rc}) for ta={ta} tb={tb} m={m} n={n} k={k}")
 
 
+def _gemm_batched(ta, tb, m, n, k, A, lda, sa, B, ldb, sb, C, ldc, sc, batch, alpha=1.0, beta=0.0):
+    rc = lib().dlt_gemm_batched(ta, tb, m, n, k, ctypes.c_void_p(A.data_ptr()), lda, _DT[A.dtype], sa,
+                                ctypes.c_void_p(B.data_ptr()), ldb, _DT[B.dtype], sb, ctypes.c_void_p(C.data_ptr()),
+                                ldc, _DT[C.dtype], sc, batch, alpha, beta, _stream())
+    if rc != 0:
+        raise RuntimeError(f"dlt_gemm_batched failed ({rc}) for ta={ta} tb={tb} m={m} n={n} k={k} batch={batch}")
+
+
 def _rowmajor(t: torch.Tensor) -> int:
     """Leading dimension of a row-major 2-D tensor (must be unit-stride in dim 1)."""
     if t.dim() != 2 or t.stride(1) != 1:
@@ -87,9 +99,13 @@ class HipGemm:
 
     stream_safe = True
 
+    SPLITK_CANDIDATES = (2, 4, 8)
+
     def __init__(self):
         self._choice = {}  # (M, N, K) -> None (library) or tile cfg of gemm_tn
         self._race = os.environ.get("DLT_GEMM_TN", "1") != "0"
+        self._splitk = {}  # wgrad (M, N, K) -> number of token slices (1 = plain accumulate GEMM)
+        self._splitk_on = os.environ.get("DLT_WGRAD_SPLITK", "1") != "0"
 
     def _lib_linear(self, x, w, y):
         M, K = x.shape
@@ -142,8 +158,11 @@ class HipGemm:
         return y
 
     def report_choices(self) -> dict:
-        return {f"M{m}xN{n}xK{k}": ("hipBLASLt" if c is None else f"gemm_tn cfg{c}")
-                for (m, n, k), c in self._choice.items()}
+        out = {f"M{m}xN{n}xK{k}": ("hipBLASLt" if c is None else f"gemm_tn cfg{c}")
+               for (m, n, k), c in self._choice.items()}
+        out.update({f"wgrad M{m}xN{n}xK{k}": f"split-K x{s}" if s > 1 else "hipBLASLt accumulate"
+                    for (m, n, k), s in self._splitk.items()})
+        return out
 
     def linear_dgrad(self, dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         M, N = dy.shape
@@ -152,10 +171,70 @@ class HipGemm:
         _gemm(0, 0, K, M, N, w, _rowmajor(w), dy, _rowmajor(dy), dx, K)
         return dx
 
+    @staticmethod
+    def _wgrad_plain(dw2, dy, x):
+        M, N = dy.shape
+        K = x.shape[1]
+        _gemm(0, 1, K, N, M, x, _rowmajor(x), dy, _rowmajor(dy), dw2, K, 1.0, 1.0)
+
+    @staticmethod
+    def _wgrad_split(dw2, dy, x, s):
+        """Split-K over tokens: s strided-batched GEMMs (slice i = rows [i*M/s, (i+1)*M/s))
+        into an fp32 [s, N, K] scratch, then one fixed-order sum into dw (hip.splitk_acc).
+        The skinny wgrads (768x768, 768x2304 outputs, K = 32768 tokens) have too few
+        output tiles for 256 CUs; slicing K multiplies the tile count by s."""
+        from . import hip
+        M, N = dy.shape
+        K = x.shape[1]
+        ms = M // s
+        lx, ly = _rowmajor(x), _rowmajor(dy)
+        part = torch.empty(s, N, K, dtype=torch.float32, device=dw2.device)
+        _gemm_batched(0, 1, K, N, ms, x, lx, ms * lx, dy, ly, ms * ly, part, K, N * K, s, 1.0, 0.0)
+        hip.splitk_acc(part, dw2)
+
+    def _pick_splitk(self, dw2, dy, x):
+        M, N = dy.shape
+        K = x.shape[1]
+        key = (M, N, K)
+        if key in self._splitk:
+            return self._splitk[key]
+        cands = [s for s in self.SPLITK_CANDIDATES if M % (s * 8) == 0 and (N * K) % 4 == 0]
+        if (not self._splitk_on or not cands or N * K > 4096 * 4096
+                or torch.cuda.is_current_stream_capturing()):
+            self._splitk[key] = 1
+            return 1
+        scratch = torch.zeros_like(dw2)  # timing must not disturb the real accumulator
+
+        def t_of(fn):
+            fn()
+            torch.cuda.synchronize()
+            best = float("inf")
+            for _ in range(3):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(3):
+                    fn()
+                e1.record()
+                e1.synchronize()
+                best = min(best, e0.elapsed_time(e1))
+            return best
+        best, choice = t_of(lambda: self._wgrad_plain(scratch, dy, x)), 1
+        for s in cands:
+            t = t_of(lambda: self._wgrad_split(scratch, dy, x, s))
+            if t < 0.93 * best:
+                best, choice = t, s
+        del scratch
+        self._splitk[key] = choice
+        return choice
+
     def wgrad_acc(self, dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
         M, N = dy.shape
         K = x.shape[1]
         dw2 = dw.view(N, K)
         if dw2.dtype != torch.float32 or not dw2.is_contiguous():
             raise ValueError("wgrad accumulator must be contiguous fp32")
-        _gemm(0, 1, K, N, M, x, _rowmajor(x), dy, _rowmajor(dy), dw2, K, 1.0, 1.0)
+        s = self._pick_splitk(dw2, dy, x)
+        if s > 1:
+            self._wgrad_split(dw2, dy, x, s)
+        else:
+            self._wgrad_plain(dw2, dy, x)

@@ -33,6 +33,7 @@ _SIGS = {
                         c_void_p, c_void_p, c_int, c_int, c_uint32, c_uint32, c_float, c_void_p],
     "dlt_embedding_fwd": [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p],
     "dlt_embedding_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
+    "dlt_splitk_acc": [c_void_p, c_void_p, ctypes.c_long, c_int, c_void_p],
     "dlt_rope_qkv_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                          c_void_p],
     "dlt_rope_qkv_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
@@ -117,6 +118,17 @@ def rope_tables(head_dim: int, seq_len: int, device=None):
     from .reference import rope_tables as rt
     c, s = rt(head_dim, seq_len, device=device)
     return c.contiguous(), s.contiguous()
+
+
+# ---------------------------------------------------------------- split-K
+def splitk_acc(part: torch.Tensor, dw: torch.Tensor) -> None:
+    """dw += part.sum(0) in fixed order (deterministic); part [splits, *dw.shape] fp32."""
+    _req(dw, torch.float32, "splitk_acc.dw")
+    _req(part, torch.float32, "splitk_acc.part")
+    n = dw.numel()
+    if part.numel() % n or n % 4:
+        raise ValueError("splitk_acc: part must hold whole copies of dw and dw.numel() % 4 == 0")
+    _chk(lib().dlt_splitk_acc(_p(part), _p(dw), n, part.numel() // n, _stream()), "splitk_acc")
 
 
 # ---------------------------------------------------------------- embedding
