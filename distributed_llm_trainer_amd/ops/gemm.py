@@ -99,7 +99,7 @@ class HipGemm:
 
     stream_safe = True
 
-    SPLITK_CANDIDATES = (2, 4, 8)
+    SPLITK_CANDIDATES = (2, 4, 8, 16)
 
     def __init__(self):
         self._choice = {}  # (M, N, K) -> None (library) or tile cfg of gemm_tn

@@ -62,3 +62,4 @@ a, b = r(8192, 8192), r(8192, 8192)
 t = bench(lambda: torch.matmul(a, b), it=10)
 print(f"square 8192^3 torch.matmul: {t:.0f} us = {2 * 8192 ** 3 / t / 1e6:.0f} TF/s")
 print(gemm.report())
+print(g.report_choices())
