@@ -74,6 +74,7 @@ struct Planner {
   int max_cand = 24;
   bool tune = true;
   bool verbose = false;
+  bool drain = true;  // DLT_GEMM_TUNE_DRAIN=0: time candidates without draining the device first
 };
 
 Planner* g = nullptr;
@@ -92,6 +93,8 @@ int init() {
   if (e && atoi(e) == 0) p->tune = false;
   e = getenv("DLT_GEMM_VERBOSE");
   p->verbose = e && atoi(e) != 0;
+  e = getenv("DLT_GEMM_TUNE_DRAIN");
+  if (e && atoi(e) == 0) p->drain = false;
   g = p;
   return 0;
 }
@@ -148,6 +151,12 @@ int build_plan(const Key& k, Plan& p, const void* A, const void* B, void* C, hip
   // Autotune on the caller's stream.  Timing needs a host sync; this runs once per
   // shape (warmup step).  beta = 0 while timing so an accumulating GEMM does not
   // disturb C (its real call comes right after with the requested beta).
+  // Drain the whole device first: with micro-step pipelining the other HIP stream may
+  // still be running compute, and under DDP an RCCL all-reduce kernel may be spinning on
+  // CUs waiting for a slower peer; either would bias the timings below towards kernels
+  // that do well on fewer CUs.  (No deadlock: every collective this rank waits for was
+  // launched by it, and peers launch collectives in the same order.)
+  if (g->drain) hipDeviceSynchronize();
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
