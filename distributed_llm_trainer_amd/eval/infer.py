@@ -15,7 +15,7 @@ import torch
 from ..data.tokenizer import get_tokenizer
 from ..models.config import GPTConfig
 from ..models.gpt import GPT
-from ..utils.checkpoint import load_checkpoint
+from ..utils.checkpoint import load_checkpoint, load_model_state
 
 
 def pick_device(name: str) -> torch.device:
@@ -30,7 +30,7 @@ def load_model(path: str, model_size: str = None, device="cpu"):
     if model_size is not None or not isinstance(cfg, GPTConfig):
         cfg = GPTConfig.from_preset(model_size or "small")
     model = GPT(cfg)
-    model.load_state_dict(ckpt["model"], strict=False)
+    load_model_state(model, ckpt["model"])
     model = model.to(device)
     if torch.device(device).type == "cuda":
         model.enable_engine()

@@ -14,7 +14,11 @@
 //   * owns one hipBLASLt handle and one device workspace per stream
 //     (DLT_GEMM_WORKSPACE_MB, default 64), so GEMMs on the compute and side streams
 //     can run concurrently (see StreamCtx),
-//   * records the chosen kernel's name for the plan report.
+//   * records the chosen kernel's name for the plan report,
+//   * accepts pinned picks (dlt_gemm_pin: key -> heuristic index) so a run can replay
+//     another run's choices without timing (ops/gemm.py DLT_GEMM_PLAN); with the same
+//     hipBLASLt build the heuristic list of a key is deterministic, so the index names
+//     the same kernel.
 // C ABI, loaded by ctypes from ops/gemm.py.
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt.h>
@@ -75,6 +79,8 @@ struct Planner {
   bool tune = true;
   bool verbose = false;
   bool drain = true;  // DLT_GEMM_TUNE_DRAIN=0: time candidates without draining the device first
+  bool fail_backup = false;  // test hook: behave as if the accumulator backup could not be allocated
+  std::map<Key, int> pins;   // key -> heuristic index (replayed plan)
 };
 
 Planner* g = nullptr;
@@ -147,6 +153,15 @@ int build_plan(const Key& k, Plan& p, const void* A, const void* B, void* C, hip
   p.algo = res[0].algo;
   p.ws = res[0].workspaceSize;
   p.candidates = n;
+  auto pin = g->pins.find(k);
+  if (pin != g->pins.end() && pin->second >= 0 && pin->second < n &&
+      res[pin->second].workspaceSize <= g->wsz) {
+    p.algo = res[pin->second].algo;
+    p.ws = res[pin->second].workspaceSize;
+    p.chosen = pin->second;
+    p.kernel = hipblaslt_ext::getKernelNameFromAlgo(g->h, p.algo);
+    return 0;
+  }
   if (!g->tune || n == 1 || capturing(s)) return 0;
   // Autotune on the caller's stream.  Timing needs a host sync; this runs once per
   // shape (warmup step).  beta = 0 while timing so an accumulating GEMM does not
@@ -157,16 +172,24 @@ int build_plan(const Key& k, Plan& p, const void* A, const void* B, void* C, hip
   // that do well on fewer CUs.  (No deadlock: every collective this rank waits for was
   // launched by it, and peers launch collectives in the same order.)
   if (g->drain) hipDeviceSynchronize();
-  hipEvent_t e0, e1;
-  hipEventCreate(&e0);
-  hipEventCreate(&e1);
   float alpha = 1.f, beta0 = 0.f;
-  std::vector<char> scratch;  // keep C intact for accumulate=1: save + restore
   size_t csize = (k.batch > 1 ? (size_t)k.sc * (k.batch - 1) : 0) + (size_t)k.ldc * k.n;
   csize *= (k.dtc == 0 ? 4 : 2);
   void* cbak = nullptr;
-  if (k.accumulate && hipMalloc(&cbak, csize) == hipSuccess)
+  if (k.accumulate) {
+    // The candidates are timed IN PLACE with beta = 0, which overwrites C.  Without a
+    // backup of the accumulator the real beta = 1 call would add to A*B instead of the
+    // old C (a silently corrupted gradient), so no backup => no timing: keep the
+    // heuristic's first pick.
+    if (g->fail_backup || hipMalloc(&cbak, csize) != hipSuccess) {
+      (void)hipGetLastError();  // do not let the failed allocation surface at the next launch check
+      return 0;
+    }
     hipMemcpyAsync(cbak, C, csize, hipMemcpyDeviceToDevice, s);
+  }
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
   float best = 1e30f;
   int bi = 0;
   for (int i = 0; i < n; ++i) {
@@ -255,6 +278,49 @@ DLT_API int dlt_gemm_batched(int ta, int tb, int m, int n, int k, const void* A,
 }
 
 DLT_API int dlt_gemm_num_plans() { return g ? (int)g->plans.size() : 0; }
+
+// Test hook: pretend the accumulator backup allocation fails (accumulating keys first
+// seen afterwards are not timed).
+DLT_API int dlt_gemm_test_fail_backup(int on) {
+  if (int rc = init()) return rc;
+  std::lock_guard<std::mutex> lk(g->mu);
+  g->fail_backup = on != 0;
+  return 0;
+}
+
+// Pin the heuristic index of a key (must be called before the key is first used).
+DLT_API int dlt_gemm_pin(int ta, int tb, int m, int n, int k, int lda, int ldb, int ldc, int dta, int dtb, int dtc,
+                         int accumulate, int batch, long long sa, long long sb, long long sc, int chosen) {
+  if (int rc = init()) return rc;
+  Key key{ta, tb, m, n, k, lda, ldb, ldc, dta, dtb, dtc, accumulate ? 1 : 0};
+  key.batch = batch;
+  key.sa = sa;
+  key.sb = sb;
+  key.sc = sc;
+  std::lock_guard<std::mutex> lk(g->mu);
+  g->pins[key] = chosen;
+  return 0;
+}
+
+// Machine-readable plan table: one line per key,
+// "ta tb m n k lda ldb ldc dta dtb dtc acc batch sa sb sc chosen" (input of dlt_gemm_pin).
+DLT_API int dlt_gemm_dump(char* buf, int len) {
+  if (!g || len <= 0) return 0;
+  std::string out;
+  std::lock_guard<std::mutex> lk(g->mu);
+  for (auto& kv : g->plans) {
+    const Key& k = kv.first;
+    char line[256];
+    snprintf(line, sizeof(line), "%d %d %d %d %d %d %d %d %d %d %d %d %d %lld %lld %lld %d\n", k.ta, k.tb, k.m, k.n,
+             k.k, k.lda, k.ldb, k.ldc, k.dta, k.dtb, k.dtc, k.accumulate, k.batch, k.sa, k.sb, k.sc,
+             kv.second.chosen);
+    out += line;
+  }
+  if (out.size() + 1 > (size_t)len) return -1;
+  memcpy(buf, out.data(), out.size());
+  buf[out.size()] = 0;
+  return (int)out.size();
+}
 
 // Dump the plan table (shape, chosen candidate, measured us) for profiles/ and logs.
 DLT_API int dlt_gemm_report(char* buf, int len) {

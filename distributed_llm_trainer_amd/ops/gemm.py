@@ -10,6 +10,16 @@ Row-major PyTorch operands are mapped onto column-major BLAS calls (a row-major
 Each distinct shape is autotuned once on first use (see ``csrc_gemm/gemm_planner.cpp``).
 If the planner library cannot be loaded, the engine uses torch.matmul (also hipBLASLt,
 default heuristics) and logs why.
+
+Reproducibility.  Autotuning picks the hipBLASLt algorithm, the split-K factor of the
+weight gradients and the hand-written-vs-library race per process by timing, so the
+summation order of a weight gradient (and the last bits of a loss curve) can differ
+between runs, or between a run and its resumed continuation.  ``DLT_GEMM_PLAN=path``
+pins them: if the file exists every choice is replayed from it (no timing); otherwise
+the first process to finish a step writes it (``save_plan``).  DDP replicas stay in
+sync regardless (the all-reduced gradient is identical on every rank).  For bitwise
+run-to-run reproducibility without a plan file use ``DLT_GEMM_TUNE=0
+DLT_WGRAD_SPLITK=0 DLT_GEMM_TN=0`` (heuristic #0 everywhere).
 """
 from __future__ import annotations
 
@@ -39,8 +49,84 @@ def lib():
         L.dlt_gemm_batched.restype = c.c_int
         L.dlt_gemm_report.argtypes = [c.c_char_p, c.c_int]
         L.dlt_gemm_report.restype = c.c_int
+        L.dlt_gemm_dump.argtypes = [c.c_char_p, c.c_int]
+        L.dlt_gemm_dump.restype = c.c_int
+        L.dlt_gemm_pin.argtypes = [c.c_int] * 13 + [c.c_longlong] * 3 + [c.c_int]
+        L.dlt_gemm_pin.restype = c.c_int
+        L.dlt_gemm_test_fail_backup.argtypes = [c.c_int]
+        L.dlt_gemm_test_fail_backup.restype = c.c_int
         _LIB = L
+        _load_plan_env()
     return _LIB
+
+
+# ---------------------------------------------------------------- plan pinning
+_PINNED = {"tn": {}, "splitk": {}}  # replayed framework-level choices (see module docstring)
+_PLAN_STATE = {"path": None, "loaded": False, "saved": False}
+_INSTANCES = []  # weak references to live HipGemm objects (for save_plan)
+
+
+def _load_plan_env() -> None:
+    path = os.environ.get("DLT_GEMM_PLAN")
+    _PLAN_STATE["path"] = path
+    if path and os.path.exists(path):
+        load_plan(path)
+
+
+def load_plan(path: str) -> None:
+    """Pin every choice recorded in a plan file written by :func:`save_plan`."""
+    import json
+    with open(path) as f:
+        plan = json.load(f)
+    L = lib()
+    for line in plan.get("hipblaslt", []):
+        v = [int(x) for x in line.split()]
+        if len(v) != 17:
+            raise ValueError(f"bad hipBLASLt plan line {line!r} in {path}")
+        rc = L.dlt_gemm_pin(*v)
+        if rc != 0:
+            raise RuntimeError(f"dlt_gemm_pin failed ({rc})")
+    _PINNED["tn"] = {tuple(int(x) for x in k.split("x")): (None if c is None else int(c))
+                     for k, c in plan.get("tn", {}).items()}
+    _PINNED["splitk"] = {tuple(int(x) for x in k.split("x")): int(c) for k, c in plan.get("splitk", {}).items()}
+    _PLAN_STATE["loaded"] = True
+
+
+def export_plan() -> dict:
+    """Every choice made so far in this process (hipBLASLt heuristic indices, the
+    hand-written GEMM race and the split-K factors of all live HipGemm objects)."""
+    buf = ctypes.create_string_buffer(1 << 20)
+    n = lib().dlt_gemm_dump(buf, len(buf))
+    if n < 0:
+        raise RuntimeError("plan table too large")
+    tn, sk = dict(_PINNED["tn"]), dict(_PINNED["splitk"])
+    for ref in _INSTANCES:
+        g = ref()
+        if g is not None:
+            tn.update(g._choice)
+            sk.update(g._splitk)
+    return {"hipblaslt": [ln for ln in buf.value[:n].decode().splitlines() if ln],
+            "tn": {"x".join(map(str, k)): c for k, c in tn.items()},
+            "splitk": {"x".join(map(str, k)): c for k, c in sk.items()}}
+
+
+def save_plan(path: str) -> None:
+    import json
+    tmp = f"{path}.tmp{os.getpid()}"
+    with open(tmp, "w") as f:
+        json.dump(export_plan(), f, indent=1)
+    os.replace(tmp, path)
+
+
+def maybe_save_plan() -> None:
+    """Called by the trainers after a step: with ``DLT_GEMM_PLAN`` set and no plan file
+    yet, write this process's choices once (rank 0 of a job, or a single process)."""
+    path = _PLAN_STATE["path"]
+    if _LIB is None or not path or _PLAN_STATE["loaded"] or _PLAN_STATE["saved"]:
+        return
+    _PLAN_STATE["saved"] = True
+    if int(os.environ.get("RANK", "0")) == 0 and not os.path.exists(path):
+        save_plan(path)
 
 
 def available() -> bool:
@@ -102,10 +188,13 @@ class HipGemm:
     SPLITK_CANDIDATES = (2, 4, 8, 16)
 
     def __init__(self):
-        self._choice = {}  # (M, N, K) -> None (library) or tile cfg of gemm_tn
+        import weakref
+        lib()  # loads DLT_GEMM_PLAN pins before any choice is made
+        self._choice = dict(_PINNED["tn"])  # (M, N, K) -> None (library) or tile cfg of gemm_tn
         self._race = os.environ.get("DLT_GEMM_TN", "1") != "0"
-        self._splitk = {}  # wgrad (M, N, K) -> number of token slices (1 = plain accumulate GEMM)
+        self._splitk = dict(_PINNED["splitk"])  # wgrad (M, N, K) -> token slices (1 = plain accumulate GEMM)
         self._splitk_on = os.environ.get("DLT_WGRAD_SPLITK", "1") != "0"
+        _INSTANCES.append(weakref.ref(self))
 
     def _lib_linear(self, x, w, y):
         M, K = x.shape

@@ -82,6 +82,15 @@ def memory_stats(device) -> dict:
             "max_allocated_gb": torch.cuda.max_memory_allocated(device) / 1e9}
 
 
+def gemm_plan_hook() -> None:
+    """After a step: write the GEMM plan file once if ``DLT_GEMM_PLAN`` asks for one
+    (``ops/gemm.py`` ``maybe_save_plan``; a no-op without the planner)."""
+    if not os.environ.get("DLT_GEMM_PLAN"):
+        return
+    from ..ops import gemm
+    gemm.maybe_save_plan()
+
+
 def unwrap_batch(batch):
     if isinstance(batch, dict):
         return batch["input_ids"]

@@ -40,7 +40,7 @@ from ..parallel.flat import FlatParamStore
 from ..utils import checkpoint as ckpt
 from ..utils import debug as dbg
 from ..utils.profiling import Profiler, range_push, range_pop
-from .common import cosine_lr, memory_stats, seed_all, select_device, setup_distributed, unwrap_batch
+from .common import cosine_lr, gemm_plan_hook, memory_stats, seed_all, select_device, setup_distributed, unwrap_batch
 from .configs import TrainingConfig
 from .optim import flat_store_optimizer
 
@@ -203,6 +203,8 @@ class DistributedTrainer:
             lr = self.optimizer.param_groups[0]["lr"]
         self.global_step += 1
         self.tokens_seen += input_ids.numel() * self.world_size
+        if self.use_engine and self.global_step >= 2:
+            gemm_plan_hook()
         out = {"loss": total.item() if sync_loss else total, "lr": lr, "tokens": self.tokens_seen}
         return out
 
@@ -222,9 +224,7 @@ class DistributedTrainer:
 
     def load_checkpoint(self, path: str):
         c = ckpt.load_checkpoint(path, map_location="cpu")
-        sd = c["model"]
-        with torch.no_grad():
-            self.model.load_state_dict(sd, strict=False)
+        ckpt.load_model_state(self.model, c["model"])
         self.store.refresh_shadow()
         self.optimizer.load_state_dict(c["optimizer"])
         self.global_step = int(c["global_step"])

@@ -33,7 +33,7 @@ from ..parallel.fsdp import FSDPRuntime
 from ..utils import checkpoint as ckpt
 from ..utils import debug as dbg
 from ..utils.profiling import Profiler
-from .common import cosine_lr, memory_stats, seed_all, select_device, setup_distributed, unwrap_batch
+from .common import cosine_lr, gemm_plan_hook, memory_stats, seed_all, select_device, setup_distributed, unwrap_batch
 from .configs import FSDPConfig, FSDPTrainingConfig
 from .optim import FlatAdamW
 
@@ -165,6 +165,8 @@ class FSDPTrainer:
             lr = self.optimizer.param_groups[0]["lr"]
         self.global_step += 1
         self.tokens_seen += input_ids.numel() * self.world_size
+        if self.global_step >= 2:
+            gemm_plan_hook()
         return {"loss": total.item() if sync_loss else total, "lr": lr, "tokens": self.tokens_seen}
 
     # ------------------------------------------------------------ checkpoints
@@ -294,6 +296,7 @@ class FSDPTrainer:
         c = ckpt.load_checkpoint(path, map_location="cpu") if (self.is_main_process or not self.distributed) else None
         meta = [None]
         if self.is_main_process or not self.distributed:
+            c["model"] = ckpt.normalize_state_dict_keys(c["model"])
             osd = c["optimizer"]
             steps = [int(float(s["step"])) for s in osd["state"].values()] if osd.get("state") else [0]
             meta[0] = (int(c["global_step"]), int(c["tokens_seen"]), max(steps) if steps else 0)

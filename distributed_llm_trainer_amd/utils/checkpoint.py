@@ -156,6 +156,37 @@ def consolidate_sharded(path: str, out: Optional[str] = None) -> Dict[str, Any]:
     return payload
 
 
+_ROPE_BUFFERS = (".rotary_emb.inv_freq", ".rotary_emb.cos_cached", ".rotary_emb.sin_cached")
+
+
+def normalize_state_dict_keys(sd: Dict[str, Any]) -> Dict[str, Any]:
+    """Drop wrapper prefixes (DDP ``module.``, ``torch.compile``'s ``_orig_mod.``,
+    FSDP / checkpoint-wrapper module names) that a checkpoint written by another
+    trainer may carry."""
+    out = {}
+    for k, v in sd.items():
+        parts = [p for p in k.split(".") if p not in ("module", "_orig_mod", "_fsdp_wrapped_module",
+                                                       "_checkpoint_wrapped_module")]
+        out[".".join(parts)] = v
+    return out
+
+
+@torch.no_grad()
+def load_model_state(model: torch.nn.Module, sd: Dict[str, Any]) -> None:
+    """Load a reference-format ``"model"`` state dict, strictly.
+
+    The only keys allowed to be missing are the RoPE buffers (deterministic, rebuilt by
+    the model); any other missing key or any unexpected key raises -- a checkpoint of a
+    different model (or one whose keys do not match) must not silently leave random
+    weights in place while training continues."""
+    res = model.load_state_dict(normalize_state_dict_keys(sd), strict=False)
+    missing = [k for k in res.missing_keys if not k.endswith(_ROPE_BUFFERS)]
+    if missing or res.unexpected_keys:
+        raise RuntimeError(f"checkpoint does not match the model: missing {missing[:8]}"
+                           f"{'...' if len(missing) > 8 else ''} ({len(missing)}), unexpected "
+                           f"{list(res.unexpected_keys)[:8]} ({len(res.unexpected_keys)})")
+
+
 def config_to_dict(cfg) -> Dict[str, Any]:
     if dataclasses.is_dataclass(cfg):
         return dataclasses.asdict(cfg)

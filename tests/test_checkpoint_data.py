@@ -116,3 +116,26 @@ def test_dummy_loader_seeded_drop_last():
     assert a.shape == (4, 16)
     dl = create_dummy_dataloader(3, 16, 100, num_batches=2, seed=1, native=False)
     assert all(x[0].shape[0] == 3 for x in dl)
+
+
+def test_load_model_state_is_strict():
+    """Loading a model state dict: wrapper prefixes are stripped, missing RoPE buffers
+    are tolerated (deterministic), anything else missing or unexpected raises instead
+    of silently leaving random weights in place."""
+    from distributed_llm_trainer_amd.models.gpt import GPT
+    from distributed_llm_trainer_amd.utils.checkpoint import load_model_state
+    cfg = GPTConfig(vocab_size=64, hidden_size=32, num_layers=1, num_heads=2, max_seq_len=16)
+    torch.manual_seed(0)
+    src = GPT(cfg)
+    dst = GPT(cfg)
+    sd = {f"module.{k}": v for k, v in src.state_dict().items() if "rotary_emb" not in k}
+    load_model_state(dst, sd)
+    assert torch.equal(dst.embed_tokens.weight, src.embed_tokens.weight)
+    bad = dict(sd)
+    bad.pop("module.layers.0.mlp.up_proj.weight")
+    with pytest.raises(RuntimeError, match="missing"):
+        load_model_state(GPT(cfg), bad)
+    extra = dict(sd)
+    extra["module.layers.5.mlp.up_proj.weight"] = torch.zeros(1)
+    with pytest.raises(RuntimeError, match="unexpected"):
+        load_model_state(GPT(cfg), extra)

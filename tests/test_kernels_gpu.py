@@ -291,7 +291,9 @@ def test_wgrad_splitk(M, N, K):
     dy = torch.randn(M, N, device=DEV).bfloat16()
     base = torch.randn(N, K, device=DEV)
     ref = base + dy.float().t() @ x.float()
-    for s in (2, 4, 8):
+    cands = [s for s in gemm.HipGemm.SPLITK_CANDIDATES if M % (s * 8) == 0]
+    assert cands, "every tested shape must exercise split-K"
+    for s in cands:  # every factor the tuner can pick
         dw = base.clone()
         g._wgrad_split(dw, dy, x, s)
         _close(dw, ref, 1e-2 * M ** 0.5, 1e-3, f"split-K x{s}")
@@ -302,6 +304,57 @@ def test_wgrad_splitk(M, N, K):
     g.wgrad_acc(dw, dy, x)
     _close(dw, ref, 1e-2 * M ** 0.5, 1e-3, "wgrad auto")
     assert (M, N, K) in g._splitk
+
+
+def test_gemm_planner_accumulate_without_backup():
+    """An accumulating GEMM whose autotune cannot back up C must not be timed in place
+    (timing with beta = 0 would overwrite the accumulator and the real call would then
+    return 2*A*B): the planner keeps the heuristic pick and dw == base + dy^T x."""
+    from distributed_llm_trainer_amd.ops import gemm
+    g = gemm.HipGemm()
+    L = gemm.lib()
+    M, N, K = 1536, 640, 320  # a key no other test uses (plans are cached per process)
+    torch.manual_seed(1)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    dy = torch.randn(M, N, device=DEV).bfloat16()
+    base = torch.randn(N, K, device=DEV)
+    ref = base + dy.float().t() @ x.float()
+    assert L.dlt_gemm_test_fail_backup(1) == 0
+    try:
+        dw = base.clone()
+        g._wgrad_plain(dw, dy, x)
+        torch.cuda.synchronize()
+    finally:
+        L.dlt_gemm_test_fail_backup(0)
+    _close(dw, ref, 1e-2 * M ** 0.5, 1e-3, "wgrad acc without backup")
+    line = [ln for ln in gemm.report().splitlines() if f"m={K} n={N} k={M} acc=1" in ln]
+    assert line and "chosen=0" in line[0], line
+
+
+def test_gemm_plan_pin_roundtrip(tmp_path):
+    """DLT_GEMM_PLAN machinery: export the plan table, and a pinned index is used for a
+    key first seen afterwards (no timing)."""
+    from distributed_llm_trainer_amd.ops import gemm
+    g = gemm.HipGemm()
+    x = torch.randn(512, 384, device=DEV).bfloat16()
+    w = torch.randn(640, 384, device=DEV).bfloat16()
+    g.linear(x, w)
+    plan = gemm.export_plan()
+    assert any(ln.split()[2:5] == ["640", "512", "384"] for ln in plan["hipblaslt"])
+    assert "512x640x384" in plan["tn"]
+    path = tmp_path / "plan.json"
+    gemm.save_plan(str(path))
+    # pin heuristic #1 for a fresh forward key (m=N, n=M, k=K in BLAS terms)
+    M, N, K = 768, 896, 384
+    assert gemm.lib().dlt_gemm_pin(1, 0, N, M, K, K, K, N, 1, 1, 1, 0, 1, 0, 0, 0, 1) == 0
+    x2 = torch.randn(M, K, device=DEV).bfloat16()
+    w2 = torch.randn(N, K, device=DEV).bfloat16()
+    y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    g._lib_linear(x2, w2, y)
+    _close(y, x2.float() @ w2.float().t(), 0.05 * K ** 0.5, 2e-2, "pinned linear")
+    line = [ln for ln in gemm.report().splitlines() if f"m={N} n={M} k={K} acc=0" in ln]
+    assert line and ("chosen=1" in line[0] or "cand=1 " in line[0]), line
+    gemm.load_plan(str(path))  # loading a saved plan re-pins without error
 
 
 @pytest.mark.parametrize("M,N,K", [(1024, 256, 128), (2048, 768, 384)])
