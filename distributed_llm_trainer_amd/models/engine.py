@@ -202,7 +202,10 @@ class GPTEngine:
         tools/wgrad_m_test.py).  Memory: ~250 MB per layer per micro-step (small).
         """
         self.acc_slot, self.acc_slots = int(slot), int(n_slots)
-        self.defer = bool(defer) and n_slots > 1
+        # A one-micro-step window defers too (DLT_DEFER_GA1=0: inline wgrads): the slot
+        # buffers then let the weight-gradient GEMMs run on the side stream, overlapped
+        # with the next layer's dgrad chain (attention/norm/SwiGLU backward).
+        self.defer = bool(defer) and (n_slots > 1 or os.environ.get("DLT_DEFER_GA1", "1") != "0")
 
     def _slot_buf(self, st, layer, name: str, M: int, N: int, device):
         key = (layer, name)

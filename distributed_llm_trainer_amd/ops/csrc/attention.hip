@@ -104,12 +104,22 @@ __device__ __forceinline__ void tile_barrier() {
   __syncthreads();
 }
 
+// Accumulator registers 8s..8s+7 as a bf16 MFMA operand: one v_cvt_pk_bf16_f32 per
+// pair (an element-wise cast after a select made hipcc emit one cvt per element plus
+// a v_perm per pair).
+typedef float floatx8_t __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ bf16x8_t acc_frag(const floatx16_t& acc, int s) {
-  bf16x8_t r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (__bf16)acc[8 * s + j];
-  return r;
+  const floatx8_t f = s ? acc.s89abcdef : acc.s01234567;
+  return __builtin_convertvector(f, bf16x8_t);
 }
+
+// Dropout select on the fp32 bit pattern: all-ones / all-zeros from keep bit `bit` of
+// `word` (v_bfe_i32), then one AND -- 2 VALU per element instead of and + cmp +
+// cndmask.  A dropped element becomes +0.0f.
+__device__ __forceinline__ uint32_t keep_ones(uint32_t word, int bit) {
+  return (uint32_t)__builtin_amdgcn_sbfe((int)word, bit, 1);
+}
+__device__ __forceinline__ float keep_and(float x, uint32_t ones) { return __uint_as_float(__float_as_uint(x) & ones); }
 
 __device__ __forceinline__ floatx16_t mfma(const bf16x8_t& a, const bf16x8_t& b, const floatx16_t& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
@@ -163,9 +173,25 @@ typedef __attribute__((address_space(3))) void* lds_vptr_t;
 typedef const __attribute__((address_space(1))) void* gbl_cvptr_t;
 __device__ __forceinline__ void glds_tile(const bf16_t* __restrict__ base, int row0, int S, int rstride, bf16_t* T,
                                           int wid, int lane) {
+  // 32-bit offsets (a head's rows span < 4 GB) on the wave-uniform base: the DMA takes
+  // the saddr form and no 64-bit address arithmetic runs per tile (fwd / dQ).
+  const char* b = reinterpret_cast<const char*>(base);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int rr = (wid * 4 + j) * 8;  // first row of this 1 KiB piece (wave-uniform)
+    const int row = rr + (lane >> 3);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    const uint32_t off = (uint32_t)(min(row0 + row, S - 1) * rstride + c * 8) * 2u;
+    __builtin_amdgcn_global_load_lds((gbl_cvptr_t)(b + off), (lds_vptr_t)(T + rr * HD), 16, 0, 0);
+  }
+}
+// The same copy with 64-bit row addressing: fewer live registers in dK/dV, which stages
+// two operands with different row strides and sits at the VGPR limit.
+__device__ __forceinline__ void glds_tile64(const bf16_t* __restrict__ base, int row0, int S, int rstride, bf16_t* T,
+                                            int wid, int lane) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int rr = (wid * 4 + j) * 8;
     const int row = rr + (lane >> 3);
     const int c = (lane & 7) ^ ((row >> 1) & 7);
     const bf16_t* g = base + (size_t)min(row0 + row, S - 1) * rstride + c * 8;
@@ -336,7 +362,7 @@ __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const b
     for (int i = 0; i < 16; ++i) {
       const float p = fast_exp2(fmaf(sacc[i], c_log2, nmc));
       fs.l += p;
-      if (DROP) sacc[i] = (words[t] & (1u << ((i & 3) + 8 * (i >> 2)))) ? p : 0.f;  // 1/(1-p) at the end
+      if (DROP) sacc[i] = keep_and(p, keep_ones(words[t], (i & 3) + 8 * (i >> 2)));  // 1/(1-p) at the end
       else sacc[i] = p;
     }
     tr_wait(vf[0][0], vf[0][1], vf[1][0], vf[1][1]);
@@ -521,13 +547,17 @@ __device__ __forceinline__ void dkdv_subtile(floatx16_t (&dka)[2], floatx16_t (&
       }
       float dp = pacc[i];
       float pd = p;
+      float dps = dp;
       if (DROP) {
-        const bool keep = mw & (1u << (8 * g + e));  // maskT word >> 4h: query qs + r
-        pd = keep ? p : 0.f;  // 1/(1-p) folded into the dV epilogue
-        dp = keep ? dp * dscale : 0.f;
+        const uint32_t ones = keep_ones(mw, 8 * g + e);  // maskT word >> 4h: query qs + r
+        pd = keep_and(p, ones);  // 1/(1-p) folded into the dV epilogue
+        dp = keep_and(dp, ones);
+        dps = fmaf(dp, dscale, -dv[e]);
+      } else {
+        dps = dp - dv[e];
       }
-      sacc[i] = pd;               // dropped P  -> dV
-      pacc[i] = p * (dp - dv[e]); // dS         -> dK
+      sacc[i] = pd;        // dropped P  -> dV
+      pacc[i] = p * dps;   // dS         -> dK
     }
   }
 #pragma unroll
@@ -598,8 +628,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     float rl = 0.f, rd = 0.f;
     uint2 mw_cur = make_uint2(0u, 0u), mw_next = make_uint2(0u, 0u);
     auto load_rows = [&](int t, int buf) {  // Q / dO tiles by LDS-DMA, row stats via registers
-      glds_tile(q + hin, t * QSTEP, S, in_rs, lds + buf * 2 * QSTEP * HD, wid, lane);
-      glds_tile(dob, t * QSTEP, S, rstride, lds + buf * 2 * QSTEP * HD + QSTEP * HD, wid, lane);
+      glds_tile64(q + hin, t * QSTEP, S, in_rs, lds + buf * 2 * QSTEP * HD, wid, lane);
+      glds_tile64(dob, t * QSTEP, S, rstride, lds + buf * 2 * QSTEP * HD + QSTEP * HD, wid, lane);
       if (DROP) {  // this lane's two 32-query keep words of tile t (consumed one tile later)
         const int w0 = (t * QSTEP) >> 5;
         mw_next = make_uint2(mcol[(size_t)w0 * S], (w0 + 1 < W) ? mcol[(size_t)(w0 + 1) * S] : 0u);
@@ -694,8 +724,12 @@ __device__ __forceinline__ void dq_tile(floatx16_t (&dqa)[2], const bf16_t* Kt, 
         p = (kA > qa || kA >= S) ? 0.f : p;
       }
       float dp = pacc[t][i];
-      if (DROP) dp = (word & (1u << ((i & 3) + 8 * (i >> 2)))) ? dp * dscale : 0.f;
-      pacc[t][i] = p * (dp - dl);
+      if (DROP) {
+        dp = keep_and(dp, keep_ones(word, (i & 3) + 8 * (i >> 2)));
+        pacc[t][i] = p * fmaf(dp, dscale, -dl);
+      } else {
+        pacc[t][i] = p * (dp - dl);
+      }
     }
   }
 #pragma unroll
