@@ -10,7 +10,10 @@ over ranks is used; rank 0 prints ONE JSON line.
 
 A "step" is one full optimizer step exactly as the trainer runs it: 4 micro-steps of
 forward+backward (dropout 0.1 on, like the reference config), gradient all-reduce,
-clip-by-global-norm and AdamW -- nothing skipped.  Data: synthetic random token ids
+clip-by-global-norm and AdamW -- nothing skipped.  The engine executes the 4
+micro-steps of 8 sequences as 2 pipelined chains of 16 (``micro_step_fusion``; the
+loss is still normalised per micro-step, so the gradient is the same GA average) --
+reported in the JSON ``config``.  Data: synthetic random token ids
 (no datasets offline); weights: random init of the real architecture.
 """
 from __future__ import annotations
@@ -44,6 +47,8 @@ def main():
     ap.add_argument("--model_override", default="",
                     help="rehearsal only: comma-separated GPTConfig overrides (e.g. hidden_size=64,num_layers=2); "
                          "the JSON line then names a custom model and vs_baseline is null")
+    ap.add_argument("--fusion", type=int, default=0,
+                    help="micro_step_fusion (DDP engine): 0 = auto, 1 = run every micro-step on its own")
     ap.add_argument("--dropout", type=float, default=None,
                     help="ablation only: override dropout/attention_dropout (reference config: 0.1)")
     args = ap.parse_args()
@@ -70,7 +75,7 @@ def main():
         from distributed_llm_trainer_amd.training.configs import TrainingConfig
         from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
         tc = TrainingConfig(batch_size=args.batch_size, gradient_accumulation_steps=args.grad_accum,
-                            max_steps=100000, mixed_precision="bf16")
+                            max_steps=100000, mixed_precision="bf16", micro_step_fusion=args.fusion)
         trainer = DistributedTrainer(cfg, tc)
     else:
         from distributed_llm_trainer_amd.training.configs import FSDPConfig, FSDPTrainingConfig
@@ -127,7 +132,9 @@ def main():
                                 else f"{args.model_size}+{args.model_override}" if overrides else args.model_size,
                        "global_batch": B * world, "seq_len": args.seq_len,
                        "parallelism": f"{args.mode}{world}", "micro_batch": args.batch_size,
-                       "grad_accum": args.grad_accum},
+                       "grad_accum": args.grad_accum,
+                       "micro_step_fusion": trainer.fusion_factor(args.grad_accum, args.batch_size, args.seq_len)
+                       if hasattr(trainer, "fusion_factor") else 1},
             "peak_gb_per_gpu": round(peak, 3), "final_loss": round(loss, 4),
             "vs_baseline_linear": None if overrides else round(tps / (12500.0 * world), 3),
         }

@@ -188,6 +188,19 @@ class GPTEngine:
         # last layers of the deferred-wgrad backward whose weight gradients run on the
         # current stream instead of the side stream (see _backward_gen)
         self.main_wgrad_layers = int(os.environ.get("DLT_MAIN_WGRAD_LAYERS", "1"))
+        # micro-step fusion (set_loss_segments): a training forward of B rows holds this
+        # many micro-steps of B / n rows each, every one with its own loss normalisation
+        self.loss_segments = 1
+
+    def set_loss_segments(self, n: int) -> None:
+        """Declare that each training forward carries ``n`` fused micro-steps.
+
+        The rows split into ``n`` equal segments; each segment's cross-entropy is a mean
+        over ITS valid targets, and the forward's loss is the mean of the segment
+        losses -- so a chain of F fused micro-steps contributes exactly what F separate
+        micro-steps contribute to the reference's ``sum_k loss_k / GA`` (also with
+        ignore_index rows, whose count differs per micro-step)."""
+        self.loss_segments = max(1, int(n))
 
     # ------------------------------------------------------- grad accumulation
     def set_accumulation(self, slot: int, n_slots: int, defer: bool = True) -> None:
@@ -323,7 +336,7 @@ class GPTEngine:
             micro = 0
         st = _StepState(ids=ids, B=B, S=S, micro=micro, train=train, recompute=recompute)
         slot, n_slots, defer = acc if acc is not None else (self.acc_slot, self.acc_slots, self.defer)
-        if need_bwd and defer and n_slots > 1:
+        if need_bwd and defer:
             st.slot, st.defer, st.last = slot, True, slot == n_slots - 1
         prov = self.provider
         ph = self.p_hidden if train else 0.0
@@ -352,9 +365,21 @@ class GPTEngine:
             # micro-step of the window stay resident for ONE lm_head wgrad GEMM
             lg_out = self._slot_buf(st, "head", "lg", B * S, Vp, nf.device)[0] if st.defer else None
             lg = self.gemm.linear(nf, hw.lm_head, out=lg_out)
-            n_valid = (targets != -100).sum()
-            row_loss = self.ops.cross_entropy_fwd_bwd(lg, targets, V, n_valid)
-            loss = row_loss.sum() / n_valid.clamp(min=1).float()
+            nseg = self.loss_segments if (train and B % self.loss_segments == 0) else 1
+            if nseg == 1:
+                n_valid = (targets != -100).sum()
+                row_loss = self.ops.cross_entropy_fwd_bwd(lg, targets, V, n_valid)
+                loss = row_loss.sum() / n_valid.clamp(min=1).float()
+            else:  # fused micro-steps: per-segment normalisation (see set_loss_segments)
+                rows = (B // nseg) * S
+                seg_losses = []
+                for k in range(nseg):
+                    tk = targets[k * rows:(k + 1) * rows]
+                    nv = (tk != -100).sum()
+                    # gradient of (1/nseg) * mean_k: the kernel divides by its count argument
+                    rl = self.ops.cross_entropy_fwd_bwd(lg[k * rows:(k + 1) * rows], tk, V, nv * nseg)
+                    seg_losses.append(rl.sum() / nv.clamp(min=1).float())
+                loss = torch.stack(seg_losses).mean()
             if need_bwd:
                 st.dlogits = lg  # now holds d(mean loss)/d(logits), unscaled
                 st.xf, st.rstdf, st.nf = xf, rstdf, nf

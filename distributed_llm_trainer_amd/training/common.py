@@ -82,6 +82,30 @@ def memory_stats(device) -> dict:
             "max_allocated_gb": torch.cuda.max_memory_allocated(device) / 1e9}
 
 
+FUSE_TOKENS = 16384  # rows of a fused micro-step chain (GEMM M) the auto rule aims for
+
+
+def micro_step_fusion(requested: int, GA: int, micro_bs: int, seq_len: int, gpu_engine: bool) -> int:
+    """Number of micro-steps executed as one chain (a divisor of GA).
+
+    Measured on one MI355X (small, micro-batch 8 x GA 4, seq 1024): chains of 16
+    sequences (F = 2, GEMM M = 16384) run 43.2 ms per optimizer step vs 46.1 ms for
+    four 8-sequence chains -- the projection GEMMs reach ~1 PF/s at M >= 16384 (vs
+    0.4-0.9 at 8192) and two chains still pipeline (profiles/r2_microbatch_ab.md).
+    ``requested`` > 0 forces F (must divide GA); 0 = auto (GPU engine only)."""
+    if requested > 0:
+        if GA % requested:
+            raise ValueError(f"micro_step_fusion={requested} must divide gradient_accumulation_steps={GA}")
+        return requested
+    if not gpu_engine or GA < 2:
+        return 1
+    best = 1
+    for f in range(1, GA + 1):
+        if GA % f == 0 and f * micro_bs * seq_len <= FUSE_TOKENS and GA // f >= 2:
+            best = f
+    return best
+
+
 def gemm_plan_hook() -> None:
     """After a step: write the GEMM plan file once if ``DLT_GEMM_PLAN`` asks for one
     (``ops/gemm.py`` ``maybe_save_plan``; a no-op without the planner)."""

@@ -47,6 +47,11 @@ class TrainingConfig:
     adam_eps: float = 1e-8
     defer_wgrad: bool = True           # one weight-grad GEMM per layer per optimizer step
     pipeline_micro_steps: bool = True  # overlap fwd(k+1) with bwd(k) on two HIP streams (engine path)
+    # execute F consecutive micro-steps as one forward/backward chain of F*batch_size rows
+    # (loss normalised per micro-step, so the gradient is the reference's GA average);
+    # 0 = auto (GPU engine: largest F with F*batch_size*seq <= 16384 tokens and >= 2
+    # chains left to pipeline), 1 = off
+    micro_step_fusion: int = 0
 
 
 @dataclass

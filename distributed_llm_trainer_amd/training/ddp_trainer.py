@@ -40,7 +40,7 @@ from ..parallel.flat import FlatParamStore
 from ..utils import checkpoint as ckpt
 from ..utils import debug as dbg
 from ..utils.profiling import Profiler, range_push, range_pop
-from .common import cosine_lr, gemm_plan_hook, memory_stats, seed_all, select_device, setup_distributed, unwrap_batch
+from .common import cosine_lr, gemm_plan_hook, memory_stats, micro_step_fusion, seed_all, select_device, setup_distributed, unwrap_batch
 from .configs import TrainingConfig
 from .optim import flat_store_optimizer
 
@@ -116,6 +116,16 @@ class DistributedTrainer:
         self.optimizer = flat_store_optimizer(self.store, c.learning_rate, (c.beta1, c.beta2), c.adam_eps,
                                               c.weight_decay, split_no_decay=True)
 
+    def fusion_factor(self, GA: int, micro_bs: int, seq_len: int) -> int:
+        gpu_engine = self.use_engine and self.device.type == "cuda" and self.loss_scale is None
+        return micro_step_fusion(self.training_config.micro_step_fusion, GA, micro_bs, seq_len, gpu_engine)
+
+    def chains_per_step(self) -> int:
+        """Engine forwards per optimizer step (dropout streams are keyed by this count)."""
+        c = self.training_config
+        GA = c.gradient_accumulation_steps
+        return GA // self.fusion_factor(GA, c.batch_size, self.model_config.max_seq_len)
+
     # --------------------------------------------------------------- schedule
     def get_lr(self, step: int) -> float:
         c = self.training_config
@@ -135,43 +145,51 @@ class DistributedTrainer:
         input_ids = unwrap_batch(batch).to(self.device, non_blocking=True)
         GA = cfg.gradient_accumulation_steps
         micro_bs = input_ids.shape[0] // GA
+        # F micro-steps per executed chain (see TrainingConfig.micro_step_fusion); the
+        # gradient is still the average of GA per-micro-step mean losses
+        F = self.fusion_factor(GA, micro_bs, input_ids.shape[1])
+        chains, chain_bs = GA // F, micro_bs * F
+        if self.use_engine:
+            self.model.engine.set_loss_segments(F)
         total = torch.zeros((), dtype=torch.float32, device=self.device)
         # micro-step pipelining (engine.train_window): from the second step on, so the
         # first one runs the GEMM autotuning on a quiet GPU
-        pipelined = (self.use_engine and GA > 1 and cfg.defer_wgrad and cfg.pipeline_micro_steps
+        pipelined = (self.use_engine and chains > 1 and cfg.defer_wgrad and cfg.pipeline_micro_steps
                      and self.loss_scale is None and self._engine_warm
                      and (self.device.type != "cuda" or getattr(self.model.engine.gemm, "stream_safe", False))
                      and os.environ.get("DLT_PIPELINE", "1") != "0")
         if pipelined:
-            ids_l = [input_ids[m * micro_bs:(m + 1) * micro_bs] for m in range(GA)]
+            ids_l = [input_ids[m * chain_bs:(m + 1) * chain_bs] for m in range(chains)]
             from ..models.engine import shift_targets
             tg_l = [shift_targets(x) for x in ids_l]
             if self.ddp is not None:
                 self.ddp.require_sync(False)
-            dloss = torch.full((), 1.0 / GA, dtype=torch.float32, device=self.device)
+            dloss = torch.full((), 1.0 / chains, dtype=torch.float32, device=self.device)
             range_push("window")
             losses = self.model.engine.train_window(
                 ids_l, tg_l, dloss, recompute=bool(self.model.gradient_checkpointing),
                 before_last=(lambda: self.ddp.require_sync(True)) if self.ddp is not None else None)
             range_pop()
             for loss in losses:
-                total += (loss / GA).detach().float()
-        for micro in range(0 if not pipelined else GA, GA):
-            ids = input_ids[micro * micro_bs:(micro + 1) * micro_bs]
+                total += (loss / chains).detach().float()
+        for micro in range(0 if not pipelined else chains, chains):
+            ids = input_ids[micro * chain_bs:(micro + 1) * chain_bs]
             if self.ddp is not None:
-                self.ddp.require_sync(micro == GA - 1)
+                self.ddp.require_sync(micro == chains - 1)
             if self.use_engine:
-                self.model.engine.set_accumulation(micro, GA, defer=cfg.defer_wgrad)
+                self.model.engine.set_accumulation(micro, chains, defer=cfg.defer_wgrad)
             range_push(f"micro{micro}")
             with self.autocast_ctx:
                 _, loss = self.model(ids, labels=ids)
-                loss = loss / GA
+                loss = loss / chains
             if self.loss_scale is not None:
                 (loss * self.loss_scale).backward()
             else:
                 loss.backward()
             range_pop()
             total += loss.detach().float()
+        if self.use_engine:
+            self.model.engine.set_loss_segments(1)
         self._engine_warm = self.use_engine
         if not self.use_engine:
             self.store.sync_grads_from_params()
@@ -230,7 +248,7 @@ class DistributedTrainer:
         self.global_step = int(c["global_step"])
         self.tokens_seen = int(c["tokens_seen"])
         if self.use_engine:  # dropout streams continue exactly where the saved run was
-            self.model.engine.micro_counter = self.global_step * self.training_config.gradient_accumulation_steps
+            self.model.engine.micro_counter = self.global_step * self.chains_per_step()
         if self.is_main_process:
             print(f"Loaded Checkpoint from {path} (step {self.global_step})")
 

@@ -133,3 +133,53 @@ def test_fsdp_trainer_pipelined_matches_sequential(strategy, sync_every):
     assert res[0][0] == res[1][0]
     for k in res[0][1]:
         assert torch.allclose(res[0][1][k], res[1][1][k], atol=1e-7, rtol=1e-6), k
+
+
+@pytest.mark.parametrize("F,pipe", [(2, True), (2, False), (4, True)])
+def test_micro_step_fusion_matches_unfused(F, pipe):
+    """micro_step_fusion=F executes F micro-steps as one chain of F*batch rows: the
+    trainer step equals the unfused GA average (dropout off: fused chains draw other
+    dropout streams by design).  Ragged ignore_index counts: the next test."""
+    from distributed_llm_trainer_amd.training.configs import TrainingConfig
+    from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
+    torch.manual_seed(14)
+    data = torch.randint(0, 256, (8, 32))
+    res = []
+    for fuse in (1, F):
+        tc = TrainingConfig(batch_size=2, gradient_accumulation_steps=4, warmup_steps=2, max_steps=10,
+                            pipeline_micro_steps=pipe, micro_step_fusion=fuse)
+        tr = DistributedTrainer(tiny(dropout=0.0, attention_dropout=0.0), tc)
+        assert tr.fusion_factor(4, 2, 32) == fuse
+        losses = [tr.train_step({"input_ids": data})["loss"] for _ in range(3)]
+        res.append((losses, tr.store.flat.clone()))
+    for a, b in zip(res[0][0], res[1][0]):
+        assert abs(a - b) < 1e-5 * max(1.0, abs(a)), (a, b)
+    assert torch.allclose(res[0][1], res[1][1], atol=1e-6, rtol=1e-5)
+
+
+def test_fused_loss_segments_normalise_per_micro_step():
+    """Engine-level check with ignore_index: a fused forward over two micro-steps whose
+    valid-target counts differ gives mean(loss_0, loss_1) and the gradient of
+    (loss_0 + loss_1) / 2 -- not the pooled token mean."""
+    torch.manual_seed(15)
+    m1 = GPT(tiny(dropout=0.0, attention_dropout=0.0))
+    m2 = copy.deepcopy(m1)
+    e1 = m1.enable_engine(seed=3)
+    e2 = m2.enable_engine(seed=3)
+    ids = torch.randint(0, 256, (4, 32))
+    tg = shift_targets(ids)
+    tg[:40] = -100  # micro-step 0 (rows 0-63) keeps 23 targets, micro-step 1 keeps 31
+    # unfused reference: two micro-steps of 2 sequences
+    e1.set_accumulation(0, 2, defer=False)
+    losses = []
+    for j in range(2):
+        loss, _, st = e1.forward(ids[2 * j:2 * j + 2], tg[64 * j:64 * (j + 1)], train=True, need_backward=True)
+        e1.backward(st, torch.full((), 0.5))
+        losses.append(loss)
+    e2.set_loss_segments(2)
+    e2.set_accumulation(0, 1, defer=False)
+    loss2, _, st2 = e2.forward(ids, tg, train=True, need_backward=True)
+    e2.backward(st2, torch.ones(()))
+    assert torch.allclose(loss2, (losses[0] + losses[1]) / 2, atol=1e-6)
+    for (n, p1), (_, p2) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert torch.allclose(p1.grad, p2.grad, atol=1e-6, rtol=1e-5), n
