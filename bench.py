@@ -48,7 +48,7 @@ def main():
                     help="rehearsal only: comma-separated GPTConfig overrides (e.g. hidden_size=64,num_layers=2); "
                          "the JSON line then names a custom model and vs_baseline is null")
     ap.add_argument("--fusion", type=int, default=0,
-                    help="micro_step_fusion (DDP engine): 0 = auto, 1 = run every micro-step on its own")
+                    help="micro_step_fusion: 0 = auto, 1 = run every micro-step on its own")
     ap.add_argument("--dropout", type=float, default=None,
                     help="ablation only: override dropout/attention_dropout (reference config: 0.1)")
     args = ap.parse_args()
@@ -81,7 +81,7 @@ def main():
         from distributed_llm_trainer_amd.training.configs import FSDPConfig, FSDPTrainingConfig
         from distributed_llm_trainer_amd.training.fsdp_trainer import FSDPTrainer
         tc = FSDPTrainingConfig(batch_size=args.batch_size, gradient_accumulation_steps=args.grad_accum,
-                                max_steps=100000)
+                                max_steps=100000, micro_step_fusion=args.fusion)
         fc = FSDPConfig(sharding_strategy=args.sharding, activation_checkpointing=not args.no_ac)
         trainer = FSDPTrainer(cfg, tc, fc)
     dev = trainer.device
@@ -133,8 +133,7 @@ def main():
                        "global_batch": B * world, "seq_len": args.seq_len,
                        "parallelism": f"{args.mode}{world}", "micro_batch": args.batch_size,
                        "grad_accum": args.grad_accum,
-                       "micro_step_fusion": trainer.fusion_factor(args.grad_accum, args.batch_size, args.seq_len)
-                       if hasattr(trainer, "fusion_factor") else 1},
+                       "micro_step_fusion": trainer.fusion_factor(args.grad_accum, args.batch_size, args.seq_len)},
             "peak_gb_per_gpu": round(peak, 3), "final_loss": round(loss, 4),
             "vs_baseline_linear": None if overrides else round(tps / (12500.0 * world), 3),
         }

@@ -76,6 +76,9 @@ class FSDPTrainingConfig:
     adam_eps: float = 1e-8
     eval_interval: int = 500
     pipeline_micro_steps: bool = True  # overlap fwd(k+1) with bwd(k) on two HIP streams
+    # F micro-steps per executed chain, as in TrainingConfig (0 = auto, 1 = off); the
+    # per-micro-step reduce-scatter (Q15 parity) then runs once per chain -- the same sum
+    micro_step_fusion: int = 0
 
 
 @dataclass

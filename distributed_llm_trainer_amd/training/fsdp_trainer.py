@@ -33,7 +33,7 @@ from ..parallel.fsdp import FSDPRuntime
 from ..utils import checkpoint as ckpt
 from ..utils import debug as dbg
 from ..utils.profiling import Profiler
-from .common import cosine_lr, gemm_plan_hook, memory_stats, seed_all, select_device, setup_distributed, unwrap_batch
+from .common import cosine_lr, gemm_plan_hook, memory_stats, micro_step_fusion, seed_all, select_device, setup_distributed, unwrap_batch
 from .configs import FSDPConfig, FSDPTrainingConfig
 from .optim import FlatAdamW
 
@@ -100,6 +100,16 @@ class FSDPTrainer:
         if self.fsdp_config.cpu_offload:
             self.optimizer.is_cuda = False  # host AdamW on the offloaded shards
 
+    def fusion_factor(self, GA: int, micro_bs: int, seq_len: int) -> int:
+        gpu = self.device.type == "cuda"
+        return micro_step_fusion(getattr(self.training_config, "micro_step_fusion", 0), GA, micro_bs, seq_len, gpu)
+
+    def chains_per_step(self) -> int:
+        """Engine forwards per optimizer step (dropout streams are keyed by this count)."""
+        tc = self.training_config
+        GA = tc.gradient_accumulation_steps
+        return GA // self.fusion_factor(GA, tc.batch_size, self.model_config.max_seq_len)
+
     def get_lr(self, step: int) -> float:
         tc = self.training_config
         return cosine_lr(step, tc.learning_rate, tc.warmup_steps, tc.max_steps, clamp=True)
@@ -115,34 +125,40 @@ class FSDPTrainer:
         input_ids = unwrap_batch(batch).to(self.device, non_blocking=True)
         GA = tc.gradient_accumulation_steps
         micro_bs = input_ids.shape[0] // GA
+        # F micro-steps per executed chain (micro_step_fusion); losses stay normalised
+        # per micro-step, so the gradient is the reference's GA average
+        F = self.fusion_factor(GA, micro_bs, input_ids.shape[1])
+        chains, chain_bs = GA // F, micro_bs * F
         total = torch.zeros((), dtype=torch.float32, device=self.device)
         rt.zero_grad()
         defer = not self.fsdp_config.sync_every_micro_step
         eng = self.model.engine
+        eng.set_loss_segments(F)
         # micro-step pipelining (GPTEngine.train_window) from the second step on (the
         # first runs the GEMM autotuning); units are shared by the two chains through
         # the runtime's reference-counted residency
-        pipelined = (GA > 1 and getattr(tc, "pipeline_micro_steps", True) and getattr(self, "_engine_warm", False)
+        pipelined = (chains > 1 and getattr(tc, "pipeline_micro_steps", True) and getattr(self, "_engine_warm", False)
                      and (self.device.type != "cuda" or getattr(eng.gemm, "stream_safe", False))
                      and os.environ.get("DLT_PIPELINE", "1") != "0")
         if pipelined:
             from ..models.engine import shift_targets
-            ids_l = [input_ids[m * micro_bs:(m + 1) * micro_bs] for m in range(GA)]
+            ids_l = [input_ids[m * chain_bs:(m + 1) * chain_bs] for m in range(chains)]
             rt.require_sync(False)
             losses = eng.train_window(ids_l, [shift_targets(x) for x in ids_l],
-                                      torch.full((), 1.0 / GA, dtype=torch.float32, device=self.device),
+                                      torch.full((), 1.0 / chains, dtype=torch.float32, device=self.device),
                                       recompute=bool(self.model.gradient_checkpointing),
                                       before_last=lambda: rt.require_sync(True), defer=defer)
             for loss in losses:
-                total += (loss / GA).detach().float()
-        for micro in range(GA if pipelined else 0, GA):
-            ids = input_ids[micro * micro_bs:(micro + 1) * micro_bs]
-            rt.require_sync(micro == GA - 1)
-            eng.set_accumulation(micro, GA, defer=defer)
+                total += (loss / chains).detach().float()
+        for micro in range(chains if pipelined else 0, chains):
+            ids = input_ids[micro * chain_bs:(micro + 1) * chain_bs]
+            rt.require_sync(micro == chains - 1)
+            eng.set_accumulation(micro, chains, defer=defer)
             _, loss = self.model(ids, labels=ids)
-            loss = loss / GA
+            loss = loss / chains
             loss.backward()
             total += loss.detach().float()
+        eng.set_loss_segments(1)
         self._engine_warm = True
         rt.finish()
         # global grad norm: local shard sumsq -> scalar all-reduce (reference X8)
@@ -284,7 +300,7 @@ class FSDPTrainer:
         rt.refresh_shadow()
         self.global_step, self.tokens_seen = int(meta["global_step"]), int(meta["tokens_seen"])
         opt.step_count = int(meta["optimizer_step"])
-        self.model.engine.micro_counter = self.global_step * self.training_config.gradient_accumulation_steps
+        self.model.engine.micro_counter = self.global_step * self.chains_per_step()
         if self.is_main_process:
             print(f"Loaded sharded checkpoint from {path} (step {self.global_step})")
 
@@ -322,7 +338,7 @@ class FSDPTrainer:
             opt.exp_avg[a:b].copy_(fm[la:lb].to(opt.exp_avg.device))
             opt.exp_avg_sq[a:b].copy_(fv[la:lb].to(opt.exp_avg_sq.device))
         self.global_step, self.tokens_seen, opt.step_count = meta[0]
-        self.model.engine.micro_counter = self.global_step * self.training_config.gradient_accumulation_steps
+        self.model.engine.micro_counter = self.global_step * self.chains_per_step()
         if self.is_main_process:
             print(f"Loaded Checkpoint from {path} (step {self.global_step})")
 

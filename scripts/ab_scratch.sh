@@ -1,8 +1,4 @@
 set -u
 mkdir -p gpurun_out
-cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/tests.log 2>&1; rc=$?; tail -2 gpurun_out/tests.log; [ $rc -eq 0 ] || exit $rc
-run() { tag=$1; shift; timeout -k 10 240 "$@" > gpurun_out/ab_$tag.log 2>&1 || { echo "fail $tag"; tail -5 gpurun_out/ab_$tag.log; exit 1; }; echo "$tag: $(tail -1 gpurun_out/ab_$tag.log | cut -c1-130)"; }
-run auto python -u bench.py --steps 20 --warmup 3
-run nofuse python -u bench.py --steps 20 --warmup 3 --fusion 1
-run auto2 python -u bench.py --steps 20 --warmup 3
+timeout -k 10 300 python -u tools/gemm_roles.py 16384 2 > gpurun_out/gemm_roles_16k.log 2>&1; echo rc=$?; head -12 gpurun_out/gemm_roles_16k.log
+M=16384 timeout -k 10 300 python -u tools/gemm_tn8_bench.py > gpurun_out/tn8_16k.log 2>&1; echo rc=$?; cat gpurun_out/tn8_16k.log

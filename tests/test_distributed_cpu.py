@@ -19,31 +19,31 @@ def _data(step, rank, n=8, seq=32, vocab=384):
     return torch.randint(0, vocab, (n, seq), generator=g)
 
 
-def _ddp_worker(rank, world, steps, bucket_mb):
+def _ddp_worker(rank, world, steps, bucket_mb, fusion=1, GA=2):
     from distributed_llm_trainer_amd.models.config import GPTConfig
     from distributed_llm_trainer_amd.training.configs import TrainingConfig
     from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
     cfg = GPTConfig(**TINY)
-    tc = TrainingConfig(batch_size=2, gradient_accumulation_steps=2, warmup_steps=1, max_steps=100,
-                        learning_rate=1e-2, bucket_cap_mb=bucket_mb)
+    tc = TrainingConfig(batch_size=2, gradient_accumulation_steps=GA, warmup_steps=1, max_steps=100,
+                        learning_rate=1e-2, bucket_cap_mb=bucket_mb, micro_step_fusion=fusion)
     tr = DistributedTrainer(cfg, tc)
     losses = []
     for s in range(steps):
-        losses.append(tr.train_step({"input_ids": _data(s, rank, n=4)})["loss"])
+        losses.append(tr.train_step({"input_ids": _data(s, rank, n=2 * GA)})["loss"])
     return tr.store.flat.clone(), losses, len(tr.ddp.buckets)
 
 
-def _single_worker_equiv(steps, world):
-    """One process, GA = world*2, consuming every rank's micro-batches in order."""
+def _single_worker_equiv(steps, world, GA=2):
+    """One process, GA = world*GA, consuming every rank's micro-batches in order."""
     from distributed_llm_trainer_amd.models.config import GPTConfig
     from distributed_llm_trainer_amd.training.configs import TrainingConfig
     from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
     cfg = GPTConfig(**TINY)
-    tc = TrainingConfig(batch_size=2, gradient_accumulation_steps=2 * world, warmup_steps=1, max_steps=100,
-                        learning_rate=1e-2)
+    tc = TrainingConfig(batch_size=2, gradient_accumulation_steps=GA * world, warmup_steps=1, max_steps=100,
+                        learning_rate=1e-2, micro_step_fusion=1)
     tr = DistributedTrainer(cfg, tc)
     for s in range(steps):
-        batch = torch.cat([_data(s, r, n=4) for r in range(world)], dim=0)
+        batch = torch.cat([_data(s, r, n=2 * GA) for r in range(world)], dim=0)
         tr.train_step({"input_ids": batch})
     return tr.store.flat.clone()
 
@@ -59,13 +59,24 @@ def test_ddp_matches_single_process(bucket_mb):
         assert nb0 > 2  # several buckets exercised
 
 
-def _fsdp_worker(rank, world, strategy, steps, ac, offload):
+@pytest.mark.parametrize("fusion,GA", [(2, 4), (2, 2)])
+def test_ddp_micro_step_fusion_matches_single_process(fusion, GA):
+    """DDP with fused micro-step chains (2 pipelined chains of 2 micro-steps, or one
+    chain): replicas stay bit-identical and equal the unfused single-process GA run."""
+    outs = run_multiprocess(_ddp_worker, world=2, args=(3, 0.05, fusion, GA))
+    (p0, _, _), (p1, _, _) = outs
+    assert torch.equal(p0, p1), "ranks diverged"
+    ref = _single_worker_equiv(3, 2, GA=GA)
+    assert torch.allclose(p0, ref, atol=2e-5, rtol=1e-4), (p0 - ref).abs().max()
+
+
+def _fsdp_worker(rank, world, strategy, steps, ac, offload, fusion=1):
     from distributed_llm_trainer_amd.models.config import GPTConfig
     from distributed_llm_trainer_amd.training.configs import FSDPConfig, FSDPTrainingConfig
     from distributed_llm_trainer_amd.training.fsdp_trainer import FSDPTrainer
     cfg = GPTConfig(**TINY)
     tc = FSDPTrainingConfig(batch_size=2, gradient_accumulation_steps=2, warmup_steps=1, max_steps=100,
-                            learning_rate=1e-2)
+                            learning_rate=1e-2, micro_step_fusion=fusion)
     fc = FSDPConfig(sharding_strategy=strategy, activation_checkpointing=ac, cpu_offload=offload,
                     reduce_dtype="fp32")
     tr = FSDPTrainer(cfg, tc, fc)
@@ -81,7 +92,7 @@ def _fsdp_single(steps, world, ac=False):
     from distributed_llm_trainer_amd.training.fsdp_trainer import FSDPTrainer
     cfg = GPTConfig(**TINY)
     tc = FSDPTrainingConfig(batch_size=2, gradient_accumulation_steps=2 * world, warmup_steps=1, max_steps=100,
-                            learning_rate=1e-2)
+                            learning_rate=1e-2, micro_step_fusion=1)
     fc = FSDPConfig(sharding_strategy="FULL_SHARD", activation_checkpointing=ac, reduce_dtype="fp32")
     tr = FSDPTrainer(cfg, tc, fc)
     for s in range(steps):
@@ -95,6 +106,16 @@ def _fsdp_single(steps, world, ac=False):
                                                  ("HYBRID_SHARD", True, False)])
 def test_fsdp_matches_single_process(strategy, ac, offload):
     outs = run_multiprocess(_fsdp_worker, world=2, args=(strategy, 3, ac, offload))
+    ref = _fsdp_single(3, 2)
+    for k in ref:
+        assert torch.equal(outs[0][k], outs[1][k]), f"{k}: ranks diverged"
+        assert torch.allclose(outs[0][k], ref[k], atol=3e-5, rtol=1e-4), (k, (outs[0][k] - ref[k]).abs().max())
+
+
+def test_fsdp_micro_step_fusion_matches_single_process():
+    """FULL_SHARD with both micro-steps fused into one chain (one reduce-scatter per
+    chain instead of per micro-step): same parameters as the unfused single process."""
+    outs = run_multiprocess(_fsdp_worker, world=2, args=("FULL_SHARD", 3, True, False, 2))
     ref = _fsdp_single(3, 2)
     for k in ref:
         assert torch.equal(outs[0][k], outs[1][k]), f"{k}: ranks diverged"

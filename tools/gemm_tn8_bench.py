@@ -26,8 +26,10 @@ def bench(fn, it=20):
     return best
 
 
-shapes = [("qkv fwd", 8192, 2304, 768), ("gu fwd", 8192, 6144, 768), ("down fwd", 8192, 768, 3072),
-          ("o fwd", 8192, 768, 768), ("lm_head fwd*", 8192, 50176, 768), ("down dgrad", 8192, 3072, 768),
+M = int(os.environ.get("M", "8192"))  # rows of the projection GEMMs (micro-step chain tokens)
+shapes = [("qkv fwd", M, 2304, 768), ("gu fwd", M, 6144, 768), ("down fwd", M, 768, 3072),
+          ("o fwd", M, 768, 768), ("lm_head fwd*", M, 50176, 768), ("down dgrad", M, 3072, 768),
+          ("qkv dgrad*", M, 768, 2304), ("gu dgrad*", M, 768, 6144),
           ("square 4096", 4096, 4096, 4096), ("square 8192", 8192, 8192, 8192)]
 only = sys.argv[1:] if len(sys.argv) > 1 else None
 for name, m, n, k in shapes:
