@@ -279,15 +279,27 @@ __global__ __launch_bounds__(256) void k_dropout_bits(uint32_t* __restrict__ mas
 // fetched once per pair from the fabric.  The XCD-aware map gives each XCD a contiguous
 // range of items instead -- all pairs of a head on one XCD, reading the head's tiles
 // through the same L2 (bijective for any grid size, like the GEMM's tile map).
-__device__ __forceinline__ void work_item(int npairs, int xcd_map, int& bh, int& pair) {
+__device__ __forceinline__ bool work_item(int nrb, int sched, int& bh, int& pair) {
   const int bid = blockIdx.x;
+  if (sched & 2) {
+    // LPT: one 64-row item per workgroup, longest first (block ids ascend in dispatch
+    // order), so short items fill the slots the long ones leave -- many more, shorter
+    // waves than the pairing.  bid % 8 == bh % 8 when B*nh % 8 == 0: a head stays on
+    // one XCD (its K/V or Q/dO tiles through one L2).
+    const int BH = gridDim.x / nrb;
+    pair = bid / BH;  // rank: 0 = longest item
+    bh = bid - pair * BH;
+    return true;
+  }
+  const int npairs = (nrb + 1) / 2;
   int wg = bid;
-  if (xcd_map) {
+  if (sched & 1) {
     const int nwg = gridDim.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
     wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   }
   bh = wg / npairs;
   pair = wg - bh * npairs;
+  return false;
 }
 
 // ============================================================================ forward
@@ -375,11 +387,14 @@ __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const b
   }
 }
 
-// Work decomposition (causal balance): a workgroup = 2 waves = one 64-query item,
-// and each workgroup processes the PAIR of items (nrb-1-p, p) one after the other,
-// so every workgroup does the same amount of work ((nrb+1) key tiles).  With one
-// item per workgroup the per-CU load would follow the round-robin dispatch, which
-// stacks items of equal length on a CU (measured 1.8x slower than balanced).
+// Work decomposition (causal balance): a workgroup = 2 waves = one 64-query item.
+// Default schedule (work_item, LPT): one item per workgroup, longest first, so the
+// short items fill in behind the long ones.  Alternative (DLT_ATTN_SCHED=pair): each
+// workgroup processes the PAIR of items (nrb-1-p, p), equal work per workgroup but
+// only ~1.5 long waves per SIMD -- a half-empty last round at 2 waves/SIMD (PMC:
+// ~1.1 resident waves per SIMD on average at B16).  Round 1 measured one item per
+// workgroup in the NATURAL order 1.8x slower than the pairing (equal-length items
+// stacked on a CU); longest-first does not stack them.
 template <bool DROP>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_attn_fwd(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
                                                     const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
@@ -392,7 +407,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const int h = lane >> 5, ql = lane & 31;
   const int nrb = (S + RB - 1) / RB;
   int bh, pair;
-  work_item((nrb + 1) / 2, xcd_map, bh, pair);
+  const bool lpt = work_item(nrb, xcd_map, bh, pair);
   const int b = bh / nh, head = bh % nh;
   const size_t hin = (size_t)b * in_bs + (size_t)head * in_hs;  // (b, head) base of q / k / v
   const int W = (S + 31) >> 5;
@@ -403,8 +418,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 
 #pragma unroll 1
   for (int it = 0; it < 2; ++it) {
-    const int qb = it == 0 ? nrb - 1 - pair : pair;  // long item first
-    if (it == 1 && qb >= nrb - 1 - pair) break;      // odd nrb: middle item once
+    const int qb = (lpt || it == 0) ? nrb - 1 - pair : pair;  // long item first
+    if (it == 1 && (lpt || qb >= nrb - 1 - pair)) break;       // odd nrb: middle item once
     const int q0 = qb * RB + wid * 32;  // this wave's first query (wave-uniform)
     const int qa = q0 + ql;
     const uint32_t* mrow = mask ? mask + (size_t)bh * W * S + min(qa, S - 1) : nullptr;  // word j at mrow[j*S]
@@ -595,7 +610,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const int h = lane >> 5, kl = lane & 31;
   const int nrb = (S + RB - 1) / RB;
   int bh, pair;
-  work_item((nrb + 1) / 2, xcd_map, bh, pair);
+  const bool lpt = work_item(nrb, xcd_map, bh, pair);
   const int b = bh / nh, head = bh % nh;
   const size_t hin = (size_t)b * in_bs + (size_t)head * in_hs;     // q / k / v
   const size_t hout = (size_t)b * out_bs + (size_t)head * out_hs;  // dk / dv
@@ -608,8 +623,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 
 #pragma unroll 1
   for (int it = 0; it < 2; ++it) {
-    const int kblk = it == 0 ? pair : nrb - 1 - pair;  // long item (early keys) first
-    if (it == 1 && kblk <= pair) break;                 // odd nrb: middle item once
+    const int kblk = (lpt || it == 0) ? pair : nrb - 1 - pair;  // long item (early keys) first
+    if (it == 1 && (lpt || kblk <= pair)) break;                 // odd nrb: middle item once
     const int k0 = kblk * RB + wid * 32;  // wave-uniform
     const int ka = k0 + kl;
     // this lane's key column of the transposed keep-bit mask: one word per 32 queries
@@ -757,7 +772,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const int h = lane >> 5, ql = lane & 31;
   const int nrb = (S + RB - 1) / RB;
   int bh, pair;
-  work_item((nrb + 1) / 2, xcd_map, bh, pair);
+  const bool lpt = work_item(nrb, xcd_map, bh, pair);
   const int b = bh / nh, head = bh % nh;
   const size_t hin = (size_t)b * in_bs + (size_t)head * in_hs;     // q / k / v
   const size_t hout = (size_t)b * out_bs + (size_t)head * out_hs;  // dq
@@ -769,8 +784,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 
 #pragma unroll 1
   for (int it = 0; it < 2; ++it) {
-    const int qb = it == 0 ? nrb - 1 - pair : pair;  // long item first
-    if (it == 1 && qb >= nrb - 1 - pair) break;
+    const int qb = (lpt || it == 0) ? nrb - 1 - pair : pair;  // long item first
+    if (it == 1 && (lpt || qb >= nrb - 1 - pair)) break;
     const int q0 = qb * RB + wid * 32;
     const int qa = q0 + ql;
     const bool qok = qa < S;
@@ -846,9 +861,16 @@ static int xcd_map_enabled() {
   if (v < 0) {
     const char* e = getenv("DLT_ATTN_XCD");
     v = (e && atoi(e) == 0) ? 0 : 1;
+    // default: one item per workgroup, longest first (see work_item; measured B8 nh12
+    // S1024: fwd 63 -> 60 us incl. the keep bits, bwd 108 -> 96 us; B16: 117 -> 105,
+    // 218 -> 197); DLT_ATTN_SCHED=pair restores the paired items
+    const char* sch = getenv("DLT_ATTN_SCHED");
+    if (!(sch && sch[0] == 'p')) v |= 2;
   }
   return v;
 }
+// grid of the MFMA kernels for a work schedule
+static inline int attn_grid(int nrb, int BH, int sched) { return (sched & 2) ? nrb * BH : ((nrb + 1) / 2) * BH; }
 // mask: uint32 [2][B*nh, ceil(S/32), S] keep-bits written by the forward when dropout
 // is on -- [0] row layout (lane = query), [1] transposed (lane = key), see
 // k_dropout_bits.
@@ -874,8 +896,8 @@ DLT_API int dlt_attn_fwd_ex(const bf16_t* q, const bf16_t* k, const bf16_t* v, b
   if (hd != HD || S <= 0 || in_rs % 8 || in_hs % 8 || in_bs % 8) return -1;
   if (thr && !mask) return -2;  // dropout needs the keep-bit buffer
   const int nrb = (S + RB - 1) / RB;
-  const dim3 grid(((nrb + 1) / 2) * B * nh);  // (head, item pair) work items, see work_item()
   const int xm = xcd_map_enabled();
+  const dim3 grid(attn_grid(nrb, B * nh, xm));  // work items, see work_item()
   const float c_log2 = scale * LOG2E;
   if (thr) {
     if (gen_mask) {
@@ -908,8 +930,8 @@ DLT_API int dlt_attn_bwd_ex(const bf16_t* q, const bf16_t* k, const bf16_t* v, c
   if ((cosT == nullptr) != (sinT == nullptr)) return -3;
   const float c_log2 = scale * LOG2E;
   const int nrb = (S + RB - 1) / RB;
-  const dim3 gk(((nrb + 1) / 2) * B * nh), gq(((nrb + 1) / 2) * B * nh);  // (head, item pair) work items
   const int xm = xcd_map_enabled();
+  const dim3 gk(attn_grid(nrb, B * nh, xm)), gq(attn_grid(nrb, B * nh, xm));  // work items, see work_item()
   // dQ first: it also produces Delta = rowsum(dO * O) (no separate kernel), which
   // dK/dV then reads.
   if (mask) {
