@@ -329,62 +329,81 @@ struct FwdState {
 template <bool MASK, bool DROP>
 __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const bf16_t* Vt, const bf16x8_t (&qf)[4],
                                          int k0, int qa, int S, int lane, float c_log2, uint2 mw) {
-  // Two 32-key halves, each a complete online-softmax step; the V^T tr-reads of a
-  // half are issued before its softmax VALU so their latency hides under it.
+  // One 64-key tile as ONE online-softmax step: S = K.Q^T of both 32-key halves first
+  // (two independent MFMA chains), one row max / rescale decision for the tile, then
+  // per half exp -> dropout -> P.V; the second half's softmax VALU runs while the
+  // first half's P.V MFMAs execute.  The row sum uses two partial sums (the single
+  // running sum was a 16-deep dependent add chain per half).
   const int h = lane >> 5, ql = lane & 31;
   // keep-bit words of this tile (prefetched with the previous tile's staging loads,
   // so no vmcnt wait lands inside the tile); this lane-half's 16 bits per half-tile
   // sit at (i&3) + 8(i>>2)
   const uint32_t words[2] = {mw.x >> (4 * h), mw.y >> (4 * h)};
+  floatx16_t sacc[2];
+  {
+    bf16x8_t kf[2][4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      kf[0][s] = lds_row8(Kt, ql, 16 * s + 8 * h);
+      kf[1][s] = lds_row8(Kt, 32 + ql, 16 * s + 8 * h);
+    }
+    sacc[0] = zero16();
+    sacc[1] = zero16();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      sacc[0] = mfma(kf[0][s], qf[s], sacc[0]);
+      sacc[1] = mfma(kf[1][s], qf[s], sacc[1]);
+    }
+  }
+  float mx0 = -INFINITY, mx1 = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      if (MASK) {
+        const int ka = k0 + 32 * t + acc_row(i, h);
+        sacc[t][i] = (ka > qa || ka >= S) ? -INFINITY : sacc[t][i];
+      }
+      if (t == 0) mx0 = fmaxf(mx0, sacc[t][i]);
+      else mx1 = fmaxf(mx1, sacc[t][i]);
+    }
+  const float mx = xhalf_max(fmaxf(mx0, mx1));
+  if (!__all((mx - fs.m) * c_log2 <= RESCALE_LOG2)) {  // rare: a row's max grew by > 2^8
+    const float m_new = fmaxf(fs.m, mx);
+    const float alpha = fast_exp2((fs.m - m_new) * c_log2);
+    fs.m = m_new;
+    fs.l *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) fs.o[dt][i] *= alpha;
+  }
+  const float nmc = -fs.m * c_log2;
+  float l0 = 0.f, l1 = 0.f;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    bf16x8_t kf[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) kf[s] = lds_row8(Kt, 32 * t + ql, 16 * s + 8 * h);
     bf16x8_t vf[2][2];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) vf[kk][dt] = tr_frag_asm(Vt, 2 * t + kk, dt, lane);
-    floatx16_t sacc = zero16();
-#pragma unroll
-    for (int s = 0; s < 4; ++s) sacc = mfma(kf[s], qf[s], sacc);
-    float mx = -INFINITY;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      if (MASK) {
-        const int ka = k0 + 32 * t + acc_row(i, h);
-        sacc[i] = (ka > qa || ka >= S) ? -INFINITY : sacc[i];
-      }
-      mx = fmaxf(mx, sacc[i]);
-    }
-    mx = xhalf_max(mx);
-    if (!__all((mx - fs.m) * c_log2 <= RESCALE_LOG2)) {  // rare: a row's max grew by > 2^8
-      const float m_new = fmaxf(fs.m, mx);
-      const float alpha = fast_exp2((fs.m - m_new) * c_log2);
-      fs.m = m_new;
-      fs.l *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) fs.o[dt][i] *= alpha;
-    }
-    const float nmc = -fs.m * c_log2;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float p = fast_exp2(fmaf(sacc[i], c_log2, nmc));
-      fs.l += p;
-      if (DROP) sacc[i] = keep_and(p, keep_ones(words[t], (i & 3) + 8 * (i >> 2)));  // 1/(1-p) at the end
-      else sacc[i] = p;
+      const float p = fast_exp2(fmaf(sacc[t][i], c_log2, nmc));
+      if (i & 1) l1 += p;
+      else l0 += p;
+      if (DROP) sacc[t][i] = keep_and(p, keep_ones(words[t], (i & 3) + 8 * (i >> 2)));  // 1/(1-p) at the end
+      else sacc[t][i] = p;
     }
     tr_wait(vf[0][0], vf[0][1], vf[1][0], vf[1][1]);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const bf16x8_t pb = acc_frag(sacc, kk);
+      const bf16x8_t pb = acc_frag(sacc[t], kk);
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) fs.o[dt] = mfma(vf[kk][dt], pb, fs.o[dt]);
     }
   }
+  fs.l += l0 + l1;
 }
 
 // Work decomposition (causal balance): a workgroup = 2 waves = one 64-query item.
