@@ -1,7 +1,8 @@
 """Isolated timing of the memory-bound HIP ops at the headline shapes (GPT-2 small,
-B=8, S=1024 -> M=8192 rows), with the effective HBM bandwidth of each.
+B=8, S=1024 -> M=8192 rows; B=16 env for the fused chain), with the effective HBM
+bandwidth of each.
 
-usage: python tools/bench_ops.py
+usage: [B=16] python tools/bench_ops.py
 """
 import os
 import sys
@@ -12,7 +13,8 @@ import torch  # noqa: E402
 from distributed_llm_trainer_amd.ops import hip, rng  # noqa: E402
 
 dev = "cuda"
-B, S, H, nh, I, V = 8, 1024, 768, 12, 3072, 50304
+B = int(os.environ.get("B", "8"))  # sequences per chain (B=16: the fused micro-step chain)
+S, H, nh, I, V = 1024, 768, 12, 3072, 50304
 M = B * S
 
 
