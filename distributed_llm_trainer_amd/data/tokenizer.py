@@ -9,7 +9,11 @@ tokenizer.  Resolution order here:
 3. ``"byte"`` -> a dependency-free byte-level tokenizer (vocab 256, ids 0..255;
    used by tests and for smoke runs on real text without network access).
 
-A tokenizer whose vocabulary is empty is rejected loudly instead of being used.
+A tokenizer whose vocabulary is empty is rejected instead of being used (offline, this
+image's transformers returns a GPT-2 tokenizer with ``vocab_size == 0`` whose ``encode``
+yields no ids).  When no usable GPT-2 tokenizer exists, ``get_tokenizer`` falls back to
+the byte tokenizer with a loud warning (``DLT_TOKENIZER_STRICT=1``: raise instead), so
+the real-data CLIs still run offline; the ids stay < 256, inside the model's vocabulary.
 """
 from __future__ import annotations
 
@@ -38,12 +42,16 @@ def get_tokenizer(name: str = "gpt2"):
         try:
             from transformers import GPT2TokenizerFast
             tok = GPT2TokenizerFast.from_pretrained(cand, local_files_only=not cand.startswith("http"))
-            if len(tok) == 0:
-                raise RuntimeError("empty vocabulary")
+            if len(tok) == 0 or tok.vocab_size < 256 or not tok.encode("hello world"):
+                raise RuntimeError(f"unusable vocabulary (vocab_size={tok.vocab_size})")
             tok.model_max_length = 10 ** 9
             return tok
         except Exception as e:  # noqa: BLE001
             err = e
-    raise RuntimeError(
-        f"could not load tokenizer {name!r} offline ({err}). Point DLT_TOKENIZER_DIR at a directory with "
-        "the GPT-2 tokenizer files, pre-tokenise to a .bin token file, or use tokenizer 'byte'.")
+    msg = (f"could not load tokenizer {name!r} offline ({err}). Point DLT_TOKENIZER_DIR at a directory with "
+           "the GPT-2 tokenizer files, pre-tokenise to a .bin token file, or use tokenizer 'byte'.")
+    if os.environ.get("DLT_TOKENIZER_STRICT") == "1":
+        raise RuntimeError(msg)
+    import warnings
+    warnings.warn(msg + " Falling back to the byte-level tokenizer (ids 0..255).", RuntimeWarning, stacklevel=2)
+    return ByteTokenizer()

@@ -139,3 +139,23 @@ def test_load_model_state_is_strict():
     extra["module.layers.5.mlp.up_proj.weight"] = torch.zeros(1)
     with pytest.raises(RuntimeError, match="unexpected"):
         load_model_state(GPT(cfg), extra)
+
+
+def test_tokenizer_offline_is_usable():
+    """get_tokenizer('gpt2') never hands out a tokenizer that encodes to nothing (this
+    image's offline transformers yields vocab_size 0): real GPT-2 BPE if its files are
+    available, else the byte tokenizer with a warning; DLT_TOKENIZER_STRICT=1 raises."""
+    import warnings
+    from distributed_llm_trainer_amd.data.tokenizer import get_tokenizer
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        tok = get_tokenizer("gpt2")
+    ids = tok.encode("once upon a time")
+    assert len(ids) > 0 and all(0 <= i < 50257 for i in ids)
+    if isinstance(tok, ByteTokenizer):
+        os.environ["DLT_TOKENIZER_STRICT"] = "1"
+        try:
+            with pytest.raises(RuntimeError, match="could not load tokenizer"):
+                get_tokenizer("gpt2")
+        finally:
+            del os.environ["DLT_TOKENIZER_STRICT"]
