@@ -74,9 +74,26 @@ __device__ __forceinline__ bf16x8_t g8_frag(const bf16_t* img, int row, int chun
 
 }  // namespace
 
+// Epilogues: EPI_STORE writes C = A.B^T (bf16).  EPI_SWIGLU_BWD is the SwiGLU backward
+// fused onto the down-projection data gradient: the tile of ds = dd . Wdown (C, never
+// stored) meets the saved gate/up activations and only dgu is written,
+//   dg = ds * u * sig(g) * (1 + g (1 - sig(g))),   du = ds * g * sig(g)
+// (gu / dgu: [M, 2I] rows, gate in columns [0, I), up in [I, 2I); N == I) -- the math
+// of k_swiglu_bwd (elementwise.hip) on the fp32 accumulator instead of a bf16 ds.
+// It removes the ds round trip (write + read of [M, I] bf16) and one launch, but at one
+// workgroup per CU the epilogue's gu/dgu traffic (4x the plain tile store) cannot
+// overlap another tile's main loop: measured 203 us vs 168 us for hipBLASLt + the
+// SwiGLU kernel at M = 16384 (plain tn8 92 us), so the planner's race
+// (HipGemm.dgrad_swiglu) keeps the unfused pair on MI355X today.
+enum { EPI_STORE = 0, EPI_SWIGLU_BWD = 1 };
+
+__device__ __forceinline__ float g8_sigmoid(float x) { return 1.f / (1.f + __expf(-x)); }
+
+template <int EPI>
 __global__ __launch_bounds__(512, 1) void k_gemm_tn8(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                      bf16_t* __restrict__ C, int M, int N, int K, int lda, int ldb,
-                                                     int ldc) {
+                                                     int ldc, const bf16_t* __restrict__ gu, bf16_t* __restrict__ dgu,
+                                                     int I) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * G8_BUF];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -227,15 +244,43 @@ __global__ __launch_bounds__(512, 1) void k_gemm_tn8(const bf16_t* __restrict__ 
 
   // epilogue: acc[nt][mt] = D[n][m] of a 16x16 tile; lane owns row m = l16, columns
   // 4*lq .. 4*lq+3
+  if constexpr (EPI == EPI_STORE) {
 #pragma unroll
-  for (int mt = 0; mt < 8; ++mt) {
-    bf16_t* crow = C + (size_t)(m0 + wr * 128 + mt * 16 + l16) * ldc + n0 + wc * 64 + lq * 4;
+    for (int mt = 0; mt < 8; ++mt) {
+      bf16_t* crow = C + (size_t)(m0 + wr * 128 + mt * 16 + l16) * ldc + n0 + wc * 64 + lq * 4;
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      u16x4 w;
+      for (int nt = 0; nt < 4; ++nt) {
+        u16x4 w;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) w.v[e] = f2bf(acc[nt][mt][e]);
-      *reinterpret_cast<u16x4*>(crow + nt * 16) = w;
+        for (int e = 0; e < 4; ++e) w.v[e] = f2bf(acc[nt][mt][e]);
+        *reinterpret_cast<u16x4*>(crow + nt * 16) = w;
+      }
+    }
+  } else {
+    const size_t ld2 = 2 * (size_t)I;
+    const int c0 = n0 + wc * 64 + lq * 4;
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+      const size_t row = (size_t)(m0 + wr * 128 + mt * 16 + l16) * ld2;
+      u16x4 gcur[4], ucur[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {  // all loads of the row block first
+        gcur[nt] = *reinterpret_cast<const u16x4*>(gu + row + c0 + nt * 16);
+        ucur[nt] = *reinterpret_cast<const u16x4*>(gu + row + I + c0 + nt * 16);
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        u16x4 og, ou;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float g = bf2f(gcur[nt].v[e]), u = bf2f(ucur[nt].v[e]), d = acc[nt][mt][e];
+          const float sg = g8_sigmoid(g);
+          og.v[e] = f2bf(d * u * sg * (1.f + g * (1.f - sg)));
+          ou.v[e] = f2bf(d * g * sg);
+        }
+        *reinterpret_cast<u16x4*>(dgu + row + c0 + nt * 16) = og;
+        *reinterpret_cast<u16x4*>(dgu + row + I + c0 + nt * 16) = ou;
+      }
     }
   }
 }
@@ -243,6 +288,15 @@ __global__ __launch_bounds__(512, 1) void k_gemm_tn8(const bf16_t* __restrict__ 
 DLT_API int dlt_gemm_tn8(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K, int lda, int ldb, int ldc,
                          hipStream_t st) {
   if (M <= 0 || N <= 0 || M % 256 || N % 256 || K % 128 || K < 128 || (lda | ldb) % 8 || ldc % 4) return -1;
-  k_gemm_tn8<<<(M / 256) * (N / 256), 512, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc);
+  k_gemm_tn8<EPI_STORE><<<(M / 256) * (N / 256), 512, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, nullptr, nullptr, 0);
+  DLT_CHECK_LAUNCH();
+}
+
+// dgu[M, 2I] = swiglu_bwd(gu, dd . Wdown) with B = Wdown^T [I, K] (K-contiguous rows):
+// the down-projection data gradient and the SwiGLU backward in one kernel.
+DLT_API int dlt_gemm_tn8_swiglu_bwd(const bf16_t* A, const bf16_t* B, const bf16_t* gu, bf16_t* dgu, int M, int I,
+                                    int K, int lda, int ldb, hipStream_t st) {
+  if (M <= 0 || I <= 0 || M % 256 || I % 256 || K % 128 || K < 128 || (lda | ldb) % 8) return -1;
+  k_gemm_tn8<EPI_SWIGLU_BWD><<<(M / 256) * (I / 256), 512, 0, st>>>(A, B, nullptr, M, I, K, lda, ldb, 0, gu, dgu, I);
   DLT_CHECK_LAUNCH();
 }

@@ -88,6 +88,8 @@ def load_plan(path: str) -> None:
             raise RuntimeError(f"dlt_gemm_pin failed ({rc})")
     _PINNED["tn"] = {tuple(int(x) for x in k.split("x")): (None if c is None else int(c))
                      for k, c in plan.get("tn", {}).items()}
+    _PINNED["tn"].update({("swiglu_bwd", *(int(x) for x in k.split("x"))): bool(c)
+                          for k, c in plan.get("fused", {}).items()})
     _PINNED["splitk"] = {tuple(int(x) for x in k.split("x")): int(c) for k, c in plan.get("splitk", {}).items()}
     _PLAN_STATE["loaded"] = True
 
@@ -106,7 +108,8 @@ def export_plan() -> dict:
             tn.update(g._choice)
             sk.update(g._splitk)
     return {"hipblaslt": [ln for ln in buf.value[:n].decode().splitlines() if ln],
-            "tn": {"x".join(map(str, k)): c for k, c in tn.items()},
+            "tn": {"x".join(map(str, k)): c for k, c in tn.items() if len(k) == 3},
+            "fused": {"x".join(map(str, k[1:])): bool(c) for k, c in tn.items() if len(k) == 4},
             "splitk": {"x".join(map(str, k)): c for k, c in sk.items()}}
 
 
@@ -194,6 +197,7 @@ class HipGemm:
         self._race = os.environ.get("DLT_GEMM_TN", "1") != "0"
         self._splitk = dict(_PINNED["splitk"])  # wgrad (M, N, K) -> token slices (1 = plain accumulate GEMM)
         self._splitk_on = os.environ.get("DLT_WGRAD_SPLITK", "1") != "0"
+        self._fuse_swiglu = os.environ.get("DLT_FUSED_SWIGLU", "1") != "0"
         _INSTANCES.append(weakref.ref(self))
 
     def _lib_linear(self, x, w, y):
@@ -246,9 +250,51 @@ class HipGemm:
             self._lib_linear(x, w, y)
         return y
 
+    def dgrad_swiglu(self, dd: torch.Tensor, wdown: torch.Tensor, gu: torch.Tensor, ops, out=None) -> torch.Tensor:
+        """dgu = swiglu_bwd(gu, dd @ Wdown): the fused hand-written kernel (GEMM with the
+        SwiGLU backward in its epilogue, ``hip.dgrad_swiglu_bwd``) or the library GEMM +
+        ``ops.swiglu_bwd``, whichever ran faster when the shape was first seen (timed
+        once, like the forward race).  ``DLT_FUSED_SWIGLU=0``: always unfused."""
+        from . import hip
+        M = dd.shape[0]
+        key = ("swiglu_bwd", M, wdown.shape[0], wdown.shape[1])
+        choice = self._choice.get(key)
+        fused_ok = (self._fuse_swiglu and dd.is_contiguous() and gu.is_contiguous()
+                    and M % 256 == 0 and wdown.shape[1] % 256 == 0 and wdown.shape[0] % 128 == 0)
+        if not fused_ok:
+            choice = False
+
+        def unfused():
+            return ops.swiglu_bwd(gu, self.linear_dgrad(dd, wdown), out=out)
+
+        def fused():
+            return hip.dgrad_swiglu_bwd(dd, wdown.t().contiguous(), gu, out=out)
+        if choice is None:
+            if torch.cuda.is_current_stream_capturing():
+                choice = False
+            else:
+                def t_of(fn):
+                    fn()
+                    torch.cuda.synchronize()
+                    best = float("inf")
+                    for _ in range(3):
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record()
+                        for _ in range(3):
+                            fn()
+                        e1.record()
+                        e1.synchronize()
+                        best = min(best, e0.elapsed_time(e1))
+                    return best
+                choice = t_of(fused) < 0.97 * t_of(unfused)
+            self._choice[key] = choice
+        return fused() if choice else unfused()
+
     def report_choices(self) -> dict:
-        out = {f"M{m}xN{n}xK{k}": ("hipBLASLt" if c is None else f"gemm_tn cfg{c}")
-               for (m, n, k), c in self._choice.items()}
+        out = {f"M{k[0]}xN{k[1]}xK{k[2]}": ("hipBLASLt" if c is None else f"gemm_tn cfg{c}")
+               for k, c in self._choice.items() if len(k) == 3}
+        out.update({f"dgrad+swiglu_bwd M{k[1]}": ("fused gemm_tn8" if c else "hipBLASLt + swiglu_bwd")
+                    for k, c in self._choice.items() if len(k) == 4})
         out.update({f"wgrad M{m}xN{n}xK{k}": f"split-K x{s}" if s > 1 else "hipBLASLt accumulate"
                     for (m, n, k), s in self._splitk.items()})
         return out

@@ -54,6 +54,8 @@ _SIGS = {
     "dlt_scale_bf16": [c_void_p, c_void_p, ctypes.c_long, c_void_p, c_void_p],
     "dlt_gemm_tn": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "dlt_gemm_tn8": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "dlt_gemm_tn8_swiglu_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                                c_void_p],
     "dlt_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                      c_uint32, c_uint32, c_float, c_int, c_void_p],
     "dlt_attn_dropout_mask": [c_void_p, c_int, c_int, c_int, c_uint32, c_uint32, c_void_p],
@@ -538,6 +540,26 @@ def gemm_tn(a: torch.Tensor, b: torch.Tensor, cfg: int, out: Optional[torch.Tens
     else:
         _chk(lib().dlt_gemm_tn(_p(a), _p(b), _p(c), M, N, K, K, K, N, cfg, _stream()), "gemm_tn")
     return c
+
+
+def dgrad_swiglu_bwd(dd: torch.Tensor, wdown_t: torch.Tensor, gu: torch.Tensor,
+                     out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """dgu = swiglu_bwd(gu, dd @ Wdown) in ONE kernel (``csrc/gemm_tn8.hip``
+    EPI_SWIGLU_BWD): the down-projection data gradient never leaves the accumulators.
+    ``wdown_t`` is Wdown^T [I, H] (row-major, H contiguous).  Returns None (nothing
+    launched) when the shape does not tile (M, I % 256, H % 128)."""
+    M, H = dd.shape
+    I = wdown_t.shape[0]
+    if M % 256 or I % 256 or H % 128 or H < 128 or wdown_t.shape[1] != H or gu.shape != (M, 2 * I):
+        return None
+    _req(dd, torch.bfloat16, "dgrad_swiglu.dd")
+    _req(wdown_t, torch.bfloat16, "dgrad_swiglu.wdown_t")
+    _req(gu, torch.bfloat16, "dgrad_swiglu.gu")
+    dgu = torch.empty(M, 2 * I, dtype=torch.bfloat16, device=dd.device) if out is None else out
+    _req(dgu, torch.bfloat16, "dgrad_swiglu.dgu", M * 2 * I)
+    _chk(lib().dlt_gemm_tn8_swiglu_bwd(_p(dd), _p(wdown_t), _p(gu), _p(dgu), M, I, H, H, H, _stream()),
+         "gemm_tn8_swiglu_bwd")
+    return dgu
 
 
 def scale_bf16(x: torch.Tensor, scale: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -357,6 +357,30 @@ def test_gemm_plan_pin_roundtrip(tmp_path):
     gemm.load_plan(str(path))  # loading a saved plan re-pins without error
 
 
+@pytest.mark.parametrize("M,H,I", [(512, 256, 512), (2048, 768, 3072)])
+def test_dgrad_swiglu_fused(M, H, I):
+    """The down-projection data gradient with the SwiGLU backward in the GEMM epilogue
+    (gemm_tn8 EPI_SWIGLU_BWD) against the fp32 reference of dd @ Wdown -> swiglu_bwd,
+    and the planner entry point (race + unfused fallback) against the unfused ops."""
+    from distributed_llm_trainer_amd.ops import gemm
+    torch.manual_seed(3)
+    dd = (torch.randn(M, H, device=DEV) * 0.5).bfloat16()
+    wdown = (torch.randn(H, I, device=DEV) / H ** 0.5).bfloat16()
+    gu = torch.randn(M, 2 * I, device=DEV).bfloat16()
+    got = hip.dgrad_swiglu_bwd(dd, wdown.t().contiguous(), gu)
+    ds = dd.float() @ wdown.float()
+    g, u = gu.float()[:, :I], gu.float()[:, I:]
+    sg = torch.sigmoid(g)
+    want = torch.cat([ds * u * sg * (1 + g * (1 - sg)), ds * g * sg], dim=1)
+    _close(got, want, 2e-2 * want.abs().max().item(), 2e-2, "fused dgrad+swiglu_bwd")
+    g2 = gemm.HipGemm()
+    out = torch.empty(M, 2 * I, device=DEV, dtype=torch.bfloat16)
+    r = g2.dgrad_swiglu(dd, wdown, gu, hip, out=out)
+    assert r.data_ptr() == out.data_ptr()
+    _close(r, want, 2e-2 * want.abs().max().item(), 2e-2, "planner dgrad_swiglu")
+    assert ("swiglu_bwd", M, H, I) in g2._choice
+
+
 @pytest.mark.parametrize("M,N,K", [(1024, 256, 128), (2048, 768, 384)])
 def test_wgrad_gemm_kernel(M, N, K):
     torch.manual_seed(0)
