@@ -15,10 +15,13 @@
 //     (DLT_GEMM_WORKSPACE_MB, default 64), so GEMMs on the compute and side streams
 //     can run concurrently (see StreamCtx),
 //   * records the chosen kernel's name for the plan report,
-//   * accepts pinned picks (dlt_gemm_pin: key -> heuristic index) so a run can replay
-//     another run's choices without timing (ops/gemm.py DLT_GEMM_PLAN); with the same
-//     hipBLASLt build the heuristic list of a key is deterministic, so the index names
-//     the same kernel.
+//   * accepts pinned picks (dlt_gemm_pin: key -> hipBLASLt solution index, from
+//     hipblaslt_ext::getIndexFromAlgo) so a run replays another run's choices without
+//     timing (ops/gemm.py DLT_GEMM_PLAN, the shipped configs/gemm_plan_mi355x.json);
+//     a pin this hipBLASLt build does not support for the problem is ignored,
+//   * DLT_GEMM_TUNE=exhaustive times EVERY supported solution (getAllAlgos), not just
+//     the heuristic's first candidates: 2-15 % faster picks on the model's shapes
+//     (profiles/r2_gemm_exhaustive.md), minutes of tuning -> an offline step.
 // C ABI, loaded by ctypes from ops/gemm.py.
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt.h>
@@ -56,6 +59,7 @@ struct Plan {
   size_t ws = 0;
   float us = -1.f;
   int chosen = 0, candidates = 0;
+  int sol = -1;  // hipBLASLt solution index (stable within one hipBLASLt build)
   std::string kernel;
 };
 
@@ -80,7 +84,9 @@ struct Planner {
   bool verbose = false;
   bool drain = true;  // DLT_GEMM_TUNE_DRAIN=0: time candidates without draining the device first
   bool fail_backup = false;  // test hook: behave as if the accumulator backup could not be allocated
-  std::map<Key, int> pins;   // key -> heuristic index (replayed plan)
+  std::map<Key, int> pins;   // key -> hipBLASLt solution index (replayed plan)
+  bool exhaustive = false;   // DLT_GEMM_TUNE=exhaustive: time every supported solution
+  int pin_misses = 0;        // pinned solutions this build rejected
 };
 
 Planner* g = nullptr;
@@ -96,7 +102,8 @@ int init() {
   e = getenv("DLT_GEMM_CANDIDATES");
   if (e) p->max_cand = atoi(e);
   e = getenv("DLT_GEMM_TUNE");
-  if (e && atoi(e) == 0) p->tune = false;
+  if (e && strcmp(e, "exhaustive") == 0) p->exhaustive = true;
+  else if (e && atoi(e) == 0) p->tune = false;
   e = getenv("DLT_GEMM_VERBOSE");
   p->verbose = e && atoi(e) != 0;
   e = getenv("DLT_GEMM_TUNE_DRAIN");
@@ -150,19 +157,66 @@ int build_plan(const Key& k, Plan& p, const void* A, const void* B, void* C, hip
                                                        (int)res.size(), res.data(), &n);
   hipblasLtMatmulPreferenceDestroy(pref);
   if (st != HIPBLAS_STATUS_SUCCESS || n == 0) return -24;
+  res.resize(n);
+  float alpha = 1.f, beta0 = 0.f;
   p.algo = res[0].algo;
   p.ws = res[0].workspaceSize;
   p.candidates = n;
-  auto pin = g->pins.find(k);
-  if (pin != g->pins.end() && pin->second >= 0 && pin->second < n &&
-      res[pin->second].workspaceSize <= g->wsz) {
-    p.algo = res[pin->second].algo;
-    p.ws = res[pin->second].workspaceSize;
-    p.chosen = pin->second;
+  auto finish = [&](int chosen) {
+    p.chosen = chosen;
+    p.sol = hipblaslt_ext::getIndexFromAlgo(p.algo);
     p.kernel = hipblaslt_ext::getKernelNameFromAlgo(g->h, p.algo);
+  };
+  // pinned solution (a replayed plan): the solution index names a kernel of this
+  // hipBLASLt build; it is used only if hipBLASLt confirms it supports this problem
+  auto pin = g->pins.find(k);
+  if (pin != g->pins.end() && pin->second >= 0) {
+    std::vector<int> idx{pin->second};
+    std::vector<hipblasLtMatmulHeuristicResult_t> r1;
+    size_t need = 0;
+    if (hipblaslt_ext::getAlgosFromIndex(g->h, idx, r1) == HIPBLAS_STATUS_SUCCESS && !r1.empty() &&
+        hipblaslt_ext::matmulIsAlgoSupported(g->h, p.desc, &alpha, p.la, p.lb, &beta0, p.lc, p.lc, r1[0].algo, need) ==
+            HIPBLAS_STATUS_SUCCESS &&
+        need <= g->wsz) {
+      p.algo = r1[0].algo;
+      p.ws = need;
+      finish(-1);
+      return 0;
+    }
+    (void)hipGetLastError();
+    ++g->pin_misses;  // stale plan entry (other hipBLASLt build): fall through to tuning
+  }
+  if (!g->tune || capturing(s)) {
+    finish(0);
     return 0;
   }
-  if (!g->tune || n == 1 || capturing(s)) return 0;
+  // candidate list: the heuristic's first max_cand, or (DLT_GEMM_TUNE=exhaustive) every
+  // solution of this GEMM type that hipBLASLt accepts for the problem -- thousands, so
+  // exhaustive tuning is an offline step whose picks are shipped as a plan file
+  // (tools/tune_gemm_plan.py, configs/gemm_plan_mi355x.json).
+  std::vector<std::pair<hipblasLtMatmulAlgo_t, size_t>> cands;
+  for (auto& r : res)  // the heuristic's candidates always compete (first, in its order)
+    if (r.workspaceSize <= g->wsz) cands.emplace_back(r.algo, r.workspaceSize);
+  if (g->exhaustive) {
+    std::vector<int> seen;
+    for (auto& c : cands) seen.push_back(hipblaslt_ext::getIndexFromAlgo(c.first));
+    std::vector<hipblasLtMatmulHeuristicResult_t> all;
+    hipblaslt_ext::getAllAlgos(g->h, hipblaslt_ext::GemmType::HIPBLASLT_GEMM, ta, tb, dt_of(k.dta), dt_of(k.dtb),
+                               dt_of(k.dtc), dt_of(k.dtc), HIPBLAS_COMPUTE_32F, all);
+    for (auto& r : all) {
+      size_t need = 0;
+      if (std::find(seen.begin(), seen.end(), hipblaslt_ext::getIndexFromAlgo(r.algo)) != seen.end()) continue;
+      if (hipblaslt_ext::matmulIsAlgoSupported(g->h, p.desc, &alpha, p.la, p.lb, &beta0, p.lc, p.lc, r.algo, need) ==
+              HIPBLAS_STATUS_SUCCESS &&
+          need <= g->wsz)
+        cands.emplace_back(r.algo, need);
+    }
+    (void)hipGetLastError();
+  }
+  if (cands.size() <= 1) {
+    finish(0);
+    return 0;
+  }
   // Autotune on the caller's stream.  Timing needs a host sync; this runs once per
   // shape (warmup step).  beta = 0 while timing so an accumulating GEMM does not
   // disturb C (its real call comes right after with the requested beta).
@@ -172,7 +226,6 @@ int build_plan(const Key& k, Plan& p, const void* A, const void* B, void* C, hip
   // that do well on fewer CUs.  (No deadlock: every collective this rank waits for was
   // launched by it, and peers launch collectives in the same order.)
   if (g->drain) hipDeviceSynchronize();
-  float alpha = 1.f, beta0 = 0.f;
   size_t csize = (k.batch > 1 ? (size_t)k.sc * (k.batch - 1) : 0) + (size_t)k.ldc * k.n;
   csize *= (k.dtc == 0 ? 4 : 2);
   void* cbak = nullptr;
@@ -183,6 +236,7 @@ int build_plan(const Key& k, Plan& p, const void* A, const void* B, void* C, hip
     // heuristic's first pick.
     if (g->fail_backup || hipMalloc(&cbak, csize) != hipSuccess) {
       (void)hipGetLastError();  // do not let the failed allocation surface at the next launch check
+      finish(0);
       return 0;
     }
     hipMemcpyAsync(cbak, C, csize, hipMemcpyDeviceToDevice, s);
@@ -190,26 +244,32 @@ int build_plan(const Key& k, Plan& p, const void* A, const void* B, void* C, hip
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  float best = 1e30f;
-  int bi = 0;
-  for (int i = 0; i < n; ++i) {
-    if (res[i].workspaceSize > g->wsz) continue;
-    bool ok = true;
-    for (int w = 0; w < 2 && ok; ++w)
-      ok = hipblasLtMatmul(sc->h, p.desc, &alpha, A, p.la, B, p.lb, &beta0, C, p.lc, C, p.lc, &res[i].algo, ws,
-                           g->wsz, s) == HIPBLAS_STATUS_SUCCESS;
-    if (!ok) continue;
+  auto time_it = [&](hipblasLtMatmulAlgo_t& algo, int warm, int iters) -> float {
+    for (int w = 0; w < warm; ++w)
+      if (hipblasLtMatmul(sc->h, p.desc, &alpha, A, p.la, B, p.lb, &beta0, C, p.lc, C, p.lc, &algo, ws, g->wsz, s) !=
+          HIPBLAS_STATUS_SUCCESS)
+        return -1.f;
     hipEventRecord(e0, s);
-    const int iters = 5;
     for (int it = 0; it < iters; ++it)
-      hipblasLtMatmul(sc->h, p.desc, &alpha, A, p.la, B, p.lb, &beta0, C, p.lc, C, p.lc, &res[i].algo, ws, g->wsz,
-                      s);
+      hipblasLtMatmul(sc->h, p.desc, &alpha, A, p.la, B, p.lb, &beta0, C, p.lc, C, p.lc, &algo, ws, g->wsz, s);
     hipEventRecord(e1, s);
     hipEventSynchronize(e1);
     float ms = 0.f;
     hipEventElapsedTime(&ms, e0, e1);
-    const float us = ms * 1000.f / iters;
-    if (us < best) { best = us; bi = i; }
+    return ms * 1000.f / iters;
+  };
+  std::vector<std::pair<float, int>> t;
+  const bool two_pass = cands.size() > 32;  // exhaustive: a short screen, then re-time the best 8
+  for (int i = 0; i < (int)cands.size(); ++i) {
+    const float us = two_pass ? time_it(cands[i].first, 1, 2) : time_it(cands[i].first, 2, 5);
+    if (us > 0) t.emplace_back(us, i);
+  }
+  (void)hipGetLastError();
+  std::sort(t.begin(), t.end());
+  if (two_pass && t.size() > 1) {
+    const int top = std::min<int>(8, (int)t.size());
+    for (int j = 0; j < top; ++j) t[j].first = time_it(cands[t[j].second].first, 1, 10);
+    std::sort(t.begin(), t.begin() + top);
   }
   if (cbak) {
     hipMemcpyAsync(C, cbak, csize, hipMemcpyDeviceToDevice, s);
@@ -218,14 +278,16 @@ int build_plan(const Key& k, Plan& p, const void* A, const void* B, void* C, hip
   }
   hipEventDestroy(e0);
   hipEventDestroy(e1);
-  p.algo = res[bi].algo;
-  p.ws = res[bi].workspaceSize;
-  p.us = best;
-  p.chosen = bi;
-  p.kernel = hipblaslt_ext::getKernelNameFromAlgo(g->h, p.algo);
+  const int bi = t.empty() ? 0 : t[0].second;
+  p.algo = cands[bi].first;
+  p.ws = cands[bi].second;
+  p.us = t.empty() ? -1.f : t[0].first;
+  p.candidates = (int)cands.size();
+  finish(bi);
   if (g->verbose)
-    fprintf(stderr, "[dlt-gemm] ta=%d tb=%d m=%d n=%d k=%d acc=%d: %d candidates, chose #%d (%.1f us, %.0f TF/s)\n", k.ta,
-            k.tb, k.m, k.n, k.k, k.accumulate, n, bi, best, 2.0 * k.m * k.n * k.k / best / 1e6);
+    fprintf(stderr, "[dlt-gemm] ta=%d tb=%d m=%d n=%d k=%d acc=%d: %zu candidates, chose #%d sol %d (%.1f us, %.0f TF/s)\n",
+            k.ta, k.tb, k.m, k.n, k.k, k.accumulate, cands.size(), bi, p.sol, p.us,
+            2.0 * k.m * k.n * k.k * k.batch / p.us / 1e6);
   return 0;
 }
 
@@ -278,6 +340,15 @@ DLT_API int dlt_gemm_batched(int ta, int tb, int m, int n, int k, const void* A,
 }
 
 DLT_API int dlt_gemm_num_plans() { return g ? (int)g->plans.size() : 0; }
+DLT_API int dlt_gemm_pin_misses() { return g ? g->pin_misses : 0; }
+
+// hipBLASLt build identifier (solution indices are only meaningful within one build)
+DLT_API int dlt_gemm_lib_version() {
+  int v = 0;
+  if (int rc = init()) return rc;
+  hipblasLtGetVersion(g->h, &v);
+  return v;
+}
 
 // Test hook: pretend the accumulator backup allocation fails (accumulating keys first
 // seen afterwards are not timed).
@@ -288,7 +359,7 @@ DLT_API int dlt_gemm_test_fail_backup(int on) {
   return 0;
 }
 
-// Pin the heuristic index of a key (must be called before the key is first used).
+// Pin the hipBLASLt solution index of a key (before the key is first used).
 DLT_API int dlt_gemm_pin(int ta, int tb, int m, int n, int k, int lda, int ldb, int ldc, int dta, int dtb, int dtc,
                          int accumulate, int batch, long long sa, long long sb, long long sc, int chosen) {
   if (int rc = init()) return rc;
@@ -303,7 +374,7 @@ DLT_API int dlt_gemm_pin(int ta, int tb, int m, int n, int k, int lda, int ldb, 
 }
 
 // Machine-readable plan table: one line per key,
-// "ta tb m n k lda ldb ldc dta dtb dtc acc batch sa sb sc chosen" (input of dlt_gemm_pin).
+// "ta tb m n k lda ldb ldc dta dtb dtc acc batch sa sb sc solution" (input of dlt_gemm_pin).
 DLT_API int dlt_gemm_dump(char* buf, int len) {
   if (!g || len <= 0) return 0;
   std::string out;
@@ -313,7 +384,7 @@ DLT_API int dlt_gemm_dump(char* buf, int len) {
     char line[256];
     snprintf(line, sizeof(line), "%d %d %d %d %d %d %d %d %d %d %d %d %d %lld %lld %lld %d\n", k.ta, k.tb, k.m, k.n,
              k.k, k.lda, k.ldb, k.ldc, k.dta, k.dtb, k.dtc, k.accumulate, k.batch, k.sa, k.sb, k.sc,
-             kv.second.chosen);
+             kv.second.sol);
     out += line;
   }
   if (out.size() + 1 > (size_t)len) return -1;
@@ -330,8 +401,8 @@ DLT_API int dlt_gemm_report(char* buf, int len) {
     const Key& k = kv.first;
     const Plan& p = kv.second;
     char line[512];
-    snprintf(line, sizeof(line), "ta=%d tb=%d m=%d n=%d k=%d acc=%d dtc=%d cand=%d chosen=%d us=%.1f %.80s\n", k.ta,
-             k.tb, k.m, k.n, k.k, k.accumulate, k.dtc, p.candidates, p.chosen, p.us, p.kernel.c_str());
+    snprintf(line, sizeof(line), "ta=%d tb=%d m=%d n=%d k=%d acc=%d dtc=%d cand=%d chosen=%d sol=%d us=%.1f %.80s\n",
+             k.ta, k.tb, k.m, k.n, k.k, k.accumulate, k.dtc, p.candidates, p.chosen, p.sol, p.us, p.kernel.c_str());
     out += line;
   }
   int n = (int)std::min<size_t>(out.size(), (size_t)len - 1);

@@ -11,15 +11,22 @@ Each distinct shape is autotuned once on first use (see ``csrc_gemm/gemm_planner
 If the planner library cannot be loaded, the engine uses torch.matmul (also hipBLASLt,
 default heuristics) and logs why.
 
-Reproducibility.  Autotuning picks the hipBLASLt algorithm, the split-K factor of the
-weight gradients and the hand-written-vs-library race per process by timing, so the
+Plans.  Autotuning picks the hipBLASLt solution, the split-K factor of the weight
+gradients and the hand-written-vs-library races per process by timing, so the
 summation order of a weight gradient (and the last bits of a loss curve) can differ
-between runs, or between a run and its resumed continuation.  ``DLT_GEMM_PLAN=path``
-pins them: if the file exists every choice is replayed from it (no timing); otherwise
-the first process to finish a step writes it (``save_plan``).  DDP replicas stay in
-sync regardless (the all-reduced gradient is identical on every rank).  For bitwise
-run-to-run reproducibility without a plan file use ``DLT_GEMM_TUNE=0
-DLT_WGRAD_SPLITK=0 DLT_GEMM_TN=0`` (heuristic #0 everywhere).
+between runs, or between a run and its resumed continuation.  A plan file pins them:
+* ``configs/gemm_plan_mi355x.json`` (shipped) holds the picks of an EXHAUSTIVE offline
+  search over every hipBLASLt solution for the headline shapes
+  (``tools/tune_gemm_plan.py``, ``DLT_GEMM_TUNE=exhaustive``; 2-15 % faster than the
+  best of the heuristic's first 24 candidates, ``profiles/r2_gemm_exhaustive.md``).  It
+  is loaded by default; keys it does not cover are tuned as usual, and pins a different
+  hipBLASLt build does not support are ignored.
+* ``DLT_GEMM_PLAN=path`` replaces it: if the file exists every choice is replayed from
+  it (no timing); otherwise the first process to finish a step writes it
+  (``save_plan``).  ``DLT_GEMM_PLAN=none``: no plan.
+DDP replicas stay in sync regardless (the all-reduced gradient is identical on every
+rank).  For bitwise run-to-run reproducibility without a plan file use
+``DLT_GEMM_TUNE=0 DLT_WGRAD_SPLITK=0 DLT_GEMM_TN=0`` (heuristic #0 everywhere).
 """
 from __future__ import annotations
 
@@ -55,6 +62,10 @@ def lib():
         L.dlt_gemm_pin.restype = c.c_int
         L.dlt_gemm_test_fail_backup.argtypes = [c.c_int]
         L.dlt_gemm_test_fail_backup.restype = c.c_int
+        L.dlt_gemm_lib_version.argtypes = []
+        L.dlt_gemm_lib_version.restype = c.c_int
+        L.dlt_gemm_pin_misses.argtypes = []
+        L.dlt_gemm_pin_misses.restype = c.c_int
         _LIB = L
         _load_plan_env()
     return _LIB
@@ -64,34 +75,49 @@ def lib():
 _PINNED = {"tn": {}, "splitk": {}}  # replayed framework-level choices (see module docstring)
 _PLAN_STATE = {"path": None, "loaded": False, "saved": False}
 _INSTANCES = []  # weak references to live HipGemm objects (for save_plan)
+SHIPPED_PLAN = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                            "configs", "gemm_plan_mi355x.json")
 
 
 def _load_plan_env() -> None:
     path = os.environ.get("DLT_GEMM_PLAN")
-    _PLAN_STATE["path"] = path
-    if path and os.path.exists(path):
-        load_plan(path)
+    if path == "none":
+        return
+    if path:
+        _PLAN_STATE["path"] = path
+        if os.path.exists(path):
+            load_plan(path)
+    elif os.path.exists(SHIPPED_PLAN):
+        load_plan(SHIPPED_PLAN, shipped=True)
 
 
-def load_plan(path: str) -> None:
-    """Pin every choice recorded in a plan file written by :func:`save_plan`."""
+def load_plan(path: str, shipped: bool = False) -> None:
+    """Pin every choice recorded in a plan file written by :func:`save_plan`.  The
+    hipBLASLt solution pins are skipped when the file was tuned with another hipBLASLt
+    build (solution indices are build-specific)."""
     import json
     with open(path) as f:
         plan = json.load(f)
     L = lib()
-    for line in plan.get("hipblaslt", []):
-        v = [int(x) for x in line.split()]
-        if len(v) != 17:
-            raise ValueError(f"bad hipBLASLt plan line {line!r} in {path}")
-        rc = L.dlt_gemm_pin(*v)
-        if rc != 0:
-            raise RuntimeError(f"dlt_gemm_pin failed ({rc})")
+    ver = int(L.dlt_gemm_lib_version())
+    if plan.get("hipblaslt_version", ver) != ver:
+        warnings.warn(f"GEMM plan {path} was tuned with hipBLASLt {plan.get('hipblaslt_version')}, this is {ver}: "
+                      "its solution pins are ignored")
+    else:
+        for line in plan.get("hipblaslt", []):
+            v = [int(x) for x in line.split()]
+            if len(v) != 17:
+                raise ValueError(f"bad hipBLASLt plan line {line!r} in {path}")
+            rc = L.dlt_gemm_pin(*v)
+            if rc != 0:
+                raise RuntimeError(f"dlt_gemm_pin failed ({rc})")
     _PINNED["tn"] = {tuple(int(x) for x in k.split("x")): (None if c is None else int(c))
                      for k, c in plan.get("tn", {}).items()}
     _PINNED["tn"].update({("swiglu_bwd", *(int(x) for x in k.split("x"))): bool(c)
                           for k, c in plan.get("fused", {}).items()})
     _PINNED["splitk"] = {tuple(int(x) for x in k.split("x")): int(c) for k, c in plan.get("splitk", {}).items()}
-    _PLAN_STATE["loaded"] = True
+    if not shipped:
+        _PLAN_STATE["loaded"] = True
 
 
 def export_plan() -> dict:
@@ -107,7 +133,8 @@ def export_plan() -> dict:
         if g is not None:
             tn.update(g._choice)
             sk.update(g._splitk)
-    return {"hipblaslt": [ln for ln in buf.value[:n].decode().splitlines() if ln],
+    return {"hipblaslt_version": int(lib().dlt_gemm_lib_version()),
+            "hipblaslt": [ln for ln in buf.value[:n].decode().splitlines() if ln and int(ln.split()[-1]) >= 0],
             "tn": {"x".join(map(str, k)): c for k, c in tn.items() if len(k) == 3},
             "fused": {"x".join(map(str, k[1:])): bool(c) for k, c in tn.items() if len(k) == 4},
             "splitk": {"x".join(map(str, k)): c for k, c in sk.items()}}

@@ -332,28 +332,47 @@ def test_gemm_planner_accumulate_without_backup():
 
 
 def test_gemm_plan_pin_roundtrip(tmp_path):
-    """DLT_GEMM_PLAN machinery: export the plan table, and a pinned index is used for a
-    key first seen afterwards (no timing)."""
+    """Plan machinery: the exported table names hipBLASLt solution indices; a pinned
+    solution is used (no timing) for a key first seen afterwards, and a pin the library
+    does not support for the problem is ignored."""
     from distributed_llm_trainer_amd.ops import gemm
     g = gemm.HipGemm()
     x = torch.randn(512, 384, device=DEV).bfloat16()
     w = torch.randn(640, 384, device=DEV).bfloat16()
     g.linear(x, w)
     plan = gemm.export_plan()
-    assert any(ln.split()[2:5] == ["640", "512", "384"] for ln in plan["hipblaslt"])
-    assert "512x640x384" in plan["tn"]
+    assert plan["hipblaslt_version"] == gemm.lib().dlt_gemm_lib_version()
+    line = [ln for ln in plan["hipblaslt"] if ln.split()[2:5] == ["640", "512", "384"]]
+    assert line, plan["hipblaslt"]
+    sol = int(line[0].split()[-1])
+    assert sol >= 0
     path = tmp_path / "plan.json"
     gemm.save_plan(str(path))
-    # pin heuristic #1 for a fresh forward key (m=N, n=M, k=K in BLAS terms)
-    M, N, K = 768, 896, 384
-    assert gemm.lib().dlt_gemm_pin(1, 0, N, M, K, K, K, N, 1, 1, 1, 0, 1, 0, 0, 0, 1) == 0
+    # pin that solution for a fresh forward key of the same (N, K) (m=N, n=M, k=K in BLAS terms)
+    M, N, K = 768, 640, 384
+    L = gemm.lib()
+    assert L.dlt_gemm_pin(1, 0, N, M, K, K, K, N, 1, 1, 1, 0, 1, 0, 0, 0, sol) == 0
     x2 = torch.randn(M, K, device=DEV).bfloat16()
     w2 = torch.randn(N, K, device=DEV).bfloat16()
     y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
     g._lib_linear(x2, w2, y)
     _close(y, x2.float() @ w2.float().t(), 0.05 * K ** 0.5, 2e-2, "pinned linear")
-    line = [ln for ln in gemm.report().splitlines() if f"m={N} n={M} k={K} acc=0" in ln]
-    assert line and ("chosen=1" in line[0] or "cand=1 " in line[0]), line
+    rep = [ln for ln in gemm.report().splitlines() if f"m={N} n={M} k={K} acc=0" in ln]
+    assert rep and f"sol={sol} " in rep[0] and "chosen=-1" in rep[0], rep
+    # a pin naming a solution of another GEMM type (an fp32-output NT weight-gradient
+    # kernel) is rejected for this bf16 TN problem and the key is tuned normally
+    dw = torch.zeros(N, K, device=DEV)
+    g._wgrad_plain(dw, torch.randn(256, N, device=DEV).bfloat16(), torch.randn(256, K, device=DEV).bfloat16())
+    wl = [ln for ln in gemm.export_plan()["hipblaslt"] if ln.split()[:2] == ["0", "1"] and ln.split()[4] == "256"]
+    assert wl
+    wsol = int(wl[0].split()[-1])
+    misses = L.dlt_gemm_pin_misses()
+    assert L.dlt_gemm_pin(1, 0, N, 896, K, K, K, N, 1, 1, 1, 0, 1, 0, 0, 0, wsol) == 0
+    x3 = torch.randn(896, K, device=DEV).bfloat16()
+    y3 = torch.empty(896, N, device=DEV, dtype=torch.bfloat16)
+    g._lib_linear(x3, w2, y3)
+    _close(y3, x3.float() @ w2.float().t(), 0.05 * K ** 0.5, 2e-2, "bogus-pin linear")
+    assert L.dlt_gemm_pin_misses() == misses + 1
     gemm.load_plan(str(path))  # loading a saved plan re-pins without error
 
 
