@@ -75,6 +75,7 @@ def lib():
 _PINNED = {"tn": {}, "splitk": {}}  # replayed framework-level choices (see module docstring)
 _PLAN_STATE = {"path": None, "loaded": False, "saved": False}
 _INSTANCES = []  # weak references to live HipGemm objects (for save_plan)
+_RACES = {}  # process-wide race outcomes, see HipGemm.__init__
 SHIPPED_PLAN = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
                             "configs", "gemm_plan_mi355x.json")
 
@@ -116,6 +117,9 @@ def load_plan(path: str, shipped: bool = False) -> None:
     _PINNED["tn"].update({("swiglu_bwd", *(int(x) for x in k.split("x"))): bool(c)
                           for k, c in plan.get("fused", {}).items()})
     _PINNED["splitk"] = {tuple(int(x) for x in k.split("x")): int(c) for k, c in plan.get("splitk", {}).items()}
+    if _RACES:
+        _RACES["tn"].update(_PINNED["tn"])
+        _RACES["splitk"].update(_PINNED["splitk"])
     if not shipped:
         _PLAN_STATE["loaded"] = True
 
@@ -220,9 +224,15 @@ class HipGemm:
     def __init__(self):
         import weakref
         lib()  # loads DLT_GEMM_PLAN pins before any choice is made
-        self._choice = dict(_PINNED["tn"])  # (M, N, K) -> None (library) or tile cfg of gemm_tn
+        # race outcomes are PROCESS-wide (shared by every HipGemm, seeded from the plan):
+        # two models / trainers in one process must not pick different kernels -- and
+        # so different summation orders -- for the same shape
+        if not _RACES:
+            _RACES["tn"] = dict(_PINNED["tn"])
+            _RACES["splitk"] = dict(_PINNED["splitk"])
+        self._choice = _RACES["tn"]  # (M, N, K) -> None (library) or tile cfg of gemm_tn
         self._race = os.environ.get("DLT_GEMM_TN", "1") != "0"
-        self._splitk = dict(_PINNED["splitk"])  # wgrad (M, N, K) -> token slices (1 = plain accumulate GEMM)
+        self._splitk = _RACES["splitk"]  # wgrad (M, N, K) -> token slices (1 = plain accumulate GEMM)
         self._splitk_on = os.environ.get("DLT_WGRAD_SPLITK", "1") != "0"
         self._fuse_swiglu = os.environ.get("DLT_FUSED_SWIGLU", "1") != "0"
         _INSTANCES.append(weakref.ref(self))
