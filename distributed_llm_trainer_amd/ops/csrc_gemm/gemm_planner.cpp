@@ -197,12 +197,14 @@ int build_plan(const Key& k, Plan& p, const void* A, const void* B, void* C, hip
   std::vector<std::pair<hipblasLtMatmulAlgo_t, size_t>> cands;
   for (auto& r : res)  // the heuristic's candidates always compete (first, in its order)
     if (r.workspaceSize <= g->wsz) cands.emplace_back(r.algo, r.workspaceSize);
+  size_t n_all = 0;
   if (g->exhaustive) {
     std::vector<int> seen;
     for (auto& c : cands) seen.push_back(hipblaslt_ext::getIndexFromAlgo(c.first));
     std::vector<hipblasLtMatmulHeuristicResult_t> all;
     hipblaslt_ext::getAllAlgos(g->h, hipblaslt_ext::GemmType::HIPBLASLT_GEMM, ta, tb, dt_of(k.dta), dt_of(k.dtb),
                                dt_of(k.dtc), dt_of(k.dtc), HIPBLAS_COMPUTE_32F, all);
+    n_all = all.size();
     for (auto& r : all) {
       size_t need = 0;
       if (std::find(seen.begin(), seen.end(), hipblaslt_ext::getIndexFromAlgo(r.algo)) != seen.end()) continue;
@@ -285,8 +287,8 @@ int build_plan(const Key& k, Plan& p, const void* A, const void* B, void* C, hip
   p.candidates = (int)cands.size();
   finish(bi);
   if (g->verbose)
-    fprintf(stderr, "[dlt-gemm] ta=%d tb=%d m=%d n=%d k=%d acc=%d: %zu candidates, chose #%d sol %d (%.1f us, %.0f TF/s)\n",
-            k.ta, k.tb, k.m, k.n, k.k, k.accumulate, cands.size(), bi, p.sol, p.us,
+    fprintf(stderr, "[dlt-gemm] ta=%d tb=%d m=%d n=%d k=%d acc=%d: %zu candidates (of %zu solutions), chose #%d sol %d (%.1f us, %.0f TF/s)\n",
+            k.ta, k.tb, k.m, k.n, k.k, k.accumulate, cands.size(), n_all, bi, p.sol, p.us,
             2.0 * k.m * k.n * k.k * k.batch / p.us / 1e6);
   return 0;
 }
