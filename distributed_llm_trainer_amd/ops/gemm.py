@@ -101,6 +101,8 @@ def load_plan(path: str, shipped: bool = False) -> None:
         plan = json.load(f)
     L = lib()
     ver = int(L.dlt_gemm_lib_version())
+    if ver < 0:  # planner could not initialise (no GPU): nothing to pin
+        return
     if plan.get("hipblaslt_version", ver) != ver:
         warnings.warn(f"GEMM plan {path} was tuned with hipBLASLt {plan.get('hipblaslt_version')}, this is {ver}: "
                       "its solution pins are ignored")
