@@ -117,7 +117,11 @@ __device__ __forceinline__ bf16x8_t acc_frag(const floatx16_t& acc, int s) {
 // `word` (v_bfe_i32), then one AND -- 2 VALU per element instead of and + cmp +
 // cndmask.  A dropped element becomes +0.0f.
 __device__ __forceinline__ uint32_t keep_ones(uint32_t word, int bit) {
-  return (uint32_t)__builtin_amdgcn_sbfe((int)word, bit, 1);
+  uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)word, bit, 1);
+  // Empty asm (no instruction, so nothing for the hazard recognizer to miss): hides
+  // that m is 0 / ~0, which stops LLVM from rewriting bfe + and as and + cmp + cndmask.
+  asm("" : "+v"(m));
+  return m;
 }
 __device__ __forceinline__ float keep_and(float x, uint32_t ones) { return __uint_as_float(__float_as_uint(x) & ones); }
 
