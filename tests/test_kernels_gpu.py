@@ -159,7 +159,7 @@ def _attn_inputs(B, nh, S, seed):
     return q, k, v
 
 
-@pytest.mark.parametrize("S", [64, 128, 200, 1024])
+@pytest.mark.parametrize("S", [64, 128, 200, 1024, 2100])
 @pytest.mark.parametrize("p", [0.0, 0.1])
 def test_attention_fwd(S, p):
     B, nh = 2, 3

@@ -41,6 +41,11 @@ def main():
         do = torch.randn_like(o)
         t_f = timeit(lambda: hip.attention_fwd_packed(qkv, a.B, a.S, a.nh, a.p, key), a.iters)
         t_b = timeit(lambda: hip.attention_bwd_packed(qkv, o, do, aux, a.p, key, a.B, a.S, a.nh, cos, sin), a.iters)
+        if a.p > 0:  # the forward kernel alone (keep bits already generated) -> bits kernel time
+            m = aux[1]
+            if m is not None:
+                t_k = timeit(lambda: hip.attention_fwd_packed(qkv, a.B, a.S, a.nh, a.p, key, mask=m), a.iters)
+                print(f"fwd kernel {t_k:.1f} us, keep-bit kernel {t_f - t_k:.1f} us")
     else:
         o, aux = hip.attention_fwd(q, k, v, a.p, key)
         do = torch.randn_like(o)
