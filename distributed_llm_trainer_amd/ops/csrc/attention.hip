@@ -319,6 +319,23 @@ __device__ __forceinline__ float xhalf_sum(float x) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+// 16-byte row stores from the split-lane accumulator layout.  Lane (row, h) holds dims
+// 32dt + 8g + 4h + [0, 4) (w[dt][g], 4 bf16 = 2 dwords).  One v_permlane32_swap of the
+// (g = 2m, 2m + 1) pair -- own g = 2m stays in the low lanes' vdst, the high lanes' g = 2m
+// lands there; own g = 2m + 1 stays in the high lanes' vsrc -- leaves lane h holding
+// dims 16m + 8h + [0, 8): 4 dwordx4 stores per row instead of 8 dwordx2 (the epilogue's
+// store issue is the tail of every work item).
+__device__ __forceinline__ void store_row16(bf16_t* __restrict__ row, const uint2 (&w)[2][4], int h) {
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const auto rx = __builtin_amdgcn_permlane32_swap(w[dt][2 * m].x, w[dt][2 * m + 1].x, false, false);
+      const auto ry = __builtin_amdgcn_permlane32_swap(w[dt][2 * m].y, w[dt][2 * m + 1].y, false, false);
+      *reinterpret_cast<uint4*>(row + 32 * dt + 16 * m + 8 * h) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+    }
+}
+
 // Rescale threshold (log2 units): the running max is only moved when some row's max
 // grew by more than 2^RESCALE_LOG2 (P is then bounded by 2^8 = 256 instead of 1,
 // exact in fp32 l/O and the same relative bf16 precision for P).  Almost every
@@ -506,15 +523,17 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     if (qa < S) {
       if (h == 0) lse[(size_t)bh * S + qa] = fs.m * (c_log2 / LOG2E) + __logf(l_tot);
       bf16_t* orow = o + (((size_t)b * S + qa) * nh + head) * HD;
+      uint2 w[2][4];
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          u16x4 w;
+          u16x4 t;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) w.v[e] = f2bf(fs.o[dt][4 * g + e] * inv_l);
-          *reinterpret_cast<u16x4*>(orow + 32 * dt + 8 * g + 4 * h) = w;
+          for (int e = 0; e < 4; ++e) t.v[e] = f2bf(fs.o[dt][4 * g + e] * inv_l);
+          w[dt][g] = __builtin_bit_cast(uint2, t);
         }
+      store_row16(orow, w, h);
     }
   }
 }
@@ -528,6 +547,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 __device__ __forceinline__ void store_head_row(bf16_t* __restrict__ dst, const floatx16_t (&a)[2], float sc, int h,
                                                const float* __restrict__ cosT, const float* __restrict__ sinT,
                                                int pos) {
+  uint2 w[2][4];
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     u16x4 w0, w1;
@@ -548,9 +568,10 @@ __device__ __forceinline__ void store_head_row(bf16_t* __restrict__ dst, const f
         w1.v[e] = f2bf(a[1][4 * g + e] * sc);
       }
     }
-    *reinterpret_cast<u16x4*>(dst + 8 * g + 4 * h) = w0;
-    *reinterpret_cast<u16x4*>(dst + 32 + 8 * g + 4 * h) = w1;
+    w[0][g] = __builtin_bit_cast(uint2, w0);
+    w[1][g] = __builtin_bit_cast(uint2, w1);
   }
+  store_row16(dst, w, h);
 }
 
 // ---------------------------------------------------------------- dK / dV
