@@ -574,6 +574,19 @@ __device__ __forceinline__ void store_head_row(bf16_t* __restrict__ dst, const f
   store_row16(dst, w, h);
 }
 
+// Per-wave timestamps for tools/cpp/attn_timing.cpp (only with -DDLT_ATTN_TIMING):
+// [workgroup][wave][8] shader-clock stamps written by lane 0 with vector stores.
+#ifdef DLT_ATTN_TIMING
+__device__ unsigned long long* g_attn_tim;
+#define ATTN_STAMP(slot)                                                                           \
+  do {                                                                                             \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();                                   \
+    if (lane == 0) g_attn_tim[((size_t)blockIdx.x * 2 + wid) * 8 + (slot)] = _t;                   \
+  } while (0)
+#else
+#define ATTN_STAMP(slot) ((void)0)
+#endif
+
 // ---------------------------------------------------------------- dK / dV
 // One workgroup per 128 keys (32 per wave); sweep query tiles of 64 (two 32-row
 // sub-tiles).  Accumulators: S and dP with queries in registers, keys on lanes.
@@ -652,6 +665,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, kl = lane & 31;
+  ATTN_STAMP(0);
   const int nrb = (S + RB - 1) / RB;
   int bh, pair;
   const bool lpt = work_item(nrb, xcd_map, bh, pair);
@@ -710,6 +724,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     store_rows(0);
     mw_cur = mw_next;
     __syncthreads();
+    ATTN_STAMP(1);
 
     // Tile qt_begin holds every diagonal sub-tile of the item (masked kind, fully
     // masked sub-tiles skipped); later full tiles are straight-line unmasked; a ragged
@@ -744,13 +759,20 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     int t = qt_begin;
     const int t_full = S / QSTEP;
     if (t < nqt) step(MSK{}, t++);
+    ATTN_STAMP(2);
     for (; t < t_full; ++t) step(UNM{}, t);
     for (; t < nqt; ++t) step(MSK{}, t);
+    ATTN_STAMP(3);
 
     if (ka < S) {
       store_head_row(dk + hout + (size_t)ka * out_rs, dka, scale, h, cosT, sinT, ka);
       store_head_row(dv + hout + (size_t)ka * out_rs, dva, DROP ? dscale : 1.f, h, nullptr, nullptr, 0);
     }
+#ifdef DLT_ATTN_TIMING
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ATTN_STAMP(4);
+    if (lane == 0) g_attn_tim[((size_t)blockIdx.x * 2 + wid) * 8 + 5] = (unsigned long long)(nqt - qt_begin);
+#endif
   }
 }
 
