@@ -29,10 +29,17 @@ def _namespace(mod, name):
 CPU_OPS = _namespace(reference, "reference")
 
 
+# HIP-only: the fused one-token decode step (eval/decode.py DecodeGraph)
+_HIP_ONLY = ("dec_norm_qkv", "dec_attn", "dec_gemv_res", "dec_norm_gu", "dec_norm_head", "DECODE_BATCHES")
+
+
 def hip_ops():
     from . import hip
     hip.lib()  # loud failure if the library is missing
-    return _namespace(hip, "hip")
+    ns = _namespace(hip, "hip")
+    for f in _HIP_ONLY:
+        setattr(ns, f, getattr(hip, f))
+    return ns
 
 
 def for_device(device) -> types.SimpleNamespace:

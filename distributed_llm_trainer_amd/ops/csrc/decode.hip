@@ -1,0 +1,375 @@
+// Fused one-token decode step (KV-cached generation, eval/decode.py) for gfx950.
+//
+// The reference's GPT.generate (gpt.py:457-484) re-runs the whole forward for every new
+// token.  The KV-cached decoder needs, per layer and token, five
+// GEMV-sized steps; written as ATen ops they were ~25 small kernels per layer (~200 per
+// token, launch/latency bound even inside a HIP graph: 1.8 ms per token for GPT-2 small).
+// Here each step is ONE kernel (5 per layer + the head), all of them bandwidth-shaped:
+//
+//   dec_norm_qkv    : h -> RMSNorm -> QKV GEMV -> RoPE(q, k) -> K/V cache row at `pos`, q
+//   dec_attn        : q . K[0..pos]^T -> softmax -> . V      (one workgroup per (b, head))
+//   dec_gemv_res    : h += o . Wo^T  /  h += s . Wdown^T      (residual add in fp32)
+//   dec_norm_gu     : h -> RMSNorm -> gate/up GEMV -> SwiGLU -> s
+//   dec_norm_head   : h -> RMSNorm -> lm_head GEMV -> fp32 logits
+//
+// GEMV shape: a wave computes 4 output rows at once, lanes across K (16-byte weight loads:
+// the weight stream, which dominates the bytes, is coalesced, and all 4 rows' loads are in
+// flight before any reduction), 16 rows per workgroup so even the 768-row projections
+// spread over 48+ workgroups; the B <= 8 activation rows are staged once per workgroup in
+// LDS as bf16; fp32 accumulation and a 6-step xor-shuffle reduction.  Numerics follow the eager decode path (eval/decode.py forward_cached): the
+// normed activations and every GEMV output are rounded to bf16 like torch's bf16 matmul,
+// the residual stream and softmax are fp32.  `pos` is a device scalar so the step can be
+// captured once in a HIP graph and replayed per token.
+#include "common.h"
+
+namespace {
+
+constexpr int DEC_NT = 256;  // 4 waves
+
+__device__ __forceinline__ float wave_sum64(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float bf_round(float x) { return bf2f(f2bf(x)); }
+
+__device__ __forceinline__ float norm_w(const void* w, int wbf16, int i) {
+  return wbf16 ? bf2f(reinterpret_cast<const bf16_t*>(w)[i]) : reinterpret_cast<const float*>(w)[i];
+}
+
+// xs[b][k] (bf16, LDS) = bf16(h[b][k] * rsqrt(mean(h[b]^2) + eps) * w[k]) for b < B.
+template <int B>
+__device__ void stage_normed(const float* __restrict__ h, int K, const void* w, int wbf16, float eps, bf16_t* xs,
+                             float* red) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+#pragma unroll
+  for (int b = 0; b < B; ++b) {
+    float ss = 0.f;
+    for (int k = tid; k < K; k += DEC_NT) {
+      const float x = h[(size_t)b * K + k];
+      ss += x * x;
+    }
+    ss = wave_sum64(ss);
+    if (lane == 0) red[b * 4 + wid] = ss;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int b = 0; b < B; ++b) {
+    const float rstd = rsqrtf((red[b * 4] + red[b * 4 + 1] + red[b * 4 + 2] + red[b * 4 + 3]) / (float)K + eps);
+    for (int k = tid; k < K; k += DEC_NT) xs[b * K + k] = f2bf(h[(size_t)b * K + k] * rstd * norm_w(w, wbf16, k));
+  }
+  __syncthreads();
+}
+
+// xs[b][k] = x[b][k] (bf16 global -> LDS)
+template <int B>
+__device__ void stage_copy(const bf16_t* __restrict__ x, int K, bf16_t* xs) {
+  for (int i = threadIdx.x; i < B * K; i += DEC_NT) xs[i] = x[i];
+  __syncthreads();
+}
+
+// acc[r][b] = sum_k W_r[k] * xs[b][k] for NR rows at once, the whole wave (lanes across K):
+// every row's weight loads are issued before any reduction, so a wave has NR x K/512
+// 16-byte loads in flight (one load round trip per group instead of one per row).
+template <int B, int NR>
+__device__ __forceinline__ void rows_dot(const bf16_t* const (&wrow)[NR], int K, const bf16_t* xs,
+                                         float (&acc)[NR][B]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+#pragma unroll
+    for (int b = 0; b < B; ++b) acc[r][b] = 0.f;
+  for (int c0 = 0; c0 * 8 < K; c0 += 64) {
+    const int c = c0 + lane;
+    const bool ok = c * 8 < K;
+    u16x8 wv[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+      if (ok) wv[r] = *reinterpret_cast<const u16x8*>(wrow[r] + c * 8);
+    if (ok) {
+#pragma unroll
+      for (int b = 0; b < B; ++b) {
+        const u16x8 xv = *reinterpret_cast<const u16x8*>(xs + b * K + c * 8);
+        float xf[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xf[e] = bf2f(xv.v[e]);
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[r][b] = fmaf(bf2f(wv[r].v[e]), xf[e], acc[r][b]);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+#pragma unroll
+    for (int b = 0; b < B; ++b) acc[r][b] = wave_sum64(acc[r][b]);
+}
+
+}  // namespace
+
+// grid (3 * nh * 4): workgroup g owns dims {8c..8c+7} u {8c+32..8c+39} (c = g % 4: the 8
+// NeoX RoPE pairs of a quarter head) of head (g / 4) % nh of block g / (4 nh) (0 q, 1 k,
+// 2 v) -- 16 rows, 4 per wave, one load round trip.
+template <int B>
+__global__ __launch_bounds__(DEC_NT) void k_dec_norm_qkv(const float* __restrict__ h, const void* __restrict__ lnw,
+                                                         int wbf16, float eps, const bf16_t* __restrict__ wqkv,
+                                                         const float* __restrict__ cosT, const float* __restrict__ sinT,
+                                                         const long* __restrict__ posp, bf16_t* __restrict__ qout,
+                                                         bf16_t* __restrict__ kc, bf16_t* __restrict__ vc, int H, int nh,
+                                                         int maxS) {
+  extern __shared__ __attribute__((aligned(16))) char dsm[];
+  bf16_t* xs = reinterpret_cast<bf16_t*>(dsm);                       // [B][H]
+  float* red = reinterpret_cast<float*>(dsm + (size_t)B * H * 2);     // [B][4]
+  float* outv = red + B * 4;                                          // [B][16]
+  stage_normed<B>(h, H, lnw, wbf16, eps, xs, red);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int quarter = blockIdx.x & 3, hb = blockIdx.x >> 2;
+  const int blk = hb / nh, head = hb % nh;
+  // local row l (0..15) -> head dim: l < 8 ? 8 quarter + l : 32 + 8 quarter + (l - 8)
+  auto dim_of = [&](int l) { return (l < 8 ? 0 : 32) + 8 * quarter + (l & 7); };
+  const bf16_t* rows[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) rows[r] = wqkv + (size_t)(blk * H + head * 64 + dim_of(wid * 4 + r)) * H;
+  float acc[4][B];
+  rows_dot<B, 4>(rows, H, xs, acc);
+  if (lane == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int b = 0; b < B; ++b) outv[b * 16 + wid * 4 + r] = bf_round(acc[r][b]);  // torch bf16 matmul output
+  }
+  __syncthreads();
+  const int pos = (int)posp[0];
+  if (threadIdx.x < B * 16) {
+    const int b = threadIdx.x >> 4, l = threadIdx.x & 15, d = dim_of(l);
+    float y = outv[b * 16 + l];
+    if (blk < 2) {  // NeoX RoPE on q and k: the partner of dim d is d +- 32 = local row l +- 8
+      const int j = d & 31;
+      const float c = cosT[(size_t)pos * 32 + j], sn = sinT[(size_t)pos * 32 + j];
+      const float x1 = outv[b * 16 + (l & 7)], x2 = outv[b * 16 + 8 + (l & 7)];
+      y = l < 8 ? x1 * c - x2 * sn : x2 * c + x1 * sn;
+    }
+    if (blk == 0)
+      qout[(size_t)b * H + head * 64 + d] = f2bf(y);
+    else
+      (blk == 1 ? kc : vc)[(((size_t)b * nh + head) * maxS + pos) * 64 + d] = f2bf(y);
+  }
+}
+
+// grid (B * nh): one (b, head).  q [B, H] bf16 (head-major 64-blocks), caches [B, nh, maxS, 64].
+// Scores in fp32 (lane = key), softmax over keys 0..pos, then o (lane = dim) summed across
+// the 4 waves in LDS.
+__global__ __launch_bounds__(DEC_NT) void k_dec_attn(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
+                                                     const bf16_t* __restrict__ vc, const long* __restrict__ posp,
+                                                     bf16_t* __restrict__ o, int H, int nh, int maxS, float scale) {
+  extern __shared__ __attribute__((aligned(16))) char dsm[];
+  float* sc = reinterpret_cast<float*>(dsm);       // [maxS] scores -> probabilities
+  float* red = sc + maxS;                          // [8]
+  float* oacc = red + 8;                           // [4][64]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int b = blockIdx.x / nh, head = blockIdx.x % nh;
+  const int len = (int)posp[0] + 1;
+  const bf16_t* K = kc + ((size_t)b * nh + head) * maxS * 64;
+  const bf16_t* V = vc + ((size_t)b * nh + head) * maxS * 64;
+  float qv[64];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const u16x8 t = *reinterpret_cast<const u16x8*>(q + (size_t)b * H + head * 64 + c * 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) qv[c * 8 + e] = bf2f(t.v[e]);
+  }
+  float mx = -INFINITY;
+  for (int j = tid; j < len; j += DEC_NT) {
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const u16x8 t = *reinterpret_cast<const u16x8*>(K + (size_t)j * 64 + c * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s = fmaf(qv[c * 8 + e], bf2f(t.v[e]), s);
+    }
+    s *= scale;
+    sc[j] = s;
+    mx = fmaxf(mx, s);
+  }
+#pragma unroll
+  for (int o2 = 32; o2 > 0; o2 >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o2, 64));
+  if (lane == 0) red[wid] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  float sum = 0.f;
+  for (int j = tid; j < len; j += DEC_NT) {
+    const float p = __expf(sc[j] - mx);
+    sc[j] = p;
+    sum += p;
+  }
+  sum = wave_sum64(sum);
+  __syncthreads();  // every red[] max read before it is overwritten
+  if (lane == 0) red[4 + wid] = sum;
+  __syncthreads();
+  const float inv = 1.f / (red[4] + red[5] + red[6] + red[7]);
+  // o[d] = sum_j p_j v_j[d]: lane (js, dc) = (tid / 8, tid % 8) loads dims 8dc..8dc+7 of
+  // keys j = js, js + 32, ... (16-byte loads, all in flight), then the 32 key slots are
+  // summed: 3 xor-shuffle steps inside the wave, the 4 waves through LDS.
+  const int dc = tid & 7, js = tid >> 3;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int j = js; j < len; j += DEC_NT / 8) {
+    const u16x8 t = *reinterpret_cast<const u16x8*>(V + (size_t)j * 64 + dc * 8);
+    const float p = sc[j];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = fmaf(p, bf2f(t.v[e]), acc[e]);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+#pragma unroll
+    for (int o2 = 32; o2 >= 8; o2 >>= 1) acc[e] += __shfl_xor(acc[e], o2, 64);
+  if (lane < 8) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) oacc[wid * 64 + dc * 8 + e] = acc[e];
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const float r = (oacc[tid] + oacc[64 + tid] + oacc[128 + tid] + oacc[192 + tid]) * inv;
+    o[(size_t)b * H + head * 64 + tid] = f2bf(r);
+  }
+}
+
+// h[b][r] += bf16(x[b] . W[r]) for the 16 rows of this workgroup (4 per wave, R rows total).
+template <int B>
+__global__ __launch_bounds__(DEC_NT) void k_dec_gemv_res(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+                                                         float* __restrict__ h, int R, int K) {
+  extern __shared__ __attribute__((aligned(16))) char dsm[];
+  bf16_t* xs = reinterpret_cast<bf16_t*>(dsm);
+  stage_copy<B>(x, K, xs);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r0 = blockIdx.x * 16 + wid * 4;
+  const bf16_t* rows[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) rows[r] = w + (size_t)min(r0 + r, R - 1) * K;
+  float acc[4][B];
+  rows_dot<B, 4>(rows, K, xs, acc);
+  if (lane == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (r0 + r < R) {
+#pragma unroll
+        for (int b = 0; b < B; ++b) h[(size_t)b * R + r0 + r] += bf_round(acc[r][b]);
+      }
+  }
+}
+
+// s[b][i] = bf16(silu(g) * u), g = bf16(n2 . Wgu[i]), u = bf16(n2 . Wgu[I + i]); 8 columns
+// per workgroup, 2 per wave (4 rows: gate, up of each).
+template <int B>
+__global__ __launch_bounds__(DEC_NT) void k_dec_norm_gu(const float* __restrict__ h, const void* __restrict__ lnw,
+                                                        int wbf16, float eps, const bf16_t* __restrict__ wgu,
+                                                        bf16_t* __restrict__ s, int H, int I) {
+  extern __shared__ __attribute__((aligned(16))) char dsm[];
+  bf16_t* xs = reinterpret_cast<bf16_t*>(dsm);
+  float* red = reinterpret_cast<float*>(dsm + (size_t)B * H * 2);
+  stage_normed<B>(h, H, lnw, wbf16, eps, xs, red);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int i0 = blockIdx.x * 8 + wid * 2;
+  const int ia = min(i0, I - 1), ib = min(i0 + 1, I - 1);
+  const bf16_t* rows[4] = {wgu + (size_t)ia * H, wgu + (size_t)(I + ia) * H, wgu + (size_t)ib * H,
+                           wgu + (size_t)(I + ib) * H};
+  float acc[4][B];
+  rows_dot<B, 4>(rows, H, xs, acc);
+  if (lane == 0) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+      if (i0 + c < I) {
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+          const float gb = bf_round(acc[2 * c][b]), ub = bf_round(acc[2 * c + 1][b]);
+          s[(size_t)b * I + i0 + c] = f2bf(gb / (1.f + __expf(-gb)) * ub);
+        }
+      }
+  }
+}
+
+// logits[b][r] = float(bf16(RMSNorm(h[b]) . E[r])) for r < V; 16 rows per workgroup.
+template <int B>
+__global__ __launch_bounds__(DEC_NT) void k_dec_norm_head(const float* __restrict__ h, const void* __restrict__ lnw,
+                                                          int wbf16, float eps, const bf16_t* __restrict__ emb,
+                                                          float* __restrict__ logits, int H, int V) {
+  extern __shared__ __attribute__((aligned(16))) char dsm[];
+  bf16_t* xs = reinterpret_cast<bf16_t*>(dsm);
+  float* red = reinterpret_cast<float*>(dsm + (size_t)B * H * 2);
+  stage_normed<B>(h, H, lnw, wbf16, eps, xs, red);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r0 = blockIdx.x * 16 + wid * 4;
+  const bf16_t* rows[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) rows[r] = emb + (size_t)min(r0 + r, V - 1) * H;
+  float acc[4][B];
+  rows_dot<B, 4>(rows, H, xs, acc);
+  if (lane == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (r0 + r < V) {
+#pragma unroll
+        for (int b = 0; b < B; ++b) logits[(size_t)b * V + r0 + r] = bf_round(acc[r][b]);
+      }
+  }
+}
+
+// ------------------------------------------------------------------------ launchers
+#define DEC_DISPATCH(B, CALL)          \
+  switch (B) {                         \
+    case 1: CALL(1); break;            \
+    case 2: CALL(2); break;            \
+    case 4: CALL(4); break;            \
+    case 8: CALL(8); break;            \
+    default: return -1;                \
+  }
+
+static size_t dec_lds(int B, int K) { return (size_t)B * K * 2 + (size_t)B * 4 * 4 + (size_t)B * 16 * 4; }
+
+DLT_API int dlt_dec_norm_qkv(const float* h, const void* lnw, int wbf16, float eps, const bf16_t* wqkv,
+                             const float* cosT, const float* sinT, const long* pos, bf16_t* qout, bf16_t* kc,
+                             bf16_t* vc, int B, int H, int nh, int maxS, hipStream_t st) {
+  if (H != nh * 64 || H % 8 || dec_lds(B, H) > 160 * 1024) return -1;
+#define L(BB)                                                                                                      \
+  k_dec_norm_qkv<BB><<<3 * nh * 4, DEC_NT, dec_lds(BB, H), st>>>(h, lnw, wbf16, eps, wqkv, cosT, sinT, pos, qout, kc, vc, \
+                                                             H, nh, maxS)
+  DEC_DISPATCH(B, L)
+#undef L
+  DLT_CHECK_LAUNCH();
+}
+
+DLT_API int dlt_dec_attn(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const long* pos, bf16_t* o, int B,
+                         int H, int nh, int maxS, float scale, hipStream_t st) {
+  const size_t lds = (size_t)maxS * 4 + 8 * 4 + 4 * 64 * 4;
+  if (H != nh * 64 || lds > 160 * 1024) return -1;
+  k_dec_attn<<<B * nh, DEC_NT, lds, st>>>(q, kc, vc, pos, o, H, nh, maxS, scale);
+  DLT_CHECK_LAUNCH();
+}
+
+DLT_API int dlt_dec_gemv_res(const bf16_t* x, const bf16_t* w, float* h, int B, int R, int K, hipStream_t st) {
+  if (K % 8 || (size_t)B * K * 2 > 160 * 1024) return -1;
+#define L(BB) k_dec_gemv_res<BB><<<(R + 15) / 16, DEC_NT, (size_t)BB * K * 2, st>>>(x, w, h, R, K)
+  DEC_DISPATCH(B, L)
+#undef L
+  DLT_CHECK_LAUNCH();
+}
+
+DLT_API int dlt_dec_norm_gu(const float* h, const void* lnw, int wbf16, float eps, const bf16_t* wgu, bf16_t* s,
+                            int B, int H, int I, hipStream_t st) {
+  if (H % 8 || dec_lds(B, H) > 160 * 1024) return -1;
+#define L(BB) k_dec_norm_gu<BB><<<(I + 7) / 8, DEC_NT, dec_lds(BB, H), st>>>(h, lnw, wbf16, eps, wgu, s, H, I)
+  DEC_DISPATCH(B, L)
+#undef L
+  DLT_CHECK_LAUNCH();
+}
+
+DLT_API int dlt_dec_norm_head(const float* h, const void* lnw, int wbf16, float eps, const bf16_t* emb,
+                              float* logits, int B, int H, int V, hipStream_t st) {
+  if (H % 8 || dec_lds(B, H) > 160 * 1024) return -1;
+#define L(BB) k_dec_norm_head<BB><<<(V + 15) / 16, DEC_NT, dec_lds(BB, H), st>>>(h, lnw, wbf16, eps, emb, logits, H, V)
+  DEC_DISPATCH(B, L)
+#undef L
+  DLT_CHECK_LAUNCH();
+}

@@ -67,6 +67,12 @@ _SIGS = {
                         c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_float, ctypes.c_long, c_int, c_int,
                         ctypes.c_long, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "dlt_rope_qk_inplace": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
+    "dlt_dec_norm_qkv": [c_void_p, c_void_p, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
+    "dlt_dec_attn": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p],
+    "dlt_dec_gemv_res": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
+    "dlt_dec_norm_gu": [c_void_p, c_void_p, c_int, c_float, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
+    "dlt_dec_norm_head": [c_void_p, c_void_p, c_int, c_float, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
 }
 
 
@@ -90,6 +96,75 @@ def lib():
             fn.restype = c_int
         _LIB = L
     return _LIB
+
+
+# ---------------------------------------------------------------- fused decode step
+DECODE_BATCHES = (1, 2, 4, 8)
+
+
+def _dec_w(t: torch.Tensor, name: str) -> None:
+    if t.dtype != torch.bfloat16 or not t.is_contiguous() or t.data_ptr() % 16:
+        raise ValueError(f"{name}: expected a contiguous, 16-byte aligned bf16 weight")
+
+
+def dec_norm_qkv(h, ln, eps, wqkv, cos, sin, pos, q_out, kc, vc, nh):
+    """h [B, H] fp32 -> RMSNorm -> QKV GEMV -> RoPE; k/v rows written into the caches
+    [B, nh, maxS, 64] at device position ``pos`` (int64 [1]); q (roped, bf16) into q_out."""
+    B, H = h.shape
+    _req(h, torch.float32, "dec.h", B * H)
+    w, wbf16 = _norm_weight(ln, H, "dec.ln1")
+    _dec_w(wqkv, "dec.wqkv")
+    _req(q_out, torch.bfloat16, "dec.q", B * H)
+    _req(pos, torch.int64, "dec.pos", 1)
+    maxS = kc.shape[2]
+    if kc.shape != (B, nh, maxS, 64) or vc.shape != kc.shape or wqkv.shape != (3 * H, H) or cos.shape[0] < maxS:
+        raise ValueError("dec_norm_qkv: shape mismatch")
+    _chk(lib().dlt_dec_norm_qkv(_p(h), _p(w), wbf16, float(eps), _p(wqkv), _p(cos), _p(sin), _p(pos), _p(q_out),
+                                _p(kc), _p(vc), B, H, nh, maxS, _stream()), "dec_norm_qkv")
+
+
+def dec_attn(q, kc, vc, pos, o_out, scale):
+    B, nh, maxS, hd = kc.shape
+    H = nh * hd
+    _req(q, torch.bfloat16, "dec.q", B * H)
+    _req(o_out, torch.bfloat16, "dec.o", B * H)
+    _chk(lib().dlt_dec_attn(_p(q), _p(kc), _p(vc), _p(pos), _p(o_out), B, H, nh, maxS, float(scale), _stream()),
+         "dec_attn")
+
+
+def dec_gemv_res(x, w, h):
+    """h += bf16(x @ w^T) (fp32 residual); x [B, K] bf16, w [R, K] bf16, h [B, R] fp32."""
+    B, K = x.shape
+    R = w.shape[0]
+    _req(x, torch.bfloat16, "dec.x", B * K)
+    _dec_w(w, "dec.w")
+    _req(h, torch.float32, "dec.h", B * R)
+    if w.shape[1] != K:
+        raise ValueError("dec_gemv_res: shape mismatch")
+    _chk(lib().dlt_dec_gemv_res(_p(x), _p(w), _p(h), B, R, K, _stream()), "dec_gemv_res")
+
+
+def dec_norm_gu(h, ln, eps, wgu, s_out):
+    B, H = h.shape
+    I = wgu.shape[0] // 2
+    _req(h, torch.float32, "dec.h", B * H)
+    w, wbf16 = _norm_weight(ln, H, "dec.ln2")
+    _dec_w(wgu, "dec.wgu")
+    _req(s_out, torch.bfloat16, "dec.s", B * I)
+    _chk(lib().dlt_dec_norm_gu(_p(h), _p(w), wbf16, float(eps), _p(wgu), _p(s_out), B, H, I, _stream()),
+         "dec_norm_gu")
+
+
+def dec_norm_head(h, ln, eps, emb, logits, V):
+    B, H = h.shape
+    _req(h, torch.float32, "dec.h", B * H)
+    w, wbf16 = _norm_weight(ln, H, "dec.norm")
+    _dec_w(emb, "dec.lm_head")
+    _req(logits, torch.float32, "dec.logits", B * V)
+    if emb.shape[0] < V or emb.shape[1] != H:
+        raise ValueError("dec_norm_head: shape mismatch")
+    _chk(lib().dlt_dec_norm_head(_p(h), _p(w), wbf16, float(eps), _p(emb), _p(logits), B, H, V, _stream()),
+         "dec_norm_head")
 
 
 def _p(t: Optional[torch.Tensor]):

@@ -233,3 +233,33 @@ def test_fsdp_sharded_checkpoint_gpu(tmp_path):
     l2 = tr2.train_step({"input_ids": data})["loss"]
     assert abs(l1 - l2) <= 1e-6 * abs(l1), (l1, l2)
     assert (tr.runtime.master_flat - tr2.runtime.master_flat).abs().max().item() < 1e-5
+
+
+@pytest.mark.parametrize("B", [1, 4])
+def test_decode_fused_kernels_match_torch_step(B, monkeypatch):
+    """The fused HIP decode step (ops/csrc/decode.hip: 5 kernels per layer) == the ATen
+    decode step: logits and the K/V cache rows it appends, over a 150-token context."""
+    from distributed_llm_trainer_amd.eval.decode import DecodeGraph, KVCache, forward_cached
+    torch.manual_seed(5)
+    m = GPT(_cfg(0.0)).to(DEV)
+    m.enable_engine()
+    m.eval()
+    cfg = m.config
+    ids = torch.randint(0, 1000, (B, 150), device=DEV)
+    steps = torch.randint(0, 1000, (B, 5), device=DEV)
+    caches = [KVCache(cfg, B, DEV, m.engine.act_dtype) for _ in range(2)]
+    graphs = []
+    with torch.no_grad():
+        for c, fused in zip(caches, ("1", "0")):
+            forward_cached(m, ids, c)
+            monkeypatch.setenv("DLT_DECODE_FUSED", fused)
+            graphs.append(DecodeGraph(m, c, c.len))
+        assert graphs[0].fused and not graphs[1].fused
+        for t in range(steps.shape[1]):
+            a = graphs[0](steps[:, t:t + 1]).clone()
+            b = graphs[1](steps[:, t:t + 1]).clone()
+            assert torch.allclose(a, b, atol=3e-2, rtol=3e-2), (t, (a - b).abs().max().item())
+            pos = caches[0].len - 1
+            for i in range(cfg.num_layers):
+                for x, y in ((caches[0].k[i], caches[1].k[i]), (caches[0].v[i], caches[1].v[i])):
+                    assert torch.allclose(x[:, :, pos].float(), y[:, :, pos].float(), atol=2e-2, rtol=2e-2)
