@@ -39,66 +39,119 @@ __device__ __forceinline__ float norm_w(const void* w, int wbf16, int i) {
 }
 
 // xs[b][k] (bf16, LDS) = bf16(h[b][k] * rsqrt(mean(h[b]^2) + eps) * w[k]) for b < B.
+// float4 loads, every row's loads issued before the reductions (the per-element loop
+// was a chain of dependent round trips: most of a kernel's time).
 template <int B>
 __device__ void stage_normed(const float* __restrict__ h, int K, const void* w, int wbf16, float eps, bf16_t* xs,
                              float* red) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nch = K >> 2;  // float4 chunks per row (K % 8 == 0)
+  float ss[B];
 #pragma unroll
   for (int b = 0; b < B; ++b) {
-    float ss = 0.f;
-    for (int k = tid; k < K; k += DEC_NT) {
-      const float x = h[(size_t)b * K + k];
-      ss += x * x;
+    ss[b] = 0.f;
+#pragma unroll 2
+    for (int c = tid; c < nch; c += DEC_NT) {
+      const float4 x = *reinterpret_cast<const float4*>(h + (size_t)b * K + 4 * c);
+      ss[b] += x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
     }
-    ss = wave_sum64(ss);
-    if (lane == 0) red[b * 4 + wid] = ss;
+  }
+#pragma unroll
+  for (int b = 0; b < B; ++b) {
+    const float t = wave_sum64(ss[b]);
+    if (lane == 0) red[b * 4 + wid] = t;
   }
   __syncthreads();
 #pragma unroll
   for (int b = 0; b < B; ++b) {
     const float rstd = rsqrtf((red[b * 4] + red[b * 4 + 1] + red[b * 4 + 2] + red[b * 4 + 3]) / (float)K + eps);
-    for (int k = tid; k < K; k += DEC_NT) xs[b * K + k] = f2bf(h[(size_t)b * K + k] * rstd * norm_w(w, wbf16, k));
+#pragma unroll 2
+    for (int c = tid; c < nch; c += DEC_NT) {
+      const float4 x = *reinterpret_cast<const float4*>(h + (size_t)b * K + 4 * c);
+      u16x4 y;
+      y.v[0] = f2bf(x.x * rstd * norm_w(w, wbf16, 4 * c));
+      y.v[1] = f2bf(x.y * rstd * norm_w(w, wbf16, 4 * c + 1));
+      y.v[2] = f2bf(x.z * rstd * norm_w(w, wbf16, 4 * c + 2));
+      y.v[3] = f2bf(x.w * rstd * norm_w(w, wbf16, 4 * c + 3));
+      *reinterpret_cast<u16x4*>(xs + b * K + 4 * c) = y;
+    }
   }
   __syncthreads();
 }
 
-// xs[b][k] = x[b][k] (bf16 global -> LDS)
+// xs[b][k] = x[b][k] (bf16 global -> LDS), 16-byte chunks, unrolled so the loads overlap
 template <int B>
 __device__ void stage_copy(const bf16_t* __restrict__ x, int K, bf16_t* xs) {
-  for (int i = threadIdx.x; i < B * K; i += DEC_NT) xs[i] = x[i];
+  const int n = B * K / 8;
+#pragma unroll 4
+  for (int c = threadIdx.x; c < n; c += DEC_NT)
+    *reinterpret_cast<u16x8*>(xs + 8 * c) = *reinterpret_cast<const u16x8*>(x + 8 * c);
   __syncthreads();
 }
 
 // acc[r][b] = sum_k W_r[k] * xs[b][k] for NR rows at once, the whole wave (lanes across K):
 // every row's weight loads are issued before any reduction, so a wave has NR x K/512
-// 16-byte loads in flight (one load round trip per group instead of one per row).
+// 16-byte loads in flight (one load round trip per group instead of one per row).  The
+// first PRE 512-element slices of every row are loaded by rows_pre() BEFORE the workgroup
+// stages its activations, so the weight stream's HBM latency overlaps the staging.
+template <int NR, int PRE>
+struct RowsPre {
+  u16x8 wv[NR][PRE];
+};
+
+template <int NR, int PRE>
+__device__ __forceinline__ void rows_pre(const bf16_t* const (&wrow)[NR], int K, RowsPre<NR, PRE>& pre) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < PRE; ++i) {
+    const int c = i * 64 + lane;
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+      if (c * 8 < K) pre.wv[r][i] = *reinterpret_cast<const u16x8*>(wrow[r] + c * 8);
+  }
+}
+
 template <int B, int NR>
+__device__ __forceinline__ void fma_slice(const u16x8 (&wv)[NR], const bf16_t* xs, int K, int c, float (&acc)[NR][B]) {
+#pragma unroll
+  for (int b = 0; b < B; ++b) {
+    const u16x8 xv = *reinterpret_cast<const u16x8*>(xs + b * K + c * 8);
+    float xf[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) xf[e] = bf2f(xv.v[e]);
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[r][b] = fmaf(bf2f(wv[r].v[e]), xf[e], acc[r][b]);
+  }
+}
+
+template <int B, int NR, int PRE>
 __device__ __forceinline__ void rows_dot(const bf16_t* const (&wrow)[NR], int K, const bf16_t* xs,
-                                         float (&acc)[NR][B]) {
+                                         const RowsPre<NR, PRE>& pre, float (&acc)[NR][B]) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int r = 0; r < NR; ++r)
 #pragma unroll
     for (int b = 0; b < B; ++b) acc[r][b] = 0.f;
-  for (int c0 = 0; c0 * 8 < K; c0 += 64) {
+#pragma unroll
+  for (int i = 0; i < PRE; ++i) {
+    const int c = i * 64 + lane;
+    if (c * 8 < K) {
+      u16x8 wv[NR];
+#pragma unroll
+      for (int r = 0; r < NR; ++r) wv[r] = pre.wv[r][i];
+      fma_slice<B, NR>(wv, xs, K, c, acc);
+    }
+  }
+#pragma unroll 4
+  for (int c0 = PRE * 64; c0 * 8 < K; c0 += 64) {
     const int c = c0 + lane;
-    const bool ok = c * 8 < K;
-    u16x8 wv[NR];
+    if (c * 8 < K) {
+      u16x8 wv[NR];
 #pragma unroll
-    for (int r = 0; r < NR; ++r)
-      if (ok) wv[r] = *reinterpret_cast<const u16x8*>(wrow[r] + c * 8);
-    if (ok) {
-#pragma unroll
-      for (int b = 0; b < B; ++b) {
-        const u16x8 xv = *reinterpret_cast<const u16x8*>(xs + b * K + c * 8);
-        float xf[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) xf[e] = bf2f(xv.v[e]);
-#pragma unroll
-        for (int r = 0; r < NR; ++r)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) acc[r][b] = fmaf(bf2f(wv[r].v[e]), xf[e], acc[r][b]);
-      }
+      for (int r = 0; r < NR; ++r) wv[r] = *reinterpret_cast<const u16x8*>(wrow[r] + c * 8);
+      fma_slice<B, NR>(wv, xs, K, c, acc);
     }
   }
 #pragma unroll
@@ -123,7 +176,6 @@ __global__ __launch_bounds__(DEC_NT) void k_dec_norm_qkv(const float* __restrict
   bf16_t* xs = reinterpret_cast<bf16_t*>(dsm);                       // [B][H]
   float* red = reinterpret_cast<float*>(dsm + (size_t)B * H * 2);     // [B][4]
   float* outv = red + B * 4;                                          // [B][16]
-  stage_normed<B>(h, H, lnw, wbf16, eps, xs, red);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int quarter = blockIdx.x & 3, hb = blockIdx.x >> 2;
   const int blk = hb / nh, head = hb % nh;
@@ -132,8 +184,11 @@ __global__ __launch_bounds__(DEC_NT) void k_dec_norm_qkv(const float* __restrict
   const bf16_t* rows[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) rows[r] = wqkv + (size_t)(blk * H + head * 64 + dim_of(wid * 4 + r)) * H;
+  RowsPre<4, 2> pre;
+  rows_pre<4, 2>(rows, H, pre);
+  stage_normed<B>(h, H, lnw, wbf16, eps, xs, red);
   float acc[4][B];
-  rows_dot<B, 4>(rows, H, xs, acc);
+  rows_dot<B, 4, 2>(rows, H, xs, pre, acc);
   if (lane == 0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -242,14 +297,16 @@ __global__ __launch_bounds__(DEC_NT) void k_dec_gemv_res(const bf16_t* __restric
                                                          float* __restrict__ h, int R, int K) {
   extern __shared__ __attribute__((aligned(16))) char dsm[];
   bf16_t* xs = reinterpret_cast<bf16_t*>(dsm);
-  stage_copy<B>(x, K, xs);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int r0 = blockIdx.x * 16 + wid * 4;
   const bf16_t* rows[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) rows[r] = w + (size_t)min(r0 + r, R - 1) * K;
+  RowsPre<4, 4> pre;
+  rows_pre<4, 4>(rows, K, pre);
+  stage_copy<B>(x, K, xs);
   float acc[4][B];
-  rows_dot<B, 4>(rows, K, xs, acc);
+  rows_dot<B, 4, 4>(rows, K, xs, pre, acc);
   if (lane == 0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -269,14 +326,16 @@ __global__ __launch_bounds__(DEC_NT) void k_dec_norm_gu(const float* __restrict_
   extern __shared__ __attribute__((aligned(16))) char dsm[];
   bf16_t* xs = reinterpret_cast<bf16_t*>(dsm);
   float* red = reinterpret_cast<float*>(dsm + (size_t)B * H * 2);
-  stage_normed<B>(h, H, lnw, wbf16, eps, xs, red);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int i0 = blockIdx.x * 8 + wid * 2;
   const int ia = min(i0, I - 1), ib = min(i0 + 1, I - 1);
   const bf16_t* rows[4] = {wgu + (size_t)ia * H, wgu + (size_t)(I + ia) * H, wgu + (size_t)ib * H,
                            wgu + (size_t)(I + ib) * H};
+  RowsPre<4, 2> pre;
+  rows_pre<4, 2>(rows, H, pre);
+  stage_normed<B>(h, H, lnw, wbf16, eps, xs, red);
   float acc[4][B];
-  rows_dot<B, 4>(rows, H, xs, acc);
+  rows_dot<B, 4, 2>(rows, H, xs, pre, acc);
   if (lane == 0) {
 #pragma unroll
     for (int c = 0; c < 2; ++c)
@@ -298,14 +357,16 @@ __global__ __launch_bounds__(DEC_NT) void k_dec_norm_head(const float* __restric
   extern __shared__ __attribute__((aligned(16))) char dsm[];
   bf16_t* xs = reinterpret_cast<bf16_t*>(dsm);
   float* red = reinterpret_cast<float*>(dsm + (size_t)B * H * 2);
-  stage_normed<B>(h, H, lnw, wbf16, eps, xs, red);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int r0 = blockIdx.x * 16 + wid * 4;
   const bf16_t* rows[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) rows[r] = emb + (size_t)min(r0 + r, V - 1) * H;
+  RowsPre<4, 2> pre;
+  rows_pre<4, 2>(rows, H, pre);
+  stage_normed<B>(h, H, lnw, wbf16, eps, xs, red);
   float acc[4][B];
-  rows_dot<B, 4>(rows, H, xs, acc);
+  rows_dot<B, 4, 2>(rows, H, xs, pre, acc);
   if (lane == 0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
