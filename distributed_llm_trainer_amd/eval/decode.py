@@ -106,7 +106,11 @@ class DecodeGraph:
     single-process parameter store (FSDP gathers are collectives: not captured).
     """
 
-    def __init__(self, model, cache: KVCache, pos: int):
+    def __init__(self, model, cache: KVCache, pos: int, sample: Optional[dict] = None):
+        """``sample`` (fused step only): dict(temperature, top_k, seed, hist, hist_base) --
+        the graph then also draws the next token (ops ``dec_sample``) into ``self.ids`` and
+        ``hist`` and advances the device position, so generation is one replay per token
+        with no host round trip."""
         self.model, self.cache = model, cache
         cfg = model.config
         dev = cache.k[0].device
@@ -115,9 +119,7 @@ class DecodeGraph:
         self.pos = torch.full((1,), pos, dtype=torch.long, device=dev)
         self.kpos = torch.arange(cfg.max_seq_len, device=dev)
         # fused HIP step (ops/csrc/decode.hip): 5 kernels per layer instead of ~25 ATen ops
-        ops = model.engine.ops
-        self.fused = (hasattr(ops, "dec_norm_qkv") and B in getattr(ops, "DECODE_BATCHES", ())
-                      and cfg.head_dim == 64 and os.environ.get("DLT_DECODE_FUSED", "1") != "0")
+        self.fused = _fused_ok(model, B)
         if self.fused:
             H, I = cfg.hidden_size, cfg.intermediate_size
             self.h = torch.empty(B, H, dtype=torch.float32, device=dev)
@@ -125,6 +127,7 @@ class DecodeGraph:
             self.ob = torch.empty(B, H, dtype=torch.bfloat16, device=dev)
             self.sb = torch.empty(B, I, dtype=torch.bfloat16, device=dev)
             self.lg = torch.empty(B, cfg.vocab_size, dtype=torch.float32, device=dev)
+        self.sample = sample if self.fused else None
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):  # warm up allocations / library plans outside the capture
@@ -134,6 +137,7 @@ class DecodeGraph:
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.logits = self._step()
+        self.pos.fill_(pos)  # the warm-up steps advanced it (sampling graph)
 
     def _step_fused(self) -> torch.Tensor:
         model, cache = self.model, self.cache
@@ -152,6 +156,11 @@ class DecodeGraph:
             ops.dec_norm_gu(self.h, w.ln2, eng.eps, w.wgu, self.sb)
             ops.dec_gemv_res(self.sb, w.wdown, self.h)
         ops.dec_norm_head(self.h, hw.norm, eng.eps, hw.lm_head, self.lg, cfg.vocab_size)
+        if self.sample is not None:
+            sm = self.sample
+            ops.dec_sample(self.lg, sm["temperature"], sm["top_k"], sm["seed"], self.pos, self.ids, sm["hist"],
+                           sm["hist_base"])
+            ops.dec_advance(self.pos)
         return self.lg
 
     def _step(self) -> torch.Tensor:
@@ -199,11 +208,23 @@ class DecodeGraph:
         return self.logits
 
 
+def _fused_ok(model, B: int) -> bool:
+    """The fused HIP decode step applies: HIP ops, a supported batch, head_dim 64."""
+    ops = model.engine.ops
+    return (hasattr(ops, "dec_norm_qkv") and B in getattr(ops, "DECODE_BATCHES", ())
+            and model.config.head_dim == 64 and os.environ.get("DLT_DECODE_FUSED", "1") != "0")
+
+
 def _graph_ok(model, device) -> bool:
     import os
     from ..parallel.flat import FlatParamStore
     return (device.type == "cuda" and os.environ.get("DLT_DECODE_GRAPH", "1") != "0"
             and isinstance(model.engine.provider, FlatParamStore))
+
+
+def _reset(cache: KVCache) -> KVCache:
+    cache.len = 0
+    return cache
 
 
 @torch.no_grad()
@@ -215,9 +236,34 @@ def kv_cached_generate(model, input_ids: torch.Tensor, max_new_tokens: int = 100
     cache = KVCache(cfg, B, input_ids.device, eng.act_dtype)
     ctx = input_ids[:, -cfg.max_seq_len:]
     logits = forward_cached(model, ctx, cache)
+    out = input_ids
+    n_dev = min(max_new_tokens - 1, cfg.max_seq_len - cache.len)
+    if (n_dev > 0 and temperature > 0 and _graph_ok(model, input_ids.device) and _fused_ok(model, B)
+            and os.environ.get("DLT_DECODE_DEVICE_LOOP", "1") != "0"):
+        # first token from the prefill logits (ATen sampling), then one graph replay per
+        # token: the fused step samples on the device and feeds itself (no host round trip)
+        lg = logits / temperature
+        if top_k > 0:
+            v, _ = torch.topk(lg, min(top_k, lg.size(-1)))
+            lg = lg.masked_fill(lg < v[:, [-1]], float("-inf"))
+        nxt = torch.multinomial(F.softmax(lg, dim=-1), num_samples=1)
+        hist = torch.empty(B, n_dev, dtype=torch.long, device=input_ids.device)
+        seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())  # torch's generator: manual_seed reproducible
+        graph = DecodeGraph(model, cache, cache.len,
+                            sample=dict(temperature=float(temperature), top_k=int(top_k), seed=seed, hist=hist,
+                                        hist_base=cache.len + 1))
+        graph.ids.copy_(nxt)
+        for _ in range(n_dev):
+            graph.graph.replay()
+        cache.len += n_dev
+        out = torch.cat([out, nxt, hist], dim=1)
+        if n_dev == max_new_tokens - 1:
+            return out
+        # context window full: continue on the host path (re-prefill cropping)
+        logits = forward_cached(model, out[:, -cfg.max_seq_len:], _reset(cache))
+        max_new_tokens -= n_dev + 1
     graph = DecodeGraph(model, cache, cache.len) if (_graph_ok(model, input_ids.device)
                                                     and cache.len < cfg.max_seq_len and max_new_tokens > 1) else None
-    out = input_ids
     for step in range(max_new_tokens):
         lg = logits / temperature
         if top_k > 0:

@@ -377,6 +377,215 @@ __global__ __launch_bounds__(DEC_NT) void k_dec_norm_head(const float* __restric
   }
 }
 
+// ---------------------------------------------------------------- top-k sampling
+// GPT.generate's sampling step (gpt.py:474-482): logits / temperature, keep the values >=
+// the k-th largest (ties kept, as masked_fill(lg < v[:, [-1]], -inf) does), softmax,
+// one multinomial draw -- one row per workgroup of 512 threads (the row is re-read from L2
+// by every pass: ~200 KB per row).  The k-th largest is found by a
+// radix select on order-preserving uint32 keys (12 + 12 + 8 bits, LDS histograms, block
+// suffix scans); the draw inverts the cumulative sum of exp(x - max) over the kept values
+// with a counter-hash uniform of (seed, position, row).  The sampled id
+// is written into the next step's input and into the generated-token history, so the
+// whole generate loop runs on the device (one graph replay per token).
+constexpr int SMP_NT = 512;
+
+__device__ __forceinline__ uint32_t f2key(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key2f(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+
+// exclusive prefix sum over the block (SMP_NT threads) of v; returns it, total in *tot
+__device__ __forceinline__ float block_excl_scan(float v, float* scr, float* tot) {
+  constexpr int NW = SMP_NT / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  float incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) scr[wid] = incl;
+  __syncthreads();
+  if (tid == 0) {
+    float a = 0.f;
+    for (int w = 0; w < NW; ++w) {  // inclusive per-wave prefix
+      a += scr[w];
+      scr[16 + w] = a;
+    }
+  }
+  __syncthreads();
+  const float base = wid ? scr[16 + wid - 1] : 0.f;
+  *tot = scr[16 + NW - 1];
+  __syncthreads();
+  return base + incl - v;
+}
+
+// The k-th largest key of the row (k >= 1): radix select over bit fields [31:20], [19:8],
+// [7:0]; key_at(j) returns this thread's j-th key (j < C), re-read from L2 each pass.
+template <typename KeyAt>
+__device__ uint32_t kth_key(KeyAt key_at, int C, int k, uint32_t* hist, float* scr, int* sel) {
+  const int tid = threadIdx.x;
+  uint32_t prefix = 0, pmask = 0;
+  const int shifts[3] = {20, 8, 0}, widths[3] = {12, 12, 8};
+#pragma unroll
+  for (int ps = 0; ps < 3; ++ps) {
+    const int sh = shifts[ps], nb = 1 << widths[ps];
+    for (int i = tid; i < nb; i += SMP_NT) hist[i] = 0;
+    __syncthreads();
+#pragma unroll 4
+    for (int j = 0; j < C; ++j) {
+      const uint32_t kj = key_at(j);
+      if ((kj & pmask) == prefix) atomicAdd(&hist[(kj >> sh) & (nb - 1)], 1u);
+    }
+    __syncthreads();
+    // counts in descending-bin order: thread t owns reversed bins [8t, 8t + 8)
+    float c[8], own = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int r = 8 * tid + q;
+      c[q] = r < nb ? (float)hist[nb - 1 - r] : 0.f;
+      own += c[q];
+    }
+    float total;
+    float before = block_excl_scan(own, scr, &total);  // keys in higher bins than this thread's
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int r = 8 * tid + q;
+      if (r < nb && before < (float)k && (float)k <= before + c[q]) {
+        sel[0] = nb - 1 - r;
+        sel[1] = k - (int)before;
+      }
+      before += c[q];
+    }
+    __syncthreads();
+    prefix |= (uint32_t)sel[0] << sh;
+    pmask |= (uint32_t)(nb - 1) << sh;
+    k = sel[1];
+    __syncthreads();
+  }
+  return prefix;
+}
+
+__global__ __launch_bounds__(SMP_NT) void k_dec_sample(const float* __restrict__ logits, int V, float temperature,
+                                                       int top_k, uint32_t seed, const long* __restrict__ posp,
+                                                       long* __restrict__ ids, long* __restrict__ hist, int hist_len,
+                                                       int hist_base) {
+  __shared__ uint32_t bins[4096];
+  __shared__ float scr[40];
+  __shared__ int sel[2];
+  const int tid = threadIdx.x, b = blockIdx.x;
+  // Thread t owns the elements i = t + SMP_NT * j (coalesced loads).  The draw inverts the
+  // cumulative sum in (thread, j) order -- any fixed order of the elements samples the
+  // same distribution.
+  const int C = (V + SMP_NT - 1) / SMP_NT;
+  const float* row = logits + (size_t)b * V;
+  auto idx_of = [&](int j) { return tid + SMP_NT * j; };
+  auto x_at = [&](int j) { const int i = idx_of(j); return i < V ? row[i] / temperature : -INFINITY; };
+  auto key_at = [&](int j) { return f2key(x_at(j)); };
+  float mx = -INFINITY;
+#pragma unroll 4
+  for (int j = 0; j < C; ++j) mx = fmaxf(mx, x_at(j));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  if ((tid & 63) == 0) scr[tid >> 6] = mx;
+  __syncthreads();
+  mx = scr[0];
+  for (int w = 1; w < SMP_NT / 64; ++w) mx = fmaxf(mx, scr[w]);
+  __syncthreads();
+  uint32_t thr = f2key(-INFINITY) + 1;  // keep every finite value
+  if (top_k > 0 && top_k < V) {
+    // Fast path: bracket the k-th largest with a value window below the max (count-only
+    // passes, no atomics), collect the <= NCAND candidates into LDS and rank them there.
+    // The radix select (LDS histograms) is the fallback for flat / tied distributions.
+    constexpr int NCAND = 1024;
+    uint32_t* cand = bins;  // reuse the histogram LDS
+    float d = 4.f;
+    int cnt = 0;
+    bool ok = false;
+    for (int it = 0; it < 8 && !ok; ++it) {
+      const float t = mx - d;
+      float own_c = 0.f;
+#pragma unroll 4
+      for (int j = 0; j < C; ++j) own_c += x_at(j) >= t ? 1.f : 0.f;
+      float tot;
+      (void)block_excl_scan(own_c, scr, &tot);
+      cnt = (int)tot;
+      if (cnt < top_k) d *= 2.f;
+      else if (cnt > NCAND) d *= 0.5f;
+      else ok = true;
+    }
+    if (ok) {
+      const float t = mx - d;
+      if (tid == 0) sel[0] = 0;
+      __syncthreads();
+#pragma unroll 4
+      for (int j = 0; j < C; ++j) {
+        const float x = x_at(j);
+        if (x >= t) cand[atomicAdd(&sel[0], 1)] = f2key(x);
+      }
+      __syncthreads();
+      // rank: the k-th largest candidate c has #{> c} < k <= #{>= c}
+      for (int i = tid; i < cnt; i += SMP_NT) {
+        const uint32_t ci = cand[i];
+        int gt = 0, ge = 0;
+        for (int m = 0; m < cnt; ++m) {
+          const uint32_t cm = cand[m];
+          gt += cm > ci;
+          ge += cm >= ci;
+        }
+        if (gt < top_k && top_k <= ge) sel[1] = (int)ci;
+      }
+      __syncthreads();
+      thr = max(thr, (uint32_t)sel[1]);
+      __syncthreads();
+    } else {
+      thr = max(thr, kth_key(key_at, C, top_k, bins, scr, sel));
+    }
+  }
+  float own = 0.f;
+#pragma unroll 4
+  for (int j = 0; j < C; ++j) {
+    const float x = x_at(j);
+    if (f2key(x) >= thr) own += __expf(x - mx);
+  }
+  float total;
+  const float before = block_excl_scan(own, scr, &total);
+  const long pos = posp[0];
+  const uint32_t h = lowbias32(seed ^ lowbias32((uint32_t)pos * 0x9E3779B9u + (uint32_t)b));
+  const float u = ((h >> 8) + 0.5f) * (1.f / 16777216.f) * total;  // (0, total)
+  if (tid == 0) sel[0] = -1;
+  __syncthreads();
+  if (own > 0.f && before <= u && u < before + own) {
+    float cum = before;
+    int pick = -1, last = -1;
+    for (int j = 0; j < C; ++j) {
+      const float x = x_at(j);
+      if (f2key(x) >= thr) {
+        cum += __expf(x - mx);
+        last = idx_of(j);
+        if (u < cum) {
+          pick = idx_of(j);
+          break;
+        }
+      }
+    }
+    sel[0] = pick >= 0 ? pick : last;  // rounding at the slice end: its last kept value
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int pick = sel[0];
+    if (pick < 0) pick = 0;  // unreachable unless every probability underflowed
+    ids[b] = pick;
+    const long t = pos + 1 - hist_base;  // the token that will sit at position pos + 1
+    if (t >= 0 && t < hist_len) hist[(size_t)b * hist_len + t] = pick;
+  }
+}
+
+__global__ void k_dec_advance(long* pos) { pos[0] += 1; }
+
 // ------------------------------------------------------------------------ launchers
 #define DEC_DISPATCH(B, CALL)          \
   switch (B) {                         \
@@ -432,5 +641,18 @@ DLT_API int dlt_dec_norm_head(const float* h, const void* lnw, int wbf16, float 
 #define L(BB) k_dec_norm_head<BB><<<(V + 15) / 16, DEC_NT, dec_lds(BB, H), st>>>(h, lnw, wbf16, eps, emb, logits, H, V)
   DEC_DISPATCH(B, L)
 #undef L
+  DLT_CHECK_LAUNCH();
+}
+
+// ids [B] (int64, the next step's input), hist [B, hist_len]: hist[b][pos + 1 - hist_base] = sampled id
+DLT_API int dlt_dec_sample(const float* logits, int B, int V, float temperature, int top_k, uint32_t seed,
+                           const long* pos, long* ids, long* hist, int hist_len, int hist_base, hipStream_t st) {
+  if (V <= 0 || temperature <= 0.f) return -1;
+  k_dec_sample<<<B, SMP_NT, 0, st>>>(logits, V, temperature, top_k, seed, pos, ids, hist, hist_len, hist_base);
+  DLT_CHECK_LAUNCH();
+}
+
+DLT_API int dlt_dec_advance(long* pos, hipStream_t st) {
+  k_dec_advance<<<1, 1, 0, st>>>(pos);
   DLT_CHECK_LAUNCH();
 }

@@ -73,6 +73,9 @@ _SIGS = {
     "dlt_dec_gemv_res": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "dlt_dec_norm_gu": [c_void_p, c_void_p, c_int, c_float, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "dlt_dec_norm_head": [c_void_p, c_void_p, c_int, c_float, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
+    "dlt_dec_sample": [c_void_p, c_int, c_int, c_float, c_int, c_uint32, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                       c_void_p],
+    "dlt_dec_advance": [c_void_p, c_void_p],
 }
 
 
@@ -165,6 +168,26 @@ def dec_norm_head(h, ln, eps, emb, logits, V):
         raise ValueError("dec_norm_head: shape mismatch")
     _chk(lib().dlt_dec_norm_head(_p(h), _p(w), wbf16, float(eps), _p(emb), _p(logits), B, H, V, _stream()),
          "dec_norm_head")
+
+
+def dec_sample(logits, temperature, top_k, seed, pos, ids, hist, hist_base):
+    """One top-k multinomial draw per row of ``logits`` [B, V] (fp32) on the device: the
+    id goes to ``ids`` (B int64, the next decode step's input) and to
+    ``hist[b, pos + 1 - hist_base]`` (int64 [B, L]) when inside the history."""
+    B, V = logits.shape
+    _req(logits, torch.float32, "dec.logits", B * V)
+    _req(pos, torch.int64, "dec.pos", 1)
+    _req(ids, torch.int64, "dec.ids", B)
+    _req(hist, torch.int64, "dec.hist")
+    if hist.dim() != 2 or hist.shape[0] != B:
+        raise ValueError("dec_sample: hist must be [B, L]")
+    _chk(lib().dlt_dec_sample(_p(logits), B, V, float(temperature), int(top_k), int(seed) & 0xFFFFFFFF, _p(pos),
+                              _p(ids), _p(hist), hist.shape[1], int(hist_base), _stream()), "dec_sample")
+
+
+def dec_advance(pos):
+    _req(pos, torch.int64, "dec.pos", 1)
+    _chk(lib().dlt_dec_advance(_p(pos), _stream()), "dec_advance")
 
 
 def _p(t: Optional[torch.Tensor]):

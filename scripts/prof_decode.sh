@@ -10,7 +10,7 @@ f=$(find gpurun_out/prof_dec -name "*kernel_stats.csv" | head -1)
 python3 -c "
 import csv
 rows=sorted(csv.DictReader(open('$f')), key=lambda r: -float(r['TotalDurationNs']))
-for r in rows[:16]: print('%-60s calls %6s avg %7.2f us' % (r['Name'][:60], r['Calls'], float(r['AverageNs'])/1e3))
+for r in rows[:24]: print('%-60s calls %6s avg %7.2f us' % (r['Name'][:60], r['Calls'], float(r['AverageNs'])/1e3))
 "
 f=$(find gpurun_out/prof_dec -name "*kernel_trace.csv" | head -1)
 python3 -c "

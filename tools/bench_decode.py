@@ -16,15 +16,16 @@ torch.manual_seed(0)
 m = GPT(GPTConfig.from_preset(size)).to("cuda")
 m.enable_engine()
 ids = torch.randint(0, 50257, (B, 32), device="cuda")
-for mode in ("0", "1"):
-    os.environ["DLT_DECODE_GRAPH"] = mode
+for mode, graph, loop in (("eager", "0", "0"), ("graph, host sampling", "1", "0"), ("graph, device loop", "1", "1")):
+    os.environ["DLT_DECODE_GRAPH"] = graph
+    os.environ["DLT_DECODE_DEVICE_LOOP"] = loop
     m.generate(ids, max_new_tokens=8)
     torch.cuda.synchronize()
     t = time.perf_counter()
     m.generate(ids, max_new_tokens=N)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t
-    print(f"{size} B={B} graph={mode}: {N / dt:.1f} steps/s, {B * N / dt:.1f} tokens/s ({dt / N * 1e3:.2f} ms/token)",
+    print(f"{size} B={B} {mode}: {N / dt:.1f} steps/s, {B * N / dt:.1f} tokens/s ({dt / N * 1e3:.2f} ms/token)",
           flush=True)
 
 # replay-only cost of the captured step (no sampling / Python in the loop)
