@@ -128,6 +128,8 @@ class DecodeGraph:
             self.sb = torch.empty(B, I, dtype=torch.bfloat16, device=dev)
             self.lg = torch.empty(B, cfg.vocab_size, dtype=torch.float32, device=dev)
         self.sample = sample if self.fused else None
+        if self.sample is not None:
+            self.sample_ws = model.engine.ops.dec_sample_workspace(B, dev)
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):  # warm up allocations / library plans outside the capture
@@ -159,7 +161,7 @@ class DecodeGraph:
         if self.sample is not None:
             sm = self.sample
             ops.dec_sample(self.lg, sm["temperature"], sm["top_k"], sm["seed"], self.pos, self.ids, sm["hist"],
-                           sm["hist_base"])
+                           sm["hist_base"], ws=self.sample_ws)
             ops.dec_advance(self.pos)
         return self.lg
 

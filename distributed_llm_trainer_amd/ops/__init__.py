@@ -30,7 +30,7 @@ CPU_OPS = _namespace(reference, "reference")
 
 
 # HIP-only: the fused one-token decode step (eval/decode.py DecodeGraph)
-_HIP_ONLY = ("dec_norm_qkv", "dec_attn", "dec_gemv_res", "dec_norm_gu", "dec_norm_head", "dec_sample", "dec_advance",
+_HIP_ONLY = ("dec_norm_qkv", "dec_attn", "dec_gemv_res", "dec_norm_gu", "dec_norm_head", "dec_sample", "dec_advance", "dec_sample_workspace",
              "DECODE_BATCHES")
 
 

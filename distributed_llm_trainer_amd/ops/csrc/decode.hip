@@ -469,14 +469,10 @@ __device__ uint32_t kth_key(KeyAt key_at, int C, int k, uint32_t* hist, float* s
   return prefix;
 }
 
-__global__ __launch_bounds__(SMP_NT) void k_dec_sample(const float* __restrict__ logits, int V, float temperature,
-                                                       int top_k, uint32_t seed, const long* __restrict__ posp,
-                                                       long* __restrict__ ids, long* __restrict__ hist, int hist_len,
-                                                       int hist_base) {
-  __shared__ uint32_t bins[4096];
-  __shared__ float scr[40];
-  __shared__ int sel[2];
-  const int tid = threadIdx.x, b = blockIdx.x;
+__device__ void sample_row(const float* __restrict__ logits, int V, float temperature, int top_k, uint32_t seed,
+                           const long* __restrict__ posp, long* __restrict__ ids, long* __restrict__ hist,
+                           int hist_len, int hist_base, int b, uint32_t* bins, float* scr, int* sel) {
+  const int tid = threadIdx.x;
   // Thread t owns the elements i = t + SMP_NT * j (coalesced loads).  The draw inverts the
   // cumulative sum in (thread, j) order -- any fixed order of the elements samples the
   // same distribution.
@@ -584,6 +580,146 @@ __global__ __launch_bounds__(SMP_NT) void k_dec_sample(const float* __restrict__
   }
 }
 
+__global__ __launch_bounds__(SMP_NT) void k_dec_sample(const float* __restrict__ logits, int V, float temperature,
+                                                       int top_k, uint32_t seed, const long* __restrict__ posp,
+                                                       long* __restrict__ ids, long* __restrict__ hist, int hist_len,
+                                                       int hist_base) {
+  __shared__ uint32_t bins[4096];
+  __shared__ float scr[40];
+  __shared__ int sel[2];
+  sample_row(logits, V, temperature, top_k, seed, posp, ids, hist, hist_len, hist_base, blockIdx.x, bins, scr, sel);
+}
+
+// Split sampler for 1 <= top_k <= 64: SMP_NS workgroups per row each take a slice of the
+// row into LDS and keep its elements >= the slice's own k-th largest (ties included, at
+// most SMP_MAXC: an element of the global top-k ranks within the top-k of its slice, so
+// the union holds every kept element); one workgroup per row then ranks the <= 2048
+// candidates and draws.  A slice that overflows SMP_MAXC sends its row to sample_row().
+constexpr int SMP_NS = 16, SMP_MAXC = 128, SMP_SLICE = 4096;
+
+__global__ __launch_bounds__(SMP_NT) void k_dec_topk_slices(const float* __restrict__ logits, int V,
+                                                            float temperature, int top_k, int* __restrict__ ws) {
+  __shared__ uint32_t keys[SMP_SLICE];
+  __shared__ uint32_t bins[4096];
+  __shared__ float scr[40];
+  __shared__ int sel[2];
+  const int tid = threadIdx.x, sl = blockIdx.x, b = blockIdx.y;
+  const int L = (V + SMP_NS - 1) / SMP_NS, lo = sl * L, n = max(0, min(V, lo + L) - lo);
+  const float* row = logits + (size_t)b * V + lo;
+  uint32_t kmax = 0;
+  for (int i = tid; i < SMP_SLICE; i += SMP_NT) {
+    const uint32_t k = i < n ? f2key(row[i] / temperature) : 0u;  // 0: below every real key
+    keys[i] = k;
+    kmax = max(kmax, k);
+  }
+  __syncthreads();
+  // ws row layout (ints): [SMP_NS] counts | [SMP_NS] max keys | [SMP_NS][SMP_MAXC] keys | idx
+  int* cnt = ws + (size_t)b * SMP_NS * (2 + 2 * SMP_MAXC);
+  int* maxk = cnt + SMP_NS;
+  int* ck = maxk + SMP_NS + sl * SMP_MAXC;
+  int* ci = maxk + SMP_NS + SMP_NS * SMP_MAXC + sl * SMP_MAXC;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o, 64));
+  if ((tid & 63) == 0) bins[tid >> 6] = kmax;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t m = 0;
+    for (int w = 0; w < SMP_NT / 64; ++w) m = max(m, bins[w]);
+    maxk[sl] = (int)m;
+  }
+  __syncthreads();
+  uint32_t lt = 1;  // keep every real element of a short slice
+  if (top_k < n) {
+    auto key_at = [&](int j) { return keys[tid + SMP_NT * j]; };
+    lt = max(lt, kth_key(key_at, SMP_SLICE / SMP_NT, top_k, bins, scr, sel));
+  }
+  if (tid == 0) sel[0] = 0;
+  __syncthreads();
+  for (int i = tid; i < n; i += SMP_NT) {
+    const uint32_t k = keys[i];
+    if (k >= lt) {
+      const int slot = atomicAdd(&sel[0], 1);
+      if (slot < SMP_MAXC) {
+        ck[slot] = (int)k;
+        ci[slot] = lo + i;
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) cnt[sl] = sel[0] <= SMP_MAXC ? sel[0] : -1;  // -1: overflow
+}
+
+__global__ __launch_bounds__(SMP_NT) void k_dec_topk_draw(const int* __restrict__ ws, const float* __restrict__ logits,
+                                                          int V, float temperature, int top_k, uint32_t seed,
+                                                          const long* __restrict__ posp, long* __restrict__ ids,
+                                                          long* __restrict__ hist, int hist_len, int hist_base) {
+  __shared__ uint32_t ckey[SMP_NS * SMP_MAXC];
+  __shared__ int cidx[SMP_NS * SMP_MAXC];
+  __shared__ uint32_t bins[4096];
+  __shared__ float scr[40];
+  __shared__ int sel[2];
+  const int tid = threadIdx.x, b = blockIdx.x;
+  const int* cnt = ws + (size_t)b * SMP_NS * (2 + 2 * SMP_MAXC);
+  const int* maxk = cnt + SMP_NS;
+  const int* ck = maxk + SMP_NS;
+  const int* ci = ck + SMP_NS * SMP_MAXC;
+  bool overflow = false;
+  uint32_t kmax = 0;
+  for (int sl = 0; sl < SMP_NS; ++sl) {
+    overflow |= cnt[sl] < 0;
+    kmax = max(kmax, (uint32_t)maxk[sl]);
+  }
+  if (overflow) {  // (uniform) a slice had more than SMP_MAXC elements tied at its threshold
+    sample_row(logits, V, temperature, top_k, seed, posp, ids, hist, hist_len, hist_base, b, bins, scr, sel);
+    return;
+  }
+  for (int i = tid; i < SMP_NS * SMP_MAXC; i += SMP_NT) {
+    const int sl = i / SMP_MAXC, j = i - sl * SMP_MAXC;
+    const bool ok = j < cnt[sl];
+    ckey[i] = ok ? (uint32_t)ck[i] : 0u;
+    cidx[i] = ok ? ci[i] : -1;
+  }
+  __syncthreads();
+  constexpr int PT = SMP_NS * SMP_MAXC / SMP_NT;  // candidates per thread: tid + SMP_NT * j
+  auto key_at = [&](int j) { return ckey[tid + SMP_NT * j]; };
+  const uint32_t thr = max(1u, kth_key(key_at, PT, top_k, bins, scr, sel));
+  const float mx = key2f(kmax);
+  float own = 0.f;
+#pragma unroll
+  for (int j = 0; j < PT; ++j) {
+    const uint32_t k = key_at(j);
+    if (k >= thr) own += __expf(key2f(k) - mx);
+  }
+  float total;
+  const float before = block_excl_scan(own, scr, &total);
+  const long pos = posp[0];
+  const uint32_t h = lowbias32(seed ^ lowbias32((uint32_t)pos * 0x9E3779B9u + (uint32_t)b));
+  const float u = ((h >> 8) + 0.5f) * (1.f / 16777216.f) * total;
+  if (tid == 0) sel[0] = -1;
+  __syncthreads();
+  if (own > 0.f && before <= u && u < before + own) {
+    float cum = before;
+    int pick = -1, last = -1;
+#pragma unroll
+    for (int j = 0; j < PT; ++j) {
+      const uint32_t k = key_at(j);
+      if (k >= thr) {
+        cum += __expf(key2f(k) - mx);
+        last = cidx[tid + SMP_NT * j];
+        if (pick < 0 && u < cum) pick = last;
+      }
+    }
+    sel[0] = pick >= 0 ? pick : last;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const int pick = sel[0] < 0 ? 0 : sel[0];
+    ids[b] = pick;
+    const long t = pos + 1 - hist_base;
+    if (t >= 0 && t < hist_len) hist[(size_t)b * hist_len + t] = pick;
+  }
+}
+
 __global__ void k_dec_advance(long* pos) { pos[0] += 1; }
 
 // ------------------------------------------------------------------------ launchers
@@ -645,10 +781,19 @@ DLT_API int dlt_dec_norm_head(const float* h, const void* lnw, int wbf16, float 
 }
 
 // ids [B] (int64, the next step's input), hist [B, hist_len]: hist[b][pos + 1 - hist_base] = sampled id
+// ws: int32 workspace of B * 16 * 258 (dlt_dec_sample_ws_ints); nullptr -> one workgroup per row
+DLT_API int dlt_dec_sample_ws_ints(int B) { return B * SMP_NS * (2 + 2 * SMP_MAXC); }
 DLT_API int dlt_dec_sample(const float* logits, int B, int V, float temperature, int top_k, uint32_t seed,
-                           const long* pos, long* ids, long* hist, int hist_len, int hist_base, hipStream_t st) {
+                           const long* pos, long* ids, long* hist, int hist_len, int hist_base, int* ws,
+                           hipStream_t st) {
   if (V <= 0 || temperature <= 0.f) return -1;
-  k_dec_sample<<<B, SMP_NT, 0, st>>>(logits, V, temperature, top_k, seed, pos, ids, hist, hist_len, hist_base);
+  if (ws && top_k >= 1 && top_k <= 64 && V <= SMP_NS * SMP_SLICE && top_k < V) {
+    k_dec_topk_slices<<<dim3(SMP_NS, B), SMP_NT, 0, st>>>(logits, V, temperature, top_k, ws);
+    k_dec_topk_draw<<<B, SMP_NT, 0, st>>>(ws, logits, V, temperature, top_k, seed, pos, ids, hist, hist_len,
+                                          hist_base);
+  } else {
+    k_dec_sample<<<B, SMP_NT, 0, st>>>(logits, V, temperature, top_k, seed, pos, ids, hist, hist_len, hist_base);
+  }
   DLT_CHECK_LAUNCH();
 }
 

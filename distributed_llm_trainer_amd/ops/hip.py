@@ -74,7 +74,8 @@ _SIGS = {
     "dlt_dec_norm_gu": [c_void_p, c_void_p, c_int, c_float, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "dlt_dec_norm_head": [c_void_p, c_void_p, c_int, c_float, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "dlt_dec_sample": [c_void_p, c_int, c_int, c_float, c_int, c_uint32, c_void_p, c_void_p, c_void_p, c_int, c_int,
-                       c_void_p],
+                       c_void_p, c_void_p],
+    "dlt_dec_sample_ws_ints": [c_int],
     "dlt_dec_advance": [c_void_p, c_void_p],
 }
 
@@ -170,11 +171,20 @@ def dec_norm_head(h, ln, eps, emb, logits, V):
          "dec_norm_head")
 
 
-def dec_sample(logits, temperature, top_k, seed, pos, ids, hist, hist_base):
+def dec_sample_workspace(B: int, device) -> torch.Tensor:
+    """Scratch of the split (16 workgroups per row) top-k sampler."""
+    return torch.empty(int(lib().dlt_dec_sample_ws_ints(B)), dtype=torch.int32, device=device)
+
+
+def dec_sample(logits, temperature, top_k, seed, pos, ids, hist, hist_base, ws=None):
     """One top-k multinomial draw per row of ``logits`` [B, V] (fp32) on the device: the
     id goes to ``ids`` (B int64, the next decode step's input) and to
-    ``hist[b, pos + 1 - hist_base]`` (int64 [B, L]) when inside the history."""
+    ``hist[b, pos + 1 - hist_base]`` (int64 [B, L]) when inside the history.  With ``ws``
+    (:func:`dec_sample_workspace`) and 1 <= top_k <= 64 the row is split over 16
+    workgroups."""
     B, V = logits.shape
+    if ws is not None:
+        _req(ws, torch.int32, "dec.sample_ws", int(lib().dlt_dec_sample_ws_ints(B)))
     _req(logits, torch.float32, "dec.logits", B * V)
     _req(pos, torch.int64, "dec.pos", 1)
     _req(ids, torch.int64, "dec.ids", B)
@@ -182,7 +192,7 @@ def dec_sample(logits, temperature, top_k, seed, pos, ids, hist, hist_base):
     if hist.dim() != 2 or hist.shape[0] != B:
         raise ValueError("dec_sample: hist must be [B, L]")
     _chk(lib().dlt_dec_sample(_p(logits), B, V, float(temperature), int(top_k), int(seed) & 0xFFFFFFFF, _p(pos),
-                              _p(ids), _p(hist), hist.shape[1], int(hist_base), _stream()), "dec_sample")
+                              _p(ids), _p(hist), hist.shape[1], int(hist_base), _p(ws), _stream()), "dec_sample")
 
 
 def dec_advance(pos):

@@ -265,8 +265,8 @@ def test_decode_fused_kernels_match_torch_step(B, monkeypatch):
                     assert torch.allclose(x[:, :, pos].float(), y[:, :, pos].float(), atol=2e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("tied", [False, True])
-def test_dec_sample_distribution(tied):
+@pytest.mark.parametrize("tied,split", [(False, False), (True, False), (False, True), (True, True)])
+def test_dec_sample_distribution(tied, split):
     """The fused top-k sampler draws from softmax(top-k(logits / T)): only top-k ids (ties
     at the k-th value kept), and empirical frequencies match the probabilities.  ``tied``
     (a few distinct values) exercises the radix-select fallback."""
@@ -280,8 +280,9 @@ def test_dec_sample_distribution(tied):
     ids = torch.empty(B, dtype=torch.long, device=DEV)
     hist = torch.empty(B, n, dtype=torch.long, device=DEV)
     pos = torch.zeros(1, dtype=torch.long, device=DEV)
+    ws = hip.dec_sample_workspace(B, DEV) if split else None
     for _ in range(n):
-        hip.dec_sample(logits, T, k, 1234, pos, ids, hist, 1)
+        hip.dec_sample(logits, T, k, 1234, pos, ids, hist, 1, ws=ws)
         hip.dec_advance(pos)
     freq = torch.zeros(B, V, device=DEV)
     freq.scatter_add_(1, hist, torch.ones_like(hist, dtype=torch.float32))
