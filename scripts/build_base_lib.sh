@@ -3,7 +3,7 @@
 # for scripts/ab_kernels.sh.  Runs on the CPU container (hipcc cross-compiles gfx950).
 set -eu
 rev=${1:-HEAD}
-tmp=$(mktemp -d)
+mkdir -p .scratch && tmp=$(mktemp -d -p "$PWD/.scratch")
 git archive "$rev" distributed_llm_trainer_amd/ops/csrc | tar -x -C "$tmp"
 objs=()
 for f in "$tmp"/distributed_llm_trainer_amd/ops/csrc/*.hip; do
