@@ -200,6 +200,11 @@ class GPTEngine:
         # activation checkpointing: keep o / lse / x2 too and skip the attention forward
         # and the o / down GEMMs in the recompute (see the module docstring)
         self.selective_recompute = os.environ.get("DLT_AC_SELECTIVE", "1") != "0"
+        # attention keep-bit masks (1 bit per causal score, two layouts) are kept from the
+        # forward for the backward while one micro-step's masks of all layers fit in this
+        # budget; beyond it (long context: 3.2 GB per layer at S = 32768, nh 12) the
+        # backward regenerates each layer's bits (one extra VALU kernel per layer)
+        self.attn_mask_budget = float(os.environ.get("DLT_ATTN_MASK_BUDGET_GB", "32")) * 1e9
 
     def set_loss_segments(self, n: int) -> None:
         """Declare that each training forward carries ``n`` fused micro-steps.
@@ -299,13 +304,17 @@ class GPTEngine:
         qkv = gm.linear(n1, w.wqkv)
         if mask is not None:
             torch.cuda.current_stream().wait_event(mask_ev)
+        kw = {"mask": mask} if mask is not None else {}
+        if pa > 0.0 and getattr(ops, "backend", "") == "hip":
+            # keep this layer's keep bits for the backward only within the memory budget
+            mask_bytes = 8 * B * cfg.num_heads * S * ((S + 31) // 32)
+            kw["store_mask"] = mask_bytes * cfg.num_layers <= self.attn_mask_budget
         if self.packed_qkv:
             ops.rope_qk_inplace(qkv, B, S, cfg.num_heads, cos, sin)
-            o, lse = ops.attention_fwd_packed(qkv, B, S, cfg.num_heads, pa, k_attn, out=sb("o", H), mask=mask)
+            o, lse = ops.attention_fwd_packed(qkv, B, S, cfg.num_heads, pa, k_attn, out=sb("o", H), **kw)
             q, k, v = qkv, None, None
         else:
             q, k, v = ops.rope_qkv_fwd(qkv, B, S, cfg.num_heads, cos, sin)
-            kw = {"mask": mask} if mask is not None else {}
             o, lse = ops.attention_fwd(q, k, v, pa, k_attn, True, out=sb("o", H), **kw)
         del qkv
         a = gm.linear(o, w.wo)

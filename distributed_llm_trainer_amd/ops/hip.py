@@ -429,12 +429,13 @@ def attention_fwd(q, k, v, p, key, causal=True, store_mask=True, out=None, mask=
     elif mask is not None:
         _req(mask, torch.int32, "attn.mask", 2 * B * nh * S * ((S + 31) // 32))
         gen = 0
-    elif store_mask:
-        # [0] row layout (lane = query), [1] transposed (lane = key) -- see attention.hip
+    else:
+        # [0] row layout (lane = query), [1] transposed (lane = key) -- see attention.hip;
+        # with store_mask=False it only lives for this call (the backward regenerates it)
         mask = torch.empty(2, B * nh, (S + 31) // 32, S, dtype=torch.int32, device=q.device)
     _chk(lib().dlt_attn_fwd(_p(q), _p(k), _p(v), _p(o), _p(lse), _p(mask), B, nh, S, hd, 1.0 / math.sqrt(hd),
                             key & 0xFFFFFFFF, thr, dscale, gen, _stream()), "attn_fwd")
-    return o, AttnAux((lse, mask))
+    return o, AttnAux((lse, mask if (store_mask or gen == 0) else None))
 
 
 def _packed_dims(qkv, B, S, nh):
@@ -463,12 +464,12 @@ def attention_fwd_packed(qkv, B, S, nh, p, key, out=None, mask=None, store_mask=
     elif mask is not None:
         _req(mask, torch.int32, "attn.mask", 2 * B * nh * S * ((S + 31) // 32))
         gen = 0
-    elif store_mask:
+    else:  # with store_mask=False it only lives for this call (the backward regenerates it)
         mask = torch.empty(2, B * nh, (S + 31) // 32, S, dtype=torch.int32, device=qkv.device)
     _chk(lib().dlt_attn_fwd_ex(_p(qkv), _off(qkv, H), _off(qkv, 2 * H), _p(o), _p(lse), _p(mask), B, nh, S, hd,
                                1.0 / math.sqrt(hd), key & 0xFFFFFFFF, thr, dscale, gen, S * 3 * H, hd, 3 * H,
                                _stream()), "attn_fwd_packed")
-    return o, AttnAux((lse, mask))
+    return o, AttnAux((lse, mask if (store_mask or gen == 0) else None))
 
 
 def attention_bwd_packed(qkv, o, do, aux, p, key, B, S, nh, cos, sin, out=None):
@@ -485,9 +486,8 @@ def attention_bwd_packed(qkv, o, do, aux, p, key, B, S, nh, cos, sin, out=None):
     _req(cos, torch.float32, "attn_bwd.cos")
     _req(sin, torch.float32, "attn_bwd.sin")
     thr = rng.keep_threshold(p)
-    if thr and mask is None:
-        _, aux2 = attention_fwd_packed(qkv, B, S, nh, p, key)
-        mask = aux2[1]
+    if thr and mask is None:  # forward ran with store_mask=False: regenerate the keep bits only
+        mask = attention_dropout_mask(B, nh, S, p, key, device=qkv.device)
     if not thr:
         mask = None
     dqkv = torch.empty(M, 3 * H, dtype=torch.bfloat16, device=qkv.device) if out is None else out
@@ -512,10 +512,8 @@ def attention_bwd(q, k, v, o, do, aux, p, key, causal=True):
         lse, mask = aux, None
     _req(lse, torch.float32, "attn_bwd.lse", B * nh * S)
     thr = rng.keep_threshold(p)
-    if thr and mask is None:
-        # regenerate the keep bits (e.g. forward ran with store_mask=False)
-        _, aux2 = attention_fwd(q, k, v, p, key, causal, store_mask=True)
-        mask = aux2[1]
+    if thr and mask is None:  # forward ran with store_mask=False: regenerate the keep bits only
+        mask = attention_dropout_mask(q.shape[0], q.shape[1], q.shape[2], p, key, device=q.device)
     if not thr:
         mask = None
     delta = torch.empty(B, nh, S, dtype=torch.float32, device=q.device)

@@ -305,3 +305,23 @@ def test_generate_device_loop_matches_host_loop(monkeypatch):
     b = m.generate(ids, max_new_tokens=24, top_k=1)
     assert a.shape == b.shape == (2, 264)
     assert (a == b).float().mean().item() > 0.97  # greedy; rare near-ties may flip
+
+
+def test_attention_masks_regenerated_beyond_budget():
+    """With the keep-bit mask budget exceeded the forward drops each layer's masks and the
+    backward regenerates them: the same gradients (the masks are a pure function of the
+    RNG key; a wrong mask would change the gradients at the 1e-1 level)."""
+    torch.manual_seed(8)
+    base = GPT(_cfg(0.1)).to(DEV)
+    ids = torch.randint(0, 1000, (2, 256), device=DEV)
+    grads = []
+    for budget in (None, 0.0):
+        m = copy.deepcopy(base)
+        eng = m.enable_engine(seed=3)
+        if budget is not None:
+            eng.attn_mask_budget = budget
+        _, loss = m(ids, labels=ids)
+        loss.backward()
+        grads.append(_grads(m))
+    for n in grads[0]:  # equal up to float-atomic summation order (embedding, norm weights)
+        assert torch.allclose(grads[0][n], grads[1][n], rtol=1e-4, atol=1e-8), n
