@@ -89,6 +89,16 @@ __device__ void stage_copy(const bf16_t* __restrict__ x, int K, bf16_t* xs) {
   __syncthreads();
 }
 
+// Weight-stream load: each weight byte is read by one workgroup once per token, so the
+// loads are nontemporal (no point keeping the lines in L2 for a reuse that never comes).
+__device__ __forceinline__ u16x8 ld_w8(const bf16_t* p) {
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const v4u t = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+  u16x8 r;
+  __builtin_memcpy(&r, &t, 16);
+  return r;
+}
+
 // acc[r][b] = sum_k W_r[k] * xs[b][k] for NR rows at once, the whole wave (lanes across K):
 // every row's weight loads are issued before any reduction, so a wave has NR x K/512
 // 16-byte loads in flight (one load round trip per group instead of one per row).  The
@@ -107,7 +117,7 @@ __device__ __forceinline__ void rows_pre(const bf16_t* const (&wrow)[NR], int K,
     const int c = i * 64 + lane;
 #pragma unroll
     for (int r = 0; r < NR; ++r)
-      if (c * 8 < K) pre.wv[r][i] = *reinterpret_cast<const u16x8*>(wrow[r] + c * 8);
+      if (c * 8 < K) pre.wv[r][i] = ld_w8(wrow[r] + c * 8);
   }
 }
 
@@ -150,7 +160,7 @@ __device__ __forceinline__ void rows_dot(const bf16_t* const (&wrow)[NR], int K,
     if (c * 8 < K) {
       u16x8 wv[NR];
 #pragma unroll
-      for (int r = 0; r < NR; ++r) wv[r] = *reinterpret_cast<const u16x8*>(wrow[r] + c * 8);
+      for (int r = 0; r < NR; ++r) wv[r] = ld_w8(wrow[r] + c * 8);
       fma_slice<B, NR>(wv, xs, K, c, acc);
     }
   }

@@ -325,3 +325,24 @@ def test_attention_masks_regenerated_beyond_budget():
         grads.append(_grads(m))
     for n in grads[0]:  # equal up to float-atomic summation order (embedding, norm weights)
         assert torch.allclose(grads[0][n], grads[1][n], rtol=1e-4, atol=1e-8), n
+
+
+def test_selective_recompute_matches_full_and_none_gpu():
+    """Activation checkpointing on the HIP path: selective recompute (default), whole-block
+    recompute (the reference's checkpoint(block)) and no recompute give the same gradients
+    (dropout on, so the replayed masks are checked too)."""
+    torch.manual_seed(9)
+    base = GPT(_cfg(0.1)).to(DEV)
+    ids = torch.randint(0, 1000, (2, 256), device=DEV)
+    grads = []
+    for recompute, selective in ((False, True), (True, True), (True, False)):
+        m = copy.deepcopy(base)
+        eng = m.enable_engine(seed=4)
+        eng.selective_recompute = selective
+        m.gradient_checkpointing = recompute
+        _, loss = m(ids, labels=ids)
+        loss.backward()
+        grads.append(_grads(m))
+    for g in grads[1:]:
+        for n in grads[0]:  # equal up to float-atomic summation order (embedding, norm weights)
+            assert torch.allclose(grads[0][n], g[n], rtol=1e-4, atol=1e-8), n
