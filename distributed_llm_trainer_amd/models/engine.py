@@ -509,6 +509,15 @@ class GPTEngine:
         # stream.  Only for providers whose hooks can be delayed (the flat DDP store).
         n_main = self.main_wgrad_layers if (side is not None and getattr(prov, "late_post_backward_ok", False)) else 0
         late = []
+        # DDP store: the head gradient hook may run before layer 0's weight gradients
+        early_head = getattr(prov, "late_post_backward_ok", False)
+
+        def head_done():
+            # embedding (tied with lm_head): scatter-add, then the head gradient hook
+            if head_ev is not None:
+                torch.cuda.current_stream().wait_event(head_ev)
+            ops.embedding_bwd(st.ids, g_x2n if early_head else g_x2, hg.embed)
+            prov.post_backward("head")
 
         def sb(layer, name, n):
             return self._slot_buf(st, layer, name, M, n, dev)[0] if st.defer else None
@@ -557,6 +566,11 @@ class GPTEngine:
             g_x2n, g_dn = ops.rmsnorm_bwd(dn1, c.x, c.rstd1, w.ln1, dx2, gr.ln1, p_prev, key_prev,
                                           want_ddelta=(i > 0), ddelta_out=sb(i - 1, "dd", H) if i > 0 else None)
             del dn1, dx2
+            if i == 0 and early_head:
+                # The head bucket (tied embedding + every norm weight) is final once the
+                # embedding scatter-add is done: issue its all-reduce now, so it overlaps
+                # the last layers' weight-gradient GEMMs instead of trailing the step.
+                head_done()
             # weight gradients (fp32 accumulate into the main-grad buffers)
             side_ctx = None
             if do_wgrad:
@@ -593,15 +607,12 @@ class GPTEngine:
                 if side_ctx is not None:
                     side_ctx.__exit__(None, None, None)
             yield
-        # embedding (tied with lm_head): scatter-add
-        if head_ev is not None:
-            torch.cuda.current_stream().wait_event(head_ev)
-        ops.embedding_bwd(st.ids, g_x2, hg.embed)
+        if not early_head:
+            head_done()
         if late:
             torch.cuda.current_stream().wait_stream(side)
             for i in late:
                 prov.post_backward(i)
-        prov.post_backward("head")
         if side is not None and do_wgrad and st.defer:
             torch.cuda.current_stream().wait_stream(side)
 

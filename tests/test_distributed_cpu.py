@@ -112,6 +112,28 @@ def test_fsdp_matches_single_process(strategy, ac, offload):
         assert torch.allclose(outs[0][k], ref[k], atol=3e-5, rtol=1e-4), (k, (outs[0][k] - ref[k]).abs().max())
 
 
+def test_ddp_three_ranks_matches_single_process():
+    """An odd world size (buckets and the 1/world factor are not powers of two)."""
+    outs = run_multiprocess(_ddp_worker, world=3, args=(2, 0.05, 2, 4))
+    for o in outs[1:]:
+        assert torch.equal(outs[0][0], o[0]), "ranks diverged"
+    ref = _single_worker_equiv(2, 3, GA=4)
+    assert torch.allclose(outs[0][0], ref, atol=2e-5, rtol=1e-4), (outs[0][0] - ref).abs().max()
+
+
+@pytest.mark.parametrize("strategy,world,local", [("FULL_SHARD", 3, 3), ("HYBRID_SHARD", 4, 2)])
+def test_fsdp_wider_worlds_match_single_process(strategy, world, local):
+    """FULL_SHARD over 3 ranks (no unit divides evenly: shard padding on every unit) and
+    HYBRID_SHARD as a 2 x 2 mesh (shard inside each "node" of 2, all-reduce across)."""
+    outs = run_multiprocess(_fsdp_worker, world=world, args=(strategy, 2, True, False),
+                            env={"LOCAL_WORLD_SIZE": str(local)})
+    ref = _fsdp_single(2, world)
+    for k in ref:
+        for r in range(1, world):
+            assert torch.equal(outs[0][k], outs[r][k]), f"{k}: rank {r} diverged"
+        assert torch.allclose(outs[0][k], ref[k], atol=3e-5, rtol=1e-4), (k, (outs[0][k] - ref[k]).abs().max())
+
+
 def test_fsdp_micro_step_fusion_matches_single_process():
     """FULL_SHARD with both micro-steps fused into one chain (one reduce-scatter per
     chain instead of per micro-step): same parameters as the unfused single process."""
