@@ -632,7 +632,8 @@ class GPTEngine:
         stream: its lm_head weight-gradient GEMM (beta = 1) and the DDP bucket
         all-reduces must see every micro-step's gradient.  Weight gradients are
         deferred (one GEMM per weight over the window), so before that point the
-        chains only add into gradients with atomics (norm weights, embedding rows).
+        chains only add into the norm-weight and embedding gradients, one backward
+        after the other (deterministic kernels, no float atomics).
 
         ``dloss`` is d(total)/d(micro-step loss) (1/GA), ``before_last`` runs before
         the last backward is issued (the DDP runtime switches its sync on there).
@@ -682,6 +683,12 @@ class GPTEngine:
                     main.wait_stream(pipe)
                 if before_last is not None:
                     before_last()
+            elif cuda and k > 0:
+                # backward k starts after backward k-1 has finished on the other stream:
+                # both add into the same norm / embedding gradients (fixed-order, non-atomic
+                # kernels), so two backwards never overlap -- a backward still overlaps
+                # the next micro-step's forward, which is what the pipelining is for.
+                stream_of(k).wait_stream(stream_of(k - 1))
             running = [(k, self._backward_gen(states[k], dloss), False)]
             states[k] = None
             if k + 1 < GA:

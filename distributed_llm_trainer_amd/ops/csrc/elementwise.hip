@@ -28,15 +28,75 @@ __global__ __launch_bounds__(256) void k_embedding_fwd(const int64_t* __restrict
   }
 }
 
-// dW[ids[m], :] += dout[m, :]   (one 256-B contiguous atomic wave-instruction per 64 lanes)
-__global__ __launch_bounds__(256) void k_embedding_bwd(const int64_t* __restrict__ ids, const float* __restrict__ dout,
-                                                       float* __restrict__ dW, int M, int H, int V) {
-  const size_t total = (size_t)M * H;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    const int m = (int)(i / H);
-    const int h = (int)(i % H);
-    DLT_DASSERT(ids[m] >= 0 && ids[m] < V);
-    unsafeAtomicAdd(dW + (size_t)ids[m] * H + h, dout[i]);
+// Deterministic scatter-add dW[v, :] += sum of dout[m, :] over ids[m] == v (SURVEY K1:
+// sorted segment-sum, no float atomics, so gradients are bitwise reproducible).  The
+// ids arrive stably sorted (sids, with perm = original positions), so the rows of one
+// token id form a run in increasing m.  Pass 1: one wave per chunk of EMB_CH sorted
+// positions walks the runs of its chunk; a run inside the chunk is added to dW directly
+// (its only writer), a run cut by a chunk edge leaves a partial in ws[chunk][0] (cut on
+// the left) or ws[chunk][1] (cut on the right only).  Pass 2: the chunk where a cut run
+// starts adds its partial and the following chunks' left partials, in chunk order.
+// Lane = 4 columns per 256-column slice; the run walk is wave-uniform.
+#define EMB_CH 16
+__global__ __launch_bounds__(256) void k_embedding_bwd_runs(const int64_t* __restrict__ sids,
+                                                            const int64_t* __restrict__ perm,
+                                                            const float* __restrict__ dout, float* __restrict__ dW,
+                                                            float* __restrict__ ws, int M, int H, int V) {
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int p0 = c * EMB_CH;
+  if (p0 >= M) return;
+  const int p1 = min(M, p0 + EMB_CH);
+  int s = p0;
+  while (s < p1) {
+    const int64_t v = sids[s];
+    DLT_DASSERT(v >= 0 && v < V);
+    int e = s + 1;
+    while (e < p1 && sids[e] == v) ++e;
+    const bool cut_l = s == p0 && p0 > 0 && sids[p0 - 1] == v;
+    const bool cut_r = e == p1 && p1 < M && sids[p1] == v;
+    float* dst = cut_l ? ws + (size_t)(2 * c) * H : cut_r ? ws + (size_t)(2 * c + 1) * H : dW + (size_t)v * H;
+    for (int col = lane * 4; col < H; col += 256) {
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int q = s; q < e; ++q) {
+        const float4 d = *reinterpret_cast<const float4*>(dout + (size_t)perm[q] * H + col);
+        a.x += d.x; a.y += d.y; a.z += d.z; a.w += d.w;
+      }
+      float4* o = reinterpret_cast<float4*>(dst + col);
+      if (!(cut_l || cut_r)) {
+        const float4 w = *o;
+        a.x += w.x; a.y += w.y; a.z += w.z; a.w += w.w;
+      }
+      *o = a;
+    }
+    s = e;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_embedding_bwd_spans(const int64_t* __restrict__ sids,
+                                                             const float* __restrict__ ws, float* __restrict__ dW,
+                                                             int M, int H) {
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int p0 = c * EMB_CH;
+  if (p0 >= M) return;
+  const int p1 = p0 + EMB_CH;
+  if (p1 >= M) return;
+  const int64_t v = sids[p1 - 1];
+  if (sids[p1] != v) return;                               // last run not cut on the right
+  if (sids[p0] == v && p0 > 0 && sids[p0 - 1] == v) return;  // run started in an earlier chunk
+  int c_end = c + 1;                                         // chunks [c+1, c_end] hold the rest
+  while ((c_end + 1) * EMB_CH < M && sids[(c_end + 1) * EMB_CH] == v) ++c_end;
+  for (int col = lane * 4; col < H; col += 256) {
+    float4 a = *reinterpret_cast<const float4*>(ws + (size_t)(2 * c + 1) * H + col);
+    for (int k = c + 1; k <= c_end; ++k) {
+      const float4 d = *reinterpret_cast<const float4*>(ws + (size_t)(2 * k) * H + col);
+      a.x += d.x; a.y += d.y; a.z += d.z; a.w += d.w;
+    }
+    float4* o = reinterpret_cast<float4*>(dW + (size_t)v * H + col);
+    const float4 w = *o;
+    a.x += w.x; a.y += w.y; a.z += w.z; a.w += w.w;
+    *o = a;
   }
 }
 
@@ -50,13 +110,18 @@ DLT_API int dlt_embedding_fwd(const int64_t* ids, const void* W, int wdt, float*
   DLT_CHECK_LAUNCH();
 }
 
-DLT_API int dlt_embedding_bwd(const int64_t* ids, const float* dout, float* dW, int M, int H, int V, hipStream_t s) {
-  const size_t total = (size_t)M * H;
-  int blocks = (int)((total + 255) / 256);
-  if (blocks > 8192) blocks = 8192;
-  k_embedding_bwd<<<blocks, 256, 0, s>>>(ids, dout, dW, M, H, V);
+// sids/perm: torch.sort(ids, stable=True); ws: 2 * ceil(M / EMB_CH) * H floats.
+DLT_API int dlt_embedding_bwd(const int64_t* sids, const int64_t* perm, const float* dout, float* dW, float* ws,
+                              int M, int H, int V, hipStream_t s) {
+  if (H % 4 || M <= 0) return -1;
+  const int chunks = (M + EMB_CH - 1) / EMB_CH;
+  const int blocks = (chunks + 3) / 4;
+  k_embedding_bwd_runs<<<blocks, 256, 0, s>>>(sids, perm, dout, dW, ws, M, H, V);
+  k_embedding_bwd_spans<<<blocks, 256, 0, s>>>(sids, ws, dW, M, H);
   DLT_CHECK_LAUNCH();
 }
+
+DLT_API int dlt_embedding_bwd_chunk() { return EMB_CH; }
 
 // ---------------------------------------------------------------- RoPE
 // qkv [B*S, 3, nh, hd] (bf16) -> q, k, v [B, nh, S, hd]; q, k rotated (NeoX half split)

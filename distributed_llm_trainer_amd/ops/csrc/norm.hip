@@ -209,24 +209,34 @@ __global__ __launch_bounds__(256) void k_rmsnorm_bwd(
   }
 }
 
-// dw[j] += sum over the partial rows; grid (ceil(H/256), 128): 128 atomics per column,
-// 8 rows per thread (latency-bound otherwise).
-__global__ __launch_bounds__(256) void k_colsum_acc(const float* __restrict__ part, float* __restrict__ dw, int rows,
-                                                    int H) {
-  const int j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= H) return;
-  const int per = (rows + gridDim.y - 1) / gridDim.y;
-  const int r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
+// dw[j] += sum over the partial rows, in a fixed order (bitwise reproducible, no
+// float atomics): one 1024-thread block per 64 columns, lane = column (256-B rows),
+// wave w sums rows w, w+16, ... into 4 interleaved accumulators, and wave 0 adds the
+// 16 wave partials in wave order.  The partials were just written (L2-resident).
+__global__ __launch_bounds__(1024) void k_colsum_acc(const float* __restrict__ part, float* __restrict__ dw, int rows,
+                                                     int H) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + lane;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  int r = r0;
-  for (; r + 3 < r1; r += 4) {
-    s0 += part[(size_t)r * H + j];
-    s1 += part[(size_t)(r + 1) * H + j];
-    s2 += part[(size_t)(r + 2) * H + j];
-    s3 += part[(size_t)(r + 3) * H + j];
+  if (j < H) {
+    int r = w;
+    for (; r + 48 < rows; r += 64) {
+      s0 += part[(size_t)r * H + j];
+      s1 += part[(size_t)(r + 16) * H + j];
+      s2 += part[(size_t)(r + 32) * H + j];
+      s3 += part[(size_t)(r + 48) * H + j];
+    }
+    for (; r < rows; r += 16) s0 += part[(size_t)r * H + j];
   }
-  for (; r < r1; ++r) s0 += part[(size_t)r * H + j];
-  if (r1 > r0) unsafeAtomicAdd(dw + j, (s0 + s1) + (s2 + s3));
+  red[w][lane] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (w == 0 && j < H) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += red[i][lane];
+    dw[j] += s;
+  }
 }
 
 static inline int nch_of(int H) {
@@ -286,6 +296,6 @@ DLT_API int dlt_rmsnorm_bwd(const bf16_t* dy, const float* x, const float* rstd,
     default: k_rmsnorm_bwd<16><<<grid, block, shm, stream>>>(ARGS); break;
   }
 #undef ARGS
-  if (dw_ws) k_colsum_acc<<<dim3((H + 255) / 256, 128), 256, 0, stream>>>(dw_ws, dw, blocks, H);
+  if (dw_ws) k_colsum_acc<<<(H + 63) / 64, 1024, 0, stream>>>(dw_ws, dw, blocks, H);
   DLT_CHECK_LAUNCH();
 }

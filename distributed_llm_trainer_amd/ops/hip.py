@@ -35,7 +35,8 @@ _SIGS = {
     "dlt_rmsnorm_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                         c_void_p, c_void_p, c_int, c_int, c_uint32, c_uint32, c_float, c_void_p],
     "dlt_embedding_fwd": [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p],
-    "dlt_embedding_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
+    "dlt_embedding_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
+    "dlt_embedding_bwd_chunk": [],
     "dlt_splitk_acc": [c_void_p, c_void_p, ctypes.c_long, c_int, c_void_p],
     "dlt_rope_qkv_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                          c_void_p],
@@ -261,15 +262,23 @@ def embedding_fwd(ids: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
 
 
 def embedding_bwd(ids: torch.Tensor, dout: torch.Tensor, dweight: torch.Tensor) -> None:
-    ids = ids.reshape(-1).contiguous()
+    """dweight[ids[m]] += dout[m], deterministically: a stable sort groups equal ids
+    (rocPRIM radix sort via torch.sort), the kernels sum each run in position order
+    with one writer per row (no float atomics)."""
+    ids = ids.reshape(-1)
     if ids.dtype != torch.int64:
         ids = ids.long()
     M = ids.numel()
     H = dweight.shape[-1]
     _req(dout, torch.float32, "embedding_bwd.dout", M * H)
     _req(dweight, torch.float32, "embedding_bwd.dweight")
-    _chk(lib().dlt_embedding_bwd(_p(ids), _p(dout), _p(dweight), M, H, dweight.shape[0], _stream()),
-         "embedding_bwd")
+    if M == 0:
+        return
+    sids, perm = torch.sort(ids, stable=True)
+    ch = lib().dlt_embedding_bwd_chunk()
+    ws = torch.empty(2 * (-(-M // ch)) * H, dtype=torch.float32, device=dout.device)
+    _chk(lib().dlt_embedding_bwd(_p(sids), _p(perm), _p(dout), _p(dweight), _p(ws), M, H, dweight.shape[0],
+                                 _stream()), "embedding_bwd")
 
 
 # ---------------------------------------------------------------- RMSNorm

@@ -26,6 +26,7 @@ differently, by design for an 8x MI355X xGMI full mesh:
 from __future__ import annotations
 
 import contextlib
+import os
 from typing import List, Optional, Tuple
 
 import torch
@@ -41,6 +42,11 @@ class DDPRuntime:
         self.rank = dist.get_rank(process_group) if dist.is_initialized() else 0
         self.reduce_dtype = reduce_dtype
         self.sync = True
+        # DLT_FORCE_COLLECTIVES=1: issue every collective even on one rank, so a one-GPU
+        # box runs the multi-GPU code path (RCCL kernels launched from the weight-gradient
+        # stream, waits, the bucket schedule) with a result that must equal no collectives
+        self.force = dist.is_initialized() and os.environ.get("DLT_FORCE_COLLECTIVES") == "1"
+        self.launched = 0
         self.handles: List[Tuple[object, Optional[torch.Tensor], int, int]] = []
         lay = store.layout
         elem = store.grad.element_size()
@@ -60,7 +66,7 @@ class DDPRuntime:
         # embedding (tied lm_head) + all norm weights: final after the embedding bwd
         self.fire_at.setdefault("head", []).append((lay.embed_offset, lay.total))
         self.buckets = [b for v in self.fire_at.values() for b in v]
-        if broadcast_init and self.world > 1:
+        if broadcast_init and (self.world > 1 or self.force):
             self.broadcast_parameters()
         store.hooks = self
 
@@ -95,12 +101,13 @@ class DDPRuntime:
         pass
 
     def post_backward(self, unit):
-        if not self.sync or self.world == 1:
+        if not self.sync or (self.world == 1 and not self.force):
             return
         for (a, b) in self.fire_at.get(unit, ()):
             self._launch(a, b)
 
     def _launch(self, a: int, b: int) -> None:
+        self.launched += 1
         g = self.store.grad[a:b]
         if self.reduce_dtype != g.dtype:
             t = g.to(self.reduce_dtype)
@@ -112,7 +119,7 @@ class DDPRuntime:
 
     def reduce_all_now(self) -> None:
         """Synchronous fallback used by the eager (non-engine) path."""
-        if self.world == 1:
+        if self.world == 1 and not self.force:
             return
         for (a, b) in self.buckets:
             self._launch(a, b)

@@ -37,6 +37,7 @@ full-size fp32 unit gradients across micro-steps and reduce-scatters once.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
@@ -123,6 +124,9 @@ class FSDPRuntime(ParamProvider):
         else:
             self.shard_world, self.shard_rank = world, rank
         self.world = dist.get_world_size() if self.dist else 1
+        # DLT_FORCE_COLLECTIVES=1 (see parallel/ddp.py): one rank still all-gathers and
+        # reduce-scatters through the process group instead of aliasing its shard
+        self.force = self.dist and os.environ.get("DLT_FORCE_COLLECTIVES") == "1"
         self.units: Dict[object, FlatUnit] = {}
         self._build_units(model)
         self._free_module_params(model)
@@ -205,7 +209,7 @@ class FSDPRuntime(ParamProvider):
         if u.full is not None and u.ag_work is None:
             return
         if u.full is None:
-            if self.shard_world == 1:  # NO_SHARD: the "gathered" buffer IS the local replica
+            if self.shard_world == 1 and not self.force:  # NO_SHARD: the "gathered" buffer IS the local replica
                 u.full = u.shard_c
                 return
             u.full = torch.empty(u.padded, dtype=self.compute_dtype, device=self.device)
@@ -256,12 +260,12 @@ class FSDPRuntime(ParamProvider):
     def _reduce(self, u: FlatUnit):
         """Sum full-size grads over ranks into this rank's fp32 shard grad (async)."""
         g = u.full_grad
-        if self.shard_world == 1:
+        if self.shard_world == 1 and not (self.force and self.strategy != "NO_SHARD"):
             # the reduce-dtype copy also on one rank: it is what stays pending until
             # finish() (half the bytes of the fp32 full grad, which is freed here)
             t = g if self.reduce_dtype == torch.float32 else g.to(self.reduce_dtype)
             work = None
-            if self.dist and self.world > 1:
+            if self.dist and (self.world > 1 or self.force):
                 work = dist.all_reduce(t, group=self.pg if self.strategy != "NO_SHARD" else None, async_op=True)
             u.rs_pending.append((work, t, None))
         else:

@@ -309,3 +309,38 @@ def test_fsdp_sharded_checkpoint_rejects_other_world_size(tmp_path):
                      FSDPConfig(reduce_dtype="fp32"))
     with pytest.raises(ValueError, match="consolidate_sharded"):
         tr.load_checkpoint(path)
+
+
+def _forced_worker(rank, world, mode, strategy="FULL_SHARD"):
+    """One rank; with DLT_FORCE_COLLECTIVES=1 every bucket / gather / reduce-scatter is
+    still issued through the process group (the multi-GPU code path)."""
+    from distributed_llm_trainer_amd.models.config import GPTConfig
+    cfg = GPTConfig(**TINY)
+    if mode == "ddp":
+        from distributed_llm_trainer_amd.training.configs import TrainingConfig
+        from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
+        tc = TrainingConfig(batch_size=2, gradient_accumulation_steps=4, warmup_steps=1, max_steps=100,
+                            learning_rate=1e-2, bucket_cap_mb=0.05, micro_step_fusion=2)
+        tr = DistributedTrainer(cfg, tc)
+    else:
+        from distributed_llm_trainer_amd.training.configs import FSDPConfig, FSDPTrainingConfig
+        from distributed_llm_trainer_amd.training.fsdp_trainer import FSDPTrainer
+        tc = FSDPTrainingConfig(batch_size=2, gradient_accumulation_steps=4, warmup_steps=1, max_steps=100,
+                                learning_rate=1e-2, micro_step_fusion=2)
+        tr = FSDPTrainer(cfg, tc, FSDPConfig(sharding_strategy=strategy, reduce_dtype="fp32"))
+    for s in range(2):
+        tr.train_step({"input_ids": _data(s, 0, n=8)})
+    launched = tr.ddp.launched if mode == "ddp" else 0
+    sd = tr._full_state() if mode != "ddp" else {"flat": tr.store.flat.detach().cpu().clone()}
+    return {k: v.detach().float().cpu() for k, v in sd.items() if "rotary" not in k}, launched
+
+
+@pytest.mark.parametrize("mode,strategy", [("ddp", None), ("fsdp", "FULL_SHARD"), ("fsdp", "NO_SHARD")])
+def test_forced_collectives_on_one_rank_are_identity(mode, strategy):
+    a, _ = run_multiprocess(_forced_worker, world=1, args=(mode, strategy))[0]
+    b, launched = run_multiprocess(_forced_worker, world=1, args=(mode, strategy),
+                                   env={"DLT_FORCE_COLLECTIVES": "1"})[0]
+    if mode == "ddp":
+        assert launched > 2
+    for k in a:
+        assert torch.equal(a[k], b[k]), k

@@ -78,6 +78,48 @@ def test_embedding():
     _close(g1, g2, 1e-4, 1e-5, "emb bwd")
 
 
+@pytest.mark.parametrize("M,dist", [(4099, "zipf"), (3000, "one_token"), (517, "two_runs"), (16, "uniform")])
+def test_embedding_bwd_deterministic(M, dist):
+    """Sorted segment-sum scatter-add: runs inside one 16-position chunk, runs cut by
+    chunk edges and runs spanning many chunks (a single token id everywhere); the result
+    matches the fp64 sum and two calls are bitwise identical (no float atomics)."""
+    torch.manual_seed(12)
+    V, H = 2000, 768
+    if dist == "zipf":  # heavy head like real text: a few ids take most positions
+        ids = torch.minimum((torch.rand(M, device=DEV) ** 4 * V).long(), torch.tensor(V - 1, device=DEV))
+    elif dist == "one_token":
+        ids = torch.full((M,), 7, device=DEV, dtype=torch.long)
+    elif dist == "two_runs":
+        ids = torch.where(torch.arange(M, device=DEV) % 3 == 0, 5, V - 1)
+    else:
+        ids = torch.randint(0, V, (M,), device=DEV)
+    dout = torch.randn(M, H, device=DEV)
+    base = torch.randn(V, H, device=DEV)
+    g1, g2 = base.clone(), base.clone()
+    hip.embedding_bwd(ids, dout, g1)
+    hip.embedding_bwd(ids, dout, g2)
+    assert torch.equal(g1, g2), "embedding_bwd is not deterministic"
+    exp = base.double().index_add_(0, ids, dout.double())
+    _close(g1, exp, 1e-4, 1e-5, "emb bwd vs fp64")
+
+
+def test_rmsnorm_bwd_dw_deterministic():
+    torch.manual_seed(13)
+    M, H = 16384, 768
+    x = torch.randn(M, H, device=DEV)
+    rstd = torch.rsqrt(x.pow(2).mean(-1) + 1e-6)
+    w = torch.rand(H, device=DEV) + 0.5
+    dy = torch.randn(M, H, device=DEV).bfloat16()
+    outs = []
+    for _ in range(2):
+        dw = torch.ones(H, device=DEV)
+        hip.rmsnorm_bwd(dy, x, rstd, w, None, dw, 0.0, 0)
+        outs.append(dw)
+    assert torch.equal(outs[0], outs[1]), "rmsnorm dw reduction is not deterministic"
+    exp = 1.0 + (dy.double() * (x.double() * rstd.double()[:, None])).sum(0)
+    _close(outs[0], exp, 1e-2, 1e-4, "dw vs fp64")
+
+
 def test_rope():
     torch.manual_seed(3)
     B, S, nh, hd = 2, 300, 12, 64

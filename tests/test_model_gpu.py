@@ -346,3 +346,25 @@ def test_selective_recompute_matches_full_and_none_gpu():
     for g in grads[1:]:
         for n in grads[0]:  # equal up to float-atomic summation order (embedding, norm weights)
             assert torch.allclose(grads[0][n], g[n], rtol=1e-4, atol=1e-8), n
+
+
+def test_training_is_bitwise_reproducible():
+    """Two identical DDP-path training runs in one process (pipelined fused chains,
+    deferred split-K weight gradients on the side stream, dropout on) end with
+    bitwise-identical parameters: every gradient reduction is fixed-order (sorted
+    embedding segment-sum, fixed-order norm-weight column sums, split-K partial sums,
+    grad-norm partials) and the GEMM choices are process-wide."""
+    from distributed_llm_trainer_amd.training.configs import TrainingConfig
+    from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
+    data = torch.randint(0, 1000, (8, 256), device=DEV, generator=torch.Generator(DEV).manual_seed(3))
+    res = []
+    for _ in range(2):
+        torch.manual_seed(3)
+        tc = TrainingConfig(batch_size=2, gradient_accumulation_steps=4, warmup_steps=1, learning_rate=1e-3,
+                            micro_step_fusion=1)
+        tr = DistributedTrainer(_cfg(0.1), tc)
+        assert tr.use_engine
+        losses = [tr.train_step({"input_ids": data})["loss"] for _ in range(3)]
+        res.append((losses, tr.store.flat.detach().clone()))
+    assert res[0][0] == res[1][0], (res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1]), (res[0][1] - res[1][1]).abs().max().item()
