@@ -37,8 +37,8 @@ __global__ __launch_bounds__(256) void k_embedding_fwd(const int64_t* __restrict
 // the left) or ws[chunk][1] (cut on the right only).  Pass 2: the chunk where a cut run
 // starts adds its partial and the following chunks' left partials, in chunk order.
 // Lane = 4 columns per 256-column slice; the run walk is wave-uniform.
-#define EMB_CH 16
-__global__ __launch_bounds__(256) void k_embedding_bwd_runs(const int64_t* __restrict__ sids,
+#define EMB_CH 4
+__global__ __launch_bounds__(256) void k_embedding_bwd_runs(const int* __restrict__ sids,
                                                             const int64_t* __restrict__ perm,
                                                             const float* __restrict__ dout, float* __restrict__ dW,
                                                             float* __restrict__ ws, int M, int H, int V) {
@@ -49,7 +49,7 @@ __global__ __launch_bounds__(256) void k_embedding_bwd_runs(const int64_t* __res
   const int p1 = min(M, p0 + EMB_CH);
   int s = p0;
   while (s < p1) {
-    const int64_t v = sids[s];
+    const int v = sids[s];
     DLT_DASSERT(v >= 0 && v < V);
     int e = s + 1;
     while (e < p1 && sids[e] == v) ++e;
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void k_embedding_bwd_runs(const int64_t* __res
   }
 }
 
-__global__ __launch_bounds__(256) void k_embedding_bwd_spans(const int64_t* __restrict__ sids,
+__global__ __launch_bounds__(256) void k_embedding_bwd_spans(const int* __restrict__ sids,
                                                              const float* __restrict__ ws, float* __restrict__ dW,
                                                              int M, int H) {
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -82,14 +82,24 @@ __global__ __launch_bounds__(256) void k_embedding_bwd_spans(const int64_t* __re
   if (p0 >= M) return;
   const int p1 = p0 + EMB_CH;
   if (p1 >= M) return;
-  const int64_t v = sids[p1 - 1];
+  const int v = sids[p1 - 1];
   if (sids[p1] != v) return;                               // last run not cut on the right
   if (sids[p0] == v && p0 > 0 && sids[p0 - 1] == v) return;  // run started in an earlier chunk
   int c_end = c + 1;                                         // chunks [c+1, c_end] hold the rest
   while ((c_end + 1) * EMB_CH < M && sids[(c_end + 1) * EMB_CH] == v) ++c_end;
   for (int col = lane * 4; col < H; col += 256) {
     float4 a = *reinterpret_cast<const float4*>(ws + (size_t)(2 * c + 1) * H + col);
-    for (int k = c + 1; k <= c_end; ++k) {
+    int k = c + 1;
+    for (; k + 7 <= c_end; k += 8) {  // 8 independent loads in flight, added in chunk order
+      float4 d[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) d[u] = *reinterpret_cast<const float4*>(ws + (size_t)(2 * (k + u)) * H + col);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        a.x += d[u].x; a.y += d[u].y; a.z += d[u].z; a.w += d[u].w;
+      }
+    }
+    for (; k <= c_end; ++k) {
       const float4 d = *reinterpret_cast<const float4*>(ws + (size_t)(2 * k) * H + col);
       a.x += d.x; a.y += d.y; a.z += d.z; a.w += d.w;
     }
@@ -110,8 +120,8 @@ DLT_API int dlt_embedding_fwd(const int64_t* ids, const void* W, int wdt, float*
   DLT_CHECK_LAUNCH();
 }
 
-// sids/perm: torch.sort(ids, stable=True); ws: 2 * ceil(M / EMB_CH) * H floats.
-DLT_API int dlt_embedding_bwd(const int64_t* sids, const int64_t* perm, const float* dout, float* dW, float* ws,
+// sids/perm: torch.sort(int32 ids, stable=True); ws: 2 * ceil(M / EMB_CH) * H floats.
+DLT_API int dlt_embedding_bwd(const int* sids, const int64_t* perm, const float* dout, float* dW, float* ws,
                               int M, int H, int V, hipStream_t s) {
   if (H % 4 || M <= 0) return -1;
   const int chunks = (M + EMB_CH - 1) / EMB_CH;

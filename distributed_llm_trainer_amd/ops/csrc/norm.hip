@@ -210,32 +210,55 @@ __global__ __launch_bounds__(256) void k_rmsnorm_bwd(
 }
 
 // dw[j] += sum over the partial rows, in a fixed order (bitwise reproducible, no
-// float atomics): one 1024-thread block per 64 columns, lane = column (256-B rows),
-// wave w sums rows w, w+16, ... into 4 interleaved accumulators, and wave 0 adds the
-// 16 wave partials in wave order.  The partials were just written (L2-resident).
+// float atomics).  One 1024-thread block per 64 columns: thread (g, q) owns columns
+// 4q..4q+3 of the slice (float4 loads, 16 threads = one 256-B row segment) and rows
+// g, g+64, ... with 8 loads in flight (the partials were written by blocks on every XCD,
+// so the reads come from the fabric: latency-bound without that parallelism); then the
+// 64 row-group sums are added through LDS in two fixed-order levels.
+__device__ __forceinline__ void f4add(float4& a, const float4 b) {
+  a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+}
+
 __global__ __launch_bounds__(1024) void k_colsum_acc(const float* __restrict__ part, float* __restrict__ dw, int rows,
                                                      int H) {
-  __shared__ float red[16][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int j = blockIdx.x * 64 + lane;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  if (j < H) {
-    int r = w;
-    for (; r + 48 < rows; r += 64) {
-      s0 += part[(size_t)r * H + j];
-      s1 += part[(size_t)(r + 16) * H + j];
-      s2 += part[(size_t)(r + 32) * H + j];
-      s3 += part[(size_t)(r + 48) * H + j];
-    }
-    for (; r < rows; r += 16) s0 += part[(size_t)r * H + j];
-  }
-  red[w][lane] = (s0 + s1) + (s2 + s3);
-  __syncthreads();
-  if (w == 0 && j < H) {
-    float s = 0.f;
+  __shared__ float red[64][65];
+  __shared__ float red2[16][64];
+  const int q = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int c0 = blockIdx.x * 64 + q * 4;
+  float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0, a3 = a0;
+  if (c0 < H) {  // H % 4 == 0: the quad is in range
+    const float* p = part + c0;
+    int r = g;
+    for (; r + 448 < rows; r += 512) {
+      float4 x[8];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) s += red[i][lane];
-    dw[j] += s;
+      for (int u = 0; u < 8; ++u) x[u] = *reinterpret_cast<const float4*>(p + (size_t)(r + 64 * u) * H);
+      f4add(a0, x[0]); f4add(a1, x[1]); f4add(a2, x[2]); f4add(a3, x[3]);
+      f4add(a0, x[4]); f4add(a1, x[5]); f4add(a2, x[6]); f4add(a3, x[7]);
+    }
+    for (; r < rows; r += 64) f4add(a0, *reinterpret_cast<const float4*>(p + (size_t)r * H));
+  }
+  f4add(a0, a1);
+  f4add(a2, a3);
+  f4add(a0, a2);
+  red[g][q * 4 + 0] = a0.x;
+  red[g][q * 4 + 1] = a0.y;
+  red[g][q * 4 + 2] = a0.z;
+  red[g][q * 4 + 3] = a0.w;
+  __syncthreads();
+  {  // level 2: thread (k, j) adds row groups 4k..4k+3 of column j
+    const int j = threadIdx.x & 63, k = threadIdx.x >> 6;
+    red2[k][j] = (red[4 * k][j] + red[4 * k + 1][j]) + (red[4 * k + 2][j] + red[4 * k + 3][j]);
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int j = blockIdx.x * 64 + threadIdx.x;
+    if (j < H) {
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) s += red2[k][threadIdx.x];
+      dw[j] += s;
+    }
   }
 }
 

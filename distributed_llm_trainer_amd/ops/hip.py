@@ -266,15 +266,15 @@ def embedding_bwd(ids: torch.Tensor, dout: torch.Tensor, dweight: torch.Tensor) 
     (rocPRIM radix sort via torch.sort), the kernels sum each run in position order
     with one writer per row (no float atomics)."""
     ids = ids.reshape(-1)
-    if ids.dtype != torch.int64:
-        ids = ids.long()
     M = ids.numel()
     H = dweight.shape[-1]
     _req(dout, torch.float32, "embedding_bwd.dout", M * H)
     _req(dweight, torch.float32, "embedding_bwd.dweight")
     if M == 0:
         return
-    sids, perm = torch.sort(ids, stable=True)
+    if dweight.shape[0] >= 2 ** 31:
+        raise ValueError("embedding_bwd: vocabulary too large for int32 ids")
+    sids, perm = torch.sort(ids.to(torch.int32), stable=True)  # 32-bit keys: half the radix passes
     ch = lib().dlt_embedding_bwd_chunk()
     ws = torch.empty(2 * (-(-M // ch)) * H, dtype=torch.float32, device=dout.device)
     _chk(lib().dlt_embedding_bwd(_p(sids), _p(perm), _p(dout), _p(dweight), _p(ws), M, H, dweight.shape[0],

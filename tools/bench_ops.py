@@ -65,6 +65,14 @@ rec("cross-entropy fwd+bwd", timeit(lambda: hip.cross_entropy_fwd_bwd(logits, tg
 ids = torch.randint(0, 50257, (M,), device=dev)
 emb = torch.randn(V, H, device=dev)
 rec("embedding fwd", timeit(lambda: hip.embedding_fwd(ids, emb)), M * H * 8)
+dout = torch.randn(M, H, device=dev)
+demb = torch.zeros(V, H, device=dev)
+rec("embedding bwd (sort + segment-sum, uniform ids)", timeit(lambda: hip.embedding_bwd(ids, dout, demb)),
+    M * H * 12)
+zipf = torch.minimum((torch.rand(M, device=dev) ** 4 * 50257).long(), torch.tensor(50256, device=dev))
+rec("embedding bwd (sort + segment-sum, zipf-like ids)", timeit(lambda: hip.embedding_bwd(zipf, dout, demb)),
+    M * H * 12)
+rec("torch.sort of the ids (part of the above)", timeit(lambda: torch.sort(ids, stable=True)), M * 16)
 P = 151_862_784
 p_, g_, m_, v_ = (torch.zeros(P, device=dev) for _ in range(4))
 sh = torch.zeros(P, device=dev, dtype=torch.bfloat16)
