@@ -26,6 +26,7 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+import distributed_llm_trainer_amd  # noqa: E402,F401  (GPU_MAX_HW_QUEUES before the HIP runtime starts)
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
