@@ -368,3 +368,33 @@ def test_training_is_bitwise_reproducible():
         res.append((losses, tr.store.flat.detach().clone()))
     assert res[0][0] == res[1][0], (res[0][0], res[1][0])
     assert torch.equal(res[0][1], res[1][1]), (res[0][1] - res[1][1]).abs().max().item()
+
+
+def test_checkpoint_resume_is_exact_gpu(tmp_path):
+    """DDP-path trainer on the GPU: 2 steps, save, a fresh trainer loads the file and runs
+    2 more steps == 4 uninterrupted steps, bit for bit (dropout streams continue at the
+    saved micro-step counter, AdamW moments/step restored, bf16 shadow re-derived; the
+    gradient reductions are fixed-order)."""
+    from distributed_llm_trainer_amd.training.configs import TrainingConfig
+    from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
+    data = [torch.randint(0, 1000, (8, 256), device=DEV, generator=torch.Generator(DEV).manual_seed(40 + s))
+            for s in range(4)]
+
+    def trainer():
+        torch.manual_seed(4)
+        tc = TrainingConfig(batch_size=2, gradient_accumulation_steps=4, warmup_steps=1, learning_rate=1e-3,
+                            max_steps=10)
+        return DistributedTrainer(_cfg(0.1), tc)
+
+    a = trainer()
+    la = [a.train_step({"input_ids": data[s]})["loss"] for s in range(4)]
+    b = trainer()
+    lb = [b.train_step({"input_ids": data[s]})["loss"] for s in range(2)]
+    path = str(tmp_path / "step2.pt")
+    b.save_checkpoint(path)
+    del b
+    c = trainer()
+    c.load_checkpoint(path)
+    lb += [c.train_step({"input_ids": data[s]})["loss"] for s in range(2, 4)]
+    assert la == lb, (la, lb)
+    assert torch.equal(a.store.flat, c.store.flat), (a.store.flat - c.store.flat).abs().max().item()
