@@ -115,6 +115,15 @@ def gemm_plan_hook() -> None:
     gemm.maybe_save_plan()
 
 
+def global_mean_loss(total: torch.Tensor, world: int) -> float:
+    """Mean of the ranks' step losses (the reference logs rank 0's local
+    loss; that line is kept, the metrics JSONL also gets this).  A collective: every
+    rank must call it on the same steps."""
+    t = total.detach().reshape(1).float().clone()
+    dist.all_reduce(t)
+    return float(t.item()) / world
+
+
 def unwrap_batch(batch):
     if isinstance(batch, dict):
         return batch["input_ids"]

@@ -40,7 +40,7 @@ from ..parallel.flat import FlatParamStore
 from ..utils import checkpoint as ckpt
 from ..utils import debug as dbg
 from ..utils.profiling import Profiler, range_push, range_pop
-from .common import cosine_lr, gemm_plan_hook, memory_stats, micro_step_fusion, seed_all, select_device, setup_distributed, unwrap_batch
+from .common import cosine_lr, gemm_plan_hook, global_mean_loss, memory_stats, micro_step_fusion, seed_all, select_device, setup_distributed, unwrap_batch
 from .configs import TrainingConfig
 from .optim import flat_store_optimizer
 
@@ -224,6 +224,8 @@ class DistributedTrainer:
         if self.use_engine and self.global_step >= 2:
             gemm_plan_hook()
         out = {"loss": total.item() if sync_loss else total, "lr": lr, "tokens": self.tokens_seen}
+        if sync_loss and self.distributed and self.world_size > 1:
+            out["loss_global"] = global_mean_loss(total, self.world_size)
         return out
 
     # ------------------------------------------------------------ checkpoints
@@ -374,6 +376,7 @@ def main(argv=None):
                   flush=True)
             if metrics_f:
                 rec = {"step": step, "loss": metrics["loss"], "lr": metrics["lr"], "tokens": metrics["tokens"],
+                       **({"loss_global": metrics["loss_global"]} if "loss_global" in metrics else {}),
                        "tokens_per_sec": tps, **trainer.get_memory_stats()}
                 if trainer._last_norm is not None:
                     rec["grad_norm"] = float(trainer._last_norm)

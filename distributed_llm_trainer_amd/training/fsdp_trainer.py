@@ -33,7 +33,7 @@ from ..parallel.fsdp import FSDPRuntime
 from ..utils import checkpoint as ckpt
 from ..utils import debug as dbg
 from ..utils.profiling import Profiler
-from .common import cosine_lr, gemm_plan_hook, memory_stats, micro_step_fusion, seed_all, select_device, setup_distributed, unwrap_batch
+from .common import cosine_lr, gemm_plan_hook, global_mean_loss, memory_stats, micro_step_fusion, seed_all, select_device, setup_distributed, unwrap_batch
 from .configs import FSDPConfig, FSDPTrainingConfig
 from .optim import FlatAdamW
 
@@ -183,7 +183,10 @@ class FSDPTrainer:
         self.tokens_seen += input_ids.numel() * self.world_size
         if self.global_step >= 2:
             gemm_plan_hook()
-        return {"loss": total.item() if sync_loss else total, "lr": lr, "tokens": self.tokens_seen}
+        out = {"loss": total.item() if sync_loss else total, "lr": lr, "tokens": self.tokens_seen}
+        if sync_loss and self.distributed and self.world_size > 1:
+            out["loss_global"] = global_mean_loss(total, self.world_size)
+        return out
 
     # ------------------------------------------------------------ checkpoints
     def _full_state(self):
@@ -456,6 +459,7 @@ def main(argv=None):
                   f"Tokens/s: {tps:,.0f} | Mem: {mem['allocated_gb']:.1f}GB", flush=True)
             if metrics_f:
                 rec = {"step": step, "loss": metrics["loss"], "lr": metrics["lr"], "tokens": metrics["tokens"],
+                       **({"loss_global": metrics["loss_global"]} if "loss_global" in metrics else {}),
                        "tokens_per_sec": tps, **mem}
                 if trainer._last_norm is not None:
                     rec["grad_norm"] = float(trainer._last_norm)

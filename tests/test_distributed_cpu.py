@@ -344,3 +344,20 @@ def test_forced_collectives_on_one_rank_are_identity(mode, strategy):
         assert launched > 2
     for k in a:
         assert torch.equal(a[k], b[k]), k
+
+
+def _loss_worker(rank, world):
+    from distributed_llm_trainer_amd.models.config import GPTConfig
+    from distributed_llm_trainer_amd.training.configs import TrainingConfig
+    from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
+    tr = DistributedTrainer(GPTConfig(**TINY), TrainingConfig(batch_size=2, gradient_accumulation_steps=2,
+                                                              warmup_steps=1, max_steps=10))
+    m = tr.train_step({"input_ids": _data(0, rank, n=4)})
+    return m["loss"], m["loss_global"]
+
+
+def test_logged_global_loss_is_the_rank_mean():
+    """the log line keeps rank 0's local loss; the metrics also carry the
+    mean over ranks (one scalar all-reduce on logged steps)."""
+    (l0, g0), (l1, g1) = run_multiprocess(_loss_worker, world=2)
+    assert g0 == g1 and abs(g0 - (l0 + l1) / 2) < 1e-6 and l0 != l1
