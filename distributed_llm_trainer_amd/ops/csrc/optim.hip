@@ -10,6 +10,7 @@
 //  * k_adamw: decoupled weight decay + bias-corrected Adam on the flat buffer, also
 //    writing the bf16 shadow weights the GEMMs consume.
 #include "common.h"
+#include <cstdlib>
 
 // Deterministic two-stage sum of squares: every block writes its partial, one block
 // adds the partials in a fixed order.  (A float atomicAdd per block made the sum --
@@ -71,6 +72,32 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
   p -= step_size * m / denom;
 }
 
+// Streaming access for the optimizer pass: every byte is touched once per step (the
+// 4.3 GB of p/g/m/v/shadow for GPT-2 small far exceed the 256 MB Infinity Cache), so
+// nontemporal loads/stores keep it from evicting anything useful (DLT_ADAMW_NT=0: plain).
+template <bool NTM>
+__device__ __forceinline__ float4 ld4(const float* a, int64_t i) {
+  if (NTM) {
+    const float4* q = reinterpret_cast<const float4*>(a) + i;
+    return make_float4(__builtin_nontemporal_load(&q->x), __builtin_nontemporal_load(&q->y),
+                       __builtin_nontemporal_load(&q->z), __builtin_nontemporal_load(&q->w));
+  }
+  return reinterpret_cast<const float4*>(a)[i];
+}
+template <bool NTM>
+__device__ __forceinline__ void st4(float* a, int64_t i, float4 x) {
+  if (NTM) {
+    float4* q = reinterpret_cast<float4*>(a) + i;
+    __builtin_nontemporal_store(x.x, &q->x);
+    __builtin_nontemporal_store(x.y, &q->y);
+    __builtin_nontemporal_store(x.z, &q->z);
+    __builtin_nontemporal_store(x.w, &q->w);
+  } else {
+    reinterpret_cast<float4*>(a)[i] = x;
+  }
+}
+
+template <bool NTM>
 __global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                                                float* __restrict__ v, bf16_t* __restrict__ shadow, int64_t n, float lr,
                                                float b1, float b2, float eps, float wd, float step_size,
@@ -83,23 +110,30 @@ __global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, const floa
     adam_elem(pp.y, gg.y * gs, mm.y, vv.y, lr, b1, b2, eps, wd, step_size, inv_bc2_sqrt);
     adam_elem(pp.z, gg.z * gs, mm.z, vv.z, lr, b1, b2, eps, wd, step_size, inv_bc2_sqrt);
     adam_elem(pp.w, gg.w * gs, mm.w, vv.w, lr, b1, b2, eps, wd, step_size, inv_bc2_sqrt);
-    reinterpret_cast<float4*>(p)[i] = pp;
-    reinterpret_cast<float4*>(m)[i] = mm;
-    reinterpret_cast<float4*>(v)[i] = vv;
+    st4<NTM>(p, i, pp);
+    st4<NTM>(m, i, mm);
+    st4<NTM>(v, i, vv);
     if (shadow) {
       u16x4 s;
       s.v[0] = f2bf(pp.x); s.v[1] = f2bf(pp.y); s.v[2] = f2bf(pp.z); s.v[3] = f2bf(pp.w);
-      reinterpret_cast<u16x4*>(shadow)[i] = s;
+      if (NTM) {
+        const uint2 w = __builtin_bit_cast(uint2, s);
+        uint32_t* q = reinterpret_cast<uint32_t*>(shadow) + 2 * i;
+        __builtin_nontemporal_store(w.x, q);
+        __builtin_nontemporal_store(w.y, q + 1);
+      } else {
+        reinterpret_cast<u16x4*>(shadow)[i] = s;
+      }
     }
   };
   // two independent float4 groups per iteration: 8 loads in flight per thread
   int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   for (; i + stride < n4; i += 2 * stride) {
     const int64_t j = i + stride;
-    const float4 p0 = reinterpret_cast<const float4*>(p)[i], p1 = reinterpret_cast<const float4*>(p)[j];
-    const float4 g0 = reinterpret_cast<const float4*>(g)[i], g1 = reinterpret_cast<const float4*>(g)[j];
-    const float4 m0 = reinterpret_cast<const float4*>(m)[i], m1 = reinterpret_cast<const float4*>(m)[j];
-    const float4 v0 = reinterpret_cast<const float4*>(v)[i], v1 = reinterpret_cast<const float4*>(v)[j];
+    const float4 p0 = ld4<NTM>(p, i), p1 = ld4<NTM>(p, j);
+    const float4 g0 = ld4<NTM>(g, i), g1 = ld4<NTM>(g, j);
+    const float4 m0 = ld4<NTM>(m, i), m1 = ld4<NTM>(m, j);
+    const float4 v0 = ld4<NTM>(v, i), v1 = ld4<NTM>(v, j);
     upd(i, p0, g0, m0, v0);
     upd(j, p1, g1, m1, v1);
   }
@@ -147,7 +181,17 @@ DLT_API int dlt_adamw(float* p, const float* g, float* m, float* v, bf16_t* shad
                       hipStream_t st) {
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return -1;
   if (shadow && ((uintptr_t)shadow & 7)) return -1;
-  k_adamw<<<flat_blocks(n), 256, 0, st>>>(p, g, m, v, shadow, n, lr, b1, b2, eps, wd, step_size, inv_bc2_sqrt, gscale);
+  static int nt = -1;
+  if (nt < 0) {
+    const char* e = getenv("DLT_ADAMW_NT");
+    nt = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  if (nt)
+    k_adamw<true><<<flat_blocks(n), 256, 0, st>>>(p, g, m, v, shadow, n, lr, b1, b2, eps, wd, step_size, inv_bc2_sqrt,
+                                                  gscale);
+  else
+    k_adamw<false><<<flat_blocks(n), 256, 0, st>>>(p, g, m, v, shadow, n, lr, b1, b2, eps, wd, step_size, inv_bc2_sqrt,
+                                                   gscale);
   DLT_CHECK_LAUNCH();
 }
 
