@@ -61,3 +61,12 @@ def test_bench_torchrun_two_ranks_contract():
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2"] + ARGS
     out = _run(cmd)
     _check(out, 2, 2, 1)
+
+
+def test_bench_torchrun_eight_ranks_contract():
+    """The driver's largest launch (8 ranks, one node) rehearsed over gloo on the CPU:
+    bucket all-reduces across 8 ranks, the max-over-ranks timing, one JSON line."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "8"] + ARGS
+    out = _run(cmd)
+    _check(out, 8, 2, 1)
