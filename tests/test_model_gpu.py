@@ -397,3 +397,47 @@ def test_checkpoint_resume_is_exact_gpu(tmp_path):
     lb += [c.train_step({"input_ids": data[s]})["loss"] for s in range(2, 4)]
     assert la == lb, (la, lb)
     assert torch.equal(a.store.flat, c.store.flat), (a.store.flat - c.store.flat).abs().max().item()
+
+
+def _fsdp_run(strategy="FULL_SHARD", offload=False, steps=3):
+    from distributed_llm_trainer_amd.training.configs import FSDPConfig, FSDPTrainingConfig
+    from distributed_llm_trainer_amd.training.fsdp_trainer import FSDPTrainer
+    data = torch.randint(0, 1000, (8, 256), device=DEV, generator=torch.Generator(DEV).manual_seed(21))
+    torch.manual_seed(21)
+    tc = FSDPTrainingConfig(batch_size=2, gradient_accumulation_steps=4, warmup_steps=1, learning_rate=1e-3)
+    tr = FSDPTrainer(_cfg(0.1), tc, FSDPConfig(sharding_strategy=strategy, cpu_offload=offload))
+    losses = [tr.train_step({"input_ids": data})["loss"] for _ in range(steps)]
+    return losses, {k: v.float().cpu().clone() for k, v in tr.runtime.state_dict_full().items()}
+
+
+@pytest.mark.parametrize("strategy", ["SHARD_GRAD_OP", "NO_SHARD", "HYBRID_SHARD"])
+def test_fsdp_strategies_match_full_shard_gpu(strategy):
+    """On one GPU every sharding strategy runs the same math as FULL_SHARD (only the
+    residency / collective schedule differs): bit-identical parameters."""
+    la, pa = _fsdp_run()
+    lb, pb = _fsdp_run(strategy)
+    assert la == lb, (la, lb)
+    for k in pa:
+        assert torch.equal(pa[k], pb[k]), k
+
+
+def test_fsdp_cpu_offload_gpu():
+    """CPU offload on the GPU: fp32 shards and AdamW on the host, the bf16 shards copied
+    to the device after each step, reduced gradients copied back.  Two offloaded runs
+    are bit-identical (no race between the host optimizer and the copies), and they
+    train like the on-device optimizer: the host computes the clip norm and AdamW in
+    another rounding order, and a last-bit change in a master weight can flip its bf16
+    shadow and is amplified by AdamW's m / sqrt(v) for near-zero gradients, so single
+    elements may drift by up to a couple of updates (lr) while the mean stays tiny."""
+    la, pa = _fsdp_run()
+    lb, pb = _fsdp_run(offload=True)
+    lc, pc = _fsdp_run(offload=True)
+    assert lb == lc, (lb, lc)
+    for k in pb:
+        assert torch.equal(pb[k], pc[k]), k
+    for a, b in zip(la, lb):
+        assert abs(a - b) <= 1e-4 * abs(a), (la, lb)
+    for k in pa:
+        d = (pa[k] - pb[k]).abs()
+        assert d.max().item() <= 2e-3, (k, d.max().item())
+        assert d.mean().item() <= 1e-5, (k, d.mean().item())
