@@ -2,6 +2,7 @@
 running the PyTorch reference ops on the GPU (identical dropout masks) and (b) the
 eager autocast model (dropout off)."""
 import copy
+import math
 
 import pytest
 import torch
@@ -441,3 +442,23 @@ def test_fsdp_cpu_offload_gpu():
         d = (pa[k] - pb[k]).abs()
         assert d.max().item() <= 2e-3, (k, d.max().item())
         assert d.mean().item() <= 1e-5, (k, d.mean().item())
+
+
+@pytest.mark.parametrize("mp", ["fp16", "fp32"])
+def test_ddp_trainer_fp16_fp32_gpu(mp):
+    """The reference's other --mixed_precision settings on the GPU (eager module path:
+    fp16 autocast with dynamic loss scaling, or fp32): the loss starts where the bf16
+    engine's does and goes down."""
+    from distributed_llm_trainer_amd.training.configs import TrainingConfig
+    from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
+    data = torch.randint(0, 1000, (8, 256), device=DEV, generator=torch.Generator(DEV).manual_seed(5))
+    res = {}
+    for m in ("bf16", mp):
+        torch.manual_seed(5)
+        tc = TrainingConfig(batch_size=2, gradient_accumulation_steps=4, warmup_steps=1, learning_rate=3e-3,
+                            mixed_precision=m)
+        tr = DistributedTrainer(_cfg(0.0), tc)
+        res[m] = [tr.train_step({"input_ids": data})["loss"] for _ in range(6)]
+    assert all(math.isfinite(x) for x in res[mp]), res
+    assert abs(res[mp][0] - res["bf16"][0]) < 2e-2 * res["bf16"][0], res
+    assert res[mp][-1] < res[mp][0] - 0.05, res
