@@ -66,3 +66,20 @@ def test_cli_fault_injection_resume_is_exact_gpu(module, tmp_path):
         assert torch.equal(a["model"][k], b["model"][k]), k
     for i, st in a["optimizer"]["state"].items():
         assert torch.equal(st["exp_avg_sq"], b["optimizer"]["state"][i]["exp_avg_sq"]), i
+
+
+def test_infer_cli_gpu(tmp_path):
+    """Train a tiny model through the DDP CLI on the GPU, then generate from its
+    final.pt with the reference-compatible infer CLI (KV-cached HIP-graph decode)."""
+    ck = str(tmp_path / "ck")
+    r = _run("distributed_llm_trainer_amd.training.ddp_trainer", ["--max_steps", "3", "--checkpoint_dir", ck], {},
+             tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    env = dict(os.environ)
+    env.pop("DLT_FORCE_CPU", None)
+    r = subprocess.run([sys.executable, "src/eval/infer.py", "--checkpoint", os.path.join(ck, "final.pt"),
+                        "--prompt", "Once upon a time,", "--max_new_tokens", "24", "--seed", "1"],
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))), env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "Once upon a time," in r.stdout, r.stdout[-2000:]
