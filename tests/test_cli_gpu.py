@@ -2,6 +2,7 @@
 the reference-compatible DDP and FSDP trainer CLIs, killed mid-way by fault injection
 and resumed, land on the uninterrupted run's weights bit for bit (every gradient
 reduction is fixed-order, dropout streams and the data stream resume exactly)."""
+import math
 import os
 import subprocess
 import sys
@@ -83,3 +84,21 @@ def test_infer_cli_gpu(tmp_path):
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "Once upon a time," in r.stdout, r.stdout[-2000:]
+
+
+@pytest.mark.parametrize("streaming", [False, True])
+def test_text_dataset_cli_gpu(tmp_path, streaming):
+    """The TinyStories / OpenWebText paths on the GPU: a text corpus (gzip for the
+    OpenWebText loader), tokenised offline, streamed or map-style, through the engine."""
+    import gzip
+    story = "Once upon a time, a little fox found a shiny stone near the river. " * 8
+    text = "\n".join(f"{i}: {story}" for i in range(400))
+    p = tmp_path / "corpus.txt.gz"
+    with gzip.open(p, "wt") as f:
+        f.write(text)
+    args = ["--max_steps", "4", "--checkpoint_dir", str(tmp_path / "ck"), "--dataset", "openwebtext",
+            "--data_path", str(p), "--no_final_save"] + (["--streaming"] if streaming else [])
+    r = _run("distributed_llm_trainer_amd.training.ddp_trainer", args, {}, tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    losses = [float(ln.split("Loss:")[1].split("|")[0]) for ln in r.stdout.splitlines() if "Loss:" in ln]
+    assert len(losses) == 4 and all(math.isfinite(x) for x in losses), r.stdout[-2000:]
