@@ -8,11 +8,15 @@
 // and for rows whose target is ignore_index), so no fp32 logits or separate
 // softmax-backward kernel ever exist.
 //
-// k_ce_row: one 512-thread block per row holds the whole row in registers (CPT
-// 16-byte chunks per thread: 13 for Vp = 50304, i.e. 52 VGPRs), so HBM sees exactly
-// one read and one write of the logits (the memory-bound minimum).  Rows too long for
-// that fall back to k_ce_fwd_bwd (online max/sum pass + gradient pass).
+// k_ce_row: one block per row holds the whole row in registers, so HBM sees exactly
+// one read and one write of the logits (the memory-bound minimum).  Default for
+// Vp <= 57344: 1024 threads x 7 16-byte chunks, held to 64 VGPRs (8 waves per SIMD,
+// two rows per CU in flight): 320 us vs 346 us per 8192 x 50304 call for 512 threads
+// x 13 chunks (94 VGPRs, five waves per SIMD), bench step -0.1 to -0.2 ms
+// (scripts/ab_ce.sh; DLT_CE_THREADS=512 selects the older shape).  Rows too long for
+// registers fall back to k_ce_fwd_bwd (online max/sum pass + gradient pass).
 #include "common.h"
+#include <cstdlib>
 
 __global__ __launch_bounds__(256) void k_ce_fwd_bwd(bf16_t* __restrict__ logits, const int64_t* __restrict__ targets,
                                                     const int64_t* __restrict__ n_valid, float* __restrict__ loss_rows,
@@ -79,14 +83,14 @@ __global__ __launch_bounds__(256) void k_ce_fwd_bwd(bf16_t* __restrict__ logits,
   }
 }
 
-template <int CPT>
-__global__ __launch_bounds__(512) void k_ce_row(bf16_t* __restrict__ logits, const int64_t* __restrict__ targets,
+template <int CPT, int NTH = 512>
+__global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH == 1024 ? 8 : 1, 8))) void k_ce_row(bf16_t* __restrict__ logits, const int64_t* __restrict__ targets,
                                                 const int64_t* __restrict__ n_valid, float* __restrict__ loss_rows,
                                                 int M, int Vp, int V) {
   // Per element only: max, one exp2 for the sum, one exp2 + scale for the gradient.
   // Column bounds are tested per 8-wide chunk (only the last chunk straddles V), and
   // the target column is patched by its owning thread per chunk, not per element.
-  __shared__ float red[8];
+  __shared__ float red[NTH / 64];
   const int row = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   bf16_t* lrow = logits + (size_t)row * Vp;
@@ -99,7 +103,7 @@ __global__ __launch_bounds__(512) void k_ce_row(bf16_t* __restrict__ logits, con
   uint4 x[CPT];  // 8 bf16 per chunk as 4 packed words
 #pragma unroll
   for (int t = 0; t < CPT; ++t) {
-    const int c = tid + 512 * t;
+    const int c = tid + NTH * t;
     if (c < nchunk) x[t] = *reinterpret_cast<const uint4*>(lrow + c * 8);
   }
   auto el = [&](int t, int e) -> float {
@@ -117,7 +121,7 @@ __global__ __launch_bounds__(512) void k_ce_row(bf16_t* __restrict__ logits, con
   float mx = -INFINITY;
 #pragma unroll
   for (int t = 0; t < CPT; ++t) {
-    const int c = tid + 512 * t;
+    const int c = tid + NTH * t;
     if (c * 8 + 8 <= V) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) mx = fmaxf(mx, el(t, e));
@@ -133,13 +137,13 @@ __global__ __launch_bounds__(512) void k_ce_row(bf16_t* __restrict__ logits, con
   __syncthreads();
   float gm = red[0];
 #pragma unroll
-  for (int w = 1; w < 8; ++w) gm = fmaxf(gm, red[w]);
+  for (int w = 1; w < NTH / 64; ++w) gm = fmaxf(gm, red[w]);
   __syncthreads();
   const float nm2 = -gm * L2E;
   float sm = 0.f;
 #pragma unroll
   for (int t = 0; t < CPT; ++t) {
-    const int c = tid + 512 * t;
+    const int c = tid + NTH * t;
     if (c * 8 + 8 <= V) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) sm += __builtin_amdgcn_exp2f(fmaf(el(t, e), L2E, nm2));
@@ -155,14 +159,14 @@ __global__ __launch_bounds__(512) void k_ce_row(bf16_t* __restrict__ logits, con
   __syncthreads();
   float gs = 0.f;
 #pragma unroll
-  for (int w = 0; w < 8; ++w) gs += red[w];
+  for (int w = 0; w < NTH / 64; ++w) gs += red[w];
   const float lse = gm + __logf(gs);
   const int64_t nv = *n_valid;
   const float inv_n = valid ? 1.f / (float)(nv > 0 ? nv : 1) : 0.f;
   const float nl2 = -lse * L2E;
 #pragma unroll
   for (int t = 0; t < CPT; ++t) {
-    const int c = tid + 512 * t;
+    const int c = tid + NTH * t;
     if (c < nchunk) {
       u16x8 o;
       if (c * 8 + 8 <= V) {
@@ -194,6 +198,15 @@ DLT_API int dlt_cross_entropy_fwd_bwd(bf16_t* logits, const int64_t* targets, co
   if (Vp % 8 || V > Vp) return -1;
   const int cpt = (Vp / 8 + 511) / 512;
 #define CE_ARGS logits, targets, n_valid, loss_rows, M, Vp, V
+  static int wide = -1;
+  if (wide < 0) {
+    const char* e = getenv("DLT_CE_THREADS");
+    wide = (e && atoi(e) == 512) ? 0 : 1;
+  }
+  if (wide && (Vp / 8 + 1023) / 1024 <= 7) {  // 1024 threads x 7 chunks (Vp <= 57344)
+    k_ce_row<7, 1024><<<M, 1024, 0, st>>>(CE_ARGS);
+    DLT_CHECK_LAUNCH();
+  }
   if (cpt <= 1) k_ce_row<1><<<M, 512, 0, st>>>(CE_ARGS);
   else if (cpt <= 2) k_ce_row<2><<<M, 512, 0, st>>>(CE_ARGS);
   else if (cpt <= 4) k_ce_row<4><<<M, 512, 0, st>>>(CE_ARGS);
