@@ -45,7 +45,7 @@ class DDPRuntime:
         # DLT_FORCE_COLLECTIVES=1: issue every collective even on one rank, so a one-GPU
         # box runs the multi-GPU code path (RCCL kernels launched from the weight-gradient
         # stream, waits, the bucket schedule) with a result that must equal no collectives
-        self.force = dist.is_initialized() and os.environ.get("DLT_FORCE_COLLECTIVES") == "1"
+        self.force = dist.is_initialized() and self.world == 1 and os.environ.get("DLT_FORCE_COLLECTIVES") == "1"
         self.launched = 0
         self.handles: List[Tuple[object, Optional[torch.Tensor], int, int]] = []
         lay = store.layout

@@ -126,7 +126,7 @@ class FSDPRuntime(ParamProvider):
         self.world = dist.get_world_size() if self.dist else 1
         # DLT_FORCE_COLLECTIVES=1 (see parallel/ddp.py): one rank still all-gathers and
         # reduce-scatters through the process group instead of aliasing its shard
-        self.force = self.dist and os.environ.get("DLT_FORCE_COLLECTIVES") == "1"
+        self.force = self.dist and self.world == 1 and os.environ.get("DLT_FORCE_COLLECTIVES") == "1"
         self.units: Dict[object, FlatUnit] = {}
         self._build_units(model)
         self._free_module_params(model)
