@@ -96,3 +96,23 @@ def test_debug_kernel_library_builds():
     from distributed_llm_trainer_amd.ops import build as kb
     path = kb.build(verbose=False, debug=True)
     assert path.endswith("_dlt_kernels_debug.so") and os.path.exists(path)
+
+
+@pytest.mark.parametrize("given,knob,expect", [("4", None, "16"), (None, None, "16"), ("32", None, "32"),
+                                               ("4", "0", "4"), ("4", "8", "8")])
+def test_package_import_raises_hw_queues(given, knob, expect):
+    """Importing the package raises GPU_MAX_HW_QUEUES before the HIP runtime starts
+    (profiles/r2_hw_queues.md); DLT_HW_QUEUES sets the minimum, 0 leaves it alone."""
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("GPU_MAX_HW_QUEUES", "DLT_HW_QUEUES")}
+    if given is not None:
+        env["GPU_MAX_HW_QUEUES"] = given
+    if knob is not None:
+        env["DLT_HW_QUEUES"] = knob
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", "import os, distributed_llm_trainer_amd; "
+                        "print(os.environ.get('GPU_MAX_HW_QUEUES'))"], cwd=root, env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == expect
