@@ -15,6 +15,7 @@
 // The residual stream is fp32 (matches the reference DDP/autocast numerics, SURVEY
 // §2.4 P9).
 #include "common.h"
+#include <cstdlib>
 
 struct f4 { float v[4]; };
 
@@ -42,7 +43,12 @@ __device__ __forceinline__ f4 ld_w4(const void* w, int wbf16, int off) {
   return ld_f4(reinterpret_cast<const float*>(w) + off);
 }
 
-template <int NCH>
+__device__ __forceinline__ void st_f4_nt(float* p, const float (&v)[4]) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) __builtin_nontemporal_store(v[e], p + e);
+}
+
+template <int NCH, bool XNT = false>
 __global__ __launch_bounds__(256) void k_add_dropout_rmsnorm_fwd(
     const float* __restrict__ resid, const bf16_t* __restrict__ delta, const void* __restrict__ w, int wbf16,
     float* __restrict__ x_out, bf16_t* __restrict__ y_out, float* __restrict__ rstd_out,
@@ -93,7 +99,10 @@ __global__ __launch_bounds__(256) void k_add_dropout_rmsnorm_fwd(
     const int c = lane + 64 * t;
     if (c < nc) {
       const size_t off = rbase + (size_t)c * 4;
-      if (x_out) st_f4(x_out + off, xv[t]);
+      if (x_out) {  // the fp32 block input is read again only by the backward
+        if (XNT) st_f4_nt(x_out + off, xv[t]);
+        else st_f4(x_out + off, xv[t]);
+      }
       const f4 ww = ld_w4(w, wbf16, c * 4);
       u16x4 y;
 #pragma unroll
@@ -269,6 +278,18 @@ static inline int nch_of(int H) {
   return n;
 }
 
+// H = 768: the fp32 block input goes out with nontemporal stores (it is read again only
+// by the backward, ~10 ms later): step -0.03 / -0.08 / -0.06 ms in three same-box pairs;
+// DLT_FWD_NT=0 selects plain stores
+static int fwd_nt() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DLT_FWD_NT");
+    v = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  return v;
+}
+
 DLT_API int dlt_add_dropout_rmsnorm_fwd(const float* resid, const bf16_t* delta, const void* w, int wbf16,
                                         float* x_out, bf16_t* y_out, float* rstd_out, int M, int H,
                                         float eps, uint32_t key, uint32_t thr, float dscale,
@@ -280,7 +301,10 @@ DLT_API int dlt_add_dropout_rmsnorm_fwd(const float* resid, const bf16_t* delta,
   switch (nch) {
     case 1: k_add_dropout_rmsnorm_fwd<1><<<grid, block, 0, stream>>>(ARGS); break;
     case 2: k_add_dropout_rmsnorm_fwd<2><<<grid, block, 0, stream>>>(ARGS); break;
-    case 3: k_add_dropout_rmsnorm_fwd<3><<<grid, block, 0, stream>>>(ARGS); break;
+    case 3:
+      if (fwd_nt()) k_add_dropout_rmsnorm_fwd<3, true><<<grid, block, 0, stream>>>(ARGS);
+      else k_add_dropout_rmsnorm_fwd<3><<<grid, block, 0, stream>>>(ARGS);
+      break;
     case 4: k_add_dropout_rmsnorm_fwd<4><<<grid, block, 0, stream>>>(ARGS); break;
     case 5: k_add_dropout_rmsnorm_fwd<5><<<grid, block, 0, stream>>>(ARGS); break;
     case 6: k_add_dropout_rmsnorm_fwd<6><<<grid, block, 0, stream>>>(ARGS); break;
