@@ -143,6 +143,7 @@ def main():
             from distributed_llm_trainer_amd.ops import gemm as gemm_mod
             if gemm_mod.available():
                 print(gemm_mod.report(), file=sys.stderr)
+                print(json.dumps(gemm_mod.race_report(), indent=1), file=sys.stderr)
     if trainer.distributed:
         dist.barrier()
         dist.destroy_process_group()

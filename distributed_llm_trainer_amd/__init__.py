@@ -23,13 +23,33 @@ def _ensure_hw_queues() -> None:
     The runtime reads the variable once, when it initialises (first GPU call), so this
     runs at import.  ``DLT_HW_QUEUES`` sets the minimum (0 = leave the variable alone).
     """
-    want = int(_os.environ.get("DLT_HW_QUEUES", "16"))
+    try:
+        want = int(_os.environ.get("DLT_HW_QUEUES", "16"))
+    except ValueError:
+        want = 16
     try:
         have = int(_os.environ.get("GPU_MAX_HW_QUEUES", "4"))
     except ValueError:
         have = 4
     if want > 0 and have < want:
-        _os.environ["GPU_MAX_HW_QUEUES"] = str(min(want, 32))
+        new = str(min(want, 32))
+        _os.environ["GPU_MAX_HW_QUEUES"] = new
+        # tell the host application once (rank 0 only) that its HIP runtime config changed
+        if _os.environ.get("RANK", "0") == "0" and _os.environ.get("DLT_QUIET", "0") != "1":
+            import sys
+            late = False
+            torch = sys.modules.get("torch")
+            if torch is not None:
+                try:
+                    late = bool(torch.cuda.is_initialized())
+                except Exception:  # pragma: no cover
+                    late = False
+            msg = (f"[distributed_llm_trainer_amd] GPU_MAX_HW_QUEUES {have} -> {new} "
+                   "(engine streams; DLT_HW_QUEUES=0 keeps the runtime default)")
+            if late:
+                msg += ("; WARNING: the HIP runtime is already initialised in this process, "
+                        "so the new value has no effect (import this package before the first GPU call)")
+            print(msg, file=sys.stderr, flush=True)
 
 
 _ensure_hw_queues()

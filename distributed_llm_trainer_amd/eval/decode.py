@@ -134,6 +134,10 @@ class DecodeGraph:
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):  # warm up allocations / library plans outside the capture
             for _ in range(2):
+                # the sampling step advances the device position: restart every warm-up
+                # step at ``pos`` so none writes K/V at pos + 1 (== max_seq_len when the
+                # prompt fills all but one slot)
+                self.pos.fill_(pos)
                 self._step()
         torch.cuda.current_stream(dev).wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
@@ -210,11 +214,22 @@ class DecodeGraph:
         return self.logits
 
 
+DEC_LDS_MAX = 160 * 1024  # bytes of LDS per workgroup on gfx950
+
+
 def _fused_ok(model, B: int) -> bool:
-    """The fused HIP decode step applies: HIP ops, a supported batch, head_dim 64."""
+    """The fused HIP decode step applies: HIP ops, a supported batch, head_dim 64, and
+    the LDS its kernels need fits one CU: ``k_dec_attn`` keeps all ``max_seq_len``
+    scores of a (batch, head) in LDS (maxS * 4 + 1056 B: max_seq_len <= ~40.7k), the
+    norm + GEMV kernels one normed bf16 row per batch entry (``dec_lds`` in decode.hip).
+    Beyond that ``DecodeGraph`` captures the ATen step instead."""
     ops = model.engine.ops
+    cfg = model.config
+    attn_lds = cfg.max_seq_len * 4 + 8 * 4 + 4 * 64 * 4
+    norm_lds = B * cfg.hidden_size * 2 + B * 4 * 4 + B * 16 * 4
     return (hasattr(ops, "dec_norm_qkv") and B in getattr(ops, "DECODE_BATCHES", ())
-            and model.config.head_dim == 64 and os.environ.get("DLT_DECODE_FUSED", "1") != "0")
+            and cfg.head_dim == 64 and attn_lds <= DEC_LDS_MAX and norm_lds <= DEC_LDS_MAX
+            and os.environ.get("DLT_DECODE_FUSED", "1") != "0")
 
 
 def _graph_ok(model, device) -> bool:

@@ -301,16 +301,30 @@ class GPTEngine:
         mask, mask_ev = self._attn_mask_async(B, S, pa, k_attn, dv)
         x, n1, rstd1 = ops.add_dropout_rmsnorm_fwd(r, d, w.ln1, self.eps, p_d, key_d, self.act_dtype,
                                                    y_out=sb("n1", H))
-        qkv = gm.linear(n1, w.wqkv)
+        fused_rope = self.packed_qkv and hasattr(gm, "linear_rope")
+        if fused_rope:  # QKV GEMM with RoPE on q/k in its epilogue (when that races faster)
+            qkv = gm.linear_rope(n1, w.wqkv, B, S, cfg.num_heads, cos, sin, ops)
+        else:
+            qkv = gm.linear(n1, w.wqkv)
         if mask is not None:
             torch.cuda.current_stream().wait_event(mask_ev)
         kw = {"mask": mask} if mask is not None else {}
         if pa > 0.0 and getattr(ops, "backend", "") == "hip":
-            # keep this layer's keep bits for the backward only within the memory budget
+            # keep this layer's keep bits for the backward only within the memory budget.
+            # The masks (two layouts, 1 bit per causal score: 8 * B * nh * S * ceil(S/32) B)
+            # grow with S^2, the saved block input (M * H * 4 B) with S: under activation
+            # checkpointing they are kept only while they cost at most as much as that
+            # input (S <= ~1k at GPT-2 shapes), so turning recompute on never keeps MORE
+            # than it saves (at S = 16k the masks are ~16x the input); the backward then
+            # regenerates them (one VALU kernel per layer, bit-identical bits).
             mask_bytes = 8 * B * cfg.num_heads * S * ((S + 31) // 32)
-            kw["store_mask"] = mask_bytes * cfg.num_layers <= self.attn_mask_budget
+            keep = mask_bytes * cfg.num_layers <= self.attn_mask_budget
+            if st.recompute:
+                keep = keep and mask_bytes <= M * H * 4
+            kw["store_mask"] = keep
         if self.packed_qkv:
-            ops.rope_qk_inplace(qkv, B, S, cfg.num_heads, cos, sin)
+            if not fused_rope:
+                ops.rope_qk_inplace(qkv, B, S, cfg.num_heads, cos, sin)
             o, lse = ops.attention_fwd_packed(qkv, B, S, cfg.num_heads, pa, k_attn, out=sb("o", H), **kw)
             q, k, v = qkv, None, None
         else:
@@ -321,8 +335,11 @@ class GPTEngine:
         x2, n2, rstd2 = ops.add_dropout_rmsnorm_fwd(x, a, w.ln2, self.eps, ph, k_resid, self.act_dtype,
                                                     y_out=sb("n2", H))
         del a
-        gu = gm.linear(n2, w.wgu)
-        s = ops.swiglu_fwd(gu, out=sb("s", I))
+        if hasattr(gm, "linear_swiglu"):  # gate/up GEMM with SwiGLU in its epilogue (when faster)
+            gu, s = gm.linear_swiglu(n2, w.wgu, ops, s_out=sb("s", I))
+        else:
+            gu = gm.linear(n2, w.wgu)
+            s = ops.swiglu_fwd(gu, out=sb("s", I))
         d_out = gm.linear(s, w.wdown)
         if save:
             c = _LayerCache(x=x, rstd1=rstd1, n1=n1, q=q, k=k, v=v, o=o, lse=lse,
@@ -349,8 +366,11 @@ class GPTEngine:
         sb = (lambda name, n: self._slot_buf(st, i, name, M, n, dv)[0]) if st.defer else (lambda name, n: None)
         _, n1, rstd1 = ops.add_dropout_rmsnorm_fwd(c.x, None, w.ln1, self.eps, 0.0, 0, self.act_dtype,
                                                    y_out=sb("n1", H))
-        qkv = gm.linear(n1, w.wqkv)
-        if self.packed_qkv:
+        if self.packed_qkv and hasattr(gm, "linear_rope"):
+            qkv = gm.linear_rope(n1, w.wqkv, B, S, cfg.num_heads, cos, sin, ops)
+            q, k, v = qkv, None, None
+        elif self.packed_qkv:
+            qkv = gm.linear(n1, w.wqkv)
             ops.rope_qk_inplace(qkv, B, S, cfg.num_heads, cos, sin)
             q, k, v = qkv, None, None
         else:
@@ -358,8 +378,11 @@ class GPTEngine:
         del qkv
         _, n2, rstd2 = ops.add_dropout_rmsnorm_fwd(c.x2, None, w.ln2, self.eps, 0.0, 0, self.act_dtype,
                                                    y_out=sb("n2", H))
-        gu = gm.linear(n2, w.wgu)
-        s = ops.swiglu_fwd(gu, out=sb("s", I))
+        if hasattr(gm, "linear_swiglu"):
+            gu, s = gm.linear_swiglu(n2, w.wgu, ops, s_out=sb("s", I))
+        else:
+            gu = gm.linear(n2, w.wgu)
+            s = ops.swiglu_fwd(gu, out=sb("s", I))
         return _LayerCache(x=c.x, rstd1=rstd1, n1=n1, q=q, k=k, v=v, o=c.o, lse=c.lse,
                            x2=c.x2, rstd2=rstd2, n2=n2, gu=gu, s=s)
 
@@ -539,12 +562,9 @@ class GPTEngine:
             w, gr = prov.layer(i), prov.layer_grads(i)
             k_attn, k_resid, k_mlp = self._keys(st.micro, i)
             # MLP
-            if hasattr(gm, "dgrad_swiglu"):  # down dgrad + SwiGLU backward (fused when faster)
-                dgu = gm.dgrad_swiglu(g_d, w.wdown, c.gu, ops, out=sb(i, "dgu", 2 * I))
-            else:
-                ds = gm.linear_dgrad(g_d, w.wdown)
-                dgu = ops.swiglu_bwd(c.gu, ds, out=sb(i, "dgu", 2 * I))
-                del ds
+            ds = gm.linear_dgrad(g_d, w.wdown)
+            dgu = ops.swiglu_bwd(c.gu, ds, out=sb(i, "dgu", 2 * I))
+            del ds
             dn2 = gm.linear_dgrad(dgu, w.wgu)
             dx2, da = ops.rmsnorm_bwd(dn2, c.x2, c.rstd2, w.ln2, g_x2, gr.ln2, ph, k_resid,
                                       ddelta_out=sb(i, "da", H))

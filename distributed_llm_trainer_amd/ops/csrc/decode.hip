@@ -207,6 +207,10 @@ __global__ __launch_bounds__(DEC_NT) void k_dec_norm_qkv(const float* __restrict
   }
   __syncthreads();
   const int pos = (int)posp[0];
+  // the cache row and the RoPE table row must exist (a caller bug otherwise: the host
+  // keeps pos < max_seq_len, see eval/decode.py); never write past the cache
+  DLT_DASSERT(pos >= 0 && pos < maxS);
+  if (pos < 0 || pos >= maxS) return;
   if (threadIdx.x < B * 16) {
     const int b = threadIdx.x >> 4, l = threadIdx.x & 15, d = dim_of(l);
     float y = outv[b * 16 + l];
@@ -235,7 +239,8 @@ __global__ __launch_bounds__(DEC_NT) void k_dec_attn(const bf16_t* __restrict__ 
   float* oacc = red + 8;                           // [4][64]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int b = blockIdx.x / nh, head = blockIdx.x % nh;
-  const int len = (int)posp[0] + 1;
+  DLT_DASSERT(posp[0] >= 0 && posp[0] < maxS);
+  const int len = (int)(posp[0] < maxS ? posp[0] + 1 : maxS);  // sc[] holds maxS scores
   const bf16_t* K = kc + ((size_t)b * nh + head) * maxS * 64;
   const bf16_t* V = vc + ((size_t)b * nh + head) * maxS * 64;
   float qv[64];

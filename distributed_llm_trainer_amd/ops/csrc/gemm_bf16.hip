@@ -1,0 +1,508 @@
+// Persistent bf16 "TN" GEMM for the transformer projections (gfx950 / MI355X):
+//   C[M,N] = A[M,K] . B[N,K]^T      (both operands K-contiguous, fp32 accumulate)
+// with fused epilogues (plain store, RoPE on q/k, SwiGLU) -- the forward GEMMs of
+// /root/reference/src/models/gpt.py:185-196 (q/k/v + RoPE), :278-280 (gate/up + SwiGLU),
+// :239 (o) and :281 (down), each packed into one GEMM.
+//
+// Why a new kernel (round 3): the projections have K = 768 (12 K-tiles), so a
+// one-tile-per-workgroup GEMM spends most of its time in the prologue (first two K-tiles
+// in flight, nothing to compute) and the epilogue (C stores, nothing to overlap).  This
+// kernel is PERSISTENT: a workgroup walks tiles b, b + G, ... and its LDS-DMA producer
+// runs straight on into the next tile's K-tiles while the current tile's last phases
+// compute, so the next tile's prologue is already in flight when the epilogue stores
+// are issued (the stores count in vmcnt but are younger than the prefetched K-tiles, so
+// the counted waits of the next tile never wait for them).
+//
+// Tile BM = 256 x BN (BN = 192: N = 768 / 2304 / 3072 / 6144 / 50304 give whole rounds
+// of 256 tiles at M = 16384; the template also takes 256), BK = 64, 512 threads = 8 waves as 4 (M) x 2 (N):
+// each wave owns 64 x BN/2 outputs = 4 x NT tiles of v_mfma_f32_16x16x32_bf16.
+// Each K-tile is consumed in 4 quadrant phases (2 m-tiles x NT/2 n-tiles x 2 k-steps):
+//   q0 = (m-half 0, n-half 0): reads A-unit 0, B n-tiles 0..NT/2-1
+//   q1 = (m-half 0, n-half 1): reads B n-tiles NT/2..NT-1
+//   q2 = (m-half 1, n-half 1): reads A-unit 1
+//   q3 = (m-half 1, n-half 0): registers only
+// Staging units (LDS-DMA, source-side XOR swizzle, conflict-free ds_read_b128):
+//   A0/A1 = the 32-row halves of every wave's 64 rows (128 rows, 2 DMA per wave),
+//   B0 = n-tiles 0..3 of both N halves (128 rows, 2 DMA), B1 = the rest (BN-128 rows).
+// Schedule (cdna_hip_programming.md §5 8-phase template): one unit per phase, restaged
+// >= 2 phases after its last read (WAR), each buffer retired by a COUNTED vmcnt(4) one
+// phase before it is read (RAW), raw s_barrier only; waves 4-7 run one barrier behind
+// waves 0-3 so every SIMD pairs one wave's MFMA segment with its partner's LDS/DMA
+// segment; MFMA clusters at s_setprio(1).
+//
+// Output layout: swapped product D = B_tile . A_tile^T, so a lane owns one output row
+// and 4 consecutive columns per 16x16 tile; one v_permlane16_swap per packed dword pair
+// regroups two neighbouring n-tiles into 8 consecutive columns -> 16-byte stores.
+//
+// Requirements (launcher-checked): M % 256 == 0, N % BN == 0, K % 128 == 0, rows
+// 16-byte aligned.
+#include "common.h"
+
+#include <type_traits>
+
+typedef __attribute__((address_space(3))) void* gb_lds_vptr_t;
+typedef const __attribute__((address_space(1))) void* gb_gbl_cvptr_t;
+
+namespace {
+
+constexpr int GB_BM = 256;
+constexpr int GB_BK = 64;
+
+__device__ __forceinline__ int gb_swz(int row, int chunk) { return row * GB_BK + ((chunk ^ ((row >> 1) & 7)) << 3); }
+
+template <int BN>
+struct GbCfg {
+  static constexpr int NT = BN / 32;           // 16-col n-tiles per wave
+  static constexpr int NH = NT / 2;            // n-tiles per quadrant
+  static constexpr int B1_DMA = (BN - 128) / 64;  // DMA instructions per wave for unit B1
+  static constexpr int IMG_A = GB_BM * GB_BK;  // elements
+  static constexpr int IMG_B = BN * GB_BK;
+  static constexpr int BUF = IMG_A + IMG_B;
+};
+
+// Tile row of the first row of 8-row group g of a staging unit.
+//   A unit q: rows {wm*64 + q*32 + 0..31 : wm = 0..3}
+//   B unit 0: rows {wn*BN/2 + 0..63 : wn = 0..1}; unit 1: rows {wn*BN/2 + 64 .. BN/2-1}
+template <int BN>
+__device__ __forceinline__ int gb_arow(int q, int g) { return (g >> 2) * 64 + q * 32 + (g & 3) * 8; }
+template <int BN>
+__device__ __forceinline__ int gb_brow(int q, int g) {
+  if (q == 0) return (g >> 3) * (BN / 2) + (g & 7) * 8;
+  constexpr int per = (BN / 2 - 64) / 8;  // groups per N half in unit 1
+  return (g / per) * (BN / 2) + 64 + (g % per) * 8;
+}
+
+}  // namespace
+
+// Epilogues.  ROPE and SWIGLU (BN = 192 only) permute the B rows of a tile so that the
+// two operands of each element-pair op land in the SAME lane: wave-local n-tile t < 3
+// and t + 3 hold, for ROPE, head dims j and j + 32 of the same 16-pair block (the tile
+// covers 3 heads = 96 rotation pairs, 48 per wave); for SWIGLU, gate and up rows of the
+// same 16 intermediate indices (the tile covers 96 intermediate indices, so the tile
+// stride in W rows is 96).  The stores use the same map, so C keeps its natural layout.
+//   STORE : C = A.B^T
+//   ROPE  : C = A.Wqkv^T with NeoX RoPE on the q and k heads (columns < rot_cols) at
+//           position row % S -- the reference's q/k/v projections + apply_rotary_pos_emb
+//           (gpt.py:185-196) in one pass; same math as k_rope_qk_inplace on the bf16
+//           GEMM output (elementwise.hip).
+//   SWIGLU: gu = A.Wgu^T (gate | up, [M, 2I]) and s = silu(g) * u ([M, I]) -- gpt.py:278-280;
+//           same math as k_swiglu_fwd on the bf16 gate/up values.
+enum { GB_EPI_STORE = 0, GB_EPI_ROPE = 1, GB_EPI_SWIGLU = 2 };
+
+struct GbEpi {
+  const float* cosT;  // ROPE: [S_tab, 32] fp32
+  const float* sinT;
+  int S;              // ROPE: sequence length (position = row % S)
+  int rot_cols;       // ROPE: columns [0, rot_cols) are rotated (2H: q and k)
+  bf16_t* s_out;      // SWIGLU: s [M, ld_s]
+  int ld_s;
+  int I;              // SWIGLU: intermediate size (gate rows [0, I), up rows [I, 2I))
+};
+
+// Column (== B row) offset of wave-local n-tile t's first column within its tile.
+template <int BN, int EPI>
+__device__ __forceinline__ int gb_ncol(int wn, int t, int I) {
+  if constexpr (EPI == GB_EPI_STORE) {
+    return wn * (BN / 2) + t * 16;
+  } else {
+    const int P = wn * 48 + (t % 3) * 16;  // rotation pair / intermediate index
+    if constexpr (EPI == GB_EPI_ROPE)
+      return (P >> 5) * 64 + (P & 31) + (t >= 3 ? 32 : 0);
+    else
+      return P + (t >= 3 ? I : 0);
+  }
+}
+// tile-local B row r (0..BN-1) -> row of B relative to the tile's base row
+template <int BN, int EPI>
+__device__ __forceinline__ int gb_bmap(int r, int I) {
+  return gb_ncol<BN, EPI>(r / (BN / 2), (r % (BN / 2)) >> 4, I) + (r & 15);
+}
+
+template <int BN, int EPI>
+__global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                      bf16_t* __restrict__ C, int M, int N, int K, int lda, int ldb,
+                                                      int ldc, int flags, GbEpi ep) {
+  static_assert(EPI == GB_EPI_STORE || BN == 192, "pair epilogues need the 192-column tile");
+  using Cf = GbCfg<BN>;
+  constexpr int TS = EPI == GB_EPI_SWIGLU ? 96 : BN;  // tile stride in B rows
+  constexpr int NT = Cf::NT, NH = Cf::NH;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * Cf::BUF];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int half = wid >> 2;                  // stagger group (waves w and w+4 share a SIMD)
+  const int wm = wid & 3, wn = wid >> 2;      // 4 (M) x 2 (N) wave grid
+  const int l16 = lane & 15, lq = lane >> 4;
+
+  const int ntn = N / BN;
+  const int ntiles = (M / GB_BM) * ntn;
+  const int G = gridDim.x;  // multiple of 8
+  const int bid = blockIdx.x;
+  // tile walk: round r, workgroup b on "XCD slot" x = b % 8 -> linear tile
+  // r*G + x*(G/8) + b/8: the workgroups of one XCD cover G/8 consecutive tiles per round
+  const int gx = G >> 3;
+  auto tile_of = [&](int r) { return r * G + (bid & 7) * gx + (bid >> 3); };
+  // linear tile -> (tile row, tile col).  With 32 workgroups per XCD slot and whole
+  // 32-tile super-tiles (GM x GN tiles, GN = 8 / 4 / 2 n-tiles), super-tile s = L / 32 is
+  // one XCD's work of one round and the super-tiles walk DOWN a super-column
+  // (column-major), so an XCD keeps the same GN B panels for consecutive rounds and its
+  // per-round operand set (GM A panels + GN B panels, ~4 MB at K = 768) fits its L2.
+  // Otherwise plain row-major.
+  const int ntm = M / GB_BM;
+  const int gn = (ntn & 7) == 0 ? 8 : (ntn & 3) == 0 ? 4 : (ntn & 1) == 0 ? 2 : 1;
+  const int gm = 32 / gn;
+  // flags (ablation only, 0 in production): bit 0 skip the C stores, bit 1 every tile
+  // reads tile (0, 0)'s operand panels (L2-resident), bits 2-3 tile order (0 = grouped
+  // column walk, 1 = row-major, 2 = grouped row walk)
+  const int order = (flags >> 2) & 3;
+  const bool grouped = order != 1 && gx == 32 && ntiles % 32 == 0 && ntm % gm == 0;
+  const int scols = ntn / gn;
+  const int srows = ntm / gm;
+  auto coords = [&](int L, int& tm, int& tn) {
+    if (grouped) {
+      const int sidx = L >> 5, i = L & 31;
+      if (order == 2) {
+        tm = (sidx / scols) * gm + i / gn;
+        tn = (sidx % scols) * gn + i % gn;
+      } else {
+        tm = (sidx % srows) * gm + i / gn;
+        tn = (sidx / srows) * gn + i % gn;
+      }
+    } else {
+      tm = L / ntn;
+      tn = L % ntn;
+    }
+  };
+
+  bf16_t* const A0i = lds;
+  bf16_t* const B0i = lds + Cf::IMG_A;
+  bf16_t* const A1i = lds + Cf::BUF;
+  bf16_t* const B1i = lds + Cf::BUF + Cf::IMG_A;
+
+  // per-lane source offsets (bytes, relative to the tile's first row at column kt*BK)
+  uint32_t oa[2][2], ob0[2], ob1[Cf::B1_DMA];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = gb_arow<BN>(q, wid * 2 + j) + (lane >> 3);
+      oa[q][j] = (uint32_t)(row * lda + (((lane & 7) ^ ((row >> 1) & 7)) << 3)) * 2u;
+    }
+  // (the swizzle follows the LDS image row; the source row goes through the epilogue's
+  // B-row map)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = gb_brow<BN>(0, wid * 2 + j) + (lane >> 3);
+    ob0[j] = (uint32_t)(gb_bmap<BN, EPI>(row, ep.I) * ldb + (((lane & 7) ^ ((row >> 1) & 7)) << 3)) * 2u;
+  }
+#pragma unroll
+  for (int j = 0; j < Cf::B1_DMA; ++j) {
+    const int row = gb_brow<BN>(1, wid * Cf::B1_DMA + j) + (lane >> 3);
+    ob1[j] = (uint32_t)(gb_bmap<BN, EPI>(row, ep.I) * ldb + (((lane & 7) ^ ((row >> 1) & 7)) << 3)) * 2u;
+  }
+
+  auto stA = [&](const bf16_t* g, int q, bf16_t* img) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_global_load_lds((gb_gbl_cvptr_t)((const char*)g + oa[q][j]),
+                                       (gb_lds_vptr_t)(img + gb_arow<BN>(q, wid * 2 + j) * GB_BK), 16, 0, 0);
+  };
+  auto stB0 = [&](const bf16_t* g, bf16_t* img) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_global_load_lds((gb_gbl_cvptr_t)((const char*)g + ob0[j]),
+                                       (gb_lds_vptr_t)(img + gb_brow<BN>(0, wid * 2 + j) * GB_BK), 16, 0, 0);
+  };
+  auto stB1 = [&](const bf16_t* g, bf16_t* img) {
+#pragma unroll
+    for (int j = 0; j < Cf::B1_DMA; ++j)
+      __builtin_amdgcn_global_load_lds((gb_gbl_cvptr_t)((const char*)g + ob1[j]),
+                                       (gb_lds_vptr_t)(img + gb_brow<BN>(1, wid * Cf::B1_DMA + j) * GB_BK), 16, 0,
+                                       0);
+  };
+
+  floatx4_t acc[NT][4];
+  bf16x8_t fa[2][2], fb0[NH][2], fb1[NH][2];
+  const int arow = wm * 64 + l16;         // + qm*32 + mt*16
+  const int brow = wn * (BN / 2) + l16;   // + qn*NH*16 + nt*16
+  auto read_a = [&](const bf16_t* img, int qm) {
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        fa[mt][s] = *reinterpret_cast<const bf16x8_t*>(img + gb_swz(arow + qm * 32 + mt * 16, s * 4 + lq));
+  };
+  auto read_b = [&](const bf16_t* img, int qn, bf16x8_t (&fb)[NH][2]) {
+#pragma unroll
+    for (int nt = 0; nt < NH; ++nt)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        fb[nt][s] = *reinterpret_cast<const bf16x8_t*>(img + gb_swz(brow + (qn * NH + nt) * 16, s * 4 + lq));
+  };
+  auto mma = [&](int qm, int qn, bf16x8_t (&fb)[NH][2]) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int nt = 0; nt < NH; ++nt)
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+          acc[qn * NH + nt][qm * 2 + mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              fb[nt][s], fa[mt][s], acc[qn * NH + nt][qm * 2 + mt], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nk = K / GB_BK;  // even, >= 2
+  int tile = tile_of(0);
+  if (tile >= ntiles) return;  // whole workgroup idle (uniform)
+  auto abase = [&](int t) {
+    int tm, tn;
+    coords(t, tm, tn);
+    if (flags & 2) tm = 0;
+    return A + (size_t)(tm * GB_BM) * lda;
+  };
+  auto bbase = [&](int t) {
+    int tm, tn;
+    coords(t, tm, tn);
+    if (flags & 2) tn = 0;
+    return B + (size_t)(tn * TS) * ldb;
+  };
+
+  // prologue: K-tile 0 of the first tile complete in buffer 0, units A0/B0 of K-tile 1
+  // in flight (their steady-state slots are phases 7 and 8)
+  {
+    const bf16_t* Ab = abase(tile);
+    const bf16_t* Bb = bbase(tile);
+    stA(Ab, 0, A0i);
+    stB0(Bb, B0i);
+    stB1(Bb, B0i);
+    stA(Ab, 1, A0i);
+    stA(Ab + GB_BK, 0, A1i);
+    stB0(Bb + GB_BK, B1i);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (half == 1) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 one barrier behind
+  }
+
+  for (int r = 0;; ++r) {
+    const int next = tile_of(r + 1);
+    const bool has_next = next < ntiles;
+    const bf16_t* const Ab = abase(tile);
+    const bf16_t* const Bb = bbase(tile);
+    const bf16_t* const An = has_next ? abase(next) : Ab;
+    const bf16_t* const Bn = has_next ? bbase(next) : Bb;
+#pragma unroll
+    for (int a = 0; a < NT; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[a][b] = floatx4_t{0.f, 0.f, 0.f, 0.f};
+
+    for (int kt = 0; kt < nk; kt += 2) {
+      // the K-tiles staged in this iteration: kt+1 (rest of it), kt+2, kt+3 -- the last
+      // two belong to the next tile at the end of this one
+      const bool inner = kt + 2 < nk;
+      const bool more = inner || has_next;
+      const bf16_t* const A2 = inner ? Ab + (kt + 2) * GB_BK : An;
+      const bf16_t* const B2 = inner ? Bb + (kt + 2) * GB_BK : Bn;
+      // ---- phase 1: buffer 0, q0 ; stage B1 of K-tile kt+1
+      read_b(B0i, 0, fb0);
+      __builtin_amdgcn_sched_barrier(0);
+      read_a(A0i, 0);
+      stB1(Bb + (kt + 1) * GB_BK, B1i);
+      __builtin_amdgcn_s_barrier();
+      mma(0, 0, fb0);
+      __builtin_amdgcn_s_barrier();
+      // ---- phase 2: q1 ; A1 of K-tile kt+1
+      read_b(B0i, 1, fb1);
+      stA(Ab + (kt + 1) * GB_BK, 1, A1i);
+      __builtin_amdgcn_s_barrier();
+      mma(0, 1, fb1);
+      __builtin_amdgcn_s_barrier();
+      // ---- phase 3: q2 ; A0 of K-tile kt+2 into buffer 0
+      read_a(A0i, 1);
+      if (more) stA(A2, 0, A0i);
+      __builtin_amdgcn_s_barrier();
+      mma(1, 1, fb1);
+      __builtin_amdgcn_s_barrier();
+      // ---- phase 4: q3 (registers) ; B0 of kt+2 ; retire K-tile kt+1
+      if (more) {
+        stB0(B2, B0i);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      mma(1, 0, fb0);
+      __builtin_amdgcn_s_barrier();
+      // ---- phase 5: buffer 1, q0 ; B1 of kt+2
+      read_b(B1i, 0, fb0);
+      __builtin_amdgcn_sched_barrier(0);
+      read_a(A1i, 0);
+      if (more) stB1(B2, B0i);
+      __builtin_amdgcn_s_barrier();
+      mma(0, 0, fb0);
+      __builtin_amdgcn_s_barrier();
+      // ---- phase 6: q1 ; A1 of kt+2
+      read_b(B1i, 1, fb1);
+      if (more) stA(A2, 1, A0i);
+      __builtin_amdgcn_s_barrier();
+      mma(0, 1, fb1);
+      __builtin_amdgcn_s_barrier();
+      // ---- phase 7: q2 ; A0 of kt+3 into buffer 1
+      read_a(A1i, 1);
+      if (more) stA(A2 + GB_BK, 0, A1i);
+      __builtin_amdgcn_s_barrier();
+      mma(1, 1, fb1);
+      __builtin_amdgcn_s_barrier();
+      // ---- phase 8: q3 ; B0 of kt+3 ; retire K-tile kt+2
+      if (more) {
+        stB0(B2 + GB_BK, B1i);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      mma(1, 0, fb0);
+      __builtin_amdgcn_s_barrier();
+    }
+
+    // ---- epilogue: acc[nt][mt] = D[n][m]; lane owns row m0 + wm*64 + mt*16 + l16 and
+    // columns (n-tile nt) + lq*4 .. +3.  permlane16_swap over n-tile pairs (2p, 2p+1):
+    // lanes with lq even end up with 8 consecutive columns of n-tile 2p, lq odd of 2p+1.
+    if (!(flags & 1)) {
+      int tm, tn;
+      coords(tile, tm, tn);
+      if (flags & 16) tm = tn = 0;
+      const int m0 = tm * GB_BM, n0 = tn * TS;
+      auto rnd = [](float v) { return bf2f(f2bf(v)); };
+      if constexpr (EPI == GB_EPI_ROPE) {
+        // all cos/sin loads first (the fragment registers are dead here), one wait.  The
+        // lane's rotation pairs are P = wn*48 + t*16 + lq*4 + e: only two distinct
+        // 4-column j blocks (t = 0 and 2 coincide mod 32)
+        float4 cs[4][2], sn[4][2];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          const int pos = (m0 + wm * 64 + mt * 16 + l16) % ep.S;
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int j = (wn * 48 + u * 16 + lq * 4) & 31;
+            if (flags & 64) {  // ablation: no table loads
+              cs[mt][u] = float4{0.6f, 0.6f, 0.6f, (float)pos};
+              sn[mt][u] = float4{0.8f, 0.8f, 0.8f, (float)j};
+            } else {
+              cs[mt][u] = *reinterpret_cast<const float4*>(ep.cosT + (size_t)pos * 32 + j);
+              sn[mt][u] = *reinterpret_cast<const float4*>(ep.sinT + (size_t)pos * 32 + j);
+            }
+          }
+        }
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int t = 0; t < 3; ++t) {
+            const int P = wn * 48 + t * 16 + lq * 4;
+            if (n0 + (P >> 5) * 64 < ep.rot_cols) {
+              const float4 c4 = cs[mt][t & 1], s4 = sn[mt][t & 1];
+              const float cc[4] = {c4.x, c4.y, c4.z, c4.w}, ss[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const float x1 = rnd(acc[t][mt][e]), x2 = rnd(acc[t + 3][mt][e]);
+                acc[t][mt][e] = x1 * cc[e] - x2 * ss[e];
+                acc[t + 3][mt][e] = x2 * cc[e] + x1 * ss[e];
+              }
+            }
+          }
+      }
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const int row = m0 + wm * 64 + mt * 16 + l16;
+        if constexpr (EPI == GB_EPI_SWIGLU) {
+          // s = silu(g) * u on the bf16-rounded gate/up values; n-tiles 0/1 of s are
+          // paired for 16-byte stores, n-tile 2 stores 8 bytes per lane
+          float sv[3][4];
+#pragma unroll
+          for (int t = 0; t < 3; ++t)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float g = rnd(acc[t][mt][e]), u = rnd(acc[t + 3][mt][e]);
+              sv[t][e] = g * (1.f / (1.f + __expf(-g))) * u;
+            }
+          bf16_t* srow = ep.s_out + (size_t)row * ep.ld_s + (size_t)tn * 96 + wn * 48;
+          uint32_t x[2], y[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            x[h] = (uint32_t)f2bf(sv[0][2 * h]) | ((uint32_t)f2bf(sv[0][2 * h + 1]) << 16);
+            y[h] = (uint32_t)f2bf(sv[1][2 * h]) | ((uint32_t)f2bf(sv[1][2 * h + 1]) << 16);
+            auto sw = __builtin_amdgcn_permlane16_swap(x[h], y[h], false, false);
+            x[h] = sw[0];
+            y[h] = sw[1];
+          }
+          *reinterpret_cast<uint4*>(srow + (lq & 1) * 16 + (lq >> 1) * 8) = uint4{x[0], x[1], y[0], y[1]};
+          const uint2 z = {(uint32_t)f2bf(sv[2][0]) | ((uint32_t)f2bf(sv[2][1]) << 16),
+                           (uint32_t)f2bf(sv[2][2]) | ((uint32_t)f2bf(sv[2][3]) << 16)};
+          *reinterpret_cast<uint2*>(srow + 32 + lq * 4) = z;
+        }
+        bf16_t* crow = C + (size_t)row * ldc + n0;
+#pragma unroll
+        for (int p = 0; p < NT / 2; ++p) {
+          uint32_t x[2], y[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            x[h] = (uint32_t)f2bf(acc[2 * p][mt][2 * h]) | ((uint32_t)f2bf(acc[2 * p][mt][2 * h + 1]) << 16);
+            y[h] = (uint32_t)f2bf(acc[2 * p + 1][mt][2 * h]) | ((uint32_t)f2bf(acc[2 * p + 1][mt][2 * h + 1]) << 16);
+            auto sw = __builtin_amdgcn_permlane16_swap(x[h], y[h], false, false);
+            x[h] = sw[0];
+            y[h] = sw[1];
+          }
+          const int t = 2 * p + (lq & 1);
+          *reinterpret_cast<uint4*>(crow + gb_ncol<BN, EPI>(wn, t, ep.I) + (lq >> 1) * 8) =
+              uint4{x[0], x[1], y[0], y[1]};
+        }
+      }
+      if (flags & 32) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (!has_next) break;
+    tile = next;
+  }
+  if (half == 0) __builtin_amdgcn_s_barrier();  // equal barrier counts for both halves
+}
+
+// grid: one workgroup per CU (at most), a multiple of 8 (XCD-slot tile walk)
+static inline int gb_grid(int ntiles) {
+  int g = ntiles < 256 ? ntiles : 256;
+  return (g + 7) & ~7;
+}
+
+static inline bool gb_shape_ok(int M, int N, int K, int lda, int ldb, int ldc) {
+  return M > 0 && N > 0 && M % 256 == 0 && K % 128 == 0 && K >= 128 && (lda | ldb | ldc) % 8 == 0;
+}
+
+// C = A . B^T (bf16).  Only the 192-column tile is instantiated: the 256-column one
+// needs 256 accumulator + fragment VGPRs per lane and spills at 8 waves per CU.
+DLT_API int dlt_gemm_bf16_tn(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K, int lda, int ldb,
+                             int ldc, int flags, hipStream_t st) {
+  if (!gb_shape_ok(M, N, K, lda, ldb, ldc) || N % 192) return -1;
+  const int ntiles = (M / 256) * (N / 192);
+  GbEpi ep{};
+  k_gemm_bf16<192, GB_EPI_STORE><<<gb_grid(ntiles), 512, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, ep);
+  DLT_CHECK_LAUNCH();
+}
+
+// qkv[M, 3H] = x . Wqkv^T with RoPE (head_dim 64) on the q and k heads: position of
+// row m = m % S, tables cos/sin [>= S, 32] fp32.
+DLT_API int dlt_gemm_bf16_qkv_rope(const bf16_t* A, const bf16_t* W, bf16_t* C, int M, int H, int K, int S,
+                                   const float* cosT, const float* sinT, int flags, hipStream_t st) {
+  const int N = 3 * H;
+  if (!gb_shape_ok(M, N, K, K, K, N) || N % 192 || H % 64 || S <= 0) return -1;
+  GbEpi ep{cosT, sinT, S, 2 * H, nullptr, 0, 0};
+  const int ntiles = (M / 256) * (N / 192);
+  k_gemm_bf16<192, GB_EPI_ROPE><<<gb_grid(ntiles), 512, 0, st>>>(A, W, C, M, N, K, K, K, N, flags, ep);
+  DLT_CHECK_LAUNCH();
+}
+
+// gu[M, 2I] = x . Wgu^T (gate rows [0, I), up rows [I, 2I)) and s[M, I] = silu(g) * u.
+DLT_API int dlt_gemm_bf16_gu_swiglu(const bf16_t* A, const bf16_t* W, bf16_t* gu, bf16_t* s_out, int M, int I, int K,
+                                    int flags, hipStream_t st) {
+  const int N = 2 * I;
+  if (!gb_shape_ok(M, N, K, K, K, N) || I % 96) return -1;
+  GbEpi ep{nullptr, nullptr, 1, 0, s_out, I, I};
+  const int ntiles = (M / 256) * (I / 96);
+  k_gemm_bf16<192, GB_EPI_SWIGLU><<<gb_grid(ntiles), 512, 0, st>>>(A, W, gu, M, N, K, K, K, N, flags, ep);
+  DLT_CHECK_LAUNCH();
+}

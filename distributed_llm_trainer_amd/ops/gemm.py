@@ -26,7 +26,7 @@ between runs, or between a run and its resumed continuation.  A plan file pins t
   (``save_plan``).  ``DLT_GEMM_PLAN=none``: no plan.
 DDP replicas stay in sync regardless (the all-reduced gradient is identical on every
 rank).  For bitwise run-to-run reproducibility without a plan file use
-``DLT_GEMM_TUNE=0 DLT_WGRAD_SPLITK=0 DLT_GEMM_TN=0`` (heuristic #0 everywhere).
+``DLT_GEMM_TUNE=0 DLT_WGRAD_SPLITK=0 DLT_GEMM_TN=0 DLT_GEMM_FUSED=0`` (heuristic #0 everywhere).
 """
 from __future__ import annotations
 
@@ -114,10 +114,15 @@ def load_plan(path: str, shipped: bool = False) -> None:
             rc = L.dlt_gemm_pin(*v)
             if rc != 0:
                 raise RuntimeError(f"dlt_gemm_pin failed ({rc})")
-    _PINNED["tn"] = {tuple(int(x) for x in k.split("x")): (None if c is None else int(c))
+    # "tn": forward-projection race ("bf16" = hand-written, null = hipBLASLt; the round-2
+    # integer tile configs of the retired gemm_tn kernels read as "library");
+    # "fused": "kind:MxNxK" -> fused epilogue picked (older keys without a kind are ignored)
+    _PINNED["tn"] = {tuple(int(x) for x in k.split("x")): ("bf16" if c == "bf16" else None)
                      for k, c in plan.get("tn", {}).items()}
-    _PINNED["tn"].update({("swiglu_bwd", *(int(x) for x in k.split("x"))): bool(c)
-                          for k, c in plan.get("fused", {}).items()})
+    for k, c in plan.get("fused", {}).items():
+        if ":" in k:
+            kind, dims = k.split(":", 1)
+            _PINNED["tn"][(kind, *(int(x) for x in dims.split("x")))] = bool(c)
     _PINNED["splitk"] = {tuple(int(x) for x in k.split("x")): int(c) for k, c in plan.get("splitk", {}).items()}
     if _RACES:
         _RACES["tn"].update(_PINNED["tn"])
@@ -142,7 +147,7 @@ def export_plan() -> dict:
     return {"hipblaslt_version": int(lib().dlt_gemm_lib_version()),
             "hipblaslt": [ln for ln in buf.value[:n].decode().splitlines() if ln and int(ln.split()[-1]) >= 0],
             "tn": {"x".join(map(str, k)): c for k, c in tn.items() if len(k) == 3},
-            "fused": {"x".join(map(str, k[1:])): bool(c) for k, c in tn.items() if len(k) == 4},
+            "fused": {f"{k[0]}:" + "x".join(map(str, k[1:])): bool(c) for k, c in tn.items() if len(k) == 4},
             "splitk": {"x".join(map(str, k)): c for k, c in sk.items()}}
 
 
@@ -163,6 +168,15 @@ def maybe_save_plan() -> None:
     _PLAN_STATE["saved"] = True
     if int(os.environ.get("RANK", "0")) == 0 and not os.path.exists(path):
         save_plan(path)
+
+
+def race_report() -> dict:
+    """Human-readable hand-written-vs-library decisions made so far in this process."""
+    for ref in _INSTANCES:
+        g = ref()
+        if g is not None:
+            return g.report_choices()
+    return {}
 
 
 def available() -> bool:
@@ -209,19 +223,40 @@ def _rowmajor(t: torch.Tensor) -> int:
     return t.stride(0)
 
 
-class HipGemm:
-    """The engine's GEMM interface on the autotuned hipBLASLt planner (one hipBLASLt
-    handle + workspace per stream, so GEMMs on the compute and side streams may overlap).
+def _time_of(fn, reps: int = 3, inner: int = 5) -> float:
+    """Best-of-``reps`` device time (ms) of ``inner`` back-to-back calls of ``fn``."""
+    fn()
+    torch.cuda.synchronize()
+    best = float("inf")
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(inner):
+            fn()
+        e1.record()
+        e1.synchronize()
+        best = min(best, e0.elapsed_time(e1))
+    return best
 
-    Forward projections (y = x W^T, both operands K-contiguous) additionally race the
-    hand-written MFMA kernel (``csrc/gemm_tn.hip``, several tile shapes) against the
-    planner's pick once per shape and keep the fastest: the library wins the large
-    shapes, the hand kernel the small-N ones (o-proj, measured 18 vs 22 us).
-    ``DLT_GEMM_TN=0`` disables the race."""
+
+class HipGemm:
+    """The engine's GEMM interface: hand-written MFMA kernels (``csrc/gemm_bf16.hip``)
+    and the autotuned hipBLASLt planner (one hipBLASLt handle + workspace per stream, so
+    GEMMs on the compute and side streams may overlap).
+
+    Forward projections race the hand-written persistent kernel against the planner's
+    pick once per shape and keep the faster (``DLT_GEMM_TN=0``: library only).  The two
+    fused forms race the same way, each against its unfused equivalent:
+      * ``linear_rope``   -- QKV projection with RoPE in the epilogue vs GEMM + ``rope_qk_inplace``
+      * ``linear_swiglu`` -- gate/up projection with SwiGLU in the epilogue vs GEMM + ``swiglu_fwd``
+    Choices are process-wide (one summation order per shape) and pinned by plan files."""
 
     stream_safe = True
 
     SPLITK_CANDIDATES = (2, 4, 8, 16)
+    # a hand-written candidate must beat the library by this factor to be picked (the
+    # timings are taken in place during the first step and are a few % noisy)
+    RACE_MARGIN = 0.97
 
     def __init__(self):
         import weakref
@@ -232,11 +267,11 @@ class HipGemm:
         if not _RACES:
             _RACES["tn"] = dict(_PINNED["tn"])
             _RACES["splitk"] = dict(_PINNED["splitk"])
-        self._choice = _RACES["tn"]  # (M, N, K) -> None (library) or tile cfg of gemm_tn
+        self._choice = _RACES["tn"]  # (M, N, K) -> "bf16" | None (library); (kind, M, N, K) -> bool (fused)
         self._race = os.environ.get("DLT_GEMM_TN", "1") != "0"
         self._splitk = _RACES["splitk"]  # wgrad (M, N, K) -> token slices (1 = plain accumulate GEMM)
         self._splitk_on = os.environ.get("DLT_WGRAD_SPLITK", "1") != "0"
-        self._fuse_swiglu = os.environ.get("DLT_FUSED_SWIGLU", "1") != "0"
+        self._fuse = os.environ.get("DLT_GEMM_FUSED", "1") != "0"
         _INSTANCES.append(weakref.ref(self))
 
     def _lib_linear(self, x, w, y):
@@ -244,34 +279,21 @@ class HipGemm:
         N = w.shape[0]
         _gemm(1, 0, N, M, K, w, _rowmajor(w), x, _rowmajor(x), y, N)
 
+    def _can_race(self, x, w) -> bool:
+        return (self._race and x.is_contiguous() and w.is_contiguous() and x.dtype == torch.bfloat16
+                and w.dtype == torch.bfloat16 and not torch.cuda.is_current_stream_capturing())
+
     def _pick(self, x, w, y):
         from . import hip
         key = (x.shape[0], w.shape[0], x.shape[1])
         if key in self._choice:
             return self._choice[key]
         choice = None
-        if (self._race and x.is_contiguous() and w.is_contiguous() and x.dtype == torch.bfloat16
-                and not torch.cuda.is_current_stream_capturing()):
-            def t_of(fn):
-                fn()
-                torch.cuda.synchronize()
-                best = float("inf")
-                for _ in range(3):
-                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    e0.record()
-                    for _ in range(5):
-                        fn()
-                    e1.record()
-                    e1.synchronize()
-                    best = min(best, e0.elapsed_time(e1))
-                return best
-            best = t_of(lambda: self._lib_linear(x, w, y))
-            for cfg in hip.GEMM_TN_TILES:
-                if hip.gemm_tn(x, w, cfg, out=y) is None:
-                    continue
-                t = t_of(lambda: hip.gemm_tn(x, w, cfg, out=y))
-                if t < 0.95 * best:
-                    best, choice = t, cfg
+        if self._can_race(x, w) and hip.gemm_bf16_fits(*key):
+            t_lib = _time_of(lambda: self._lib_linear(x, w, y))
+            t_hand = _time_of(lambda: hip.gemm_bf16(x, w, out=y))
+            if t_hand < self.RACE_MARGIN * t_lib:
+                choice = "bf16"
         self._choice[key] = choice
         return choice
 
@@ -281,58 +303,72 @@ class HipGemm:
         if out is not None and (out.shape != (M, N) or not out.is_contiguous() or out.dtype != x.dtype):
             raise ValueError("linear: out must be a contiguous [M, N] tensor of the input dtype")
         y = torch.empty(M, N, dtype=x.dtype, device=x.device) if out is None else out
-        cfg = self._pick(x, w, y)
-        if cfg is not None:
+        if self._pick(x, w, y) == "bf16":
             from . import hip
-            hip.gemm_tn(x, w, cfg, out=y)
+            hip.gemm_bf16(x, w, out=y)
         else:
             self._lib_linear(x, w, y)
         return y
 
-    def dgrad_swiglu(self, dd: torch.Tensor, wdown: torch.Tensor, gu: torch.Tensor, ops, out=None) -> torch.Tensor:
-        """dgu = swiglu_bwd(gu, dd @ Wdown): the fused hand-written kernel (GEMM with the
-        SwiGLU backward in its epilogue, ``hip.dgrad_swiglu_bwd``) or the library GEMM +
-        ``ops.swiglu_bwd``, whichever ran faster when the shape was first seen (timed
-        once, like the forward race).  ``DLT_FUSED_SWIGLU=0``: always unfused."""
-        from . import hip
-        M = dd.shape[0]
-        key = ("swiglu_bwd", M, wdown.shape[0], wdown.shape[1])
+    def _fused_pick(self, kind, x, w, fused, unfused) -> bool:
+        key = (kind, x.shape[0], w.shape[0], x.shape[1])
         choice = self._choice.get(key)
-        fused_ok = (self._fuse_swiglu and dd.is_contiguous() and gu.is_contiguous()
-                    and M % 256 == 0 and wdown.shape[1] % 256 == 0 and wdown.shape[0] % 128 == 0)
-        if not fused_ok:
-            choice = False
+        if choice is None:
+            if not (self._fuse and self._can_race(x, w)):
+                return False  # not recorded: decided again when racing is possible
+            choice = _time_of(fused, inner=3) < self.RACE_MARGIN * _time_of(unfused, inner=3)
+            self._choice[key] = choice
+        return bool(choice)
+
+    def linear_rope(self, x: torch.Tensor, w: torch.Tensor, B: int, S: int, nh: int, cos: torch.Tensor,
+                    sin: torch.Tensor, ops) -> torch.Tensor:
+        """qkv = x @ Wqkv^T with RoPE applied in place to the q and k heads (the packed
+        layout the attention kernels read): the fused hand-written GEMM or the linear +
+        ``ops.rope_qk_inplace`` pair, whichever ran faster when the shape was first seen."""
+        from . import hip
+        M = x.shape[0]
+        y = torch.empty(M, w.shape[0], dtype=x.dtype, device=x.device)
 
         def unfused():
-            return ops.swiglu_bwd(gu, self.linear_dgrad(dd, wdown), out=out)
+            self.linear(x, w, out=y)
+            ops.rope_qk_inplace(y, B, S, nh, cos, sin)
 
         def fused():
-            return hip.dgrad_swiglu_bwd(dd, wdown.t().contiguous(), gu, out=out)
-        if choice is None:
-            if torch.cuda.is_current_stream_capturing():
-                choice = False
-            else:
-                def t_of(fn):
-                    fn()
-                    torch.cuda.synchronize()
-                    best = float("inf")
-                    for _ in range(3):
-                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                        e0.record()
-                        for _ in range(3):
-                            fn()
-                        e1.record()
-                        e1.synchronize()
-                        best = min(best, e0.elapsed_time(e1))
-                    return best
-                choice = t_of(fused) < 0.97 * t_of(unfused)
-            self._choice[key] = choice
-        return fused() if choice else unfused()
+            hip.gemm_qkv_rope(x, w, S, cos, sin, out=y)
+        ok = (w.shape[0] == 3 * nh * 64 and hip.gemm_bf16_fits(M, w.shape[0], x.shape[1]) and M % S == 0
+              and cos.dtype == torch.float32 and cos.is_contiguous() and sin.is_contiguous())
+        if ok and self._fused_pick("rope", x, w, fused, unfused):
+            fused()
+        else:
+            unfused()
+        return y
+
+    def linear_swiglu(self, x: torch.Tensor, w: torch.Tensor, ops, s_out: torch.Tensor = None):
+        """(gu, s): gu = x @ Wgu^T and s = silu(gate) * up, fused in the GEMM epilogue or
+        as linear + ``ops.swiglu_fwd`` (raced once per shape like :meth:`linear`)."""
+        from . import hip
+        M = x.shape[0]
+        I2 = w.shape[0]
+        gu = torch.empty(M, I2, dtype=x.dtype, device=x.device)
+        s = torch.empty(M, I2 // 2, dtype=x.dtype, device=x.device) if s_out is None else s_out
+
+        def unfused():
+            self.linear(x, w, out=gu)
+            ops.swiglu_fwd(gu, out=s)
+
+        def fused():
+            hip.gemm_gu_swiglu(x, w, gu_out=gu, s_out=s)
+        ok = I2 % 192 == 0 and hip.gemm_bf16_fits(M, I2, x.shape[1]) and s.is_contiguous()
+        if ok and self._fused_pick("swiglu", x, w, fused, unfused):
+            fused()
+        else:
+            unfused()
+        return gu, s
 
     def report_choices(self) -> dict:
-        out = {f"M{k[0]}xN{k[1]}xK{k[2]}": ("hipBLASLt" if c is None else f"gemm_tn cfg{c}")
+        out = {f"M{k[0]}xN{k[1]}xK{k[2]}": ("hipBLASLt" if c is None else "hand-written gemm_bf16")
                for k, c in self._choice.items() if len(k) == 3}
-        out.update({f"dgrad+swiglu_bwd M{k[1]}": ("fused gemm_tn8" if c else "hipBLASLt + swiglu_bwd")
+        out.update({f"{k[0]} M{k[1]}xN{k[2]}xK{k[3]}": ("fused gemm_bf16" if c else "unfused (linear + kernel)")
                     for k, c in self._choice.items() if len(k) == 4})
         out.update({f"wgrad M{m}xN{n}xK{k}": f"split-K x{s}" if s > 1 else "hipBLASLt accumulate"
                     for (m, n, k), s in self._splitk.items()})

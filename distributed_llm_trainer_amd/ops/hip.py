@@ -53,10 +53,10 @@ _SIGS = {
     "dlt_add_bf16_f32": [c_void_p, c_void_p, c_int64, c_void_p],
     "dlt_wgrad_gemm": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
     "dlt_scale_bf16": [c_void_p, c_void_p, ctypes.c_long, c_void_p, c_void_p],
-    "dlt_gemm_tn": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
-    "dlt_gemm_tn8": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
-    "dlt_gemm_tn8_swiglu_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
-                                c_void_p],
+    "dlt_gemm_bf16_tn": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "dlt_gemm_bf16_qkv_rope": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
+                               c_void_p],
+    "dlt_gemm_bf16_gu_swiglu": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
     "dlt_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                      c_uint32, c_uint32, c_float, c_int, c_void_p],
     "dlt_attn_dropout_mask": [c_void_p, c_int, c_int, c_int, c_uint32, c_uint32, c_void_p],
@@ -631,50 +631,69 @@ def wgrad_gemm(dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, splits: int 
     return True
 
 
-# ------------------------------------------------------------------ TN GEMM
-GEMM_TN_TILES = {0: (256, 256), 1: (256, 128), 2: (128, 128), 3: (128, 64), 4: (64, 128),
-                 5: (256, 256)}  # 5 = the 8-phase pipelined kernel (csrc/gemm_tn8.hip), K % 128
+# ------------------------------------------------- projection GEMMs (csrc/gemm_bf16.hip)
+def gemm_bf16_fits(M: int, N: int, K: int) -> bool:
+    """Shapes the persistent 256 x 192 MFMA kernel tiles exactly."""
+    return M > 0 and M % 256 == 0 and N % 192 == 0 and K % 128 == 0 and K >= 128
 
 
-def gemm_tn(a: torch.Tensor, b: torch.Tensor, cfg: int, out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
-    """C[M,N] = A[M,K] @ B[N,K]^T (bf16, fp32 accumulate) with the hand-written MFMA
-    kernel (``csrc/gemm_tn.hip``, or ``csrc/gemm_tn8.hip`` for cfg 5) in tile
-    configuration ``cfg``.  Returns None (nothing launched) when the shape does not tile
-    for that configuration."""
+def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """C[M,N] = A[M,K] @ B[N,K]^T (bf16 in/out, fp32 accumulate) with the hand-written
+    persistent MFMA kernel.  Returns None (nothing launched) when the shape does not
+    tile (M % 256, N % 192, K % 128)."""
     M, K = a.shape
     N = b.shape[0]
-    bm, bn = GEMM_TN_TILES[cfg]
-    if M % bm or N % bn or K % (128 if cfg == 5 else 64) or b.shape[1] != K:
+    if not gemm_bf16_fits(M, N, K) or b.shape[1] != K:
         return None
-    _req(a, torch.bfloat16, "gemm_tn.a")
-    _req(b, torch.bfloat16, "gemm_tn.b")
+    _req(a, torch.bfloat16, "gemm_bf16.a")
+    _req(b, torch.bfloat16, "gemm_bf16.b")
     c = torch.empty(M, N, dtype=torch.bfloat16, device=a.device) if out is None else out
-    _req(c, torch.bfloat16, "gemm_tn.c", M * N)
-    if cfg == 5:
-        _chk(lib().dlt_gemm_tn8(_p(a), _p(b), _p(c), M, N, K, K, K, N, _stream()), "gemm_tn8")
-    else:
-        _chk(lib().dlt_gemm_tn(_p(a), _p(b), _p(c), M, N, K, K, K, N, cfg, _stream()), "gemm_tn")
+    _req(c, torch.bfloat16, "gemm_bf16.c", M * N)
+    _chk(lib().dlt_gemm_bf16_tn(_p(a), _p(b), _p(c), M, N, K, K, K, N, 0, _stream()), "gemm_bf16")
     return c
 
 
-def dgrad_swiglu_bwd(dd: torch.Tensor, wdown_t: torch.Tensor, gu: torch.Tensor,
-                     out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
-    """dgu = swiglu_bwd(gu, dd @ Wdown) in ONE kernel (``csrc/gemm_tn8.hip``
-    EPI_SWIGLU_BWD): the down-projection data gradient never leaves the accumulators.
-    ``wdown_t`` is Wdown^T [I, H] (row-major, H contiguous).  Returns None (nothing
-    launched) when the shape does not tile (M, I % 256, H % 128)."""
-    M, H = dd.shape
-    I = wdown_t.shape[0]
-    if M % 256 or I % 256 or H % 128 or H < 128 or wdown_t.shape[1] != H or gu.shape != (M, 2 * I):
+def gemm_qkv_rope(x: torch.Tensor, wqkv: torch.Tensor, S: int, cos: torch.Tensor, sin: torch.Tensor,
+                  out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """qkv[M, 3H] = x @ Wqkv^T with NeoX RoPE applied to the q and k heads (head_dim 64,
+    position of row m = m % S) in the GEMM epilogue -- the packed-QKV projection and
+    ``rope_qk_inplace`` in one kernel.  cos/sin: [>= S, 32] fp32.  None if the shape
+    does not tile (3H % 192, M % 256, K % 128)."""
+    M, K = x.shape
+    N = wqkv.shape[0]
+    H = N // 3
+    if (not gemm_bf16_fits(M, N, K) or N % 3 or H % 64 or wqkv.shape[1] != K or M % S
+            or cos.shape[-1] != 32 or cos.shape[0] < S):
         return None
-    _req(dd, torch.bfloat16, "dgrad_swiglu.dd")
-    _req(wdown_t, torch.bfloat16, "dgrad_swiglu.wdown_t")
-    _req(gu, torch.bfloat16, "dgrad_swiglu.gu")
-    dgu = torch.empty(M, 2 * I, dtype=torch.bfloat16, device=dd.device) if out is None else out
-    _req(dgu, torch.bfloat16, "dgrad_swiglu.dgu", M * 2 * I)
-    _chk(lib().dlt_gemm_tn8_swiglu_bwd(_p(dd), _p(wdown_t), _p(gu), _p(dgu), M, I, H, H, H, _stream()),
-         "gemm_tn8_swiglu_bwd")
-    return dgu
+    _req(x, torch.bfloat16, "gemm_qkv_rope.x")
+    _req(wqkv, torch.bfloat16, "gemm_qkv_rope.w")
+    _req(cos, torch.float32, "gemm_qkv_rope.cos")
+    _req(sin, torch.float32, "gemm_qkv_rope.sin", cos.numel())
+    c = torch.empty(M, N, dtype=torch.bfloat16, device=x.device) if out is None else out
+    _req(c, torch.bfloat16, "gemm_qkv_rope.out", M * N)
+    _chk(lib().dlt_gemm_bf16_qkv_rope(_p(x), _p(wqkv), _p(c), M, H, K, S, _p(cos), _p(sin), 0, _stream()),
+         "gemm_qkv_rope")
+    return c
+
+
+def gemm_gu_swiglu(x: torch.Tensor, wgu: torch.Tensor, gu_out: Optional[torch.Tensor] = None,
+                   s_out: Optional[torch.Tensor] = None):
+    """(gu[M, 2I], s[M, I]) with gu = x @ Wgu^T (gate rows [0, I), up rows [I, 2I)) and
+    s = silu(gate) * up computed in the GEMM epilogue.  None if the shape does not tile
+    (I % 96, M % 256, K % 128)."""
+    M, K = x.shape
+    I2 = wgu.shape[0]
+    I = I2 // 2
+    if not gemm_bf16_fits(M, I2, K) or I2 % 2 or I % 96 or wgu.shape[1] != K:
+        return None
+    _req(x, torch.bfloat16, "gemm_gu_swiglu.x")
+    _req(wgu, torch.bfloat16, "gemm_gu_swiglu.w")
+    gu = torch.empty(M, I2, dtype=torch.bfloat16, device=x.device) if gu_out is None else gu_out
+    s = torch.empty(M, I, dtype=torch.bfloat16, device=x.device) if s_out is None else s_out
+    _req(gu, torch.bfloat16, "gemm_gu_swiglu.gu", M * I2)
+    _req(s, torch.bfloat16, "gemm_gu_swiglu.s", M * I)
+    _chk(lib().dlt_gemm_bf16_gu_swiglu(_p(x), _p(wgu), _p(gu), _p(s), M, I, K, 0, _stream()), "gemm_gu_swiglu")
+    return gu, s
 
 
 def scale_bf16(x: torch.Tensor, scale: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:

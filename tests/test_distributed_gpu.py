@@ -135,7 +135,7 @@ def test_rccl_forced_collectives_one_rank(mode):
     parameters must equal the run without collectives bit for bit."""
     # timing-free GEMM choices, so the two processes run the same kernels
     env = {"DLT_FORCE_CPU": None, "DLT_BACKEND": "nccl", "DLT_GEMM_TUNE": "0", "DLT_WGRAD_SPLITK": "0",
-           "DLT_GEMM_TN": "0", "DLT_FUSED_SWIGLU": "0"}
+           "DLT_GEMM_TN": "0", "DLT_GEMM_FUSED": "0"}
     a, _ = run_multiprocess(_forced, world=1, args=(mode,), env=env, timeout=240)[0]
     b, launched = run_multiprocess(_forced, world=1, args=(mode,), env={**env, "DLT_FORCE_COLLECTIVES": "1"},
                                    timeout=240)[0]

@@ -418,30 +418,6 @@ def test_gemm_plan_pin_roundtrip(tmp_path):
     gemm.load_plan(str(path))  # loading a saved plan re-pins without error
 
 
-@pytest.mark.parametrize("M,H,I", [(512, 256, 512), (2048, 768, 3072)])
-def test_dgrad_swiglu_fused(M, H, I):
-    """The down-projection data gradient with the SwiGLU backward in the GEMM epilogue
-    (gemm_tn8 EPI_SWIGLU_BWD) against the fp32 reference of dd @ Wdown -> swiglu_bwd,
-    and the planner entry point (race + unfused fallback) against the unfused ops."""
-    from distributed_llm_trainer_amd.ops import gemm
-    torch.manual_seed(3)
-    dd = (torch.randn(M, H, device=DEV) * 0.5).bfloat16()
-    wdown = (torch.randn(H, I, device=DEV) / H ** 0.5).bfloat16()
-    gu = torch.randn(M, 2 * I, device=DEV).bfloat16()
-    got = hip.dgrad_swiglu_bwd(dd, wdown.t().contiguous(), gu)
-    ds = dd.float() @ wdown.float()
-    g, u = gu.float()[:, :I], gu.float()[:, I:]
-    sg = torch.sigmoid(g)
-    want = torch.cat([ds * u * sg * (1 + g * (1 - sg)), ds * g * sg], dim=1)
-    _close(got, want, 2e-2 * want.abs().max().item(), 2e-2, "fused dgrad+swiglu_bwd")
-    g2 = gemm.HipGemm()
-    out = torch.empty(M, 2 * I, device=DEV, dtype=torch.bfloat16)
-    r = g2.dgrad_swiglu(dd, wdown, gu, hip, out=out)
-    assert r.data_ptr() == out.data_ptr()
-    _close(r, want, 2e-2 * want.abs().max().item(), 2e-2, "planner dgrad_swiglu")
-    assert ("swiglu_bwd", M, H, I) in g2._choice
-
-
 @pytest.mark.parametrize("M,N,K", [(1024, 256, 128), (2048, 768, 384)])
 def test_wgrad_gemm_kernel(M, N, K):
     torch.manual_seed(0)
@@ -475,21 +451,96 @@ def test_attention_fwd_growing_max_rescales(p):
     _close(o, o2.float(), 2e-2, 2e-2, "o(growing)")
 
 
-@pytest.mark.parametrize("cfg", sorted(hip.GEMM_TN_TILES))
-@pytest.mark.parametrize("shape", [(512, 768, 768), (256, 2304, 768), (256, 768, 3072)])
-def test_gemm_tn(cfg, shape):
-    """Hand-written MFMA GEMM C = A B^T against an fp32 torch reference."""
-    M, N, K = shape
-    torch.manual_seed(cfg)
-    a = torch.randn(M, K, device=DEV).bfloat16()
-    b = torch.randn(N, K, device=DEV).bfloat16()
-    c = hip.gemm_tn(a, b, cfg)
-    bm, bn = hip.GEMM_TN_TILES[cfg]
-    if M % bm or N % bn:
-        assert c is None
+def _relerr(got, want):
+    """max |got - want| / max |want| (per tensor)."""
+    return ((got.float() - want.float()).abs().max() / want.float().abs().max()).item()
+
+
+# the model's forward-projection shapes at the fused-chain size (M = 16384 rows), a
+# medium-size projection, and small multi-round / partial-round grids
+@pytest.mark.parametrize("M,N,K", [(16384, 2304, 768), (16384, 768, 768), (16384, 768, 3072), (16384, 6144, 768),
+                                   (4096, 3072, 1024), (512, 384, 256), (2560, 1152, 384)])
+def test_gemm_bf16(M, N, K):
+    """Persistent hand-written MFMA GEMM C = A B^T (csrc/gemm_bf16.hip) vs fp32 torch:
+    every element within bf16 output rounding (relative to the tensor's max)."""
+    torch.manual_seed(M + N + K)
+    a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
+    b = (torch.rand(N, K, device=DEV) * 2 - 1).bfloat16()
+    c = hip.gemm_bf16(a, b)
+    assert c is not None
+    want = a.float() @ b.float().t()
+    assert _relerr(c, want) < 8e-3
+    _close(c, want, 8e-3 * want.abs().max().item(), 8e-3, "gemm_bf16")
+    assert hip.gemm_bf16(a[:, :K - 64].contiguous(), b[:, :K - 64].contiguous()) is None  # K % 128
+
+
+@pytest.mark.parametrize("B,S,nh,K", [(16, 1024, 12, 768), (4, 256, 25, 1600 // 128 * 128), (2, 512, 16, 1024)])
+def test_gemm_qkv_rope(B, S, nh, K):
+    """QKV GEMM with NeoX RoPE on q/k in the epilogue == fp32 GEMM -> bf16 -> RoPE (the
+    unfused GEMM + rope_qk_inplace math), at GPT-2 small (nh 12), an xl-like head count
+    (nh 25, packed stride 3*25*64 = 4800) and medium (nh 16)."""
+    torch.manual_seed(nh)
+    M, H = B * S, nh * 64
+    x = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
+    w = ((torch.rand(3 * H, K, device=DEV) * 2 - 1) / K ** 0.5).bfloat16()
+    cos, sin = hip.rope_tables(64, 1024 if S <= 1024 else S, device=DEV)
+    got = hip.gemm_qkv_rope(x, w, S, cos, sin)
+    if (3 * H) % 192:
+        assert got is None
         return
-    ref = a.float() @ b.float().t()
-    _close(c, ref, 2e-2 * ref.abs().max().item(), 1e-2, f"gemm_tn cfg{cfg}")
+    y = (x.float() @ w.float().t()).bfloat16()
+    q, k, v = ref.rope_qkv_fwd(y, B, S, nh, cos, sin)  # [B, nh, S, 64]
+    want = torch.cat([t.transpose(1, 2).reshape(M, H) for t in (q, k, v)], dim=1)
+    assert _relerr(got, want) < 1e-2
+    _close(got, want.float(), 1e-2 * want.float().abs().max().item(), 1e-2, "qkv+rope")
+
+
+@pytest.mark.parametrize("M,I,K", [(16384, 3072, 768), (4096, 4096, 1024), (2048, 6400, 1536)])
+def test_gemm_gu_swiglu(M, I, K):
+    """gate/up GEMM with SwiGLU in the epilogue: gu == fp32 GEMM (bf16 rounding) and
+    s == silu(g) * u of the bf16-rounded g, u (the swiglu_fwd math)."""
+    torch.manual_seed(I)
+    x = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
+    w = ((torch.rand(2 * I, K, device=DEV) * 2 - 1) / K ** 0.5).bfloat16()
+    r = hip.gemm_gu_swiglu(x, w)
+    if I % 96:
+        assert r is None
+        return
+    gu, s = r
+    want = x.float() @ w.float().t()
+    assert _relerr(gu, want) < 8e-3
+    gb = want.bfloat16().float()
+    g, u = gb[:, :I], gb[:, I:]
+    ws = g * torch.sigmoid(g) * u
+    assert _relerr(s, ws) < 1e-2
+    _close(s, ws, 1e-2 * ws.abs().max().item(), 1e-2, "swiglu s")
+
+
+def test_planner_fused_races_match_unfused():
+    """HipGemm.linear_rope / linear_swiglu (whatever the race picks) == the unfused
+    library GEMM + kernel, and the choices are recorded process-wide."""
+    from distributed_llm_trainer_amd.ops import gemm
+    torch.manual_seed(4)
+    g = gemm.HipGemm()
+    B, S, nh, K, I = 8, 1024, 12, 768, 3072
+    M = B * S
+    x = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
+    wqkv = ((torch.rand(3 * nh * 64, K, device=DEV) * 2 - 1) / K ** 0.5).bfloat16()
+    wgu = ((torch.rand(2 * I, K, device=DEV) * 2 - 1) / K ** 0.5).bfloat16()
+    cos, sin = hip.rope_tables(64, S, device=DEV)
+    qkv = g.linear_rope(x, wqkv, B, S, nh, cos, sin, hip)
+    y = torch.empty_like(qkv)
+    g._lib_linear(x, wqkv, y)
+    hip.rope_qk_inplace(y, B, S, nh, cos, sin)
+    assert _relerr(qkv, y) < 1e-2
+    gu, s = g.linear_swiglu(x, wgu, hip)
+    gu2 = torch.empty_like(gu)
+    g._lib_linear(x, wgu, gu2)
+    s2 = hip.swiglu_fwd(gu2)
+    assert _relerr(gu, gu2) < 1e-2 and _relerr(s, s2) < 2e-2
+    assert ("rope", M, 3 * nh * 64, K) in g._choice and ("swiglu", M, 2 * I, K) in g._choice
+    plan = gemm.export_plan()
+    assert f"rope:{M}x{3 * nh * 64}x{K}" in plan["fused"]
 
 
 def test_scale_bf16():

@@ -462,3 +462,35 @@ def test_ddp_trainer_fp16_fp32_gpu(mp):
     assert all(math.isfinite(x) for x in res[mp]), res
     assert abs(res[mp][0] - res["bf16"][0]) < 2e-2 * res["bf16"][0], res
     assert res[mp][-1] < res[mp][0] - 0.05, res
+
+
+def test_generate_prompt_fills_all_but_one_slot(monkeypatch):
+    """A prompt of max_seq_len - 1 tokens: the sampling graph's warm-up steps must not
+    write K/V at position max_seq_len (one row past the cache); the device
+    loop and the host loop generate the same greedy tokens through the cropped tail."""
+    torch.manual_seed(11)
+    m = GPT(_cfg(0.0)).to(DEV)
+    m.enable_engine()
+    m.eval()
+    ids = torch.randint(0, 1000, (2, 255), device=DEV)  # max_seq_len 256
+    monkeypatch.setenv("DLT_DECODE_DEVICE_LOOP", "1")
+    a = m.generate(ids, max_new_tokens=6, top_k=1)
+    monkeypatch.setenv("DLT_DECODE_DEVICE_LOOP", "0")
+    b = m.generate(ids, max_new_tokens=6, top_k=1)
+    assert a.shape == b.shape == (2, 261)
+    assert (a == b).float().mean().item() > 0.97
+
+
+def test_fused_decode_falls_back_beyond_lds():
+    """max_seq_len beyond what k_dec_attn keeps in LDS (scores of every cached key): the
+    fused step is not used and generation still runs (ATen graph step)."""
+    from distributed_llm_trainer_amd.eval.decode import _fused_ok
+    cfg = GPTConfig(vocab_size=1000, hidden_size=256, num_layers=1, num_heads=4, max_seq_len=48 * 1024,
+                    intermediate_size=512, dropout=0.0, attention_dropout=0.0)
+    torch.manual_seed(12)
+    m = GPT(cfg).to(DEV)
+    m.enable_engine()
+    m.eval()
+    assert not _fused_ok(m, 1)
+    out = m.generate(torch.randint(0, 1000, (1, 16), device=DEV), max_new_tokens=4, top_k=5)
+    assert out.shape == (1, 20)

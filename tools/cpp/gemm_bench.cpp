@@ -1,0 +1,352 @@
+// Standalone timing / correctness harness for the hand-written bf16 GEMM kernels
+// (no torch import: a fresh GPU box runs it in seconds).
+//   build: hipcc -O3 --offload-arch=gfx950 -mllvm -amdgpu-mfma-vgpr-form \
+//          -I distributed_llm_trainer_amd/ops/csrc tools/cpp/gemm_bench.cpp -lhipblaslt -o tools/cpp/gemm_bench
+//   run:   tools/cpp/gemm_bench [kernel] [M N K ...]
+// Operands are uniform [-1, 1) (DVFS-honest, cdna_hip_programming.md §5.4 rule 25); every
+// kernel is checked against an fp32 reference on sampled rows before it is timed.
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include <hipblaslt/hipblaslt.h>
+
+#include "gemm_bf16.hip"
+#include "elementwise.hip"
+
+#define CK(x)                                                                   \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                  \
+    }                                                                           \
+  } while (0)
+
+__global__ void k_fill(bf16_t* p, size_t n, uint32_t seed) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  for (; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t h = lowbias32((uint32_t)i * 2654435761u ^ seed ^ (uint32_t)(i >> 32));
+    float v = (float)(h >> 8) * (1.0f / 8388608.0f) - 1.0f;
+    p[i] = f2bf(v);
+  }
+}
+
+// fp32 reference of rows [r0, r0 + nr): C[m][n] = sum_k A[m][k] B[n][k]
+__global__ void k_ref(const bf16_t* A, const bf16_t* B, float* C, int r0, int nr, int N, int K) {
+  int n = blockIdx.x * blockDim.x + threadIdx.x;
+  int m = blockIdx.y;
+  if (n >= N || m >= nr) return;
+  const bf16_t* a = A + (size_t)(r0 + m) * K;
+  const bf16_t* b = B + (size_t)n * K;
+  float s = 0.f;
+  for (int k = 0; k < K; ++k) s += bf2f(a[k]) * bf2f(b[k]);
+  C[(size_t)m * N + n] = s;
+}
+
+typedef int (*launch_fn)(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, hipStream_t);
+
+template <int FLAGS>
+static int run_bf16(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K, hipStream_t s) {
+  return dlt_gemm_bf16_tn(A, B, C, M, N, K, K, K, N, FLAGS, s);
+}
+
+// hipBLASLt reference (system ROCm 7.2 library, best of the first 24 heuristic candidates,
+// chosen once per shape): C^T[N,M] = op_T(B)[N,K] . A^T  in column-major terms
+static hipblasLtHandle_t g_h = nullptr;
+static void* g_ws = nullptr;
+static const size_t g_wsz = 64 << 20;
+struct BlasPlan {
+  int M = 0, N = 0, K = 0;
+  hipblasLtMatmulDesc_t md;
+  hipblasLtMatrixLayout_t la, lb, lc;
+  hipblasLtMatmulAlgo_t algo;
+  bool ok = false;
+};
+static BlasPlan g_plan;
+static int run_blas(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K, hipStream_t s) {
+  float alpha = 1.f, beta = 0.f;
+  if (!g_h) {
+    hipblasLtCreate(&g_h);
+    hipMalloc(&g_ws, g_wsz);
+  }
+  BlasPlan& p = g_plan;
+  if (p.M != M || p.N != N || p.K != K) {
+    p.M = M, p.N = N, p.K = K, p.ok = false;
+    hipblasLtMatmulDescCreate(&p.md, HIPBLAS_COMPUTE_32F, HIP_R_32F);
+    hipblasOperation_t ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
+    hipblasLtMatmulDescSetAttribute(p.md, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta));
+    hipblasLtMatmulDescSetAttribute(p.md, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb));
+    hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, K, N, K);
+    hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, K, M, K);
+    hipblasLtMatrixLayoutCreate(&p.lc, HIP_R_16BF, N, M, N);
+    hipblasLtMatmulPreference_t pref;
+    hipblasLtMatmulPreferenceCreate(&pref);
+    hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &g_wsz, sizeof(g_wsz));
+    hipblasLtMatmulHeuristicResult_t res[24];
+    int n = 0;
+    hipblasLtMatmulAlgoGetHeuristic(g_h, p.md, p.la, p.lb, p.lc, p.lc, pref, 24, res, &n);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    float best = 1e30f;
+    for (int i = 0; i < n; ++i) {
+      if (res[i].workspaceSize > g_wsz) continue;
+      if (hipblasLtMatmul(g_h, p.md, &alpha, B, p.la, A, p.lb, &beta, C, p.lc, C, p.lc, &res[i].algo, g_ws, g_wsz, s))
+        continue;
+      hipEventRecord(e0, s);
+      for (int j = 0; j < 5; ++j)
+        hipblasLtMatmul(g_h, p.md, &alpha, B, p.la, A, p.lb, &beta, C, p.lc, C, p.lc, &res[i].algo, g_ws, g_wsz, s);
+      hipEventRecord(e1, s);
+      hipEventSynchronize(e1);
+      float ms;
+      hipEventElapsedTime(&ms, e0, e1);
+      if (ms < best) best = ms, p.algo = res[i].algo, p.ok = true;
+    }
+  }
+  if (!p.ok) return -5;
+  return (int)hipblasLtMatmul(g_h, p.md, &alpha, B, p.la, A, p.lb, &beta, C, p.lc, C, p.lc, &p.algo, g_ws, g_wsz, s);
+}
+
+struct Kern {
+  const char* name;
+  launch_fn fn;
+};
+
+static float bfr(float v) {
+  uint32_t u;
+  memcpy(&u, &v, 4);
+  u = (u + 0x7fff + ((u >> 16) & 1)) & 0xffff0000u;
+  memcpy(&v, &u, 4);
+  return v;
+}
+static float bff(bf16_t h) {
+  uint32_t u = (uint32_t)h << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+template <typename F>
+static float time_us(F fn, hipStream_t st, int it = 20) {
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int w = 0; w < 3; ++w) fn();
+  float best = 1e30f;
+  for (int rep = 0; rep < 5; ++rep) {
+    CK(hipEventRecord(e0, st));
+    for (int i = 0; i < it; ++i) fn();
+    CK(hipEventRecord(e1, st));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    best = std::fmin(best, ms * 1000.f / it);
+  }
+  return best;
+}
+
+// fused-epilogue checks (RoPE on the QKV GEMM, SwiGLU on the gate/up GEMM) against the
+// fp32 reference rows + host epilogue, and timings vs hipBLASLt + the separate kernel
+static int epi_main(int M, int H, int I, int S) {
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  const int K = H;
+  // RoPE tables [S, 32]
+  std::vector<float> hc((size_t)S * 32), hs((size_t)S * 32);
+  for (int p = 0; p < S; ++p)
+    for (int j = 0; j < 32; ++j) {
+      float invf = 1.0f / powf(10000.f, (2.f * j) / 64.f);
+      hc[p * 32 + j] = cosf(p * invf);
+      hs[p * 32 + j] = sinf(p * invf);
+    }
+  float *dc, *ds;
+  CK(hipMalloc(&dc, hc.size() * 4));
+  CK(hipMalloc(&ds, hs.size() * 4));
+  CK(hipMemcpy(dc, hc.data(), hc.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(ds, hs.data(), hs.size() * 4, hipMemcpyHostToDevice));
+  const int nr = 32, r0 = (M / 3) & ~7;
+  for (int which = 0; which < 2; ++which) {
+    const int N = which == 0 ? 3 * H : 2 * I;
+    bf16_t *A, *B, *C, *C2, *Sb = nullptr, *Sb2 = nullptr;
+    CK(hipMalloc(&A, (size_t)M * K * 2));
+    CK(hipMalloc(&B, (size_t)N * K * 2));
+    CK(hipMalloc(&C, (size_t)M * N * 2));
+    CK(hipMalloc(&C2, (size_t)M * N * 2));
+    if (which == 1) {
+      CK(hipMalloc(&Sb, (size_t)M * I * 2));
+      CK(hipMalloc(&Sb2, (size_t)M * I * 2));
+    }
+    k_fill<<<1024, 256, 0, st>>>(A, (size_t)M * K, 11);
+    k_fill<<<1024, 256, 0, st>>>(B, (size_t)N * K, 12);
+    float* R;
+    CK(hipMalloc(&R, (size_t)nr * N * 4));
+    k_ref<<<dim3((N + 255) / 256, nr), 256, 0, st>>>(A, B, R, r0, nr, N, K);
+    std::vector<float> ref((size_t)nr * N);
+    CK(hipMemcpyAsync(ref.data(), R, ref.size() * 4, hipMemcpyDeviceToHost, st));
+    CK(hipStreamSynchronize(st));
+    auto fused = [&]() {
+      if (which == 0) return dlt_gemm_bf16_qkv_rope(A, B, C, M, H, K, S, dc, ds, 0, st);
+      return dlt_gemm_bf16_gu_swiglu(A, B, C, Sb, M, I, K, 0, st);
+    };
+    auto unfused = [&]() {
+      int rc = run_blas(A, B, C2, M, N, K, st);
+      if (rc) return rc;
+      if (which == 0) return dlt_rope_qk_inplace(C2, dc, ds, M, S, H / 64, 64, st);
+      return dlt_swiglu_fwd(C2, Sb2, M, I, st);
+    };
+    CK(hipMemsetAsync(C, 0xff, (size_t)M * N * 2, st));
+    if (fused() != 0) {
+      printf("fused launch failed\n");
+      return 1;
+    }
+    CK(hipStreamSynchronize(st));
+    std::vector<bf16_t> got((size_t)nr * N), sgot;
+    CK(hipMemcpy(got.data(), C + (size_t)r0 * N, got.size() * 2, hipMemcpyDeviceToHost));
+    if (which == 1) {
+      sgot.resize((size_t)nr * I);
+      CK(hipMemcpy(sgot.data(), Sb + (size_t)r0 * I, sgot.size() * 2, hipMemcpyDeviceToHost));
+    }
+    double e1 = 0, m1 = 0, e2 = 0, m2 = 0;
+    for (int r = 0; r < nr; ++r) {
+      const float* rr = ref.data() + (size_t)r * N;
+      const int pos = (r0 + r) % S;
+      if (which == 0) {
+        for (int c = 0; c < N; ++c) {
+          float want = bfr(rr[c]);
+          const int head = c / 64, j = c % 64;
+          if (c < 2 * H) {
+            const int jj = j & 31;
+            const float cc = hc[pos * 32 + jj], ss = hs[pos * 32 + jj];
+            const float x1 = bfr(rr[head * 64 + jj]), x2 = bfr(rr[head * 64 + jj + 32]);
+            want = j < 32 ? x1 * cc - x2 * ss : x2 * cc + x1 * ss;
+          }
+          const double d = std::fabs((double)bff(got[(size_t)r * N + c]) - want);
+          if (!(d <= e1)) e1 = d;
+          m1 = std::fmax(m1, std::fabs(want));
+        }
+      } else {
+        for (int c = 0; c < N; ++c) {
+          const double d = std::fabs((double)bff(got[(size_t)r * N + c]) - rr[c]);
+          if (!(d <= e1)) e1 = d;
+          m1 = std::fmax(m1, std::fabs(rr[c]));
+        }
+        for (int c = 0; c < I; ++c) {
+          const float g = bfr(rr[c]), u = bfr(rr[I + c]);
+          const float want = g / (1.f + expf(-g)) * u;
+          const double d = std::fabs((double)bff(sgot[(size_t)r * I + c]) - want);
+          if (!(d <= e2)) e2 = d;
+          m2 = std::fmax(m2, std::fabs(want));
+        }
+      }
+    }
+    const float tf = time_us(fused, st), tu = time_us(unfused, st);
+    float tx = 0.f, tp = 0.f;
+    if (which == 0)
+      tx = time_us([&]() { return dlt_gemm_bf16_qkv_rope(A, B, C, M, H, K, S, dc, ds, 64, st); }, st);
+    tp = time_us([&]() { return dlt_gemm_bf16_tn(A, B, C, M, N, K, K, K, N, 0, st); }, st);
+    printf("  plain bf16 %.1f us, rope without table loads %.1f us\n", tp, tx);
+    printf("%s M=%d N=%d K=%d: fused %.1f us | hipBLASLt + %s %.1f us | err %.1e%s%.1e\n",
+           which == 0 ? "qkv+rope" : "gu+swiglu", M, N, K, tf, which == 0 ? "rope" : "swiglu", tu, e1 / m1,
+           which == 1 ? " s err " : "", which == 1 ? e2 / m2 : 0.0);
+    fflush(stdout);
+    CK(hipFree(A));
+    CK(hipFree(B));
+    CK(hipFree(C));
+    CK(hipFree(C2));
+    CK(hipFree(R));
+    if (Sb) CK(hipFree(Sb));
+    if (Sb2) CK(hipFree(Sb2));
+  }
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc > 1 && !strcmp(argv[1], "epi")) return epi_main(16384, 768, 3072, 1024);
+  std::vector<Kern> kerns = {{"blas", run_blas},         {"bf16", run_bf16<0>},      {"rowmaj", run_bf16<4>},
+                             {"rowwalk", run_bf16<8>}, {"nostore", run_bf16<1>},   {"l2ops", run_bf16<2>},
+                             {"l2nost", run_bf16<3>},    {"c0", run_bf16<16>},       {"stsync", run_bf16<32>}};
+  std::string only = (argc > 1 && strcmp(argv[1], "all")) ? std::string(",") + argv[1] + "," : "all";
+  std::vector<int> shp;
+  for (int i = 2; i < argc; ++i) shp.push_back(atoi(argv[i]));
+  if (shp.empty()) {
+    int d[] = {16384, 768, 768, 16384, 768, 1536, 16384, 768, 3072, 16384, 768, 6144,
+               16384, 2304, 768, 16384, 6144, 768, 16384, 3072, 768};
+    shp.assign(d, d + sizeof(d) / sizeof(int));
+  }
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (size_t si = 0; si + 2 < shp.size(); si += 3) {
+    const int M = shp[si], N = shp[si + 1], K = shp[si + 2];
+    bf16_t *A, *B, *C;
+    CK(hipMalloc(&A, (size_t)M * K * 2));
+    CK(hipMalloc(&B, (size_t)N * K * 2));
+    CK(hipMalloc(&C, (size_t)M * N * 2));
+    k_fill<<<1024, 256, 0, st>>>(A, (size_t)M * K, 1);
+    k_fill<<<1024, 256, 0, st>>>(B, (size_t)N * K, 2);
+    const int nr = 64, r0 = M / 2 - 17 > 0 ? (M / 3) & ~7 : 0;
+    float* R;
+    CK(hipMalloc(&R, (size_t)nr * N * 4));
+    k_ref<<<dim3((N + 255) / 256, nr), 256, 0, st>>>(A, B, R, r0, nr, N, K);
+    std::vector<float> ref((size_t)nr * N);
+    CK(hipMemcpyAsync(ref.data(), R, ref.size() * 4, hipMemcpyDeviceToHost, st));
+    CK(hipStreamSynchronize(st));
+    const double fl = 2.0 * M * N * K;
+    printf("M=%d N=%d K=%d:", M, N, K);
+    for (auto& kr : kerns) {
+      if (only != "all" && only.find(std::string(",") + kr.name + ",") == std::string::npos) continue;
+      CK(hipMemsetAsync(C, 0xff, (size_t)M * N * 2, st));
+      int rc = kr.fn(A, B, C, M, N, K, st);
+      if (rc != 0) {
+        printf(" | %s n/a(%d)", kr.name, rc);
+        continue;
+      }
+      CK(hipStreamSynchronize(st));
+      std::vector<bf16_t> got((size_t)nr * N);
+      CK(hipMemcpy(got.data(), C + (size_t)r0 * N, got.size() * 2, hipMemcpyDeviceToHost));
+      double maxerr = 0, maxref = 0;
+      for (size_t i = 0; i < got.size(); ++i) {
+        uint32_t u = (uint32_t)got[i] << 16;
+        float g;
+        memcpy(&g, &u, 4);
+        double d = std::fabs((double)g - ref[i]);
+        if (!(d <= maxerr)) maxerr = d;  // NaN-propagating
+        maxref = std::fmax(maxref, std::fabs(ref[i]));
+      }
+      // full-matrix poison check on the last rows too (unwritten tiles stay 0xffff = NaN)
+      std::vector<bf16_t> tail((size_t)8 * N);
+      CK(hipMemcpy(tail.data(), C + (size_t)(M - 8) * N, tail.size() * 2, hipMemcpyDeviceToHost));
+      int poisoned = 0;
+      for (auto v : tail) poisoned += (v == 0xffff);
+      for (int w = 0; w < 3; ++w) kr.fn(A, B, C, M, N, K, st);
+      const int it = 20;
+      float best = 1e30f;
+      for (int rep = 0; rep < 5; ++rep) {
+        CK(hipEventRecord(e0, st));
+        for (int i = 0; i < it; ++i) kr.fn(A, B, C, M, N, K, st);
+        CK(hipEventRecord(e1, st));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        best = std::fmin(best, ms * 1000.f / it);
+      }
+      printf(" | %s %7.1f us %5.0f TF err %.1e%s", kr.name, best, fl / best / 1e6, maxerr / maxref,
+             poisoned ? " POISON" : "");
+      fflush(stdout);
+    }
+    printf("\n");
+    fflush(stdout);
+    CK(hipFree(A));
+    CK(hipFree(B));
+    CK(hipFree(C));
+    CK(hipFree(R));
+  }
+  return 0;
+}
