@@ -183,7 +183,7 @@ class GPT(nn.Module):
             provider = FlatParamStore(self, dev, compute_dtype=compute_dtype)
             self.store = provider
         if ops is None:
-            ops = ops_mod.for_device(dev)
+            ops = ops_mod.for_device(dev, head_dim=self.config.head_dim)
         gemm = None
         if dev.type == "cuda" and ops.backend == "hip":
             import os

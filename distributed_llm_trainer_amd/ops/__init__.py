@@ -43,10 +43,29 @@ def hip_ops():
     return ns
 
 
-def for_device(device) -> types.SimpleNamespace:
+# the attention-side ops whose HIP kernels are specialised for head_dim 64
+_ATTN_FUNCS = ("rope_qkv_fwd", "rope_qkv_bwd", "attention_fwd", "attention_bwd", "rope_qk_inplace",
+               "attention_fwd_packed", "attention_bwd_packed")
+
+
+def for_device(device, head_dim: int = 64) -> types.SimpleNamespace:
+    """Op namespace for ``device``.  On the GPU every op is a HIP kernel, except that a
+    model whose head_dim is not 64 (the reference allows any ``hidden % heads == 0``,
+    ``config.py:38-39``) runs RoPE + attention through the PyTorch reference ops ON THE
+    GPU (``attn_backend == "reference"``, with a one-time warning) while the norms,
+    SwiGLU, cross-entropy, embedding, optimizer and GEMMs stay native."""
     dev = torch.device(device)
     if dev.type == "cuda":
         if os.environ.get("DLT_ALLOW_REFERENCE_ON_GPU") == "1":
             return _namespace(reference, "reference")
-        return hip_ops()
+        ns = hip_ops()
+        ns.attn_backend = "hip"
+        if head_dim != 64:
+            import warnings
+            warnings.warn(f"head_dim {head_dim}: the HIP attention kernels are specialised for head_dim 64; "
+                          "RoPE + attention run as PyTorch ops on the GPU for this model")
+            for f in _ATTN_FUNCS:
+                setattr(ns, f, getattr(reference, f))
+            ns.attn_backend = "reference"
+        return ns
     return CPU_OPS

@@ -354,6 +354,7 @@ def main(argv=None):
         dbg.check_replicas(trainer.store.flat)
     start_time = time.time()
     start_step = trainer.global_step
+    tokens0 = trainer.tokens_seen  # tokens of a resumed run's earlier steps are not this run's throughput
     steady_t0, steady_tok0, steady_ckpt = None, 0, 0.0
     for step in range(start_step, tc.max_steps):
         dbg.maybe_inject_fault(step, trainer.rank)
@@ -371,7 +372,7 @@ def main(argv=None):
             steady_t0, steady_tok0 = time.time(), trainer.tokens_seen
         if do_log and trainer.is_main_process:
             elapsed = time.time() - start_time
-            tps = (metrics["tokens"] - start_step * 0) / max(elapsed, 1e-9)
+            tps = (metrics["tokens"] - tokens0) / max(elapsed, 1e-9)
             print(f"Step {step:6d} | Loss: {metrics['loss']:.4f} | LR: {metrics['lr']:.2e} | Tokens/sec: {tps:,.0f}",
                   flush=True)
             if metrics_f:

@@ -438,6 +438,7 @@ def main(argv=None):
     data_iter = iter(dataloader)
     start_time = time.time()
     start_step = trainer.global_step
+    tokens0 = trainer.tokens_seen  # tokens of a resumed run's earlier steps are not this run's throughput
     steady_t0, steady_tok0, steady_ckpt = None, 0, 0.0
     for step in range(start_step, tc.max_steps):
         dbg.maybe_inject_fault(step, trainer.rank)
@@ -453,7 +454,7 @@ def main(argv=None):
             steady_t0, steady_tok0 = time.time(), trainer.tokens_seen
         if do_log and trainer.is_main_process:
             elapsed = time.time() - start_time
-            tps = metrics["tokens"] / max(elapsed, 1e-9)
+            tps = (metrics["tokens"] - tokens0) / max(elapsed, 1e-9)
             mem = trainer.get_memory_stats()
             print(f"Step {step:6d} | Loss: {metrics['loss']:.4f} | LR: {metrics['lr']:.2e} | "
                   f"Tokens/s: {tps:,.0f} | Mem: {mem['allocated_gb']:.1f}GB", flush=True)

@@ -15,6 +15,10 @@ Fixes vs the reference:
   names (``models.config.GPTConfig``, ``__main__.TrainingConfig``,
   ``training.{ddp,fsdp}_trainer.*``) -- so both our checkpoints and the reference's
   load with ``weights_only=True``: nothing in the file is executed.
+* Reverse direction: the config objects are pickled under the reference's class paths
+  (``models.config.GPTConfig``, ``__main__.TrainingConfig`` / ``__main__.FSDPConfig``),
+  so the reference's own loader reads our files without this package installed
+  (``tests/test_checkpoint_data.py::test_checkpoint_readable_by_reference_loader``).
 * FSDP SHARDED_STATE_DICT (discussed, not implemented, in the reference): per-rank
   shard files + ``meta.json``; ``consolidate_sharded`` turns one into the full format
   (``python -m distributed_llm_trainer_amd.utils.checkpoint consolidate DIR OUT``).
@@ -69,18 +73,122 @@ def register_safe_globals() -> None:
     _REGISTERED = True
 
 
+# Reverse compatibility: the config objects of a checkpoint are
+# pickled under the class paths the REFERENCE writes -- ``models.config.GPTConfig``
+# (its model package, imported with ``src`` on sys.path) and ``__main__.TrainingConfig``
+# / ``__main__.FSDPConfig`` (its trainers run as scripts) -- so the reference's loader
+# (``src/eval/infer.py:15-21,53-57``: ``from models.config import GPTConfig`` plus a
+# placeholder ``TrainingConfig`` in ``__main__``) reads our files without this package.
+_REF_PATHS = {"GPTConfig": ("models.config", "GPTConfig"), "TrainingConfig": ("__main__", "TrainingConfig"),
+              "FSDPTrainingConfig": ("__main__", "TrainingConfig"), "FSDPConfig": ("__main__", "FSDPConfig")}
+_REF_ALIASES: Dict[Any, Any] = {}
+
+
+def _ref_alias(cls):
+    """Subclass of ``cls`` whose pickled name is the reference's class path."""
+    if cls not in _REF_ALIASES:
+        module, name = _REF_PATHS[cls.__name__]
+        _REF_ALIASES[cls] = type(name, (cls,), {"__module__": module, "__qualname__": name})
+    return _REF_ALIASES[cls]
+
+
+def _to_reference_pickle(payload: Dict[str, Any]):
+    """(payload with config objects re-classed to their reference aliases, list of
+    (module, name, alias) the pickler must be able to look up)."""
+    out, need = dict(payload), []
+    for k, v in payload.items():
+        name = type(v).__name__
+        if k.endswith("_config") and dataclasses.is_dataclass(v) and not isinstance(v, type) and name in _REF_PATHS:
+            base = type(v) if type(v) not in _REF_ALIASES.values() else type(v).__mro__[1]
+            alias = _ref_alias(base)
+            obj = alias.__new__(alias)
+            obj.__dict__.update(v.__dict__)
+            out[k] = obj
+            need.append((alias.__module__, alias.__qualname__, alias))
+    return out, need
+
+
+class _RefModules:
+    """Make ``module.name`` resolve to the alias classes while pickling (pickle checks
+    that a class is importable under the path it writes), then restore sys.modules."""
+
+    def __init__(self, need):
+        self.need = need
+        self.saved = []
+
+    def __enter__(self):
+        import sys
+        import types
+        for module, name, alias in self.need:
+            parts = module.split(".")
+            for i in range(1, len(parts) + 1):
+                mn = ".".join(parts[:i])
+                if mn not in sys.modules:
+                    self.saved.append(("mod", mn, None))
+                    sys.modules[mn] = types.ModuleType(mn)
+                    if i > 1:
+                        setattr(sys.modules[".".join(parts[:i - 1])], parts[i - 1], sys.modules[mn])
+            mod = sys.modules[module]
+            self.saved.append(("attr", module, (name, getattr(mod, name, _MISSING))))
+            setattr(mod, name, alias)
+        return self
+
+    def __exit__(self, *exc):
+        import sys
+        for kind, mn, extra in reversed(self.saved):
+            if kind == "attr":
+                name, old = extra
+                if old is _MISSING:
+                    delattr(sys.modules[mn], name)
+                else:
+                    setattr(sys.modules[mn], name, old)
+            else:
+                sys.modules.pop(mn, None)
+        return False
+
+
+_MISSING = object()
+
+
 def save_checkpoint(path: str, payload: Dict[str, Any]) -> None:
     d = os.path.dirname(path)
     if d:
         os.makedirs(d, exist_ok=True)
     tmp = f"{path}.tmp.{os.getpid()}"
-    torch.save(payload, tmp)
+    payload, need = _to_reference_pickle(payload)
+    with _RefModules(need):
+        torch.save(payload, tmp)
     os.replace(tmp, path)
+
+
+def _canonical_config(v):
+    """A config object unpickled through one of the reference-path aliases, as an
+    instance of this package's own class (dataclass ``==`` compares classes).  The
+    reference pickles both trainers' TrainingConfig as ``__main__.TrainingConfig``: the
+    field set tells the DDP and FSDP schemas apart."""
+    from ..training.configs import FSDPConfig, FSDPTrainingConfig, TrainingConfig
+    bases = (GPTConfig, TrainingConfig, FSDPTrainingConfig, FSDPConfig)
+    if type(v) in bases or not any(isinstance(v, b) for b in bases):
+        return v
+    base = next(b for b in bases if isinstance(v, b))
+    if base in (TrainingConfig, FSDPTrainingConfig):
+        keys = set(v.__dict__)
+        base = max((TrainingConfig, FSDPTrainingConfig),
+                   key=lambda c: len(keys & {f.name for f in dataclasses.fields(c)}) - len(
+                       {f.name for f in dataclasses.fields(c)} - keys))
+    obj = base.__new__(base)
+    obj.__dict__.update(v.__dict__)
+    return obj
 
 
 def load_checkpoint(path: str, map_location="cpu") -> Dict[str, Any]:
     register_safe_globals()
-    return torch.load(path, map_location=map_location, weights_only=True)
+    ck = torch.load(path, map_location=map_location, weights_only=True)
+    if isinstance(ck, dict):
+        for k in list(ck):
+            if k.endswith("_config"):
+                ck[k] = _canonical_config(ck[k])
+    return ck
 
 
 SHARDED_FORMAT = "dlt-fsdp-sharded-v1"

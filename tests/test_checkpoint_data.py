@@ -51,6 +51,92 @@ def test_reference_format_checkpoint_loads_weights_only(tmp_path):
     assert c["global_step"] == 3 and c["model_config"].hidden_size == 32
 
 
+_REF_LOADER = r"""
+import importlib.abc, sys, types, dataclasses
+class _Block(importlib.abc.MetaPathFinder):
+    def find_spec(self, name, path, target=None):
+        if name.split(".")[0] in ("distributed_llm_trainer_amd", "src"):
+            raise ImportError("blocked: " + name)
+        return None
+sys.meta_path.insert(0, _Block())
+import torch
+# the reference process: models.config.GPTConfig (a dataclass) and the placeholder
+# TrainingConfig / FSDPConfig classes of its __main__ (infer.py:19-21)
+@dataclasses.dataclass
+class GPTConfig:
+    vocab_size: int = 50257
+    hidden_size: int = 768
+    num_layers: int = 12
+    num_heads: int = 12
+    intermediate_size: int = None
+    max_seq_len: int = 1024
+models = types.ModuleType("models"); cfgmod = types.ModuleType("models.config")
+GPTConfig.__module__ = "models.config"; cfgmod.GPTConfig = GPTConfig; models.config = cfgmod
+sys.modules["models"], sys.modules["models.config"] = models, cfgmod
+class TrainingConfig: pass
+class FSDPConfig: pass
+main = sys.modules["__main__"]; main.TrainingConfig = TrainingConfig; main.FSDPConfig = FSDPConfig
+TrainingConfig.__module__ = FSDPConfig.__module__ = "__main__"
+torch.serialization.add_safe_globals([GPTConfig, TrainingConfig, FSDPConfig])
+ck = torch.load(sys.argv[1], map_location="cpu", weights_only=True)
+assert "distributed_llm_trainer_amd" not in sys.modules
+mc = ck["model_config"]
+assert type(mc) is GPTConfig and mc.hidden_size == int(sys.argv[2]), (type(mc), mc.__dict__)
+assert type(ck["training_config"]) is TrainingConfig
+if len(sys.argv) > 3:
+    assert type(ck["fsdp_config"]) is FSDPConfig and ck["fsdp_config"].sharding_strategy == sys.argv[3]
+assert "embed_tokens.weight" in ck["model"]
+print("REF-LOAD-OK", ck["global_step"])
+"""
+
+
+def _ref_load(path, hidden, fsdp=None):
+    import subprocess
+    import sys
+    args = [sys.executable, "-c", _REF_LOADER, str(path), str(hidden)] + ([fsdp] if fsdp else [])
+    r = subprocess.run(args, capture_output=True, text=True, cwd="/", timeout=300,
+                       env={k: v for k, v in __import__("os").environ.items() if k != "PYTHONPATH"})
+    assert r.returncode == 0 and "REF-LOAD-OK" in r.stdout, r.stderr[-3000:]
+
+
+def test_checkpoint_readable_by_reference_loader(tmp_path):
+    """Reverse direction: a DDP checkpoint written by this package
+    pickles its configs as models.config.GPTConfig / __main__.TrainingConfig, so a
+    process WITHOUT this package (import blocked) loads it with weights_only=True given
+    only the reference's own classes -- and our side still loads it too."""
+    from distributed_llm_trainer_amd.training.configs import TrainingConfig
+    from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
+    cfg = GPTConfig(vocab_size=128, hidden_size=64, num_layers=1, num_heads=2, max_seq_len=32,
+                    dropout=0.0, attention_dropout=0.0)
+    tr = DistributedTrainer(cfg, TrainingConfig(batch_size=2, gradient_accumulation_steps=1, warmup_steps=1))
+    path = tmp_path / "final.pt"
+    tr.save_checkpoint(str(path))
+    raw = open(path, "rb").read()
+    assert b"distributed_llm_trainer_amd" not in raw
+    _ref_load(path, 64)
+    c = load_checkpoint(str(path))
+    assert c["model_config"].hidden_size == 64 and isinstance(c["model_config"], GPTConfig)
+    import sys
+    assert "models.config" not in sys.modules  # the pickling aliases were removed again
+    # saving again what was loaded (alias instances) keeps the reference paths
+    save_checkpoint(str(tmp_path / "again.pt"), c)
+    _ref_load(tmp_path / "again.pt", 64)
+
+
+def test_fsdp_checkpoint_readable_by_reference_loader(tmp_path):
+    """Same for the FSDP trainer's FULL_STATE_DICT file (adds __main__.FSDPConfig)."""
+    from distributed_llm_trainer_amd.training.configs import FSDPConfig, FSDPTrainingConfig
+    path = tmp_path / "fsdp.pt"
+    cfg = GPTConfig(vocab_size=128, hidden_size=48, num_layers=1, num_heads=2, max_seq_len=32)
+    save_checkpoint(str(path), {"model": {"embed_tokens.weight": torch.zeros(128, 48)},
+                                "optimizer": {"state": {}, "param_groups": []}, "global_step": 5, "tokens_seen": 7,
+                                "model_config": cfg, "training_config": FSDPTrainingConfig(),
+                                "fsdp_config": FSDPConfig(sharding_strategy="SHARD_GRAD_OP")})
+    _ref_load(path, 48, "SHARD_GRAD_OP")
+    c = load_checkpoint(str(path))
+    assert c["fsdp_config"].sharding_strategy == "SHARD_GRAD_OP"
+
+
 def test_atomic_save(tmp_path):
     p = str(tmp_path / "a" / "b.pt")
     save_checkpoint(p, {"x": torch.arange(3)})
