@@ -50,6 +50,9 @@ def main():
                          "the JSON line then names a custom model and vs_baseline is null")
     ap.add_argument("--fusion", type=int, default=0,
                     help="micro_step_fusion: 0 = auto, 1 = run every micro-step on its own")
+    ap.add_argument("--memory_lean", action="store_true",
+                    help="TrainingConfig.defer_wgrad=False (the trainer's --memory_lean): per-chain weight "
+                         "gradients, lower peak memory")
     ap.add_argument("--dropout", type=float, default=None,
                     help="ablation only: override dropout/attention_dropout (reference config: 0.1)")
     args = ap.parse_args()
@@ -76,7 +79,8 @@ def main():
         from distributed_llm_trainer_amd.training.configs import TrainingConfig
         from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
         tc = TrainingConfig(batch_size=args.batch_size, gradient_accumulation_steps=args.grad_accum,
-                            max_steps=100000, mixed_precision="bf16", micro_step_fusion=args.fusion)
+                            max_steps=100000, mixed_precision="bf16", micro_step_fusion=args.fusion,
+                            defer_wgrad=not args.memory_lean)
         trainer = DistributedTrainer(cfg, tc)
     else:
         from distributed_llm_trainer_amd.training.configs import FSDPConfig, FSDPTrainingConfig
@@ -134,7 +138,8 @@ def main():
                        "global_batch": B * world, "seq_len": args.seq_len,
                        "parallelism": f"{args.mode}{world}", "micro_batch": args.batch_size,
                        "grad_accum": args.grad_accum,
-                       "micro_step_fusion": trainer.fusion_factor(args.grad_accum, args.batch_size, args.seq_len)},
+                       "micro_step_fusion": trainer.fusion_factor(args.grad_accum, args.batch_size, args.seq_len),
+                       **({"memory_lean": True} if args.memory_lean else {})},
             "peak_gb_per_gpu": round(peak, 3), "final_loss": round(loss, 4),
             "vs_baseline_linear": None if overrides else round(tps / (12500.0 * world), 3),
         }

@@ -402,6 +402,33 @@ __global__ __launch_bounds__(256) void k_splitk_acc(const float4* __restrict__ p
   }
 }
 
+// out[i] = bf16(sum_{s < splits} part[s * n + i]) -- the split-K weight gradient written
+// straight in the reduce dtype (FSDP: the per-micro-step unit gradient IS the
+// reduce-scatter send buffer, no fp32 zero / accumulate / cast passes).  Fixed order.
+__global__ __launch_bounds__(256) void k_splitk_sum_bf16(const float4* __restrict__ part, uint2* __restrict__ out,
+                                                         long n4, int splits) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    float4 a = part[i];
+    for (int s = 1; s < splits; ++s) {
+      const float4 p = part[(long)s * n4 + i];
+      a.x += p.x;
+      a.y += p.y;
+      a.z += p.z;
+      a.w += p.w;
+    }
+    out[i] = uint2{(uint32_t)f2bf(a.x) | ((uint32_t)f2bf(a.y) << 16), (uint32_t)f2bf(a.z) | ((uint32_t)f2bf(a.w) << 16)};
+  }
+}
+
+DLT_API int dlt_splitk_sum_bf16(const float* part, bf16_t* out, long n, int splits, hipStream_t s) {
+  if (n <= 0 || (n & 3) || splits < 1) return -1;
+  const long n4 = n / 4;
+  const int blocks = (int)std::min<long>((n4 + 255) / 256, 2048);
+  hipLaunchKernelGGL(k_splitk_sum_bf16, dim3(blocks), dim3(256), 0, s, reinterpret_cast<const float4*>(part),
+                     reinterpret_cast<uint2*>(out), n4, splits);
+  return (int)hipGetLastError();
+}
+
 DLT_API int dlt_splitk_acc(const float* part, float* dw, long n, int splits, hipStream_t s) {
   if (n <= 0 || (n & 3) || splits < 1) return -1;
   const long n4 = n / 4;

@@ -437,7 +437,32 @@ class HipGemm:
         self._splitk[key] = choice
         return choice
 
+    def wgrad_set(self, dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
+        """dw (bf16, overwritten) = dy^T @ x: a weight gradient written straight in the
+        reduce dtype (the FSDP runtime's per-micro-step send buffer).  Library GEMM with
+        beta = 0 and a bf16 D, or the raced split-K slices summed into bf16 in fixed order."""
+        from . import hip
+        M, N = dy.shape
+        K = x.shape[1]
+        dw2 = dw.view(N, K)
+        if dw2.dtype != torch.bfloat16 or not dw2.is_contiguous():
+            raise ValueError("wgrad_set output must be contiguous bf16")
+        key = (M, N, K)
+        s = self._splitk.get(key)
+        if s is None:  # race on an fp32 scratch like wgrad_acc (same key, same decision)
+            s = self._pick_splitk(torch.zeros(N, K, dtype=torch.float32, device=dw.device), dy, x)
+        if s > 1:
+            ms = M // s
+            lx, ly = _rowmajor(x), _rowmajor(dy)
+            part = torch.empty(s, N, K, dtype=torch.float32, device=dw.device)
+            _gemm_batched(0, 1, K, N, ms, x, lx, ms * lx, dy, ly, ms * ly, part, K, N * K, s, 1.0, 0.0)
+            hip.splitk_sum_bf16(part, dw2)
+        else:
+            _gemm(0, 1, K, N, M, x, _rowmajor(x), dy, _rowmajor(dy), dw2, K, 1.0, 0.0)
+
     def wgrad_acc(self, dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
+        if dw.dtype == torch.bfloat16:  # a reduce-dtype gradient buffer (first and only write)
+            return self.wgrad_set(dw, dy, x)
         M, N = dy.shape
         K = x.shape[1]
         dw2 = dw.view(N, K)

@@ -38,6 +38,7 @@ _SIGS = {
     "dlt_embedding_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "dlt_embedding_bwd_chunk": [],
     "dlt_splitk_acc": [c_void_p, c_void_p, ctypes.c_long, c_int, c_void_p],
+    "dlt_splitk_sum_bf16": [c_void_p, c_void_p, ctypes.c_long, c_int, c_void_p],
     "dlt_rope_qkv_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                          c_void_p],
     "dlt_rope_qkv_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
@@ -243,6 +244,16 @@ def splitk_acc(part: torch.Tensor, dw: torch.Tensor) -> None:
     if part.numel() % n or n % 4:
         raise ValueError("splitk_acc: part must hold whole copies of dw and dw.numel() % 4 == 0")
     _chk(lib().dlt_splitk_acc(_p(part), _p(dw), n, part.numel() // n, _stream()), "splitk_acc")
+
+
+def splitk_sum_bf16(part: torch.Tensor, out: torch.Tensor) -> None:
+    """out (bf16) = part.sum(0) in fixed order; part [splits, *out.shape] fp32."""
+    _req(out, torch.bfloat16, "splitk_sum_bf16.out")
+    _req(part, torch.float32, "splitk_sum_bf16.part")
+    n = out.numel()
+    if part.numel() % n or n % 4 or out.data_ptr() % 8:
+        raise ValueError("splitk_sum_bf16: part must hold whole copies of out, out.numel() % 4 == 0")
+    _chk(lib().dlt_splitk_sum_bf16(_p(part), _p(out), n, part.numel() // n, _stream()), "splitk_sum_bf16")
 
 
 # ---------------------------------------------------------------- embedding

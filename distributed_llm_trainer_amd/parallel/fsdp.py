@@ -88,6 +88,7 @@ class FlatUnit:
         self.rs_pending = []
         self.refs = 0            # chains (forward / backward of a micro-step) using `full`
         self.ready_ev = None     # HIP event: `full` is complete (recorded after the gather wait)
+        self.norm_grad = None    # bf16-gradient mode: fp32 ln1 | ln2 gradients of the micro-step
 
     def local_slice(self) -> Tuple[int, int]:
         return self.rank * self.shard, (self.rank + 1) * self.shard
@@ -127,6 +128,19 @@ class FSDPRuntime(ParamProvider):
         # DLT_FORCE_COLLECTIVES=1 (see parallel/ddp.py): one rank still all-gathers and
         # reduce-scatters through the process group instead of aliasing its shard
         self.force = self.dist and self.world == 1 and os.environ.get("DLT_FORCE_COLLECTIVES") == "1"
+        # Per-micro-step unit gradients straight in the reduce dtype: with bf16 reduction
+        # on every micro-step (the reference's FSDP schedule) the weight-gradient GEMMs
+        # write the bf16 send buffer directly (beta = 0, HipGemm.wgrad_set), the norm
+        # weights accumulate in a tiny fp32 side buffer that is cast into it before the
+        # reduce-scatter -- no fp32 zero / accumulate / cast passes over the unit.
+        self.bf16_grads = (reduce_dtype == torch.bfloat16 and sync_every_micro_step and self.device.type == "cuda"
+                           and os.environ.get("DLT_FSDP_BF16_GRADS", "1") != "0")
+        # limit_all_gathers (reference fsdp_trainer.py:296): at most this many prefetched
+        # (issued ahead of use, not yet consumed) all-gathers in flight -- one per
+        # micro-step chain (GPTEngine.train_window runs two chains)
+        self.max_prefetch = 2 if limit_all_gathers else 1 << 30
+        self._prefetched = set()
+        self._rep_stream = None  # HYBRID_SHARD: replicate all-reduces off the compute stream
         self.units: Dict[object, FlatUnit] = {}
         self._build_units(model)
         self._free_module_params(model)
@@ -205,6 +219,18 @@ class FSDPRuntime(ParamProvider):
             p.grad = None
 
     # ---------------------------------------------------------- collectives
+    def _prefetch(self, u: FlatUnit):
+        """Issue an all-gather ahead of use, within the limit_all_gathers budget (a
+        unit that does not get one is gathered synchronously when it is acquired)."""
+        if u.full is not None:
+            return
+        self._prefetched = {x for x in self._prefetched if x.ag_work is not None and x.refs == 0}
+        if len(self._prefetched) >= self.max_prefetch:
+            return
+        self._gather(u, async_op=True)
+        if u.ag_work is not None:
+            self._prefetched.add(u)
+
     def _gather(self, u: FlatUnit, async_op: bool):
         if u.full is not None and u.ag_work is None:
             return
@@ -236,6 +262,7 @@ class FSDPRuntime(ParamProvider):
     # when the last user releases it, every user's stream waits for the gather's
     # completion event, and the buffer is recorded on every stream that read it.
     def _acquire(self, u: FlatUnit):
+        self._prefetched.discard(u)
         self._wait_gather(u)
         if u.full is not None and u.full.is_cuda:
             cur = torch.cuda.current_stream(self.device)
@@ -272,6 +299,20 @@ class FSDPRuntime(ParamProvider):
             src = g if self.reduce_dtype == torch.float32 else g.to(self.reduce_dtype)
             out = torch.empty(u.shard, dtype=src.dtype, device=self.device)
             work = dist.reduce_scatter_tensor(out, src, group=self.pg, async_op=True)
+            if self.rep_pg is not None and self.strategy == "HYBRID_SHARD":
+                # replicate all-reduce chained behind the reduce-scatter on a side stream:
+                # overlaps the rest of the backward instead of running inside finish()
+                if self._rep_stream is None:
+                    self._rep_stream = torch.cuda.Stream(self.device) if out.is_cuda else None
+                ctx = torch.cuda.stream(self._rep_stream) if self._rep_stream is not None else None
+                if ctx is not None:
+                    with ctx:
+                        work.wait()  # device-side: the side stream waits for the reduce-scatter
+                        out.record_stream(self._rep_stream)
+                        work = dist.all_reduce(out, group=self.rep_pg, async_op=True)
+                else:
+                    work.wait()
+                    work = dist.all_reduce(out, group=self.rep_pg, async_op=True)
             u.rs_pending.append((work, out, src))
         u.full_grad = None
 
@@ -279,8 +320,6 @@ class FSDPRuntime(ParamProvider):
         for work, out, _src in u.rs_pending:
             if work is not None:
                 work.wait()
-            if self.rep_pg is not None and self.strategy == "HYBRID_SHARD":
-                dist.all_reduce(out, group=self.rep_pg)
             if out.numel() != u.shard:  # NO_SHARD: full buffer == shard
                 out = out[:u.shard]
             if out.is_cuda:  # produced on the backward's stream (maybe the pipeline stream)
@@ -319,17 +358,27 @@ class FSDPRuntime(ParamProvider):
 
     def layer_grads(self, i):
         u = self.units[i]
-        if u.full_grad is None:
-            u.full_grad = torch.zeros(u.padded, dtype=torch.float32, device=self.device)
         H, I = self.cfg.hidden_size, self.cfg.intermediate_size
+        if u.full_grad is None:
+            if self.bf16_grads:  # every segment is written (not accumulated) once per micro-step
+                u.full_grad = torch.empty(u.padded, dtype=torch.bfloat16, device=self.device)
+                if u.padded > u.numel:
+                    u.full_grad[u.numel:].zero_()
+                u.norm_grad = torch.zeros(2 * H, dtype=torch.float32, device=self.device)
+            else:
+                u.full_grad = torch.zeros(u.padded, dtype=torch.float32, device=self.device)
         p = f"layers.{i}."
         g = u.full_grad
+        if g.dtype == torch.bfloat16:
+            ln1, ln2 = u.norm_grad[:H], u.norm_grad[H:]
+        else:
+            ln1 = self._view(u, g, p + "input_layernorm.weight")
+            ln2 = self._view(u, g, p + "post_attention_layernorm.weight")
         return LayerGrads(wqkv=self._view(u, g, p + "attention.q_proj.weight", 3 * H, H),
                           wo=self._view(u, g, p + "attention.o_proj.weight", H, H),
                           wgu=self._view(u, g, p + "mlp.gate_proj.weight", 2 * I, H),
                           wdown=self._view(u, g, p + "mlp.down_proj.weight", H, I),
-                          ln1=self._view(u, g, p + "input_layernorm.weight"),
-                          ln2=self._view(u, g, p + "post_attention_layernorm.weight"))
+                          ln1=ln1, ln2=ln2)
 
     def head(self):
         u = self.units["head"]
@@ -361,7 +410,7 @@ class FSDPRuntime(ParamProvider):
         self._acquire(u)
         nxt = self._next(uid, True)
         if nxt is not None:  # forward prefetch of the next unit
-            self._gather(self.units[nxt], async_op=True)
+            self._prefetch(self.units[nxt])
 
     def post_forward(self, uid):
         # the root stays gathered until its backward (like FSDP's root unit)
@@ -373,10 +422,17 @@ class FSDPRuntime(ParamProvider):
         if self.prefetch == "BACKWARD_PRE":
             nxt = self._next(uid, False)
             if nxt is not None and nxt != "head":
-                self._gather(self.units[nxt], async_op=True)
+                self._prefetch(self.units[nxt])
 
     def post_backward(self, uid):
         u = self.units[uid]
+        if u.full_grad is not None and u.full_grad.dtype == torch.bfloat16 and uid != "head":
+            # the norm-weight gradients (fp32 side buffer) into the bf16 send buffer
+            H = self.cfg.hidden_size
+            p = f"layers.{uid}."
+            self._view(u, u.full_grad, p + "input_layernorm.weight").copy_(u.norm_grad[:H])
+            self._view(u, u.full_grad, p + "post_attention_layernorm.weight").copy_(u.norm_grad[H:])
+            u.norm_grad = None
         do_reduce = self.sync or self.sync_every_micro_step
         if do_reduce:
             self._reduce(u)
@@ -384,7 +440,7 @@ class FSDPRuntime(ParamProvider):
         if uid != "head" and self.prefetch == "BACKWARD_POST":
             nxt = self._next(uid, False)
             if nxt is not None and nxt != "head":
-                self._gather(self.units[nxt], async_op=True)
+                self._prefetch(self.units[nxt])
 
     def require_sync(self, flag: bool):
         self.sync = bool(flag)
@@ -404,25 +460,27 @@ class FSDPRuntime(ParamProvider):
         self.shard_c_flat.copy_(self.master_flat.to(self.device).to(self.compute_dtype))
 
     # ------------------------------------------------------------ state dict
-    @torch.no_grad()
-    def full_param_flat(self, uid, to_rank0_only: bool = True) -> Optional[torch.Tensor]:
-        """Gather a unit's fp32 master params (FULL_STATE_DICT)."""
-        u = self.units[uid]
-        src = u.master.to(self.device)
-        if self.shard_world == 1:
-            return src.cpu()
-        out = torch.empty(u.padded, dtype=torch.float32, device=self.device)
-        dist.all_gather_into_tensor(out, src, group=self.pg)
-        return out.cpu()
+    def _is_rank0(self) -> bool:
+        return not self.dist or dist.get_rank() == 0
 
     @torch.no_grad()
-    def gather_shard_tensor(self, uid, shard: torch.Tensor) -> torch.Tensor:
+    def full_param_flat(self, uid, rank0_only: bool = False) -> Optional[torch.Tensor]:
+        """Gather a unit's fp32 master params (FULL_STATE_DICT).  With ``rank0_only``
+        (the reference's ``FullStateDictConfig(offload_to_cpu=True, rank0_only=True)``,
+        ``fsdp_trainer.py:447``) only rank 0 gets the host copy; the other ranks take part
+        in the device all-gather and return None."""
+        return self.gather_shard_tensor(uid, self.units[uid].master, rank0_only=rank0_only)
+
+    @torch.no_grad()
+    def gather_shard_tensor(self, uid, shard: torch.Tensor, rank0_only: bool = False) -> Optional[torch.Tensor]:
         u = self.units[uid]
         src = shard.to(self.device).float()
         if self.shard_world == 1:
-            return src.cpu()
+            return src.cpu() if (not rank0_only or self._is_rank0()) else None
         out = torch.empty(u.padded, dtype=torch.float32, device=self.device)
         dist.all_gather_into_tensor(out, src, group=self.pg)
+        if rank0_only and not self._is_rank0():
+            return None  # the device buffer is freed at once: no host copy on this rank
         return out.cpu()
 
     @torch.no_grad()
@@ -432,14 +490,17 @@ class FSDPRuntime(ParamProvider):
         u.master.copy_(full[a:b].to(u.master.device))
         u.shard_c.copy_(full[a:b].to(self.device).to(self.compute_dtype))
 
-    def state_dict_full(self) -> Dict[str, torch.Tensor]:
-        """Reference-format fp32 state dict (gathers every unit); RoPE buffers added."""
+    def state_dict_full(self, rank0_only: bool = False) -> Optional[Dict[str, torch.Tensor]]:
+        """Reference-format fp32 state dict (gathers every unit; collective).  With
+        ``rank0_only`` the other ranks return None and never hold a host copy."""
         sd = {}
         for uid, u in self.units.items():
-            full = self.full_param_flat(uid)
+            full = self.full_param_flat(uid, rank0_only=rank0_only)
+            if full is None:
+                continue
             for s in u.segs:
                 sd[s.name] = full[s.offset:s.offset + s.numel].view(s.shape).clone()
-        return sd
+        return sd if (not rank0_only or self._is_rank0()) else None
 
 
 def _hybrid_groups():

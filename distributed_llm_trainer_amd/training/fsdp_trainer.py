@@ -8,8 +8,8 @@ Differences from the reference by design:
 * Activation checkpointing (default ON, like the reference) recomputes each block
   from its saved fp32 input; dropout masks replay bit-exactly (counter RNG).
 * ``HYBRID_SHARD`` is implemented (the reference documents but does not map it).
-* fp16: a loss scale is applied (the reference has none for FSDP fp16, Q11) --
-  fp16 runs through the eager path; bf16 is the fused path.
+* Precision (``FSDPConfig.mixed_precision``): see ``_setup_model`` for the bf16 /
+  fp16 / fp32 policies.
 * Seeded init, so every rank shards the same initial model (Q13).
 * Checkpoints: FULL_STATE_DICT format of the reference (fp32 params with the same
   keys + FQN-keyed, unflattened optimizer state, one param group); loading reads
@@ -189,9 +189,14 @@ class FSDPTrainer:
         return out
 
     # ------------------------------------------------------------ checkpoints
-    def _full_state(self):
+    def _full_state(self, rank0_only: bool = False):
+        """FULL_STATE_DICT (collective).  ``rank0_only``: None on ranks > 0, which never
+        hold a host copy (what save_checkpoint uses, like the reference's
+        ``FullStateDictConfig(offload_to_cpu=True, rank0_only=True)``)."""
         rt = self.runtime
-        sd = rt.state_dict_full()
+        sd = rt.state_dict_full(rank0_only=rank0_only)
+        if sd is None:
+            return None
         # RoPE buffers (reference checkpoints carry them) in module order
         out = {}
         for k, v in self.model.state_dict().items():
@@ -203,15 +208,17 @@ class FSDPTrainer:
                 out[k] = v.detach().cpu().clone()
         return out
 
-    def _full_optim_state(self):
+    def _full_optim_state(self, rank0_only: bool = False):
         rt, opt = self.runtime, self.optimizer
         state, names = {}, []
         order = [n for n, _ in self.model.named_parameters()]
         pieces = {}
         for uid, u in rt.units.items():
             a, b = rt.unit_offsets[uid]
-            m = rt.gather_shard_tensor(uid, opt.exp_avg[a:b])
-            v = rt.gather_shard_tensor(uid, opt.exp_avg_sq[a:b])
+            m = rt.gather_shard_tensor(uid, opt.exp_avg[a:b], rank0_only=rank0_only)
+            v = rt.gather_shard_tensor(uid, opt.exp_avg_sq[a:b], rank0_only=rank0_only)
+            if m is None:
+                continue
             for s in u.segs:
                 pieces[s.name] = (m[s.offset:s.offset + s.numel].view(s.shape).clone(),
                                   v[s.offset:s.offset + s.numel].view(s.shape).clone())
@@ -221,13 +228,15 @@ class FSDPTrainer:
             state[n] = {"step": torch.tensor(float(opt.step_count)), "exp_avg": pieces[n][0],
                         "exp_avg_sq": pieces[n][1]}
             names.append(n)
+        if not pieces:
+            return None  # rank > 0 under rank0_only
         g = {k: v for k, v in opt.param_groups[0].items()}
         g["params"] = names
         return {"state": state, "param_groups": [g]}
 
     def save_checkpoint(self, path: str):
-        model_sd = self._full_state()          # collective: every rank participates
-        optim_sd = self._full_optim_state()    # collective
+        model_sd = self._full_state(rank0_only=True)          # collective; None on ranks > 0
+        optim_sd = self._full_optim_state(rank0_only=True)    # collective
         if self.is_main_process:
             ckpt.save_checkpoint(path, {
                 "model": model_sd, "optimizer": optim_sd, "global_step": self.global_step,

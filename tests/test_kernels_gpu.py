@@ -578,3 +578,26 @@ def test_add_bf16_into_f32():
     assert hip.add_bf16_into_f32(dst, src)
     assert torch.equal(dst, want)
     assert not hip.add_bf16_into_f32(dst[:13], src[:13])  # outside the vector path: caller falls back
+
+
+@pytest.mark.parametrize("B,S,nh", [(2, 1024, 25), (16, 1024, 12)])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attention_packed_real_shapes(B, S, nh, p):
+    """The packed attention kernels at the model's own shapes -- xl (nh 25: packed row
+    stride 3*25*64 = 4800) and the GPT-2-small fused chain (B16 x nh 12) -- against the
+    fp32 reference of the whole chain, with per-tensor relative-error bounds."""
+    torch.manual_seed(B * nh + S)
+    H = nh * 64
+    raw = torch.randn(B * S, 3 * H, device=DEV).bfloat16()
+    cos, sin = hip.rope_tables(64, S, device=DEV)
+    key = rng.site_key(3, 1, 4, rng.SITE_ATTN)
+    packed = hip.rope_qk_inplace(raw.clone(), B, S, nh, cos, sin)
+    o, aux = hip.attention_fwd_packed(packed, B, S, nh, p, key)
+    o_ref, lse_ref = ref.attention_fwd_packed(packed.float(), B, S, nh, p, key)
+    assert _relerr(o, o_ref) < 1.5e-2
+    _close(aux[0], lse_ref, 2e-3, 1e-3, "lse")
+    do = torch.randn(B * S, H, device=DEV).bfloat16()
+    got = hip.attention_bwd_packed(packed, o, do, aux, p, key, B, S, nh, cos, sin)
+    want = ref.attention_bwd_packed(packed.float(), o.float(), do.float(), lse_ref, p, key, B, S, nh, cos, sin)
+    for blk, name in ((slice(0, H), "dq"), (slice(H, 2 * H), "dk"), (slice(2 * H, 3 * H), "dv")):
+        assert _relerr(got[:, blk], want[:, blk]) < 2e-2, name

@@ -79,6 +79,28 @@ def test_trainer_pipelined_step_matches_sequential():
     assert torch.allclose(res[0][1], res[1][1], atol=1e-7, rtol=1e-6)
 
 
+def test_trainer_memory_lean_matches_deferred():
+    """--memory_lean (defer_wgrad=False: each pipelined chain runs its own weight
+    gradients, no slot buffers) trains like the default deferred schedule (same sums in
+    another order: allclose, not bitwise)."""
+    from distributed_llm_trainer_amd.training.configs import TrainingConfig
+    from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
+    torch.manual_seed(14)
+    data = torch.randint(0, 256, (8, 32))
+    res = []
+    for defer in (True, False):
+        tc = TrainingConfig(batch_size=2, gradient_accumulation_steps=4, warmup_steps=2, max_steps=10,
+                            defer_wgrad=defer)
+        tr = DistributedTrainer(tiny(), tc)
+        losses = [tr.train_step({"input_ids": data})["loss"] for _ in range(3)]
+        res.append((losses, tr.store.flat.clone()))
+        if not defer:
+            assert not tr.model.engine._slots  # nothing deferred, no slot buffers
+    for a, b in zip(res[0][0], res[1][0]):
+        assert abs(a - b) < 1e-5
+    assert torch.allclose(res[0][1], res[1][1], atol=1e-6, rtol=1e-5)
+
+
 def test_packed_qkv_reference_matches_split():
     torch.manual_seed(14)
     B, S, nh, hd = 2, 24, 3, 16
