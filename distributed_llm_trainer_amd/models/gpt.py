@@ -182,10 +182,18 @@ class GPT(nn.Module):
             from ..parallel.flat import FlatParamStore
             provider = FlatParamStore(self, dev, compute_dtype=compute_dtype)
             self.store = provider
+        torch_ops_on_gpu = False
         if ops is None:
-            ops = ops_mod.for_device(dev, head_dim=self.config.head_dim)
+            if dev.type == "cuda" and act_dtype != torch.bfloat16:
+                # fp16 / fp32 models (--mixed_precision fp16|fp32): the HIP kernels store
+                # bf16 activations, so the engine's schedule runs with PyTorch ops on the
+                # GPU for the elementwise / norm / attention work and hipBLASLt GEMMs
+                ops = ops_mod.CPU_OPS
+                torch_ops_on_gpu = True
+            else:
+                ops = ops_mod.for_device(dev, head_dim=self.config.head_dim)
         gemm = None
-        if dev.type == "cuda" and ops.backend == "hip":
+        if dev.type == "cuda" and (ops.backend == "hip" or torch_ops_on_gpu):
             import os
             from ..ops import gemm as gemm_mod
             if os.environ.get("DLT_GEMM", "planner") == "planner" and gemm_mod.available():

@@ -97,7 +97,18 @@ __device__ __forceinline__ void st4(float* a, int64_t i, float4 x) {
   }
 }
 
-template <bool NTM, int OCC = 1>
+// 16-bit shadow conversion: bf16 (the fused engine) or fp16 (--mixed_precision fp16)
+template <bool F16>
+__device__ __forceinline__ uint16_t to_shadow(float x) {
+  if constexpr (F16) {
+    _Float16 h = (_Float16)x;
+    return __builtin_bit_cast(uint16_t, h);
+  } else {
+    return f2bf(x);
+  }
+}
+
+template <bool NTM, int OCC = 1, bool F16 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void k_adamw(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                                                float* __restrict__ v, bf16_t* __restrict__ shadow, int64_t n, float lr,
                                                float b1, float b2, float eps, float wd, float step_size,
@@ -115,7 +126,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
     st4<NTM>(v, i, vv);
     if (shadow) {
       u16x4 s;
-      s.v[0] = f2bf(pp.x); s.v[1] = f2bf(pp.y); s.v[2] = f2bf(pp.z); s.v[3] = f2bf(pp.w);
+      s.v[0] = to_shadow<F16>(pp.x); s.v[1] = to_shadow<F16>(pp.y);
+      s.v[2] = to_shadow<F16>(pp.z); s.v[3] = to_shadow<F16>(pp.w);
       if (NTM) {
         const uint2 w = __builtin_bit_cast(uint2, s);
         uint32_t* q = reinterpret_cast<uint32_t*>(shadow) + 2 * i;
@@ -145,7 +157,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       float pp = p[i], mm = m[i], vv = v[i];
       adam_elem(pp, g[i] * gs, mm, vv, lr, b1, b2, eps, wd, step_size, inv_bc2_sqrt);
       p[i] = pp; m[i] = mm; v[i] = vv;
-      if (shadow) shadow[i] = f2bf(pp);
+      if (shadow) shadow[i] = to_shadow<F16>(pp);
     }
   }
 }
@@ -202,6 +214,17 @@ DLT_API int dlt_adamw(float* p, const float* g, float* m, float* v, bf16_t* shad
   else
     k_adamw<false><<<flat_blocks(n), 256, 0, st>>>(p, g, m, v, shadow, n, lr, b1, b2, eps, wd, step_size, inv_bc2_sqrt,
                                                    gscale);
+  DLT_CHECK_LAUNCH();
+}
+
+// AdamW with an fp16 shadow (the engine's --mixed_precision fp16 weights)
+DLT_API int dlt_adamw_f16(float* p, const float* g, float* m, float* v, bf16_t* shadow, int64_t n, float lr, float b1,
+                          float b2, float eps, float wd, float step_size, float inv_bc2_sqrt, const float* gscale,
+                          hipStream_t st) {
+  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return -1;
+  if (shadow && ((uintptr_t)shadow & 7)) return -1;
+  k_adamw<false, 1, true><<<flat_blocks(n), 256, 0, st>>>(p, g, m, v, shadow, n, lr, b1, b2, eps, wd, step_size,
+                                                          inv_bc2_sqrt, gscale);
   DLT_CHECK_LAUNCH();
 }
 

@@ -50,6 +50,8 @@ _SIGS = {
     "dlt_clip_coef": [c_void_p, c_void_p, c_float, c_float, c_float, c_void_p],
     "dlt_adamw": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float, c_float,
                   c_float, c_float, c_float, c_void_p, c_void_p],
+    "dlt_adamw_f16": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float, c_float,
+                      c_float, c_float, c_float, c_void_p, c_void_p],
     "dlt_cast_bf16": [c_void_p, c_void_p, c_int64, c_void_p],
     "dlt_add_bf16_f32": [c_void_p, c_void_p, c_int64, c_void_p],
     "dlt_wgrad_gemm": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
@@ -604,12 +606,13 @@ def adamw_flat(param, grad, exp_avg, exp_avg_sq, shadow, lr, beta1, beta2, eps, 
     n = param.numel()
     for t, nm in ((param, "param"), (grad, "grad"), (exp_avg, "exp_avg"), (exp_avg_sq, "exp_avg_sq")):
         _req(t, torch.float32, "adamw." + nm, n)
-    if shadow is not None and (shadow.dtype != torch.bfloat16 or shadow.numel() != n):
-        raise ValueError("adamw.shadow must be bf16 of the same numel")
+    if shadow is not None and (shadow.dtype not in (torch.bfloat16, torch.float16) or shadow.numel() != n):
+        raise ValueError("adamw.shadow must be bf16 or fp16 of the same numel")
     bc1 = 1.0 - beta1 ** step
     bc2 = 1.0 - beta2 ** step
-    _chk(lib().dlt_adamw(_p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), _p(shadow), n, lr, beta1, beta2, eps, wd,
-                         lr / bc1, 1.0 / math.sqrt(bc2), _p(gscale), _stream()), "adamw")
+    fn = lib().dlt_adamw_f16 if (shadow is not None and shadow.dtype == torch.float16) else lib().dlt_adamw
+    _chk(fn(_p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), _p(shadow), n, lr, beta1, beta2, eps, wd,
+            lr / bc1, 1.0 / math.sqrt(bc2), _p(gscale), _stream()), "adamw")
 
 
 def add_bf16_into_f32(dst: torch.Tensor, src: torch.Tensor) -> bool:

@@ -192,7 +192,10 @@ class FSDPRuntime(ParamProvider):
         if pin:
             self.master_flat = self.master_flat.pin_memory()
             self.grad_flat = self.grad_flat.pin_memory()
-        self.shard_c_flat = torch.zeros(total, dtype=self.compute_dtype, device=self.device)
+        if self.compute_dtype == torch.float32 and not self.cpu_offload:
+            self.shard_c_flat = self.master_flat  # fp32 policy: the master shard IS the all-gather input
+        else:
+            self.shard_c_flat = torch.zeros(total, dtype=self.compute_dtype, device=self.device)
         off = 0
         self.unit_offsets = {}
         for uid in order:
@@ -457,7 +460,8 @@ class FSDPRuntime(ParamProvider):
 
     def refresh_shadow(self):
         """Re-derive the device compute-dtype shards from the fp32 masters."""
-        self.shard_c_flat.copy_(self.master_flat.to(self.device).to(self.compute_dtype))
+        if self.shard_c_flat is not self.master_flat:
+            self.shard_c_flat.copy_(self.master_flat.to(self.device).to(self.compute_dtype))
 
     # ------------------------------------------------------------ state dict
     def _is_rank0(self) -> bool:

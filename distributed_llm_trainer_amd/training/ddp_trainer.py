@@ -77,21 +77,29 @@ class DistributedTrainer:
         mp = self.training_config.mixed_precision
         cuda = self.device.type == "cuda"
         if use_engine is None:
-            use_engine = (not cuda) or mp == "bf16"
+            use_engine = True
         self.use_engine = use_engine
         self.autocast_ctx = contextlib.nullcontext()
         self.loss_scale = None
+        self._good_steps = 0
+        # reference ddp_trainer.py:129-152: bf16 autocast, fp16 autocast + GradScaler, or
+        # fp32.  Here every mode runs the fused engine with fp32 master weights and a
+        # compute-dtype shadow: bf16 on the HIP kernels; fp16 / fp32 with PyTorch ops on
+        # the GPU + hipBLASLt GEMMs (GPT.enable_engine) and, for fp16, dynamic loss scaling
+        # (2^16, x0.5 and skip on inf/nan, x2 after 2000 good steps: GradScaler defaults)
         if cuda and mp == "bf16":
             self.dtype = torch.bfloat16
         elif cuda and mp == "fp16":
             self.dtype = torch.float16
-            self.autocast_ctx = torch.autocast(device_type="cuda", dtype=torch.float16)
             self.loss_scale = 2.0 ** 16
+            if not use_engine:
+                self.autocast_ctx = torch.autocast(device_type="cuda", dtype=torch.float16)
         else:
             self.dtype = torch.float32
         if self.is_main_process:
-            path = "fused HIP engine" if (use_engine and cuda) else ("fused engine (CPU reference ops)"
-                                                                    if use_engine else "eager")
+            path = ("fused HIP engine" if self.dtype == torch.bfloat16 else "fused engine (PyTorch ops + hipBLASLt "
+                    "on the GPU)") if (use_engine and cuda) else ("fused engine (CPU reference ops)"
+                                                                  if use_engine else "eager")
             print(f"Device: {self.device}")
             print(f"Mixed precision: {mp} (dtype: {self.dtype}) | execution: {path}")
 
@@ -102,7 +110,8 @@ class DistributedTrainer:
         if self.is_main_process:
             print(f"Model parameters: {count_parameters(self.model):,}")
         if self.use_engine:
-            eng = self.model.enable_engine(seed=self.training_config.seed + 1000003 * self.rank)
+            act = self.dtype if self.device.type == "cuda" else None
+            eng = self.model.enable_engine(seed=self.training_config.seed + 1000003 * self.rank, act_dtype=act)
             self.store = self.model.store
         else:
             self.store = FlatParamStore(self.model, self.device, compute_dtype=torch.float32)
@@ -203,12 +212,15 @@ class DistributedTrainer:
         div = float(self.world_size) * (self.loss_scale or 1.0)
         scale = self.optimizer.compute_scale(cfg.grad_clip, grad_div=div)
         skip = False
-        if self.loss_scale is not None:  # fp16 dynamic loss scaling
+        if self.loss_scale is not None:  # fp16 dynamic loss scaling (the all-reduced grads: one decision)
             if not torch.isfinite(scale[0]).item():
                 self.loss_scale /= 2.0
+                self._good_steps = 0
                 skip = True
-            elif (self.global_step + 1) % 2000 == 0:
-                self.loss_scale *= 2.0
+            else:
+                self._good_steps += 1
+                if self._good_steps % 2000 == 0:
+                    self.loss_scale *= 2.0
         if not skip:
             self.optimizer.step(scale)
             if not self.use_engine:
@@ -385,6 +397,7 @@ def main(argv=None):
                   flush=True)
             if metrics_f:
                 rec = {"step": step, "loss": metrics["loss"], "lr": metrics["lr"], "tokens": metrics["tokens"],
+                       "elapsed_s": elapsed,
                        **({"loss_global": metrics["loss_global"]} if "loss_global" in metrics else {}),
                        "tokens_per_sec": tps, **trainer.get_memory_stats()}
                 if trainer._last_norm is not None:

