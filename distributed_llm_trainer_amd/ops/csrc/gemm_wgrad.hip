@@ -1,152 +1,342 @@
-// Weight-gradient GEMM:  C[N,K] (fp32, row-major) += A[M,N]^T . B[M,K]  (bf16 in).
+// Weight-gradient GEMM for the deferred wgrads of the transformer block (gfx950 / MI355X):
+//   dW[Nr, Nc] (fp32)  (+)=  dY[T, Nr]^T . X[T, Nc]        (bf16 in, fp32 accumulate)
+// -- the weight gradients of the projections of /root/reference/src/models/gpt.py:185-187,239
+// (q/k/v/o) and :278-281 (gate/up/down), reduced over the T = GA x B x S tokens of one
+// gradient-accumulation window (models/engine.py defers them to one GEMM per weight).
 //
-// Every projection's wgrad has this shape (dW = dY^T X with the reduction over the
-// B*S = 8192 token rows).  Both operands are stored with the reduction dim OUTER
-// (M-major), the one layout the library heuristics handle badly on gfx950
-// (180-700 TF/s measured, tools/wgrad_test.py).  Here both MFMA operands are read
-// straight out of row-major LDS tiles with ds_read_b64_tr_b16 (hardware transpose),
-// so no transposed copy of the activations or gradients is ever materialised, and
-// the fp32 result is accumulated in place into the optimizer's main-grad buffer
-// (fused "wgrad += " -- no bf16 round trip, no separate add kernel).
+// Both operands are TOKEN-major: the reduction index is the outer (row) index, so an MFMA
+// fragment -- 8 consecutive tokens of one output row or column -- is a column of the
+// row-major tile.  Tiles are staged row-major by LDS-DMA (whole 128/256-byte token rows,
+// fully coalesced) and the fragments are read with ds_read_b64_tr_b16, the hardware
+// transpose (cdna_hip_programming.md T10): two 4-token reads per 16x16x32 operand.
 //
-//   tile 128 (n) x 128 (k) per 256-thread workgroup, 4 waves as 2x2, each wave 64x64
-//   = 2x2 v_mfma_f32_32x32x16_bf16 accumulators; reduction staged 64 rows at a time
-//   through double-buffered LDS (register-staged global loads issued before the
-//   MFMAs of the current stage); split over M (gridDim.z) when the output has too
-//   few tiles to fill 256 CUs, combined with fp32 atomics (the L2-side atomic rate,
-//   1.3 TB/s, bounds that combine; splits are chosen to keep it small).
+// Structure: the persistent projection GEMM's pipeline (gemm_bf16.hip) -- 256 (rows of dW)
+// x 192 (columns) tiles, BK = 64 tokens, 512 threads = 8 waves as 4 (M) x 2 (N), each wave
+// 64 x 96 = 4 x 6 tiles of v_mfma_f32_16x16x32_bf16, 4 quadrant phases per K-tile, one
+// staging unit per phase (restaged >= 2 phases after its last read, retired by a counted
+// vmcnt(4) one phase before it is read), waves 4-7 one barrier behind 0-3.  Staging units
+// are separate row-major LDS images:
+//   A0 / A1: the 32-column halves of every wave's 64 rows of dW   [64 tok][128] (256-B rows)
+//   B0: n-tiles 0..3 of both N halves [64 tok][128];  B1: n-tiles 4..5 [64 tok][64] (128-B rows)
+// Source-side XOR swizzle of the 16-byte chunks of a token row (pc = lc ^ 2v(t)) makes
+// every transposed read conflict-free: a 32-lane half reads 8 token rows x 32 bytes, which
+// land on 8 distinct 32-byte bank slots (v(t) distinct over those rows; for 128-byte
+// rows the even / odd rows already sit in different bank halves).
+//
+// The reduction over T is split over workgroups (`splits`, chosen by the caller so that
+// tiles x splits fills the 256 CUs): each split writes its fp32 partial tile and
+// k_splitk_acc (elementwise.hip) adds the partials into dW in a FIXED order -- no float
+// atomics, bitwise run-to-run reproducible (DDP replicas stay identical).  With one split
+// the kernel adds straight into dW.
+//
+// Requirements (launcher-checked): Nr % 256 == 0, Nc % 192 == 0, T % 128 == 0, 16-byte
+// aligned rows.
 #include "common.h"
 
-#define WG_BN 128
-#define WG_BK 128
-#define WG_BM 64   // reduction rows per stage
+typedef __attribute__((address_space(3))) void* gw_lds_vptr_t;
+typedef short gw_sx8_t __attribute__((ext_vector_type(8)));
+typedef const __attribute__((address_space(1))) void* gw_gbl_cvptr_t;
 
-typedef __attribute__((address_space(3))) shortx4_t lds_sx4_t;
-typedef short sx8_t __attribute__((ext_vector_type(8)));
+namespace {
 
-// LDS tile [64 rows][128 bf16] (256-B rows); 16-B chunk c of row r at chunk c ^ ((r & 3) << 2):
-// the 4-row x 4-chunk footprint of one half-wave's transposed reads hits 16 distinct slots.
-__device__ __forceinline__ int wg_off(int row, int col) {
-  return row * 128 + ((((col >> 3) ^ ((row & 3) << 2))) << 3) + (col & 7);
+constexpr int GW_BK = 64;
+constexpr int GW_IMG_A = GW_BK * 128;  // elements of one A unit image / B0
+constexpr int GW_IMG_B1 = GW_BK * 64;
+constexpr int GW_BUF = 2 * GW_IMG_A + GW_IMG_A + GW_IMG_B1;  // A0, A1, B0, B1
+
+// chunk swizzle of token row t: 256-byte rows (16 chunks) / 128-byte rows (8 chunks)
+__device__ __forceinline__ int gw_v256(int t) { return (t & 3) | (((t >> 3) & 1) << 2); }
+__device__ __forceinline__ int gw_v128(int t) { return ((t >> 1) & 1) | (((t >> 3) & 1) << 1); }
+
+// image column -> column offset inside the tile's operand range
+//   A unit q: image col j -> dW row wm*64 + q*32 + (j & 31), wm = j / 32
+//   B0: image col j -> dW col (j / 64) * 96 + (j & 63);  B1: j -> (j / 32) * 96 + 64 + (j & 31)
+__device__ __forceinline__ int gw_amap(int q, int j) { return (j >> 5) * 64 + q * 32 + (j & 31); }
+__device__ __forceinline__ int gw_b0map(int j) { return (j >> 6) * 96 + (j & 63); }
+__device__ __forceinline__ int gw_b1map(int j) { return (j >> 5) * 96 + 64 + (j & 31); }
+
+// LDS byte offset of (token row t, column col) in an image with 256- or 128-byte rows
+template <int ROWB>
+__device__ __forceinline__ uint32_t gw_off(int t, int col) {
+  const int lc = col >> 3;
+  const int pc = lc ^ (2 * (ROWB == 256 ? gw_v256(t) : gw_v128(t)));
+  return (uint32_t)(t * ROWB + pc * 16 + (col & 7) * 2);
 }
 
-// 32x32x16 operand fragment for rows (=reduction index) 16*s + 8*h + {0..7} and
-// column c0 + (lane & 31): two transposed 4-row reads.
-__device__ __forceinline__ bf16x8_t wg_frag(const bf16_t* T, int s, int c0, int lane) {
-  const int h = lane >> 5, i = lane & 15;
-  const int col = c0 + 16 * ((lane >> 4) & 1) + 4 * (i & 3);
-  const int r = 16 * s + 8 * h + (i >> 2);
-  const shortx4_t a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_sx4_t*)(T + wg_off(r, col)));
-  const shortx4_t b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_sx4_t*)(T + wg_off(r + 4, col)));
-  sx8_t c = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+__device__ __forceinline__ shortx4_t gw_tr4(uint32_t addr) {
+  shortx4_t r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr));
+  return r;
+}
+
+// 16x16x32 operand fragment: tokens 32s + 8g + 0..7 (g = lane >> 4) of image column
+// 16k + (lane & 15).  For those token rows the swizzle value v(t) is the same for every
+// s and read half (t & 3 and bit 3 of t only depend on the lane), so a lane's address is
+//   img + lbase + (32s + 4h) * ROWB + 32 * (k ^ v)
+// with lbase / v per lane and 32 * (k ^ v) precomputed per k: the reads share a few base
+// registers and take (32s + 4h) * ROWB as an immediate offset.
+}  // namespace
+
+template <int ROWB>
+struct GwLane {
+  uint32_t base;  // (8g + q) * ROWB + 16 * ((i >> 1) & 1) + 8 * (i & 1)
+  int v;
+  __device__ __forceinline__ void init(int lane) {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2;
+    const int t = 8 * g + q;
+    base = (uint32_t)(t * ROWB + 16 * ((i >> 1) & 1) + 8 * (i & 1));
+    v = ROWB == 256 ? gw_v256(t) : gw_v128(t);
+  }
+  __device__ __forceinline__ uint32_t koff(int k) const { return (uint32_t)(32 * (k ^ v)); }
+};
+
+template <int ROWB>
+__device__ __forceinline__ bf16x8_t gw_frag(uint32_t img_lane_k, int s) {
+  const shortx4_t a = gw_tr4(img_lane_k + (uint32_t)(32 * s) * ROWB);
+  const shortx4_t b = gw_tr4(img_lane_k + (uint32_t)(32 * s + 4) * ROWB);
+  gw_sx8_t c = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
   return __builtin_bit_cast(bf16x8_t, c);
 }
 
-struct WgStage { u16x8 a[4], b[4]; };
+namespace {
+}  // namespace
 
-__device__ __forceinline__ void wg_load(WgStage& st, const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
-                                        int m0, int n0, int k0, int N, int K, int tid) {
-  // 64 rows x 16 chunks (16 B) per operand = 1024 chunks -> 4 per thread
+__global__ __launch_bounds__(512, 1) void k_gemm_wgrad(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X,
+                                                       float* __restrict__ out, int T, int Nr, int Nc, int ldy,
+                                                       int ldx, int splits, int accumulate) {
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * GW_BUF];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int half = wid >> 2;
+  const int wm = wid & 3, wn = wid >> 2;
+  const int l16 = lane & 15, lq = lane >> 4;
+
+  // workgroup -> (split, tile): the splits of one tile are consecutive workgroup ids
+  // (they share nothing but are issued together); tiles row-major over (Nr / 256, Nc / 192)
+  const int ntc = Nc / 192;
+  const int split = blockIdx.x % splits, tile = blockIdx.x / splits;
+  const int r0 = (tile / ntc) * 256, c0 = (tile % ntc) * 192;
+  const int npair = T / (2 * GW_BK);
+  const int p0 = (int)(((long)split * npair) / splits), p1 = (int)(((long)(split + 1) * npair) / splits);
+  const int kt0 = 2 * p0, nk = 2 * (p1 - p0);  // K-tiles [kt0, kt0 + nk), nk even >= 2
+
+  // images of buffer b (element offsets into lds): A0, A1, B0, B1.  DMA destinations are
+  // LDS pointers; the asm transposed reads take the 32-bit LDS address (the low word of
+  // the generic address of a __shared__ object, as in attention.hip)
+  auto eA = [&](int b, int q) { return b * GW_BUF + q * GW_IMG_A; };
+  auto eB0 = [&](int b) { return b * GW_BUF + 2 * GW_IMG_A; };
+  auto eB1 = [&](int b) { return b * GW_BUF + 3 * GW_IMG_A; };
+  auto laddr = [&](int e) { return (uint32_t)(uintptr_t)(lds + e); };
+  auto imgA = [&](int b, int q) { return laddr(eA(b, q)); };
+  auto imgB0 = [&](int b) { return laddr(eB0(b)); };
+  auto imgB1 = [&](int b) { return laddr(eB1(b)); };
+
+  // per-lane source offsets (bytes from the K-tile's first token row at the tile's column
+  // origin): 16 KB units = 16 DMA instructions (2 per wave, 4 token rows each), B1 = 8
+  // (1 per wave, 8 rows each)
+  uint32_t oa[2][2], ob0[2], ob1;
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int c = tid + 256 * u;
-    const int r = c >> 4, ch = c & 15;
-    st.a[u] = *reinterpret_cast<const u16x8*>(A + (size_t)(m0 + r) * N + n0 + ch * 8);
-    st.b[u] = *reinterpret_cast<const u16x8*>(B + (size_t)(m0 + r) * K + k0 + ch * 8);
+  for (int j = 0; j < 2; ++j) {
+    const int e = (wid * 2 + j) * 64 + lane;  // chunk index in the image
+    const int t = e >> 4, pc = e & 15;
+    const int lc = pc ^ (2 * gw_v256(t));
+#pragma unroll
+    for (int q = 0; q < 2; ++q) oa[q][j] = (uint32_t)(t * ldy + gw_amap(q, lc * 8)) * 2u;
+    ob0[j] = (uint32_t)(t * ldx + gw_b0map(lc * 8)) * 2u;
   }
-}
-
-__device__ __forceinline__ void wg_store(const WgStage& st, bf16_t* TA, bf16_t* TB, int tid) {
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int c = tid + 256 * u;
-    const int r = c >> 4, ch = c & 15;
-    *reinterpret_cast<u16x8*>(TA + wg_off(r, ch * 8)) = st.a[u];
-    *reinterpret_cast<u16x8*>(TB + wg_off(r, ch * 8)) = st.b[u];
+  {
+    const int e = wid * 64 + lane;
+    const int t = e >> 3, pc = e & 7;
+    const int lc = pc ^ (2 * gw_v128(t));
+    ob1 = (uint32_t)(t * ldx + gw_b1map(lc * 8)) * 2u;
   }
-}
-
-__global__ __launch_bounds__(256, 2) void k_wgrad_gemm(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
-                                                       float* __restrict__ C, int M, int N, int K, int rows_per_split,
-                                                       int use_atomics) {
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * 2 * WG_BM * 128];  // [buf][A|B][64][128]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wid >> 1, wk = wid & 1;
-  const int tiles_k = K / WG_BK;
-  // XCD-aware: consecutive blocks (round-robin over the 8 XCDs) get tiles sharing B columns
-  const int tile = blockIdx.x;
-  const int tn = tile / tiles_k, tk = tile % tiles_k;
-  const int n0 = tn * WG_BN, k0 = tk * WG_BK;
-  const int m_begin = blockIdx.y * rows_per_split;
-  const int m_end = min(M, m_begin + rows_per_split);
-  const int nst = (m_end - m_begin) / WG_BM;
-
-  floatx16_t acc[2][2];
+  const bf16_t* const Ab = dY + (size_t)kt0 * GW_BK * ldy + r0;
+  const bf16_t* const Bb = X + (size_t)kt0 * GW_BK * ldx + c0;
+  auto stA = [&](int kt, int q, int b) {  // kt relative to kt0
+    const char* g = (const char*)(Ab + (size_t)kt * GW_BK * ldy);
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_global_load_lds((gw_gbl_cvptr_t)(g + oa[q][j]),
+                                       (gw_lds_vptr_t)(lds + eA(b, q) + (wid * 2 + j) * 512), 16, 0, 0);
+  };
+  auto stB0 = [&](int kt, int b) {
+    const char* g = (const char*)(Bb + (size_t)kt * GW_BK * ldx);
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_global_load_lds((gw_gbl_cvptr_t)(g + ob0[j]),
+                                       (gw_lds_vptr_t)(lds + eB0(b) + (wid * 2 + j) * 512), 16, 0, 0);
+  };
+  auto stB1 = [&](int kt, int b) {
+    const char* g = (const char*)(Bb + (size_t)kt * GW_BK * ldx);
+    __builtin_amdgcn_global_load_lds((gw_gbl_cvptr_t)(g + ob1),
+                                     (gw_lds_vptr_t)(lds + eB1(b) + wid * 512), 16, 0, 0);
+  };
 
-  WgStage st;
-  if (nst > 0) {
-    wg_load(st, A, B, m_begin, n0, k0, N, K, tid);
-    wg_store(st, lds, lds + WG_BM * 128, tid);
+  floatx4_t acc[6][4];
+#pragma unroll
+  for (int a = 0; a < 6; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = floatx4_t{0.f, 0.f, 0.f, 0.f};
+  bf16x8_t fa[2][2], fb0[3][2], fb1[3][2];
+
+  GwLane<256> L256;
+  GwLane<128> L128;
+  L256.init(lane);
+  L128.init(lane);
+  // per-lane read bases: A fragments k = 2 wm + mt (16-column blocks of the A image), B0
+  // k = 4 wn + nt, B1 k = 2 wn + j
+  uint32_t ka[2], kb0[4], kb1[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    ka[j] = L256.base + L256.koff(2 * wm + j);
+    kb1[j] = L128.base + L128.koff(2 * wn + j);
   }
-  __syncthreads();
-  for (int s = 0; s < nst; ++s) {
-    const int cur = s & 1;
-    const bool more = s + 1 < nst;
-    if (more) wg_load(st, A, B, m_begin + (s + 1) * WG_BM, n0, k0, N, K, tid);
-    const bf16_t* TA = lds + cur * 2 * WG_BM * 128;
-    const bf16_t* TB = TA + WG_BM * 128;
 #pragma unroll
-    for (int ks = 0; ks < WG_BM / 16; ++ks) {
-      const bf16x8_t a0 = wg_frag(TA, ks, wn * 64, lane);
-      const bf16x8_t a1 = wg_frag(TA, ks, wn * 64 + 32, lane);
-      const bf16x8_t b0 = wg_frag(TB, ks, wk * 64, lane);
-      const bf16x8_t b1 = wg_frag(TB, ks, wk * 64 + 32, lane);
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[1][1], 0, 0, 0);
-    }
-    if (more) {
-      bf16_t* NA = lds + (cur ^ 1) * 2 * WG_BM * 128;
-      wg_store(st, NA, NA + WG_BM * 128, tid);
-    }
-    __syncthreads();
-  }
-  // epilogue: D[n][k] with k = lane column, n = accumulator row
-  const int h = lane >> 5;
+  for (int j = 0; j < 4; ++j) kb0[j] = L256.base + L256.koff(4 * wn + j);
+  auto read_a = [&](int b, int qm) {
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+    for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int kc = k0 + wk * 64 + b * 32 + (lane & 31);
+      for (int s = 0; s < 2; ++s) fa[mt][s] = gw_frag<256>(imgA(b, qm) + ka[mt], s);
+  };
+  // n-half 0: n-tiles 0..2 (B0); n-half 1: n-tile 3 (B0) and 4..5 (B1)
+  auto read_b = [&](int b, int qn, bf16x8_t (&fb)[3][2]) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int nr = n0 + wn * 64 + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-        float* p = C + (size_t)nr * K + kc;
-        if (use_atomics) unsafeAtomicAdd(p, acc[a][b][i]);
-        else *p += acc[a][b][i];
+    for (int s = 0; s < 2; ++s) {
+      if (qn == 0) {
+#pragma unroll
+        for (int nt = 0; nt < 3; ++nt) fb[nt][s] = gw_frag<256>(imgB0(b) + kb0[nt], s);
+      } else {
+        fb[0][s] = gw_frag<256>(imgB0(b) + kb0[3], s);
+        fb[1][s] = gw_frag<128>(imgB1(b) + kb1[0], s);
+        fb[2][s] = gw_frag<128>(imgB1(b) + kb1[1], s);
       }
     }
+  };
+  // retire this wave's transposed reads (asm, invisible to the compiler's lgkmcnt
+  // tracking: the fragments are in/out operands so no MFMA is scheduled above the wait)
+  auto lds_wait = [&](bf16x8_t (&fb)[3][2]) {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(fa[0][0]), "+v"(fa[0][1]), "+v"(fa[1][0]), "+v"(fa[1][1]), "+v"(fb[0][0]), "+v"(fb[0][1]),
+                   "+v"(fb[1][0]), "+v"(fb[1][1]), "+v"(fb[2][0]), "+v"(fb[2][1])::"memory");
+  };
+  auto mma = [&](int qm, int qn, bf16x8_t (&fb)[3][2]) {
+    lds_wait(fb);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int nt = 0; nt < 3; ++nt)
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+          acc[qn * 3 + nt][qm * 2 + mt] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nt][s], fa[mt][s], acc[qn * 3 + nt][qm * 2 + mt], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // prologue: K-tile 0 complete in buffer 0, A0/B0 of K-tile 1 in flight
+  stA(0, 0, 0);
+  stB0(0, 0);
+  stB1(0, 0);
+  stA(0, 1, 0);
+  stA(1, 0, 1);
+  stB0(1, 1);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (half == 1) __builtin_amdgcn_s_barrier();
+
+  for (int kt = 0; kt < nk; kt += 2) {
+    const bool more = kt + 2 < nk;
+    // ---- phase 1: buffer 0, q0 ; B1 of K-tile kt+1
+    read_b(0, 0, fb0);
+    read_a(0, 0);
+    stB1(kt + 1, 1);
+    __builtin_amdgcn_s_barrier();
+    mma(0, 0, fb0);
+    __builtin_amdgcn_s_barrier();
+    // ---- phase 2: q1 ; A1 of kt+1
+    read_b(0, 1, fb1);
+    stA(kt + 1, 1, 1);
+    __builtin_amdgcn_s_barrier();
+    mma(0, 1, fb1);
+    __builtin_amdgcn_s_barrier();
+    // ---- phase 3: q2 ; A0 of kt+2 into buffer 0
+    read_a(0, 1);
+    if (more) stA(kt + 2, 0, 0);
+    __builtin_amdgcn_s_barrier();
+    mma(1, 1, fb1);
+    __builtin_amdgcn_s_barrier();
+    // ---- phase 4: q3 (registers) ; B0 of kt+2 ; retire kt+1
+    if (more) {
+      stB0(kt + 2, 0);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    mma(1, 0, fb0);
+    __builtin_amdgcn_s_barrier();
+    // ---- phase 5: buffer 1, q0 ; B1 of kt+2
+    read_b(1, 0, fb0);
+    read_a(1, 0);
+    if (more) stB1(kt + 2, 0);
+    __builtin_amdgcn_s_barrier();
+    mma(0, 0, fb0);
+    __builtin_amdgcn_s_barrier();
+    // ---- phase 6: q1 ; A1 of kt+2
+    read_b(1, 1, fb1);
+    if (more) stA(kt + 2, 1, 0);
+    __builtin_amdgcn_s_barrier();
+    mma(0, 1, fb1);
+    __builtin_amdgcn_s_barrier();
+    // ---- phase 7: q2 ; A0 of kt+3 into buffer 1
+    read_a(1, 1);
+    if (more) stA(kt + 3, 0, 1);
+    __builtin_amdgcn_s_barrier();
+    mma(1, 1, fb1);
+    __builtin_amdgcn_s_barrier();
+    // ---- phase 8: q3 ; B0 of kt+3 ; retire kt+2
+    if (more) {
+      stB0(kt + 3, 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    mma(1, 0, fb0);
+    __builtin_amdgcn_s_barrier();
+  }
+  if (half == 0) __builtin_amdgcn_s_barrier();
+
+  // epilogue: acc[nt][mt] = D[n][m]: lane owns dW row r0 + wm*64 + mt*16 + l16 and the 4
+  // consecutive columns c0 + wn*96 + nt*16 + lq*4 .. +3 (one float4)
+  float* const dst = out + (accumulate ? 0 : (size_t)split * Nr * Nc);
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    float* row = dst + (size_t)(r0 + wm * 64 + mt * 16 + l16) * Nc + c0 + wn * 96 + lq * 4;
+#pragma unroll
+    for (int nt = 0; nt < 6; ++nt) {
+      float4* p = reinterpret_cast<float4*>(row + nt * 16);
+      float4 v = {acc[nt][mt][0], acc[nt][mt][1], acc[nt][mt][2], acc[nt][mt][3]};
+      if (accumulate) {
+        const float4 o = *p;
+        v.x += o.x;
+        v.y += o.y;
+        v.z += o.z;
+        v.w += o.w;
+      }
+      *p = v;
+    }
+  }
 }
 
-// C[N,K] += A[M,N]^T B[M,K]; returns -1 if the shape is not supported (caller falls back).
-DLT_API int dlt_wgrad_gemm(const bf16_t* A, const bf16_t* B, float* C, int M, int N, int K, int splits,
-                           hipStream_t st) {
-  if (M % WG_BM || N % WG_BN || K % WG_BK || M <= 0) return -1;
-  const int tiles = (N / WG_BN) * (K / WG_BK);
-  if (splits <= 0) {  // aim for >= ~1 workgroup per CU; each extra split costs N*K*4 B of atomics
-    splits = 1;
-    while (tiles * splits < 200 && splits < 4 && (M / WG_BM) % (splits * 2) == 0 && M / (splits * 2) >= 1024)
-      splits *= 2;
-  }
-  const int rows = ((M / WG_BM + splits - 1) / splits) * WG_BM;
-  k_wgrad_gemm<<<dim3(tiles, splits), 256, 0, st>>>(A, B, C, M, N, K, rows, splits > 1 ? 1 : 0);
+// dW[Nr, Nc] (fp32) += dY[T, Nr]^T . X[T, Nc].  splits == 1: accumulated in place; splits
+// > 1: the fp32 partials go to `part` [splits, Nr, Nc] (the caller sums them into dW in a
+// fixed order).  Returns -1 (nothing launched) for shapes outside the tiling.
+DLT_API int dlt_gemm_wgrad(const bf16_t* dY, const bf16_t* X, float* dW, float* part, int T, int Nr, int Nc, int ldy,
+                           int ldx, int splits, hipStream_t st) {
+  if (T <= 0 || T % 128 || Nr % 256 || Nc % 192 || (ldy | ldx) % 8 || splits < 1 || splits > T / 128) return -1;
+  if (splits > 1 && part == nullptr) return -1;
+  const int tiles = (Nr / 256) * (Nc / 192);
+  k_gemm_wgrad<<<tiles * splits, 512, 0, st>>>(dY, X, splits > 1 ? part : dW, T, Nr, Nc, ldy, ldx, splits,
+                                               splits > 1 ? 0 : 1);
   DLT_CHECK_LAUNCH();
 }

@@ -23,7 +23,8 @@ between runs, or between a run and its resumed continuation.  A plan file pins t
   hipBLASLt build does not support are ignored.
 * ``DLT_GEMM_PLAN=path`` replaces it: if the file exists every choice is replayed from
   it (no timing); otherwise the first process to finish a step writes it
-  (``save_plan``).  ``DLT_GEMM_PLAN=none``: no plan.
+  (``save_plan``).  ``DLT_GEMM_PLAN=none``: no plan.  ``DLT_GEMM_PLAN_OUT=path`` keeps
+  the shipped plan and writes it, merged with the choices raced in this process, to path.
 DDP replicas stay in sync regardless (the all-reduced gradient is identical on every
 rank).  For bitwise run-to-run reproducibility without a plan file use
 ``DLT_GEMM_TUNE=0 DLT_WGRAD_SPLITK=0 DLT_GEMM_TN=0 DLT_GEMM_FUSED=0`` (heuristic #0 everywhere).
@@ -72,7 +73,7 @@ def lib():
 
 
 # ---------------------------------------------------------------- plan pinning
-_PINNED = {"tn": {}, "splitk": {}}  # replayed framework-level choices (see module docstring)
+_PINNED = {"tn": {}, "splitk": {}, "hipblaslt": {}}  # replayed choices (see module docstring)
 _PLAN_STATE = {"path": None, "loaded": False, "saved": False}
 _INSTANCES = []  # weak references to live HipGemm objects (for save_plan)
 _RACES = {}  # process-wide race outcomes, see HipGemm.__init__
@@ -90,6 +91,9 @@ def _load_plan_env() -> None:
             load_plan(path)
     elif os.path.exists(SHIPPED_PLAN):
         load_plan(SHIPPED_PLAN, shipped=True)
+        # DLT_GEMM_PLAN_OUT=path: start from the shipped plan and write the merged plan
+        # (shipped pins + this process's new races) after the first step
+        _PLAN_STATE["path"] = os.environ.get("DLT_GEMM_PLAN_OUT") or None
 
 
 def load_plan(path: str, shipped: bool = False) -> None:
@@ -114,6 +118,7 @@ def load_plan(path: str, shipped: bool = False) -> None:
             rc = L.dlt_gemm_pin(*v)
             if rc != 0:
                 raise RuntimeError(f"dlt_gemm_pin failed ({rc})")
+            _PINNED["hipblaslt"][tuple(v[:-1])] = line
     # "tn": forward-projection race ("bf16" = hand-written, null = hipBLASLt; the round-2
     # integer tile configs of the retired gemm_tn kernels read as "library");
     # "fused": "kind:MxNxK" -> fused epilogue picked (older keys without a kind are ignored)
@@ -144,8 +149,13 @@ def export_plan() -> dict:
         if g is not None:
             tn.update(g._choice)
             sk.update(g._splitk)
+    # pins loaded from a plan but not exercised by this process are carried over
+    hl = dict(_PINNED["hipblaslt"])
+    for ln in buf.value[:n].decode().splitlines():
+        if ln and int(ln.split()[-1]) >= 0:
+            hl[tuple(int(x) for x in ln.split()[:-1])] = ln
     return {"hipblaslt_version": int(lib().dlt_gemm_lib_version()),
-            "hipblaslt": [ln for ln in buf.value[:n].decode().splitlines() if ln and int(ln.split()[-1]) >= 0],
+            "hipblaslt": [hl[k] for k in sorted(hl)],
             "tn": {"x".join(map(str, k)): c for k, c in tn.items() if len(k) == 3},
             "fused": {f"{k[0]}:" + "x".join(map(str, k[1:])): bool(c) for k, c in tn.items() if len(k) == 4},
             "splitk": {"x".join(map(str, k)): c for k, c in sk.items()}}
@@ -271,6 +281,7 @@ class HipGemm:
         self._race = os.environ.get("DLT_GEMM_TN", "1") != "0"
         self._splitk = _RACES["splitk"]  # wgrad (M, N, K) -> token slices (1 = plain accumulate GEMM)
         self._splitk_on = os.environ.get("DLT_WGRAD_SPLITK", "1") != "0"
+        self._hand_wgrad = os.environ.get("DLT_WGRAD_HAND", "1") != "0"
         self._fuse = os.environ.get("DLT_GEMM_FUSED", "1") != "0"
         _INSTANCES.append(weakref.ref(self))
 
@@ -278,6 +289,12 @@ class HipGemm:
         M, K = x.shape
         N = w.shape[0]
         _gemm(1, 0, N, M, K, w, _rowmajor(w), x, _rowmajor(x), y, N)
+
+    @staticmethod
+    def _hand_ok(*ts) -> bool:
+        """Operands the hand-written kernels take (race outcomes are keyed by shape only,
+        so a dtype check must precede every cached hand-written pick)."""
+        return all(t.dtype == torch.bfloat16 and t.is_contiguous() for t in ts)
 
     def _can_race(self, x, w) -> bool:
         return (self._race and x.is_contiguous() and w.is_contiguous() and x.dtype == torch.bfloat16
@@ -303,7 +320,7 @@ class HipGemm:
         if out is not None and (out.shape != (M, N) or not out.is_contiguous() or out.dtype != x.dtype):
             raise ValueError("linear: out must be a contiguous [M, N] tensor of the input dtype")
         y = torch.empty(M, N, dtype=x.dtype, device=x.device) if out is None else out
-        if self._pick(x, w, y) == "bf16":
+        if self._race and self._hand_ok(x, w) and self._pick(x, w, y) == "bf16":
             from . import hip
             hip.gemm_bf16(x, w, out=y)
         else:
@@ -311,6 +328,8 @@ class HipGemm:
         return y
 
     def _fused_pick(self, kind, x, w, fused, unfused) -> bool:
+        if not (self._fuse and self._hand_ok(x, w)):
+            return False
         key = (kind, x.shape[0], w.shape[0], x.shape[1])
         choice = self._choice.get(key)
         if choice is None:
@@ -370,7 +389,8 @@ class HipGemm:
                for k, c in self._choice.items() if len(k) == 3}
         out.update({f"{k[0]} M{k[1]}xN{k[2]}xK{k[3]}": ("fused gemm_bf16" if c else "unfused (linear + kernel)")
                     for k, c in self._choice.items() if len(k) == 4})
-        out.update({f"wgrad M{m}xN{n}xK{k}": f"split-K x{s}" if s > 1 else "hipBLASLt accumulate"
+        out.update({f"wgrad M{m}xN{n}xK{k}": (f"hand-written gemm_wgrad x{-s}" if s < 0 else
+                                              f"hipBLASLt split-K x{s}" if s > 1 else "hipBLASLt accumulate")
                     for (m, n, k), s in self._splitk.items()})
         return out
 
@@ -402,14 +422,46 @@ class HipGemm:
         _gemm_batched(0, 1, K, N, ms, x, lx, ms * lx, dy, ly, ms * ly, part, K, N * K, s, 1.0, 0.0)
         hip.splitk_acc(part, dw2)
 
+    @staticmethod
+    def _wgrad_hand(dw2, dy, x, s, to_bf16=False):
+        """The hand-written 256 x 192 MFMA weight-gradient kernel (csrc/gemm_wgrad.hip)
+        with s token splits.  fp32 dw2: accumulated in place (s = 1) or partials + one
+        fixed-order sum; bf16 dw2 (wgrad_set): partials summed straight into bf16."""
+        from . import hip
+        M, N = dy.shape
+        K = x.shape[1]
+        if not to_bf16:
+            if not hip.gemm_wgrad(dw2, dy, x, s):
+                raise RuntimeError(f"hand wgrad cannot tile {M}x{N}x{K}")
+            return
+        part = torch.empty(s, N, K, dtype=torch.float32, device=dw2.device)
+        if s == 1:
+            part.zero_()
+            ok = hip.gemm_wgrad(part[0], dy, x, 1)
+        else:
+            ok = hip.gemm_wgrad(part[0], dy, x, s, part=part)  # part[0] is a scratch target
+        if not ok:
+            raise RuntimeError(f"hand wgrad cannot tile {M}x{N}x{K}")
+        hip.splitk_sum_bf16(part, dw2)
+
     def _pick_splitk(self, dw2, dy, x):
+        """Weight-gradient race, per (M, N, K): hipBLASLt plain (1) / hipBLASLt split-K
+        (s > 1) / the hand-written kernel with s splits (-s).  Recorded in the plan."""
+        from . import hip
         M, N = dy.shape
         K = x.shape[1]
         key = (M, N, K)
         if key in self._splitk:
             return self._splitk[key]
         cands = [s for s in self.SPLITK_CANDIDATES if M % (s * 8) == 0 and (N * K) % 4 == 0]
-        if (not self._splitk_on or not cands or N * K > 4096 * 4096
+        hand = (self._hand_wgrad and x.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16
+                and hip.wgrad_fits(M, N, K) and x.is_contiguous() and dy.is_contiguous())
+        if hand:  # whole rounds of 256 workgroups, plus a few fixed depths (sweep in
+            # profiles/r3_wgrad.md: the best split is shape-specific, 5..16 here)
+            tiles = (N // 256) * (K // 192)
+            hs = {max(1, (256 * r) // tiles) for r in (1, 2, 3)} | {4, 8, 16}
+            cands += [-h for h in sorted(hs) if h <= min(64, M // 128)]
+        if (not (self._splitk_on or hand) or not cands or N * K > 4096 * 4096
                 or torch.cuda.is_current_stream_capturing()):
             self._splitk[key] = 1
             return 1
@@ -430,12 +482,22 @@ class HipGemm:
             return best
         best, choice = t_of(lambda: self._wgrad_plain(scratch, dy, x)), 1
         for s in cands:
-            t = t_of(lambda: self._wgrad_split(scratch, dy, x, s))
-            if t < 0.93 * best:
+            if s > 1 and not self._splitk_on:
+                continue
+            t = t_of(lambda: self._wgrad_hand(scratch, dy, x, -s) if s < 0 else self._wgrad_split(scratch, dy, x, s))
+            if t < (self.RACE_MARGIN if s < 0 else 0.93) * best:
                 best, choice = t, s
         del scratch
         self._splitk[key] = choice
         return choice
+
+    def _resolve(self, s, dy, x):
+        """A recorded hand-written pick (-s) falls back to the library when the operands
+        do not suit the kernel or DLT_WGRAD_HAND=0: split-K x s if the tokens divide,
+        else the plain accumulate GEMM."""
+        if s < 0 and not (self._hand_wgrad and self._hand_ok(dy, x)):
+            s = -s if self._splitk_on and -s in self.SPLITK_CANDIDATES and dy.shape[0] % (-s * 8) == 0 else 1
+        return s
 
     def wgrad_set(self, dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
         """dw (bf16, overwritten) = dy^T @ x: a weight gradient written straight in the
@@ -451,7 +513,10 @@ class HipGemm:
         s = self._splitk.get(key)
         if s is None:  # race on an fp32 scratch like wgrad_acc (same key, same decision)
             s = self._pick_splitk(torch.zeros(N, K, dtype=torch.float32, device=dw.device), dy, x)
-        if s > 1:
+        s = self._resolve(s, dy, x)
+        if s < 0:
+            self._wgrad_hand(dw2, dy, x, -s, to_bf16=True)
+        elif s > 1:
             ms = M // s
             lx, ly = _rowmajor(x), _rowmajor(dy)
             part = torch.empty(s, N, K, dtype=torch.float32, device=dw.device)
@@ -468,8 +533,10 @@ class HipGemm:
         dw2 = dw.view(N, K)
         if dw2.dtype != torch.float32 or not dw2.is_contiguous():
             raise ValueError("wgrad accumulator must be contiguous fp32")
-        s = self._pick_splitk(dw2, dy, x)
-        if s > 1:
+        s = self._resolve(self._pick_splitk(dw2, dy, x), dy, x)
+        if s < 0:
+            self._wgrad_hand(dw2, dy, x, -s)
+        elif s > 1:
             self._wgrad_split(dw2, dy, x, s)
         else:
             self._wgrad_plain(dw2, dy, x)

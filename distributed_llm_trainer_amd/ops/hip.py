@@ -54,7 +54,7 @@ _SIGS = {
                       c_float, c_float, c_float, c_void_p, c_void_p],
     "dlt_cast_bf16": [c_void_p, c_void_p, c_int64, c_void_p],
     "dlt_add_bf16_f32": [c_void_p, c_void_p, c_int64, c_void_p],
-    "dlt_wgrad_gemm": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
+    "dlt_gemm_wgrad": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "dlt_scale_bf16": [c_void_p, c_void_p, ctypes.c_long, c_void_p, c_void_p],
     "dlt_gemm_bf16_tn": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "dlt_gemm_bf16_qkv_rope": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
@@ -631,17 +631,41 @@ def cast_bf16(x: torch.Tensor, y: torch.Tensor) -> None:
 
 
 # ---------------------------------------------------------------- wgrad GEMM
-def wgrad_gemm(dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, splits: int = 0) -> bool:
-    """dw[N,K] (fp32) += dy[M,N]^T @ x[M,K] with the hand-written MFMA kernel.
-    Returns False (nothing launched) when the shape is outside the kernel's tiling."""
-    M, N = dy.shape
-    K = x.shape[1]
-    if M % 64 or N % 128 or K % 128:
+def wgrad_fits(T: int, Nr: int, Nc: int) -> bool:
+    """Shapes the 256 x 192 weight-gradient kernel tiles exactly (T in 128-token pairs)."""
+    return T > 0 and T % 128 == 0 and Nr % 256 == 0 and Nc % 192 == 0
+
+
+def wgrad_splits(T: int, Nr: int, Nc: int, target: int = 256) -> int:
+    """Split-K factor that brings tiles x splits closest to `target` workgroups (one per
+    CU), capped by the number of 128-token pairs."""
+    tiles = (Nr // 256) * (Nc // 192)
+    return max(1, min(T // 128, (target + tiles // 2) // tiles))
+
+
+def gemm_wgrad(dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, splits: int = 0,
+               part: Optional[torch.Tensor] = None) -> bool:
+    """dw[Nr,Nc] (fp32) += dy[T,Nr]^T @ x[T,Nc] with the hand-written MFMA kernel
+    (csrc/gemm_wgrad.hip).  splits == 0 picks the CU-filling split; with splits > 1 the
+    fp32 partials go to `part` ([splits, Nr, Nc], allocated if None) and are summed into
+    dw in fixed split order (deterministic).  Returns False (nothing launched) when the
+    shape does not tile."""
+    T, Nr = dy.shape
+    Nc = x.shape[1]
+    if not wgrad_fits(T, Nr, Nc) or dy.stride(1) != 1 or x.stride(1) != 1 or dy.stride(0) % 8 or x.stride(0) % 8:
         return False
-    _req(dy, torch.bfloat16, "wgrad.dy")
-    _req(x, torch.bfloat16, "wgrad.x", M * K)
-    _req(dw, torch.float32, "wgrad.dw", N * K)
-    _chk(lib().dlt_wgrad_gemm(_p(dy), _p(x), _p(dw), M, N, K, splits, _stream()), "wgrad_gemm")
+    _req(dw, torch.float32, "wgrad.dw", Nr * Nc)
+    if dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16 or x.shape[0] != T:
+        raise ValueError("gemm_wgrad: bf16 dy[T,Nr] / x[T,Nc] expected")
+    if splits <= 0:
+        splits = wgrad_splits(T, Nr, Nc)
+    splits = min(splits, T // 128)
+    if splits > 1 and (part is None or part.numel() < splits * Nr * Nc):
+        part = torch.empty(splits * Nr * Nc, device=dw.device, dtype=torch.float32)
+    _chk(lib().dlt_gemm_wgrad(_p(dy), _p(x), _p(dw), _p(part) if splits > 1 else None, T, Nr, Nc,
+                              dy.stride(0), x.stride(0), splits, _stream()), "gemm_wgrad")
+    if splits > 1:
+        _chk(lib().dlt_splitk_acc(_p(part), _p(dw), Nr * Nc, splits, _stream()), "splitk_acc")
     return True
 
 

@@ -109,7 +109,7 @@ def micro_step_fusion(requested: int, GA: int, micro_bs: int, seq_len: int, gpu_
 def gemm_plan_hook() -> None:
     """After a step: write the GEMM plan file once if ``DLT_GEMM_PLAN`` asks for one
     (``ops/gemm.py`` ``maybe_save_plan``; a no-op without the planner)."""
-    if not os.environ.get("DLT_GEMM_PLAN"):
+    if not (os.environ.get("DLT_GEMM_PLAN") or os.environ.get("DLT_GEMM_PLAN_OUT")):
         return
     from ..ops import gemm
     gemm.maybe_save_plan()

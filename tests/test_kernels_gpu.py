@@ -418,16 +418,25 @@ def test_gemm_plan_pin_roundtrip(tmp_path):
     gemm.load_plan(str(path))  # loading a saved plan re-pins without error
 
 
-@pytest.mark.parametrize("M,N,K", [(1024, 256, 128), (2048, 768, 384)])
-def test_wgrad_gemm_kernel(M, N, K):
+@pytest.mark.parametrize("T,Nr,Nc", [(1024, 256, 192), (2048, 768, 384), (4096, 2304, 768)])
+def test_gemm_wgrad_kernel(T, Nr, Nc):
+    """Hand-written weight-gradient GEMM (in-place and split-K + fixed-order sum) vs
+    the fp32 torch reference; split-K results are bitwise repeatable."""
     torch.manual_seed(0)
-    dy = torch.randn(M, N, device=DEV).bfloat16()
-    x = torch.randn(M, K, device=DEV).bfloat16()
-    for splits in (1, 2, 0):
-        dw = torch.randn(N, K, device=DEV)
-        ref = dw + dy.float().t() @ x.float()
-        assert hip.wgrad_gemm(dw, dy, x, splits)
-        _close(dw, ref, 1e-3 * M ** 0.5, 1e-4, f"wgrad splits={splits}")
+    dy = torch.randn(T, Nr, device=DEV).bfloat16()
+    x = torch.randn(T, Nc, device=DEV).bfloat16()
+    base = torch.randn(Nr, Nc, device=DEV)
+    ref = base + dy.float().t() @ x.float()
+    outs = {}
+    for splits in (1, 3, 0):
+        dw = base.clone()
+        assert hip.gemm_wgrad(dw, dy, x, splits)
+        _close(dw, ref, 1e-3 * T ** 0.5, 1e-4, f"wgrad splits={splits}")
+        outs[splits] = dw
+    dw = base.clone()
+    assert hip.gemm_wgrad(dw, dy, x, 0)
+    assert torch.equal(dw, outs[0]), "split-K wgrad not deterministic"
+    assert not hip.gemm_wgrad(base, dy[:, :128], x), "untileable shape must be refused"
 
 
 @pytest.mark.parametrize("p", [0.0, 0.1])

@@ -17,6 +17,7 @@
 
 #include "gemm_bf16.hip"
 #include "elementwise.hip"
+#include "gemm_wgrad.hip"
 
 #define CK(x)                                                                   \
   do {                                                                          \
@@ -265,8 +266,121 @@ static int epi_main(int M, int H, int I, int S) {
   return 0;
 }
 
+// dW[Nr, Nc] += dY[T, Nr]^T X[T, Nc]: hand-written wgrad (split-K partials + fixed-order
+// sum) vs hipBLASLt (best of 24 heuristic candidates, fp32 C, beta = 1)
+__global__ void k_ref_wgrad(const bf16_t* dY, const bf16_t* X, float* R, const int* rows, int nr, int T, int Nr,
+                            int Nc) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  int ri = blockIdx.y;
+  if (c >= Nc || ri >= nr) return;
+  const int r = rows[ri];
+  float s = 0.f;
+  for (int t = 0; t < T; ++t) s += bf2f(dY[(size_t)t * Nr + r]) * bf2f(X[(size_t)t * Nc + c]);
+  R[(size_t)ri * Nc + c] = s;
+}
+
+static int wgrad_main(std::vector<int> shp) {
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  hipblasLtHandle_t h;
+  hipblasLtCreate(&h);
+  void* ws;
+  CK(hipMalloc(&ws, g_wsz));
+  for (size_t si = 0; si + 2 < shp.size(); si += 3) {
+    const int T = shp[si], Nr = shp[si + 1], Nc = shp[si + 2];
+    bf16_t *dY, *X;
+    float *dW, *dW2, *part;
+    CK(hipMalloc(&dY, (size_t)T * Nr * 2));
+    CK(hipMalloc(&X, (size_t)T * Nc * 2));
+    CK(hipMalloc(&dW, (size_t)Nr * Nc * 4));
+    CK(hipMalloc(&dW2, (size_t)Nr * Nc * 4));
+    k_fill<<<1024, 256, 0, st>>>(dY, (size_t)T * Nr, 21);
+    k_fill<<<1024, 256, 0, st>>>(X, (size_t)T * Nc, 22);
+    const int tiles = (Nr / 256) * (Nc / 192);
+    int S = getenv("GW_SPLITS") ? atoi(getenv("GW_SPLITS")) : (256 + tiles / 2) / tiles;
+    if (S < 1) S = 1;
+    CK(hipMalloc(&part, (size_t)S * Nr * Nc * 4));
+    auto hand = [&]() {
+      int rc = dlt_gemm_wgrad(dY, X, dW, part, T, Nr, Nc, Nr, Nc, S, st);
+      if (rc == 0 && S > 1) rc = dlt_splitk_acc(part, dW, (long)Nr * Nc, S, st);
+      return rc;
+    };
+    // correctness: dW starts at 0; sampled rows vs the fp32 reference
+    CK(hipMemsetAsync(dW, 0, (size_t)Nr * Nc * 4, st));
+    if (hand() != 0) {
+      printf("wgrad T=%d Nr=%d Nc=%d: n/a\n", T, Nr, Nc);
+      continue;
+    }
+    const int nr = 8;
+    std::vector<int> rows(nr);
+    for (int i = 0; i < nr; ++i) rows[i] = (i * 977 + 13) % Nr;
+    int* drows;
+    float* R;
+    CK(hipMalloc(&drows, nr * 4));
+    CK(hipMalloc(&R, (size_t)nr * Nc * 4));
+    CK(hipMemcpy(drows, rows.data(), nr * 4, hipMemcpyHostToDevice));
+    k_ref_wgrad<<<dim3((Nc + 255) / 256, nr), 256, 0, st>>>(dY, X, R, drows, nr, T, Nr, Nc);
+    std::vector<float> ref((size_t)nr * Nc), got((size_t)Nr * Nc);
+    CK(hipMemcpyAsync(ref.data(), R, ref.size() * 4, hipMemcpyDeviceToHost, st));
+    CK(hipMemcpyAsync(got.data(), dW, got.size() * 4, hipMemcpyDeviceToHost, st));
+    CK(hipStreamSynchronize(st));
+    double maxerr = 0, maxref = 0;
+    for (int i = 0; i < nr; ++i)
+      for (int c = 0; c < Nc; ++c) {
+        const double d = std::fabs((double)got[(size_t)rows[i] * Nc + c] - ref[(size_t)i * Nc + c]);
+        if (!(d <= maxerr)) maxerr = d;
+        maxref = std::fmax(maxref, std::fabs(ref[(size_t)i * Nc + c]));
+      }
+    // hipBLASLt: C[Nc, Nr] (col-major) += op_N(X [Nc, T]) op_T(dY [Nr, T])
+    hipblasLtMatmulDesc_t md;
+    hipblasLtMatmulDescCreate(&md, HIPBLAS_COMPUTE_32F, HIP_R_32F);
+    hipblasOperation_t ta = HIPBLAS_OP_N, tb = HIPBLAS_OP_T;
+    hipblasLtMatmulDescSetAttribute(md, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta));
+    hipblasLtMatmulDescSetAttribute(md, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb));
+    hipblasLtMatrixLayout_t la, lb, lc;
+    hipblasLtMatrixLayoutCreate(&la, HIP_R_16BF, Nc, T, Nc);
+    hipblasLtMatrixLayoutCreate(&lb, HIP_R_16BF, Nr, T, Nr);
+    hipblasLtMatrixLayoutCreate(&lc, HIP_R_32F, Nc, Nr, Nc);
+    hipblasLtMatmulPreference_t pref;
+    hipblasLtMatmulPreferenceCreate(&pref);
+    hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &g_wsz, sizeof(g_wsz));
+    hipblasLtMatmulHeuristicResult_t res[24];
+    int n = 0;
+    hipblasLtMatmulAlgoGetHeuristic(h, md, la, lb, lc, lc, pref, 24, res, &n);
+    float alpha = 1.f, beta = 1.f, tb_best = 1e30f;
+    for (int i = 0; i < n; ++i) {
+      if (res[i].workspaceSize > g_wsz) continue;
+      auto blas = [&]() {
+        return (int)hipblasLtMatmul(h, md, &alpha, X, la, dY, lb, &beta, dW2, lc, dW2, lc, &res[i].algo, ws, g_wsz,
+                                    st);
+      };
+      if (blas()) continue;
+      tb_best = std::fmin(tb_best, time_us(blas, st, 5));
+    }
+    const float th = time_us(hand, st, 5);
+    const double fl = 2.0 * T * Nr * Nc;
+    printf("wgrad T=%d Nr=%d Nc=%d: hand (splits %d) %7.1f us %5.0f TF err %.1e | hipBLASLt %7.1f us %5.0f TF\n", T,
+           Nr, Nc, S, th, fl / th / 1e6, maxerr / maxref, tb_best, fl / tb_best / 1e6);
+    fflush(stdout);
+    CK(hipFree(dY));
+    CK(hipFree(X));
+    CK(hipFree(dW));
+    CK(hipFree(dW2));
+    CK(hipFree(part));
+    CK(hipFree(R));
+    CK(hipFree(drows));
+  }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc > 1 && !strcmp(argv[1], "epi")) return epi_main(16384, 768, 3072, 1024);
+  if (argc > 1 && !strcmp(argv[1], "wgrad")) {
+    std::vector<int> v;
+    for (int i = 2; i < argc; ++i) v.push_back(atoi(argv[i]));
+    if (v.empty()) v = {32768, 2304, 768, 32768, 768, 768, 32768, 6144, 768, 32768, 768, 3072};
+    return wgrad_main(v);
+  }
   std::vector<Kern> kerns = {{"blas", run_blas},         {"bf16", run_bf16<0>},      {"rowmaj", run_bf16<4>},
                              {"rowwalk", run_bf16<8>}, {"nostore", run_bf16<1>},   {"l2ops", run_bf16<2>},
                              {"l2nost", run_bf16<3>},    {"c0", run_bf16<16>},       {"stsync", run_bf16<32>}};
