@@ -43,6 +43,11 @@ __device__ __forceinline__ uint32_t drop_bits(uint32_t key, uint64_t idx) {
   return (idx & 1) ? (h >> 16) : (h & 0xffffu);
 }
 
+// sigmoid with the hardware reciprocal (v_rcp_f32, 1 ulp): the IEEE division hipcc
+// emits for `1.f / x` is a ~10-instruction sequence, which dominated the SwiGLU GEMM
+// epilogue.  Every SwiGLU kernel uses this one so the fused and unfused paths agree.
+__device__ __forceinline__ float dlt_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

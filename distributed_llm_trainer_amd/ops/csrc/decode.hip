@@ -358,7 +358,7 @@ __global__ __launch_bounds__(DEC_NT) void k_dec_norm_gu(const float* __restrict_
 #pragma unroll
         for (int b = 0; b < B; ++b) {
           const float gb = bf_round(acc[2 * c][b]), ub = bf_round(acc[2 * c + 1][b]);
-          s[(size_t)b * I + i0 + c] = f2bf(gb / (1.f + __expf(-gb)) * ub);
+          s[(size_t)b * I + i0 + c] = f2bf(gb * dlt_sigmoid(gb) * ub);
         }
       }
   }

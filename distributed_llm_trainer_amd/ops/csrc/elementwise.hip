@@ -306,7 +306,7 @@ DLT_API int dlt_rope_qkv_bwd(const bf16_t* dq, const float* dqf, const bf16_t* d
 }
 
 // ---------------------------------------------------------------- SwiGLU
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float sigmoidf_(float x) { return dlt_sigmoid(x); }
 
 // gu [M, 2I] = [gate | up] -> a [M, I] = silu(gate) * up
 __global__ __launch_bounds__(256) void k_swiglu_fwd(const bf16_t* __restrict__ gu, bf16_t* __restrict__ a, int M, int I) {

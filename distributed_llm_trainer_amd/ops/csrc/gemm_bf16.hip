@@ -118,6 +118,18 @@ __device__ __forceinline__ int gb_bmap(int r, int I) {
   return gb_ncol<BN, EPI>(r / (BN / 2), (r % (BN / 2)) >> 4, I) + (r & 15);
 }
 
+// 4 fp32 -> 4 bf16 (RNE) as two v_cvt_pk_bf16_f32; and back (exact)
+typedef __bf16 gb_bf16x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint2 gb_pack(const floatx4_t& v) {
+  return __builtin_bit_cast(uint2, __builtin_convertvector(v, gb_bf16x4_t));
+}
+__device__ __forceinline__ void gb_unpack(uint2 p, float (&f)[4]) {
+  f[0] = __uint_as_float(p.x << 16);
+  f[1] = __uint_as_float(p.x & 0xffff0000u);
+  f[2] = __uint_as_float(p.y << 16);
+  f[3] = __uint_as_float(p.y & 0xffff0000u);
+}
+
 template <int BN, int EPI>
 __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                       bf16_t* __restrict__ C, int M, int N, int K, int lda, int ldb,
@@ -152,7 +164,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
   const int gm = 32 / gn;
   // flags (ablation only, 0 in production): bit 0 skip the C stores, bit 1 every tile
   // reads tile (0, 0)'s operand panels (L2-resident), bits 2-3 tile order (0 = grouped
-  // column walk, 1 = row-major, 2 = grouped row walk)
+  // column walk, 1 = row-major, 2 = grouped row walk), 16 every tile stores to tile (0, 0),
+  // 32 s_waitcnt vmcnt(0) after the stores
   const int order = (flags >> 2) & 3;
   const bool grouped = order != 1 && gx == 32 && ntiles % 32 == 0 && ntm % gm == 0;
   const int scols = ntn / gn;
@@ -366,12 +379,14 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
     // ---- epilogue: acc[nt][mt] = D[n][m]; lane owns row m0 + wm*64 + mt*16 + l16 and
     // columns (n-tile nt) + lq*4 .. +3.  permlane16_swap over n-tile pairs (2p, 2p+1):
     // lanes with lq even end up with 8 consecutive columns of n-tile 2p, lq odd of 2p+1.
+    // Every f32 -> bf16 conversion is one v_cvt_pk_bf16_f32 per PAIR (gb_pack); the
+    // per-element cast plus shift/or packing it replaces was ~40 % of the plain epilogue's
+    // VALU, and the fused epilogues take their bf16-rounded inputs from the same packs.
     if (!(flags & 1)) {
       int tm, tn;
       coords(tile, tm, tn);
       if (flags & 16) tm = tn = 0;
       const int m0 = tm * GB_BM, n0 = tn * TS;
-      auto rnd = [](float v) { return bf2f(f2bf(v)); };
       if constexpr (EPI == GB_EPI_ROPE) {
         // all cos/sin loads first (the fragment registers are dead here), one wait.  The
         // lane's rotation pairs are P = wn*48 + t*16 + lq*4 + e: only two distinct
@@ -383,13 +398,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
 #pragma unroll
           for (int u = 0; u < 2; ++u) {
             const int j = (wn * 48 + u * 16 + lq * 4) & 31;
-            if (flags & 64) {  // ablation: no table loads
-              cs[mt][u] = float4{0.6f, 0.6f, 0.6f, (float)pos};
-              sn[mt][u] = float4{0.8f, 0.8f, 0.8f, (float)j};
-            } else {
-              cs[mt][u] = *reinterpret_cast<const float4*>(ep.cosT + (size_t)pos * 32 + j);
-              sn[mt][u] = *reinterpret_cast<const float4*>(ep.sinT + (size_t)pos * 32 + j);
-            }
+            cs[mt][u] = *reinterpret_cast<const float4*>(ep.cosT + (size_t)pos * 32 + j);
+            sn[mt][u] = *reinterpret_cast<const float4*>(ep.sinT + (size_t)pos * 32 + j);
           }
         }
 #pragma unroll
@@ -400,11 +410,13 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
             if (n0 + (P >> 5) * 64 < ep.rot_cols) {
               const float4 c4 = cs[mt][t & 1], s4 = sn[mt][t & 1];
               const float cc[4] = {c4.x, c4.y, c4.z, c4.w}, ss[4] = {s4.x, s4.y, s4.z, s4.w};
+              float x1[4], x2[4];
+              gb_unpack(gb_pack(acc[t][mt]), x1);  // the bf16 GEMM output the unfused path rotates
+              gb_unpack(gb_pack(acc[t + 3][mt]), x2);
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
-                const float x1 = rnd(acc[t][mt][e]), x2 = rnd(acc[t + 3][mt][e]);
-                acc[t][mt][e] = x1 * cc[e] - x2 * ss[e];
-                acc[t + 3][mt][e] = x2 * cc[e] + x1 * ss[e];
+                acc[t][mt][e] = x1[e] * cc[e] - x2[e] * ss[e];
+                acc[t + 3][mt][e] = x2[e] * cc[e] + x1[e] * ss[e];
               }
             }
           }
@@ -412,40 +424,40 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
         const int row = m0 + wm * 64 + mt * 16 + l16;
+        uint2 pk[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) pk[t] = gb_pack(acc[t][mt]);
         if constexpr (EPI == GB_EPI_SWIGLU) {
-          // s = silu(g) * u on the bf16-rounded gate/up values; n-tiles 0/1 of s are
-          // paired for 16-byte stores, n-tile 2 stores 8 bytes per lane
-          float sv[3][4];
+          // s = silu(g) * u on the bf16-rounded gate/up values (the packs stored as gu);
+          // n-tiles 0/1 of s are paired for 16-byte stores, n-tile 2 stores 8 bytes per lane
+          uint2 sp[3];
 #pragma unroll
-          for (int t = 0; t < 3; ++t)
+          for (int t = 0; t < 3; ++t) {
+            float g[4], u[4];
+            gb_unpack(pk[t], g);
+            gb_unpack(pk[t + 3], u);
+            floatx4_t sv;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float g = rnd(acc[t][mt][e]), u = rnd(acc[t + 3][mt][e]);
-              sv[t][e] = g * (1.f / (1.f + __expf(-g))) * u;
-            }
+            for (int e = 0; e < 4; ++e) sv[e] = g[e] * dlt_sigmoid(g[e]) * u[e];
+            sp[t] = gb_pack(sv);
+          }
           bf16_t* srow = ep.s_out + (size_t)row * ep.ld_s + (size_t)tn * 96 + wn * 48;
-          uint32_t x[2], y[2];
+          uint32_t x[2] = {sp[0].x, sp[0].y}, y[2] = {sp[1].x, sp[1].y};
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            x[h] = (uint32_t)f2bf(sv[0][2 * h]) | ((uint32_t)f2bf(sv[0][2 * h + 1]) << 16);
-            y[h] = (uint32_t)f2bf(sv[1][2 * h]) | ((uint32_t)f2bf(sv[1][2 * h + 1]) << 16);
             auto sw = __builtin_amdgcn_permlane16_swap(x[h], y[h], false, false);
             x[h] = sw[0];
             y[h] = sw[1];
           }
           *reinterpret_cast<uint4*>(srow + (lq & 1) * 16 + (lq >> 1) * 8) = uint4{x[0], x[1], y[0], y[1]};
-          const uint2 z = {(uint32_t)f2bf(sv[2][0]) | ((uint32_t)f2bf(sv[2][1]) << 16),
-                           (uint32_t)f2bf(sv[2][2]) | ((uint32_t)f2bf(sv[2][3]) << 16)};
-          *reinterpret_cast<uint2*>(srow + 32 + lq * 4) = z;
+          *reinterpret_cast<uint2*>(srow + 32 + lq * 4) = sp[2];
         }
         bf16_t* crow = C + (size_t)row * ldc + n0;
 #pragma unroll
         for (int p = 0; p < NT / 2; ++p) {
-          uint32_t x[2], y[2];
+          uint32_t x[2] = {pk[2 * p].x, pk[2 * p].y}, y[2] = {pk[2 * p + 1].x, pk[2 * p + 1].y};
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            x[h] = (uint32_t)f2bf(acc[2 * p][mt][2 * h]) | ((uint32_t)f2bf(acc[2 * p][mt][2 * h + 1]) << 16);
-            y[h] = (uint32_t)f2bf(acc[2 * p + 1][mt][2 * h]) | ((uint32_t)f2bf(acc[2 * p + 1][mt][2 * h + 1]) << 16);
             auto sw = __builtin_amdgcn_permlane16_swap(x[h], y[h], false, false);
             x[h] = sw[0];
             y[h] = sw[1];

@@ -246,11 +246,8 @@ static int epi_main(int M, int H, int I, int S) {
       }
     }
     const float tf = time_us(fused, st), tu = time_us(unfused, st);
-    float tx = 0.f, tp = 0.f;
-    if (which == 0)
-      tx = time_us([&]() { return dlt_gemm_bf16_qkv_rope(A, B, C, M, H, K, S, dc, ds, 64, st); }, st);
-    tp = time_us([&]() { return dlt_gemm_bf16_tn(A, B, C, M, N, K, K, K, N, 0, st); }, st);
-    printf("  plain bf16 %.1f us, rope without table loads %.1f us\n", tp, tx);
+    const float tp = time_us([&]() { return dlt_gemm_bf16_tn(A, B, C, M, N, K, K, K, N, 0, st); }, st);
+    printf("  plain bf16 %.1f us\n", tp);
     printf("%s M=%d N=%d K=%d: fused %.1f us | hipBLASLt + %s %.1f us | err %.1e%s%.1e\n",
            which == 0 ? "qkv+rope" : "gu+swiglu", M, N, K, tf, which == 0 ? "rope" : "swiglu", tu, e1 / m1,
            which == 1 ? " s err " : "", which == 1 ? e2 / m2 : 0.0);
@@ -373,7 +370,95 @@ static int wgrad_main(std::vector<int> shp) {
   return 0;
 }
 
+// Can memory-bound work overlap a GEMM?  hipBLASLt gate/up GEMM (G) and the SwiGLU
+// elementwise kernel (E), alone, concurrently on two full-chip streams, and on
+// disjoint CU masks (hipExtStreamCreateWithCUMask).
+static int overlap_main() {
+  const int M = 16384, N = 6144, K = 768, I = 3072;
+  bf16_t *A, *B, *C, *gu, *sb;
+  CK(hipMalloc(&A, (size_t)M * K * 2));
+  CK(hipMalloc(&B, (size_t)N * K * 2));
+  CK(hipMalloc(&C, (size_t)M * N * 2));
+  CK(hipMalloc(&gu, (size_t)M * N * 2));
+  CK(hipMalloc(&sb, (size_t)M * I * 2));
+  k_fill<<<1024, 256>>>(A, (size_t)M * K, 1);
+  k_fill<<<1024, 256>>>(B, (size_t)N * K, 2);
+  k_fill<<<1024, 256>>>(gu, (size_t)M * N, 3);
+  CK(hipDeviceSynchronize());
+  hipDeviceProp_t prop;
+  CK(hipGetDeviceProperties(&prop, 0));
+  const int ncu = prop.multiProcessorCount;
+  auto mk = [&](int lo, int hi, int stride) {  // CUs [lo, hi) (or every stride-th) -> stream
+    std::vector<uint32_t> m((ncu + 31) / 32, 0u);
+    for (int c = 0; c < ncu; ++c) {
+      const bool on = stride ? ((c % stride) < hi - lo) : (c >= lo && c < hi);
+      if (on) m[c / 32] |= 1u << (c % 32);
+    }
+    hipStream_t s;
+    CK(hipExtStreamCreateWithCUMask(&s, (uint32_t)m.size(), m.data()));
+    return s;
+  };
+  hipStream_t s0, s1;
+  CK(hipStreamCreateWithFlags(&s0, hipStreamNonBlocking));
+  CK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  auto G = [&](hipStream_t s) { return run_blas(A, B, C, M, N, K, s); };
+  auto E = [&](hipStream_t s) { return dlt_swiglu_fwd(gu, sb, M, I, s); };
+  G(s0);
+  CK(hipDeviceSynchronize());
+  const int reps = 20;
+  auto wall = [&](auto&& body) {
+    body();
+    CK(hipDeviceSynchronize());
+    float best = 1e30f;
+    for (int r = 0; r < 3; ++r) {
+      CK(hipEventRecord(e0, 0));
+      CK(hipDeviceSynchronize());
+      body();
+      CK(hipDeviceSynchronize());
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      best = std::fmin(best, ms);
+    }
+    return best * 1000.f / reps;
+  };
+  auto run = [&](const char* name, hipStream_t sg, hipStream_t se, int ne_per_g) {
+    const float tg = wall([&]() { for (int i = 0; i < reps; ++i) G(sg); });
+    const float te = wall([&]() { for (int i = 0; i < reps * ne_per_g; ++i) E(se); });
+    const float tb = wall([&]() {
+      for (int i = 0; i < reps; ++i) {
+        G(sg);
+        for (int j = 0; j < ne_per_g; ++j) E(se);
+      }
+    });
+    printf("%-28s G %7.1f us | E x%d %7.1f us | both %7.1f us (serial sum %7.1f, saved %5.1f%%)\n", name, tg,
+           ne_per_g, te, tb, tg + te, 100.f * (tg + te - tb) / (tg + te));
+    fflush(stdout);
+  };
+  run("two full-chip streams", s0, s1, 1);
+  run("two full-chip streams E x2", s0, s1, 2);
+  for (int k : {16, 32, 64}) {
+    char nm[64];
+    snprintf(nm, sizeof nm, "mask G %d / E %d (low)", ncu - k, k);
+    run(nm, mk(k, ncu, 0), mk(0, k, 0), 1);
+    snprintf(nm, sizeof nm, "mask G %d / E %d (strided)", ncu - k, k);
+    // strided: CU c in E iff c % (ncu/k) == 0
+    std::vector<uint32_t> me((ncu + 31) / 32, 0u), mg((ncu + 31) / 32, 0u);
+    for (int c = 0; c < ncu; ++c) ((c % (ncu / k)) == 0 ? me : mg)[c / 32] |= 1u << (c % 32);
+    hipStream_t sg, se;
+    CK(hipExtStreamCreateWithCUMask(&sg, (uint32_t)mg.size(), mg.data()));
+    CK(hipExtStreamCreateWithCUMask(&se, (uint32_t)me.size(), me.data()));
+    run(nm, sg, se, 1);
+  }
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 1 && !strcmp(argv[1], "overlap")) return overlap_main();
   if (argc > 1 && !strcmp(argv[1], "epi")) return epi_main(16384, 768, 3072, 1024);
   if (argc > 1 && !strcmp(argv[1], "wgrad")) {
     std::vector<int> v;
