@@ -200,6 +200,10 @@ class GPTEngine:
         # activation checkpointing: keep o / lse / x2 too and skip the attention forward
         # and the o / down GEMMs in the recompute (see the module docstring)
         self.selective_recompute = os.environ.get("DLT_AC_SELECTIVE", "1") != "0"
+        # ... and, within this many bytes of kept GEMM outputs, the packed QKV and gate/up
+        # GEMM outputs as well, so the recompute reduces to the norms and SwiGLU (sized for
+        # 288 GB of HBM: GPT-2 small/medium keep both; see _ac_keep)
+        self.ac_budget = float(os.environ.get("DLT_AC_BUDGET_GB", "48")) * 1e9
         # attention keep-bit masks (1 bit per causal score, two layouts) are kept from the
         # forward for the backward while one micro-step's masks of all layers fit in this
         # budget; beyond it (long context: 3.2 GB per layer at S = 32768, nh 12) the
@@ -283,6 +287,21 @@ class GPTEngine:
         mask.record_stream(main)
         return mask, ev
 
+    def _ac_keep(self, M: int):
+        """(keep_qkv, keep_gu) under activation checkpointing: GEMM outputs kept instead of
+        recomputed, greedily by recompute time saved per byte (the QKV output first),
+        while every layer of the two micro-steps a pipelined window holds fits in
+        ``ac_budget``.  Whole-block recompute (``DLT_AC_SELECTIVE=0``) keeps nothing."""
+        if not self.selective_recompute:
+            return False, False
+        cfg = self.cfg
+        per_layer_chains = cfg.num_layers * 2 * (2 if self.act_dtype == torch.bfloat16 else 4)
+        qkv = M * 3 * cfg.hidden_size * per_layer_chains
+        gu = M * 2 * cfg.intermediate_size * per_layer_chains
+        keep_qkv = qkv <= self.ac_budget
+        keep_gu = keep_qkv and qkv + gu <= self.ac_budget
+        return keep_qkv, keep_gu
+
     def _layer_forward(self, st: _StepState, i: int, r, d, key_d: int, p_d: float,
                        save: bool):
         ops, gm, cfg = self.ops, self.gemm, self.cfg
@@ -345,7 +364,15 @@ class GPTEngine:
             c = _LayerCache(x=x, rstd1=rstd1, n1=n1, q=q, k=k, v=v, o=o, lse=lse,
                             x2=x2, rstd2=rstd2, n2=n2, gu=gu, s=s)
         elif st.recompute:
-            c = _LayerCache(x=x, o=o, lse=lse, x2=x2) if self.selective_recompute else _LayerCache(x=x)
+            if self.selective_recompute:
+                keep_qkv, keep_gu = self._ac_keep(M)
+                c = _LayerCache(x=x, o=o, lse=lse, x2=x2)
+                if keep_qkv and self.packed_qkv:
+                    c.q = q
+                if keep_gu:
+                    c.gu = gu
+            else:
+                c = _LayerCache(x=x)
         else:
             c = None
         return x2, d_out, c
@@ -353,7 +380,8 @@ class GPTEngine:
     def _layer_recompute(self, st: _StepState, i: int, c: _LayerCache) -> _LayerCache:
         """Activation-checkpoint recompute of layer ``i`` for the backward.  Whole-block
         recompute from the saved input, or (selective, the default) only the tensors the
-        backward reads that were not kept: n1 / q(k, v) and n2 / gu / s.  Same kernels on
+        backward reads that were not kept: n1 / q(k, v) and n2 / gu / s (the QKV and
+        gate/up GEMMs are skipped when the forward kept their outputs, _ac_keep).  Same kernels on
         the same inputs as the forward, so every recomputed tensor is bit-identical."""
         if c.o is None:
             return self._layer_forward(st, i, c.x, None, 0, 0.0, save=True)[2]
@@ -366,7 +394,10 @@ class GPTEngine:
         sb = (lambda name, n: self._slot_buf(st, i, name, M, n, dv)[0]) if st.defer else (lambda name, n: None)
         _, n1, rstd1 = ops.add_dropout_rmsnorm_fwd(c.x, None, w.ln1, self.eps, 0.0, 0, self.act_dtype,
                                                    y_out=sb("n1", H))
-        if self.packed_qkv and hasattr(gm, "linear_rope"):
+        if c.q is not None:  # QKV output kept by the forward (_ac_keep)
+            qkv = c.q
+            q, k, v = qkv, None, None
+        elif self.packed_qkv and hasattr(gm, "linear_rope"):
             qkv = gm.linear_rope(n1, w.wqkv, B, S, cfg.num_heads, cos, sin, ops)
             q, k, v = qkv, None, None
         elif self.packed_qkv:
@@ -374,11 +405,15 @@ class GPTEngine:
             ops.rope_qk_inplace(qkv, B, S, cfg.num_heads, cos, sin)
             q, k, v = qkv, None, None
         else:
+            qkv = gm.linear(n1, w.wqkv)
             q, k, v = ops.rope_qkv_fwd(qkv, B, S, cfg.num_heads, cos, sin)
         del qkv
         _, n2, rstd2 = ops.add_dropout_rmsnorm_fwd(c.x2, None, w.ln2, self.eps, 0.0, 0, self.act_dtype,
                                                    y_out=sb("n2", H))
-        if hasattr(gm, "linear_swiglu"):
+        if c.gu is not None:  # gate/up output kept by the forward (_ac_keep)
+            gu = c.gu
+            s = ops.swiglu_fwd(gu, out=sb("s", I))
+        elif hasattr(gm, "linear_swiglu"):
             gu, s = gm.linear_swiglu(n2, w.wgu, ops, s_out=sb("s", I))
         else:
             gu = gm.linear(n2, w.wgu)

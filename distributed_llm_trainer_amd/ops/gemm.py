@@ -128,12 +128,18 @@ def load_plan(path: str, shipped: bool = False) -> None:
         if ":" in k:
             kind, dims = k.split(":", 1)
             _PINNED["tn"][(kind, *(int(x) for x in dims.split("x")))] = bool(c)
-    _PINNED["splitk"] = {tuple(int(x) for x in k.split("x")): int(c) for k, c in plan.get("splitk", {}).items()}
+    _PINNED["splitk"] = {_splitk_key(k): int(c) for k, c in plan.get("splitk", {}).items()}
     if _RACES:
         _RACES["tn"].update(_PINNED["tn"])
         _RACES["splitk"].update(_PINNED["splitk"])
     if not shipped:
         _PLAN_STATE["loaded"] = True
+
+
+def _splitk_key(text: str):
+    """'MxNxK' -> (M, N, K); 'MxNxKxbf16' -> (M, N, K, 'bf16') (the bf16-output race)."""
+    parts = text.split("x")
+    return tuple(p if p == "bf16" else int(p) for p in parts)
 
 
 def export_plan() -> dict:
@@ -389,9 +395,10 @@ class HipGemm:
                for k, c in self._choice.items() if len(k) == 3}
         out.update({f"{k[0]} M{k[1]}xN{k[2]}xK{k[3]}": ("fused gemm_bf16" if c else "unfused (linear + kernel)")
                     for k, c in self._choice.items() if len(k) == 4})
-        out.update({f"wgrad M{m}xN{n}xK{k}": (f"hand-written gemm_wgrad x{-s}" if s < 0 else
-                                              f"hipBLASLt split-K x{s}" if s > 1 else "hipBLASLt accumulate")
-                    for (m, n, k), s in self._splitk.items()})
+        out.update({f"wgrad{' (bf16 out)' if len(key) == 4 else ''} M{key[0]}xN{key[1]}xK{key[2]}":
+                    (f"hand-written gemm_wgrad x{-s}" if s < 0 else
+                     f"hipBLASLt split-K x{s}" if s > 1 else "hipBLASLt plain")
+                    for key, s in self._splitk.items()})
         return out
 
     def linear_dgrad(self, dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
@@ -439,18 +446,42 @@ class HipGemm:
             part.zero_()
             ok = hip.gemm_wgrad(part[0], dy, x, 1)
         else:
-            ok = hip.gemm_wgrad(part[0], dy, x, s, part=part)  # part[0] is a scratch target
+            ok = hip.gemm_wgrad(None, dy, x, s, part=part)  # partials only
         if not ok:
             raise RuntimeError(f"hand wgrad cannot tile {M}x{N}x{K}")
         hip.splitk_sum_bf16(part, dw2)
 
-    def _pick_splitk(self, dw2, dy, x):
-        """Weight-gradient race, per (M, N, K): hipBLASLt plain (1) / hipBLASLt split-K
-        (s > 1) / the hand-written kernel with s splits (-s).  Recorded in the plan."""
+    def _run_wgrad(self, dw2, dy, x, s, to_bf16):
+        """One weight-gradient route: s = 1 hipBLASLt plain (beta 1 into fp32, or beta 0
+        with a bf16 D), s > 1 hipBLASLt split-K, s < 0 the hand-written kernel with -s
+        splits; bf16 outputs take the fp32 partials summed straight into bf16."""
         from . import hip
         M, N = dy.shape
         K = x.shape[1]
-        key = (M, N, K)
+        if s < 0:
+            self._wgrad_hand(dw2, dy, x, -s, to_bf16=to_bf16)
+        elif s > 1 and to_bf16:
+            ms = M // s
+            lx, ly = _rowmajor(x), _rowmajor(dy)
+            part = torch.empty(s, N, K, dtype=torch.float32, device=dw2.device)
+            _gemm_batched(0, 1, K, N, ms, x, lx, ms * lx, dy, ly, ms * ly, part, K, N * K, s, 1.0, 0.0)
+            hip.splitk_sum_bf16(part, dw2)
+        elif s > 1:
+            self._wgrad_split(dw2, dy, x, s)
+        elif to_bf16:
+            _gemm(0, 1, K, N, M, x, _rowmajor(x), dy, _rowmajor(dy), dw2, K, 1.0, 0.0)
+        else:
+            self._wgrad_plain(dw2, dy, x)
+
+    def _pick_splitk(self, dw2, dy, x, to_bf16=False):
+        """Weight-gradient race, per (M, N, K) and output dtype: hipBLASLt plain (1) /
+        hipBLASLt split-K (s > 1) / the hand-written kernel with s splits (-s).  The
+        bf16-output routes (wgrad_set) race separately, key (M, N, K, "bf16"): the
+        library's bf16-D kernels are different (and slower) ones.  Recorded in the plan."""
+        from . import hip
+        M, N = dy.shape
+        K = x.shape[1]
+        key = (M, N, K, "bf16") if to_bf16 else (M, N, K)
         if key in self._splitk:
             return self._splitk[key]
         cands = [s for s in self.SPLITK_CANDIDATES if M % (s * 8) == 0 and (N * K) % 4 == 0]
@@ -465,7 +496,8 @@ class HipGemm:
                 or torch.cuda.is_current_stream_capturing()):
             self._splitk[key] = 1
             return 1
-        scratch = torch.zeros_like(dw2)  # timing must not disturb the real accumulator
+        # timing must not disturb the real accumulator / gradient buffer
+        scratch = torch.zeros(N, K, dtype=torch.bfloat16 if to_bf16 else torch.float32, device=dy.device)
 
         def t_of(fn):
             fn()
@@ -480,11 +512,11 @@ class HipGemm:
                 e1.synchronize()
                 best = min(best, e0.elapsed_time(e1))
             return best
-        best, choice = t_of(lambda: self._wgrad_plain(scratch, dy, x)), 1
+        best, choice = t_of(lambda: self._run_wgrad(scratch, dy, x, 1, to_bf16)), 1
         for s in cands:
             if s > 1 and not self._splitk_on:
                 continue
-            t = t_of(lambda: self._wgrad_hand(scratch, dy, x, -s) if s < 0 else self._wgrad_split(scratch, dy, x, s))
+            t = t_of(lambda: self._run_wgrad(scratch, dy, x, s, to_bf16))
             if t < (self.RACE_MARGIN if s < 0 else 0.93) * best:
                 best, choice = t, s
         del scratch
@@ -501,29 +533,16 @@ class HipGemm:
 
     def wgrad_set(self, dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
         """dw (bf16, overwritten) = dy^T @ x: a weight gradient written straight in the
-        reduce dtype (the FSDP runtime's per-micro-step send buffer).  Library GEMM with
-        beta = 0 and a bf16 D, or the raced split-K slices summed into bf16 in fixed order."""
-        from . import hip
+        reduce dtype (the FSDP runtime's per-micro-step send buffer): the raced bf16 route
+        (library GEMM with beta = 0 and a bf16 D, or split-K / hand-written partials
+        summed into bf16 in fixed order)."""
         M, N = dy.shape
         K = x.shape[1]
         dw2 = dw.view(N, K)
         if dw2.dtype != torch.bfloat16 or not dw2.is_contiguous():
             raise ValueError("wgrad_set output must be contiguous bf16")
-        key = (M, N, K)
-        s = self._splitk.get(key)
-        if s is None:  # race on an fp32 scratch like wgrad_acc (same key, same decision)
-            s = self._pick_splitk(torch.zeros(N, K, dtype=torch.float32, device=dw.device), dy, x)
-        s = self._resolve(s, dy, x)
-        if s < 0:
-            self._wgrad_hand(dw2, dy, x, -s, to_bf16=True)
-        elif s > 1:
-            ms = M // s
-            lx, ly = _rowmajor(x), _rowmajor(dy)
-            part = torch.empty(s, N, K, dtype=torch.float32, device=dw.device)
-            _gemm_batched(0, 1, K, N, ms, x, lx, ms * lx, dy, ly, ms * ly, part, K, N * K, s, 1.0, 0.0)
-            hip.splitk_sum_bf16(part, dw2)
-        else:
-            _gemm(0, 1, K, N, M, x, _rowmajor(x), dy, _rowmajor(dy), dw2, K, 1.0, 0.0)
+        s = self._resolve(self._pick_splitk(dw2, dy, x, to_bf16=True), dy, x)
+        self._run_wgrad(dw2, dy, x, s, True)
 
     def wgrad_acc(self, dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
         if dw.dtype == torch.bfloat16:  # a reduce-dtype gradient buffer (first and only write)
@@ -534,9 +553,4 @@ class HipGemm:
         if dw2.dtype != torch.float32 or not dw2.is_contiguous():
             raise ValueError("wgrad accumulator must be contiguous fp32")
         s = self._resolve(self._pick_splitk(dw2, dy, x), dy, x)
-        if s < 0:
-            self._wgrad_hand(dw2, dy, x, -s)
-        elif s > 1:
-            self._wgrad_split(dw2, dy, x, s)
-        else:
-            self._wgrad_plain(dw2, dy, x)
+        self._run_wgrad(dw2, dy, x, s, False)

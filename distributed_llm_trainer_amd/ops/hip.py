@@ -643,18 +643,24 @@ def wgrad_splits(T: int, Nr: int, Nc: int, target: int = 256) -> int:
     return max(1, min(T // 128, (target + tiles // 2) // tiles))
 
 
-def gemm_wgrad(dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, splits: int = 0,
+def gemm_wgrad(dw: Optional[torch.Tensor], dy: torch.Tensor, x: torch.Tensor, splits: int = 0,
                part: Optional[torch.Tensor] = None) -> bool:
     """dw[Nr,Nc] (fp32) += dy[T,Nr]^T @ x[T,Nc] with the hand-written MFMA kernel
     (csrc/gemm_wgrad.hip).  splits == 0 picks the CU-filling split; with splits > 1 the
     fp32 partials go to `part` ([splits, Nr, Nc], allocated if None) and are summed into
-    dw in fixed split order (deterministic).  Returns False (nothing launched) when the
-    shape does not tile."""
+    dw in fixed split order (deterministic).  dw = None with splits > 1: only the
+    partials are written (the caller reduces them, e.g. straight into bf16).  Returns
+    False (nothing launched) when the shape does not tile."""
     T, Nr = dy.shape
     Nc = x.shape[1]
     if not wgrad_fits(T, Nr, Nc) or dy.stride(1) != 1 or x.stride(1) != 1 or dy.stride(0) % 8 or x.stride(0) % 8:
         return False
-    _req(dw, torch.float32, "wgrad.dw", Nr * Nc)
+    if dw is None:
+        if splits <= 1 or part is None or part.dtype != torch.float32 or part.numel() < splits * Nr * Nc \
+                or not part.is_contiguous():
+            raise ValueError("gemm_wgrad: partials-only mode needs splits > 1 and an fp32 part buffer")
+    else:
+        _req(dw, torch.float32, "wgrad.dw", Nr * Nc)
     if dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16 or x.shape[0] != T:
         raise ValueError("gemm_wgrad: bf16 dy[T,Nr] / x[T,Nc] expected")
     if splits <= 0:
@@ -662,9 +668,9 @@ def gemm_wgrad(dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, splits: int 
     splits = min(splits, T // 128)
     if splits > 1 and (part is None or part.numel() < splits * Nr * Nc):
         part = torch.empty(splits * Nr * Nc, device=dw.device, dtype=torch.float32)
-    _chk(lib().dlt_gemm_wgrad(_p(dy), _p(x), _p(dw), _p(part) if splits > 1 else None, T, Nr, Nc,
-                              dy.stride(0), x.stride(0), splits, _stream()), "gemm_wgrad")
-    if splits > 1:
+    _chk(lib().dlt_gemm_wgrad(_p(dy), _p(x), _p(dw) if dw is not None else None, _p(part) if splits > 1 else None,
+                              T, Nr, Nc, dy.stride(0), x.stride(0), splits, _stream()), "gemm_wgrad")
+    if splits > 1 and dw is not None:
         _chk(lib().dlt_splitk_acc(_p(part), _p(dw), Nr * Nc, splits, _stream()), "splitk_acc")
     return True
 

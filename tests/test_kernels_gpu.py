@@ -552,6 +552,39 @@ def test_planner_fused_races_match_unfused():
     assert f"rope:{M}x{3 * nh * 64}x{K}" in plan["fused"]
 
 
+@pytest.mark.parametrize("choice", [-1, -3, 1, 2])
+def test_planner_wgrad_choices_fp32_and_bf16(choice):
+    """Every weight-gradient route of HipGemm -- hand-written kernel in place (-1) or with
+    split-K partials (-3), hipBLASLt plain (1) or split-K (2) -- into an fp32 accumulator
+    (wgrad_acc) and straight into a bf16 buffer (wgrad_set, the FSDP reduce-dtype path)
+    against the fp32 reference."""
+    from distributed_llm_trainer_amd.ops import gemm
+    torch.manual_seed(5)
+    g = gemm.HipGemm()
+    T, N, K = 2048, 768, 384
+    dy = torch.randn(T, N, device=DEV).bfloat16()
+    x = torch.randn(T, K, device=DEV).bfloat16()
+    keys = [(T, N, K), (T, N, K, "bf16")]  # fp32-accumulate and bf16-output races
+    saved = {k: g._splitk.get(k, "absent") for k in keys}
+    for k in keys:
+        g._splitk[k] = choice
+    try:
+        base = torch.randn(N, K, device=DEV)
+        ref = dy.float().t() @ x.float()
+        dw = base.clone()
+        g.wgrad_acc(dw, dy, x)
+        _close(dw, base + ref, 1e-3 * T ** 0.5, 1e-4, f"wgrad_acc {choice}")
+        db = torch.empty(N, K, device=DEV, dtype=torch.bfloat16)
+        g.wgrad_set(db, dy, x)
+        assert _relerr(db, ref) < 1e-2, f"wgrad_set {choice}"
+    finally:
+        for k in keys:
+            if saved[k] == "absent":
+                g._splitk.pop(k, None)
+            else:
+                g._splitk[k] = saved[k]
+
+
 def test_scale_bf16():
     x = torch.randn(64, 768, device=DEV).bfloat16()
     s = torch.tensor(0.25, device=DEV)

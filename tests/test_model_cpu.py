@@ -104,26 +104,36 @@ def test_dropout_recompute_replays_masks():
         assert torch.allclose(p1.grad, p2.grad, atol=1e-7, rtol=1e-5), n
 
 
-def test_selective_recompute_matches_full_recompute():
+@pytest.mark.parametrize("packed", [True, False])
+def test_selective_recompute_matches_full_recompute(packed):
     """Selective checkpointing (keeps o / lse / x2, recomputes only norm -> QKV -> RoPE and
-    norm -> gate/up -> SwiGLU) gives bit-identical gradients to whole-block recompute and
-    to no recompute at all."""
+    norm -> gate/up -> SwiGLU), its budgeted form (also keeps the QKV / gate-up GEMM
+    outputs: recomputes only the norms and SwiGLU) and whole-block recompute give
+    bit-identical gradients to no recompute at all -- on the packed-QKV path and on the
+    split q/k/v path."""
     torch.manual_seed(3)
     cfg = tiny(dropout=0.1, attention_dropout=0.1)
     base = GPT(cfg)
     ids = torch.randint(0, 256, (2, 32))
     grads = []
-    for ac, selective in ((False, True), (True, False), (True, True)):
+    for ac, selective, budget in ((False, True, 0.0), (True, False, 0.0), (True, True, 0.0), (True, True, 1e12),
+                                  (True, True, None)):
         m = copy.deepcopy(base)
         m.enable_engine(seed=5)
+        if budget is None:  # exactly the QKV outputs of both chains of a window
+            esize = torch.empty((), dtype=m.engine.act_dtype).element_size()
+            budget = 2 * 32 * 3 * cfg.hidden_size * cfg.num_layers * 2 * esize
+        m.engine.packed_qkv = packed and m.engine.packed_qkv
         m.gradient_checkpointing = ac
         m.engine.selective_recompute = selective
+        m.engine.ac_budget = budget
         _, loss = m(ids, labels=ids)
         loss.backward()
         grads.append([p.grad.clone() for p in m.parameters()])
-    for g_full, g_sel, g_none in zip(grads[1], grads[2], grads[0]):
-        assert torch.equal(g_full, g_sel)
-        assert torch.equal(g_none, g_sel)
+    assert m.engine._ac_keep(2 * 32) == (True, False)  # the last budget fits QKV only
+    for g in grads[1:]:
+        for a, b in zip(grads[0], g):
+            assert torch.equal(a, b)
 
 
 def test_dropout_gradient_finite_difference():

@@ -328,17 +328,21 @@ def test_attention_masks_regenerated_beyond_budget():
 
 
 def test_selective_recompute_matches_full_and_none_gpu():
-    """Activation checkpointing on the HIP path: selective recompute (default), whole-block
-    recompute (the reference's checkpoint(block)) and no recompute give the same gradients
-    (dropout on, so the replayed masks are checked too)."""
+    """Activation checkpointing on the HIP path: selective recompute (with and without the
+    kept GEMM outputs of the memory budget), whole-block recompute (the reference's
+    checkpoint(block)) and no recompute give the same gradients (dropout on, so the
+    replayed masks are checked too)."""
     torch.manual_seed(9)
     base = GPT(_cfg(0.1)).to(DEV)
     ids = torch.randint(0, 1000, (2, 256), device=DEV)
     grads = []
-    for recompute, selective in ((False, True), (True, True), (True, False)):
+    # (budget 0: the QKV / gate-up GEMMs are recomputed; 1e12: their outputs are kept)
+    for recompute, selective, budget in ((False, True, 0.0), (True, True, 0.0), (True, True, 1e12),
+                                         (True, False, 0.0)):
         m = copy.deepcopy(base)
         eng = m.enable_engine(seed=4)
         eng.selective_recompute = selective
+        eng.ac_budget = budget
         m.gradient_checkpointing = recompute
         _, loss = m(ids, labels=ids)
         loss.backward()

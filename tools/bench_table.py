@@ -18,6 +18,7 @@ REF = {("ddp", "small", 1): 12500, ("ddp", "small", 2): 24100, ("ddp", "small", 
 
 CONFIGS = {
     "ddp_small": ["--model_size", "small", "--batch_size", "8", "--grad_accum", "4"],
+    "ddp_small_lean": ["--model_size", "small", "--batch_size", "8", "--grad_accum", "4", "--memory_lean"],
     "fsdp_small": ["--mode", "fsdp", "--model_size", "small", "--batch_size", "8", "--grad_accum", "4"],
     "ddp_medium": ["--model_size", "medium", "--batch_size", "4", "--grad_accum", "8"],
     "fsdp_medium": ["--mode", "fsdp", "--model_size", "medium", "--batch_size", "4", "--grad_accum", "8"],
@@ -55,7 +56,7 @@ def main():
         for name in a.configs.split(","):
             res = run(n, CONFIGS[name], a.steps, a.warmup, a.timeout)
             mode, size = name.split("_")[0], name.split("_")[1]
-            ref = REF.get((mode, size, n))
+            ref = REF.get((mode, size, n)) if name.count("_") == 1 else None  # variants: no reference row
             vs = f"{res['value'] / ref:.1f}x ({ref:,})" if ref else "--"
             lines.append(f"| {n} | {name} | {res['value']:,.0f} | {res['ms_per_step']:.1f} | "
                          f"{res['peak_gb_per_gpu']:.1f} | {res['final_loss']:.3f} | {vs} |")
