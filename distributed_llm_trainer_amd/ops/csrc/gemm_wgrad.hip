@@ -29,8 +29,8 @@
 // atomics, bitwise run-to-run reproducible (DDP replicas stay identical).  With one split
 // the kernel adds straight into dW.
 //
-// Requirements (launcher-checked): Nr % 256 == 0, Nc % 192 == 0, T % 128 == 0, 16-byte
-// aligned rows.
+// Requirements (launcher-checked): Nr % 128 == 0 (a last half tile when Nr % 256 == 128),
+// Nc % 192 == 0, T % 128 == 0, 16-byte aligned rows.
 #include "common.h"
 
 typedef __attribute__((address_space(3))) void* gw_lds_vptr_t;
@@ -111,11 +111,24 @@ __global__ __launch_bounds__(512, 1) void k_gemm_wgrad(const bf16_t* __restrict_
   const int wm = wid & 3, wn = wid >> 2;
   const int l16 = lane & 15, lq = lane >> 4;
 
-  // workgroup -> (split, tile): the splits of one tile are consecutive workgroup ids
-  // (they share nothing but are issued together); tiles row-major over (Nr / 256, Nc / 192)
+  // workgroup -> (row tile, split, column tile), XCD-aware: the dispatcher deals workgroup
+  // ids round-robin to the 8 XCDs, so ids i, i + 8, ... share an XCD's L2.  A unit u =
+  // (row tile, split) reads one [T / splits, 256] slab of dY, which every column tile of
+  // that row needs: the ntc column tiles of unit u are ids 8 * (ntc * (u / 8) + c) + u % 8,
+  // all on XCD u % 8 and dispatched together, so the slab is fetched from HBM once, not
+  // ntc times (the 3.3 GB dlogits slab of the lm_head gradient was read 4x before).
+  // The grid is padded to whole groups of 8 units; padding workgroups exit at once.
   const int ntc = Nc / 192;
-  const int split = blockIdx.x % splits, tile = blockIdx.x / splits;
-  const int r0 = (tile / ntc) * 256, c0 = (tile % ntc) * 192;
+  const int nunits = ((Nr + 255) / 256) * splits;
+  const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3;
+  const int u = (q / ntc) * 8 + xcd;
+  if (u >= nunits) return;  // padding (uniform over the workgroup, before any barrier)
+  const int split = u % splits;
+  const int r0 = (u / splits) * 256, c0 = (q % ntc) * 192;
+  // Nr % 256 == 128 (the 50304-row lm_head / embedding gradient): the last row tile has
+  // 128 valid dW rows -- its other half re-reads valid columns (no out-of-bounds reads
+  // at the end of dY) and stores nothing (wm >= 2 is wave-uniform)
+  const bool half_tile = r0 + 256 > Nr;
   const int npair = T / (2 * GW_BK);
   const int p0 = (int)(((long)split * npair) / splits), p1 = (int)(((long)(split + 1) * npair) / splits);
   const int kt0 = 2 * p0, nk = 2 * (p1 - p0);  // K-tiles [kt0, kt0 + nk), nk even >= 2
@@ -141,7 +154,11 @@ __global__ __launch_bounds__(512, 1) void k_gemm_wgrad(const bf16_t* __restrict_
     const int t = e >> 4, pc = e & 15;
     const int lc = pc ^ (2 * gw_v256(t));
 #pragma unroll
-    for (int q = 0; q < 2; ++q) oa[q][j] = (uint32_t)(t * ldy + gw_amap(q, lc * 8)) * 2u;
+    for (int q = 0; q < 2; ++q) {
+      int col = gw_amap(q, lc * 8);
+      if (half_tile) col &= 127;
+      oa[q][j] = (uint32_t)(t * ldy + col) * 2u;
+    }
     ob0[j] = (uint32_t)(t * ldx + gw_b0map(lc * 8)) * 2u;
   }
   {
@@ -309,6 +326,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_wgrad(const bf16_t* __restrict_
   // epilogue: acc[nt][mt] = D[n][m]: lane owns dW row r0 + wm*64 + mt*16 + l16 and the 4
   // consecutive columns c0 + wn*96 + nt*16 + lq*4 .. +3 (one float4)
   float* const dst = out + (accumulate ? 0 : (size_t)split * Nr * Nc);
+  if (half_tile && wm >= 2) return;  // rows past Nr (wave-uniform; no barrier follows)
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) {
     float* row = dst + (size_t)(r0 + wm * 64 + mt * 16 + l16) * Nc + c0 + wn * 96 + lq * 4;
@@ -333,10 +351,10 @@ __global__ __launch_bounds__(512, 1) void k_gemm_wgrad(const bf16_t* __restrict_
 // fixed order).  Returns -1 (nothing launched) for shapes outside the tiling.
 DLT_API int dlt_gemm_wgrad(const bf16_t* dY, const bf16_t* X, float* dW, float* part, int T, int Nr, int Nc, int ldy,
                            int ldx, int splits, hipStream_t st) {
-  if (T <= 0 || T % 128 || Nr % 256 || Nc % 192 || (ldy | ldx) % 8 || splits < 1 || splits > T / 128) return -1;
+  if (T <= 0 || T % 128 || Nr % 128 || Nc % 192 || (ldy | ldx) % 8 || splits < 1 || splits > T / 128) return -1;
   if (splits > 1 && part == nullptr) return -1;
-  const int tiles = (Nr / 256) * (Nc / 192);
-  k_gemm_wgrad<<<tiles * splits, 512, 0, st>>>(dY, X, splits > 1 ? part : dW, T, Nr, Nc, ldy, ldx, splits,
+  const int units = ((Nr + 255) / 256) * splits;  // (row tile, split) pairs, padded to 8s
+  k_gemm_wgrad<<<((units + 7) / 8) * 8 * (Nc / 192), 512, 0, st>>>(dY, X, splits > 1 ? part : dW, T, Nr, Nc, ldy, ldx, splits,
                                                splits > 1 ? 0 : 1);
   DLT_CHECK_LAUNCH();
 }

@@ -484,16 +484,18 @@ class HipGemm:
         key = (M, N, K, "bf16") if to_bf16 else (M, N, K)
         if key in self._splitk:
             return self._splitk[key]
-        cands = [s for s in self.SPLITK_CANDIDATES if M % (s * 8) == 0 and (N * K) % 4 == 0]
+        # library split-K: skinny outputs only (its [s, N, K] fp32 scratch)
+        cands = [s for s in self.SPLITK_CANDIDATES if M % (s * 8) == 0 and (N * K) % 4 == 0
+                 and N * K <= 4096 * 4096]
         hand = (self._hand_wgrad and x.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16
                 and hip.wgrad_fits(M, N, K) and x.is_contiguous() and dy.is_contiguous())
         if hand:  # whole rounds of 256 workgroups, plus a few fixed depths (sweep in
-            # profiles/r3_wgrad.md: the best split is shape-specific, 5..16 here)
-            tiles = (N // 256) * (K // 192)
-            hs = {max(1, (256 * r) // tiles) for r in (1, 2, 3)} | {4, 8, 16}
-            cands += [-h for h in sorted(hs) if h <= min(64, M // 128)]
-        if (not (self._splitk_on or hand) or not cands or N * K > 4096 * 4096
-                or torch.cuda.is_current_stream_capturing()):
+            # profiles/r3_wgrad.md: the best split is shape-specific, 5..16 here); the
+            # split partials ([s, N, K] fp32) stay under ~1 GB
+            tiles = ((N + 255) // 256) * (K // 192)
+            hs = {max(1, (256 * r) // tiles) for r in (1, 2, 3)} | {2, 3, 4, 8, 16}
+            cands += [-h for h in sorted(hs) if h <= min(64, M // 128) and (h == 1 or h * N * K * 4 <= 1 << 30)]
+        if (not (self._splitk_on or hand) or not cands or torch.cuda.is_current_stream_capturing()):
             self._splitk[key] = 1
             return 1
         # timing must not disturb the real accumulator / gradient buffer

@@ -632,14 +632,15 @@ def cast_bf16(x: torch.Tensor, y: torch.Tensor) -> None:
 
 # ---------------------------------------------------------------- wgrad GEMM
 def wgrad_fits(T: int, Nr: int, Nc: int) -> bool:
-    """Shapes the 256 x 192 weight-gradient kernel tiles exactly (T in 128-token pairs)."""
-    return T > 0 and T % 128 == 0 and Nr % 256 == 0 and Nc % 192 == 0
+    """Shapes the 256 x 192 weight-gradient kernel tiles (T in 128-token pairs; a last
+    half row tile when Nr % 256 == 128)."""
+    return T > 0 and T % 128 == 0 and Nr % 128 == 0 and Nc % 192 == 0
 
 
 def wgrad_splits(T: int, Nr: int, Nc: int, target: int = 256) -> int:
     """Split-K factor that brings tiles x splits closest to `target` workgroups (one per
     CU), capped by the number of 128-token pairs."""
-    tiles = (Nr // 256) * (Nc // 192)
+    tiles = ((Nr + 255) // 256) * (Nc // 192)
     return max(1, min(T // 128, (target + tiles // 2) // tiles))
 
 

@@ -418,10 +418,12 @@ def test_gemm_plan_pin_roundtrip(tmp_path):
     gemm.load_plan(str(path))  # loading a saved plan re-pins without error
 
 
-@pytest.mark.parametrize("T,Nr,Nc", [(1024, 256, 192), (2048, 768, 384), (4096, 2304, 768)])
+@pytest.mark.parametrize("T,Nr,Nc", [(1024, 256, 192), (2048, 768, 384), (4096, 2304, 768), (1024, 384, 192),
+                                     (2048, 50304, 768)])
 def test_gemm_wgrad_kernel(T, Nr, Nc):
     """Hand-written weight-gradient GEMM (in-place and split-K + fixed-order sum) vs
-    the fp32 torch reference; split-K results are bitwise repeatable."""
+    the fp32 torch reference; split-K results are bitwise repeatable.  Nr % 256 == 128
+    (384; the 50304-row lm_head gradient) runs a last half row tile."""
     torch.manual_seed(0)
     dy = torch.randn(T, Nr, device=DEV).bfloat16()
     x = torch.randn(T, Nc, device=DEV).bfloat16()
@@ -436,7 +438,7 @@ def test_gemm_wgrad_kernel(T, Nr, Nc):
     dw = base.clone()
     assert hip.gemm_wgrad(dw, dy, x, 0)
     assert torch.equal(dw, outs[0]), "split-K wgrad not deterministic"
-    assert not hip.gemm_wgrad(base, dy[:, :128], x), "untileable shape must be refused"
+    assert not hip.gemm_wgrad(base, dy[:, :64], x), "untileable shape must be refused"
 
 
 @pytest.mark.parametrize("p", [0.0, 0.1])

@@ -293,7 +293,7 @@ static int wgrad_main(std::vector<int> shp) {
     CK(hipMalloc(&dW2, (size_t)Nr * Nc * 4));
     k_fill<<<1024, 256, 0, st>>>(dY, (size_t)T * Nr, 21);
     k_fill<<<1024, 256, 0, st>>>(X, (size_t)T * Nc, 22);
-    const int tiles = (Nr / 256) * (Nc / 192);
+    const int tiles = ((Nr + 255) / 256) * (Nc / 192);
     int S = getenv("GW_SPLITS") ? atoi(getenv("GW_SPLITS")) : (256 + tiles / 2) / tiles;
     if (S < 1) S = 1;
     CK(hipMalloc(&part, (size_t)S * Nr * Nc * 4));
@@ -463,7 +463,7 @@ int main(int argc, char** argv) {
   if (argc > 1 && !strcmp(argv[1], "wgrad")) {
     std::vector<int> v;
     for (int i = 2; i < argc; ++i) v.push_back(atoi(argv[i]));
-    if (v.empty()) v = {32768, 2304, 768, 32768, 768, 768, 32768, 6144, 768, 32768, 768, 3072};
+    if (v.empty()) v = {32768, 2304, 768, 32768, 768, 768, 32768, 6144, 768, 32768, 768, 3072, 32768, 50304, 768};
     return wgrad_main(v);
   }
   std::vector<Kern> kerns = {{"blas", run_blas},         {"bf16", run_bf16<0>},      {"rowmaj", run_bf16<4>},
