@@ -51,8 +51,8 @@ def main():
     ap.add_argument("--fusion", type=int, default=0,
                     help="micro_step_fusion: 0 = auto, 1 = run every micro-step on its own")
     ap.add_argument("--memory_lean", action="store_true",
-                    help="TrainingConfig.defer_wgrad=False (the trainer's --memory_lean): per-chain weight "
-                         "gradients, lower peak memory")
+                    help="the trainer's --memory_lean (TrainingConfig.defer_roles='qkv,o'): gate/up, down "
+                         "and lm_head weight gradients per chain, lower peak memory")
     ap.add_argument("--dropout", type=float, default=None,
                     help="ablation only: override dropout/attention_dropout (reference config: 0.1)")
     args = ap.parse_args()
@@ -77,10 +77,10 @@ def main():
         cfg.dropout = cfg.attention_dropout = args.dropout
     if args.mode == "ddp":
         from distributed_llm_trainer_amd.training.configs import TrainingConfig
-        from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
+        from distributed_llm_trainer_amd.training.ddp_trainer import LEAN_DEFER_ROLES, DistributedTrainer
         tc = TrainingConfig(batch_size=args.batch_size, gradient_accumulation_steps=args.grad_accum,
                             max_steps=100000, mixed_precision="bf16", micro_step_fusion=args.fusion,
-                            defer_wgrad=not args.memory_lean)
+                            defer_roles=LEAN_DEFER_ROLES if args.memory_lean else "all")
         trainer = DistributedTrainer(cfg, tc)
     else:
         from distributed_llm_trainer_amd.training.configs import FSDPConfig, FSDPTrainingConfig

@@ -183,6 +183,9 @@ class GPTEngine:
         self.p_hidden = float(cfg.dropout)
         # deferred weight gradients (see set_accumulation)
         self.acc_slot, self.acc_slots, self.defer = 0, 1, False
+        # which weight gradients a deferred window defers (the others run per micro-step):
+        # all by default; the memory-lean mode keeps only the small-operand ones (qkv, o)
+        self.defer_roles = frozenset(self.ROLES)
         self._slots = {}
         self._side = None  # weight-gradient side stream (lazily created)
         self._mask_side = None  # attention keep-bit side stream
@@ -237,6 +240,21 @@ class GPTEngine:
         # buffers then let the weight-gradient GEMMs run on the side stream, overlapped
         # with the next layer's dgrad chain (attention/norm/SwiGLU backward).
         self.defer = bool(defer) and (n_slots > 1 or os.environ.get("DLT_DEFER_GA1", "1") != "0")
+
+    # slot-buffer name -> the weight gradient it feeds (X or dY operand)
+    _SLOT_ROLE = {"n1": "qkv", "dqkv": "qkv", "o": "o", "da": "o", "n2": "gu", "dgu": "gu", "s": "down", "dd": "down",
+                  "lg": "head", "nf": "head"}
+    ROLES = ("qkv", "o", "gu", "down", "head")
+
+    def _deferred(self, st, role: str) -> bool:
+        return st.defer and role in self.defer_roles
+
+    def _sb(self, st, layer, name: str, M: int, N: int, device):
+        """The micro-step's slice of a slot buffer when ``name``'s weight gradient is
+        deferred, else None (the producing kernel allocates as usual)."""
+        if not self._deferred(st, self._SLOT_ROLE[name]):
+            return None
+        return self._slot_buf(st, layer, name, M, N, device)[0]
 
     def _slot_buf(self, st, layer, name: str, M: int, N: int, device):
         key = (layer, name)
@@ -314,7 +332,7 @@ class GPTEngine:
 
         M, H, I = B * S, cfg.hidden_size, cfg.intermediate_size
         dv = r.device
-        sb = (lambda name, n: self._slot_buf(st, i, name, M, n, dv)[0]) if st.defer else (lambda name, n: None)
+        sb = lambda name, n: self._sb(st, i, name, M, n, dv)  # noqa: E731
         # attention keep-bits depend only on the RNG key: build them on a side stream
         # so the VALU-only hashing overlaps the norm + QKV GEMM + RoPE below
         mask, mask_ev = self._attn_mask_async(B, S, pa, k_attn, dv)
@@ -391,7 +409,7 @@ class GPTEngine:
         cos, sin = self.rope(S, c.x.device)
         M, H, I = B * S, cfg.hidden_size, cfg.intermediate_size
         dv = c.x.device
-        sb = (lambda name, n: self._slot_buf(st, i, name, M, n, dv)[0]) if st.defer else (lambda name, n: None)
+        sb = lambda name, n: self._sb(st, i, name, M, n, dv)  # noqa: E731
         _, n1, rstd1 = ops.add_dropout_rmsnorm_fwd(c.x, None, w.ln1, self.eps, 0.0, 0, self.act_dtype,
                                                    y_out=sb("n1", H))
         if c.q is not None:  # QKV output kept by the forward (_ac_keep)
@@ -471,7 +489,7 @@ class GPTEngine:
         if targets is not None:
             # [M, Vp]; with deferred weight gradients the logits (-> dlogits) of every
             # micro-step of the window stay resident for ONE lm_head wgrad GEMM
-            lg_out = self._slot_buf(st, "head", "lg", B * S, Vp, nf.device)[0] if st.defer else None
+            lg_out = self._sb(st, "head", "lg", B * S, Vp, nf.device)
             lg = self.gemm.linear(nf, hw.lm_head, out=lg_out)
             nseg = self.loss_segments if (train and B % self.loss_segments == 0) else 1
             if nseg == 1:
@@ -527,11 +545,14 @@ class GPTEngine:
         hw, hg = prov.head(), prov.head_grads()
         M, H, I = B * S, cfg.hidden_size, cfg.intermediate_size
         dev = st.dlogits.device
-        do_wgrad = (not st.defer) or st.last
-        side = self._wgrad_stream(dev) if (do_wgrad and st.defer) else None
+        # deferred roles: one GEMM over the window at the last micro-step (side stream);
+        # the others (defer_roles) run in every micro-step's own backward, inline
+        dfr = {r: self._deferred(st, r) for r in self.ROLES}
+        win = st.last and any(dfr.values())  # this backward runs the window's deferred GEMMs
+        side = self._wgrad_stream(dev) if win else None
         # lm_head: dnf = dlogits @ E ; dE += dlogits^T @ (nf * dloss)
         dnf = gm.linear_dgrad(st.dlogits, hw.lm_head)
-        nf_out = self._slot_buf(st, "head", "nf", M, H, dev)[0] if st.defer else None
+        nf_out = self._sb(st, "head", "nf", M, H, dev)
         if st.nf.dtype == torch.bfloat16:
             nf_scaled = ops.scale_bf16(st.nf, dloss, out=nf_out)
         else:
@@ -539,7 +560,7 @@ class GPTEngine:
             if nf_out is not None:
                 nf_scaled = nf_out.copy_(nf_scaled)
         head_ev = None
-        if not st.defer:
+        if not dfr["head"]:
             gm.wgrad_acc(hg.embed, st.dlogits, nf_scaled)
         elif st.last:
             # ONE [Vp, H] wgrad GEMM over all GA*M rows of the window (K = 32768 instead
@@ -578,7 +599,7 @@ class GPTEngine:
             prov.post_backward("head")
 
         def sb(layer, name, n):
-            return self._slot_buf(st, layer, name, M, n, dev)[0] if st.defer else None
+            return self._sb(st, layer, name, M, n, dev)
 
         def full(layer, name, n):
             return self._slot_buf(st, layer, name, M, n, dev)[1]
@@ -628,28 +649,44 @@ class GPTEngine:
                 head_done()
             # weight gradients (fp32 accumulate into the main-grad buffers)
             side_ctx = None
-            if do_wgrad:
-                if st.defer:
-                    # One GEMM per weight over the whole accumulation window.  The
-                    # slot buffers are persistent, so these can run on a side stream
-                    # concurrently with the next layer's dgrad chain (the small-output
-                    # wgrads leave most CUs idle); the layer's gradient hook (DDP
-                    # bucket all-reduce) is issued from the same stream.
-                    if side is not None and i >= n_main:
-                        ev = torch.cuda.Event()
-                        ev.record()
-                        side.wait_event(ev)
-                        side_ctx = torch.cuda.stream(side)
-                        side_ctx.__enter__()
+            # deferred: one GEMM per weight over the whole accumulation window.  The
+            # slot buffers are persistent, so these can run on a side stream
+            # concurrently with the next layer's dgrad chain (the small-output
+            # wgrads leave most CUs idle); the layer's gradient hook (DDP
+            # bucket all-reduce) is issued from the same stream.
+            if win:
+                if side is not None and i >= n_main:
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    side.wait_event(ev)
+                    side_ctx = torch.cuda.stream(side)
+                    side_ctx.__enter__()
+                if dfr["down"]:
                     gm.wgrad_acc(gr.wdown, full(i, "dd", H), full(i, "s", I))
+                if dfr["gu"]:
                     gm.wgrad_acc(gr.wgu, full(i, "dgu", 2 * I), full(i, "n2", H))
+                if dfr["o"]:
                     gm.wgrad_acc(gr.wo, full(i, "da", H), full(i, "o", H))
+                if dfr["qkv"]:
                     gm.wgrad_acc(gr.wqkv, full(i, "dqkv", 3 * H), full(i, "n1", H))
-                else:
+            if not all(dfr.values()):  # the per-micro-step ones, on this backward's stream
+                if side_ctx is not None:
+                    side_ctx.__exit__(None, None, None)
+                if not dfr["down"]:
                     gm.wgrad_acc(gr.wdown, g_d, c.s)
+                if not dfr["gu"]:
                     gm.wgrad_acc(gr.wgu, dgu, c.n2)
+                if not dfr["o"]:
                     gm.wgrad_acc(gr.wo, da, c.o)
+                if not dfr["qkv"]:
                     gm.wgrad_acc(gr.wqkv, dqkv, c.n1)
+                if side_ctx is not None:
+                    # the gradient hook goes out from the side stream, after both halves
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    side.wait_event(ev)
+                    side_ctx = torch.cuda.stream(side)
+                    side_ctx.__enter__()
             del dgu, da, dqkv
             g_x2, g_d = g_x2n, g_dn
             st.caches[i] = None
@@ -668,7 +705,7 @@ class GPTEngine:
             torch.cuda.current_stream().wait_stream(side)
             for i in late:
                 prov.post_backward(i)
-        if side is not None and do_wgrad and st.defer:
+        if side is not None:
             torch.cuda.current_stream().wait_stream(side)
 
     # ------------------------------------------------------ pipelined window

@@ -46,6 +46,9 @@ class TrainingConfig:
     lr_schedule_fix: bool = True       # set LR before the step + clamp cosine (Q5/Q6)
     adam_eps: float = 1e-8
     defer_wgrad: bool = True           # one weight-grad GEMM per layer per optimizer step
+    # which weight gradients defer_wgrad defers: "all", or a comma list of qkv / o / gu / down
+    # / head (the others run in each micro-step chain's backward); --memory_lean: "qkv,o"
+    defer_roles: str = "all"
     pipeline_micro_steps: bool = True  # overlap fwd(k+1) with bwd(k) on two HIP streams (engine path)
     # execute F consecutive micro-steps as one forward/backward chain of F*batch_size rows
     # (loss normalised per micro-step, so the gradient is the reference's GA average);

@@ -112,6 +112,7 @@ class DistributedTrainer:
         if self.use_engine:
             act = self.dtype if self.device.type == "cuda" else None
             eng = self.model.enable_engine(seed=self.training_config.seed + 1000003 * self.rank, act_dtype=act)
+            eng.defer_roles = parse_defer_roles(self.training_config.defer_roles)
             self.store = self.model.store
         else:
             self.store = FlatParamStore(self.model, self.device, compute_dtype=torch.float32)
@@ -175,8 +176,8 @@ class DistributedTrainer:
                 self.ddp.require_sync(False)
             dloss = torch.full((), 1.0 / chains, dtype=torch.float32, device=self.device)
             range_push("window")
-            # defer_wgrad=False (--memory_lean): each chain's weight gradients run in its own
-            # backward, so no [GA*M, N] slot buffers and no window-wide dlogits are kept
+            # defer_wgrad=False: each chain's weight gradients run in its own backward, so no
+            # [GA*M, N] slot buffers and no window-wide dlogits are kept (defer_roles: per role)
             losses = self.model.engine.train_window(
                 ids_l, tg_l, dloss, recompute=bool(self.model.gradient_checkpointing),
                 before_last=(lambda: self.ddp.require_sync(True)) if self.ddp is not None else None,
@@ -274,6 +275,21 @@ class DistributedTrainer:
 
 
 # --------------------------------------------------------------------------- CLI
+LEAN_DEFER_ROLES = "qkv,o"
+
+
+def parse_defer_roles(text: str) -> frozenset:
+    """TrainingConfig.defer_roles -> the engine's role set ("all" or a comma list)."""
+    from ..models.engine import GPTEngine
+    if text.strip() in ("", "all"):
+        return frozenset(GPTEngine.ROLES)
+    roles = frozenset(r.strip() for r in text.split(",") if r.strip())
+    bad = roles - set(GPTEngine.ROLES)
+    if bad:
+        raise ValueError(f"defer_roles: unknown roles {sorted(bad)} (choose from {GPTEngine.ROLES})")
+    return roles
+
+
 def build_parser() -> argparse.ArgumentParser:
     p = argparse.ArgumentParser(description="MI355X DDP trainer (reference-compatible CLI)")
     p.add_argument("--model_size", type=str, default="small", choices=["small", "medium", "large", "xl"])
@@ -302,8 +318,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--metrics_jsonl", type=str, default=None)
     p.add_argument("--no_final_save", action="store_true")
     p.add_argument("--memory_lean", action="store_true",
-                   help="weight gradients in each micro-step chain's own backward (no deferred-wgrad slot "
-                        "buffers, no window-wide dlogits): ~1/3 of the peak memory at a few %% lower throughput")
+                   help="defer only the small-operand weight gradients (qkv, o) to the end of the accumulation "
+                        "window; gate/up, down and lm_head run in each micro-step chain's own backward (no "
+                        "[GA*M, 2I] slot buffers, no window-wide dlogits): ~2/3 of the peak memory")
     return p
 
 
@@ -334,7 +351,7 @@ def main(argv=None):
     if args.seq_len:
         model_config.max_seq_len = args.seq_len
     if args.memory_lean:
-        tc.defer_wgrad = False
+        tc.defer_roles = LEAN_DEFER_ROLES
 
     trainer = DistributedTrainer(model_config, tc)
     if tc.resume_from:

@@ -79,26 +79,43 @@ def test_trainer_pipelined_step_matches_sequential():
     assert torch.allclose(res[0][1], res[1][1], atol=1e-7, rtol=1e-6)
 
 
-def test_trainer_memory_lean_matches_deferred():
-    """--memory_lean (defer_wgrad=False: each pipelined chain runs its own weight
-    gradients, no slot buffers) trains like the default deferred schedule (same sums in
-    another order: allclose, not bitwise)."""
+@pytest.mark.parametrize("recompute", [False, True])
+def test_trainer_memory_lean_matches_deferred(recompute):
+    """Per-role deferral: --memory_lean (defer_roles 'qkv,o': gate/up, down and lm_head
+    weight gradients in each pipelined chain's own backward), single roles, and no
+    deferral at all (defer_wgrad=False, no slot buffers) train like the default deferred
+    schedule (same sums in another order: allclose, not bitwise)."""
     from distributed_llm_trainer_amd.training.configs import TrainingConfig
-    from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
+    from distributed_llm_trainer_amd.training.ddp_trainer import LEAN_DEFER_ROLES, DistributedTrainer
     torch.manual_seed(14)
     data = torch.randint(0, 256, (8, 32))
     res = []
-    for defer in (True, False):
+    variants = [(True, "all"), (True, LEAN_DEFER_ROLES), (True, "gu,head"), (True, "down"), (False, "all")]
+    for defer, roles in variants:
         tc = TrainingConfig(batch_size=2, gradient_accumulation_steps=4, warmup_steps=2, max_steps=10,
-                            defer_wgrad=defer)
-        tr = DistributedTrainer(tiny(), tc)
+                            defer_wgrad=defer, defer_roles=roles)
+        cfg = tiny()
+        cfg.gradient_checkpointing = recompute
+        tr = DistributedTrainer(cfg, tc)
         losses = [tr.train_step({"input_ids": data})["loss"] for _ in range(3)]
         res.append((losses, tr.store.flat.clone()))
+        slots = {name for (_, name) in tr.model.engine._slots}
         if not defer:
-            assert not tr.model.engine._slots  # nothing deferred, no slot buffers
-    for a, b in zip(res[0][0], res[1][0]):
-        assert abs(a - b) < 1e-5
-    assert torch.allclose(res[0][1], res[1][1], atol=1e-6, rtol=1e-5)
+            assert not slots  # nothing deferred, no slot buffers
+        elif roles == LEAN_DEFER_ROLES:
+            assert slots == {"n1", "dqkv", "o", "da"}, slots
+    for losses, flat in res[1:]:
+        for a, b in zip(res[0][0], losses):
+            assert abs(a - b) < 1e-5
+        assert torch.allclose(res[0][1], flat, atol=1e-6, rtol=1e-5)
+
+
+def test_defer_roles_parse():
+    from distributed_llm_trainer_amd.training.ddp_trainer import parse_defer_roles
+    assert parse_defer_roles("all") == {"qkv", "o", "gu", "down", "head"}
+    assert parse_defer_roles(" qkv , o") == {"qkv", "o"}
+    with pytest.raises(ValueError):
+        parse_defer_roles("qkv,mlp")
 
 
 def test_packed_qkv_reference_matches_split():
