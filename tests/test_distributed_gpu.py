@@ -108,11 +108,12 @@ def _forced(rank, world, mode):
     unit all-gather / reduce-scatter anyway (the multi-GPU code path on one GPU)."""
     from distributed_llm_trainer_amd.models.config import GPTConfig
     import torch.distributed as dist
-    if mode == "ddp":
+    if mode.startswith("ddp"):
         from distributed_llm_trainer_amd.training.configs import TrainingConfig
-        from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
+        from distributed_llm_trainer_amd.training.ddp_trainer import LEAN_DEFER_ROLES, DistributedTrainer
         tc = TrainingConfig(batch_size=2, gradient_accumulation_steps=4, warmup_steps=1, max_steps=100,
-                            learning_rate=1e-3, bucket_cap_mb=1.0)
+                            learning_rate=1e-3, bucket_cap_mb=1.0,
+                            defer_roles=LEAN_DEFER_ROLES if mode == "ddp_lean" else "all")
         tr = DistributedTrainer(GPTConfig(**TINY), tc)
     else:
         from distributed_llm_trainer_amd.training.configs import FSDPConfig, FSDPTrainingConfig
@@ -123,23 +124,24 @@ def _forced(rank, world, mode):
     assert tr.device.type == "cuda" and dist.get_backend() == "nccl"
     for s in range(STEPS):
         tr.train_step({"input_ids": torch.cat([_data(s, 0), _data(s, 1)])})
-    launched = tr.ddp.launched if mode == "ddp" else -1
-    sd = tr._full_state() if mode != "ddp" else {"flat": tr.store.flat}
+    launched = tr.ddp.launched if mode.startswith("ddp") else -1
+    sd = tr._full_state() if mode == "fsdp" else {"flat": tr.store.flat}
     return {k: v.detach().float().cpu().clone() for k, v in sd.items() if "rotary" not in k}, launched
 
 
-@pytest.mark.parametrize("mode", ["ddp", "fsdp"])
+@pytest.mark.parametrize("mode", ["ddp", "ddp_lean", "fsdp"])
 def test_rccl_forced_collectives_one_rank(mode):
     """RCCL kernels launched from the weight-gradient / pipeline streams, with the
     bucket and unit schedules of a multi-GPU run: a 1-rank sum is the identity, so the
-    parameters must equal the run without collectives bit for bit."""
+    parameters must equal the run without collectives bit for bit.  ddp_lean: per-role
+    deferral (bucket hooks issued after both the side-stream and the per-chain wgrads)."""
     # timing-free GEMM choices, so the two processes run the same kernels
     env = {"DLT_FORCE_CPU": None, "DLT_BACKEND": "nccl", "DLT_GEMM_TUNE": "0", "DLT_WGRAD_SPLITK": "0",
-           "DLT_GEMM_TN": "0", "DLT_GEMM_FUSED": "0"}
+           "DLT_GEMM_TN": "0", "DLT_GEMM_FUSED": "0", "DLT_WGRAD_HAND": "0"}
     a, _ = run_multiprocess(_forced, world=1, args=(mode,), env=env, timeout=240)[0]
     b, launched = run_multiprocess(_forced, world=1, args=(mode,), env={**env, "DLT_FORCE_COLLECTIVES": "1"},
                                    timeout=240)[0]
-    if mode == "ddp":
+    if mode.startswith("ddp"):
         assert launched > 2
     for k in a:
         assert torch.equal(a[k], b[k]), (k, (a[k] - b[k]).abs().max().item())
