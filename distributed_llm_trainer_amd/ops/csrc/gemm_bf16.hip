@@ -120,6 +120,7 @@ __device__ __forceinline__ int gb_bmap(int r, int I) {
 
 // 4 fp32 -> 4 bf16 (RNE) as two v_cvt_pk_bf16_f32; and back (exact)
 typedef __bf16 gb_bf16x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t gb_u32x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint2 gb_pack(const floatx4_t& v) {
   return __builtin_bit_cast(uint2, __builtin_convertvector(v, gb_bf16x4_t));
 }
@@ -463,8 +464,12 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
             y[h] = sw[1];
           }
           const int t = 2 * p + (lq & 1);
-          *reinterpret_cast<uint4*>(crow + gb_ncol<BN, EPI>(wn, t, ep.I) + (lq >> 1) * 8) =
-              uint4{x[0], x[1], y[0], y[1]};
+          gb_u32x4_t* cp = reinterpret_cast<gb_u32x4_t*>(crow + gb_ncol<BN, EPI>(wn, t, ep.I) + (lq >> 1) * 8);
+          const gb_u32x4_t cv = {x[0], x[1], y[0], y[1]};
+          if (flags & 128)  // nontemporal (streaming) C stores
+            __builtin_nontemporal_store(cv, cp);
+          else
+            *cp = cv;
         }
       }
       if (flags & 32) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
