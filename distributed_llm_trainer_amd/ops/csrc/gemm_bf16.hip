@@ -497,7 +497,9 @@ DLT_API int dlt_gemm_bf16_tn(const bf16_t* A, const bf16_t* B, bf16_t* C, int M,
   if (!gb_shape_ok(M, N, K, lda, ldb, ldc) || N % 192) return -1;
   const int ntiles = (M / 256) * (N / 192);
   GbEpi ep{};
-  k_gemm_bf16<192, GB_EPI_STORE><<<gb_grid(ntiles), 512, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, ep);
+  // flags & 256: one tile per workgroup (grid = tiles) instead of the persistent grid
+  const int grid = (flags & 256) ? ((ntiles + 7) & ~7) : gb_grid(ntiles);
+  k_gemm_bf16<192, GB_EPI_STORE><<<grid, 512, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, ep);
   DLT_CHECK_LAUNCH();
 }
 
