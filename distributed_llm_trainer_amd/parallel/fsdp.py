@@ -433,8 +433,9 @@ class FSDPRuntime(ParamProvider):
             # the norm-weight gradients (fp32 side buffer) into the bf16 send buffer
             H = self.cfg.hidden_size
             p = f"layers.{uid}."
-            self._view(u, u.full_grad, p + "input_layernorm.weight").copy_(u.norm_grad[:H])
-            self._view(u, u.full_grad, p + "post_attention_layernorm.weight").copy_(u.norm_grad[H:])
+            torch._foreach_copy_([self._view(u, u.full_grad, p + "input_layernorm.weight"),
+                                  self._view(u, u.full_grad, p + "post_attention_layernorm.weight")],
+                                 [u.norm_grad[:H], u.norm_grad[H:]])  # one multi-tensor launch
             u.norm_grad = None
         do_reduce = self.sync or self.sync_every_micro_step
         if do_reduce:
