@@ -98,40 +98,18 @@ __device__ __forceinline__ bf16x8_t gw_frag(uint32_t img_lane_k, int s) {
   return __builtin_bit_cast(bf16x8_t, c);
 }
 
-namespace {
-}  // namespace
-
-__global__ __launch_bounds__(512, 1) void k_gemm_wgrad(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X,
-                                                       float* __restrict__ out, int T, int Nr, int Nc, int ldy,
-                                                       int ldx, int splits, int accumulate) {
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * GW_BUF];
+// One (256-row x 192-column dW tile, K-tile range) segment: prologue, the 8-phase main
+// loop over K-tiles [kt0, kt0 + nk) (nk even >= 2), epilogue into dst (row stride ldd;
+// accumulate: dst += acc, else dst = acc).  Ends with every wave past its last LDS read,
+// so a workgroup may run segments back to back (stream-K).
+__device__ __forceinline__ void gw_segment(bf16_t* lds, const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X,
+                                           int r0, int c0, int kt0, int nk, bool half_tile, int ldy, int ldx,
+                                           float* __restrict__ dst, int ldd, bool accumulate) {
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int half = wid >> 2;
   const int wm = wid & 3, wn = wid >> 2;
   const int l16 = lane & 15, lq = lane >> 4;
-
-  // workgroup -> (row tile, split, column tile), XCD-aware: the dispatcher deals workgroup
-  // ids round-robin to the 8 XCDs, so ids i, i + 8, ... share an XCD's L2.  A unit u =
-  // (row tile, split) reads one [T / splits, 256] slab of dY, which every column tile of
-  // that row needs: the ntc column tiles of unit u are ids 8 * (ntc * (u / 8) + c) + u % 8,
-  // all on XCD u % 8 and dispatched together, so the slab is fetched from HBM once, not
-  // ntc times (the 3.3 GB dlogits slab of the lm_head gradient was read 4x before).
-  // The grid is padded to whole groups of 8 units; padding workgroups exit at once.
-  const int ntc = Nc / 192;
-  const int nunits = ((Nr + 255) / 256) * splits;
-  const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3;
-  const int u = (q / ntc) * 8 + xcd;
-  if (u >= nunits) return;  // padding (uniform over the workgroup, before any barrier)
-  const int split = u % splits;
-  const int r0 = (u / splits) * 256, c0 = (q % ntc) * 192;
-  // Nr % 256 == 128 (the 50304-row lm_head / embedding gradient): the last row tile has
-  // 128 valid dW rows -- its other half re-reads valid columns (no out-of-bounds reads
-  // at the end of dY) and stores nothing (wm >= 2 is wave-uniform)
-  const bool half_tile = r0 + 256 > Nr;
-  const int npair = T / (2 * GW_BK);
-  const int p0 = (int)(((long)split * npair) / splits), p1 = (int)(((long)(split + 1) * npair) / splits);
-  const int kt0 = 2 * p0, nk = 2 * (p1 - p0);  // K-tiles [kt0, kt0 + nk), nk even >= 2
 
   // images of buffer b (element offsets into lds): A0, A1, B0, B1.  DMA destinations are
   // LDS pointers; the asm transposed reads take the 32-bit LDS address (the low word of
@@ -323,13 +301,12 @@ __global__ __launch_bounds__(512, 1) void k_gemm_wgrad(const bf16_t* __restrict_
   }
   if (half == 0) __builtin_amdgcn_s_barrier();
 
-  // epilogue: acc[nt][mt] = D[n][m]: lane owns dW row r0 + wm*64 + mt*16 + l16 and the 4
-  // consecutive columns c0 + wn*96 + nt*16 + lq*4 .. +3 (one float4)
-  float* const dst = out + (accumulate ? 0 : (size_t)split * Nr * Nc);
-  if (half_tile && wm >= 2) return;  // rows past Nr (wave-uniform; no barrier follows)
+  // epilogue: acc[nt][mt] = D[n][m]: lane owns tile row wm*64 + mt*16 + l16 and the 4
+  // consecutive columns wn*96 + nt*16 + lq*4 .. +3 (one float4)
+  if (half_tile && wm >= 2) return;  // rows past Nr (wave-uniform; no barrier follows in this segment)
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) {
-    float* row = dst + (size_t)(r0 + wm * 64 + mt * 16 + l16) * Nc + c0 + wn * 96 + lq * 4;
+    float* row = dst + (size_t)(wm * 64 + mt * 16 + l16) * ldd + wn * 96 + lq * 4;
 #pragma unroll
     for (int nt = 0; nt < 6; ++nt) {
       float4* p = reinterpret_cast<float4*>(row + nt * 16);
@@ -344,6 +321,146 @@ __global__ __launch_bounds__(512, 1) void k_gemm_wgrad(const bf16_t* __restrict_
       *p = v;
     }
   }
+}
+
+__global__ __launch_bounds__(512, 1) void k_gemm_wgrad(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X,
+                                                       float* __restrict__ out, int T, int Nr, int Nc, int ldy,
+                                                       int ldx, int splits, int accumulate) {
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * GW_BUF];
+  // workgroup -> (row tile, split, column tile), XCD-aware: the dispatcher deals workgroup
+  // ids round-robin to the 8 XCDs, so ids i, i + 8, ... share an XCD's L2.  A unit u =
+  // (row tile, split) reads one [T / splits, 256] slab of dY, which every column tile of
+  // that row needs: the ntc column tiles of unit u are ids 8 * (ntc * (u / 8) + c) + u % 8,
+  // all on XCD u % 8 and dispatched together, so the slab is fetched from HBM once, not
+  // ntc times (the 3.3 GB dlogits slab of the lm_head gradient was read 4x before).
+  // The grid is padded to whole groups of 8 units; padding workgroups exit at once.
+  const int ntc = Nc / 192;
+  const int nunits = ((Nr + 255) / 256) * splits;
+  const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3;
+  const int u = (q / ntc) * 8 + xcd;
+  if (u >= nunits) return;  // padding (uniform over the workgroup, before any barrier)
+  const int split = u % splits;
+  const int r0 = (u / splits) * 256, c0 = (q % ntc) * 192;
+  // Nr % 256 == 128 (the 50304-row lm_head / embedding gradient): the last row tile has
+  // 128 valid dW rows -- its other half re-reads valid columns (no out-of-bounds reads
+  // at the end of dY) and stores nothing (wm >= 2 is wave-uniform)
+  const bool half_tile = r0 + 256 > Nr;
+  const int npair = T / (2 * GW_BK);
+  const int p0 = (int)(((long)split * npair) / splits), p1 = (int)(((long)(split + 1) * npair) / splits);
+  float* const dst = out + (accumulate ? 0 : (size_t)split * Nr * Nc) + (size_t)r0 * Nc + c0;
+  gw_segment(lds, dY, X, r0, c0, 2 * p0, 2 * (p1 - p0), half_tile, ldy, ldx, dst, Nc, accumulate != 0);
+}
+
+// ---------------------------------------------------------------- stream-K (round 3)
+// The split-K grid above runs tiles x splits workgroups in whole rounds of 256, each
+// round ending in a chip-wide burst of fp32 partial stores, and writes s full partial
+// copies of dW for the fixed-order sum.  Stream-K instead gives each of G = Gc x ntc
+// resident workgroups an equal contiguous share of the (row tile, 128-token pair)
+// iteration space of ONE column tile c (column-major over c, so the ntc workgroups with
+// the same share index g read the same dY rows at the same time -- they are dispatched
+// together on one XCD, ids 8 * (ntc * (g / 8) + c) + g % 8, as above).  A share crossing
+// row tiles runs one segment per row tile: a segment covering a whole tile accumulates
+// straight into dW, a partial one writes its fp32 tile to its slot part[c][g][j] (j = row
+// tile - the share's first row tile), and k_wgrad_sk_fix adds the slots of every split
+// tile into dW in increasing g -- a fixed order, bitwise reproducible, no atomics.
+struct GwSk {
+  int npair, nrt, Wc, Gc, maxseg;
+  __device__ __forceinline__ long s_of(int g) const { return (long)g * Wc / Gc; }  // first iteration of share g
+  // share containing iteration i
+  __device__ __forceinline__ int g_of(long i) const {
+    int g = (int)((i * Gc) / Wc);
+    while (g + 1 < Gc && s_of(g + 1) <= i) ++g;
+    while (g > 0 && s_of(g) > i) --g;
+    return g;
+  }
+};
+
+__global__ __launch_bounds__(512, 1) void k_gemm_wgrad_sk(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X,
+                                                          float* __restrict__ dW, float* __restrict__ part, int Nr,
+                                                          int Nc, int ldy, int ldx, GwSk sk) {
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * GW_BUF];
+  const int ntc = Nc / 192;
+  const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3;
+  const int c = q % ntc, g = (q / ntc) * 8 + xcd;
+  if (g >= sk.Gc) return;  // padding (uniform, before any barrier)
+  const int c0 = c * 192;
+  const long e = sk.s_of(g + 1);
+  long i = sk.s_of(g);
+  const int rt_first = (int)(i / sk.npair);
+  while (i < e) {  // wave-uniform
+    const int rt = (int)(i / sk.npair), p0 = (int)(i - (long)rt * sk.npair);
+    const int p1 = (int)min((long)sk.npair, p0 + (e - i));
+    const int r0 = rt * 256;
+    const bool whole = p0 == 0 && p1 == sk.npair;
+    float* dst = whole ? dW + (size_t)r0 * Nc + c0
+                       : part + (((size_t)c * sk.Gc + g) * sk.maxseg + (rt - rt_first)) * (256 * 192);
+    gw_segment(lds, dY, X, r0, c0, 2 * p0, 2 * (p1 - p0), r0 + 256 > Nr, ldy, ldx, dst, whole ? Nc : 192, whole);
+    i += p1 - p0;
+  }
+}
+
+// dW tile (rt, c) += sum over the shares g_lo..g_hi that split it of their slots, in
+// increasing g.  Grid: (12, tiles); each block sums 1/12 of the tile (4096 floats).
+__global__ __launch_bounds__(256) void k_wgrad_sk_fix(const float* __restrict__ part, float* __restrict__ dW, int Nr,
+                                                      int Nc, GwSk sk) {
+  const int ntc = Nc / 192;
+  const int tile = blockIdx.y, rt = tile / ntc, c = tile - rt * ntc;
+  const long i0 = (long)rt * sk.npair, i1 = i0 + sk.npair - 1;
+  const int g_lo = sk.g_of(i0), g_hi = sk.g_of(i1);
+  if (g_lo == g_hi) return;  // one share ran the whole tile into dW
+  const int rows = min(256, Nr - rt * 256);
+  for (int k = blockIdx.x * 256 + threadIdx.x; k < 256 * 192 / 4; k += gridDim.x * 256) {
+    const int r = (k * 4) / 192, col = (k * 4) % 192;
+    if (r >= rows) break;  // k grows with r: the rest of this thread's elements are past Nr too
+    float4* d = reinterpret_cast<float4*>(dW + (size_t)(rt * 256 + r) * Nc + c * 192 + col);
+    float4 a = *d;
+    for (int g = g_lo; g <= g_hi; ++g) {
+      const int j = rt - (int)(sk.s_of(g) / sk.npair);
+      const float4 p = reinterpret_cast<const float4*>(part + (((size_t)c * sk.Gc + g) * sk.maxseg + j) * (256 * 192))[k];
+      a.x += p.x;
+      a.y += p.y;
+      a.z += p.z;
+      a.w += p.w;
+    }
+    *d = a;
+  }
+}
+
+static inline GwSk gw_sk_plan(int T, int Nr, int Nc, int Gc_req) {
+  GwSk sk{};
+  sk.npair = T / 128;
+  sk.nrt = (Nr + 255) / 256;
+  sk.Wc = sk.nrt * sk.npair;
+  const int ntc = Nc / 192;
+  int Gc = Gc_req > 0 ? Gc_req : 256 / ntc;
+  Gc = Gc < 1 ? 1 : (Gc > sk.Wc ? sk.Wc : Gc);
+  sk.Gc = Gc;
+  // a share of ceil(Wc / Gc) iterations touches at most ceil(share / npair) + 1 row tiles
+  const int share = (sk.Wc + Gc - 1) / Gc;
+  sk.maxseg = (share + sk.npair - 1) / sk.npair + 1;
+  return sk;
+}
+
+// Floats of scratch the stream-K weight gradient needs (0 = shape does not tile).
+DLT_API long dlt_gemm_wgrad_sk_scratch(int T, int Nr, int Nc, int Gc) {
+  if (T <= 0 || T % 128 || Nr % 128 || Nc % 192) return 0;
+  const GwSk sk = gw_sk_plan(T, Nr, Nc, Gc);
+  return (long)(Nc / 192) * sk.Gc * sk.maxseg * 256 * 192;
+}
+
+// dW[Nr, Nc] (fp32) += dY[T, Nr]^T . X[T, Nc], stream-K over Gc shares per column tile
+// (Gc <= 0: 256 / column tiles, one workgroup per CU); `part` holds
+// dlt_gemm_wgrad_sk_scratch() floats.  Deterministic (fixed-order fixup).
+DLT_API int dlt_gemm_wgrad_sk(const bf16_t* dY, const bf16_t* X, float* dW, float* part, int T, int Nr, int Nc,
+                              int ldy, int ldx, int Gc, hipStream_t st) {
+  if (T <= 0 || T % 128 || Nr % 128 || Nc % 192 || (ldy | ldx) % 8 || !dW || !part) return -1;
+  const GwSk sk = gw_sk_plan(T, Nr, Nc, Gc);
+  const int ntc = Nc / 192;
+  k_gemm_wgrad_sk<<<((sk.Gc + 7) / 8) * 8 * ntc, 512, 0, st>>>(dY, X, dW, part, Nr, Nc, ldy, ldx, sk);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  k_wgrad_sk_fix<<<dim3(12, sk.nrt * ntc), 256, 0, st>>>(part, dW, Nr, Nc, sk);
+  DLT_CHECK_LAUNCH();
 }
 
 // dW[Nr, Nc] (fp32) += dY[T, Nr]^T . X[T, Nc].  splits == 1: accumulated in place; splits

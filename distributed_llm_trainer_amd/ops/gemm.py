@@ -396,7 +396,8 @@ class HipGemm:
         out.update({f"{k[0]} M{k[1]}xN{k[2]}xK{k[3]}": ("fused gemm_bf16" if c else "unfused (linear + kernel)")
                     for k, c in self._choice.items() if len(k) == 4})
         out.update({f"wgrad{' (bf16 out)' if len(key) == 4 else ''} M{key[0]}xN{key[1]}xK{key[2]}":
-                    (f"hand-written gemm_wgrad x{-s}" if s < 0 else
+                    ("hand-written gemm_wgrad stream-K" if s == self.STREAMK else
+                     f"hand-written gemm_wgrad x{-s}" if s < 0 else
                      f"hipBLASLt split-K x{s}" if s > 1 else "hipBLASLt plain")
                     for key, s in self._splitk.items()})
         return out
@@ -451,6 +452,9 @@ class HipGemm:
             raise RuntimeError(f"hand wgrad cannot tile {M}x{N}x{K}")
         hip.splitk_sum_bf16(part, dw2)
 
+    # splitk plan value of the stream-K hand-written weight gradient (hip.gemm_wgrad_sk)
+    STREAMK = -1024
+
     def _run_wgrad(self, dw2, dy, x, s, to_bf16):
         """One weight-gradient route: s = 1 hipBLASLt plain (beta 1 into fp32, or beta 0
         with a bf16 D), s > 1 hipBLASLt split-K, s < 0 the hand-written kernel with -s
@@ -458,8 +462,11 @@ class HipGemm:
         from . import hip
         M, N = dy.shape
         K = x.shape[1]
-        if s < 0:
-            self._wgrad_hand(dw2, dy, x, -s, to_bf16=to_bf16)
+        if s == self.STREAMK and not to_bf16:
+            if not hip.gemm_wgrad_sk(dw2, dy, x):
+                raise RuntimeError(f"stream-K wgrad cannot tile {M}x{N}x{K}")
+        elif s < 0:
+            self._wgrad_hand(dw2, dy, x, -s if s != self.STREAMK else 8, to_bf16=to_bf16)
         elif s > 1 and to_bf16:
             ms = M // s
             lx, ly = _rowmajor(x), _rowmajor(dy)
@@ -495,6 +502,8 @@ class HipGemm:
             tiles = ((N + 255) // 256) * (K // 192)
             hs = {max(1, (256 * r) // tiles) for r in (1, 2, 3)} | {2, 3, 4, 8, 16}
             cands += [-h for h in sorted(hs) if h <= min(64, M // 128) and (h == 1 or h * N * K * 4 <= 1 << 30)]
+            if not to_bf16:  # stream-K (fp32 accumulate only)
+                cands.append(self.STREAMK)
         if (not (self._splitk_on or hand) or not cands or torch.cuda.is_current_stream_capturing()):
             self._splitk[key] = 1
             return 1

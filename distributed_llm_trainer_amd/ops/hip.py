@@ -55,6 +55,8 @@ _SIGS = {
     "dlt_cast_bf16": [c_void_p, c_void_p, c_int64, c_void_p],
     "dlt_add_bf16_f32": [c_void_p, c_void_p, c_int64, c_void_p],
     "dlt_gemm_wgrad": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "dlt_gemm_wgrad_sk": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+                          c_void_p],
     "dlt_scale_bf16": [c_void_p, c_void_p, ctypes.c_long, c_void_p, c_void_p],
     "dlt_gemm_bf16_tn": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "dlt_gemm_bf16_qkv_rope": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
@@ -102,6 +104,8 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = argt
             fn.restype = c_int
+        L.dlt_gemm_wgrad_sk_scratch.argtypes = [c_int, c_int, c_int, c_int]
+        L.dlt_gemm_wgrad_sk_scratch.restype = ctypes.c_long
         _LIB = L
     return _LIB
 
@@ -673,6 +677,28 @@ def gemm_wgrad(dw: Optional[torch.Tensor], dy: torch.Tensor, x: torch.Tensor, sp
                               T, Nr, Nc, dy.stride(0), x.stride(0), splits, _stream()), "gemm_wgrad")
     if splits > 1 and dw is not None:
         _chk(lib().dlt_splitk_acc(_p(part), _p(dw), Nr * Nc, splits, _stream()), "splitk_acc")
+    return True
+
+
+def gemm_wgrad_sk(dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, shares: int = 0) -> bool:
+    """dw[Nr,Nc] (fp32) += dy[T,Nr]^T @ x[T,Nc], stream-K form of the hand-written kernel
+    (csrc/gemm_wgrad.hip k_gemm_wgrad_sk): one resident workgroup per CU walks an equal
+    share of (row tile, token pair) work of one column tile; tiles split between shares
+    are summed into dw in fixed share order (bitwise reproducible).  Pays off when a
+    share is a sizable part of a tile (gate/up 6144 x 768 and lm_head 50304 x 768 at
+    T = 32768: 275 / 2273 us vs 312 / 2422 for the best split-K, profiles/r3_wgrad.md).
+    Returns False when the shape does not tile."""
+    T, Nr = dy.shape
+    Nc = x.shape[1]
+    if not wgrad_fits(T, Nr, Nc) or dy.stride(1) != 1 or x.stride(1) != 1 or dy.stride(0) % 8 or x.stride(0) % 8:
+        return False
+    _req(dw, torch.float32, "wgrad_sk.dw", Nr * Nc)
+    if dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16 or x.shape[0] != T:
+        raise ValueError("gemm_wgrad_sk: bf16 dy[T,Nr] / x[T,Nc] expected")
+    n = int(lib().dlt_gemm_wgrad_sk_scratch(T, Nr, Nc, shares))
+    part = torch.empty(n, device=dw.device, dtype=torch.float32)
+    _chk(lib().dlt_gemm_wgrad_sk(_p(dy), _p(x), _p(dw), _p(part), T, Nr, Nc, dy.stride(0), x.stride(0), shares,
+                                 _stream()), "gemm_wgrad_sk")
     return True
 
 

@@ -441,6 +441,44 @@ def test_gemm_wgrad_kernel(T, Nr, Nc):
     assert not hip.gemm_wgrad(base, dy[:, :64], x), "untileable shape must be refused"
 
 
+@pytest.mark.parametrize("T,Nr,Nc,shares", [(32768, 6144, 768, 0), (4096, 2304, 768, 0), (2048, 384, 192, 5),
+                                            (8192, 50304, 768, 0), (1024, 256, 192, 3), (4096, 768, 3072, 7)])
+def test_gemm_wgrad_stream_k(T, Nr, Nc, shares):
+    """Stream-K weight gradient (k_gemm_wgrad_sk + the fixed-order fixup): accumulates
+    into dw like the split-K kernel, matches the fp32 reference on the whole output
+    (shares crossing row tiles, whole tiles written straight into dw, the half row tile
+    of Nr % 256 == 128), and is bitwise repeatable."""
+    torch.manual_seed(1)
+    dy = torch.randn(T, Nr, device=DEV).bfloat16()
+    x = torch.randn(T, Nc, device=DEV).bfloat16()
+    base = torch.randn(Nr, Nc, device=DEV)
+    ref = base + dy.float().t() @ x.float()
+    dw = base.clone()
+    assert hip.gemm_wgrad_sk(dw, dy, x, shares)
+    _close(dw, ref, 1e-3 * T ** 0.5, 1e-4, f"wgrad stream-K {T}x{Nr}x{Nc}")
+    dw2 = base.clone()
+    assert hip.gemm_wgrad_sk(dw2, dy, x, shares)
+    assert torch.equal(dw, dw2), "stream-K wgrad not deterministic"
+    assert not hip.gemm_wgrad_sk(base, dy[:, :64], x), "untileable shape must be refused"
+
+
+def test_planner_stream_k_route():
+    """The planner's stream-K pick (splitk value STREAMK) runs the stream-K kernel for an
+    fp32 accumulator and falls back to the split kernel for a bf16 output."""
+    from distributed_llm_trainer_amd.ops import gemm
+    g = gemm.HipGemm()
+    T, N, K = 4096, 2304, 768
+    dy = torch.randn(T, N, device=DEV).bfloat16()
+    x = torch.randn(T, K, device=DEV).bfloat16()
+    want = dy.float().t() @ x.float()
+    dw = torch.zeros(N, K, device=DEV)
+    g._run_wgrad(dw, dy, x, g.STREAMK, False)
+    _close(dw, want, 1e-3 * T ** 0.5, 1e-4, "planner stream-K fp32")
+    dwb = torch.zeros(N, K, device=DEV, dtype=torch.bfloat16)
+    g._run_wgrad(dwb, dy, x, g.STREAMK, True)
+    _close(dwb.float(), want, 2e-2 * T ** 0.5, 1e-2, "planner stream-K bf16 fallback")
+
+
 @pytest.mark.parametrize("p", [0.0, 0.1])
 def test_attention_fwd_growing_max_rescales(p):
     """Scores rise steeply along the keys, so the running row max grows by far more

@@ -294,10 +294,14 @@ static int wgrad_main(std::vector<int> shp) {
     k_fill<<<1024, 256, 0, st>>>(dY, (size_t)T * Nr, 21);
     k_fill<<<1024, 256, 0, st>>>(X, (size_t)T * Nc, 22);
     const int tiles = ((Nr + 255) / 256) * (Nc / 192);
+    // GW_SPLITS=-1: the stream-K kernel (GW_GC shares per column tile, default 256 / tiles)
     int S = getenv("GW_SPLITS") ? atoi(getenv("GW_SPLITS")) : (256 + tiles / 2) / tiles;
-    if (S < 1) S = 1;
-    CK(hipMalloc(&part, (size_t)S * Nr * Nc * 4));
+    const int Gc = getenv("GW_GC") ? atoi(getenv("GW_GC")) : 0;
+    if (S == 0) S = 1;
+    const size_t nscr = S < 0 ? (size_t)dlt_gemm_wgrad_sk_scratch(T, Nr, Nc, Gc) : (size_t)S * Nr * Nc;
+    CK(hipMalloc(&part, nscr * 4));
     auto hand = [&]() {
+      if (S < 0) return dlt_gemm_wgrad_sk(dY, X, dW, part, T, Nr, Nc, Nr, Nc, Gc, st);
       int rc = dlt_gemm_wgrad(dY, X, dW, part, T, Nr, Nc, Nr, Nc, S, st);
       if (rc == 0 && S > 1) rc = dlt_splitk_acc(part, dW, (long)Nr * Nc, S, st);
       return rc;
@@ -328,6 +332,27 @@ static int wgrad_main(std::vector<int> shp) {
         if (!(d <= maxerr)) maxerr = d;
         maxref = std::fmax(maxref, std::fabs(ref[(size_t)i * Nc + c]));
       }
+    if (S < 0) {  // stream-K: bitwise run-to-run, and the whole dW against the split-K kernel
+      std::vector<float> again((size_t)Nr * Nc), split((size_t)Nr * Nc);
+      CK(hipMemsetAsync(dW, 0, (size_t)Nr * Nc * 4, st));
+      if (hand() != 0) return 1;
+      CK(hipMemcpyAsync(again.data(), dW, again.size() * 4, hipMemcpyDeviceToHost, st));
+      float* p2;
+      CK(hipMalloc(&p2, (size_t)4 * Nr * Nc * 4));
+      CK(hipMemsetAsync(dW2, 0, (size_t)Nr * Nc * 4, st));
+      if (dlt_gemm_wgrad(dY, X, dW2, p2, T, Nr, Nc, Nr, Nc, 4, st) || dlt_splitk_acc(p2, dW2, (long)Nr * Nc, 4, st)) return 1;
+      CK(hipMemcpyAsync(split.data(), dW2, split.size() * 4, hipMemcpyDeviceToHost, st));
+      CK(hipStreamSynchronize(st));
+      CK(hipFree(p2));
+      double md = 0, mr = 0;
+      for (size_t k = 0; k < split.size(); ++k) {
+        const double d = std::fabs((double)again[k] - split[k]);
+        if (!(d <= md)) md = d;
+        mr = std::fmax(mr, std::fabs(split[k]));
+      }
+      printf("  stream-K: %s run to run, whole dW vs split-K x4 max |diff| / max %.1e, scratch %.0f MB\n",
+             memcmp(again.data(), got.data(), got.size() * 4) ? "NOT bitwise" : "bitwise", md / mr, nscr * 4 / 1e6);
+    }
     // hipBLASLt: C[Nc, Nr] (col-major) += op_N(X [Nc, T]) op_T(dY [Nr, T])
     hipblasLtMatmulDesc_t md;
     hipblasLtMatmulDescCreate(&md, HIPBLAS_COMPUTE_32F, HIP_R_32F);
