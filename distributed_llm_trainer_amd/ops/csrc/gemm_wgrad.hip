@@ -400,23 +400,31 @@ __global__ __launch_bounds__(512, 1) void k_gemm_wgrad_sk(const bf16_t* __restri
 }
 
 // dW tile (rt, c) += sum over the shares g_lo..g_hi that split it of their slots, in
-// increasing g.  Grid: (12, tiles); each block sums 1/12 of the tile (4096 floats).
+// increasing g.  Grid: (GW_FIX_SPLIT, tiles); each block sums 1/GW_FIX_SPLIT of the tile.
+// The slot index of every share is computed once per block (64-bit divisions) into LDS.
+constexpr int GW_FIX_SPLIT = 48;
 __global__ __launch_bounds__(256) void k_wgrad_sk_fix(const float* __restrict__ part, float* __restrict__ dW, int Nr,
                                                       int Nc, GwSk sk) {
+  __shared__ int jt[256];
   const int ntc = Nc / 192;
   const int tile = blockIdx.y, rt = tile / ntc, c = tile - rt * ntc;
   const long i0 = (long)rt * sk.npair, i1 = i0 + sk.npair - 1;
   const int g_lo = sk.g_of(i0), g_hi = sk.g_of(i1);
   if (g_lo == g_hi) return;  // one share ran the whole tile into dW
+  const int nsh = g_hi - g_lo + 1;
+  for (int t = threadIdx.x; t < nsh && t < 256; t += 256) jt[t] = rt - (int)(sk.s_of(g_lo + t) / sk.npair);
+  __syncthreads();
   const int rows = min(256, Nr - rt * 256);
+  const float4* pc = reinterpret_cast<const float4*>(part) + ((size_t)c * sk.Gc + g_lo) * sk.maxseg * (256 * 192 / 4);
+  const size_t gstride = (size_t)sk.maxseg * (256 * 192 / 4);  // float4s between consecutive shares' slot 0
   for (int k = blockIdx.x * 256 + threadIdx.x; k < 256 * 192 / 4; k += gridDim.x * 256) {
     const int r = (k * 4) / 192, col = (k * 4) % 192;
     if (r >= rows) break;  // k grows with r: the rest of this thread's elements are past Nr too
     float4* d = reinterpret_cast<float4*>(dW + (size_t)(rt * 256 + r) * Nc + c * 192 + col);
     float4 a = *d;
-    for (int g = g_lo; g <= g_hi; ++g) {
-      const int j = rt - (int)(sk.s_of(g) / sk.npair);
-      const float4 p = reinterpret_cast<const float4*>(part + (((size_t)c * sk.Gc + g) * sk.maxseg + j) * (256 * 192))[k];
+    for (int t = 0; t < nsh; ++t) {
+      const int j = t < 256 ? jt[t] : rt - (int)(sk.s_of(g_lo + t) / sk.npair);
+      const float4 p = pc[t * gstride + (size_t)j * (256 * 192 / 4) + k];
       a.x += p.x;
       a.y += p.y;
       a.z += p.z;
@@ -459,7 +467,7 @@ DLT_API int dlt_gemm_wgrad_sk(const bf16_t* dY, const bf16_t* X, float* dW, floa
   k_gemm_wgrad_sk<<<((sk.Gc + 7) / 8) * 8 * ntc, 512, 0, st>>>(dY, X, dW, part, Nr, Nc, ldy, ldx, sk);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  k_wgrad_sk_fix<<<dim3(12, sk.nrt * ntc), 256, 0, st>>>(part, dW, Nr, Nc, sk);
+  k_wgrad_sk_fix<<<dim3(GW_FIX_SPLIT, sk.nrt * ntc), 256, 0, st>>>(part, dW, Nr, Nc, sk);
   DLT_CHECK_LAUNCH();
 }
 

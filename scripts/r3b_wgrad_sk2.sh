@@ -1,0 +1,12 @@
+#!/bin/bash
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+mkdir -p gpurun_out
+o=gpurun_out/wgrad_sk2.log; : > $o
+run() { echo "== $*" >> $o; env "$@" >> $o 2>&1 || { tail -5 $o; exit 1; }; }
+for shp in "2304 768:7" "768 768:16" "6144 768:8" "768 3072:5" "50304 768:2"; do
+  dims=${shp%%:*}; sp=${shp##*:}
+  for s in $sp; do run GW_SPLITS=$s timeout -k 10 120 tools/cpp/gemm_bench wgrad 32768 $dims; done
+  run GW_SPLITS=-1 timeout -k 10 120 tools/cpp/gemm_bench wgrad 32768 $dims
+done
+grep -E "wgrad T|stream-K" $o
