@@ -532,9 +532,29 @@ class GPTEngine:
     def backward(self, st: _StepState, dloss: torch.Tensor) -> None:
         _drain(self._backward_gen(st, dloss))
 
-    def _backward_gen(self, st: _StepState, dloss: torch.Tensor):
-        """Generator form of :meth:`backward` (yields after every block)."""
+    def _backward_gen(self, st: _StepState, dloss: torch.Tensor, prev: Optional[dict] = None,
+                      mine: Optional[dict] = None):
+        """Generator form of :meth:`backward` (yields after every block).
+
+        ``prev`` / ``mine`` (overlapped backwards, see train_window): the progress events
+        of the previous micro-step's backward, and the dict this backward records its own
+        into -- "norm" after the final-norm weight gradient, layer ``i`` after every
+        gradient layer ``i`` shares with the other micro-steps (norm weights, per-micro-
+        step weight gradients), "embed" after the embedding scatter-add.  Every write
+        into a shared gradient buffer waits for the previous backward's matching event,
+        so the accumulation order -- and every bit of the result -- is the sequential
+        one.  ``prev`` must be fully issued (its events recorded) before this runs."""
         ops, gm, cfg, prov = self.ops, self.gemm, self.cfg, self.provider
+
+        def wait_prev(unit):
+            if prev is not None:
+                torch.cuda.current_stream().wait_event(prev[unit])
+
+        def mark(unit):
+            if mine is not None:
+                ev = torch.cuda.Event()
+                ev.record()
+                mine[unit] = ev
         B, S = st.B, st.S
         L = cfg.num_layers
         ph = self.p_hidden if st.train else 0.0
@@ -560,8 +580,12 @@ class GPTEngine:
             if nf_out is not None:
                 nf_scaled = nf_out.copy_(nf_scaled)
         head_ev = None
+        head_late = None  # overlapped backwards: the per-micro-step head wgrad waits for "embed"
         if not dfr["head"]:
-            gm.wgrad_acc(hg.embed, st.dlogits, nf_scaled)
+            if prev is not None:
+                head_late = (st.dlogits, nf_scaled)
+            else:
+                gm.wgrad_acc(hg.embed, st.dlogits, nf_scaled)
         elif st.last:
             # ONE [Vp, H] wgrad GEMM over all GA*M rows of the window (K = 32768 instead
             # of 4 x 8192), on the weight-gradient stream so it overlaps the layer
@@ -572,11 +596,14 @@ class GPTEngine:
                 ev = torch.cuda.Event()
                 ev.record()
                 side.wait_event(ev)
+                if prev is not None:  # after the previous backward's embedding scatter-add
+                    side.wait_event(prev["embed"])
                 with torch.cuda.stream(side):
                     gm.wgrad_acc(hg.embed, lg_all, nf_all)
                     head_ev = torch.cuda.Event()
                     head_ev.record()
             else:
+                wait_prev("embed")
                 gm.wgrad_acc(hg.embed, lg_all, nf_all)
         st.dlogits = None
         key_last = self._keys(st.micro, L - 1)[2]
@@ -595,7 +622,11 @@ class GPTEngine:
             # embedding (tied with lm_head): scatter-add, then the head gradient hook
             if head_ev is not None:
                 torch.cuda.current_stream().wait_event(head_ev)
+            wait_prev("embed")
+            if head_late is not None:
+                gm.wgrad_acc(hg.embed, *head_late)
             ops.embedding_bwd(st.ids, g_x2n if early_head else g_x2, hg.embed)
+            mark("embed")
             prov.post_backward("head")
 
         def sb(layer, name, n):
@@ -604,13 +635,16 @@ class GPTEngine:
         def full(layer, name, n):
             return self._slot_buf(st, layer, name, M, n, dev)[1]
 
+        wait_prev("norm")
         g_x2, g_d = ops.rmsnorm_bwd(dnf, st.xf, st.rstdf, hw.norm, None, hg.norm,
                                     ph, key_last, dy_scale=dloss, want_ddelta=True, ddelta_out=sb(L - 1, "dd", H))
+        mark("norm")
         del dnf
         cos, sin = self.rope(S, g_x2.device)
 
         for i in reversed(range(L)):
             prov.pre_backward(i)
+            wait_prev(i)
             c = st.caches[i]
             if st.recompute:
                 # Re-run (part of) the layer forward from the saved tensors; masks replay exactly.
@@ -698,6 +732,7 @@ class GPTEngine:
             finally:
                 if side_ctx is not None:
                     side_ctx.__exit__(None, None, None)
+            mark(i)
             yield
         if not early_head:
             head_done()
@@ -735,10 +770,21 @@ class GPTEngine:
         since two backwards may overlap on the GPU.
         Returns the GA micro-step losses (device scalars, unscaled).  Dropout streams,
         numerics and gradients are identical to running the micro-steps one by one.
+
+        Overlapped backwards (flat DDP store, ``DLT_BWD_OVERLAP=1`` default): backward k
+        does not wait for backward k-1 to finish, only -- per shared gradient buffer --
+        for the matching progress event of it (final norm, each layer, the embedding;
+        see _backward_gen), so the two backwards run concurrently a few layers apart,
+        with the sequential accumulation order.  The schedule becomes
+        F0 | B0+F1 | B0+B1 | B1 instead of F0 | B0+F1 | B1 (only the first forward and the
+        tail of the last backward run without a partner).
         """
         GA = len(micro_ids)
         dev = micro_ids[0].device
         cuda = dev.type == "cuda"
+        overlap = (cuda and GA > 1 and getattr(self.provider, "late_post_backward_ok", False)
+                   and os.environ.get("DLT_BWD_OVERLAP", "1") != "0")
+        prog: List[dict] = [dict() for _ in range(GA)]
         self.set_accumulation(0, GA, defer=defer)
         main = pipe = None
         if cuda:
@@ -771,17 +817,19 @@ class GPTEngine:
             losses[0], _, states[0] = _drain(fwd(0))
         for k in range(GA):
             if k == GA - 1:
-                if cuda and GA > 1:
+                if cuda and GA > 1 and not overlap:
                     main.wait_stream(pipe)
                 if before_last is not None:
                     before_last()
-            elif cuda and k > 0:
+            elif cuda and k > 0 and not overlap:
                 # backward k starts after backward k-1 has finished on the other stream:
                 # both add into the same norm / embedding gradients (fixed-order, non-atomic
                 # kernels), so two backwards never overlap -- a backward still overlaps
                 # the next micro-step's forward, which is what the pipelining is for.
                 stream_of(k).wait_stream(stream_of(k - 1))
-            running = [(k, self._backward_gen(states[k], dloss), False)]
+            # overlapped: backward k-1 is fully issued by now (its events exist)
+            ev_args = (prog[k - 1] if k > 0 else None, prog[k]) if overlap else (None, None)
+            running = [(k, self._backward_gen(states[k], dloss, *ev_args), False)]
             states[k] = None
             if k + 1 < GA:
                 running.append((k + 1, fwd(k + 1), True))
@@ -795,6 +843,8 @@ class GPTEngine:
                             running.remove(item)
                             if is_fwd:
                                 losses[j], _, states[j] = stop.value
+        if overlap:  # the optimizer (current stream) must see every backward's gradients
+            main.wait_stream(pipe)
         return losses
 
 
