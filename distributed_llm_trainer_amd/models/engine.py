@@ -529,11 +529,21 @@ class GPTEngine:
             self._side = torch.cuda.Stream(dev)
         return self._side
 
+    def _head_wgrad_buf(self, like: torch.Tensor) -> torch.Tensor:
+        """Persistent fp32 buffer for the window's lm_head weight gradient."""
+        buf = getattr(self, "_lmbuf", None)
+        if buf is None or buf.shape != like.shape or buf.device != like.device or buf.dtype != like.dtype:
+            if buf is not None and buf.is_cuda:
+                torch.cuda.synchronize(buf.device)
+            buf = torch.empty_like(like)
+            self._lmbuf = buf
+        return buf
+
     def backward(self, st: _StepState, dloss: torch.Tensor) -> None:
         _drain(self._backward_gen(st, dloss))
 
     def _backward_gen(self, st: _StepState, dloss: torch.Tensor, prev: Optional[dict] = None,
-                      mine: Optional[dict] = None):
+                      mine: Optional[dict] = None, ready: Optional[list] = None):
         """Generator form of :meth:`backward` (yields after every block).
 
         ``prev`` / ``mine`` (overlapped backwards, see train_window): the progress events
@@ -543,7 +553,10 @@ class GPTEngine:
         step weight gradients), "embed" after the embedding scatter-add.  Every write
         into a shared gradient buffer waits for the previous backward's matching event,
         so the accumulation order -- and every bit of the result -- is the sequential
-        one.  ``prev`` must be fully issued (its events recorded) before this runs."""
+        one.  Each wait is issued after ``prev`` recorded the event (the window scheduler
+        keeps ``prev`` at least one block ahead).  ``ready``: events after the forwards of
+        the window's other micro-steps (streams this backward's window-wide lm_head
+        weight gradient does not otherwise wait for)."""
         ops, gm, cfg, prov = self.ops, self.gemm, self.cfg, self.provider
 
         def wait_prev(unit):
@@ -580,6 +593,7 @@ class GPTEngine:
             if nf_out is not None:
                 nf_scaled = nf_out.copy_(nf_scaled)
         head_ev = None
+        head_add = None  # the window's lm_head weight gradient, added after the scatter-adds
         head_late = None  # overlapped backwards: the per-micro-step head wgrad waits for "embed"
         if not dfr["head"]:
             if prev is not None:
@@ -589,22 +603,28 @@ class GPTEngine:
         elif st.last:
             # ONE [Vp, H] wgrad GEMM over all GA*M rows of the window (K = 32768 instead
             # of 4 x 8192), on the weight-gradient stream so it overlaps the layer
-            # backward; the embedding scatter-add below (same buffer) waits for it.
+            # backward.  It goes to its own buffer, added into the embedding gradient
+            # after the last scatter-add (head_done): the same order in every schedule
+            # (sequential, pipelined, overlapped), so it may run whenever its operands exist.
             lg_all = self._slot_buf(st, "head", "lg", M, hw.lm_head.shape[0], dev)[1]
             nf_all = self._slot_buf(st, "head", "nf", M, H, dev)[1]
+            head_add = self._head_wgrad_buf(hg.embed)
+
+            def issue_head():
+                head_add.zero_()
+                gm.wgrad_acc(head_add, lg_all, nf_all)
             if side is not None:
                 ev = torch.cuda.Event()
                 ev.record()
                 side.wait_event(ev)
-                if prev is not None:  # after the previous backward's embedding scatter-add
-                    side.wait_event(prev["embed"])
+                for e in ready or ():
+                    side.wait_event(e)
                 with torch.cuda.stream(side):
-                    gm.wgrad_acc(hg.embed, lg_all, nf_all)
+                    issue_head()
                     head_ev = torch.cuda.Event()
                     head_ev.record()
             else:
-                wait_prev("embed")
-                gm.wgrad_acc(hg.embed, lg_all, nf_all)
+                issue_head()
         st.dlogits = None
         key_last = self._keys(st.micro, L - 1)[2]
         # The side stream lags the dgrad chain by a few layers' worth of weight-gradient
@@ -626,6 +646,8 @@ class GPTEngine:
             if head_late is not None:
                 gm.wgrad_acc(hg.embed, *head_late)
             ops.embedding_bwd(st.ids, g_x2n if early_head else g_x2, hg.embed)
+            if head_add is not None:
+                hg.embed.add_(head_add)
             mark("embed")
             prov.post_backward("head")
 
@@ -744,9 +766,60 @@ class GPTEngine:
             torch.cuda.current_stream().wait_stream(side)
 
     # ------------------------------------------------------ pipelined window
+    def _window_ffbb(self, micro_ids, micro_targets, dloss, recompute, defer, sync_hook, before_last):
+        """Two-chain window F0 || F1 | B0 || B1 (see train_window)."""
+        dev = micro_ids[0].device
+        self.set_accumulation(0, 2, defer=defer)
+        main = torch.cuda.current_stream(dev)
+        if self._pipe is None:
+            self._pipe = torch.cuda.Stream(dev)
+        p0 = self._pipe
+        self.rope(micro_ids[0].shape[1], dev)
+        self._wgrad_stream(dev)  # created before the fork
+        p0.wait_stream(main)
+        streams = [p0, main]
+        losses: List[Any] = [None, None]
+        states: List[Any] = [None, None]
+        ready: List[Any] = []
+        # forwards: chain 0 first in every round (micro-step numbering = dropout streams)
+        gens = [self._forward_gen(micro_ids[k], micro_targets[k], True, recompute, need_backward=True,
+                                  acc=(k, 2, defer)) for k in range(2)]
+        live = [0, 1]
+        while live:
+            for k in list(live):
+                with torch.cuda.stream(streams[k]):
+                    try:
+                        next(gens[k])
+                    except StopIteration as stop:
+                        live.remove(k)
+                        losses[k], _, states[k] = stop.value
+                        if k == 0:
+                            ev = torch.cuda.Event()
+                            ev.record()
+                            ready.append(ev)
+        prog: List[dict] = [dict(), dict()]
+        bgens = [self._backward_gen(states[0], dloss, None, prog[0]),
+                 self._backward_gen(states[1], dloss, prog[0], prog[1], ready=ready)]
+        states = [None, None]
+        if sync_hook is None and before_last is not None:
+            raise ValueError("the ffbb window schedule needs sync_hook (per-block sync flag)")
+        live = [0, 1]
+        while live:  # B0 always issues its block first: B1's waits find B0's events recorded
+            for k in list(live):
+                if sync_hook is not None:
+                    sync_hook(k == 1)
+                with torch.cuda.stream(streams[k]):
+                    try:
+                        next(bgens[k])
+                    except StopIteration:
+                        live.remove(k)
+        main.wait_stream(p0)
+        return losses
+
     def train_window(self, micro_ids: List[torch.Tensor], micro_targets: List[torch.Tensor],
                      dloss: torch.Tensor, recompute: bool = False,
-                     before_last: Optional[Callable[[], None]] = None, defer: bool = True) -> List[torch.Tensor]:
+                     before_last: Optional[Callable[[], None]] = None, defer: bool = True,
+                     sync_hook: Optional[Callable[[bool], None]] = None) -> List[torch.Tensor]:
         """Forward + backward of a whole gradient-accumulation window.
 
         Schedule (GA = 4):  F0 | B0+F1 | B1+F2 | B2+F3 | B3, where "Bk+Fk+1" issues the
@@ -778,6 +851,14 @@ class GPTEngine:
         with the sequential accumulation order.  The schedule becomes
         F0 | B0+F1 | B0+B1 | B1 instead of F0 | B0+F1 | B1 (only the first forward and the
         tail of the last backward run without a partner).
+
+        Two chains (the headline B8 x GA4 as 2 x 16), ``DLT_WINDOW_SCHED=ffbb`` (default with
+        every weight gradient deferred; ``fb`` = the schedule above): F0 || F1,
+        then B0 || B1 with B1 one block behind B0 (its per-buffer waits, above) -- no
+        phase without a partner chain; chain 0 runs on a stream of its own, the weight
+        gradients on the side stream.  ``sync_hook(last)`` is called before every
+        backward block (the DDP runtime's per-micro-step sync flag; ``before_last`` is not
+        used by this schedule).
         """
         GA = len(micro_ids)
         dev = micro_ids[0].device
@@ -785,6 +866,11 @@ class GPTEngine:
         overlap = (cuda and GA > 1 and getattr(self.provider, "late_post_backward_ok", False)
                    and os.environ.get("DLT_BWD_OVERLAP", "1") != "0")
         prog: List[dict] = [dict() for _ in range(GA)]
+        # ffbb: the default for two chains with every weight gradient deferred (the
+        # memory-lean modes keep fb: both forwards' activations live at once cost ~5 GB)
+        sched = os.environ.get("DLT_WINDOW_SCHED", "ffbb" if self.defer_roles == frozenset(self.ROLES) else "fb")
+        if overlap and GA == 2 and defer and sched == "ffbb":
+            return self._window_ffbb(micro_ids, micro_targets, dloss, recompute, defer, sync_hook, before_last)
         self.set_accumulation(0, GA, defer=defer)
         main = pipe = None
         if cuda:

@@ -181,6 +181,7 @@ class DistributedTrainer:
             losses = self.model.engine.train_window(
                 ids_l, tg_l, dloss, recompute=bool(self.model.gradient_checkpointing),
                 before_last=(lambda: self.ddp.require_sync(True)) if self.ddp is not None else None,
+                sync_hook=self.ddp.require_sync if self.ddp is not None else None,
                 defer=cfg.defer_wgrad)
             range_pop()
             for loss in losses:

@@ -191,6 +191,39 @@ def test_pipelined_window_matches_sequential_gpu(recompute):
         assert torch.equal(g1[n], g2[n]), (n, (g1[n] - g2[n]).abs().max().item())
 
 
+@pytest.mark.parametrize("recompute", [False, True])
+def test_window_ffbb_matches_sequential_gpu(recompute, monkeypatch):
+    """Two-chain window F0 || F1 | B0 || B1 (DLT_WINDOW_SCHED=ffbb: both forwards, then both
+    backwards concurrently, B1 one block behind B0 with per-buffer waits) == the sequential
+    schedule: same losses, bit-identical gradients."""
+    from distributed_llm_trainer_amd.models.engine import shift_targets
+    monkeypatch.setenv("DLT_WINDOW_SCHED", "ffbb")
+    torch.manual_seed(6)
+    base = GPT(_cfg(0.1)).to(DEV)
+    m1, m2 = copy.deepcopy(base), copy.deepcopy(base)
+    e1, e2 = m1.enable_engine(seed=9), m2.enable_engine(seed=9)
+    assert getattr(e2.provider, "late_post_backward_ok", False)
+    m1.gradient_checkpointing = m2.gradient_checkpointing = recompute
+    GA = 2
+    data = torch.randint(0, 1000, (GA, 4, 256), device=DEV)
+    seq = []
+    for j in range(GA):
+        e1.set_accumulation(j, GA, defer=True)
+        _, loss = m1(data[j], labels=data[j])
+        (loss / GA).backward()
+        seq.append(loss.item())
+    flags = []
+    win = e2.train_window([data[j] for j in range(GA)], [shift_targets(data[j]) for j in range(GA)],
+                          torch.full((), 1.0 / GA, device=DEV), recompute=recompute, sync_hook=flags.append)
+    torch.cuda.synchronize()
+    assert flags and flags[0] is False and flags[-1] is True
+    for a, b in zip(seq, win):
+        assert a == b.item(), (seq, [w.item() for w in win])
+    g1, g2 = _grads(m1), _grads(m2)
+    for n in g1:
+        assert torch.equal(g1[n], g2[n]), (n, (g1[n] - g2[n]).abs().max().item())
+
+
 @pytest.mark.parametrize("ac", [True, False])
 def test_fsdp_pipelined_matches_sequential_gpu(ac):
     """FSDP trainer on one GPU: pipelined micro-steps (two HIP streams sharing gathered
