@@ -205,8 +205,16 @@ class GPTEngine:
         self.selective_recompute = os.environ.get("DLT_AC_SELECTIVE", "1") != "0"
         # ... and, within this many bytes of kept GEMM outputs, the packed QKV and gate/up
         # GEMM outputs as well, so the recompute reduces to the norms and SwiGLU (sized for
-        # 288 GB of HBM: GPT-2 small/medium keep both; see _ac_keep)
-        self.ac_budget = float(os.environ.get("DLT_AC_BUDGET_GB", "48")) * 1e9
+        # 288 GB of HBM: GPT-2 small/medium/xl keep both; see _ac_keep)
+        # (default: a third of the GPU's memory -- 96 GB of MI355X's 288 GB: FSDP xl then
+        # keeps both GEMM outputs, 55.6k -> 61.3k tok/s at 68.8 -> 88.6 GB; 48 GB off-GPU)
+        env_budget = os.environ.get("DLT_AC_BUDGET_GB")
+        if env_budget is not None:
+            self.ac_budget = float(env_budget) * 1e9
+        elif torch.cuda.is_available():
+            self.ac_budget = torch.cuda.get_device_properties(torch.cuda.current_device()).total_memory / 3.0
+        else:
+            self.ac_budget = 48e9
         # attention keep-bit masks (1 bit per causal score, two layouts) are kept from the
         # forward for the backward while one micro-step's masks of all layers fit in this
         # budget; beyond it (long context: 3.2 GB per layer at S = 32768, nh 12) the
