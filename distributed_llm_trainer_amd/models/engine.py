@@ -871,13 +871,13 @@ class GPTEngine:
         GA = len(micro_ids)
         dev = micro_ids[0].device
         cuda = dev.type == "cuda"
-        overlap = (cuda and GA > 1 and getattr(self.provider, "late_post_backward_ok", False)
+        overlap = (cuda and GA > 1 and getattr(self.provider, "overlap_backward_ok", False)
                    and os.environ.get("DLT_BWD_OVERLAP", "1") != "0")
         prog: List[dict] = [dict() for _ in range(GA)]
         # ffbb: the default for two chains with every weight gradient deferred (the
         # memory-lean modes keep fb: both forwards' activations live at once cost ~5 GB)
         sched = os.environ.get("DLT_WINDOW_SCHED", "ffbb" if self.defer_roles == frozenset(self.ROLES) else "fb")
-        if overlap and GA == 2 and defer and sched == "ffbb":
+        if overlap and GA == 2 and defer and sched == "ffbb" and getattr(self.provider, "late_post_backward_ok", False):
             return self._window_ffbb(micro_ids, micro_targets, dloss, recompute, defer, sync_hook, before_last)
         self.set_accumulation(0, GA, defer=defer)
         main = pipe = None

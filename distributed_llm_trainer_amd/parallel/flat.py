@@ -83,6 +83,9 @@ class FlatParamStore(ParamProvider):
     side_stream_hooks = True
     # ... and may be delayed to the end of the backward (engine ``main_wgrad_layers``)
     late_post_backward_ok = True
+    # two micro-steps' backwards may run concurrently, ordered per shared gradient buffer by
+    # progress events (GPTEngine.train_window)
+    overlap_backward_ok = True
 
     def __init__(self, model, device, compute_dtype=torch.bfloat16, grad_dtype=torch.float32):
         self.model = model

@@ -95,6 +95,12 @@ class FlatUnit:
 
 
 class FSDPRuntime(ParamProvider):
+    # Overlapped backwards (GPTEngine.train_window): every micro-step gets fresh unit
+    # gradient buffers (layer_grads / head_grads, reduced and dropped in post_backward), the
+    # host issues the two backwards' hooks in sequential order, and the shard gradients
+    # are only accumulated in finish() -- nothing two backwards write is shared.
+    overlap_backward_ok = True
+
     def __init__(self, model, device, sharding_strategy: str = "FULL_SHARD", compute_dtype=torch.bfloat16,
                  reduce_dtype=torch.bfloat16, cpu_offload: bool = False, backward_prefetch: str = "BACKWARD_PRE",
                  limit_all_gathers: bool = True, sync_every_micro_step: bool = True, process_group=None,
