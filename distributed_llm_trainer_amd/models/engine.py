@@ -877,7 +877,9 @@ class GPTEngine:
         # ffbb: the default for two chains with every weight gradient deferred (the
         # memory-lean modes keep fb: both forwards' activations live at once cost ~5 GB)
         sched = os.environ.get("DLT_WINDOW_SCHED", "ffbb" if self.defer_roles == frozenset(self.ROLES) else "fb")
-        if overlap and GA == 2 and defer and sched == "ffbb" and getattr(self.provider, "late_post_backward_ok", False):
+        # (flat DDP store only: an FSDP unit's per-micro-step gradient buffers are handed out
+        # by the provider in backward order, so two backwards must not be issued interleaved)
+        if overlap and GA == 2 and sched == "ffbb" and getattr(self.provider, "late_post_backward_ok", False):
             return self._window_ffbb(micro_ids, micro_targets, dloss, recompute, defer, sync_hook, before_last)
         self.set_accumulation(0, GA, defer=defer)
         main = pipe = None

@@ -156,7 +156,8 @@ class FSDPTrainer:
             losses = eng.train_window(ids_l, [shift_targets(x) for x in ids_l],
                                       torch.full((), ls / chains, dtype=torch.float32, device=self.device),
                                       recompute=bool(self.model.gradient_checkpointing),
-                                      before_last=lambda: rt.require_sync(True), defer=defer)
+                                      before_last=lambda: rt.require_sync(True), defer=defer,
+                                      sync_hook=rt.require_sync)
             for loss in losses:
                 total += (loss / chains).detach().float()
         for micro in range(chains if pipelined else 0, chains):
