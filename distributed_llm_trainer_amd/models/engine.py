@@ -876,10 +876,11 @@ class GPTEngine:
         prog: List[dict] = [dict() for _ in range(GA)]
         # ffbb: the default for two chains with every weight gradient deferred (the
         # memory-lean modes keep fb: both forwards' activations live at once cost ~5 GB)
-        sched = os.environ.get("DLT_WINDOW_SCHED", "ffbb" if self.defer_roles == frozenset(self.ROLES) else "fb")
-        # (flat DDP store only: an FSDP unit's per-micro-step gradient buffers are handed out
-        # by the provider in backward order, so two backwards must not be issued interleaved)
-        if overlap and GA == 2 and sched == "ffbb" and getattr(self.provider, "late_post_backward_ok", False):
+        # (FSDP, per-micro-step weight gradients: ffbb measured no faster, 1.5x the memory;
+        # DLT_WINDOW_SCHED=ffbb still runs it, bit-exact -- profiles/r3_window_ffbb.md)
+        sched = os.environ.get("DLT_WINDOW_SCHED",
+                               "ffbb" if defer and self.defer_roles == frozenset(self.ROLES) else "fb")
+        if overlap and GA == 2 and sched == "ffbb":
             return self._window_ffbb(micro_ids, micro_targets, dloss, recompute, defer, sync_hook, before_last)
         self.set_accumulation(0, GA, defer=defer)
         main = pipe = None

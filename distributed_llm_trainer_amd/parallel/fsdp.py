@@ -89,6 +89,7 @@ class FlatUnit:
         self.refs = 0            # chains (forward / backward of a micro-step) using `full`
         self.ready_ev = None     # HIP event: `full` is complete (recorded after the gather wait)
         self.norm_grad = None    # bf16-gradient mode: fp32 ln1 | ln2 gradients of the micro-step
+        self.head_q = []         # root unit: gradient buffers of backwards issued but not yet reduced
 
     def local_slice(self) -> Tuple[int, int]:
         return self.rank * self.shard, (self.rank + 1) * self.shard
@@ -397,11 +398,19 @@ class FSDPRuntime(ParamProvider):
         return HeadWeights(embed=e, lm_head=e, norm=self._view(u, u.full, "norm.weight"))
 
     def head_grads(self):
+        """A fresh root-unit gradient buffer per backward (FIFO): the two-chain window
+        issues both backwards interleaved, each asks for its buffer at its start, and
+        post_backward("head") reduces them in the same order."""
         u = self.units["head"]
-        if u.full_grad is None:
-            u.full_grad = torch.zeros(u.padded, dtype=torch.float32, device=self.device)
+        if self.sync_every_micro_step:
+            g = torch.zeros(u.padded, dtype=torch.float32, device=self.device)
+            u.head_q.append(g)
+        else:  # accumulated over the micro-steps until the synchronising one
+            if u.full_grad is None:
+                u.full_grad = torch.zeros(u.padded, dtype=torch.float32, device=self.device)
+            g = u.full_grad
         H, Vp = self.cfg.hidden_size, self.cfg.vocab_size_padded
-        return HeadGrads(embed=u.full_grad[:Vp * H].view(Vp, H), norm=self._view(u, u.full_grad, "norm.weight"))
+        return HeadGrads(embed=g[:Vp * H].view(Vp, H), norm=self._view(u, g, "norm.weight"))
 
     # ------------------------------------------------------------------- hooks
     def _next(self, uid, forward: bool):
@@ -443,6 +452,8 @@ class FSDPRuntime(ParamProvider):
                                   self._view(u, u.full_grad, p + "post_attention_layernorm.weight")],
                                  [u.norm_grad[:H], u.norm_grad[H:]])  # one multi-tensor launch
             u.norm_grad = None
+        if uid == "head" and u.head_q:
+            u.full_grad = u.head_q.pop(0)
         do_reduce = self.sync or self.sync_every_micro_step
         if do_reduce:
             self._reduce(u)
@@ -464,6 +475,7 @@ class FSDPRuntime(ParamProvider):
         self.grad_flat.zero_()
         for u in self.units.values():
             u.full_grad = None
+            u.head_q.clear()
 
     def refresh_shadow(self):
         """Re-derive the device compute-dtype shards from the fp32 masters."""
