@@ -878,8 +878,11 @@ class GPTEngine:
         # memory-lean modes keep fb: both forwards' activations live at once cost ~5 GB)
         # (FSDP, per-micro-step weight gradients: ffbb measured no faster, 1.5x the memory;
         # DLT_WINDOW_SCHED=ffbb still runs it, bit-exact -- profiles/r3_window_ffbb.md)
+        # (measured per model: GPT-2 small +0.9-1.1 % with ffbb, medium -1.3 % -- its larger
+        # GEMMs already fill the GPU alone, so two forwards only contend)
         sched = os.environ.get("DLT_WINDOW_SCHED",
-                               "ffbb" if defer and self.defer_roles == frozenset(self.ROLES) else "fb")
+                               "ffbb" if (defer and self.defer_roles == frozenset(self.ROLES)
+                                          and self.cfg.hidden_size <= 768) else "fb")
         if overlap and GA == 2 and sched == "ffbb":
             return self._window_ffbb(micro_ids, micro_targets, dloss, recompute, defer, sync_hook, before_last)
         self.set_accumulation(0, GA, defer=defer)
