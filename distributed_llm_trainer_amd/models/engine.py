@@ -314,19 +314,24 @@ class GPTEngine:
         return mask, ev
 
     def _ac_keep(self, M: int):
-        """(keep_qkv, keep_gu) under activation checkpointing: GEMM outputs kept instead of
-        recomputed, greedily by recompute time saved per byte (the QKV output first),
-        while every layer of the two micro-steps a pipelined window holds fits in
-        ``ac_budget``.  Whole-block recompute (``DLT_AC_SELECTIVE=0``) keeps nothing."""
+        """(keep_qkv, keep_gu, keep_rest) under activation checkpointing: tensors kept
+        instead of recomputed, greedily by recompute time saved per byte -- the QKV GEMM
+        output, the gate/up GEMM output, then the two normed inputs and the SwiGLU output
+        (memory-bound recomputes: 3 bytes of traffic per byte kept) -- while every layer of
+        the two micro-steps a pipelined window holds fits in ``ac_budget``.  With all
+        three nothing is recomputed.  Whole-block recompute (``DLT_AC_SELECTIVE=0``) keeps
+        nothing."""
         if not self.selective_recompute:
-            return False, False
+            return False, False, False
         cfg = self.cfg
         per_layer_chains = cfg.num_layers * 2 * (2 if self.act_dtype == torch.bfloat16 else 4)
         qkv = M * 3 * cfg.hidden_size * per_layer_chains
         gu = M * 2 * cfg.intermediate_size * per_layer_chains
+        rest = M * (2 * cfg.hidden_size + cfg.intermediate_size) * per_layer_chains
         keep_qkv = qkv <= self.ac_budget
         keep_gu = keep_qkv and qkv + gu <= self.ac_budget
-        return keep_qkv, keep_gu
+        keep_rest = keep_gu and qkv + gu + rest <= self.ac_budget and os.environ.get("DLT_AC_KEEP_REST", "1") != "0"
+        return keep_qkv, keep_gu, keep_rest
 
     def _layer_forward(self, st: _StepState, i: int, r, d, key_d: int, p_d: float,
                        save: bool):
@@ -391,12 +396,14 @@ class GPTEngine:
                             x2=x2, rstd2=rstd2, n2=n2, gu=gu, s=s)
         elif st.recompute:
             if self.selective_recompute:
-                keep_qkv, keep_gu = self._ac_keep(M)
+                keep_qkv, keep_gu, keep_rest = self._ac_keep(M)
                 c = _LayerCache(x=x, o=o, lse=lse, x2=x2)
                 if keep_qkv and self.packed_qkv:
                     c.q = q
                 if keep_gu:
                     c.gu = gu
+                if keep_rest and keep_qkv and self.packed_qkv:  # nothing left to recompute
+                    c.n1, c.rstd1, c.n2, c.rstd2, c.s = n1, rstd1, n2, rstd2, s
             else:
                 c = _LayerCache(x=x)
         else:
@@ -411,6 +418,8 @@ class GPTEngine:
         the same inputs as the forward, so every recomputed tensor is bit-identical."""
         if c.o is None:
             return self._layer_forward(st, i, c.x, None, 0, 0.0, save=True)[2]
+        if c.n1 is not None and c.s is not None and c.q is not None and c.gu is not None:
+            return c  # the forward kept everything (_ac_keep within the budget)
         ops, gm, cfg = self.ops, self.gemm, self.cfg
         B, S = st.B, st.S
         w = self.provider.layer(i)

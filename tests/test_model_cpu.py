@@ -107,22 +107,26 @@ def test_dropout_recompute_replays_masks():
 @pytest.mark.parametrize("packed", [True, False])
 def test_selective_recompute_matches_full_recompute(packed):
     """Selective checkpointing (keeps o / lse / x2, recomputes only norm -> QKV -> RoPE and
-    norm -> gate/up -> SwiGLU), its budgeted form (also keeps the QKV / gate-up GEMM
-    outputs: recomputes only the norms and SwiGLU) and whole-block recompute give
-    bit-identical gradients to no recompute at all -- on the packed-QKV path and on the
-    split q/k/v path."""
+    norm -> gate/up -> SwiGLU), its budgeted forms (also keeps the QKV output; the QKV and
+    gate-up outputs: recomputes only the norms and SwiGLU; everything: recomputes nothing)
+    and whole-block recompute give bit-identical gradients to no recompute at all -- on the
+    packed-QKV path and on the split q/k/v path."""
     torch.manual_seed(3)
     cfg = tiny(dropout=0.1, attention_dropout=0.1)
     base = GPT(cfg)
     ids = torch.randint(0, 256, (2, 32))
     grads = []
+    M, H, I, L = 2 * 32, cfg.hidden_size, cfg.intermediate_size, cfg.num_layers
+    keeps = []
     for ac, selective, budget in ((False, True, 0.0), (True, False, 0.0), (True, True, 0.0), (True, True, 1e12),
-                                  (True, True, None)):
+                                  (True, True, "qkv"), (True, True, "qkv+gu")):
         m = copy.deepcopy(base)
         m.enable_engine(seed=5)
-        if budget is None:  # exactly the QKV outputs of both chains of a window
-            esize = torch.empty((), dtype=m.engine.act_dtype).element_size()
-            budget = 2 * 32 * 3 * cfg.hidden_size * cfg.num_layers * 2 * esize
+        esize = torch.empty((), dtype=m.engine.act_dtype).element_size()
+        if budget == "qkv":  # exactly the QKV outputs of both chains of a window
+            budget = M * 3 * H * L * 2 * esize
+        elif budget == "qkv+gu":
+            budget = M * (3 * H + 2 * I) * L * 2 * esize
         m.engine.packed_qkv = packed and m.engine.packed_qkv
         m.gradient_checkpointing = ac
         m.engine.selective_recompute = selective
@@ -130,7 +134,8 @@ def test_selective_recompute_matches_full_recompute(packed):
         _, loss = m(ids, labels=ids)
         loss.backward()
         grads.append([p.grad.clone() for p in m.parameters()])
-    assert m.engine._ac_keep(2 * 32) == (True, False)  # the last budget fits QKV only
+        keeps.append(m.engine._ac_keep(M))
+    assert keeps[3] == (True, True, True) and keeps[4] == (True, False, False) and keeps[5] == (True, True, False)
     for g in grads[1:]:
         for a, b in zip(grads[0], g):
             assert torch.equal(a, b)

@@ -369,9 +369,12 @@ def test_selective_recompute_matches_full_and_none_gpu():
     base = GPT(_cfg(0.1)).to(DEV)
     ids = torch.randint(0, 1000, (2, 256), device=DEV)
     grads = []
-    # (budget 0: the QKV / gate-up GEMMs are recomputed; 1e12: their outputs are kept)
-    for recompute, selective, budget in ((False, True, 0.0), (True, True, 0.0), (True, True, 1e12),
-                                         (True, False, 0.0)):
+    # (budget 0: the QKV / gate-up GEMMs are recomputed; "gemm": their outputs are kept, the
+    # norms and SwiGLU recomputed; 1e12: everything kept, nothing recomputed)
+    cfg = base.config
+    gemm_only = 2 * 256 * (3 * cfg.hidden_size + 2 * cfg.intermediate_size) * cfg.num_layers * 2 * 2
+    for recompute, selective, budget in ((False, True, 0.0), (True, True, 0.0), (True, True, gemm_only),
+                                         (True, True, 1e12), (True, False, 0.0)):
         m = copy.deepcopy(base)
         eng = m.enable_engine(seed=4)
         eng.selective_recompute = selective
