@@ -889,9 +889,14 @@ class GPTEngine:
         # DLT_WINDOW_SCHED=ffbb still runs it, bit-exact -- profiles/r3_window_ffbb.md)
         # (measured per model: GPT-2 small +0.9-1.1 % with ffbb, medium -1.3 % -- its larger
         # GEMMs already fill the GPU alone, so two forwards only contend)
+        # ... and only without gradient collectives: with the DDP bucket all-reduces in flight
+        # (more than one rank, or DLT_FORCE_COLLECTIVES) ffbb measured 692-697k vs fb 775-777k
+        # tok/s on one RCCL rank -- the RCCL kernels starve for CUs next to three busy streams
+        hooks = getattr(self.provider, "hooks", None)
+        comm = bool(getattr(hooks, "collectives", False))
         sched = os.environ.get("DLT_WINDOW_SCHED",
                                "ffbb" if (defer and self.defer_roles == frozenset(self.ROLES)
-                                          and self.cfg.hidden_size <= 768) else "fb")
+                                          and self.cfg.hidden_size <= 768 and not comm) else "fb")
         if overlap and GA == 2 and sched == "ffbb":
             return self._window_ffbb(micro_ids, micro_targets, dloss, recompute, defer, sync_hook, before_last)
         self.set_accumulation(0, GA, defer=defer)

@@ -136,5 +136,10 @@ class DDPRuntime:
         self.handles.clear()
 
     @property
+    def collectives(self) -> bool:
+        """Whether bucket all-reduces are actually issued (world > 1, or forced on one rank)."""
+        return self.world > 1 or self.force
+
+    @property
     def grad_div(self) -> float:
         return float(self.world)
