@@ -783,6 +783,30 @@ class GPTEngine:
             torch.cuda.current_stream().wait_stream(side)
 
     # ------------------------------------------------------ pipelined window
+    def window_schedule(self, GA: int, defer: bool, cuda: bool = True):
+        """(overlapped backwards?, "ffbb" | "fb") for a window of GA chains.
+
+        Overlapped backwards: providers that allow them (``overlap_backward_ok``: the flat
+        DDP store, the FSDP runtime), ``DLT_BWD_OVERLAP=0`` turns them off.  ffbb (two
+        chains only, needs overlap) is the default when every weight gradient is deferred
+        (the memory-lean modes keep fb: both forwards' activations live at once cost ~5 GB;
+        FSDP's per-micro-step weight gradients: measured no faster, 1.5x the memory), the
+        model is GPT-2-small-sized (small +0.9-1.1 %, medium -1.3 %: its larger GEMMs fill
+        the GPU alone, two forwards only contend) and no gradient collective runs (with the
+        DDP bucket all-reduces in flight ffbb measured 692-697k vs fb 775-777k tok/s on one
+        forced RCCL rank: the RCCL kernels starve for CUs next to three busy streams).
+        ``DLT_WINDOW_SCHED=fb|ffbb`` overrides (profiles/r3_window_ffbb.md)."""
+        overlap = (cuda and GA > 1 and getattr(self.provider, "overlap_backward_ok", False)
+                   and os.environ.get("DLT_BWD_OVERLAP", "1") != "0")
+        hooks = getattr(self.provider, "hooks", None)
+        comm = bool(getattr(hooks, "collectives", False))
+        sched = os.environ.get("DLT_WINDOW_SCHED",
+                               "ffbb" if (defer and self.defer_roles == frozenset(self.ROLES)
+                                          and self.cfg.hidden_size <= 768 and not comm) else "fb")
+        if not (overlap and GA == 2 and sched == "ffbb"):
+            sched = "fb"
+        return overlap, sched
+
     def _window_ffbb(self, micro_ids, micro_targets, dloss, recompute, defer, sync_hook, before_last):
         """Two-chain window F0 || F1 | B0 || B1 (see train_window)."""
         dev = micro_ids[0].device
@@ -880,24 +904,9 @@ class GPTEngine:
         GA = len(micro_ids)
         dev = micro_ids[0].device
         cuda = dev.type == "cuda"
-        overlap = (cuda and GA > 1 and getattr(self.provider, "overlap_backward_ok", False)
-                   and os.environ.get("DLT_BWD_OVERLAP", "1") != "0")
+        overlap, sched = self.window_schedule(GA, defer, cuda)
         prog: List[dict] = [dict() for _ in range(GA)]
-        # ffbb: the default for two chains with every weight gradient deferred (the
-        # memory-lean modes keep fb: both forwards' activations live at once cost ~5 GB)
-        # (FSDP, per-micro-step weight gradients: ffbb measured no faster, 1.5x the memory;
-        # DLT_WINDOW_SCHED=ffbb still runs it, bit-exact -- profiles/r3_window_ffbb.md)
-        # (measured per model: GPT-2 small +0.9-1.1 % with ffbb, medium -1.3 % -- its larger
-        # GEMMs already fill the GPU alone, so two forwards only contend)
-        # ... and only without gradient collectives: with the DDP bucket all-reduces in flight
-        # (more than one rank, or DLT_FORCE_COLLECTIVES) ffbb measured 692-697k vs fb 775-777k
-        # tok/s on one RCCL rank -- the RCCL kernels starve for CUs next to three busy streams
-        hooks = getattr(self.provider, "hooks", None)
-        comm = bool(getattr(hooks, "collectives", False))
-        sched = os.environ.get("DLT_WINDOW_SCHED",
-                               "ffbb" if (defer and self.defer_roles == frozenset(self.ROLES)
-                                          and self.cfg.hidden_size <= 768 and not comm) else "fb")
-        if overlap and GA == 2 and sched == "ffbb":
+        if sched == "ffbb":
             return self._window_ffbb(micro_ids, micro_targets, dloss, recompute, defer, sync_hook, before_last)
         self.set_accumulation(0, GA, defer=defer)
         main = pipe = None

@@ -222,3 +222,31 @@ def test_fused_loss_segments_normalise_per_micro_step():
     assert torch.allclose(loss2, (losses[0] + losses[1]) / 2, atol=1e-6)
     for (n, p1), (_, p2) in zip(m1.named_parameters(), m2.named_parameters()):
         assert torch.allclose(p1.grad, p2.grad, atol=1e-6, rtol=1e-5), n
+
+
+def test_window_schedule_choice(monkeypatch):
+    """Two-chain window schedule: ffbb only with overlapped backwards, two chains, every
+    weight gradient deferred, a GPT-2-small-sized model and no gradient collectives in
+    flight; fb otherwise (profiles/r3_window_ffbb.md)."""
+    import types
+    monkeypatch.delenv("DLT_WINDOW_SCHED", raising=False)
+    monkeypatch.delenv("DLT_BWD_OVERLAP", raising=False)
+    torch.manual_seed(0)
+    m = GPT(tiny())
+    e = m.enable_engine(seed=1)
+    assert getattr(e.provider, "overlap_backward_ok", False)
+    assert e.window_schedule(2, True, cuda=True) == (True, "ffbb")
+    assert e.window_schedule(4, True, cuda=True) == (True, "fb")          # more than two chains
+    assert e.window_schedule(2, False, cuda=True) == (True, "fb")         # per-micro-step weight grads
+    assert e.window_schedule(2, True, cuda=False) == (False, "fb")        # no streams on the CPU
+    e.defer_roles = frozenset(("qkv", "o"))                               # memory-lean
+    assert e.window_schedule(2, True, cuda=True) == (True, "fb")
+    e.defer_roles = frozenset(e.ROLES)
+    e.provider.hooks = types.SimpleNamespace(collectives=True)            # DDP buckets in flight
+    assert e.window_schedule(2, True, cuda=True) == (True, "fb")
+    e.provider.hooks = types.SimpleNamespace(collectives=False)
+    monkeypatch.setenv("DLT_BWD_OVERLAP", "0")
+    assert e.window_schedule(2, True, cuda=True) == (False, "fb")
+    monkeypatch.delenv("DLT_BWD_OVERLAP")
+    monkeypatch.setenv("DLT_WINDOW_SCHED", "fb")
+    assert e.window_schedule(2, True, cuda=True) == (True, "fb")
