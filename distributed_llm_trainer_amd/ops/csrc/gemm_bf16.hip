@@ -486,6 +486,12 @@ static inline int gb_grid(int ntiles) {
   return (g + 7) & ~7;
 }
 
+// flags & 256: one tile per workgroup (grid = tiles, a multiple of 8) instead of the
+// persistent grid -- frees CUs between tiles when other streams run kernels alongside
+static inline int gb_launch_grid(int ntiles, int flags) {
+  return (flags & 256) ? ((ntiles + 7) & ~7) : gb_grid(ntiles);
+}
+
 static inline bool gb_shape_ok(int M, int N, int K, int lda, int ldb, int ldc) {
   return M > 0 && N > 0 && M % 256 == 0 && K % 128 == 0 && K >= 128 && (lda | ldb | ldc) % 8 == 0;
 }
@@ -497,9 +503,7 @@ DLT_API int dlt_gemm_bf16_tn(const bf16_t* A, const bf16_t* B, bf16_t* C, int M,
   if (!gb_shape_ok(M, N, K, lda, ldb, ldc) || N % 192) return -1;
   const int ntiles = (M / 256) * (N / 192);
   GbEpi ep{};
-  // flags & 256: one tile per workgroup (grid = tiles) instead of the persistent grid
-  const int grid = (flags & 256) ? ((ntiles + 7) & ~7) : gb_grid(ntiles);
-  k_gemm_bf16<192, GB_EPI_STORE><<<grid, 512, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, ep);
+  k_gemm_bf16<192, GB_EPI_STORE><<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, ep);
   DLT_CHECK_LAUNCH();
 }
 
@@ -511,7 +515,7 @@ DLT_API int dlt_gemm_bf16_qkv_rope(const bf16_t* A, const bf16_t* W, bf16_t* C, 
   if (!gb_shape_ok(M, N, K, K, K, N) || N % 192 || H % 64 || S <= 0) return -1;
   GbEpi ep{cosT, sinT, S, 2 * H, nullptr, 0, 0};
   const int ntiles = (M / 256) * (N / 192);
-  k_gemm_bf16<192, GB_EPI_ROPE><<<gb_grid(ntiles), 512, 0, st>>>(A, W, C, M, N, K, K, K, N, flags, ep);
+  k_gemm_bf16<192, GB_EPI_ROPE><<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(A, W, C, M, N, K, K, K, N, flags, ep);
   DLT_CHECK_LAUNCH();
 }
 
@@ -522,6 +526,6 @@ DLT_API int dlt_gemm_bf16_gu_swiglu(const bf16_t* A, const bf16_t* W, bf16_t* gu
   if (!gb_shape_ok(M, N, K, K, K, N) || I % 96) return -1;
   GbEpi ep{nullptr, nullptr, 1, 0, s_out, I, I};
   const int ntiles = (M / 256) * (I / 96);
-  k_gemm_bf16<192, GB_EPI_SWIGLU><<<gb_grid(ntiles), 512, 0, st>>>(A, W, gu, M, N, K, K, K, N, flags, ep);
+  k_gemm_bf16<192, GB_EPI_SWIGLU><<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(A, W, gu, M, N, K, K, K, N, flags, ep);
   DLT_CHECK_LAUNCH();
 }

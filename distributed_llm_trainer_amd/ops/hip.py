@@ -703,6 +703,11 @@ def gemm_wgrad_sk(dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, shares: i
 
 
 # ------------------------------------------------- projection GEMMs (csrc/gemm_bf16.hip)
+# launch flags of the hand projection GEMMs; DLT_GEMM_FLAGS=256 = one tile per workgroup
+# instead of the persistent grid (A/B knob for overlapped schedules)
+_GB_FLAGS = int(os.environ.get("DLT_GEMM_FLAGS", "0")) & 256
+
+
 def gemm_bf16_fits(M: int, N: int, K: int) -> bool:
     """Shapes the persistent 256 x 192 MFMA kernel tiles exactly."""
     return M > 0 and M % 256 == 0 and N % 192 == 0 and K % 128 == 0 and K >= 128
@@ -720,7 +725,7 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = No
     _req(b, torch.bfloat16, "gemm_bf16.b")
     c = torch.empty(M, N, dtype=torch.bfloat16, device=a.device) if out is None else out
     _req(c, torch.bfloat16, "gemm_bf16.c", M * N)
-    _chk(lib().dlt_gemm_bf16_tn(_p(a), _p(b), _p(c), M, N, K, K, K, N, 0, _stream()), "gemm_bf16")
+    _chk(lib().dlt_gemm_bf16_tn(_p(a), _p(b), _p(c), M, N, K, K, K, N, _GB_FLAGS, _stream()), "gemm_bf16")
     return c
 
 
@@ -742,7 +747,7 @@ def gemm_qkv_rope(x: torch.Tensor, wqkv: torch.Tensor, S: int, cos: torch.Tensor
     _req(sin, torch.float32, "gemm_qkv_rope.sin", cos.numel())
     c = torch.empty(M, N, dtype=torch.bfloat16, device=x.device) if out is None else out
     _req(c, torch.bfloat16, "gemm_qkv_rope.out", M * N)
-    _chk(lib().dlt_gemm_bf16_qkv_rope(_p(x), _p(wqkv), _p(c), M, H, K, S, _p(cos), _p(sin), 0, _stream()),
+    _chk(lib().dlt_gemm_bf16_qkv_rope(_p(x), _p(wqkv), _p(c), M, H, K, S, _p(cos), _p(sin), _GB_FLAGS, _stream()),
          "gemm_qkv_rope")
     return c
 
@@ -763,7 +768,7 @@ def gemm_gu_swiglu(x: torch.Tensor, wgu: torch.Tensor, gu_out: Optional[torch.Te
     s = torch.empty(M, I, dtype=torch.bfloat16, device=x.device) if s_out is None else s_out
     _req(gu, torch.bfloat16, "gemm_gu_swiglu.gu", M * I2)
     _req(s, torch.bfloat16, "gemm_gu_swiglu.s", M * I)
-    _chk(lib().dlt_gemm_bf16_gu_swiglu(_p(x), _p(wgu), _p(gu), _p(s), M, I, K, 0, _stream()), "gemm_gu_swiglu")
+    _chk(lib().dlt_gemm_bf16_gu_swiglu(_p(x), _p(wgu), _p(gu), _p(s), M, I, K, _GB_FLAGS, _stream()), "gemm_gu_swiglu")
     return gu, s
 
 
