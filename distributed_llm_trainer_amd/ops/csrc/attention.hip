@@ -32,6 +32,10 @@
 // bf16 (= the [M, H] GEMM layout);  lse, delta: [B*nh, S] fp32 (natural-log lse).
 #include "common.h"
 
+#ifndef DLT_ATTN_KREAD_ASM
+#define DLT_ATTN_KREAD_ASM 1
+#endif
+
 #include <type_traits>
 
 #define HD 64
@@ -92,6 +96,26 @@ __device__ __forceinline__ bf16x8_t tr_frag_asm(const bf16_t* T, int kk, int dt,
   const shortx4_t b = lds_tr4_asm(T, r1 + 8, col);
   shortx8_t c = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
   return __builtin_bit_cast(bf16x8_t, c);
+}
+// Row-fragment read through inline asm (see lds_tr4_asm for the protocol), so several
+// reads can be in flight under one counted wait (the intrinsic form drew one
+// lgkmcnt(0) per MFMA pair).
+__device__ __forceinline__ bf16x8_t lds_row8_asm(const bf16_t* T, int row, int col) {
+  bf16x8_t r;
+  const uint32_t addr = (uint32_t)(uintptr_t)(T + swz_off(row, col));
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(addr));
+  return r;
+}
+// Oldest four of eight outstanding LDS reads retired (LDS returns in order; no SMEM
+// load is issued inside a tile step).
+__device__ __forceinline__ void lgkm_wait4(bf16x8_t& a, bf16x8_t& b, bf16x8_t& c, bf16x8_t& d) {
+  asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d)::"memory");
+}
+__device__ __forceinline__ float max16(const floatx16_t& a) {
+  const float m0 = fmaxf(fmaxf(a[0], a[1]), a[2]), m1 = fmaxf(fmaxf(a[3], a[4]), a[5]);
+  const float m2 = fmaxf(fmaxf(a[6], a[7]), a[8]), m3 = fmaxf(fmaxf(a[9], a[10]), a[11]);
+  const float m4 = fmaxf(fmaxf(a[12], a[13]), a[14]);
+  return fmaxf(fmaxf(fmaxf(m0, m1), m2), fmaxf(fmaxf(m3, m4), a[15]));
 }
 // Retire outstanding LDS reads; the fragments are in/out operands so no consumer can
 // be scheduled above the wait.
@@ -363,6 +387,21 @@ __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const b
   floatx16_t sacc[2];
   {
     bf16x8_t kf[2][4];
+#if DLT_ATTN_KREAD_ASM
+    // all eight K fragments in flight at once, one counted wait per half
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) kf[t][s] = lds_row8_asm(Kt, 32 * t + ql, 16 * s + 8 * h);
+    lgkm_wait4(kf[0][0], kf[0][1], kf[0][2], kf[0][3]);
+    sacc[0] = zero16();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) sacc[0] = mfma(kf[0][s], qf[s], sacc[0]);
+    tr_wait(kf[1][0], kf[1][1], kf[1][2], kf[1][3]);
+    sacc[1] = zero16();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) sacc[1] = mfma(kf[1][s], qf[s], sacc[1]);
+#else
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       kf[0][s] = lds_row8(Kt, ql, 16 * s + 8 * h);
@@ -375,20 +414,19 @@ __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const b
       sacc[0] = mfma(kf[0][s], qf[s], sacc[0]);
       sacc[1] = mfma(kf[1][s], qf[s], sacc[1]);
     }
+#endif
   }
-  float mx0 = -INFINITY, mx1 = -INFINITY;
+  if (MASK) {
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      if (MASK) {
+      for (int i = 0; i < 16; ++i) {
         const int ka = k0 + 32 * t + acc_row(i, h);
         sacc[t][i] = (ka > qa || ka >= S) ? -INFINITY : sacc[t][i];
       }
-      if (t == 0) mx0 = fmaxf(mx0, sacc[t][i]);
-      else mx1 = fmaxf(mx1, sacc[t][i]);
-    }
-  const float mx = xhalf_max(fmaxf(mx0, mx1));
+  }
+  // row max as a depth-3 max3 tree per half (a linear fmaxf chain is 9 dependent ops)
+  const float mx = xhalf_max(fmaxf(max16(sacc[0]), max16(sacc[1])));
   if (!__all((mx - fs.m) * c_log2 <= RESCALE_LOG2)) {  // rare: a row's max grew by > 2^8
     const float m_new = fmaxf(fs.m, mx);
     const float alpha = fast_exp2((fs.m - m_new) * c_log2);
@@ -787,11 +825,26 @@ __device__ __forceinline__ void dq_tile(floatx16_t (&dqa)[2], const bf16_t* Kt, 
   for (int t = 0; t < 2; ++t) {
     sacc[t] = zero16();
     pacc[t] = zero16();
+#if DLT_ATTN_KREAD_ASM
+    // the half-tile's K and V fragments in flight at once, one counted wait each
+    bf16x8_t kf[4], vf[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) kf[s] = lds_row8_asm(Kt, 32 * t + ql, 16 * s + 8 * h);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) vf[s] = lds_row8_asm(Vt, 32 * t + ql, 16 * s + 8 * h);
+    lgkm_wait4(kf[0], kf[1], kf[2], kf[3]);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) sacc[t] = mfma(kf[s], qf[s], sacc[t]);
+    tr_wait(vf[0], vf[1], vf[2], vf[3]);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) pacc[t] = mfma(vf[s], df[s], pacc[t]);
+#else
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       sacc[t] = mfma(lds_row8(Kt, 32 * t + ql, 16 * s + 8 * h), qf[s], sacc[t]);
       pacc[t] = mfma(lds_row8(Vt, 32 * t + ql, 16 * s + 8 * h), df[s], pacc[t]);
     }
+#endif
   }
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
