@@ -219,8 +219,8 @@ __global__ __launch_bounds__(256) void k_rmsnorm_bwd(
 }
 
 // dw[j] += sum over the partial rows, in a fixed order (bitwise reproducible, no
-// float atomics).  One 1024-thread block per 64 columns: thread (g, q) owns columns
-// 4q..4q+3 of the slice (float4 loads, 16 threads = one 256-B row segment) and rows
+// float atomics).  One 64*QN-thread block per 4*QN columns: thread (g, q) owns columns
+// 4q..4q+3 of the slice (float4 loads, QN threads = one row segment) and rows
 // g, g+64, ... with 8 loads in flight (the partials were written by blocks on every XCD,
 // so the reads come from the fabric: latency-bound without that parallelism); then the
 // 64 row-group sums are added through LDS in two fixed-order levels.
@@ -228,12 +228,14 @@ __device__ __forceinline__ void f4add(float4& a, const float4 b) {
   a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
 }
 
-__global__ __launch_bounds__(1024) void k_colsum_acc(const float* __restrict__ part, float* __restrict__ dw, int rows,
-                                                     int H) {
-  __shared__ float red[64][65];
-  __shared__ float red2[16][64];
-  const int q = threadIdx.x & 15, g = threadIdx.x >> 4;
-  const int c0 = blockIdx.x * 64 + q * 4;
+template <int QN>
+__global__ __launch_bounds__(64 * QN) void k_colsum_acc(const float* __restrict__ part, float* __restrict__ dw, int rows,
+                                                       int H) {
+  constexpr int C = 4 * QN;  // columns per block
+  __shared__ float red[64][C + 1];
+  __shared__ float red2[16][C];
+  const int q = threadIdx.x % QN, g = threadIdx.x / QN;
+  const int c0 = blockIdx.x * C + q * 4;
   float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0, a3 = a0;
   if (c0 < H) {  // H % 4 == 0: the quad is in range
     const float* p = part + c0;
@@ -256,12 +258,12 @@ __global__ __launch_bounds__(1024) void k_colsum_acc(const float* __restrict__ p
   red[g][q * 4 + 3] = a0.w;
   __syncthreads();
   {  // level 2: thread (k, j) adds row groups 4k..4k+3 of column j
-    const int j = threadIdx.x & 63, k = threadIdx.x >> 6;
+    const int j = threadIdx.x % C, k = threadIdx.x / C;
     red2[k][j] = (red[4 * k][j] + red[4 * k + 1][j]) + (red[4 * k + 2][j] + red[4 * k + 3][j]);
   }
   __syncthreads();
-  if (threadIdx.x < 64) {
-    const int j = blockIdx.x * 64 + threadIdx.x;
+  if (threadIdx.x < C) {
+    const int j = blockIdx.x * C + threadIdx.x;
     if (j < H) {
       float s = 0.f;
 #pragma unroll
@@ -343,6 +345,14 @@ DLT_API int dlt_rmsnorm_bwd(const bf16_t* dy, const float* x, const float* rstd,
     default: k_rmsnorm_bwd<16><<<grid, block, shm, stream>>>(ARGS); break;
   }
 #undef ARGS
-  if (dw_ws) k_colsum_acc<<<(H + 63) / 64, 1024, 0, stream>>>(dw_ws, dw, blocks, H);
+  if (dw_ws) {
+    // 16-column blocks of 256 threads (48 for H = 768) slot into the CUs that the other
+    // micro-step chain's kernels leave free; 64-column blocks of 1024 threads waited for
+    // a whole free CU (45 us in the overlapped step vs 6 us alone).  Same summation order
+    // either way (DLT_COLSUM_WIDE=1: the 1024-thread form).
+    static const bool wide = getenv("DLT_COLSUM_WIDE") && atoi(getenv("DLT_COLSUM_WIDE")) == 1;
+    if (wide) k_colsum_acc<16><<<(H + 63) / 64, 1024, 0, stream>>>(dw_ws, dw, blocks, H);
+    else k_colsum_acc<4><<<(H + 15) / 16, 256, 0, stream>>>(dw_ws, dw, blocks, H);
+  }
   DLT_CHECK_LAUNCH();
 }
