@@ -819,6 +819,21 @@ class GPTEngine:
         self._wgrad_stream(dev)  # created before the fork
         p0.wait_stream(main)
         streams = [p0, main]
+        # the hand projection GEMM's persistent grid leaves CUs to the other chain
+        # (DLT_FFBB_GEMM_GRID, default 192 of 256 workgroups: +0.05-0.5 % in three same-box
+        # A/Bs, docs/KERNELS.md; results unchanged, each output tile is still computed
+        # whole by one workgroup)
+        cap = int(os.environ.get("DLT_FFBB_GEMM_GRID", "192"))
+        prev_cap = self.ops.gemm_grid_cap(cap) if cap and hasattr(self.ops, "gemm_grid_cap") else None
+        try:
+            return self._window_ffbb_body(micro_ids, micro_targets, dloss, recompute, defer, sync_hook, before_last,
+                                          main, p0, streams)
+        finally:
+            if prev_cap is not None:
+                self.ops.gemm_grid_cap(prev_cap)
+
+    def _window_ffbb_body(self, micro_ids, micro_targets, dloss, recompute, defer, sync_hook, before_last,
+                          main, p0, streams):
         losses: List[Any] = [None, None]
         states: List[Any] = [None, None]
         ready: List[Any] = []

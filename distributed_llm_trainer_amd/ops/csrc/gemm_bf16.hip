@@ -488,8 +488,12 @@ static inline int gb_grid(int ntiles) {
 
 // flags & 256: one tile per workgroup (grid = tiles, a multiple of 8) instead of the
 // persistent grid -- frees CUs between tiles when other streams run kernels alongside
+// flags >> 16 (A/B knob): cap the persistent grid at 8 * (flags >> 16) workgroups, so
+// kernels of the other stream keep the remaining CUs
 static inline int gb_launch_grid(int ntiles, int flags) {
-  return (flags & 256) ? ((ntiles + 7) & ~7) : gb_grid(ntiles);
+  if (flags & 256) return (ntiles + 7) & ~7;
+  const int g = gb_grid(ntiles), cap = 8 * ((flags >> 16) & 0xff);
+  return cap && cap < g ? cap : g;
 }
 
 static inline bool gb_shape_ok(int M, int N, int K, int lda, int ldb, int ldc) {

@@ -680,6 +680,10 @@ def gemm_wgrad(dw: Optional[torch.Tensor], dy: torch.Tensor, x: torch.Tensor, sp
     return True
 
 
+# DLT_WGRAD_SK_SHARES=n: n shares per column tile instead of 256 / column tiles (A/B knob)
+_SK_SHARES = int(os.environ.get("DLT_WGRAD_SK_SHARES", "0"))
+
+
 def gemm_wgrad_sk(dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, shares: int = 0) -> bool:
     """dw[Nr,Nc] (fp32) += dy[T,Nr]^T @ x[T,Nc], stream-K form of the hand-written kernel
     (csrc/gemm_wgrad.hip k_gemm_wgrad_sk): one resident workgroup per CU walks an equal
@@ -695,6 +699,7 @@ def gemm_wgrad_sk(dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, shares: i
     _req(dw, torch.float32, "wgrad_sk.dw", Nr * Nc)
     if dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16 or x.shape[0] != T:
         raise ValueError("gemm_wgrad_sk: bf16 dy[T,Nr] / x[T,Nc] expected")
+    shares = shares or _SK_SHARES
     n = int(lib().dlt_gemm_wgrad_sk_scratch(T, Nr, Nc, shares))
     part = torch.empty(n, device=dw.device, dtype=torch.float32)
     _chk(lib().dlt_gemm_wgrad_sk(_p(dy), _p(x), _p(dw), _p(part), T, Nr, Nc, dy.stride(0), x.stride(0), shares,
@@ -704,8 +709,21 @@ def gemm_wgrad_sk(dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, shares: i
 
 # ------------------------------------------------- projection GEMMs (csrc/gemm_bf16.hip)
 # launch flags of the hand projection GEMMs; DLT_GEMM_FLAGS=256 = one tile per workgroup
-# instead of the persistent grid (A/B knob for overlapped schedules)
-_GB_FLAGS = int(os.environ.get("DLT_GEMM_FLAGS", "0")) & 256
+# instead of the persistent grid; DLT_GEMM_GRID=n caps the persistent grid at n (multiple
+# of 8) workgroups (A/B knobs for overlapped schedules)
+_GB_FLAGS = (int(os.environ.get("DLT_GEMM_FLAGS", "0")) & 256) | \
+    ((min(int(os.environ.get("DLT_GEMM_GRID", "0")), 2040) // 8) << 16)
+
+
+def gemm_grid_cap(n: int) -> int:
+    """Cap the persistent grid of the hand projection GEMMs at ``n`` workgroups (a
+    multiple of 8; 0 = one per CU) for the launches that follow; returns the previous
+    cap.  Each output tile is still computed whole by one workgroup, so results do not
+    change.  The ``ffbb`` window sets 192: the other chain's kernels keep 64 CUs."""
+    global _GB_FLAGS
+    prev = 8 * ((_GB_FLAGS >> 16) & 0xff)
+    _GB_FLAGS = (_GB_FLAGS & 0xffff) | ((min(max(int(n), 0), 2040) // 8) << 16)
+    return prev
 
 
 def gemm_bf16_fits(M: int, N: int, K: int) -> bool:

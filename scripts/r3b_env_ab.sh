@@ -4,7 +4,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 mkdir -p gpurun_out
-for rep in 1 2; do
+for rep in $(seq 1 ${REPS:-2}); do
   for spec in $VARIANTS; do
     name=${spec%%:*}; kv=${spec#*:}
     env $(echo "$kv" | tr ',' ' ') timeout -k 10 300 python bench.py --steps ${STEPS:-20} --warmup 3 $BENCH_ARGS \
