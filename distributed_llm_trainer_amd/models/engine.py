@@ -735,24 +735,24 @@ class GPTEngine:
                     side_ctx = torch.cuda.stream(side)
                     side_ctx.__enter__()
                 if dfr["down"]:
-                    gm.wgrad_acc(gr.wdown, full(i, "dd", H), full(i, "s", I))
+                    _wgrad(gm, gr.wdown, full(i, "dd", H), full(i, "s", I))
                 if dfr["gu"]:
-                    gm.wgrad_acc(gr.wgu, full(i, "dgu", 2 * I), full(i, "n2", H))
+                    _wgrad(gm, gr.wgu, full(i, "dgu", 2 * I), full(i, "n2", H))
                 if dfr["o"]:
-                    gm.wgrad_acc(gr.wo, full(i, "da", H), full(i, "o", H))
+                    _wgrad(gm, gr.wo, full(i, "da", H), full(i, "o", H))
                 if dfr["qkv"]:
-                    gm.wgrad_acc(gr.wqkv, full(i, "dqkv", 3 * H), full(i, "n1", H))
+                    _wgrad(gm, gr.wqkv, full(i, "dqkv", 3 * H), full(i, "n1", H))
             if not all(dfr.values()):  # the per-micro-step ones, on this backward's stream
                 if side_ctx is not None:
                     side_ctx.__exit__(None, None, None)
                 if not dfr["down"]:
-                    gm.wgrad_acc(gr.wdown, g_d, c.s)
+                    _wgrad(gm, gr.wdown, g_d, c.s)
                 if not dfr["gu"]:
-                    gm.wgrad_acc(gr.wgu, dgu, c.n2)
+                    _wgrad(gm, gr.wgu, dgu, c.n2)
                 if not dfr["o"]:
-                    gm.wgrad_acc(gr.wo, da, c.o)
+                    _wgrad(gm, gr.wo, da, c.o)
                 if not dfr["qkv"]:
-                    gm.wgrad_acc(gr.wqkv, dqkv, c.n1)
+                    _wgrad(gm, gr.wqkv, dqkv, c.n1)
                 if side_ctx is not None:
                     # the gradient hook goes out from the side stream, after both halves
                     ev = torch.cuda.Event()
@@ -799,7 +799,7 @@ class GPTEngine:
         overlap = (cuda and GA > 1 and getattr(self.provider, "overlap_backward_ok", False)
                    and os.environ.get("DLT_BWD_OVERLAP", "1") != "0")
         hooks = getattr(self.provider, "hooks", None)
-        comm = bool(getattr(hooks, "collectives", False))
+        comm = bool(getattr(hooks, "collectives", False) or getattr(self.provider, "collectives", False))
         sched = os.environ.get("DLT_WINDOW_SCHED",
                                "ffbb" if (defer and self.defer_roles == frozenset(self.ROLES)
                                           and self.cfg.hidden_size <= 768 and not comm) else "fb")
@@ -986,6 +986,15 @@ class GPTEngine:
         return losses
 
 
+def _wgrad(gm, dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
+    """A layer weight gradient: accumulated into the provider's fp32 buffer, or written
+    once per micro-step into a bf16 reduce-scatter buffer (FSDPRuntime.bf16_grads)."""
+    if dw.dtype == torch.bfloat16:
+        gm.wgrad_set(dw, dy, x)
+    else:
+        gm.wgrad_acc(dw, dy, x)
+
+
 class _TorchGemm:
     """Plain library GEMMs (hipBLASLt on ROCm via torch.matmul).
 
@@ -1014,7 +1023,17 @@ class _TorchGemm:
     def linear_dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         return torch.matmul(dy, w)
 
+    @staticmethod
+    def wgrad_set(dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
+        """dw (bf16, overwritten) = dy^T @ x (the FSDP bf16 send-buffer mode)."""
+        dw2 = dw.view(dy.shape[1], x.shape[1])
+        if dw2.dtype != torch.bfloat16 or not dw2.is_contiguous():
+            raise ValueError("wgrad_set output must be contiguous bf16")
+        torch.matmul(dy.t(), x, out=dw2)
+
     def wgrad_acc(self, dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
+        if dw.dtype == torch.bfloat16:
+            raise ValueError("wgrad_acc accumulates into fp32; use wgrad_set for a bf16 gradient")
         dw2 = dw.view(dy.shape[1], x.shape[1])
         if dy.dtype == torch.float32:
             dw2.addmm_(dy.t(), x)

@@ -89,6 +89,14 @@ __device__ __forceinline__ int gb_brow(int q, int g) {
 //           same math as k_swiglu_fwd on the bf16 gate/up values.
 enum { GB_EPI_STORE = 0, GB_EPI_ROPE = 1, GB_EPI_SWIGLU = 2 };
 
+// Diagnostic build only (tools/cpp/gemm_bench.cpp defines GB_STAMPS): per-wave s_memtime
+// sums of the first K-iteration of a tile, the rest of its K-loop and its epilogue, plus
+// the kernel's shader-clock / real-time span, written by lane 0 to gb_stamp_buf.
+#ifdef GB_STAMPS
+__device__ unsigned long long* gb_stamp_buf;
+#define GB_T() __builtin_amdgcn_s_memtime()
+#endif
+
 struct GbEpi {
   const float* cosT;  // ROPE: [S_tab, 32] fp32
   const float* sinT;
@@ -267,6 +275,10 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
   };
 
   const int nk = K / GB_BK;  // even, >= 2
+#ifdef GB_STAMPS
+  const uint64_t s_k0 = GB_T(), s_r0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t a_it0 = 0, a_rest = 0, a_epi = 0, ntl = 0, t1 = 0;
+#endif
   int tile = tile_of(0);
   if (tile >= ntiles) return;  // whole workgroup idle (uniform)
   auto abase = [&](int t) {
@@ -282,6 +294,12 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
     return B + (size_t)(tn * TS) * ldb;
   };
 
+  // flags & 512 (ablation only): the workgroups of odd XCD-slot rows start (flags >> 24) x
+  // 1024 shader cycles late, so their tile epilogues fall between the others'
+  if ((flags & 512) && ((bid >> 3) & 1)) {
+    const uint64_t t0 = __builtin_amdgcn_s_memtime(), d = (uint64_t)((uint32_t)flags >> 24) << 10;
+    while (__builtin_amdgcn_s_memtime() - t0 < d) __builtin_amdgcn_s_sleep(2);
+  }
   // prologue: K-tile 0 of the first tile complete in buffer 0, units A0/B0 of K-tile 1
   // in flight (their steady-state slots are phases 7 and 8)
   {
@@ -309,6 +327,9 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
     for (int a = 0; a < NT; ++a)
 #pragma unroll
       for (int b = 0; b < 4; ++b) acc[a][b] = floatx4_t{0.f, 0.f, 0.f, 0.f};
+#ifdef GB_STAMPS
+    const uint64_t t0 = GB_T();
+#endif
 
     for (int kt = 0; kt < nk; kt += 2) {
       // the K-tiles staged in this iteration: kt+1 (rest of it), kt+2, kt+3 -- the last
@@ -375,7 +396,13 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
       __builtin_amdgcn_s_barrier();
       mma(1, 0, fb0);
       __builtin_amdgcn_s_barrier();
+#ifdef GB_STAMPS
+      if (kt == 0) t1 = GB_T();
+#endif
     }
+#ifdef GB_STAMPS
+    const uint64_t t2 = GB_T();
+#endif
 
     // ---- epilogue: acc[nt][mt] = D[n][m]; lane owns row m0 + wm*64 + mt*16 + l16 and
     // columns (n-tile nt) + lq*4 .. +3.  permlane16_swap over n-tile pairs (2p, 2p+1):
@@ -474,10 +501,34 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
       }
       if (flags & 32) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+#ifdef GB_STAMPS
+    {
+      const uint64_t t3 = GB_T();
+      a_it0 += t1 - t0;
+      a_rest += t2 - t1;
+      a_epi += t3 - t2;
+      ++ntl;
+    }
+#endif
     if (!has_next) break;
     tile = next;
   }
   if (half == 0) __builtin_amdgcn_s_barrier();  // equal barrier counts for both halves
+#ifdef GB_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const uint64_t s_k1 = GB_T(), s_r1 = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0) {
+    unsigned long long* o = gb_stamp_buf + (size_t)(bid * 8 + wid) * 8;
+    o[0] = a_it0;
+    o[1] = a_rest;
+    o[2] = a_epi;
+    o[3] = ntl;
+    o[4] = s_k1 - s_k0;
+    o[5] = s_r1 - s_r0;
+    o[6] = s_k0;
+    o[7] = s_r0;
+  }
+#endif
 }
 
 // grid: one workgroup per CU (at most), a multiple of 8 (XCD-slot tile walk)

@@ -556,8 +556,10 @@ class HipGemm:
         self._run_wgrad(dw2, dy, x, s, True)
 
     def wgrad_acc(self, dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
-        if dw.dtype == torch.bfloat16:  # a reduce-dtype gradient buffer (first and only write)
-            return self.wgrad_set(dw, dy, x)
+        """dw (fp32) += dy^T @ x.  A bf16 ``dw`` is refused: overwriting is ``wgrad_set``'s
+        contract, and silently switching to it would drop an earlier contribution."""
+        if dw.dtype == torch.bfloat16:
+            raise ValueError("wgrad_acc accumulates into fp32; use wgrad_set for a bf16 gradient")
         M, N = dy.shape
         K = x.shape[1]
         dw2 = dw.view(N, K)

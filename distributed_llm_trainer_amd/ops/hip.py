@@ -22,7 +22,7 @@ from . import rng
 _LIB = None
 # DLT_KERNEL_DEBUG=1 loads the bounds-checked build (ops/build.py --debug);
 # DLT_KERNEL_LIB=<file in ops/> loads another build of the same sources (same-box A/B
-# of a kernel change: scripts/ab_kernels.sh)
+# of a kernel change: tools/ab/ab_kernels.sh)
 _LIBPATH = os.path.join(os.path.dirname(os.path.abspath(__file__)),
                         "_dlt_kernels_debug.so" if os.environ.get("DLT_KERNEL_DEBUG") == "1"
                         else os.path.basename(os.environ.get("DLT_KERNEL_LIB", "_dlt_kernels.so")))

@@ -153,6 +153,13 @@ class FSDPRuntime(ParamProvider):
         self._free_module_params(model)
         self.hooks = None
 
+    @property
+    def collectives(self) -> bool:
+        """True when all-gathers / reduce-scatters go through the process group (several
+        ranks, or one rank with DLT_FORCE_COLLECTIVES=1): GPTEngine.window_schedule then
+        keeps the fb window."""
+        return bool(self.dist and (self.world > 1 or self.force))
+
     # ------------------------------------------------------------------ build
     def _unit_layout(self, uid):
         cfg = self.cfg

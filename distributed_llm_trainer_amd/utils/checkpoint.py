@@ -110,7 +110,9 @@ def _to_reference_pickle(payload: Dict[str, Any]):
 
 class _RefModules:
     """Make ``module.name`` resolve to the alias classes while pickling (pickle checks
-    that a class is importable under the path it writes), then restore sys.modules."""
+    that a class is importable under the path it writes), then restore sys.modules and
+    every attribute it set.  Process-wide while active: checkpoints are saved from the
+    trainer's main thread only."""
 
     def __init__(self, need):
         self.need = need
@@ -127,7 +129,12 @@ class _RefModules:
                     self.saved.append(("mod", mn, None))
                     sys.modules[mn] = types.ModuleType(mn)
                     if i > 1:
-                        setattr(sys.modules[".".join(parts[:i - 1])], parts[i - 1], sys.modules[mn])
+                        # the parent's attribute too: a real parent package imported
+                        # earlier must not keep pointing at the stand-in afterwards
+                        parent = ".".join(parts[:i - 1])
+                        pmod = sys.modules[parent]
+                        self.saved.append(("attr", parent, (parts[i - 1], getattr(pmod, parts[i - 1], _MISSING))))
+                        setattr(pmod, parts[i - 1], sys.modules[mn])
             mod = sys.modules[module]
             self.saved.append(("attr", module, (name, getattr(mod, name, _MISSING))))
             setattr(mod, name, alias)
@@ -138,10 +145,14 @@ class _RefModules:
         for kind, mn, extra in reversed(self.saved):
             if kind == "attr":
                 name, old = extra
+                mod = sys.modules.get(mn)
+                if mod is None:
+                    continue
                 if old is _MISSING:
-                    delattr(sys.modules[mn], name)
+                    if hasattr(mod, name):
+                        delattr(mod, name)
                 else:
-                    setattr(sys.modules[mn], name, old)
+                    setattr(mod, name, old)
             else:
                 sys.modules.pop(mn, None)
         return False

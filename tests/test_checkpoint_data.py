@@ -123,6 +123,20 @@ def test_checkpoint_readable_by_reference_loader(tmp_path):
     _ref_load(tmp_path / "again.pt", 64)
 
 
+def test_checkpoint_save_restores_existing_parent_package(tmp_path, monkeypatch):
+    """Saving with a real (unrelated) ``models`` package already imported must leave it
+    as it was: no ``models.config`` attribute pointing at the pickling stand-in."""
+    import sys
+    import types
+    real = types.ModuleType("models")
+    monkeypatch.setitem(sys.modules, "models", real)
+    cfg = GPTConfig(vocab_size=128, hidden_size=64, num_layers=1, num_heads=2, max_seq_len=32)
+    save_checkpoint(str(tmp_path / "c.pt"), {"model": {}, "model_config": cfg})
+    assert sys.modules["models"] is real and not hasattr(real, "config")
+    assert "models.config" not in sys.modules
+    assert load_checkpoint(str(tmp_path / "c.pt"))["model_config"].hidden_size == 64
+
+
 def test_fsdp_checkpoint_readable_by_reference_loader(tmp_path):
     """Same for the FSDP trainer's FULL_STATE_DICT file (adds __main__.FSDPConfig)."""
     from distributed_llm_trainer_amd.training.configs import FSDPConfig, FSDPTrainingConfig

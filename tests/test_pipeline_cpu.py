@@ -250,3 +250,28 @@ def test_window_schedule_choice(monkeypatch):
     monkeypatch.delenv("DLT_BWD_OVERLAP")
     monkeypatch.setenv("DLT_WINDOW_SCHED", "fb")
     assert e.window_schedule(2, True, cuda=True) == (True, "fb")
+    monkeypatch.delenv("DLT_WINDOW_SCHED")
+    # a provider that reports its own collectives (FSDPRuntime.collectives) keeps fb too
+    e.provider.hooks = None
+    e.provider.collectives = True
+    assert e.window_schedule(2, True, cuda=True) == (True, "fb")
+
+
+def test_wgrad_set_and_acc_contracts():
+    """wgrad_acc accumulates into fp32 and refuses bf16; wgrad_set overwrites a bf16
+    buffer (both GEMM backends: the FSDP bf16 send-buffer mode must not depend on which
+    one the engine uses)."""
+    from distributed_llm_trainer_amd.models.engine import _TorchGemm, _wgrad
+    g = _TorchGemm()
+    torch.manual_seed(0)
+    dy, x = torch.randn(64, 24), torch.randn(64, 16)
+    ref_ = dy.t() @ x
+    acc = torch.ones(24, 16)
+    g.wgrad_acc(acc, dy, x)
+    assert torch.allclose(acc, 1 + ref_, atol=1e-4)
+    db = torch.full((24, 16), float("nan"), dtype=torch.bfloat16)
+    _wgrad(g, db, dy.bfloat16(), x.bfloat16())
+    assert torch.isfinite(db.float()).all()
+    assert (db.float() - ref_).norm() / ref_.norm() < 2e-2
+    with pytest.raises(ValueError):
+        g.wgrad_acc(db, dy.bfloat16(), x.bfloat16())

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Attention kernel change: GPU numerics tests, standalone kernel timings (base vs new lib),
-# then an alternating bench.py A/B.  usage: bash scripts/ab_attn.sh [rounds]
+# then an alternating bench.py A/B.  usage: bash tools/ab/ab_attn.sh [rounds]
 set -u
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q -m gpu -k "attn or attention or dropout" --timeout 120 --timeout-method thread > gpurun_out/attn_tests.log 2>&1
@@ -12,4 +12,4 @@ for v in base new; do
     echo "$v B$b: $(tail -3 gpurun_out/attn_$v$b.log | tr '\n' ' ')"
   done
 done
-bash scripts/ab_kernels.sh ${1:-2}
+bash tools/ab/ab_kernels.sh ${1:-2}

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Same-box A/B of the decode kernels: ops/_dlt_kernels_base.so (scripts/build_base_lib.sh)
+# Same-box A/B of the decode kernels: ops/_dlt_kernels_base.so (tools/ab/build_base_lib.sh)
 # against the current ops/_dlt_kernels.so, tools/bench_decode.py, alternating.
 set -u
 mkdir -p gpurun_out

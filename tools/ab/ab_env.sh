@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of one env knob on one box: bench.py for each value, two alternating rounds.
-# usage: VAR=DLT_CE_CHUNKS VALUES="1 4 8" bash scripts/ab_env.sh
+# usage: VAR=DLT_CE_CHUNKS VALUES="1 4 8" bash tools/ab/ab_env.sh
 set -u
 mkdir -p gpurun_out
 for r in 1 2; do

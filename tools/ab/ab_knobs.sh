@@ -1,6 +1,6 @@
 #!/bin/bash
 # Same-box A/B of environment knobs on the default bench (alternating, 2 rounds).
-# usage: bash scripts/ab_knobs.sh "NAME=VAL ..." "NAME=VAL ..." ...   ("" = defaults)
+# usage: bash tools/ab/ab_knobs.sh "NAME=VAL ..." "NAME=VAL ..." ...   ("" = defaults)
 set -u
 mkdir -p gpurun_out
 for r in 1 2; do

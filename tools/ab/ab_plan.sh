@@ -1,6 +1,6 @@
 #!/bin/bash
 # Same-box A/B of two GEMM plan files over the bench-table configurations (alternating).
-# usage: bash scripts/ab_plan.sh PLAN_A PLAN_B
+# usage: bash tools/ab/ab_plan.sh PLAN_A PLAN_B
 set -u
 mkdir -p gpurun_out
 A=$1; B=$2

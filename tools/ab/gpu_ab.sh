@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU session: full -m gpu suite, then bench A/B over env toggles.  Stops at the first
-# fault / abort / timeout.  Usage: VARIANTS="DLT_PIPELINE=0 DLT_PACKED_QKV=0" bash scripts/gpu_ab.sh
+# fault / abort / timeout.  Usage: VARIANTS="DLT_PIPELINE=0 DLT_PACKED_QKV=0" bash tools/ab/gpu_ab.sh
 set -u
 mkdir -p gpurun_out
 if [ "${TESTS:-1}" = "1" ]; then

@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 hardware-counter passes (one rocprofv3 run per pass, counters within the
-# per-block limits; never combined with trace domains).  Usage: bash scripts/pmc.sh <tag> <python args...>
+# per-block limits; never combined with trace domains).  Usage: bash tools/ab/pmc.sh <tag> <python args...>
 set -u
 tag=$1; shift
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null

@@ -1,7 +1,7 @@
 #!/bin/bash
 # rocprofv3 kernel trace of bench.py for one (micro-batch, grad-accum) config, summarised
 # by tools/step_profile.py into gpurun_out/step_profile_B<b>_GA<g>.md
-#   usage: bash scripts/prof_cfg.sh B GA [extra bench args]
+#   usage: bash tools/ab/prof_cfg.sh B GA [extra bench args]
 set -u
 B=$1; GA=$2; shift 2
 mkdir -p gpurun_out

@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 kernel trace of bench.py + the last-step breakdown (tools/step_profile.py).
-# usage: [env knobs] bash scripts/prof_step.sh NAME [bench args]
+# usage: [env knobs] bash tools/ab/prof_step.sh NAME [bench args]
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export HSA_ENABLE_IPC_MODE_LEGACY=0

@@ -7,4 +7,4 @@ mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 200 --timeout-method thread \
   -k "wgrad or planner or stream" > gpurun_out/sk_tests.log 2>&1 || { tail -30 gpurun_out/sk_tests.log; exit 1; }
 tail -2 gpurun_out/sk_tests.log
-PLANS='sk: prev:splitk/32768x6144x768=-8,splitk/32768x50304x768=-2' bash scripts/r3b_plan_ab.sh
+PLANS='sk: prev:splitk/32768x6144x768=-8,splitk/32768x50304x768=-2' bash tools/ab/r3b_plan_ab.sh

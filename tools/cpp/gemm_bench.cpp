@@ -495,7 +495,9 @@ int main(int argc, char** argv) {
                              {"rowwalk", run_bf16<8>}, {"nostore", run_bf16<1>},   {"l2ops", run_bf16<2>},
                              {"l2nost", run_bf16<3>},    {"c0", run_bf16<16>},       {"stsync", run_bf16<32>},
                              {"nt", run_bf16<128>},      {"ntrow", run_bf16<132>},   {"np", run_bf16<256>},
-                             {"nprow", run_bf16<260>}};
+                             {"nprow", run_bf16<260>},   {"d4", run_bf16<512 | (4 << 24)>},
+                             {"d8", run_bf16<512 | (8 << 24)>}, {"d13", run_bf16<512 | (13 << 24)>},
+                             {"d20", run_bf16<512 | (20 << 24)>}};
   std::string only = (argc > 1 && strcmp(argv[1], "all")) ? std::string(",") + argv[1] + "," : "all";
   std::vector<int> shp;
   for (int i = 2; i < argc; ++i) shp.push_back(atoi(argv[i]));

@@ -1,4 +1,4 @@
-"""Summarise rocprofv3 --pmc passes (scripts/pmc.sh) into per-kernel hardware metrics.
+"""Summarise rocprofv3 --pmc passes (tools/ab/pmc.sh) into per-kernel hardware metrics.
 
 Per kernel name (averaged over its dispatches; counters of different passes are joined
 by kernel name, so each metric is an average over the same kind of dispatch):
