@@ -691,9 +691,12 @@ class GPTEngine:
             w, gr = prov.layer(i), prov.layer_grads(i)
             k_attn, k_resid, k_mlp = self._keys(st.micro, i)
             # MLP
-            ds = gm.linear_dgrad(g_d, w.wdown)
-            dgu = ops.swiglu_bwd(c.gu, ds, out=sb(i, "dgu", 2 * I))
-            del ds
+            if hasattr(gm, "linear_dgrad_swiglu"):  # down dgrad with the SwiGLU backward in its epilogue (when faster)
+                dgu = gm.linear_dgrad_swiglu(g_d, w.wdown, c.gu, ops, out=sb(i, "dgu", 2 * I))
+            else:
+                ds = gm.linear_dgrad(g_d, w.wdown)
+                dgu = ops.swiglu_bwd(c.gu, ds, out=sb(i, "dgu", 2 * I))
+                del ds
             dn2 = gm.linear_dgrad(dgu, w.wgu)
             dx2, da = ops.rmsnorm_bwd(dn2, c.x2, c.rstd2, w.ln2, g_x2, gr.ln2, ph, k_resid,
                                       ddelta_out=sb(i, "da", H))

@@ -37,6 +37,7 @@
 // Requirements (launcher-checked): M % 256 == 0, N % BN == 0, K % 128 == 0, rows
 // 16-byte aligned.
 #include "common.h"
+#include "gemm_common.h"
 
 #include <type_traits>
 
@@ -47,6 +48,11 @@ namespace {
 
 constexpr int GB_BM = 256;
 constexpr int GB_BK = 64;
+// LDS-transposed C stores (flags & 1024): per wave one 16-row x 96-column staging block,
+// rows padded to 104 elements (52 dwords: the 8-row lane groups of the ds_write_b128
+// land on disjoint banks)
+constexpr int GB_STG_ROW = 104;
+constexpr int GB_STG = 8 * 16 * GB_STG_ROW;
 
 __device__ __forceinline__ int gb_swz(int row, int chunk) { return row * GB_BK + ((chunk ^ ((row >> 1) & 7)) << 3); }
 
@@ -87,7 +93,11 @@ __device__ __forceinline__ int gb_brow(int q, int g) {
 //           GEMM output (elementwise.hip).
 //   SWIGLU: gu = A.Wgu^T (gate | up, [M, 2I]) and s = silu(g) * u ([M, I]) -- gpt.py:278-280;
 //           same math as k_swiglu_fwd on the bf16 gate/up values.
-enum { GB_EPI_STORE = 0, GB_EPI_ROPE = 1, GB_EPI_SWIGLU = 2 };
+//   SWIGLU_BWD (data-gradient form, BT): ds = dd . Wdown (the down projection's input
+//           gradient, [M, I]) and, per element, the SwiGLU backward of gpt.py:280 on the
+//           kept gu = [gate | up] (same math as k_swiglu_bwd on the bf16-rounded ds):
+//           dgu[:, j] = ds * u * sig(g) * (1 + g (1 - sig(g))), dgu[:, I + j] = ds * silu(g).
+enum { GB_EPI_STORE = 0, GB_EPI_ROPE = 1, GB_EPI_SWIGLU = 2, GB_EPI_SWIGLU_BWD = 3 };
 
 // Diagnostic build only (tools/cpp/gemm_bench.cpp defines GB_STAMPS): per-wave s_memtime
 // sums of the first K-iteration of a tile, the rest of its K-loop and its epilogue, plus
@@ -105,12 +115,13 @@ struct GbEpi {
   bf16_t* s_out;      // SWIGLU: s [M, ld_s]
   int ld_s;
   int I;              // SWIGLU: intermediate size (gate rows [0, I), up rows [I, 2I))
+  const bf16_t* gu_in;  // SWIGLU_BWD: kept gu [M, 2I] (row stride ld_s)
 };
 
 // Column (== B row) offset of wave-local n-tile t's first column within its tile.
 template <int BN, int EPI>
 __device__ __forceinline__ int gb_ncol(int wn, int t, int I) {
-  if constexpr (EPI == GB_EPI_STORE) {
+  if constexpr (EPI == GB_EPI_STORE || EPI == GB_EPI_SWIGLU_BWD) {
     return wn * (BN / 2) + t * 16;
   } else {
     const int P = wn * 48 + (t % 3) * 16;  // rotation pair / intermediate index
@@ -139,15 +150,25 @@ __device__ __forceinline__ void gb_unpack(uint2 p, float (&f)[4]) {
   f[3] = __uint_as_float(p.y & 0xffff0000u);
 }
 
-template <int BN, int EPI>
+// BT = false: C = A . B^T with B[N, K] (the forward projections, K contiguous in both).
+// BT = true (data gradients): C = A . B with B[K, N] read AS STORED -- dX = dY . W for a
+// weight W[Nred, Nout] -- the B staging units become reduction-major images (B0: 64
+// reduction rows x 128 columns = n-tiles 0..3 of both N halves, B1: 64 x 64 = n-tiles
+// 4..5), filled by LDS-DMA of whole 256 / 128-byte row pieces with a per-row XOR chunk
+// swizzle and read with ds_read_b64_tr_b16 (gemm_common.h, as k_gemm_wgrad reads its
+// token-major operands).  Same unit sizes and DMA counts per wave, so the 8-phase
+// schedule and its counted waits are unchanged.
+template <int BN, int EPI, bool BT = false>
 __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                       bf16_t* __restrict__ C, int M, int N, int K, int lda, int ldb,
                                                       int ldc, int flags, GbEpi ep) {
   static_assert(EPI == GB_EPI_STORE || BN == 192, "pair epilogues need the 192-column tile");
+  static_assert(!BT || (BN == 192 && (EPI == GB_EPI_STORE || EPI == GB_EPI_SWIGLU_BWD)),
+                "the reduction-major B form is the 192-column data-gradient kernel");
   using Cf = GbCfg<BN>;
   constexpr int TS = EPI == GB_EPI_SWIGLU ? 96 : BN;  // tile stride in B rows
   constexpr int NT = Cf::NT, NH = Cf::NH;
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * Cf::BUF];
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * Cf::BUF + GB_STG];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int half = wid >> 2;                  // stagger group (waves w and w+4 share a SIMD)
@@ -211,15 +232,31 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
     }
   // (the swizzle follows the LDS image row; the source row goes through the epilogue's
   // B-row map)
+  if constexpr (BT) {
+    // reduction-major B: DMA piece e of unit B0 = 16-byte chunk pc of reduction row t
+    // (16 chunks per 256-byte image row), source chunk lc = pc ^ 2 v(t) (gemm_common.h)
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int row = gb_brow<BN>(0, wid * 2 + j) + (lane >> 3);
-    ob0[j] = (uint32_t)(gb_bmap<BN, EPI>(row, ep.I) * ldb + (((lane & 7) ^ ((row >> 1) & 7)) << 3)) * 2u;
-  }
+    for (int j = 0; j < 2; ++j) {
+      const int e = (wid * 2 + j) * 64 + lane;
+      const int t = e >> 4, lc = (e & 15) ^ (2 * gw_v256(t));
+      ob0[j] = (uint32_t)(t * ldb + gw_b0map(lc * 8)) * 2u;
+    }
+    {
+      const int e = wid * 64 + lane;
+      const int t = e >> 3, lc = (e & 7) ^ (2 * gw_v128(t));
+      ob1[0] = (uint32_t)(t * ldb + gw_b1map(lc * 8)) * 2u;
+    }
+  } else {
 #pragma unroll
-  for (int j = 0; j < Cf::B1_DMA; ++j) {
-    const int row = gb_brow<BN>(1, wid * Cf::B1_DMA + j) + (lane >> 3);
-    ob1[j] = (uint32_t)(gb_bmap<BN, EPI>(row, ep.I) * ldb + (((lane & 7) ^ ((row >> 1) & 7)) << 3)) * 2u;
+    for (int j = 0; j < 2; ++j) {
+      const int row = gb_brow<BN>(0, wid * 2 + j) + (lane >> 3);
+      ob0[j] = (uint32_t)(gb_bmap<BN, EPI>(row, ep.I) * ldb + (((lane & 7) ^ ((row >> 1) & 7)) << 3)) * 2u;
+    }
+#pragma unroll
+    for (int j = 0; j < Cf::B1_DMA; ++j) {
+      const int row = gb_brow<BN>(1, wid * Cf::B1_DMA + j) + (lane >> 3);
+      ob1[j] = (uint32_t)(gb_bmap<BN, EPI>(row, ep.I) * ldb + (((lane & 7) ^ ((row >> 1) & 7)) << 3)) * 2u;
+    }
   }
 
   auto stA = [&](const bf16_t* g, int q, bf16_t* img) {
@@ -231,16 +268,21 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
   auto stB0 = [&](const bf16_t* g, bf16_t* img) {
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-      __builtin_amdgcn_global_load_lds((gb_gbl_cvptr_t)((const char*)g + ob0[j]),
-                                       (gb_lds_vptr_t)(img + gb_brow<BN>(0, wid * 2 + j) * GB_BK), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(
+          (gb_gbl_cvptr_t)((const char*)g + ob0[j]),
+          (gb_lds_vptr_t)(img + (BT ? (wid * 2 + j) * 512 : gb_brow<BN>(0, wid * 2 + j) * GB_BK)), 16, 0, 0);
   };
   auto stB1 = [&](const bf16_t* g, bf16_t* img) {
 #pragma unroll
     for (int j = 0; j < Cf::B1_DMA; ++j)
-      __builtin_amdgcn_global_load_lds((gb_gbl_cvptr_t)((const char*)g + ob1[j]),
-                                       (gb_lds_vptr_t)(img + gb_brow<BN>(1, wid * Cf::B1_DMA + j) * GB_BK), 16, 0,
-                                       0);
+      __builtin_amdgcn_global_load_lds(
+          (gb_gbl_cvptr_t)((const char*)g + ob1[j]),
+          (gb_lds_vptr_t)(img + (BT ? GW_IMG_A + wid * 512 : gb_brow<BN>(1, wid * Cf::B1_DMA + j) * GB_BK)), 16, 0,
+          0);
   };
+  // operand pointer of K-tile kt (relative): A and the K-major B advance along the row,
+  // the reduction-major B by whole rows
+  auto bk = [&](const bf16_t* g, int kt) { return BT ? g + (size_t)kt * GB_BK * ldb : g + kt * GB_BK; };
 
   floatx4_t acc[NT][4];
   bf16x8_t fa[2][2], fb0[NH][2], fb1[NH][2];
@@ -253,15 +295,51 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
       for (int s = 0; s < 2; ++s)
         fa[mt][s] = *reinterpret_cast<const bf16x8_t*>(img + gb_swz(arow + qm * 32 + mt * 16, s * 4 + lq));
   };
+  // BT: per-lane transposed-read bases (gemm_common.h): B0 n-tile k = 4 wn + nt, B1 k = 2 wn + j
+  uint32_t kb0[4], kb1[2];
+  if constexpr (BT) {
+    GwLane<256> L256;
+    GwLane<128> L128;
+    L256.init(lane);
+    L128.init(lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) kb0[j] = L256.base + L256.koff(4 * wn + j);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) kb1[j] = L128.base + L128.koff(2 * wn + j);
+  }
   auto read_b = [&](const bf16_t* img, int qn, bf16x8_t (&fb)[NH][2]) {
+    if constexpr (BT) {
+      // n-half 0: n-tiles 0..2 (B0); n-half 1: n-tile 3 (B0) and 4..5 (B1)
+      const uint32_t i0 = (uint32_t)(uintptr_t)img, i1 = i0 + GW_IMG_A * 2;
 #pragma unroll
-    for (int nt = 0; nt < NH; ++nt)
+      for (int s = 0; s < 2; ++s) {
+        if (qn == 0) {
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
-        fb[nt][s] = *reinterpret_cast<const bf16x8_t*>(img + gb_swz(brow + (qn * NH + nt) * 16, s * 4 + lq));
+          for (int nt = 0; nt < NH; ++nt) fb[nt][s] = gw_frag<256>(i0 + kb0[nt], s);
+        } else {
+          fb[0][s] = gw_frag<256>(i0 + kb0[3], s);
+          fb[1][s] = gw_frag<128>(i1 + kb1[0], s);
+          fb[2][s] = gw_frag<128>(i1 + kb1[1], s);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int nt = 0; nt < NH; ++nt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          fb[nt][s] = *reinterpret_cast<const bf16x8_t*>(img + gb_swz(brow + (qn * NH + nt) * 16, s * 4 + lq));
+    }
   };
   auto mma = [&](int qm, int qn, bf16x8_t (&fb)[NH][2]) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (BT) {
+      // the transposed reads are asm (invisible to the compiler's lgkmcnt tracking): the
+      // fragments are in/out operands of the wait so no MFMA is scheduled above it
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(fa[0][0]), "+v"(fa[0][1]), "+v"(fa[1][0]), "+v"(fa[1][1]), "+v"(fb[0][0]), "+v"(fb[0][1]),
+                     "+v"(fb[1][0]), "+v"(fb[1][1]), "+v"(fb[2][0]), "+v"(fb[2][1])::"memory");
+    } else {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
@@ -291,7 +369,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
     int tm, tn;
     coords(t, tm, tn);
     if (flags & 2) tn = 0;
-    return B + (size_t)(tn * TS) * ldb;
+    return BT ? B + (size_t)tn * TS : B + (size_t)(tn * TS) * ldb;
   };
 
   // flags & 512 (ablation only): the workgroups of odd XCD-slot rows start (flags >> 24) x
@@ -310,7 +388,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
     stB1(Bb, B0i);
     stA(Ab, 1, A0i);
     stA(Ab + GB_BK, 0, A1i);
-    stB0(Bb + GB_BK, B1i);
+    stB0(bk(Bb, 1), B1i);
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (half == 1) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 one barrier behind
@@ -337,12 +415,12 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
       const bool inner = kt + 2 < nk;
       const bool more = inner || has_next;
       const bf16_t* const A2 = inner ? Ab + (kt + 2) * GB_BK : An;
-      const bf16_t* const B2 = inner ? Bb + (kt + 2) * GB_BK : Bn;
+      const bf16_t* const B2 = inner ? bk(Bb, kt + 2) : Bn;
       // ---- phase 1: buffer 0, q0 ; stage B1 of K-tile kt+1
       read_b(B0i, 0, fb0);
       __builtin_amdgcn_sched_barrier(0);
       read_a(A0i, 0);
-      stB1(Bb + (kt + 1) * GB_BK, B1i);
+      stB1(bk(Bb, kt + 1), B1i);
       __builtin_amdgcn_s_barrier();
       mma(0, 0, fb0);
       __builtin_amdgcn_s_barrier();
@@ -390,7 +468,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
       __builtin_amdgcn_s_barrier();
       // ---- phase 8: q3 ; B0 of kt+3 ; retire K-tile kt+2
       if (more) {
-        stB0(B2 + GB_BK, B1i);
+        stB0(bk(B2, 1), B1i);
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       }
       __builtin_amdgcn_s_barrier();
@@ -481,6 +559,34 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
           *reinterpret_cast<uint2*>(srow + 32 + lq * 4) = sp[2];
         }
         bf16_t* crow = C + (size_t)row * ldc + n0;
+        if (EPI == GB_EPI_STORE && !BT && (flags & 1024)) {
+          // LDS-transposed stores: the lane's three 16-byte chunks (8 consecutive columns
+          // each) go to the wave's staging block, then every store instruction writes
+          // 5.33 whole 192-byte row segments (12 lanes per row, consecutive lanes on
+          // consecutive 16 bytes) instead of 16 rows x 64 bytes.  Wave-local: the wave
+          // reads back only what it wrote (LDS operations of one wave stay in order).
+          bf16_t* stg = lds + 2 * Cf::BUF + wid * (16 * GB_STG_ROW);
+#pragma unroll
+          for (int p = 0; p < NT / 2; ++p) {
+            uint32_t x[2] = {pk[2 * p].x, pk[2 * p].y}, y[2] = {pk[2 * p + 1].x, pk[2 * p + 1].y};
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              auto sw = __builtin_amdgcn_permlane16_swap(x[h], y[h], false, false);
+              x[h] = sw[0];
+              y[h] = sw[1];
+            }
+            const int chunk = 4 * p + 2 * (lq & 1) + (lq >> 1);
+            *reinterpret_cast<gb_u32x4_t*>(stg + l16 * GB_STG_ROW + chunk * 8) = gb_u32x4_t{x[0], x[1], y[0], y[1]};
+          }
+          bf16_t* cblk = C + (size_t)(m0 + wm * 64 + mt * 16) * ldc + n0 + wn * 96;
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            const int e = i * 64 + lane, r = e / 12, c = e - r * 12;
+            const gb_u32x4_t v = *reinterpret_cast<const gb_u32x4_t*>(stg + r * GB_STG_ROW + c * 8);
+            *reinterpret_cast<gb_u32x4_t*>(cblk + (size_t)r * ldc + c * 8) = v;
+          }
+          continue;
+        }
 #pragma unroll
         for (int p = 0; p < NT / 2; ++p) {
           uint32_t x[2] = {pk[2 * p].x, pk[2 * p].y}, y[2] = {pk[2 * p + 1].x, pk[2 * p + 1].y};
@@ -491,12 +597,40 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
             y[h] = sw[1];
           }
           const int t = 2 * p + (lq & 1);
-          gb_u32x4_t* cp = reinterpret_cast<gb_u32x4_t*>(crow + gb_ncol<BN, EPI>(wn, t, ep.I) + (lq >> 1) * 8);
+          const int col = gb_ncol<BN, EPI>(wn, t, ep.I) + (lq >> 1) * 8;
           const gb_u32x4_t cv = {x[0], x[1], y[0], y[1]};
-          if (flags & 128)  // nontemporal (streaming) C stores
-            __builtin_nontemporal_store(cv, cp);
-          else
-            *cp = cv;
+          if constexpr (EPI == GB_EPI_SWIGLU_BWD) {
+            // 8 consecutive ds values (bf16-rounded, as the unfused kernel reads them)
+            // against the kept gate / up values of the same columns; C = dgu [M, 2I]
+            const bf16_t* grow = ep.gu_in + (size_t)row * ep.ld_s + n0 + col;
+            const gb_u32x4_t gv = *reinterpret_cast<const gb_u32x4_t*>(grow);
+            const gb_u32x4_t uv = *reinterpret_cast<const gb_u32x4_t*>(grow + ep.I);
+            gb_u32x4_t og, ou;
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+              float d[2] = {__uint_as_float(cv[h] << 16), __uint_as_float(cv[h] & 0xffff0000u)};
+              float g[2] = {__uint_as_float(gv[h] << 16), __uint_as_float(gv[h] & 0xffff0000u)};
+              float u[2] = {__uint_as_float(uv[h] << 16), __uint_as_float(uv[h] & 0xffff0000u)};
+              floatx4_t r;
+#pragma unroll
+              for (int e = 0; e < 2; ++e) {
+                const float sg = dlt_sigmoid(g[e]);
+                r[e] = d[e] * u[e] * sg * (1.f + g[e] * (1.f - sg));
+                r[2 + e] = d[e] * g[e] * sg;
+              }
+              const uint2 pr = gb_pack(r);  // (dg0, dg1), (du0, du1)
+              og[h] = pr.x;
+              ou[h] = pr.y;
+            }
+            *reinterpret_cast<gb_u32x4_t*>(crow + col) = og;
+            *reinterpret_cast<gb_u32x4_t*>(crow + ep.I + col) = ou;
+          } else {
+            gb_u32x4_t* cp = reinterpret_cast<gb_u32x4_t*>(crow + col);
+            if (flags & 128)  // nontemporal (streaming) C stores
+              __builtin_nontemporal_store(cv, cp);
+            else
+              *cp = cv;
+          }
         }
       }
       if (flags & 32) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -571,6 +705,30 @@ DLT_API int dlt_gemm_bf16_qkv_rope(const bf16_t* A, const bf16_t* W, bf16_t* C, 
   GbEpi ep{cosT, sinT, S, 2 * H, nullptr, 0, 0};
   const int ntiles = (M / 256) * (N / 192);
   k_gemm_bf16<192, GB_EPI_ROPE><<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(A, W, C, M, N, K, K, K, N, flags, ep);
+  DLT_CHECK_LAUNCH();
+}
+
+// Data gradient dX[M, Nout] = dY[M, Nred] . W[Nred, Nout] with W read as stored (the
+// input gradients of every projection: q/k/v, o, gate/up, down and the tied lm_head).
+DLT_API int dlt_gemm_bf16_nn(const bf16_t* dY, const bf16_t* W, bf16_t* dX, int M, int Nout, int Nred, int ldy,
+                             int ldw, int ldx, int flags, hipStream_t st) {
+  if (!gb_shape_ok(M, Nout, Nred, ldy, ldw, ldx) || Nout % 192) return -1;
+  const int ntiles = (M / 256) * (Nout / 192);
+  GbEpi ep{};
+  k_gemm_bf16<192, GB_EPI_STORE, true>
+      <<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(dY, W, dX, M, Nout, Nred, ldy, ldw, ldx, flags, ep);
+  DLT_CHECK_LAUNCH();
+}
+
+// Down-projection data gradient fused with the SwiGLU backward: ds = dd[M, H] . Wdown[H, I]
+// (bf16-rounded) and dgu[M, 2I] from ds and the kept gu[M, 2I] (k_swiglu_bwd's math).
+DLT_API int dlt_gemm_bf16_down_swiglu_bwd(const bf16_t* dd, const bf16_t* Wdown, const bf16_t* gu, bf16_t* dgu, int M,
+                                          int I, int H, int flags, hipStream_t st) {
+  if (!gb_shape_ok(M, I, H, H, I, 2 * I) || I % 192) return -1;
+  const int ntiles = (M / 256) * (I / 192);
+  GbEpi ep{nullptr, nullptr, 1, 0, nullptr, 2 * I, I, gu};
+  k_gemm_bf16<192, GB_EPI_SWIGLU_BWD, true>
+      <<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(dd, Wdown, dgu, M, I, H, H, I, 2 * I, flags, ep);
   DLT_CHECK_LAUNCH();
 }
 

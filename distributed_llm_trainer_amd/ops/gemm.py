@@ -289,6 +289,7 @@ class HipGemm:
         self._splitk_on = os.environ.get("DLT_WGRAD_SPLITK", "1") != "0"
         self._hand_wgrad = os.environ.get("DLT_WGRAD_HAND", "1") != "0"
         self._fuse = os.environ.get("DLT_GEMM_FUSED", "1") != "0"
+        self._dgrad_on = os.environ.get("DLT_GEMM_DGRAD", "1") != "0"
         _INSTANCES.append(weakref.ref(self))
 
     def _lib_linear(self, x, w, y):
@@ -333,13 +334,17 @@ class HipGemm:
             self._lib_linear(x, w, y)
         return y
 
-    def _fused_pick(self, kind, x, w, fused, unfused) -> bool:
-        if not (self._fuse and self._hand_ok(x, w)):
+    def _fused_pick(self, kind, x, w, fused, unfused, key=None) -> bool:
+        """Race a hand-written kernel (``fused``) against its library equivalent once
+        per key; kinds "rope" / "swiglu" / "dswiglu" are fused epilogues
+        (``DLT_GEMM_FUSED=0`` turns them off), "dgrad" the plain data-gradient GEMM."""
+        on = self._fuse if kind != "dgrad" else True
+        if not (on and self._hand_ok(x, w)):
             return False
-        key = (kind, x.shape[0], w.shape[0], x.shape[1])
+        key = key or (kind, x.shape[0], w.shape[0], x.shape[1])
         choice = self._choice.get(key)
         if choice is None:
-            if not (self._fuse and self._can_race(x, w)):
+            if not self._can_race(x, w):
                 return False  # not recorded: decided again when racing is possible
             choice = _time_of(fused, inner=3) < self.RACE_MARGIN * _time_of(unfused, inner=3)
             self._choice[key] = choice
@@ -393,7 +398,9 @@ class HipGemm:
     def report_choices(self) -> dict:
         out = {f"M{k[0]}xN{k[1]}xK{k[2]}": ("hipBLASLt" if c is None else "hand-written gemm_bf16")
                for k, c in self._choice.items() if len(k) == 3}
-        out.update({f"{k[0]} M{k[1]}xN{k[2]}xK{k[3]}": ("fused gemm_bf16" if c else "unfused (linear + kernel)")
+        out.update({f"{k[0]} M{k[1]}xN{k[2]}xK{k[3]}": (("hand-written gemm_dgrad" if c else "hipBLASLt")
+                                                       if k[0] == "dgrad" else
+                                                       ("fused gemm_bf16" if c else "unfused (linear + kernel)"))
                     for k, c in self._choice.items() if len(k) == 4})
         out.update({f"wgrad{' (bf16 out)' if len(key) == 4 else ''} M{key[0]}xN{key[1]}xK{key[2]}":
                     ("hand-written gemm_wgrad stream-K" if s == self.STREAMK else
@@ -402,12 +409,51 @@ class HipGemm:
                     for key, s in self._splitk.items()})
         return out
 
-    def linear_dgrad(self, dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    def _lib_dgrad(self, dy, w, dx):
         M, N = dy.shape
         K = w.shape[1]
-        dx = torch.empty(M, K, dtype=dy.dtype, device=dy.device)
         _gemm(0, 0, K, M, N, w, _rowmajor(w), dy, _rowmajor(dy), dx, K)
+
+    def linear_dgrad(self, dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
+        """dX[M, K] = dY[M, N] @ W[N, K]: the hand-written reduction-major-B kernel
+        (``hip.gemm_dgrad``, W read as stored) or hipBLASLt, raced once per shape (kind
+        "dgrad" in the plan's "fused" table; ``DLT_GEMM_DGRAD=0``: library only)."""
+        from . import hip
+        M, N = dy.shape
+        K = w.shape[1]
+        dx = torch.empty(M, K, dtype=dy.dtype, device=dy.device) if out is None else out
+        ok = self._dgrad_on and self._race and hip.gemm_bf16_fits(M, K, N) and self._hand_ok(dy, w, dx)
+        if ok and self._fused_pick("dgrad", dy, w, lambda: hip.gemm_dgrad(dy, w, out=dx),
+                                   lambda: self._lib_dgrad(dy, w, dx), key=("dgrad", M, K, N)):
+            hip.gemm_dgrad(dy, w, out=dx)
+        else:
+            self._lib_dgrad(dy, w, dx)
         return dx
+
+    def linear_dgrad_swiglu(self, dd: torch.Tensor, wdown: torch.Tensor, gu: torch.Tensor, ops,
+                            out: torch.Tensor = None) -> torch.Tensor:
+        """dgu[M, 2I]: the down projection's data gradient ds = dd @ Wdown and the SwiGLU
+        backward against the kept gu, fused in one hand-written kernel
+        (``hip.gemm_down_swiglu_bwd``) or as ``linear_dgrad`` + ``ops.swiglu_bwd`` --
+        raced once per shape (kind "dswiglu")."""
+        from . import hip
+        M, H = dd.shape
+        I = wdown.shape[1]
+        dgu = torch.empty(M, 2 * I, dtype=dd.dtype, device=dd.device) if out is None else out
+
+        def unfused():
+            ds = self.linear_dgrad(dd, wdown)
+            ops.swiglu_bwd(gu, ds, out=dgu)
+
+        def fused():
+            hip.gemm_down_swiglu_bwd(dd, wdown, gu, out=dgu)
+        ok = (self._dgrad_on and hip.gemm_bf16_fits(M, I, H) and tuple(gu.shape) == (M, 2 * I)
+              and self._hand_ok(gu, dgu))
+        if ok and self._fused_pick("dswiglu", dd, wdown, fused, unfused, key=("dswiglu", M, I, H)):
+            fused()
+        else:
+            unfused()
+        return dgu
 
     @staticmethod
     def _wgrad_plain(dw2, dy, x):

@@ -62,6 +62,8 @@ _SIGS = {
     "dlt_gemm_bf16_qkv_rope": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                                c_void_p],
     "dlt_gemm_bf16_gu_swiglu": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
+    "dlt_gemm_bf16_nn": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "dlt_gemm_bf16_down_swiglu_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
     "dlt_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                      c_uint32, c_uint32, c_float, c_int, c_void_p],
     "dlt_attn_dropout_mask": [c_void_p, c_int, c_int, c_int, c_uint32, c_uint32, c_void_p],
@@ -788,6 +790,43 @@ def gemm_gu_swiglu(x: torch.Tensor, wgu: torch.Tensor, gu_out: Optional[torch.Te
     _req(s, torch.bfloat16, "gemm_gu_swiglu.s", M * I)
     _chk(lib().dlt_gemm_bf16_gu_swiglu(_p(x), _p(wgu), _p(gu), _p(s), M, I, K, _GB_FLAGS, _stream()), "gemm_gu_swiglu")
     return gu, s
+
+
+def gemm_dgrad(dy: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """dX[M, Nout] = dY[M, Nred] @ W[Nred, Nout] with W read as stored (the data gradient
+    of a projection y = x @ W^T) by the hand-written persistent MFMA kernel in its
+    reduction-major-B form.  None (nothing launched) when the shape does not tile
+    (M % 256, Nout % 192, Nred % 128)."""
+    M, Nred = dy.shape
+    Nout = w.shape[1]
+    if not gemm_bf16_fits(M, Nout, Nred) or w.shape[0] != Nred:
+        return None
+    _req(dy, torch.bfloat16, "gemm_dgrad.dy")
+    _req(w, torch.bfloat16, "gemm_dgrad.w")
+    c = torch.empty(M, Nout, dtype=torch.bfloat16, device=dy.device) if out is None else out
+    _req(c, torch.bfloat16, "gemm_dgrad.out", M * Nout)
+    _chk(lib().dlt_gemm_bf16_nn(_p(dy), _p(w), _p(c), M, Nout, Nred, Nred, Nout, Nout, _GB_FLAGS, _stream()),
+         "gemm_dgrad")
+    return c
+
+
+def gemm_down_swiglu_bwd(dd: torch.Tensor, wdown: torch.Tensor, gu: torch.Tensor,
+                         out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """dgu[M, 2I] = SwiGLU backward of ds = dd[M, H] @ Wdown[H, I] (bf16-rounded) against
+    the kept gu[M, 2I] -- the down projection's data gradient and ``swiglu_bwd`` in one
+    kernel (same math and roundings as the unfused pair).  None if it does not tile."""
+    M, H = dd.shape
+    I = wdown.shape[1]
+    if not gemm_bf16_fits(M, I, H) or wdown.shape[0] != H or tuple(gu.shape) != (M, 2 * I):
+        return None
+    _req(dd, torch.bfloat16, "gemm_down_swiglu_bwd.dd")
+    _req(wdown, torch.bfloat16, "gemm_down_swiglu_bwd.w")
+    _req(gu, torch.bfloat16, "gemm_down_swiglu_bwd.gu")
+    c = torch.empty(M, 2 * I, dtype=torch.bfloat16, device=dd.device) if out is None else out
+    _req(c, torch.bfloat16, "gemm_down_swiglu_bwd.out", M * 2 * I)
+    _chk(lib().dlt_gemm_bf16_down_swiglu_bwd(_p(dd), _p(wdown), _p(gu), _p(c), M, I, H, _GB_FLAGS, _stream()),
+         "gemm_down_swiglu_bwd")
+    return c
 
 
 def scale_bf16(x: torch.Tensor, scale: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:

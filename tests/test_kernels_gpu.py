@@ -565,6 +565,69 @@ def test_gemm_gu_swiglu(M, I, K):
     _close(s, ws, 1e-2 * ws.abs().max().item(), 1e-2, "swiglu s")
 
 
+@pytest.mark.parametrize("M,Nout,Nred", [(512, 768, 2304), (512, 768, 768), (256, 768, 6144), (512, 3072, 768),
+                                          (256, 768, 50304), (256, 1600, 4800), (512, 192, 128)])
+def test_gemm_dgrad_vs_fp32(M, Nout, Nred):
+    """Data gradient dX = dY @ W (W[Nred, Nout] read as stored) on the hand-written
+    reduction-major-B kernel against the fp32 product -- every dgrad role of the step
+    (q/k/v 2304, o 768, gate/up 6144, down 768 -> 3072, lm_head 50304) plus shapes that do
+    not tile (None, nothing launched)."""
+    torch.manual_seed(Nred)
+    dy = (torch.rand(M, Nred, device=DEV) * 2 - 1).bfloat16()
+    w = ((torch.rand(Nred, Nout, device=DEV) * 2 - 1) / Nred ** 0.5).bfloat16()
+    r = hip.gemm_dgrad(dy, w)
+    if Nout % 192:
+        assert r is None
+        return
+    want = dy.float() @ w.float()
+    assert torch.isfinite(r.float()).all()
+    assert _relerr(r, want) < 8e-3, _relerr(r, want)
+
+
+def test_gemm_down_swiglu_bwd_vs_fp32():
+    """Down-projection dgrad with the SwiGLU backward in the epilogue == the fp32 product
+    rounded to bf16 (what the unfused dgrad writes) through k_swiglu_bwd's math, and ==
+    hip.swiglu_bwd on the library dgrad within bf16 rounding."""
+    torch.manual_seed(7)
+    M, H, I = 512, 768, 3072
+    dd = (torch.rand(M, H, device=DEV) * 2 - 1).bfloat16()
+    wd = ((torch.rand(H, I, device=DEV) * 2 - 1) / H ** 0.5).bfloat16()
+    gu = (torch.randn(M, 2 * I, device=DEV) * 2).bfloat16()
+    dgu = hip.gemm_down_swiglu_bwd(dd, wd, gu)
+    ds = (dd.float() @ wd.float()).bfloat16().float()
+    g, u = gu.float()[:, :I], gu.float()[:, I:]
+    sg = torch.sigmoid(g)
+    want = torch.cat([ds * u * sg * (1 + g * (1 - sg)), ds * g * sg], dim=1)
+    assert torch.isfinite(dgu.float()).all()
+    assert _relerr(dgu, want) < 1.5e-2, _relerr(dgu, want)
+    ref_k = hip.swiglu_bwd(gu, (dd.float() @ wd.float()).bfloat16())
+    assert _relerr(dgu, ref_k.float()) < 1.5e-2
+
+
+def test_planner_dgrad_races_match_library():
+    """HipGemm.linear_dgrad / linear_dgrad_swiglu (whatever the race picks) == the
+    library dgrad (+ swiglu_bwd); the choices are recorded under kinds dgrad / dswiglu."""
+    from distributed_llm_trainer_amd.ops import gemm
+    torch.manual_seed(5)
+    g = gemm.HipGemm()
+    M, H, I = 4096, 768, 3072
+    dy = (torch.rand(M, 3 * H, device=DEV) * 2 - 1).bfloat16()
+    w = ((torch.rand(3 * H, H, device=DEV) * 2 - 1) / H ** 0.5).bfloat16()
+    dx = g.linear_dgrad(dy, w)
+    dx2 = torch.empty_like(dx)
+    g._lib_dgrad(dy, w, dx2)
+    assert _relerr(dx, dx2.float()) < 1e-2
+    dd = (torch.rand(M, H, device=DEV) * 2 - 1).bfloat16()
+    wd = ((torch.rand(H, I, device=DEV) * 2 - 1) / H ** 0.5).bfloat16()
+    gu = (torch.randn(M, 2 * I, device=DEV) * 2).bfloat16()
+    dgu = g.linear_dgrad_swiglu(dd, wd, gu, hip)
+    ds = torch.empty(M, I, dtype=torch.bfloat16, device=DEV)
+    g._lib_dgrad(dd, wd, ds)
+    assert _relerr(dgu, hip.swiglu_bwd(gu, ds).float()) < 1.5e-2
+    kinds = {k[0] for k in g._choice if len(k) == 4}
+    assert {"dgrad", "dswiglu"} <= kinds
+
+
 def test_planner_fused_races_match_unfused():
     """HipGemm.linear_rope / linear_swiglu (whatever the race picks) == the unfused
     library GEMM + kernel, and the choices are recorded process-wide."""

@@ -263,6 +263,171 @@ static int epi_main(int M, int H, int I, int S) {
   return 0;
 }
 
+// ---------------------------------------------------------------- data gradients
+// dX[M, Nout] = dY[M, Nred] . W[Nred, Nout] (W as stored): k_gemm_bf16<.., BT = true> vs
+// hipBLASLt (N, N), and the down-projection dgrad fused with the SwiGLU backward vs
+// hipBLASLt + k_swiglu_bwd.
+__global__ void k_ref_nn(const bf16_t* A, const bf16_t* W, float* C, int r0, int nr, int N, int K) {
+  int n = blockIdx.x * blockDim.x + threadIdx.x;
+  int m = blockIdx.y;
+  if (n >= N || m >= nr) return;
+  const bf16_t* a = A + (size_t)(r0 + m) * K;
+  float s = 0.f;
+  for (int k = 0; k < K; ++k) s += bf2f(a[k]) * bf2f(W[(size_t)k * N + n]);
+  C[(size_t)m * N + n] = s;
+}
+
+static BlasPlan g_plan_nn;
+static int run_blas_nn(const bf16_t* A, const bf16_t* W, bf16_t* C, int M, int N, int K, hipStream_t s) {
+  float alpha = 1.f, beta = 0.f;
+  if (!g_h) {
+    hipblasLtCreate(&g_h);
+    CK(hipMalloc(&g_ws, g_wsz));
+  }
+  BlasPlan& p = g_plan_nn;
+  if (p.M != M || p.N != N || p.K != K) {
+    p.M = M, p.N = N, p.K = K, p.ok = false;
+    hipblasLtMatmulDescCreate(&p.md, HIPBLAS_COMPUTE_32F, HIP_R_32F);
+    hipblasOperation_t ta = HIPBLAS_OP_N, tb = HIPBLAS_OP_N;
+    hipblasLtMatmulDescSetAttribute(p.md, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta));
+    hipblasLtMatmulDescSetAttribute(p.md, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb));
+    hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, N, K, N);  // W row-major [K, N] = col-major [N, K]
+    hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, K, M, K);  // dY row-major [M, K] = col-major [K, M]
+    hipblasLtMatrixLayoutCreate(&p.lc, HIP_R_16BF, N, M, N);
+    hipblasLtMatmulPreference_t pref;
+    hipblasLtMatmulPreferenceCreate(&pref);
+    hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &g_wsz, sizeof(g_wsz));
+    hipblasLtMatmulHeuristicResult_t res[24];
+    int n = 0;
+    hipblasLtMatmulAlgoGetHeuristic(g_h, p.md, p.la, p.lb, p.lc, p.lc, pref, 24, res, &n);
+    float best = 1e30f;
+    for (int i = 0; i < n; ++i) {
+      if (res[i].workspaceSize > g_wsz) continue;
+      if (hipblasLtMatmul(g_h, p.md, &alpha, W, p.la, A, p.lb, &beta, C, p.lc, C, p.lc, &res[i].algo, g_ws, g_wsz, s))
+        continue;
+      const float t = time_us(
+          [&]() {
+            return (int)hipblasLtMatmul(g_h, p.md, &alpha, W, p.la, A, p.lb, &beta, C, p.lc, C, p.lc, &res[i].algo,
+                                        g_ws, g_wsz, s);
+          },
+          s, 3);
+      if (t < best) best = t, p.algo = res[i].algo, p.ok = true;
+    }
+  }
+  if (!p.ok) return -5;
+  return (int)hipblasLtMatmul(g_h, p.md, &alpha, W, p.la, A, p.lb, &beta, C, p.lc, C, p.lc, &p.algo, g_ws, g_wsz, s);
+}
+
+static int dgrad_main(std::vector<int> shp) {
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  for (size_t si = 0; si + 2 < shp.size(); si += 3) {
+    const int M = shp[si], N = shp[si + 1], K = shp[si + 2];  // dX[M, N] = dY[M, K] . W[K, N]
+    bf16_t *A, *W, *C;
+    CK(hipMalloc(&A, (size_t)M * K * 2));
+    CK(hipMalloc(&W, (size_t)K * N * 2));
+    CK(hipMalloc(&C, (size_t)M * N * 2));
+    k_fill<<<1024, 256, 0, st>>>(A, (size_t)M * K, 21);
+    k_fill<<<1024, 256, 0, st>>>(W, (size_t)K * N, 22);
+    const int nr = 32, r0 = (M / 3) & ~7;
+    float* R;
+    CK(hipMalloc(&R, (size_t)nr * N * 4));
+    k_ref_nn<<<dim3((N + 255) / 256, nr), 256, 0, st>>>(A, W, R, r0, nr, N, K);
+    std::vector<float> ref((size_t)nr * N);
+    CK(hipMemcpyAsync(ref.data(), R, ref.size() * 4, hipMemcpyDeviceToHost, st));
+    CK(hipStreamSynchronize(st));
+    const double fl = 2.0 * M * N * K;
+    printf("dgrad M=%d N=%d K=%d:", M, N, K);
+    for (int v = 0; v < 3; ++v) {
+      auto fn = [&]() {
+        if (v == 2) return run_blas_nn(A, W, C, M, N, K, st);
+        return dlt_gemm_bf16_nn(A, W, C, M, N, K, K, N, N, v == 1 ? 1 : 0, st);
+      };
+      CK(hipMemsetAsync(C, 0xff, (size_t)M * N * 2, st));
+      int rc = fn();
+      if (rc) {
+        printf(" | v%d n/a(%d)", v, rc);
+        continue;
+      }
+      CK(hipStreamSynchronize(st));
+      double e = 0, mref = 0;
+      if (v != 1) {
+        std::vector<bf16_t> got((size_t)nr * N);
+        CK(hipMemcpy(got.data(), C + (size_t)r0 * N, got.size() * 2, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < got.size(); ++i) {
+          const double d = std::fabs((double)bff(got[i]) - ref[i]);
+          if (!(d <= e)) e = d;
+          mref = std::fmax(mref, std::fabs(ref[i]));
+        }
+      }
+      const float t = time_us(fn, st);
+      printf(" | %s %7.1f us %5.0f TF err %.1e", v == 0 ? "hand" : v == 1 ? "nostore" : "blas", t, fl / t / 1e6,
+             mref > 0 ? e / mref : 0.0);
+      fflush(stdout);
+    }
+    printf("\n");
+    CK(hipFree(A));
+    CK(hipFree(W));
+    CK(hipFree(C));
+    CK(hipFree(R));
+  }
+  // down dgrad + SwiGLU backward (M 16384, H 768, I 3072)
+  {
+    const int M = 16384, H = 768, I = 3072;
+    bf16_t *dd, *Wd, *gu, *dgu, *dgu2, *ds;
+    CK(hipMalloc(&dd, (size_t)M * H * 2));
+    CK(hipMalloc(&Wd, (size_t)H * I * 2));
+    CK(hipMalloc(&gu, (size_t)M * 2 * I * 2));
+    CK(hipMalloc(&dgu, (size_t)M * 2 * I * 2));
+    CK(hipMalloc(&dgu2, (size_t)M * 2 * I * 2));
+    CK(hipMalloc(&ds, (size_t)M * I * 2));
+    k_fill<<<1024, 256, 0, st>>>(dd, (size_t)M * H, 31);
+    k_fill<<<1024, 256, 0, st>>>(Wd, (size_t)H * I, 32);
+    k_fill<<<1024, 256, 0, st>>>(gu, (size_t)M * 2 * I, 33);
+    const int nr = 32, r0 = (M / 3) & ~7;
+    float* R;
+    CK(hipMalloc(&R, (size_t)nr * I * 4));
+    k_ref_nn<<<dim3((I + 255) / 256, nr), 256, 0, st>>>(dd, Wd, R, r0, nr, I, H);
+    std::vector<float> ref((size_t)nr * I);
+    std::vector<bf16_t> hgu((size_t)nr * 2 * I), got((size_t)nr * 2 * I);
+    CK(hipMemcpyAsync(ref.data(), R, ref.size() * 4, hipMemcpyDeviceToHost, st));
+    CK(hipMemcpyAsync(hgu.data(), gu + (size_t)r0 * 2 * I, hgu.size() * 2, hipMemcpyDeviceToHost, st));
+    auto fused = [&]() { return dlt_gemm_bf16_down_swiglu_bwd(dd, Wd, gu, dgu, M, I, H, 0, st); };
+    auto unfused = [&]() {
+      int rc = run_blas_nn(dd, Wd, ds, M, I, H, st);
+      return rc ? rc : dlt_swiglu_bwd(gu, ds, dgu2, M, I, st);
+    };
+    CK(hipMemsetAsync(dgu, 0xff, (size_t)M * 2 * I * 2, st));
+    if (fused()) {
+      printf("fused down+swiglu_bwd launch failed\n");
+      return 1;
+    }
+    CK(hipStreamSynchronize(st));
+    CK(hipMemcpy(got.data(), dgu + (size_t)r0 * 2 * I, got.size() * 2, hipMemcpyDeviceToHost));
+    double e = 0, mref = 0;
+    for (int r = 0; r < nr; ++r)
+      for (int c = 0; c < I; ++c) {
+        const float d = bfr(ref[(size_t)r * I + c]);
+        const float g = bff(hgu[(size_t)r * 2 * I + c]), u = bff(hgu[(size_t)r * 2 * I + I + c]);
+        const float sg = 1.f / (1.f + expf(-g));
+        const float w0 = d * u * sg * (1.f + g * (1.f - sg)), w1 = d * g * sg;
+        const double e0 = std::fabs((double)bff(got[(size_t)r * 2 * I + c]) - w0);
+        const double e1 = std::fabs((double)bff(got[(size_t)r * 2 * I + I + c]) - w1);
+        e = std::fmax(e, std::fmax(e0, e1));
+        if (!(e0 == e0) || !(e1 == e1)) e = NAN;
+        mref = std::fmax(mref, std::fmax(std::fabs(w0), std::fabs(w1)));
+      }
+    const float tf = time_us(fused, st), tu = time_us(unfused, st);
+    const float tb = time_us([&]() { return run_blas_nn(dd, Wd, ds, M, I, H, st); }, st);
+    const float th = time_us([&]() { return dlt_gemm_bf16_nn(dd, Wd, ds, M, I, H, H, I, I, 0, st); }, st);
+    printf("down dgrad + swiglu_bwd: fused %.1f us | hipBLASLt + k_swiglu_bwd %.1f us (dgrad alone %.1f, hand dgrad "
+           "alone %.1f) | err %.1e\n",
+           tf, tu, tb, th, mref > 0 ? e / mref : 0.0);
+    fflush(stdout);
+  }
+  return 0;
+}
+
 // dW[Nr, Nc] += dY[T, Nr]^T X[T, Nc]: hand-written wgrad (split-K partials + fixed-order
 // sum) vs hipBLASLt (best of 24 heuristic candidates, fp32 C, beta = 1)
 __global__ void k_ref_wgrad(const bf16_t* dY, const bf16_t* X, float* R, const int* rows, int nr, int T, int Nr,
@@ -485,6 +650,12 @@ static int overlap_main() {
 int main(int argc, char** argv) {
   if (argc > 1 && !strcmp(argv[1], "overlap")) return overlap_main();
   if (argc > 1 && !strcmp(argv[1], "epi")) return epi_main(16384, 768, 3072, 1024);
+  if (argc > 1 && !strcmp(argv[1], "dgrad")) {
+    std::vector<int> v;
+    for (int i = 2; i < argc; ++i) v.push_back(atoi(argv[i]));
+    if (v.empty()) v = {16384, 768, 2304, 16384, 768, 768, 16384, 768, 6144, 16384, 3072, 768, 16384, 768, 50304};
+    return dgrad_main(v);
+  }
   if (argc > 1 && !strcmp(argv[1], "wgrad")) {
     std::vector<int> v;
     for (int i = 2; i < argc; ++i) v.push_back(atoi(argv[i]));
@@ -497,7 +668,7 @@ int main(int argc, char** argv) {
                              {"nt", run_bf16<128>},      {"ntrow", run_bf16<132>},   {"np", run_bf16<256>},
                              {"nprow", run_bf16<260>},   {"d4", run_bf16<512 | (4 << 24)>},
                              {"d8", run_bf16<512 | (8 << 24)>}, {"d13", run_bf16<512 | (13 << 24)>},
-                             {"d20", run_bf16<512 | (20 << 24)>}};
+                             {"d20", run_bf16<512 | (20 << 24)>}, {"lt", run_bf16<1024>}};
   std::string only = (argc > 1 && strcmp(argv[1], "all")) ? std::string(",") + argv[1] + "," : "all";
   std::vector<int> shp;
   for (int i = 2; i < argc; ++i) shp.push_back(atoi(argv[i]));
