@@ -187,6 +187,9 @@ class GPTEngine:
         # all by default; the memory-lean mode keeps only the small-operand ones (qkv, o)
         self.defer_roles = frozenset(self.ROLES)
         self._slots = {}
+        # dY-operand slot ring (ffbb window, see _window_ffbb): 0 = one slot per layer
+        self._ring = 0
+        self._ring_done = {}
         self._side = None  # weight-gradient side stream (lazily created)
         self._mask_side = None  # attention keep-bit side stream
         self._pipe = None  # second compute stream of train_window
@@ -264,8 +267,12 @@ class GPTEngine:
             return None
         return self._slot_buf(st, layer, name, M, N, device)[0]
 
+    # slot buffers written by the backward (the dY operands of the deferred weight gradients)
+    _DY_SLOTS = frozenset(("dqkv", "da", "dgu", "dd"))
+
     def _slot_buf(self, st, layer, name: str, M: int, N: int, device):
-        key = (layer, name)
+        # ffbb ring: the dY operands of layer i live in ring slot i % R (see _window_ffbb)
+        key = (("ring", layer % self._ring), name) if self._ring and name in self._DY_SLOTS else (layer, name)
         buf = self._slots.get(key)
         if buf is None or buf.shape != (self.acc_slots * M, N) or buf.device != device:
             if buf is not None and buf.is_cuda:
@@ -684,6 +691,14 @@ class GPTEngine:
         for i in reversed(range(L)):
             prov.pre_backward(i)
             wait_prev(i)
+            if self._ring:
+                # dY ring: this block writes layer i's dgu / da / dqkv (slot i % R) and layer
+                # i-1's dd (slot (i-1) % R); their previous occupants are layers i+R and
+                # i-1+R, whose window weight gradients were issued (side stream, in layer
+                # order) by the last backward before this block was issued
+                ev = self._ring_done.get(i - 1 + self._ring)
+                if ev is not None:
+                    torch.cuda.current_stream().wait_event(ev)
             c = st.caches[i]
             if st.recompute:
                 # Re-run (part of) the layer forward from the saved tensors; masks replay exactly.
@@ -745,6 +760,10 @@ class GPTEngine:
                     _wgrad(gm, gr.wo, full(i, "da", H), full(i, "o", H))
                 if dfr["qkv"]:
                     _wgrad(gm, gr.wqkv, full(i, "dqkv", 3 * H), full(i, "n1", H))
+                if self._ring:
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    self._ring_done[i] = ev
             if not all(dfr.values()):  # the per-micro-step ones, on this backward's stream
                 if side_ctx is not None:
                     side_ctx.__exit__(None, None, None)
@@ -828,10 +847,21 @@ class GPTEngine:
         # whole by one workgroup)
         cap = int(os.environ.get("DLT_FFBB_GEMM_GRID", "192"))
         prev_cap = self.ops.gemm_grid_cap(cap) if cap and hasattr(self.ops, "gemm_grid_cap") else None
+        # The two backwards run a block apart and the last one issues each layer's window
+        # weight gradients right after its own block, so a layer's dY operands (dqkv, da,
+        # dgu, dd: ~650 MB per layer at the headline shape) are dead a few layers later:
+        # they live in a ring of R slots instead of one slot per layer (DLT_SLOT_RING,
+        # default 3; 0 = per layer).  A block waits for the weight gradients of the
+        # layer whose slot it reuses.
+        ring = int(os.environ.get("DLT_SLOT_RING", "3")) if defer else 0
+        self._ring = ring if 2 <= ring < self.cfg.num_layers else 0
+        self._ring_done = {}
         try:
             return self._window_ffbb_body(micro_ids, micro_targets, dloss, recompute, defer, sync_hook, before_last,
                                           main, p0, streams)
         finally:
+            self._ring = 0
+            self._ring_done = {}
             if prev_cap is not None:
                 self.ops.gemm_grid_cap(prev_cap)
 

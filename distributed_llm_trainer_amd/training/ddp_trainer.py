@@ -12,8 +12,9 @@ MI355X design:
   RCCL as soon as each group of layers finishes its backward.
 * Loss is accumulated on the device; the only host sync per optimizer step is the
   logged loss value (the reference syncs on every micro-step, Q10).
-* fp32 / fp16 run the eager module path (autocast + dynamic loss scaling for fp16);
-  on CPU the fused executor runs with the PyTorch reference ops in fp32.
+* fp32 / fp16 run the same fused executor with fp32 master weights and a shadow in the
+  compute dtype (fp16 with dynamic loss scaling, GradScaler's defaults); on CPU the
+  fused executor runs with the PyTorch reference ops in fp32.
 
 Intentional fixes (documented in README "Divergences"): LR is set before the
 optimizer step and the cosine is clamped (Q5/Q6, switch off with

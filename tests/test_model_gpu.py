@@ -191,13 +191,16 @@ def test_pipelined_window_matches_sequential_gpu(recompute):
         assert torch.equal(g1[n], g2[n]), (n, (g1[n] - g2[n]).abs().max().item())
 
 
-@pytest.mark.parametrize("recompute", [False, True])
-def test_window_ffbb_matches_sequential_gpu(recompute, monkeypatch):
+@pytest.mark.parametrize("recompute,ring", [(False, "0"), (True, "0"), (False, "2"), (True, "2")])
+def test_window_ffbb_matches_sequential_gpu(recompute, ring, monkeypatch):
     """Two-chain window F0 || F1 | B0 || B1 (DLT_WINDOW_SCHED=ffbb: both forwards, then both
     backwards concurrently, B1 one block behind B0 with per-buffer waits) == the sequential
-    schedule: same losses, bit-identical gradients."""
+    schedule: same losses, bit-identical gradients -- with one dY slot per layer (ring 0)
+    and with the dY operands in a 2-slot ring (reused while the other backward and the
+    side-stream weight gradients are still running)."""
     from distributed_llm_trainer_amd.models.engine import shift_targets
     monkeypatch.setenv("DLT_WINDOW_SCHED", "ffbb")
+    monkeypatch.setenv("DLT_SLOT_RING", ring)
     torch.manual_seed(6)
     base = GPT(_cfg(0.1)).to(DEV)
     m1, m2 = copy.deepcopy(base), copy.deepcopy(base)
