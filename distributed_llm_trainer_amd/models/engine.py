@@ -163,6 +163,7 @@ class _StepState:
     rstdf: Any = None
     nf: Any = None
     dlogits: Any = None
+    ce_scale: float = 1.0
     d_last: Any = None  # bf16 d of last layer (input of final norm)
 
 
@@ -176,6 +177,10 @@ class GPTEngine:
         self.seed = int(seed) & 0xFFFFFFFF
         self.eps = eps
         self.micro_counter = 0
+        # fp16: the cross-entropy gradient is stored pre-multiplied by this factor (the
+        # trainer's loss scale) so it does not underflow; the backward divides it out
+        # where it applies dloss (the lm_head weight / data gradients)
+        self.ce_grad_scale = 1.0
         self.gemm = gemm or _TorchGemm()
         self._rope = {}
         # dropout probabilities (zeroed in eval mode)
@@ -518,7 +523,7 @@ class GPTEngine:
             nseg = self.loss_segments if (train and B % self.loss_segments == 0) else 1
             if nseg == 1:
                 n_valid = (targets != -100).sum()
-                row_loss = self.ops.cross_entropy_fwd_bwd(lg, targets, V, n_valid)
+                row_loss = self.ops.cross_entropy_fwd_bwd(lg, targets, V, n_valid, self.ce_grad_scale)
                 loss = row_loss.sum() / n_valid.clamp(min=1).float()
             else:  # fused micro-steps: per-segment normalisation (see set_loss_segments)
                 rows = (B // nseg) * S
@@ -527,11 +532,13 @@ class GPTEngine:
                     tk = targets[k * rows:(k + 1) * rows]
                     nv = (tk != -100).sum()
                     # gradient of (1/nseg) * mean_k: the kernel divides by its count argument
-                    rl = self.ops.cross_entropy_fwd_bwd(lg[k * rows:(k + 1) * rows], tk, V, nv * nseg)
+                    rl = self.ops.cross_entropy_fwd_bwd(lg[k * rows:(k + 1) * rows], tk, V, nv * nseg,
+                                                        self.ce_grad_scale)
                     seg_losses.append(rl.sum() / nv.clamp(min=1).float())
                 loss = torch.stack(seg_losses).mean()
             if need_bwd:
-                st.dlogits = lg  # now holds d(mean loss)/d(logits), unscaled
+                st.dlogits = lg  # now holds ce_grad_scale * d(mean loss)/d(logits)
+                st.ce_scale = self.ce_grad_scale
                 st.xf, st.rstdf, st.nf = xf, rstdf, nf
         if return_logits or targets is None:
             lg2 = self.gemm.linear(nf, hw.lm_head)
@@ -610,10 +617,11 @@ class GPTEngine:
         # lm_head: dnf = dlogits @ E ; dE += dlogits^T @ (nf * dloss)
         dnf = gm.linear_dgrad(st.dlogits, hw.lm_head)
         nf_out = self._sb(st, "head", "nf", M, H, dev)
-        if st.nf.dtype == torch.bfloat16:
-            nf_scaled = ops.scale_bf16(st.nf, dloss, out=nf_out)
+        inv_ce = 1.0 / st.ce_scale  # the pre-scaled CE gradient (fp16), see ce_grad_scale
+        if st.nf.dtype in (torch.bfloat16, torch.float16):
+            nf_scaled = ops.scale_bf16(st.nf, dloss, out=nf_out, mul=inv_ce)
         else:
-            nf_scaled = st.nf * dloss
+            nf_scaled = st.nf * (dloss * inv_ce)
             if nf_out is not None:
                 nf_scaled = nf_out.copy_(nf_scaled)
         head_ev = None
@@ -683,7 +691,8 @@ class GPTEngine:
 
         wait_prev("norm")
         g_x2, g_d = ops.rmsnorm_bwd(dnf, st.xf, st.rstdf, hw.norm, None, hg.norm,
-                                    ph, key_last, dy_scale=dloss, want_ddelta=True, ddelta_out=sb(L - 1, "dd", H))
+                                    ph, key_last, dy_scale=dloss, want_ddelta=True, ddelta_out=sb(L - 1, "dd", H),
+                                    dy_mul=inv_ce)
         mark("norm")
         del dnf
         cos, sin = self.rope(S, g_x2.device)

@@ -184,10 +184,11 @@ class GPT(nn.Module):
             self.store = provider
         torch_ops_on_gpu = False
         if ops is None:
-            if dev.type == "cuda" and act_dtype != torch.bfloat16:
-                # fp16 / fp32 models (--mixed_precision fp16|fp32): the HIP kernels store
-                # bf16 activations, so the engine's schedule runs with PyTorch ops on the
-                # GPU for the elementwise / norm / attention work and hipBLASLt GEMMs
+            if dev.type == "cuda" and act_dtype not in (torch.bfloat16, torch.float16):
+                # fp32 models (--mixed_precision fp32, the reference/debug mode): the HIP
+                # kernels move 16-bit activations, so the engine's schedule runs with
+                # PyTorch ops on the GPU and hipBLASLt fp32 GEMMs.  bf16 and fp16 run the
+                # HIP kernels (instantiated for both formats, csrc/common.h HK).
                 ops = ops_mod.CPU_OPS
                 torch_ops_on_gpu = True
             else:

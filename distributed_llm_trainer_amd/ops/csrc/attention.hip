@@ -132,9 +132,19 @@ __device__ __forceinline__ void tile_barrier() {
 // pair (an element-wise cast after a select made hipcc emit one cvt per element plus
 // a v_perm per pair).
 typedef float floatx8_t __attribute__((ext_vector_type(8)));
+// HK = 1 (fp16 activations): the same registers as fp16 (RNE), kept in the bf16x8_t
+// container type -- fragments are raw 16-byte operands; only mfma<HK> reads their format.
+template <int HK = 0>
 __device__ __forceinline__ bf16x8_t acc_frag(const floatx16_t& acc, int s) {
   const floatx8_t f = s ? acc.s89abcdef : acc.s01234567;
-  return __builtin_convertvector(f, bf16x8_t);
+  if constexpr (HK == 0) return __builtin_convertvector(f, bf16x8_t);
+  else return __builtin_bit_cast(bf16x8_t, __builtin_convertvector(f, f16x8_t));
+}
+// element j of a 16-bit fragment as float
+template <int HK>
+__device__ __forceinline__ float frag_f(const bf16x8_t& v, int j) {
+  if constexpr (HK == 0) return (float)v[j];
+  else return (float)__builtin_bit_cast(f16x8_t, v)[j];
 }
 
 // Dropout select on the fp32 bit pattern: all-ones / all-zeros from keep bit `bit` of
@@ -149,8 +159,12 @@ __device__ __forceinline__ uint32_t keep_ones(uint32_t word, int bit) {
 }
 __device__ __forceinline__ float keep_and(float x, uint32_t ones) { return __uint_as_float(__float_as_uint(x) & ones); }
 
+template <int HK = 0>
 __device__ __forceinline__ floatx16_t mfma(const bf16x8_t& a, const bf16x8_t& b, const floatx16_t& c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  if constexpr (HK == 0) return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c, 0,
+                                                  0, 0);
 }
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
@@ -371,7 +385,7 @@ struct FwdState {
   float m, l;  // running max (raw score units) and per-lane partial row sum
 };
 
-template <bool MASK, bool DROP>
+template <bool MASK, bool DROP, int HK = 0>
 __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const bf16_t* Vt, const bf16x8_t (&qf)[4],
                                          int k0, int qa, int S, int lane, float c_log2, uint2 mw) {
   // One 64-key tile as ONE online-softmax step: S = K.Q^T of both 32-key halves first
@@ -396,11 +410,11 @@ __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const b
     lgkm_wait4(kf[0][0], kf[0][1], kf[0][2], kf[0][3]);
     sacc[0] = zero16();
 #pragma unroll
-    for (int s = 0; s < 4; ++s) sacc[0] = mfma(kf[0][s], qf[s], sacc[0]);
+    for (int s = 0; s < 4; ++s) sacc[0] = mfma<HK>(kf[0][s], qf[s], sacc[0]);
     tr_wait(kf[1][0], kf[1][1], kf[1][2], kf[1][3]);
     sacc[1] = zero16();
 #pragma unroll
-    for (int s = 0; s < 4; ++s) sacc[1] = mfma(kf[1][s], qf[s], sacc[1]);
+    for (int s = 0; s < 4; ++s) sacc[1] = mfma<HK>(kf[1][s], qf[s], sacc[1]);
 #else
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -411,8 +425,8 @@ __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const b
     sacc[1] = zero16();
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      sacc[0] = mfma(kf[0][s], qf[s], sacc[0]);
-      sacc[1] = mfma(kf[1][s], qf[s], sacc[1]);
+      sacc[0] = mfma<HK>(kf[0][s], qf[s], sacc[0]);
+      sacc[1] = mfma<HK>(kf[1][s], qf[s], sacc[1]);
     }
 #endif
   }
@@ -457,9 +471,9 @@ __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const b
     tr_wait(vf[0][0], vf[0][1], vf[1][0], vf[1][1]);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const bf16x8_t pb = acc_frag(sacc[t], kk);
+      const bf16x8_t pb = acc_frag<HK>(sacc[t], kk);
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt) fs.o[dt] = mfma(vf[kk][dt], pb, fs.o[dt]);
+      for (int dt = 0; dt < 2; ++dt) fs.o[dt] = mfma<HK>(vf[kk][dt], pb, fs.o[dt]);
     }
   }
   fs.l += l0 + l1;
@@ -473,7 +487,7 @@ __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const b
 // ~1.1 resident waves per SIMD on average at B16).  Round 1 measured one item per
 // workgroup in the NATURAL order 1.8x slower than the pairing (equal-length items
 // stacked on a CU); longest-first does not stack them.
-template <bool DROP>
+template <bool DROP, int HK = 0>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_attn_fwd(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
                                                     const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
                                                     float* __restrict__ lse, const uint32_t* __restrict__ mask,
@@ -537,9 +551,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       const bf16_t* Vt = Kt + KVB * HD;
       const int k0 = kb * KVB;
       if (!MASKED)
-        fwd_tile<false, DROP>(fs, Kt, Vt, qf, k0, qa, S, lane, c_log2, mw_cur);
+        fwd_tile<false, DROP, HK>(fs, Kt, Vt, qf, k0, qa, S, lane, c_log2, mw_cur);
       else if (k0 <= q0 + 31)
-        fwd_tile<true, DROP>(fs, Kt, Vt, qf, k0, qa, S, lane, c_log2, mw_cur);
+        fwd_tile<true, DROP, HK>(fs, Kt, Vt, qf, k0, qa, S, lane, c_log2, mw_cur);
       mw_cur = mw_next;
       tile_barrier();
     };
@@ -568,7 +582,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         for (int g = 0; g < 4; ++g) {
           u16x4 t;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) t.v[e] = f2bf(fs.o[dt][4 * g + e] * inv_l);
+          for (int e = 0; e < 4; ++e) t.v[e] = f2h<HK>(fs.o[dt][4 * g + e] * inv_l);
           w[dt][g] = __builtin_bit_cast(uint2, t);
         }
       store_row16(orow, w, h);
@@ -582,6 +596,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 // position `pos` is applied first: the partner of dim j < 32 is j + 32, i.e. the same
 // register of the other dt -- the rotation needs no data exchange.  (Replaces the
 // separate repack kernel that read dq/dk back and wrote the packed [M, 3H] gradient.)
+template <int HK = 0>
 __device__ __forceinline__ void store_head_row(bf16_t* __restrict__ dst, const floatx16_t (&a)[2], float sc, int h,
                                                const float* __restrict__ cosT, const float* __restrict__ sinT,
                                                int pos) {
@@ -596,14 +611,14 @@ __device__ __forceinline__ void store_head_row(bf16_t* __restrict__ dst, const f
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float x1 = a[0][4 * g + e] * sc, x2 = a[1][4 * g + e] * sc;
-        w0.v[e] = f2bf(fmaf(x1, cc[e], x2 * ss[e]));
-        w1.v[e] = f2bf(fmaf(x2, cc[e], -x1 * ss[e]));
+        w0.v[e] = f2h<HK>(fmaf(x1, cc[e], x2 * ss[e]));
+        w1.v[e] = f2h<HK>(fmaf(x2, cc[e], -x1 * ss[e]));
       }
     } else {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        w0.v[e] = f2bf(a[0][4 * g + e] * sc);
-        w1.v[e] = f2bf(a[1][4 * g + e] * sc);
+        w0.v[e] = f2h<HK>(a[0][4 * g + e] * sc);
+        w1.v[e] = f2h<HK>(a[1][4 * g + e] * sc);
       }
     }
     w[0][g] = __builtin_bit_cast(uint2, w0);
@@ -628,7 +643,7 @@ __device__ unsigned long long* g_attn_tim;
 // ---------------------------------------------------------------- dK / dV
 // One workgroup per 128 keys (32 per wave); sweep query tiles of 64 (two 32-row
 // sub-tiles).  Accumulators: S and dP with queries in registers, keys on lanes.
-template <bool MASK, bool DROP>
+template <bool MASK, bool DROP, int HK = 0>
 __device__ __forceinline__ void dkdv_subtile(floatx16_t (&dka)[2], floatx16_t (&dva)[2], const bf16_t* Qt,
                                              const bf16_t* Dt, const float* rl, const float* rd,
                                              uint32_t mw, const bf16x8_t (&kf)[4], const bf16x8_t (&vf)[4],
@@ -637,8 +652,8 @@ __device__ __forceinline__ void dkdv_subtile(floatx16_t (&dka)[2], floatx16_t (&
   floatx16_t sacc = zero16(), pacc = zero16();
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    sacc = mfma(lds_row8(Qt, kl, 16 * s + 8 * h), kf[s], sacc);
-    pacc = mfma(lds_row8(Dt, kl, 16 * s + 8 * h), vf[s], pacc);
+    sacc = mfma<HK>(lds_row8(Qt, kl, 16 * s + 8 * h), kf[s], sacc);
+    pacc = mfma<HK>(lds_row8(Dt, kl, 16 * s + 8 * h), vf[s], pacc);
   }
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
@@ -672,19 +687,19 @@ __device__ __forceinline__ void dkdv_subtile(floatx16_t (&dka)[2], floatx16_t (&
   }
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    const bf16x8_t pb = acc_frag(sacc, s);
-    const bf16x8_t sb = acc_frag(pacc, s);
+    const bf16x8_t pb = acc_frag<HK>(sacc, s);
+    const bf16x8_t sb = acc_frag<HK>(pacc, s);
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt) {
-      dva[dt] = mfma(tr_frag(Dt, s, dt, lane), pb, dva[dt]);
-      dka[dt] = mfma(tr_frag(Qt, s, dt, lane), sb, dka[dt]);
+      dva[dt] = mfma<HK>(tr_frag(Dt, s, dt, lane), pb, dva[dt]);
+      dka[dt] = mfma<HK>(tr_frag(Qt, s, dt, lane), sb, dka[dt]);
     }
   }
 }
 
 // Work items: 64 keys (2 waves x 32); a workgroup processes the pair of key blocks
 // (p, nrb-1-p) -- equal work per workgroup (see the forward).
-template <bool DROP>
+template <bool DROP, int HK = 0>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_attn_bwd_dkdv(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
                                                          const bf16_t* __restrict__ v,
                                                          const bf16_t* __restrict__ dout,
@@ -784,10 +799,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         const bf16_t* Ds = Dt + 32 * qt * HD;
         const uint32_t mw = (qt ? mw1 : mw0) >> (4 * h);
         if (!MASKED)
-          dkdv_subtile<false, DROP>(dka, dva, Qs, Ds, rlp + 32 * qt, rdp + 32 * qt, mw, kf, vf, qs, ka, S, lane,
+          dkdv_subtile<false, DROP, HK>(dka, dva, Qs, Ds, rlp + 32 * qt, rdp + 32 * qt, mw, kf, vf, qs, ka, S, lane,
                                     c_log2, dscale);
         else if (qs + 31 >= k0)
-          dkdv_subtile<true, DROP>(dka, dva, Qs, Ds, rlp + 32 * qt, rdp + 32 * qt, mw, kf, vf, qs, ka, S, lane,
+          dkdv_subtile<true, DROP, HK>(dka, dva, Qs, Ds, rlp + 32 * qt, rdp + 32 * qt, mw, kf, vf, qs, ka, S, lane,
                                    c_log2, dscale);
       }
       if (more) store_rows(cur ^ 1);
@@ -803,8 +818,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     ATTN_STAMP(3);
 
     if (ka < S) {
-      store_head_row(dk + hout + (size_t)ka * out_rs, dka, scale, h, cosT, sinT, ka);
-      store_head_row(dv + hout + (size_t)ka * out_rs, dva, DROP ? dscale : 1.f, h, nullptr, nullptr, 0);
+      store_head_row<HK>(dk + hout + (size_t)ka * out_rs, dka, scale, h, cosT, sinT, ka);
+      store_head_row<HK>(dv + hout + (size_t)ka * out_rs, dva, DROP ? dscale : 1.f, h, nullptr, nullptr, 0);
     }
 #ifdef DLT_ATTN_TIMING
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -815,7 +830,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 }
 
 // ---------------------------------------------------------------------- dQ
-template <bool MASK, bool DROP>
+template <bool MASK, bool DROP, int HK = 0>
 __device__ __forceinline__ void dq_tile(floatx16_t (&dqa)[2], const bf16_t* Kt, const bf16_t* Vt,
                                         const bf16x8_t (&qf)[4], const bf16x8_t (&df)[4], int k0, int qa, int S,
                                         int lane, float c_log2, float nl2, float dl, float dscale, uint2 mw) {
@@ -834,15 +849,15 @@ __device__ __forceinline__ void dq_tile(floatx16_t (&dqa)[2], const bf16_t* Kt, 
     for (int s = 0; s < 4; ++s) vf[s] = lds_row8_asm(Vt, 32 * t + ql, 16 * s + 8 * h);
     lgkm_wait4(kf[0], kf[1], kf[2], kf[3]);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) sacc[t] = mfma(kf[s], qf[s], sacc[t]);
+    for (int s = 0; s < 4; ++s) sacc[t] = mfma<HK>(kf[s], qf[s], sacc[t]);
     tr_wait(vf[0], vf[1], vf[2], vf[3]);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) pacc[t] = mfma(vf[s], df[s], pacc[t]);
+    for (int s = 0; s < 4; ++s) pacc[t] = mfma<HK>(vf[s], df[s], pacc[t]);
 #else
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      sacc[t] = mfma(lds_row8(Kt, 32 * t + ql, 16 * s + 8 * h), qf[s], sacc[t]);
-      pacc[t] = mfma(lds_row8(Vt, 32 * t + ql, 16 * s + 8 * h), df[s], pacc[t]);
+      sacc[t] = mfma<HK>(lds_row8(Kt, 32 * t + ql, 16 * s + 8 * h), qf[s], sacc[t]);
+      pacc[t] = mfma<HK>(lds_row8(Vt, 32 * t + ql, 16 * s + 8 * h), df[s], pacc[t]);
     }
 #endif
   }
@@ -868,13 +883,13 @@ __device__ __forceinline__ void dq_tile(floatx16_t (&dqa)[2], const bf16_t* Kt, 
   }
 #pragma unroll
   for (int kk = 0; kk < 4; ++kk) {
-    const bf16x8_t sb = acc_frag(pacc[kk >> 1], kk & 1);
+    const bf16x8_t sb = acc_frag<HK>(pacc[kk >> 1], kk & 1);
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt) dqa[dt] = mfma(tr_frag(Kt, kk, dt, lane), sb, dqa[dt]);
+    for (int dt = 0; dt < 2; ++dt) dqa[dt] = mfma<HK>(tr_frag(Kt, kk, dt, lane), sb, dqa[dt]);
   }
 }
 
-template <bool DROP>
+template <bool DROP, int HK = 0>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_attn_bwd_dq(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
                                                        const bf16_t* __restrict__ v, const bf16_t* __restrict__ dout,
                                                        const bf16_t* __restrict__ o,
@@ -920,7 +935,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       df[s] = load_row8(dout + orow + 16 * s + 8 * h, qok);
       const bf16x8_t of = load_row8(o + orow + 16 * s + 8 * h, qok);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dsum += (float)df[s][j] * (float)of[j];
+      for (int j = 0; j < 8; ++j) dsum += frag_f<HK>(df[s], j) * frag_f<HK>(of, j);
     }
     const float nl2 = qok ? -lse[(size_t)bh * S + qc] * LOG2E : 0.f;
     const float dl = xhalf_sum(dsum);
@@ -950,9 +965,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       const bf16_t* Vt = Kt + KVB * HD;
       const int k0 = kb * KVB;
       if (!MASKED)
-        dq_tile<false, DROP>(dqa, Kt, Vt, qf, df, k0, qa, S, lane, c_log2, nl2, dl, dscale, mw_cur);
+        dq_tile<false, DROP, HK>(dqa, Kt, Vt, qf, df, k0, qa, S, lane, c_log2, nl2, dl, dscale, mw_cur);
       else if (k0 <= q0 + 31)
-        dq_tile<true, DROP>(dqa, Kt, Vt, qf, df, k0, qa, S, lane, c_log2, nl2, dl, dscale, mw_cur);
+        dq_tile<true, DROP, HK>(dqa, Kt, Vt, qf, df, k0, qa, S, lane, c_log2, nl2, dl, dscale, mw_cur);
       mw_cur = mw_next;
       tile_barrier();
     };
@@ -968,7 +983,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     } else if (kb < nkv) {
       step(B0{}, MSK{}, kb);
     }
-    if (qok) store_head_row(dq + hout + (size_t)qa * out_rs, dqa, scale, h, cosT, sinT, qa);
+    if (qok) store_head_row<HK>(dq + hout + (size_t)qa * out_rs, dqa, scale, h, cosT, sinT, qa);
   }
 }
 
@@ -1011,7 +1026,7 @@ DLT_API int dlt_attn_dropout_mask(uint32_t* mask, int B, int nh, int S, uint32_t
 // packed [B*S, 3H] QKV GEMM output (bs = S*3H, hs = 64, rs = 3H; k, v = q + H, q + 2H).
 DLT_API int dlt_attn_fwd_ex(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, uint32_t* mask,
                             int B, int nh, int S, int hd, float scale, uint32_t key, uint32_t thr, float dscale,
-                            int gen_mask, long in_bs, int in_hs, int in_rs, hipStream_t st) {
+                            int gen_mask, long in_bs, int in_hs, int in_rs, int hk, hipStream_t st) {
   if (hd != HD || S <= 0 || in_rs % 8 || in_hs % 8 || in_bs % 8) return -1;
   if (thr && !mask) return -2;  // dropout needs the keep-bit buffer
   const int nrb = (S + RB - 1) / RB;
@@ -1023,18 +1038,20 @@ DLT_API int dlt_attn_fwd_ex(const bf16_t* q, const bf16_t* k, const bf16_t* v, b
       const int rc = dlt_attn_dropout_mask(mask, B, nh, S, key, thr, st);
       if (rc) return rc;
     }
-    k_attn_fwd<true><<<grid, NT, 0, st>>>(q, k, v, o, lse, mask, S, nh, c_log2, dscale, in_bs, in_hs, in_rs, xm);
+    DLT_HK_DISPATCH(hk, k_attn_fwd<true, HKC><<<grid, NT, 0, st>>>(q, k, v, o, lse, mask, S, nh, c_log2, dscale,
+                                                                  in_bs, in_hs, in_rs, xm));
   } else {
-    k_attn_fwd<false><<<grid, NT, 0, st>>>(q, k, v, o, lse, nullptr, S, nh, c_log2, dscale, in_bs, in_hs, in_rs, xm);
+    DLT_HK_DISPATCH(hk, k_attn_fwd<false, HKC><<<grid, NT, 0, st>>>(q, k, v, o, lse, nullptr, S, nh, c_log2, dscale,
+                                                                   in_bs, in_hs, in_rs, xm));
   }
   DLT_CHECK_LAUNCH();
 }
 
 DLT_API int dlt_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, uint32_t* mask,
                          int B, int nh, int S, int hd, float scale, uint32_t key, uint32_t thr, float dscale,
-                         int gen_mask, hipStream_t st) {
+                         int gen_mask, int hk, hipStream_t st) {
   return dlt_attn_fwd_ex(q, k, v, o, lse, mask, B, nh, S, hd, scale, key, thr, dscale, gen_mask,
-                         (long)nh * S * HD, S * HD, HD, st);
+                         (long)nh * S * HD, S * HD, HD, hk, st);
 }
 
 // dq/dk/dv use the (out_bs, out_hs, out_rs) layout; with cosT/sinT ([>= S, 32] fp32)
@@ -1044,7 +1061,7 @@ DLT_API int dlt_attn_bwd_ex(const bf16_t* q, const bf16_t* k, const bf16_t* v, c
                             const float* lse, const uint32_t* mask, float* delta_ws, bf16_t* dq, bf16_t* dk,
                             bf16_t* dv, int B, int nh, int S, int hd, float scale, float dscale, long in_bs,
                             int in_hs, int in_rs, long out_bs, int out_hs, int out_rs, const float* cosT,
-                            const float* sinT, hipStream_t st) {
+                            const float* sinT, int hk, hipStream_t st) {
   if (hd != HD || S <= 0 || in_rs % 8 || in_hs % 8 || in_bs % 8 || out_rs % 4 || out_hs % 4 || out_bs % 4) return -1;
   if ((cosT == nullptr) != (sinT == nullptr)) return -3;
   const float c_log2 = scale * LOG2E;
@@ -1055,23 +1072,27 @@ DLT_API int dlt_attn_bwd_ex(const bf16_t* q, const bf16_t* k, const bf16_t* v, c
   // dK/dV then reads.
   if (mask) {
     const uint32_t* maskT = mask + (size_t)B * nh * S * ((S + 31) / 32);
-    k_attn_bwd_dq<true><<<gq, NT, 0, st>>>(q, k, v, dout, o, lse, delta_ws, mask, dq, S, nh, c_log2, scale, dscale,
-                                           in_bs, in_hs, in_rs, out_bs, out_hs, out_rs, cosT, sinT, xm);
-    k_attn_bwd_dkdv<true><<<gk, NT, 0, st>>>(q, k, v, dout, lse, delta_ws, maskT, dk, dv, S, nh, c_log2, scale,
-                                             dscale, in_bs, in_hs, in_rs, out_bs, out_hs, out_rs, cosT, sinT, xm);
+    DLT_HK_DISPATCH(hk, k_attn_bwd_dq<true, HKC><<<gq, NT, 0, st>>>(
+                            q, k, v, dout, o, lse, delta_ws, mask, dq, S, nh, c_log2, scale, dscale, in_bs, in_hs,
+                            in_rs, out_bs, out_hs, out_rs, cosT, sinT, xm));
+    DLT_HK_DISPATCH(hk, k_attn_bwd_dkdv<true, HKC><<<gk, NT, 0, st>>>(
+                            q, k, v, dout, lse, delta_ws, maskT, dk, dv, S, nh, c_log2, scale, dscale, in_bs, in_hs,
+                            in_rs, out_bs, out_hs, out_rs, cosT, sinT, xm));
   } else {
-    k_attn_bwd_dq<false><<<gq, NT, 0, st>>>(q, k, v, dout, o, lse, delta_ws, mask, dq, S, nh, c_log2, scale, dscale,
-                                            in_bs, in_hs, in_rs, out_bs, out_hs, out_rs, cosT, sinT, xm);
-    k_attn_bwd_dkdv<false><<<gk, NT, 0, st>>>(q, k, v, dout, lse, delta_ws, mask, dk, dv, S, nh, c_log2, scale,
-                                              dscale, in_bs, in_hs, in_rs, out_bs, out_hs, out_rs, cosT, sinT, xm);
+    DLT_HK_DISPATCH(hk, k_attn_bwd_dq<false, HKC><<<gq, NT, 0, st>>>(
+                            q, k, v, dout, o, lse, delta_ws, mask, dq, S, nh, c_log2, scale, dscale, in_bs, in_hs,
+                            in_rs, out_bs, out_hs, out_rs, cosT, sinT, xm));
+    DLT_HK_DISPATCH(hk, k_attn_bwd_dkdv<false, HKC><<<gk, NT, 0, st>>>(
+                            q, k, v, dout, lse, delta_ws, mask, dk, dv, S, nh, c_log2, scale, dscale, in_bs, in_hs,
+                            in_rs, out_bs, out_hs, out_rs, cosT, sinT, xm));
   }
   DLT_CHECK_LAUNCH();
 }
 
 DLT_API int dlt_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,
                          const float* lse, const uint32_t* mask, float* delta_ws, bf16_t* dq, bf16_t* dk, bf16_t* dv,
-                         int B, int nh, int S, int hd, float scale, float dscale, hipStream_t st) {
+                         int B, int nh, int S, int hd, float scale, float dscale, int hk, hipStream_t st) {
   const long bs = (long)nh * S * HD;
   return dlt_attn_bwd_ex(q, k, v, o, dout, lse, mask, delta_ws, dq, dk, dv, B, nh, S, hd, scale, dscale, bs, S * HD,
-                         HD, bs, S * HD, HD, nullptr, nullptr, st);
+                         HD, bs, S * HD, HD, nullptr, nullptr, hk, st);
 }

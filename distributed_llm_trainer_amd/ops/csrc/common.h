@@ -28,6 +28,37 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return __builtin_bit_cast(uint16_t, b);
 }
 
+// 16-bit activation formats.  HK = 0: bf16 (the default compute dtype); HK = 1: fp16
+// (--mixed_precision fp16: the same kernels instantiated for IEEE half, RNE casts).
+// Kernels that move activations as raw 16-bit words take HK as a template parameter and
+// their launchers an `hk` argument (0 / 1).
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+template <int HK>
+__device__ __forceinline__ float h2f(uint16_t u) {
+  if constexpr (HK == 0) return __uint_as_float(((uint32_t)u) << 16);
+  else return (float)__builtin_bit_cast(_Float16, u);
+}
+template <int HK>
+__device__ __forceinline__ uint16_t f2h(float f) {
+  if constexpr (HK == 0) {
+    __bf16 b = (__bf16)f;
+    return __builtin_bit_cast(uint16_t, b);
+  } else {
+    return __builtin_bit_cast(uint16_t, (_Float16)f);
+  }
+}
+// launcher helper: run F<0> or F<1> by the runtime format
+#define DLT_HK_DISPATCH(hk, ...) \
+  do {                           \
+    if ((hk) == 1) {             \
+      constexpr int HKC = 1;     \
+      __VA_ARGS__;               \
+    } else {                     \
+      constexpr int HKC = 0;     \
+      __VA_ARGS__;               \
+    }                            \
+  } while (0)
+
 __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
   x ^= x >> 16;
   x *= 0x7feb352du;

@@ -7,7 +7,7 @@
 #include "common.h"
 
 // ---------------------------------------------------------------- embedding
-// out[m, :] = float(W[ids[m], :]); W is fp32 (wdt=0) or bf16 (wdt=1).
+// out[m, :] = float(W[ids[m], :]); W is fp32 (wdt=0), bf16 (wdt=1) or fp16 (wdt=2).
 __global__ __launch_bounds__(256) void k_embedding_fwd(const int64_t* __restrict__ ids, const void* __restrict__ W,
                                                        int wdt, float* __restrict__ out, int M, int H, int V) {
   const int q = H >> 2;  // float4 per row
@@ -20,9 +20,12 @@ __global__ __launch_bounds__(256) void k_embedding_fwd(const int64_t* __restrict
     float4 v;
     if (wdt == 0) {
       v = *(reinterpret_cast<const float4*>(W) + (size_t)id * q + c);
-    } else {
+    } else if (wdt == 1) {
       const u16x4 b = *(reinterpret_cast<const u16x4*>(W) + (size_t)id * q + c);
       v = make_float4(bf2f(b.v[0]), bf2f(b.v[1]), bf2f(b.v[2]), bf2f(b.v[3]));
+    } else {
+      const u16x4 b = *(reinterpret_cast<const u16x4*>(W) + (size_t)id * q + c);
+      v = make_float4(h2f<1>(b.v[0]), h2f<1>(b.v[1]), h2f<1>(b.v[2]), h2f<1>(b.v[3]));
     }
     *(reinterpret_cast<float4*>(out) + i) = v;
   }
@@ -139,6 +142,7 @@ DLT_API int dlt_embedding_bwd_chunk() { return EMB_CH; }
 // One thread = one 8-wide chunk of each rotation half (16-B vectors; the partner
 // element of column j is j + hd/2 in NeoX rotate_half).  32-bit index math only
 // (64-bit div/mod is emulated on the GPU and cost ~30 % of this kernel).
+template <int HK = 0>
 __global__ __launch_bounds__(256) void k_rope_qkv_fwd(const bf16_t* __restrict__ qkv, const float* __restrict__ cosT,
                                                       const float* __restrict__ sinT, bf16_t* __restrict__ q,
                                                       bf16_t* __restrict__ k, bf16_t* __restrict__ v,
@@ -168,9 +172,9 @@ __global__ __launch_bounds__(256) void k_rope_qkv_fwd(const bf16_t* __restrict__
       const float ss[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float x1 = bf2f(a.v[e]), x2 = bf2f(c.v[e]);
-        o1.v[e] = f2bf(x1 * cc[e] - x2 * ss[e]);
-        o2.v[e] = f2bf(x2 * cc[e] + x1 * ss[e]);
+        const float x1 = h2f<HK>(a.v[e]), x2 = h2f<HK>(c.v[e]);
+        o1.v[e] = f2h<HK>(x1 * cc[e] - x2 * ss[e]);
+        o2.v[e] = f2h<HK>(x2 * cc[e] + x1 * ss[e]);
       }
     }
     *reinterpret_cast<u16x8*>(dst + j) = o1;
@@ -180,6 +184,7 @@ __global__ __launch_bounds__(256) void k_rope_qkv_fwd(const bf16_t* __restrict__
 
 // dq, dk, dv [B, nh, S, hd] -> dqkv [B*S, 3*nh*hd] (inverse rotation for dq, dk).
 // dq may be fp32 (dqf != nullptr) or bf16.
+template <int HK = 0>
 __global__ __launch_bounds__(256) void k_rope_qkv_bwd(const bf16_t* __restrict__ dq, const float* __restrict__ dqf,
                                                       const bf16_t* __restrict__ dk, const bf16_t* __restrict__ dv,
                                                       const float* __restrict__ cosT, const float* __restrict__ sinT,
@@ -211,12 +216,12 @@ __global__ __launch_bounds__(256) void k_rope_qkv_bwd(const bf16_t* __restrict__
       const u16x8 a = *reinterpret_cast<const u16x8*>(src + j);
       const u16x8 c = *reinterpret_cast<const u16x8*>(src + half + j);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { g1[e] = bf2f(a.v[e]); g2[e] = bf2f(c.v[e]); }
+      for (int e = 0; e < 8; ++e) { g1[e] = h2f<HK>(a.v[e]); g2[e] = h2f<HK>(c.v[e]); }
     }
     u16x8 o1, o2;
     if (sec == 2) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { o1.v[e] = f2bf(g1[e]); o2.v[e] = f2bf(g2[e]); }
+      for (int e = 0; e < 8; ++e) { o1.v[e] = f2h<HK>(g1[e]); o2.v[e] = f2h<HK>(g2[e]); }
     } else {
       const float* cp = cosT + s * half + j;
       const float* sp = sinT + s * half + j;
@@ -226,8 +231,8 @@ __global__ __launch_bounds__(256) void k_rope_qkv_bwd(const bf16_t* __restrict__
       const float ss[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        o1.v[e] = f2bf(g1[e] * cc[e] + g2[e] * ss[e]);
-        o2.v[e] = f2bf(g2[e] * cc[e] - g1[e] * ss[e]);
+        o1.v[e] = f2h<HK>(g1[e] * cc[e] + g2[e] * ss[e]);
+        o2.v[e] = f2h<HK>(g2[e] * cc[e] - g1[e] * ss[e]);
       }
     }
     bf16_t* dst = dqkv + (size_t)m * (3 * nh * hd) + (sec * nh + h) * hd;
@@ -241,6 +246,7 @@ __global__ __launch_bounds__(256) void k_rope_qkv_bwd(const bf16_t* __restrict__
 // kernels then read q/k/v straight from this buffer (dlt_attn_fwd_ex), so no head-major
 // copies are written (2/3 of the traffic of k_rope_qkv_fwd, and its backward
 // disappears into the attention epilogue).
+template <int HK = 0>
 __global__ __launch_bounds__(256) void k_rope_qk_inplace(bf16_t* __restrict__ qkv, const float* __restrict__ cosT,
                                                          const float* __restrict__ sinT, int M, int S, int nh,
                                                          int hd) {
@@ -266,9 +272,9 @@ __global__ __launch_bounds__(256) void k_rope_qk_inplace(bf16_t* __restrict__ qk
     u16x8 o1, o2;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float x1 = bf2f(a.v[e]), x2 = bf2f(c.v[e]);
-      o1.v[e] = f2bf(x1 * cc[e] - x2 * ss[e]);
-      o2.v[e] = f2bf(x2 * cc[e] + x1 * ss[e]);
+      const float x1 = h2f<HK>(a.v[e]), x2 = h2f<HK>(c.v[e]);
+      o1.v[e] = f2h<HK>(x1 * cc[e] - x2 * ss[e]);
+      o2.v[e] = f2h<HK>(x2 * cc[e] + x1 * ss[e]);
     }
     *reinterpret_cast<u16x8*>(p + j) = o1;
     *reinterpret_cast<u16x8*>(p + half + j) = o2;
@@ -281,27 +287,28 @@ static inline int ew_blocks(size_t total) {
 }
 
 DLT_API int dlt_rope_qkv_fwd(const bf16_t* qkv, const float* cosT, const float* sinT, bf16_t* q, bf16_t* k,
-                             bf16_t* v, int B, int S, int nh, int hd, hipStream_t st) {
+                             bf16_t* v, int B, int S, int nh, int hd, int hk, hipStream_t st) {
   if (hd % 16 || (long)B * S * 3 * nh * hd >= (1L << 31)) return -1;
   const size_t total = (size_t)B * S * 3 * nh * (hd / 16);
-  k_rope_qkv_fwd<<<ew_blocks(total), 256, 0, st>>>(qkv, cosT, sinT, q, k, v, B, S, nh, hd);
+  DLT_HK_DISPATCH(hk, k_rope_qkv_fwd<HKC><<<ew_blocks(total), 256, 0, st>>>(qkv, cosT, sinT, q, k, v, B, S, nh, hd));
   DLT_CHECK_LAUNCH();
 }
 
 DLT_API int dlt_rope_qk_inplace(bf16_t* qkv, const float* cosT, const float* sinT, int M, int S, int nh, int hd,
-                                hipStream_t st) {
+                                int hk, hipStream_t st) {
   if (hd % 16 || S <= 0 || M % S || (long)M * 3 * nh * hd >= (1L << 31)) return -1;
   const size_t total = (size_t)M * 2 * nh * (hd / 16);
-  k_rope_qk_inplace<<<ew_blocks(total), 256, 0, st>>>(qkv, cosT, sinT, M, S, nh, hd);
+  DLT_HK_DISPATCH(hk, k_rope_qk_inplace<HKC><<<ew_blocks(total), 256, 0, st>>>(qkv, cosT, sinT, M, S, nh, hd));
   DLT_CHECK_LAUNCH();
 }
 
 DLT_API int dlt_rope_qkv_bwd(const bf16_t* dq, const float* dqf, const bf16_t* dk, const bf16_t* dv,
-                             const float* cosT, const float* sinT, bf16_t* dqkv, int B, int S, int nh, int hd,
+                             const float* cosT, const float* sinT, bf16_t* dqkv, int B, int S, int nh, int hd, int hk,
                              hipStream_t st) {
   if (hd % 16 || (long)B * S * 3 * nh * hd >= (1L << 31)) return -1;
   const size_t total = (size_t)B * S * 3 * nh * (hd / 16);
-  k_rope_qkv_bwd<<<ew_blocks(total), 256, 0, st>>>(dq, dqf, dk, dv, cosT, sinT, dqkv, B, S, nh, hd);
+  DLT_HK_DISPATCH(hk, k_rope_qkv_bwd<HKC><<<ew_blocks(total), 256, 0, st>>>(dq, dqf, dk, dv, cosT, sinT, dqkv, B, S,
+                                                                             nh, hd));
   DLT_CHECK_LAUNCH();
 }
 
@@ -309,6 +316,7 @@ DLT_API int dlt_rope_qkv_bwd(const bf16_t* dq, const float* dqf, const bf16_t* d
 __device__ __forceinline__ float sigmoidf_(float x) { return dlt_sigmoid(x); }
 
 // gu [M, 2I] = [gate | up] -> a [M, I] = silu(gate) * up
+template <int HK = 0>
 __global__ __launch_bounds__(256) void k_swiglu_fwd(const bf16_t* __restrict__ gu, bf16_t* __restrict__ a, int M, int I) {
   const int q = I >> 3;
   const size_t total = (size_t)M * q;
@@ -320,13 +328,14 @@ __global__ __launch_bounds__(256) void k_swiglu_fwd(const bf16_t* __restrict__ g
     u16x8 o;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float gv = bf2f(g.v[e]);
-      o.v[e] = f2bf(gv * sigmoidf_(gv) * bf2f(u.v[e]));
+      const float gv = h2f<HK>(g.v[e]);
+      o.v[e] = f2h<HK>(gv * sigmoidf_(gv) * h2f<HK>(u.v[e]));
     }
     *reinterpret_cast<u16x8*>(a + m * I + c) = o;
   }
 }
 
+template <int HK = 0>
 __global__ __launch_bounds__(256) void k_swiglu_bwd(const bf16_t* __restrict__ gu, const bf16_t* __restrict__ da,
                                                     bf16_t* __restrict__ dgu, int M, int I) {
   const int q = I >> 3;
@@ -340,10 +349,10 @@ __global__ __launch_bounds__(256) void k_swiglu_bwd(const bf16_t* __restrict__ g
     u16x8 og, ou;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float gv = bf2f(g.v[e]), uv = bf2f(u.v[e]), dv = bf2f(d.v[e]);
+      const float gv = h2f<HK>(g.v[e]), uv = h2f<HK>(u.v[e]), dv = h2f<HK>(d.v[e]);
       const float sg = sigmoidf_(gv);
-      og.v[e] = f2bf(dv * uv * sg * (1.f + gv * (1.f - sg)));
-      ou.v[e] = f2bf(dv * gv * sg);
+      og.v[e] = f2h<HK>(dv * uv * sg * (1.f + gv * (1.f - sg)));
+      ou.v[e] = f2h<HK>(dv * gv * sg);
     }
     *reinterpret_cast<u16x8*>(dgu + m * 2 * I + c) = og;
     *reinterpret_cast<u16x8*>(dgu + m * 2 * I + I + c) = ou;
@@ -352,34 +361,36 @@ __global__ __launch_bounds__(256) void k_swiglu_bwd(const bf16_t* __restrict__ g
 
 // y = x * (*scale) for a bf16 tensor and a device fp32 scalar (the autograd output
 // gradient), one pass -- replaces an upcast + multiply + downcast kernel chain.
+template <int HK = 0>
 __global__ __launch_bounds__(256) void k_scale_bf16(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
-                                                    long n8, const float* __restrict__ scale) {
-  const float sc = *scale;
+                                                    long n8, const float* __restrict__ scale, float mul) {
+  const float sc = *scale * mul;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
     u16x8 v = reinterpret_cast<const u16x8*>(x)[i];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v.v[e] = f2bf(bf2f(v.v[e]) * sc);
+    for (int e = 0; e < 8; ++e) v.v[e] = f2h<HK>(h2f<HK>(v.v[e]) * sc);
     reinterpret_cast<u16x8*>(y)[i] = v;
   }
 }
 
-DLT_API int dlt_scale_bf16(const bf16_t* x, bf16_t* y, long n, const float* scale, hipStream_t st) {
+DLT_API int dlt_scale_bf16(const bf16_t* x, bf16_t* y, long n, const float* scale, float mul, int hk,
+                           hipStream_t st) {
   if (n % 8) return -1;
   const long n8 = n / 8;
   const int blocks = (int)((n8 + 255) / 256 < 4096 ? (n8 + 255) / 256 : 4096);
-  k_scale_bf16<<<blocks, 256, 0, st>>>(x, y, n8, scale);
+  DLT_HK_DISPATCH(hk, k_scale_bf16<HKC><<<blocks, 256, 0, st>>>(x, y, n8, scale, mul));
   DLT_CHECK_LAUNCH();
 }
 
-DLT_API int dlt_swiglu_fwd(const bf16_t* gu, bf16_t* a, int M, int I, hipStream_t st) {
+DLT_API int dlt_swiglu_fwd(const bf16_t* gu, bf16_t* a, int M, int I, int hk, hipStream_t st) {
   if (I % 8) return -1;
-  k_swiglu_fwd<<<ew_blocks((size_t)M * (I / 8)), 256, 0, st>>>(gu, a, M, I);
+  DLT_HK_DISPATCH(hk, k_swiglu_fwd<HKC><<<ew_blocks((size_t)M * (I / 8)), 256, 0, st>>>(gu, a, M, I));
   DLT_CHECK_LAUNCH();
 }
 
-DLT_API int dlt_swiglu_bwd(const bf16_t* gu, const bf16_t* da, bf16_t* dgu, int M, int I, hipStream_t st) {
+DLT_API int dlt_swiglu_bwd(const bf16_t* gu, const bf16_t* da, bf16_t* dgu, int M, int I, int hk, hipStream_t st) {
   if (I % 8) return -1;
-  k_swiglu_bwd<<<ew_blocks((size_t)M * (I / 8)), 256, 0, st>>>(gu, da, dgu, M, I);
+  DLT_HK_DISPATCH(hk, k_swiglu_bwd<HKC><<<ew_blocks((size_t)M * (I / 8)), 256, 0, st>>>(gu, da, dgu, M, I));
   DLT_CHECK_LAUNCH();
 }
 

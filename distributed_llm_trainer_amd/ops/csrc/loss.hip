@@ -18,9 +18,10 @@
 #include "common.h"
 #include <cstdlib>
 
+template <int HK = 0>
 __global__ __launch_bounds__(256) void k_ce_fwd_bwd(bf16_t* __restrict__ logits, const int64_t* __restrict__ targets,
                                                     const int64_t* __restrict__ n_valid, float* __restrict__ loss_rows,
-                                                    int M, int Vp, int V) {
+                                                    int M, int Vp, int V, float gscale) {
   __shared__ float sm_m[4], sm_s[4];
   const int row = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -37,7 +38,7 @@ __global__ __launch_bounds__(256) void k_ce_fwd_bwd(bf16_t* __restrict__ logits,
     float lm = -INFINITY;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      v[e] = (c * 8 + e < V) ? bf2f(x.v[e]) : -INFINITY;
+      v[e] = (c * 8 + e < V) ? h2f<HK>(x.v[e]) : -INFINITY;
       lm = fmaxf(lm, v[e]);
     }
     if (lm > mx) { sm *= __expf(mx - lm); mx = lm; }
@@ -61,10 +62,10 @@ __global__ __launch_bounds__(256) void k_ce_fwd_bwd(bf16_t* __restrict__ logits,
 #pragma unroll
   for (int w = 0; w < 4; ++w) gs += (sm_m[w] == -INFINITY) ? 0.f : sm_s[w] * __expf(sm_m[w] - gm);
   const float lse = gm + __logf(gs);
-  if (tid == 0) loss_rows[row] = valid ? (lse - bf2f(lrow[tgt])) : 0.f;
+  if (tid == 0) loss_rows[row] = valid ? (lse - h2f<HK>(lrow[tgt])) : 0.f;
   __syncthreads();  // everyone has read lrow[tgt] before it is overwritten
   const int64_t nv = *n_valid;
-  const float inv_n = valid ? 1.f / (float)(nv > 0 ? nv : 1) : 0.f;
+  const float inv_n = valid ? gscale / (float)(nv > 0 ? nv : 1) : 0.f;
   // pass 2: gradient in place
   for (int c = tid; c < nchunk; c += 256) {
     u16x8 x = *reinterpret_cast<const u16x8*>(lrow + c * 8);
@@ -73,20 +74,23 @@ __global__ __launch_bounds__(256) void k_ce_fwd_bwd(bf16_t* __restrict__ logits,
       const int col = c * 8 + e;
       float g = 0.f;
       if (col < V) {
-        g = __expf(bf2f(x.v[e]) - lse);
+        g = __expf(h2f<HK>(x.v[e]) - lse);
         if (col == tgt) g -= 1.f;
         g *= inv_n;
       }
-      x.v[e] = f2bf(g);
+      x.v[e] = f2h<HK>(g);
     }
     *reinterpret_cast<u16x8*>(lrow + c * 8) = x;
   }
 }
 
-template <int CPT, int NTH = 512, bool CE_NT = false>
+// gscale: factor on the gradient only (1 for bf16; the fp16 path stores the gradient
+// pre-multiplied by the loss scale so it does not underflow fp16, and the engine divides
+// the scale back out where it applies dloss)
+template <int CPT, int NTH = 512, bool CE_NT = false, int HK = 0>
 __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH == 1024 ? 8 : 1, 8))) void k_ce_row(bf16_t* __restrict__ logits, const int64_t* __restrict__ targets,
                                                 const int64_t* __restrict__ n_valid, float* __restrict__ loss_rows,
-                                                int M, int Vp, int V) {
+                                                int M, int Vp, int V, float gscale) {
   // Per element only: max, one exp2 for the sum, one exp2 + scale for the gradient.
   // Column bounds are tested per 8-wide chunk (only the last chunk straddles V), and
   // the target column is patched by its owning thread per chunk, not per element.
@@ -116,7 +120,8 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH == 1024
   }
   auto el = [&](int t, int e) -> float {
     const uint32_t w = e < 2 ? (e == 0 ? x[t].x : x[t].x) : e < 4 ? x[t].y : e < 6 ? x[t].z : x[t].w;
-    return __uint_as_float((e & 1) ? (w & 0xffff0000u) : (w << 16));
+    if constexpr (HK == 0) return __uint_as_float((e & 1) ? (w & 0xffff0000u) : (w << 16));
+    else return h2f<1>((uint16_t)((e & 1) ? (w >> 16) : (w & 0xffffu)));
   };
   // Keep only the raw bf16 words live across the passes (52 VGPRs at CPT 13): the
   // empty asm makes the compiler re-convert per pass instead of holding 104 floats.
@@ -170,7 +175,7 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH == 1024
   for (int w = 0; w < NTH / 64; ++w) gs += red[w];
   const float lse = gm + __logf(gs);
   const int64_t nv = *n_valid;
-  const float inv_n = valid ? 1.f / (float)(nv > 0 ? nv : 1) : 0.f;
+  const float inv_n = valid ? gscale / (float)(nv > 0 ? nv : 1) : 0.f;
   const float nl2 = -lse * L2E;
 #pragma unroll
   for (int t = 0; t < CPT; ++t) {
@@ -179,11 +184,11 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH == 1024
       u16x8 o;
       if (c * 8 + 8 <= V) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o.v[e] = f2bf(__builtin_amdgcn_exp2f(fmaf(el(t, e), L2E, nl2)) * inv_n);
+        for (int e = 0; e < 8; ++e) o.v[e] = f2h<HK>(__builtin_amdgcn_exp2f(fmaf(el(t, e), L2E, nl2)) * inv_n);
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          o.v[e] = f2bf(c * 8 + e < V ? __builtin_amdgcn_exp2f(fmaf(el(t, e), L2E, nl2)) * inv_n : 0.f);
+          o.v[e] = f2h<HK>(c * 8 + e < V ? __builtin_amdgcn_exp2f(fmaf(el(t, e), L2E, nl2)) * inv_n : 0.f);
       }
       if (c == tchunk) {
         const int e = (int)(tgt & 7);
@@ -191,7 +196,7 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH == 1024
 #pragma unroll
         for (int j = 0; j < 8; ++j) l = (j == e) ? el(t, j) : l;
         loss_rows[row] = lse - l;
-        const uint16_t gt = f2bf((__builtin_amdgcn_exp2f(fmaf(l, L2E, nl2)) - 1.f) * inv_n);
+        const uint16_t gt = f2h<HK>((__builtin_amdgcn_exp2f(fmaf(l, L2E, nl2)) - 1.f) * inv_n);
 #pragma unroll
         for (int j = 0; j < 8; ++j) o.v[j] = (j == e) ? gt : o.v[j];
       }
@@ -210,11 +215,30 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH == 1024
   if (!valid && tid == 0) loss_rows[row] = 0.f;
 }
 
+template <int HK>
+static void ce_launch(int wide, int nt, int cpt, hipStream_t st, bf16_t* logits, const int64_t* targets,
+                      const int64_t* n_valid, float* loss_rows, int M, int Vp, int V, float gscale) {
+#define CE_ARGS logits, targets, n_valid, loss_rows, M, Vp, V, gscale
+  if (wide && (Vp / 8 + 1023) / 1024 <= 7) {  // 1024 threads x 7 chunks (Vp <= 57344)
+    if (nt) k_ce_row<7, 1024, true, HK><<<M, 1024, 0, st>>>(CE_ARGS);
+    else k_ce_row<7, 1024, false, HK><<<M, 1024, 0, st>>>(CE_ARGS);
+    return;
+  }
+  if (cpt <= 1) k_ce_row<1, 512, false, HK><<<M, 512, 0, st>>>(CE_ARGS);
+  else if (cpt <= 2) k_ce_row<2, 512, false, HK><<<M, 512, 0, st>>>(CE_ARGS);
+  else if (cpt <= 4) k_ce_row<4, 512, false, HK><<<M, 512, 0, st>>>(CE_ARGS);
+  else if (cpt <= 8) k_ce_row<8, 512, false, HK><<<M, 512, 0, st>>>(CE_ARGS);
+  else if (cpt <= 13) k_ce_row<13, 512, false, HK><<<M, 512, 0, st>>>(CE_ARGS);
+  else if (cpt <= 16) k_ce_row<16, 512, false, HK><<<M, 512, 0, st>>>(CE_ARGS);
+  else k_ce_fwd_bwd<HK><<<M, 256, 0, st>>>(CE_ARGS);
+#undef CE_ARGS
+}
+
+// hk: logits format (0 bf16, 1 fp16); gscale multiplies the in-place gradient
 DLT_API int dlt_cross_entropy_fwd_bwd(bf16_t* logits, const int64_t* targets, const int64_t* n_valid,
-                                      float* loss_rows, int M, int Vp, int V, hipStream_t st) {
+                                      float* loss_rows, int M, int Vp, int V, float gscale, int hk, hipStream_t st) {
   if (Vp % 8 || V > Vp) return -1;
   const int cpt = (Vp / 8 + 511) / 512;
-#define CE_ARGS logits, targets, n_valid, loss_rows, M, Vp, V
   static int wide = -1;
   if (wide < 0) {
     const char* e = getenv("DLT_CE_THREADS");
@@ -228,18 +252,6 @@ DLT_API int dlt_cross_entropy_fwd_bwd(bf16_t* logits, const int64_t* targets, co
     const char* e = getenv("DLT_CE_NT");
     nt = (e && atoi(e) == 0) ? 0 : 1;
   }
-  if (wide && (Vp / 8 + 1023) / 1024 <= 7) {  // 1024 threads x 7 chunks (Vp <= 57344)
-    if (nt) k_ce_row<7, 1024, true><<<M, 1024, 0, st>>>(CE_ARGS);
-    else k_ce_row<7, 1024><<<M, 1024, 0, st>>>(CE_ARGS);
-    DLT_CHECK_LAUNCH();
-  }
-  if (cpt <= 1) k_ce_row<1><<<M, 512, 0, st>>>(CE_ARGS);
-  else if (cpt <= 2) k_ce_row<2><<<M, 512, 0, st>>>(CE_ARGS);
-  else if (cpt <= 4) k_ce_row<4><<<M, 512, 0, st>>>(CE_ARGS);
-  else if (cpt <= 8) k_ce_row<8><<<M, 512, 0, st>>>(CE_ARGS);
-  else if (cpt <= 13) k_ce_row<13><<<M, 512, 0, st>>>(CE_ARGS);
-  else if (cpt <= 16) k_ce_row<16><<<M, 512, 0, st>>>(CE_ARGS);
-  else k_ce_fwd_bwd<<<M, 256, 0, st>>>(CE_ARGS);
-#undef CE_ARGS
+  DLT_HK_DISPATCH(hk, ce_launch<HKC>(wide, nt, cpt, st, logits, targets, n_valid, loss_rows, M, Vp, V, gscale));
   DLT_CHECK_LAUNCH();
 }

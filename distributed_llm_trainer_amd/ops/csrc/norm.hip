@@ -26,18 +26,20 @@ __device__ __forceinline__ f4 ld_f4(const float* p) {
 __device__ __forceinline__ void st_f4(float* p, const float (&v)[4]) {
   *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
 }
-__device__ __forceinline__ void ld_bf4(const bf16_t* p, float (&v)[4]) {
+template <int HK>
+__device__ __forceinline__ void ld_h4(const bf16_t* p, float (&v)[4]) {
   const u16x4 d = *reinterpret_cast<const u16x4*>(p);
 #pragma unroll
-  for (int e = 0; e < 4; ++e) v[e] = bf2f(d.v[e]);
+  for (int e = 0; e < 4; ++e) v[e] = h2f<HK>(d.v[e]);
 }
 
-// Norm weight: fp32 (flat master, DDP path) or bf16 (the gathered FSDP unit) -- read in
-// place, so the FSDP path needs no per-call weight upcast kernel.
-__device__ __forceinline__ f4 ld_w4(const void* w, int wbf16, int off) {
-  if (wbf16) {
+// Norm weight: fp32 (flat master, DDP path) or 16-bit in the activation format (the
+// gathered FSDP unit) -- read in place, so the FSDP path needs no per-call weight upcast.
+template <int HK>
+__device__ __forceinline__ f4 ld_w4(const void* w, int w16, int off) {
+  if (w16) {
     f4 r;
-    ld_bf4(reinterpret_cast<const bf16_t*>(w) + off, r.v);
+    ld_h4<HK>(reinterpret_cast<const bf16_t*>(w) + off, r.v);
     return r;
   }
   return ld_f4(reinterpret_cast<const float*>(w) + off);
@@ -48,7 +50,7 @@ __device__ __forceinline__ void st_f4_nt(float* p, const float (&v)[4]) {
   for (int e = 0; e < 4; ++e) __builtin_nontemporal_store(v[e], p + e);
 }
 
-template <int NCH, bool XNT = false>
+template <int NCH, bool XNT = false, int HK = 0>
 __global__ __launch_bounds__(256) void k_add_dropout_rmsnorm_fwd(
     const float* __restrict__ resid, const bf16_t* __restrict__ delta, const void* __restrict__ w, int wbf16,
     float* __restrict__ x_out, bf16_t* __restrict__ y_out, float* __restrict__ rstd_out,
@@ -74,7 +76,7 @@ __global__ __launch_bounds__(256) void k_add_dropout_rmsnorm_fwd(
       }
       if (delta) {
         float d[4];
-        ld_bf4(delta + off, d);
+        ld_h4<HK>(delta + off, d);
         if (thr) {
 #pragma unroll
           for (int e = 0; e < 4; e += 2) {
@@ -103,26 +105,26 @@ __global__ __launch_bounds__(256) void k_add_dropout_rmsnorm_fwd(
         if (XNT) st_f4_nt(x_out + off, xv[t]);
         else st_f4(x_out + off, xv[t]);
       }
-      const f4 ww = ld_w4(w, wbf16, c * 4);
+      const f4 ww = ld_w4<HK>(w, wbf16, c * 4);
       u16x4 y;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) y.v[e] = f2bf(xv[t][e] * rstd * ww.v[e]);
+      for (int e = 0; e < 4; ++e) y.v[e] = f2h<HK>(xv[t][e] * rstd * ww.v[e]);
       *reinterpret_cast<u16x4*>(y_out + off) = y;
     }
   }
 }
 
-template <int NCH>
+template <int NCH, int HK = 0>
 __global__ __launch_bounds__(256) void k_rmsnorm_bwd(
     const bf16_t* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ rstd_in,
     const void* __restrict__ w, int wbf16, const float* dres, float* dx_out,
     bf16_t* __restrict__ ddelta, float* __restrict__ dw, float* __restrict__ dw_part,
-    const float* __restrict__ dy_scale, int M, int H, uint32_t key, uint32_t thr, float dscale) {
+    const float* __restrict__ dy_scale, float dy_mul, int M, int H, uint32_t key, uint32_t thr, float dscale) {
   extern __shared__ __attribute__((aligned(16))) float smem[];  // [4][H]
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int nc = H >> 2;
-  const float sc = dy_scale ? *dy_scale : 1.f;
+  const float sc = (dy_scale ? *dy_scale : 1.f) * dy_mul;
   const float invH = 1.f / (float)H;
   float dwacc[NCH][4];
   float wv[NCH][4];
@@ -132,7 +134,7 @@ __global__ __launch_bounds__(256) void k_rmsnorm_bwd(
 #pragma unroll
     for (int e = 0; e < 4; ++e) { dwacc[t][e] = 0.f; wv[t][e] = 0.f; }
     if (c < nc) {
-      const f4 a = ld_w4(w, wbf16, c * 4);
+      const f4 a = ld_w4<HK>(w, wbf16, c * 4);
 #pragma unroll
       for (int e = 0; e < 4; ++e) wv[t][e] = a.v[e];
     }
@@ -149,7 +151,7 @@ __global__ __launch_bounds__(256) void k_rmsnorm_bwd(
       for (int e = 0; e < 4; ++e) { dv[t][e] = 0.f; xx[t][e] = 0.f; rr[t][e] = 0.f; }
       if (c < nc) {
         const size_t off = rbase + (size_t)c * 4;
-        ld_bf4(dy + off, dv[t]);
+        ld_h4<HK>(dy + off, dv[t]);
         const f4 a = ld_f4(x + off);
 #pragma unroll
         for (int e = 0; e < 4; ++e) xx[t][e] = a.v[e];
@@ -188,12 +190,12 @@ __global__ __launch_bounds__(256) void k_rmsnorm_bwd(
 #pragma unroll
             for (int e = 0; e < 4; e += 2) {
               const uint32_t h = lowbias32(key ^ (uint32_t)((off + e) >> 1));
-              o.v[e] = f2bf(((h & 0xffffu) >= thr) ? dx[e] * dscale : 0.f);
-              o.v[e + 1] = f2bf(((h >> 16) >= thr) ? dx[e + 1] * dscale : 0.f);
+              o.v[e] = f2h<HK>(((h & 0xffffu) >= thr) ? dx[e] * dscale : 0.f);
+              o.v[e + 1] = f2h<HK>(((h >> 16) >= thr) ? dx[e + 1] * dscale : 0.f);
             }
           } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) o.v[e] = f2bf(dx[e]);
+            for (int e = 0; e < 4; ++e) o.v[e] = f2h<HK>(dx[e]);
           }
           *reinterpret_cast<u16x4*>(ddelta + off) = o;
         }
@@ -292,37 +294,73 @@ static int fwd_nt() {
   return v;
 }
 
+template <int HK>
+static void rmsnorm_fwd_launch(int nch, dim3 grid, dim3 block, hipStream_t stream, const float* resid,
+                               const bf16_t* delta, const void* w, int wbf16, float* x_out, bf16_t* y_out,
+                               float* rstd_out, int M, int H, float eps, uint32_t key, uint32_t thr, float dscale);
+
+// hk: activation format of delta / y_out / a 16-bit weight (0 bf16, 1 fp16)
 DLT_API int dlt_add_dropout_rmsnorm_fwd(const float* resid, const bf16_t* delta, const void* w, int wbf16,
                                         float* x_out, bf16_t* y_out, float* rstd_out, int M, int H,
-                                        float eps, uint32_t key, uint32_t thr, float dscale,
+                                        float eps, uint32_t key, uint32_t thr, float dscale, int hk,
                                         hipStream_t stream) {
   if (H % 4 != 0 || H > 4096) return -1;
   const dim3 grid((M + 3) / 4), block(256);
   const int nch = nch_of(H);
-#define ARGS resid, delta, w, wbf16, x_out, y_out, rstd_out, M, H, eps, key, thr, dscale
-  switch (nch) {
-    case 1: k_add_dropout_rmsnorm_fwd<1><<<grid, block, 0, stream>>>(ARGS); break;
-    case 2: k_add_dropout_rmsnorm_fwd<2><<<grid, block, 0, stream>>>(ARGS); break;
-    case 3:
-      if (fwd_nt()) k_add_dropout_rmsnorm_fwd<3, true><<<grid, block, 0, stream>>>(ARGS);
-      else k_add_dropout_rmsnorm_fwd<3><<<grid, block, 0, stream>>>(ARGS);
-      break;
-    case 4: k_add_dropout_rmsnorm_fwd<4><<<grid, block, 0, stream>>>(ARGS); break;
-    case 5: k_add_dropout_rmsnorm_fwd<5><<<grid, block, 0, stream>>>(ARGS); break;
-    case 6: k_add_dropout_rmsnorm_fwd<6><<<grid, block, 0, stream>>>(ARGS); break;
-    case 7: k_add_dropout_rmsnorm_fwd<7><<<grid, block, 0, stream>>>(ARGS); break;
-    case 8: k_add_dropout_rmsnorm_fwd<8><<<grid, block, 0, stream>>>(ARGS); break;
-    case 12: k_add_dropout_rmsnorm_fwd<12><<<grid, block, 0, stream>>>(ARGS); break;
-    default: k_add_dropout_rmsnorm_fwd<16><<<grid, block, 0, stream>>>(ARGS); break;
-  }
-#undef ARGS
+  DLT_HK_DISPATCH(hk, rmsnorm_fwd_launch<HKC>(nch, grid, block, stream, resid, delta, w, wbf16, x_out, y_out,
+                                              rstd_out, M, H, eps, key, thr, dscale));
   DLT_CHECK_LAUNCH();
 }
 
+template <int HK>
+static void rmsnorm_fwd_launch(int nch, dim3 grid, dim3 block, hipStream_t stream, const float* resid,
+                               const bf16_t* delta, const void* w, int wbf16, float* x_out, bf16_t* y_out,
+                               float* rstd_out, int M, int H, float eps, uint32_t key, uint32_t thr, float dscale) {
+#define ARGS resid, delta, w, wbf16, x_out, y_out, rstd_out, M, H, eps, key, thr, dscale
+  switch (nch) {
+    case 1: k_add_dropout_rmsnorm_fwd<1, false, HK><<<grid, block, 0, stream>>>(ARGS); break;
+    case 2: k_add_dropout_rmsnorm_fwd<2, false, HK><<<grid, block, 0, stream>>>(ARGS); break;
+    case 3:
+      if (fwd_nt()) k_add_dropout_rmsnorm_fwd<3, true, HK><<<grid, block, 0, stream>>>(ARGS);
+      else k_add_dropout_rmsnorm_fwd<3, false, HK><<<grid, block, 0, stream>>>(ARGS);
+      break;
+    case 4: k_add_dropout_rmsnorm_fwd<4, false, HK><<<grid, block, 0, stream>>>(ARGS); break;
+    case 5: k_add_dropout_rmsnorm_fwd<5, false, HK><<<grid, block, 0, stream>>>(ARGS); break;
+    case 6: k_add_dropout_rmsnorm_fwd<6, false, HK><<<grid, block, 0, stream>>>(ARGS); break;
+    case 7: k_add_dropout_rmsnorm_fwd<7, false, HK><<<grid, block, 0, stream>>>(ARGS); break;
+    case 8: k_add_dropout_rmsnorm_fwd<8, false, HK><<<grid, block, 0, stream>>>(ARGS); break;
+    case 12: k_add_dropout_rmsnorm_fwd<12, false, HK><<<grid, block, 0, stream>>>(ARGS); break;
+    default: k_add_dropout_rmsnorm_fwd<16, false, HK><<<grid, block, 0, stream>>>(ARGS); break;
+  }
+#undef ARGS
+}
+
+template <int HK>
+static void rmsnorm_bwd_launch(int nch, dim3 grid, dim3 block, size_t shm, hipStream_t stream, const bf16_t* dy,
+                               const float* x, const float* rstd, const void* w, int wbf16, const float* dres,
+                               float* dx_out, bf16_t* ddelta, float* dw, float* dw_ws, const float* dy_scale,
+                               float dy_mul, int M, int H, uint32_t key, uint32_t thr, float dscale) {
+#define ARGS dy, x, rstd, w, wbf16, dres, dx_out, ddelta, dw, dw_ws, dy_scale, dy_mul, M, H, key, thr, dscale
+  switch (nch) {
+    case 1: k_rmsnorm_bwd<1, HK><<<grid, block, shm, stream>>>(ARGS); break;
+    case 2: k_rmsnorm_bwd<2, HK><<<grid, block, shm, stream>>>(ARGS); break;
+    case 3: k_rmsnorm_bwd<3, HK><<<grid, block, shm, stream>>>(ARGS); break;
+    case 4: k_rmsnorm_bwd<4, HK><<<grid, block, shm, stream>>>(ARGS); break;
+    case 5: k_rmsnorm_bwd<5, HK><<<grid, block, shm, stream>>>(ARGS); break;
+    case 6: k_rmsnorm_bwd<6, HK><<<grid, block, shm, stream>>>(ARGS); break;
+    case 7: k_rmsnorm_bwd<7, HK><<<grid, block, shm, stream>>>(ARGS); break;
+    case 8: k_rmsnorm_bwd<8, HK><<<grid, block, shm, stream>>>(ARGS); break;
+    case 12: k_rmsnorm_bwd<12, HK><<<grid, block, shm, stream>>>(ARGS); break;
+    default: k_rmsnorm_bwd<16, HK><<<grid, block, shm, stream>>>(ARGS); break;
+  }
+#undef ARGS
+}
+
+// hk: activation format of dy / ddelta / a 16-bit weight (0 bf16, 1 fp16)
 DLT_API int dlt_rmsnorm_bwd(const bf16_t* dy, const float* x, const float* rstd, const void* w, int wbf16,
                             const float* dres, float* dx_out, bf16_t* ddelta, float* dw, float* dw_ws,
-                            const float* dy_scale, int M, int H, uint32_t key, uint32_t thr,
-                            float dscale, hipStream_t stream) {
+                            const float* dy_scale, float dy_mul, int M, int H, uint32_t key, uint32_t thr,
+                            float dscale, int hk, hipStream_t stream) {
   if (H % 4 != 0 || H > 4096) return -1;
   // enough waves to cover HBM latency (~2 rows per wave at M = 8192), few enough
   // blocks that the per-block dw atomics stay negligible
@@ -331,20 +369,8 @@ DLT_API int dlt_rmsnorm_bwd(const bf16_t* dy, const float* x, const float* rstd,
   const dim3 grid(blocks), block(256);
   const size_t shm = (size_t)4 * H * sizeof(float);
   const int nch = nch_of(H);
-#define ARGS dy, x, rstd, w, wbf16, dres, dx_out, ddelta, dw, dw_ws, dy_scale, M, H, key, thr, dscale
-  switch (nch) {
-    case 1: k_rmsnorm_bwd<1><<<grid, block, shm, stream>>>(ARGS); break;
-    case 2: k_rmsnorm_bwd<2><<<grid, block, shm, stream>>>(ARGS); break;
-    case 3: k_rmsnorm_bwd<3><<<grid, block, shm, stream>>>(ARGS); break;
-    case 4: k_rmsnorm_bwd<4><<<grid, block, shm, stream>>>(ARGS); break;
-    case 5: k_rmsnorm_bwd<5><<<grid, block, shm, stream>>>(ARGS); break;
-    case 6: k_rmsnorm_bwd<6><<<grid, block, shm, stream>>>(ARGS); break;
-    case 7: k_rmsnorm_bwd<7><<<grid, block, shm, stream>>>(ARGS); break;
-    case 8: k_rmsnorm_bwd<8><<<grid, block, shm, stream>>>(ARGS); break;
-    case 12: k_rmsnorm_bwd<12><<<grid, block, shm, stream>>>(ARGS); break;
-    default: k_rmsnorm_bwd<16><<<grid, block, shm, stream>>>(ARGS); break;
-  }
-#undef ARGS
+  DLT_HK_DISPATCH(hk, rmsnorm_bwd_launch<HKC>(nch, grid, block, shm, stream, dy, x, rstd, w, wbf16, dres, dx_out,
+                                              ddelta, dw, dw_ws, dy_scale, dy_mul, M, H, key, thr, dscale));
   if (dw_ws) {
     // 16-column blocks of 256 threads (48 for H = 768) slot into the CUs that the other
     // micro-step chain's kernels leave free; 64-column blocks of 1024 threads waited for

@@ -31,21 +31,22 @@ c_void_p, c_int, c_float, c_uint32, c_int64 = ctypes.c_void_p, ctypes.c_int, cty
 
 _SIGS = {
     "dlt_add_dropout_rmsnorm_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
-                                    c_int, c_float, c_uint32, c_uint32, c_float, c_void_p],
+                                    c_int, c_float, c_uint32, c_uint32, c_float, c_int, c_void_p],
     "dlt_rmsnorm_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                        c_void_p, c_void_p, c_int, c_int, c_uint32, c_uint32, c_float, c_void_p],
+                        c_void_p, c_void_p, c_float, c_int, c_int, c_uint32, c_uint32, c_float, c_int, c_void_p],
     "dlt_embedding_fwd": [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p],
     "dlt_embedding_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "dlt_embedding_bwd_chunk": [],
     "dlt_splitk_acc": [c_void_p, c_void_p, ctypes.c_long, c_int, c_void_p],
     "dlt_splitk_sum_bf16": [c_void_p, c_void_p, ctypes.c_long, c_int, c_void_p],
     "dlt_rope_qkv_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                         c_void_p],
-    "dlt_rope_qkv_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                          c_int, c_void_p],
-    "dlt_swiglu_fwd": [c_void_p, c_void_p, c_int, c_int, c_void_p],
-    "dlt_swiglu_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
-    "dlt_cross_entropy_fwd_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
+    "dlt_rope_qkv_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                         c_int, c_int, c_void_p],
+    "dlt_swiglu_fwd": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
+    "dlt_swiglu_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
+    "dlt_cross_entropy_fwd_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int,
+                                  c_void_p],
     "dlt_sumsq": [c_void_p, c_int64, c_void_p, c_void_p, c_void_p],
     "dlt_clip_coef": [c_void_p, c_void_p, c_float, c_float, c_float, c_void_p],
     "dlt_adamw": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float, c_float,
@@ -57,7 +58,7 @@ _SIGS = {
     "dlt_gemm_wgrad": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "dlt_gemm_wgrad_sk": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                           c_void_p],
-    "dlt_scale_bf16": [c_void_p, c_void_p, ctypes.c_long, c_void_p, c_void_p],
+    "dlt_scale_bf16": [c_void_p, c_void_p, ctypes.c_long, c_void_p, c_float, c_int, c_void_p],
     "dlt_gemm_bf16_tn": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "dlt_gemm_bf16_qkv_rope": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                                c_void_p],
@@ -65,16 +66,16 @@ _SIGS = {
     "dlt_gemm_bf16_nn": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "dlt_gemm_bf16_down_swiglu_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
     "dlt_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
-                     c_uint32, c_uint32, c_float, c_int, c_void_p],
+                     c_uint32, c_uint32, c_float, c_int, c_int, c_void_p],
     "dlt_attn_dropout_mask": [c_void_p, c_int, c_int, c_int, c_uint32, c_uint32, c_void_p],
     "dlt_attn_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                     c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_float, c_void_p],
+                     c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_float, c_int, c_void_p],
     "dlt_attn_fwd_ex": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                        c_float, c_uint32, c_uint32, c_float, c_int, ctypes.c_long, c_int, c_int, c_void_p],
+                        c_float, c_uint32, c_uint32, c_float, c_int, ctypes.c_long, c_int, c_int, c_int, c_void_p],
     "dlt_attn_bwd_ex": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                         c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_float, ctypes.c_long, c_int, c_int,
-                        ctypes.c_long, c_int, c_int, c_void_p, c_void_p, c_void_p],
-    "dlt_rope_qk_inplace": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
+                        ctypes.c_long, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p],
+    "dlt_rope_qk_inplace": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "dlt_dec_norm_qkv": [c_void_p, c_void_p, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
     "dlt_dec_attn": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p],
@@ -236,6 +237,24 @@ def _req(t: torch.Tensor, dtype, name: str, numel: Optional[int] = None):
         raise ValueError(f"{name}: must be 16-byte aligned")
 
 
+# 16-bit activation formats of the kernels (csrc/common.h HK): bf16 = 0, fp16 = 1
+_HK = {torch.bfloat16: 0, torch.float16: 1}
+
+
+def _hk(t: torch.Tensor, name: str) -> int:
+    if t.dtype not in _HK:
+        raise TypeError(f"{name}: expected bf16 or fp16 activations, got {t.dtype}")
+    return _HK[t.dtype]
+
+
+def _req_act(t: torch.Tensor, dtype, name: str, numel: Optional[int] = None) -> int:
+    """_req for a 16-bit activation tensor of the given format; returns its HK code."""
+    if dtype not in _HK:
+        raise TypeError(f"{name}: the HIP kernels take bf16 or fp16 activations, not {dtype}")
+    _req(t, dtype, name, numel)
+    return _HK[dtype]
+
+
 # ------------------------------------------------------------------ tables
 def rope_tables(head_dim: int, seq_len: int, device=None):
     from .reference import rope_tables as rt
@@ -271,12 +290,12 @@ def embedding_fwd(ids: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
         ids = ids.long()
     M = ids.numel()
     V, H = weight.shape
-    if weight.dtype not in (torch.float32, torch.bfloat16):
-        raise TypeError("embedding weight must be fp32 or bf16")
+    wdt = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}.get(weight.dtype)
+    if wdt is None:
+        raise TypeError("embedding weight must be fp32, bf16 or fp16")
     _req(weight, weight.dtype, "embedding.weight")
     out = torch.empty(M, H, dtype=torch.float32, device=weight.device)
-    _chk(lib().dlt_embedding_fwd(_p(ids), _p(weight), 0 if weight.dtype == torch.float32 else 1, _p(out), M, H,
-                                 V, _stream()), "embedding_fwd")
+    _chk(lib().dlt_embedding_fwd(_p(ids), _p(weight), wdt, _p(out), M, H, V, _stream()), "embedding_fwd")
     return out
 
 
@@ -301,31 +320,31 @@ def embedding_bwd(ids: torch.Tensor, dout: torch.Tensor, dweight: torch.Tensor) 
 
 
 # ---------------------------------------------------------------- RMSNorm
-def _norm_weight(weight: torch.Tensor, H: int, name: str):
-    """(tensor, is_bf16): fp32 and bf16 norm weights are read in place by the kernels
-    (bf16 = the gathered FSDP unit); other dtypes are upcast once."""
-    if weight.dtype not in (torch.float32, torch.bfloat16):
+def _norm_weight(weight: torch.Tensor, H: int, name: str, act=torch.bfloat16):
+    """(tensor, is_16bit): fp32 norm weights, and 16-bit ones in the activation format
+    (the gathered FSDP unit), are read in place by the kernels; others are upcast once."""
+    if weight.dtype not in (torch.float32, act):
         weight = weight.float()
-    align = 8 if weight.dtype == torch.bfloat16 else 16  # u16x4 / float4 loads
+    align = 8 if weight.dtype != torch.float32 else 16  # u16x4 / float4 loads
     if not weight.is_contiguous() or weight.data_ptr() % align:
         weight = weight.contiguous().clone()
     if not weight.is_cuda or weight.numel() != H:
         raise ValueError(f"{name}: expected a GPU tensor of {H} elements")
-    return weight, int(weight.dtype == torch.bfloat16)
+    return weight, int(weight.dtype != torch.float32)
 
 
 def add_dropout_rmsnorm_fwd(resid, delta, weight, eps, p, key, out_dtype=torch.bfloat16, y_out=None):
     src = resid if resid is not None else delta
     M, H = src.shape
-    if out_dtype != torch.bfloat16:
-        raise TypeError("HIP rmsnorm emits bf16")
+    if out_dtype not in _HK:
+        raise TypeError("HIP rmsnorm emits bf16 or fp16")
     if resid is not None:
         _req(resid, torch.float32, "rmsnorm.resid", M * H)
     if delta is not None:
-        _req(delta, torch.bfloat16, "rmsnorm.delta", M * H)
-    w, wbf16 = _norm_weight(weight, H, "rmsnorm.weight")
-    y = torch.empty(M, H, dtype=torch.bfloat16, device=src.device) if y_out is None else y_out
-    _req(y, torch.bfloat16, "rmsnorm.y", M * H)
+        _req_act(delta, out_dtype, "rmsnorm.delta", M * H)
+    w, wbf16 = _norm_weight(weight, H, "rmsnorm.weight", out_dtype)
+    y = torch.empty(M, H, dtype=out_dtype, device=src.device) if y_out is None else y_out
+    hk = _req_act(y, out_dtype, "rmsnorm.y", M * H)
     rstd = torch.empty(M, dtype=torch.float32, device=src.device)
     if delta is None:
         x, xo = resid, None       # x is just the residual: no copy
@@ -336,34 +355,36 @@ def add_dropout_rmsnorm_fwd(resid, delta, weight, eps, p, key, out_dtype=torch.b
     dscale = 1.0 / (1.0 - p) if thr else 1.0
     _chk(lib().dlt_add_dropout_rmsnorm_fwd(_p(resid), _p(delta), _p(w), wbf16, _p(xo), _p(y), _p(rstd), M, H,
                                            float(eps),
-                                           key & 0xFFFFFFFF, thr, dscale, _stream()), "add_dropout_rmsnorm_fwd")
+                                           key & 0xFFFFFFFF, thr, dscale, hk, _stream()), "add_dropout_rmsnorm_fwd")
     return x, y, rstd
 
 
 def rmsnorm_bwd(dy, x, rstd, weight, dres, dweight, p_prev, key_prev, dy_scale=None, want_ddelta=True,
-                ddelta_out=None):
+                ddelta_out=None, dy_mul: float = 1.0):
     M, H = x.shape
-    _req(dy, torch.bfloat16, "rmsnorm_bwd.dy", M * H)
+    act = dy.dtype
+    hk = _req_act(dy, act, "rmsnorm_bwd.dy", M * H)
     _req(x, torch.float32, "rmsnorm_bwd.x", M * H)
     _req(rstd, torch.float32, "rmsnorm_bwd.rstd", M)
     if dres is not None:
         _req(dres, torch.float32, "rmsnorm_bwd.dres", M * H)
     _req(dweight, torch.float32, "rmsnorm_bwd.dweight", H)
-    w, wbf16 = _norm_weight(weight, H, "rmsnorm_bwd.weight")
+    w, wbf16 = _norm_weight(weight, H, "rmsnorm_bwd.weight", act)
     scale_t = None
     if dy_scale is not None:
         scale_t = dy_scale.reshape(1).float().contiguous()
     dx = torch.empty(M, H, dtype=torch.float32, device=x.device)
     dd = None
     if want_ddelta:
-        dd = torch.empty(M, H, dtype=torch.bfloat16, device=x.device) if ddelta_out is None else ddelta_out
-        _req(dd, torch.bfloat16, "rmsnorm_bwd.ddelta", M * H)
+        dd = torch.empty(M, H, dtype=act, device=x.device) if ddelta_out is None else ddelta_out
+        _req(dd, act, "rmsnorm_bwd.ddelta", M * H)
     thr = rng.keep_threshold(p_prev)
     dscale = 1.0 / (1.0 - p_prev) if thr else 1.0
     # per-block dw partials (two-stage column reduction instead of same-address atomics)
     ws = torch.empty(min((M + 3) // 4, 1024) * H, dtype=torch.float32, device=x.device)
     _chk(lib().dlt_rmsnorm_bwd(_p(dy), _p(x), _p(rstd), _p(w), wbf16, _p(dres), _p(dx), _p(dd), _p(dweight), _p(ws),
-                               _p(scale_t), M, H, key_prev & 0xFFFFFFFF, thr, dscale, _stream()), "rmsnorm_bwd")
+                               _p(scale_t), float(dy_mul), M, H, key_prev & 0xFFFFFFFF, thr, dscale, hk, _stream()),
+         "rmsnorm_bwd")
     return dx, dd
 
 
@@ -373,28 +394,30 @@ def rope_qkv_fwd(qkv, B, S, nh, cos, sin):
     hd = threeH // (3 * nh)
     if M != B * S or hd * 3 * nh != threeH:
         raise ValueError("rope_qkv_fwd: bad shapes")
-    _req(qkv, torch.bfloat16, "rope.qkv")
+    hk = _req_act(qkv, qkv.dtype, "rope.qkv")
     if cos.shape[0] < S or cos.shape[1] != hd // 2:
         raise ValueError("rope tables too short")
-    q = torch.empty(B, nh, S, hd, dtype=torch.bfloat16, device=qkv.device)
+    q = torch.empty(B, nh, S, hd, dtype=qkv.dtype, device=qkv.device)
     k = torch.empty_like(q)
     v = torch.empty_like(q)
-    _chk(lib().dlt_rope_qkv_fwd(_p(qkv), _p(cos), _p(sin), _p(q), _p(k), _p(v), B, S, nh, hd, _stream()),
+    _chk(lib().dlt_rope_qkv_fwd(_p(qkv), _p(cos), _p(sin), _p(q), _p(k), _p(v), B, S, nh, hd, hk, _stream()),
          "rope_qkv_fwd")
     return q, k, v
 
 
 def rope_qkv_bwd(dq, dk, dv, cos, sin, out=None):
     B, nh, S, hd = dk.shape
+    act = dk.dtype
     for t, n in ((dk, "dk"), (dv, "dv")):
-        _req(t, torch.bfloat16, "rope_bwd." + n, B * nh * S * hd)
+        hk = _req_act(t, act, "rope_bwd." + n, B * nh * S * hd)
     dqf = dq if dq.dtype == torch.float32 else None
-    dqb = dq if dq.dtype == torch.bfloat16 else None
+    dqb = dq if dq.dtype == act else None
     _req(dq, dq.dtype, "rope_bwd.dq", B * nh * S * hd)
     if out is None:
-        out = torch.empty(B * S, 3 * nh * hd, dtype=torch.bfloat16, device=dk.device)
-    _req(out, torch.bfloat16, "rope_bwd.out", B * S * 3 * nh * hd)
-    _chk(lib().dlt_rope_qkv_bwd(_p(dqb), _p(dqf), _p(dk), _p(dv), _p(cos), _p(sin), _p(out), B, S, nh, hd, _stream()),
+        out = torch.empty(B * S, 3 * nh * hd, dtype=act, device=dk.device)
+    _req(out, act, "rope_bwd.out", B * S * 3 * nh * hd)
+    _chk(lib().dlt_rope_qkv_bwd(_p(dqb), _p(dqf), _p(dk), _p(dv), _p(cos), _p(sin), _p(out), B, S, nh, hd, hk,
+                                _stream()),
          "rope_qkv_bwd")
     return out
 
@@ -405,12 +428,12 @@ def rope_qk_inplace(qkv, B, S, nh, cos, sin):
     hd = threeH // (3 * nh)
     if M != B * S or hd * 3 * nh != threeH or hd % 16:
         raise ValueError("rope_qk_inplace: bad shapes")
-    _req(qkv, torch.bfloat16, "rope_qk.qkv")
+    hk = _req_act(qkv, qkv.dtype, "rope_qk.qkv")
     if cos.shape[0] < S or cos.shape[1] != hd // 2 or sin.shape != cos.shape:
         raise ValueError("rope tables too short")
     _req(cos, torch.float32, "rope_qk.cos")
     _req(sin, torch.float32, "rope_qk.sin")
-    _chk(lib().dlt_rope_qk_inplace(_p(qkv), _p(cos), _p(sin), M, S, nh, hd, _stream()), "rope_qk_inplace")
+    _chk(lib().dlt_rope_qk_inplace(_p(qkv), _p(cos), _p(sin), M, S, nh, hd, hk, _stream()), "rope_qk_inplace")
     return qkv
 
 
@@ -443,11 +466,11 @@ def attention_fwd(q, k, v, p, key, causal=True, store_mask=True, out=None, mask=
         raise NotImplementedError("only causal attention is implemented (the model is a causal LM)")
     B, nh, S, hd = q.shape
     for t, n in ((q, "q"), (k, "k"), (v, "v")):
-        _req(t, torch.bfloat16, "attn." + n, B * nh * S * hd)
+        hk = _req_act(t, q.dtype, "attn." + n, B * nh * S * hd)
     if hd != 64:
         raise NotImplementedError(f"attention kernel is specialised for head_dim 64 (got {hd})")
-    o = torch.empty(B * S, nh * hd, dtype=torch.bfloat16, device=q.device) if out is None else out
-    _req(o, torch.bfloat16, "attn.o", B * S * nh * hd)
+    o = torch.empty(B * S, nh * hd, dtype=q.dtype, device=q.device) if out is None else out
+    _req(o, q.dtype, "attn.o", B * S * nh * hd)
     lse = torch.empty(B, nh, S, dtype=torch.float32, device=q.device)
     thr = rng.keep_threshold(p)
     dscale = 1.0 / (1.0 - p) if thr else 1.0
@@ -462,7 +485,7 @@ def attention_fwd(q, k, v, p, key, causal=True, store_mask=True, out=None, mask=
         # with store_mask=False it only lives for this call (the backward regenerates it)
         mask = torch.empty(2, B * nh, (S + 31) // 32, S, dtype=torch.int32, device=q.device)
     _chk(lib().dlt_attn_fwd(_p(q), _p(k), _p(v), _p(o), _p(lse), _p(mask), B, nh, S, hd, 1.0 / math.sqrt(hd),
-                            key & 0xFFFFFFFF, thr, dscale, gen, _stream()), "attn_fwd")
+                            key & 0xFFFFFFFF, thr, dscale, gen, hk, _stream()), "attn_fwd")
     return o, AttnAux((lse, mask if (store_mask or gen == 0) else None))
 
 
@@ -473,7 +496,7 @@ def _packed_dims(qkv, B, S, nh):
         raise ValueError("packed attention: qkv must be [B*S, 3*nh*hd]")
     if hd != 64:
         raise NotImplementedError(f"attention kernel is specialised for head_dim 64 (got {hd})")
-    _req(qkv, torch.bfloat16, "attn.qkv")
+    _req_act(qkv, qkv.dtype, "attn.qkv")
     return M, nh * hd, hd
 
 
@@ -481,8 +504,9 @@ def attention_fwd_packed(qkv, B, S, nh, p, key, out=None, mask=None, store_mask=
     """Causal attention reading q/k/v straight from the packed (roped) [B*S, 3H] QKV.
     Returns (o [B*S, H] bf16, aux) like :func:`attention_fwd`."""
     M, H, hd = _packed_dims(qkv, B, S, nh)
-    o = torch.empty(M, H, dtype=torch.bfloat16, device=qkv.device) if out is None else out
-    _req(o, torch.bfloat16, "attn.o", M * H)
+    hk = _HK[qkv.dtype]
+    o = torch.empty(M, H, dtype=qkv.dtype, device=qkv.device) if out is None else out
+    _req(o, qkv.dtype, "attn.o", M * H)
     lse = torch.empty(B, nh, S, dtype=torch.float32, device=qkv.device)
     thr = rng.keep_threshold(p)
     dscale = 1.0 / (1.0 - p) if thr else 1.0
@@ -495,7 +519,7 @@ def attention_fwd_packed(qkv, B, S, nh, p, key, out=None, mask=None, store_mask=
     else:  # with store_mask=False it only lives for this call (the backward regenerates it)
         mask = torch.empty(2, B * nh, (S + 31) // 32, S, dtype=torch.int32, device=qkv.device)
     _chk(lib().dlt_attn_fwd_ex(_p(qkv), _off(qkv, H), _off(qkv, 2 * H), _p(o), _p(lse), _p(mask), B, nh, S, hd,
-                               1.0 / math.sqrt(hd), key & 0xFFFFFFFF, thr, dscale, gen, S * 3 * H, hd, 3 * H,
+                               1.0 / math.sqrt(hd), key & 0xFFFFFFFF, thr, dscale, gen, S * 3 * H, hd, 3 * H, hk,
                                _stream()), "attn_fwd_packed")
     return o, AttnAux((lse, mask if (store_mask or gen == 0) else None))
 
@@ -505,8 +529,9 @@ def attention_bwd_packed(qkv, o, do, aux, p, key, B, S, nh, cos, sin, out=None):
     [B*S, 3H] (gradient w.r.t. the pre-rotation QKV GEMM output); dq/dk/dv are written
     into it by the attention kernels with the inverse rotation in their epilogue."""
     M, H, hd = _packed_dims(qkv, B, S, nh)
+    hk = _HK[qkv.dtype]
     for t, nm in ((o, "o"), (do, "do")):
-        _req(t, torch.bfloat16, "attn_bwd." + nm, M * H)
+        _req(t, qkv.dtype, "attn_bwd." + nm, M * H)
     lse, mask = aux if isinstance(aux, tuple) else (aux, None)
     _req(lse, torch.float32, "attn_bwd.lse", B * nh * S)
     if cos.shape[0] < S or cos.shape[1] != hd // 2 or sin.shape != cos.shape:
@@ -518,14 +543,14 @@ def attention_bwd_packed(qkv, o, do, aux, p, key, B, S, nh, cos, sin, out=None):
         mask = attention_dropout_mask(B, nh, S, p, key, device=qkv.device)
     if not thr:
         mask = None
-    dqkv = torch.empty(M, 3 * H, dtype=torch.bfloat16, device=qkv.device) if out is None else out
-    _req(dqkv, torch.bfloat16, "attn_bwd.dqkv", M * 3 * H)
+    dqkv = torch.empty(M, 3 * H, dtype=qkv.dtype, device=qkv.device) if out is None else out
+    _req(dqkv, qkv.dtype, "attn_bwd.dqkv", M * 3 * H)
     delta = torch.empty(B, nh, S, dtype=torch.float32, device=qkv.device)
     dscale = 1.0 / (1.0 - p) if thr else 1.0
     st = S * 3 * H
     _chk(lib().dlt_attn_bwd_ex(_p(qkv), _off(qkv, H), _off(qkv, 2 * H), _p(o), _p(do), _p(lse), _p(mask), _p(delta),
                                _p(dqkv), _off(dqkv, H), _off(dqkv, 2 * H), B, nh, S, hd, 1.0 / math.sqrt(hd), dscale,
-                               st, hd, 3 * H, st, hd, 3 * H, _p(cos), _p(sin), _stream()), "attn_bwd_packed")
+                               st, hd, 3 * H, st, hd, 3 * H, _p(cos), _p(sin), hk, _stream()), "attn_bwd_packed")
     return dqkv
 
 
@@ -533,7 +558,7 @@ def attention_bwd(q, k, v, o, do, aux, p, key, causal=True):
     B, nh, S, hd = q.shape
     n = B * nh * S * hd
     for t, nm in ((q, "q"), (k, "k"), (v, "v"), (o, "o"), (do, "do")):
-        _req(t, torch.bfloat16, "attn_bwd." + nm, n)
+        hk = _req_act(t, q.dtype, "attn_bwd." + nm, n)
     if isinstance(aux, tuple):
         lse, mask = aux
     else:
@@ -550,43 +575,46 @@ def attention_bwd(q, k, v, o, do, aux, p, key, causal=True):
     dv = torch.empty_like(v)
     dscale = 1.0 / (1.0 - p) if thr else 1.0
     _chk(lib().dlt_attn_bwd(_p(q), _p(k), _p(v), _p(o), _p(do), _p(lse), _p(mask), _p(delta), _p(dq), _p(dk), _p(dv),
-                            B, nh, S, hd, 1.0 / math.sqrt(hd), dscale, _stream()), "attn_bwd")
+                            B, nh, S, hd, 1.0 / math.sqrt(hd), dscale, hk, _stream()), "attn_bwd")
     return dq, dk, dv
 
 
 # ----------------------------------------------------------------- SwiGLU
 def swiglu_fwd(gu, out=None):
     M, twoI = gu.shape
-    _req(gu, torch.bfloat16, "swiglu.gu")
+    hk = _req_act(gu, gu.dtype, "swiglu.gu")
     if out is None:
-        out = torch.empty(M, twoI // 2, dtype=torch.bfloat16, device=gu.device)
-    _req(out, torch.bfloat16, "swiglu.out", M * twoI // 2)
-    _chk(lib().dlt_swiglu_fwd(_p(gu), _p(out), M, twoI // 2, _stream()), "swiglu_fwd")
+        out = torch.empty(M, twoI // 2, dtype=gu.dtype, device=gu.device)
+    _req(out, gu.dtype, "swiglu.out", M * twoI // 2)
+    _chk(lib().dlt_swiglu_fwd(_p(gu), _p(out), M, twoI // 2, hk, _stream()), "swiglu_fwd")
     return out
 
 
 def swiglu_bwd(gu, da, out=None):
     M, twoI = gu.shape
-    _req(gu, torch.bfloat16, "swiglu_bwd.gu")
-    _req(da, torch.bfloat16, "swiglu_bwd.da", M * twoI // 2)
+    hk = _req_act(gu, gu.dtype, "swiglu_bwd.gu")
+    _req(da, gu.dtype, "swiglu_bwd.da", M * twoI // 2)
     if out is None:
         out = torch.empty_like(gu)
-    _req(out, torch.bfloat16, "swiglu_bwd.out", M * twoI)
-    _chk(lib().dlt_swiglu_bwd(_p(gu), _p(da), _p(out), M, twoI // 2, _stream()), "swiglu_bwd")
+    _req(out, gu.dtype, "swiglu_bwd.out", M * twoI)
+    _chk(lib().dlt_swiglu_bwd(_p(gu), _p(da), _p(out), M, twoI // 2, hk, _stream()), "swiglu_bwd")
     return out
 
 
 # ------------------------------------------------------------ cross-entropy
-def cross_entropy_fwd_bwd(logits, targets, vocab, n_valid):
+def cross_entropy_fwd_bwd(logits, targets, vocab, n_valid, grad_scale: float = 1.0):
+    """Per-row loss; the logits buffer (bf16 or fp16) is overwritten by
+    grad_scale * (softmax - onehot) / n_valid (fp16: grad_scale = the loss scale, so the
+    gradient does not underflow)."""
     M, Vp = logits.shape
-    _req(logits, torch.bfloat16, "ce.logits")
+    hk = _req_act(logits, logits.dtype, "ce.logits")
     targets = targets.contiguous()
     if targets.dtype != torch.int64 or targets.numel() != M:
         raise ValueError("ce.targets must be int64 [M]")
     nv = n_valid.reshape(1).to(torch.int64).contiguous()
     loss = torch.empty(M, dtype=torch.float32, device=logits.device)
-    _chk(lib().dlt_cross_entropy_fwd_bwd(_p(logits), _p(targets), _p(nv), _p(loss), M, Vp, vocab, _stream()),
-         "cross_entropy")
+    _chk(lib().dlt_cross_entropy_fwd_bwd(_p(logits), _p(targets), _p(nv), _p(loss), M, Vp, vocab,
+                                         float(grad_scale), hk, _stream()), "cross_entropy")
     return loss
 
 
@@ -829,14 +857,16 @@ def gemm_down_swiglu_bwd(dd: torch.Tensor, wdown: torch.Tensor, gu: torch.Tensor
     return c
 
 
-def scale_bf16(x: torch.Tensor, scale: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """y = x * scale with a device scalar (no host sync); falls back for odd sizes."""
-    _req(x, torch.bfloat16, "scale_bf16.x")
+def scale_bf16(x: torch.Tensor, scale: torch.Tensor, out: Optional[torch.Tensor] = None,
+               mul: float = 1.0) -> torch.Tensor:
+    """y = x * scale * mul with a device scalar (no host sync) and a host factor, x bf16
+    or fp16; falls back for odd sizes."""
+    hk = _req_act(x, x.dtype, "scale_bf16.x")
     s = scale.reshape(1).float().contiguous()
     if x.numel() % 8:
-        y = (x.float() * s).to(torch.bfloat16)
+        y = (x.float() * s * mul).to(x.dtype)
         return y if out is None else out.copy_(y)
     y = torch.empty_like(x) if out is None else out
-    _req(y, torch.bfloat16, "scale_bf16.out", x.numel())
-    _chk(lib().dlt_scale_bf16(_p(x), _p(y), x.numel(), _p(s), _stream()), "scale_bf16")
+    _req(y, x.dtype, "scale_bf16.out", x.numel())
+    _chk(lib().dlt_scale_bf16(_p(x), _p(y), x.numel(), _p(s), float(mul), hk, _stream()), "scale_bf16")
     return y

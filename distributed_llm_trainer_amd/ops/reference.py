@@ -63,7 +63,7 @@ def add_dropout_rmsnorm_fwd(resid: Optional[torch.Tensor], delta: Optional[torch
 def rmsnorm_bwd(dy: torch.Tensor, x: torch.Tensor, rstd: torch.Tensor, weight: torch.Tensor,
                 dres: Optional[torch.Tensor], dweight: torch.Tensor, p_prev: float, key_prev: int,
                 dy_scale: Optional[torch.Tensor] = None,
-                want_ddelta: bool = True, ddelta_out=None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+                want_ddelta: bool = True, ddelta_out=None, dy_mul: float = 1.0) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     """Backward of add_dropout_rmsnorm.
 
     dx = dres + J_rmsnorm^T dy ; ddelta = dropout_bwd(dx) (grad for the delta that was
@@ -74,6 +74,8 @@ def rmsnorm_bwd(dy: torch.Tensor, x: torch.Tensor, rstd: torch.Tensor, weight: t
     dy = dy.float()
     if dy_scale is not None:
         dy = dy * dy_scale.float()
+    if dy_mul != 1.0:
+        dy = dy * dy_mul
     r = rstd.float().unsqueeze(-1)
     xh = x.float() * r
     w = weight.float()
@@ -254,8 +256,9 @@ def swiglu_bwd(gu: torch.Tensor, da: torch.Tensor, out=None) -> torch.Tensor:
 
 # ------------------------------------------------------ cross-entropy (fused with grad)
 def cross_entropy_fwd_bwd(logits: torch.Tensor, targets: torch.Tensor, vocab: int,
-                          n_valid: torch.Tensor) -> torch.Tensor:
-    """Per-row loss [M] fp32; ``logits`` [M, Vp] is overwritten with dloss_mean/dlogits.
+                          n_valid: torch.Tensor, grad_scale: float = 1.0) -> torch.Tensor:
+    """Per-row loss [M] fp32; ``logits`` [M, Vp] is overwritten with
+    grad_scale * dloss_mean/dlogits.
 
     Columns >= vocab are padding and get zero gradient.  Rows whose target is
     IGNORE_INDEX get zero loss and zero gradient.  ``n_valid`` is a 0-dim tensor.
@@ -268,7 +271,7 @@ def cross_entropy_fwd_bwd(logits: torch.Tensor, targets: torch.Tensor, vocab: in
     loss = torch.where(valid, lse - picked, torch.zeros_like(lse))
     grad = torch.exp(lf - lse.unsqueeze(1))
     grad.scatter_add_(1, tgt.unsqueeze(1), -torch.ones_like(picked).unsqueeze(1))
-    grad = grad * (valid.float() / n_valid.float().clamp(min=1)).unsqueeze(1)
+    grad = grad * (valid.float() * grad_scale / n_valid.float().clamp(min=1)).unsqueeze(1)
     logits.zero_()
     logits[:, :vocab] = grad.to(logits.dtype)
     return loss
@@ -295,7 +298,7 @@ def sumsq(x: torch.Tensor, out: torch.Tensor) -> None:
     out += x.float().pow(2).sum()
 
 
-def scale_bf16(x: torch.Tensor, scale: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
-    """y = x * scale (scale: 0-d/1-element device tensor), result in x's dtype."""
-    y = (x.float() * scale.reshape(()).float()).to(x.dtype)
+def scale_bf16(x: torch.Tensor, scale: torch.Tensor, out: torch.Tensor = None, mul: float = 1.0) -> torch.Tensor:
+    """y = x * scale * mul (scale: 0-d/1-element device tensor), result in x's dtype."""
+    y = (x.float() * scale.reshape(()).float() * mul).to(x.dtype)
     return y if out is None else out.copy_(y)

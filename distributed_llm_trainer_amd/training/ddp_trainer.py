@@ -85,9 +85,10 @@ class DistributedTrainer:
         self._good_steps = 0
         # reference ddp_trainer.py:129-152: bf16 autocast, fp16 autocast + GradScaler, or
         # fp32.  Here every mode runs the fused engine with fp32 master weights and a
-        # compute-dtype shadow: bf16 on the HIP kernels; fp16 / fp32 with PyTorch ops on
-        # the GPU + hipBLASLt GEMMs (GPT.enable_engine) and, for fp16, dynamic loss scaling
-        # (2^16, x0.5 and skip on inf/nan, x2 after 2000 good steps: GradScaler defaults)
+        # compute-dtype shadow: bf16 and fp16 on the HIP kernels (fp16: the same kernels
+        # instantiated for IEEE half, hipBLASLt fp16 GEMMs, dynamic loss scaling -- 2^16,
+        # x0.5 and skip on inf/nan, x2 after 2000 good steps: GradScaler defaults); fp32
+        # (the reference / debug mode) with PyTorch ops on the GPU + hipBLASLt GEMMs
         if cuda and mp == "bf16":
             self.dtype = torch.bfloat16
         elif cuda and mp == "fp16":
@@ -98,9 +99,9 @@ class DistributedTrainer:
         else:
             self.dtype = torch.float32
         if self.is_main_process:
-            path = ("fused HIP engine" if self.dtype == torch.bfloat16 else "fused engine (PyTorch ops + hipBLASLt "
-                    "on the GPU)") if (use_engine and cuda) else ("fused engine (CPU reference ops)"
-                                                                  if use_engine else "eager")
+            path = ("fused HIP engine" if self.dtype in (torch.bfloat16, torch.float16) else
+                    "fused engine (PyTorch ops + hipBLASLt on the GPU: fp32 reference mode)") if (use_engine and cuda) \
+                else ("fused engine (CPU reference ops)" if use_engine else "eager")
             print(f"Device: {self.device}")
             print(f"Mixed precision: {mp} (dtype: {self.dtype}) | execution: {path}")
 
@@ -162,6 +163,9 @@ class DistributedTrainer:
         chains, chain_bs = GA // F, micro_bs * F
         if self.use_engine:
             self.model.engine.set_loss_segments(F)
+            # fp16: the cross-entropy gradient is stored pre-scaled by the loss scale (no
+            # fp16 underflow); the engine divides it out where dloss is applied
+            self.model.engine.ce_grad_scale = float(self.loss_scale or 1.0)
         total = torch.zeros((), dtype=torch.float32, device=self.device)
         # micro-step pipelining (engine.train_window): from the second step on, so the
         # first one runs the GEMM autotuning on a quiet GPU

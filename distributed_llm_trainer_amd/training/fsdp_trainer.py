@@ -57,7 +57,8 @@ class FSDPTrainer:
         # Precision policies (reference fsdp_trainer.py:223-234: bf16 -> MixedPrecision(bf16,
         # bf16, bf16), fp16 -> all fp16, otherwise none).  Master shards are always fp32;
         # the gathered compute copy, the activations and the reduce-scatter wire take the
-        # policy dtype.  bf16 runs the HIP kernels; fp16 / fp32 run the same schedule with
+        # policy dtype.  bf16 and fp16 run the HIP kernels (fp16: IEEE-half instances,
+        # hipBLASLt fp16 GEMMs); fp32 (reference / debug mode) runs the same schedule with
         # PyTorch ops on the GPU + hipBLASLt GEMMs (GPT.enable_engine).  fp16 adds a
         # dynamic loss scale the reference lacks (Q11): the global grad sumsq is
         # all-reduced anyway for clipping, so an inf/nan on ANY rank's shard skips the step
@@ -149,6 +150,9 @@ class FSDPTrainer:
                      and (self.device.type != "cuda" or getattr(eng.gemm, "stream_safe", False))
                      and os.environ.get("DLT_PIPELINE", "1") != "0")
         ls = self.loss_scale or 1.0
+        # fp16: the cross-entropy gradient is stored pre-scaled by the loss scale (no fp16
+        # underflow); the engine divides it out where dloss (= ls / chains) is applied
+        eng.ce_grad_scale = float(ls)
         if pipelined:
             from ..models.engine import shift_targets
             ids_l = [input_ids[m * chain_bs:(m + 1) * chain_bs] for m in range(chains)]

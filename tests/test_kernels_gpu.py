@@ -746,3 +746,78 @@ def test_attention_packed_real_shapes(B, S, nh, p):
     want = ref.attention_bwd_packed(packed.float(), o.float(), do.float(), lse_ref, p, key, B, S, nh, cos, sin)
     for blk, name in ((slice(0, H), "dq"), (slice(H, 2 * H), "dk"), (slice(2 * H, 3 * H), "dv")):
         assert _relerr(got[:, blk], want[:, blk]) < 2e-2, name
+
+
+# ------------------------------------------------------------------ fp16 (HK = 1)
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_fp16_attention_packed_vs_fp32(p):
+    """--mixed_precision fp16: the packed attention kernels instantiated for IEEE half
+    (v_mfma_f32_32x32x16_f16, fp16 P / dS operands) against the fp32 reference of the
+    whole chain (RoPE in place, causal attention with dropout, inverse RoPE in the
+    backward epilogue), per-tensor relative error."""
+    torch.manual_seed(61)
+    B, S, nh = 2, 512, 4
+    H = nh * 64
+    raw = torch.randn(B * S, 3 * H, device=DEV).half()
+    cos, sin = hip.rope_tables(64, S, device=DEV)
+    key = rng.site_key(5, 2, 1, rng.SITE_ATTN)
+    packed = hip.rope_qk_inplace(raw.clone(), B, S, nh, cos, sin)
+    want_packed = ref.rope_qk_inplace(raw.float().clone(), B, S, nh, cos, sin)
+    assert packed.dtype == torch.float16 and _relerr(packed, want_packed) < 2e-3
+    o, aux = hip.attention_fwd_packed(packed, B, S, nh, p, key)
+    assert o.dtype == torch.float16
+    o_ref, lse_ref = ref.attention_fwd_packed(packed.float(), B, S, nh, p, key)
+    assert _relerr(o, o_ref) < 4e-3, _relerr(o, o_ref)
+    _close(aux[0], lse_ref, 2e-3, 1e-3, "lse fp16")
+    do = torch.randn(B * S, H, device=DEV).half()
+    got = hip.attention_bwd_packed(packed, o, do, aux, p, key, B, S, nh, cos, sin)
+    assert got.dtype == torch.float16
+    want = ref.attention_bwd_packed(packed.float(), o.float(), do.float(), lse_ref, p, key, B, S, nh, cos, sin)
+    for blk, name in ((slice(0, H), "dq"), (slice(H, 2 * H), "dk"), (slice(2 * H, 3 * H), "dv")):
+        e = _relerr(got[:, blk], want[:, blk])
+        assert e < 6e-3, (name, e)
+
+
+def test_fp16_norm_swiglu_ce_scale_vs_fp32():
+    """The elementwise / norm / loss kernels in fp16 against fp32 references: residual +
+    dropout + RMSNorm forward and backward (fp16 delta, y, dy, ddelta), SwiGLU forward /
+    backward, cross-entropy with the loss-scaled in-place gradient, scale."""
+    torch.manual_seed(62)
+    M, H, I, V = 512, 768, 3072, 1000
+    key = rng.site_key(1, 2, 3, rng.SITE_RESID)
+    r = torch.randn(M, H, device=DEV)
+    d = torch.randn(M, H, device=DEV).half()
+    w = torch.rand(H, device=DEV) + 0.5
+    x, y, rstd = hip.add_dropout_rmsnorm_fwd(r, d, w, 1e-6, 0.1, key, out_dtype=torch.float16)
+    xr, yr, rstdr = ref.add_dropout_rmsnorm_fwd(r, d.float(), w, 1e-6, 0.1, key, out_dtype=torch.float32)
+    assert y.dtype == torch.float16 and _relerr(y, yr) < 1e-3
+    _close(x, xr, 1e-5, 1e-5, "x fp16 path")
+    dy = torch.randn(M, H, device=DEV).half()
+    dres = torch.randn(M, H, device=DEV)
+    dw1, dw2 = torch.zeros(H, device=DEV), torch.zeros(H, device=DEV)
+    dx, dd = hip.rmsnorm_bwd(dy, x, rstd, w, dres, dw1, 0.1, key, dy_mul=0.5)
+    dxr, ddr = ref.rmsnorm_bwd(dy.float(), xr, rstdr, w, dres, dw2, 0.1, key, dy_mul=0.5)
+    assert dd.dtype == torch.float16
+    assert _relerr(dx, dxr) < 1e-4 and _relerr(dd, ddr) < 1e-3 and _relerr(dw1, dw2) < 1e-4
+    gu = (torch.randn(M, 2 * I, device=DEV) * 2).half()
+    s = hip.swiglu_fwd(gu)
+    g, u = gu.float()[:, :I], gu.float()[:, I:]
+    assert s.dtype == torch.float16 and _relerr(s, g * torch.sigmoid(g) * u) < 1e-3
+    da = torch.randn(M, I, device=DEV).half()
+    dgu = hip.swiglu_bwd(gu, da)
+    dgu_r = ref.swiglu_bwd(gu.float(), da.float())
+    assert _relerr(dgu, dgu_r) < 1e-3
+    Vp = 1024
+    logits = torch.randn(M, Vp, device=DEV).half()
+    tgt = torch.randint(0, V, (M,), device=DEV)
+    tgt[::7] = -100
+    nv = (tgt != -100).sum()
+    lg_ref = logits.float().clone()
+    loss_r = ref.cross_entropy_fwd_bwd(lg_ref, tgt, V, nv, grad_scale=4096.0)
+    lg = logits.clone()
+    loss = hip.cross_entropy_fwd_bwd(lg, tgt, V, nv, grad_scale=4096.0)
+    _close(loss, loss_r, 2e-3, 1e-3, "ce loss fp16")
+    assert _relerr(lg, lg_ref) < 2e-3  # the gradient is representable (no fp16 underflow)
+    sc = torch.full((), 0.25, device=DEV)
+    z = hip.scale_bf16(d, sc, mul=2.0)
+    assert z.dtype == torch.float16 and torch.equal(z, (d.float() * 0.5).half())

@@ -43,10 +43,10 @@ st = S * 3 * H
 for name, bs, hs in (("normal", st, hd), ("one head (L2)", 0, 0)):
     def fwd():
         lib().dlt_attn_fwd_ex(_p(qkv), _off(qkv, H), _off(qkv, 2 * H), _p(o), _p(lse), _p(mask), B, nh, S, hd,
-                              1.0 / math.sqrt(hd), key & 0xFFFFFFFF, thr, ds, 0, bs, hs, 3 * H, _stream())
+                              1.0 / math.sqrt(hd), key & 0xFFFFFFFF, thr, ds, 0, bs, hs, 3 * H, 0, _stream())
 
     def bwd():
         lib().dlt_attn_bwd_ex(_p(qkv), _off(qkv, H), _off(qkv, 2 * H), _p(o), _p(do), _p(lse), _p(mask), _p(delta),
                               _p(dqkv), _off(dqkv, H), _off(dqkv, 2 * H), B, nh, S, hd, 1.0 / math.sqrt(hd), ds,
-                              bs, hs, 3 * H, st, hd, 3 * H, _p(cos), _p(sin), _stream())
+                              bs, hs, 3 * H, st, hd, 3 * H, _p(cos), _p(sin), 0, _stream())
     print(f"{name:14s} fwd {timeit(fwd):6.1f} us  bwd (dQ + dK/dV) {timeit(bwd):6.1f} us", flush=True)

@@ -19,9 +19,9 @@ int main() {
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
   for (int drop = 0; drop < 2; ++drop) {
     unsigned thr = drop ? 6554 : 0;
-    for (int i = 0; i < 3; ++i) dlt_attn_fwd(q, k, v, o, lse, mask, B, nh, S, hd, 0.125f, 77, thr, 1.f / 0.9f, 1, 0);
+    for (int i = 0; i < 3; ++i) dlt_attn_fwd(q, k, v, o, lse, mask, B, nh, S, hd, 0.125f, 77, thr, 1.f / 0.9f, 1, 0, 0);
     hipEventRecord(e0, 0);
-    for (int i = 0; i < 20; ++i) dlt_attn_fwd(q, k, v, o, lse, mask, B, nh, S, hd, 0.125f, 77, thr, 1.f / 0.9f, 1, 0);
+    for (int i = 0; i < 20; ++i) dlt_attn_fwd(q, k, v, o, lse, mask, B, nh, S, hd, 0.125f, 77, thr, 1.f / 0.9f, 1, 0, 0);
     hipEventRecord(e1, 0); hipEventSynchronize(e1);
     float ms; hipEventElapsedTime(&ms, e0, e1);
     printf("dropout=%d fwd %.1f us\n", drop, ms * 1000 / 20);

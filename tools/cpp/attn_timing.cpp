@@ -30,10 +30,10 @@ int main(int argc, char** argv) {
   (void)hipMalloc(&tim, (size_t)G * 2 * 8 * 8);
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_attn_tim), &tim, sizeof(tim));
   const unsigned thr = 6554;
-  dlt_attn_fwd(q, k, v, o, lse, mask, B, nh, S, hd, 0.125f, 77, thr, 1.f / 0.9f, 1, 0);
-  for (int i = 0; i < 3; ++i) dlt_attn_bwd(q, k, v, o, dout, lse, mask, delta, dq, dk, dv, B, nh, S, hd, 0.125f, 1.f / 0.9f, 0);
+  dlt_attn_fwd(q, k, v, o, lse, mask, B, nh, S, hd, 0.125f, 77, thr, 1.f / 0.9f, 1, 0, 0);
+  for (int i = 0; i < 3; ++i) dlt_attn_bwd(q, k, v, o, dout, lse, mask, delta, dq, dk, dv, B, nh, S, hd, 0.125f, 1.f / 0.9f, 0, 0);
   (void)hipMemset(tim, 0, (size_t)G * 2 * 8 * 8);
-  dlt_attn_bwd(q, k, v, o, dout, lse, mask, delta, dq, dk, dv, B, nh, S, hd, 0.125f, 1.f / 0.9f, 0);
+  dlt_attn_bwd(q, k, v, o, dout, lse, mask, delta, dq, dk, dv, B, nh, S, hd, 0.125f, 1.f / 0.9f, 0, 0);
   (void)hipDeviceSynchronize();
   std::vector<unsigned long long> h((size_t)G * 2 * 8);
   (void)hipMemcpy(h.data(), tim, h.size() * 8, hipMemcpyDeviceToHost);

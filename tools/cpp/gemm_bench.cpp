@@ -197,8 +197,8 @@ static int epi_main(int M, int H, int I, int S) {
     auto unfused = [&]() {
       int rc = run_blas(A, B, C2, M, N, K, st);
       if (rc) return rc;
-      if (which == 0) return dlt_rope_qk_inplace(C2, dc, ds, M, S, H / 64, 64, st);
-      return dlt_swiglu_fwd(C2, Sb2, M, I, st);
+      if (which == 0) return dlt_rope_qk_inplace(C2, dc, ds, M, S, H / 64, 64, 0, st);
+      return dlt_swiglu_fwd(C2, Sb2, M, I, 0, st);
     };
     CK(hipMemsetAsync(C, 0xff, (size_t)M * N * 2, st));
     if (fused() != 0) {
@@ -395,7 +395,7 @@ static int dgrad_main(std::vector<int> shp) {
     auto fused = [&]() { return dlt_gemm_bf16_down_swiglu_bwd(dd, Wd, gu, dgu, M, I, H, 0, st); };
     auto unfused = [&]() {
       int rc = run_blas_nn(dd, Wd, ds, M, I, H, st);
-      return rc ? rc : dlt_swiglu_bwd(gu, ds, dgu2, M, I, st);
+      return rc ? rc : dlt_swiglu_bwd(gu, ds, dgu2, M, I, 0, st);
     };
     CK(hipMemsetAsync(dgu, 0xff, (size_t)M * 2 * I * 2, st));
     if (fused()) {
@@ -595,7 +595,7 @@ static int overlap_main() {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   auto G = [&](hipStream_t s) { return run_blas(A, B, C, M, N, K, s); };
-  auto E = [&](hipStream_t s) { return dlt_swiglu_fwd(gu, sb, M, I, s); };
+  auto E = [&](hipStream_t s) { return dlt_swiglu_fwd(gu, sb, M, I, 0, s); };
   G(s0);
   CK(hipDeviceSynchronize());
   const int reps = 20;
