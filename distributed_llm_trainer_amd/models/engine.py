@@ -838,14 +838,21 @@ class GPTEngine:
             sched = "fb"
         return overlap, sched
 
-    def _window_ffbb(self, micro_ids, micro_targets, dloss, recompute, defer, sync_hook, before_last):
-        """Two-chain window F0 || F1 | B0 || B1 (see train_window)."""
+    def _window_ffbb(self, micro_ids, micro_targets, dloss, recompute, defer, sync_hook, before_last,
+                     serial=False):
+        """Two-chain window F0 || F1 | B0 || B1 (see train_window).  ``serial``: the same
+        block order with both chains on the current stream (the trainers' first step,
+        whose GEMM races must time on a quiet GPU) -- same kernels, same results, and
+        the same dY slot ring, so the first step does not need per-layer dY slots."""
         dev = micro_ids[0].device
         self.set_accumulation(0, 2, defer=defer)
         main = torch.cuda.current_stream(dev)
-        if self._pipe is None:
-            self._pipe = torch.cuda.Stream(dev)
-        p0 = self._pipe
+        if serial:
+            p0 = main
+        else:
+            if self._pipe is None:
+                self._pipe = torch.cuda.Stream(dev)
+            p0 = self._pipe
         self.rope(micro_ids[0].shape[1], dev)
         self._wgrad_stream(dev)  # created before the fork
         p0.wait_stream(main)
@@ -854,7 +861,7 @@ class GPTEngine:
         # (DLT_FFBB_GEMM_GRID, default 192 of 256 workgroups: +0.05-0.5 % in three same-box
         # A/Bs, docs/KERNELS.md; results unchanged, each output tile is still computed
         # whole by one workgroup)
-        cap = int(os.environ.get("DLT_FFBB_GEMM_GRID", "192"))
+        cap = int(os.environ.get("DLT_FFBB_GEMM_GRID", "192")) if not serial else 0
         prev_cap = self.ops.gemm_grid_cap(cap) if cap and hasattr(self.ops, "gemm_grid_cap") else None
         # The two backwards run a block apart and the last one issues each layer's window
         # weight gradients right after its own block, so a layer's dY operands (dqkv, da,
@@ -865,6 +872,9 @@ class GPTEngine:
         ring = int(os.environ.get("DLT_SLOT_RING", "3")) if defer else 0
         self._ring = ring if 2 <= ring < self.cfg.num_layers else 0
         self._ring_done = {}
+        if self._ring:  # per-layer dY slots of an earlier schedule would only hold memory
+            for key in [k for k in self._slots if k[1] in self._DY_SLOTS and not isinstance(k[0], tuple)]:
+                del self._slots[key]
         try:
             return self._window_ffbb_body(micro_ids, micro_targets, dloss, recompute, defer, sync_hook, before_last,
                                           main, p0, streams)
@@ -917,7 +927,7 @@ class GPTEngine:
     def train_window(self, micro_ids: List[torch.Tensor], micro_targets: List[torch.Tensor],
                      dloss: torch.Tensor, recompute: bool = False,
                      before_last: Optional[Callable[[], None]] = None, defer: bool = True,
-                     sync_hook: Optional[Callable[[bool], None]] = None) -> List[torch.Tensor]:
+                     sync_hook: Optional[Callable[[bool], None]] = None, serial: bool = False) -> List[torch.Tensor]:
         """Forward + backward of a whole gradient-accumulation window.
 
         Schedule (GA = 4):  F0 | B0+F1 | B1+F2 | B2+F3 | B3, where "Bk+Fk+1" issues the
@@ -964,7 +974,10 @@ class GPTEngine:
         overlap, sched = self.window_schedule(GA, defer, cuda)
         prog: List[dict] = [dict() for _ in range(GA)]
         if sched == "ffbb":
-            return self._window_ffbb(micro_ids, micro_targets, dloss, recompute, defer, sync_hook, before_last)
+            return self._window_ffbb(micro_ids, micro_targets, dloss, recompute, defer, sync_hook, before_last,
+                                     serial=serial)
+        if serial:
+            raise ValueError("serial=True is the single-stream form of the ffbb window only")
         self.set_accumulation(0, GA, defer=defer)
         main = pipe = None
         if cuda:
@@ -1031,7 +1044,7 @@ class GPTEngine:
 def _wgrad(gm, dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
     """A layer weight gradient: accumulated into the provider's fp32 buffer, or written
     once per micro-step into a bf16 reduce-scatter buffer (FSDPRuntime.bf16_grads)."""
-    if dw.dtype == torch.bfloat16:
+    if dw.dtype in (torch.bfloat16, torch.float16):
         gm.wgrad_set(dw, dy, x)
     else:
         gm.wgrad_acc(dw, dy, x)
@@ -1069,13 +1082,13 @@ class _TorchGemm:
     def wgrad_set(dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
         """dw (bf16, overwritten) = dy^T @ x (the FSDP bf16 send-buffer mode)."""
         dw2 = dw.view(dy.shape[1], x.shape[1])
-        if dw2.dtype != torch.bfloat16 or not dw2.is_contiguous():
-            raise ValueError("wgrad_set output must be contiguous bf16")
+        if dw2.dtype not in (torch.bfloat16, torch.float16) or not dw2.is_contiguous():
+            raise ValueError("wgrad_set output must be contiguous bf16 / fp16")
         torch.matmul(dy.t(), x, out=dw2)
 
     def wgrad_acc(self, dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
-        if dw.dtype == torch.bfloat16:
-            raise ValueError("wgrad_acc accumulates into fp32; use wgrad_set for a bf16 gradient")
+        if dw.dtype in (torch.bfloat16, torch.float16):
+            raise ValueError("wgrad_acc accumulates into fp32; use wgrad_set for a 16-bit gradient")
         dw2 = dw.view(dy.shape[1], x.shape[1])
         if dy.dtype == torch.float32:
             dw2.addmm_(dy.t(), x)

@@ -416,6 +416,7 @@ __global__ __launch_bounds__(256) void k_splitk_acc(const float4* __restrict__ p
 // out[i] = bf16(sum_{s < splits} part[s * n + i]) -- the split-K weight gradient written
 // straight in the reduce dtype (FSDP: the per-micro-step unit gradient IS the
 // reduce-scatter send buffer, no fp32 zero / accumulate / cast passes).  Fixed order.
+template <int HK = 0>
 __global__ __launch_bounds__(256) void k_splitk_sum_bf16(const float4* __restrict__ part, uint2* __restrict__ out,
                                                          long n4, int splits) {
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
@@ -427,16 +428,18 @@ __global__ __launch_bounds__(256) void k_splitk_sum_bf16(const float4* __restric
       a.z += p.z;
       a.w += p.w;
     }
-    out[i] = uint2{(uint32_t)f2bf(a.x) | ((uint32_t)f2bf(a.y) << 16), (uint32_t)f2bf(a.z) | ((uint32_t)f2bf(a.w) << 16)};
+    out[i] = uint2{(uint32_t)f2h<HK>(a.x) | ((uint32_t)f2h<HK>(a.y) << 16),
+                   (uint32_t)f2h<HK>(a.z) | ((uint32_t)f2h<HK>(a.w) << 16)};
   }
 }
 
-DLT_API int dlt_splitk_sum_bf16(const float* part, bf16_t* out, long n, int splits, hipStream_t s) {
+// hk: output format (0 bf16, 1 fp16)
+DLT_API int dlt_splitk_sum_bf16(const float* part, bf16_t* out, long n, int splits, int hk, hipStream_t s) {
   if (n <= 0 || (n & 3) || splits < 1) return -1;
   const long n4 = n / 4;
   const int blocks = (int)std::min<long>((n4 + 255) / 256, 2048);
-  hipLaunchKernelGGL(k_splitk_sum_bf16, dim3(blocks), dim3(256), 0, s, reinterpret_cast<const float4*>(part),
-                     reinterpret_cast<uint2*>(out), n4, splits);
+  DLT_HK_DISPATCH(hk, k_splitk_sum_bf16<HKC><<<blocks, 256, 0, s>>>(reinterpret_cast<const float4*>(part),
+                                                                   reinterpret_cast<uint2*>(out), n4, splits));
   return (int)hipGetLastError();
 }
 

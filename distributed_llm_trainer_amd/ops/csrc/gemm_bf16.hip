@@ -182,26 +182,41 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
   // tile walk: round r, workgroup b on "XCD slot" x = b % 8 -> linear tile
   // r*G + x*(G/8) + b/8: the workgroups of one XCD cover G/8 consecutive tiles per round
   const int gx = G >> 3;
-  auto tile_of = [&](int r) { return r * G + (bid & 7) * gx + (bid >> 3); };
+  // order 3 (flags bits 2-3): XCD row bands -- XCD slot x owns tile rows
+  // [x * ntm/8, (x+1) * ntm/8) and walks every column tile over them (ntm/8 rows x
+  // gx/(ntm/8) columns per round), so its A panels (ntm/8 x 384 KB at K = 768) stay in
+  // its L2 for the whole kernel and every B panel is read once per XCD.  For the lm_head
+  // (64 x 262 tiles) the grouped walk re-reads each A panel 131 times from beyond L2.
+  const int ntm = M / GB_BM;
+  const bool xband = ((flags >> 2) & 3) == 3 && (ntm & 7) == 0 && gx % (ntm >> 3) == 0;
+  const int band = xband ? (ntm >> 3) * ntn : 0;  // tiles per XCD slot
+  auto tile_of = [&](int r) {
+    return xband ? (bid & 7) * band + r * gx + (bid >> 3) : r * G + (bid & 7) * gx + (bid >> 3);
+  };
+  const int tend = xband ? ((bid & 7) + 1) * band : ntiles;  // first tile past this workgroup's range
   // linear tile -> (tile row, tile col).  With 32 workgroups per XCD slot and whole
   // 32-tile super-tiles (GM x GN tiles, GN = 8 / 4 / 2 n-tiles), super-tile s = L / 32 is
   // one XCD's work of one round and the super-tiles walk DOWN a super-column
   // (column-major), so an XCD keeps the same GN B panels for consecutive rounds and its
   // per-round operand set (GM A panels + GN B panels, ~4 MB at K = 768) fits its L2.
   // Otherwise plain row-major.
-  const int ntm = M / GB_BM;
   const int gn = (ntn & 7) == 0 ? 8 : (ntn & 3) == 0 ? 4 : (ntn & 1) == 0 ? 2 : 1;
   const int gm = 32 / gn;
   // flags (ablation only, 0 in production): bit 0 skip the C stores, bit 1 every tile
   // reads tile (0, 0)'s operand panels (L2-resident), bits 2-3 tile order (0 = grouped
-  // column walk, 1 = row-major, 2 = grouped row walk), 16 every tile stores to tile (0, 0),
+  // column walk, 1 = row-major, 2 = grouped row walk, 3 = XCD row bands), 16 every tile
+  // stores to tile (0, 0),
   // 32 s_waitcnt vmcnt(0) after the stores
   const int order = (flags >> 2) & 3;
   const bool grouped = order != 1 && gx == 32 && ntiles % 32 == 0 && ntm % gm == 0;
   const int scols = ntn / gn;
   const int srows = ntm / gm;
   auto coords = [&](int L, int& tm, int& tn) {
-    if (grouped) {
+    if (xband) {
+      const int rpx = ntm >> 3, x = L / band, j = L - x * band;
+      tm = x * rpx + j % rpx;
+      tn = j / rpx;
+    } else if (grouped) {
       const int sidx = L >> 5, i = L & 31;
       if (order == 2) {
         tm = (sidx / scols) * gm + i / gn;
@@ -358,7 +373,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
   uint64_t a_it0 = 0, a_rest = 0, a_epi = 0, ntl = 0, t1 = 0;
 #endif
   int tile = tile_of(0);
-  if (tile >= ntiles) return;  // whole workgroup idle (uniform)
+  if (tile >= tend) return;  // whole workgroup idle (uniform)
   auto abase = [&](int t) {
     int tm, tn;
     coords(t, tm, tn);
@@ -396,7 +411,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
 
   for (int r = 0;; ++r) {
     const int next = tile_of(r + 1);
-    const bool has_next = next < ntiles;
+    const bool has_next = next < tend;
     const bf16_t* const Ab = abase(tile);
     const bf16_t* const Bb = bbase(tile);
     const bf16_t* const An = has_next ? abase(next) : Ab;

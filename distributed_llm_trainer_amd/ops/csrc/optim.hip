@@ -162,9 +162,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
   }
 }
 
+template <int HK = 0>
 __global__ __launch_bounds__(256) void k_cast_bf16(const float* __restrict__ x, bf16_t* __restrict__ y, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    y[i] = f2bf(x[i]);
+    y[i] = f2h<HK>(x[i]);
 }
 
 static inline int flat_blocks(int64_t n) {
@@ -230,26 +231,29 @@ DLT_API int dlt_adamw_f16(float* p, const float* g, float* m, float* v, bf16_t* 
 
 // dst[i] += float(src[i]): the FSDP runtime folds a bf16 reduce-scatter output into the
 // fp32 shard gradient in one pass (8 elements per lane, 16 B bf16 + 32 B fp32 loads).
+template <int HK = 0>
 __global__ __launch_bounds__(256) void k_add_bf16_f32(float* __restrict__ dst, const bf16_t* __restrict__ src,
                                                       int64_t n8) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
     const u16x8 s = reinterpret_cast<const u16x8*>(src)[i];
     float4* d = reinterpret_cast<float4*>(dst) + 2 * i;
     float4 a = d[0], b = d[1];
-    a.x += bf2f(s.v[0]); a.y += bf2f(s.v[1]); a.z += bf2f(s.v[2]); a.w += bf2f(s.v[3]);
-    b.x += bf2f(s.v[4]); b.y += bf2f(s.v[5]); b.z += bf2f(s.v[6]); b.w += bf2f(s.v[7]);
+    a.x += h2f<HK>(s.v[0]); a.y += h2f<HK>(s.v[1]); a.z += h2f<HK>(s.v[2]); a.w += h2f<HK>(s.v[3]);
+    b.x += h2f<HK>(s.v[4]); b.y += h2f<HK>(s.v[5]); b.z += h2f<HK>(s.v[6]); b.w += h2f<HK>(s.v[7]);
     d[0] = a;
     d[1] = b;
   }
 }
 
-DLT_API int dlt_add_bf16_f32(float* dst, const bf16_t* src, int64_t n, hipStream_t st) {
+// hk: src format (0 bf16, 1 fp16)
+DLT_API int dlt_add_bf16_f32(float* dst, const bf16_t* src, int64_t n, int hk, hipStream_t st) {
   if (n % 8) return -1;
-  k_add_bf16_f32<<<flat_blocks(n / 2), 256, 0, st>>>(dst, src, n / 8);
+  DLT_HK_DISPATCH(hk, k_add_bf16_f32<HKC><<<flat_blocks(n / 2), 256, 0, st>>>(dst, src, n / 8));
   DLT_CHECK_LAUNCH();
 }
 
-DLT_API int dlt_cast_bf16(const float* x, bf16_t* y, int64_t n, hipStream_t st) {
-  k_cast_bf16<<<flat_blocks(n * 4), 256, 0, st>>>(x, y, n);
+// hk: output format (0 bf16, 1 fp16)
+DLT_API int dlt_cast_bf16(const float* x, bf16_t* y, int64_t n, int hk, hipStream_t st) {
+  DLT_HK_DISPATCH(hk, k_cast_bf16<HKC><<<flat_blocks(n * 4), 256, 0, st>>>(x, y, n));
   DLT_CHECK_LAUNCH();
 }

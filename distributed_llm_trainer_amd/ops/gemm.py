@@ -554,7 +554,7 @@ class HipGemm:
             self._splitk[key] = 1
             return 1
         # timing must not disturb the real accumulator / gradient buffer
-        scratch = torch.zeros(N, K, dtype=torch.bfloat16 if to_bf16 else torch.float32, device=dy.device)
+        scratch = torch.zeros(N, K, dtype=dw2.dtype, device=dy.device)
 
         def t_of(fn):
             fn()
@@ -596,16 +596,16 @@ class HipGemm:
         M, N = dy.shape
         K = x.shape[1]
         dw2 = dw.view(N, K)
-        if dw2.dtype != torch.bfloat16 or not dw2.is_contiguous():
-            raise ValueError("wgrad_set output must be contiguous bf16")
+        if dw2.dtype not in (torch.bfloat16, torch.float16) or dw2.dtype != dy.dtype or not dw2.is_contiguous():
+            raise ValueError("wgrad_set output must be contiguous bf16 / fp16 (the operands' dtype)")
         s = self._resolve(self._pick_splitk(dw2, dy, x, to_bf16=True), dy, x)
         self._run_wgrad(dw2, dy, x, s, True)
 
     def wgrad_acc(self, dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
         """dw (fp32) += dy^T @ x.  A bf16 ``dw`` is refused: overwriting is ``wgrad_set``'s
         contract, and silently switching to it would drop an earlier contribution."""
-        if dw.dtype == torch.bfloat16:
-            raise ValueError("wgrad_acc accumulates into fp32; use wgrad_set for a bf16 gradient")
+        if dw.dtype in (torch.bfloat16, torch.float16):
+            raise ValueError("wgrad_acc accumulates into fp32; use wgrad_set for a 16-bit gradient")
         M, N = dy.shape
         K = x.shape[1]
         dw2 = dw.view(N, K)

@@ -38,7 +38,7 @@ _SIGS = {
     "dlt_embedding_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "dlt_embedding_bwd_chunk": [],
     "dlt_splitk_acc": [c_void_p, c_void_p, ctypes.c_long, c_int, c_void_p],
-    "dlt_splitk_sum_bf16": [c_void_p, c_void_p, ctypes.c_long, c_int, c_void_p],
+    "dlt_splitk_sum_bf16": [c_void_p, c_void_p, ctypes.c_long, c_int, c_int, c_void_p],
     "dlt_rope_qkv_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                          c_int, c_void_p],
     "dlt_rope_qkv_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
@@ -53,8 +53,8 @@ _SIGS = {
                   c_float, c_float, c_float, c_void_p, c_void_p],
     "dlt_adamw_f16": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float, c_float,
                       c_float, c_float, c_float, c_void_p, c_void_p],
-    "dlt_cast_bf16": [c_void_p, c_void_p, c_int64, c_void_p],
-    "dlt_add_bf16_f32": [c_void_p, c_void_p, c_int64, c_void_p],
+    "dlt_cast_bf16": [c_void_p, c_void_p, c_int64, c_int, c_void_p],
+    "dlt_add_bf16_f32": [c_void_p, c_void_p, c_int64, c_int, c_void_p],
     "dlt_gemm_wgrad": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "dlt_gemm_wgrad_sk": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                           c_void_p],
@@ -274,13 +274,13 @@ def splitk_acc(part: torch.Tensor, dw: torch.Tensor) -> None:
 
 
 def splitk_sum_bf16(part: torch.Tensor, out: torch.Tensor) -> None:
-    """out (bf16) = part.sum(0) in fixed order; part [splits, *out.shape] fp32."""
-    _req(out, torch.bfloat16, "splitk_sum_bf16.out")
+    """out (bf16 or fp16) = part.sum(0) in fixed order; part [splits, *out.shape] fp32."""
+    hk = _req_act(out, out.dtype, "splitk_sum_bf16.out")
     _req(part, torch.float32, "splitk_sum_bf16.part")
     n = out.numel()
     if part.numel() % n or n % 4 or out.data_ptr() % 8:
         raise ValueError("splitk_sum_bf16: part must hold whole copies of out, out.numel() % 4 == 0")
-    _chk(lib().dlt_splitk_sum_bf16(_p(part), _p(out), n, part.numel() // n, _stream()), "splitk_sum_bf16")
+    _chk(lib().dlt_splitk_sum_bf16(_p(part), _p(out), n, part.numel() // n, hk, _stream()), "splitk_sum_bf16")
 
 
 # ---------------------------------------------------------------- embedding
@@ -650,18 +650,18 @@ def adamw_flat(param, grad, exp_avg, exp_avg_sq, shadow, lr, beta1, beta2, eps, 
 
 
 def add_bf16_into_f32(dst: torch.Tensor, src: torch.Tensor) -> bool:
-    """dst (fp32) += src (bf16) in one kernel; False (nothing launched) if the shapes or
-    alignment do not fit the 8-wide vector path."""
+    """dst (fp32) += src (bf16 or fp16) in one kernel; False (nothing launched) if the
+    shapes or alignment do not fit the 8-wide vector path."""
     n = dst.numel()
     if (src.numel() != n or n % 8 or not dst.is_contiguous() or not src.is_contiguous()
-            or dst.dtype != torch.float32 or src.dtype != torch.bfloat16 or dst.data_ptr() % 16 or src.data_ptr() % 16):
+            or dst.dtype != torch.float32 or src.dtype not in _HK or dst.data_ptr() % 16 or src.data_ptr() % 16):
         return False
-    _chk(lib().dlt_add_bf16_f32(_p(dst), _p(src), n, _stream()), "add_bf16_f32")
+    _chk(lib().dlt_add_bf16_f32(_p(dst), _p(src), n, _HK[src.dtype], _stream()), "add_bf16_f32")
     return True
 
 
 def cast_bf16(x: torch.Tensor, y: torch.Tensor) -> None:
-    _chk(lib().dlt_cast_bf16(_p(x), _p(y), x.numel(), _stream()), "cast_bf16")
+    _chk(lib().dlt_cast_bf16(_p(x), _p(y), x.numel(), _HK[y.dtype], _stream()), "cast_bf16")
 
 
 # ---------------------------------------------------------------- wgrad GEMM
@@ -738,10 +738,15 @@ def gemm_wgrad_sk(dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, shares: i
 
 
 # ------------------------------------------------- projection GEMMs (csrc/gemm_bf16.hip)
-# launch flags of the hand projection GEMMs; DLT_GEMM_FLAGS=256 = one tile per workgroup
-# instead of the persistent grid; DLT_GEMM_GRID=n caps the persistent grid at n (multiple
-# of 8) workgroups (A/B knobs for overlapped schedules)
-_GB_FLAGS = (int(os.environ.get("DLT_GEMM_FLAGS", "0")) & 256) | \
+# launch flags of the hand projection GEMMs; DLT_GEMM_FLAGS bit 256 = one tile per
+# workgroup instead of the persistent grid; DLT_GEMM_GRID=n caps the persistent grid at n
+# (multiple of 8) workgroups (A/B knobs for overlapped schedules)
+# Production flags (round 4): 1024 = LDS-transposed C stores (whole 192-byte row
+# segments per store instruction: the plain epilogue's cycles -26 %), 12 = XCD row-band
+# tile walk (an XCD keeps its A panels in its L2); tools/cpp/gemm_stamps.cpp and
+# profiles/r4_gemm_forward.md.  DLT_GEMM_FLAGS=n replaces them (bits 256 / 1024 / 12).
+_GB_DEFAULT_FLAGS = 1024 | 12
+_GB_FLAGS = (int(os.environ.get("DLT_GEMM_FLAGS", str(_GB_DEFAULT_FLAGS))) & (256 | 1024 | 12)) | \
     ((min(int(os.environ.get("DLT_GEMM_GRID", "0")), 2040) // 8) << 16)
 
 

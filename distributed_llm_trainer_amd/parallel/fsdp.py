@@ -140,7 +140,10 @@ class FSDPRuntime(ParamProvider):
         # write the bf16 send buffer directly (beta = 0, HipGemm.wgrad_set), the norm
         # weights accumulate in a tiny fp32 side buffer that is cast into it before the
         # reduce-scatter -- no fp32 zero / accumulate / cast passes over the unit.
-        self.bf16_grads = (reduce_dtype == torch.bfloat16 and sync_every_micro_step and self.device.type == "cuda"
+        # (bf16, and fp16 under the fp16 policy: "bf16_grads" = 16-bit gradients in the
+        # reduce dtype, which must equal the compute dtype the GEMM operands use)
+        self.bf16_grads = (reduce_dtype in (torch.bfloat16, torch.float16) and reduce_dtype == compute_dtype
+                           and sync_every_micro_step and self.device.type == "cuda"
                            and os.environ.get("DLT_FSDP_BF16_GRADS", "1") != "0")
         # limit_all_gathers (reference fsdp_trainer.py:296): at most this many prefetched
         # (issued ahead of use, not yet consumed) all-gathers in flight -- one per
@@ -343,7 +346,7 @@ class FSDPRuntime(ParamProvider):
                 out.record_stream(torch.cuda.current_stream(out.device))
             if self.cpu_offload:
                 u.grad.add_(out.cpu())
-            elif not (out.is_cuda and out.dtype == torch.bfloat16 and _add_bf16(u.grad, out)):
+            elif not (out.is_cuda and out.dtype in (torch.bfloat16, torch.float16) and _add_bf16(u.grad, out)):
                 u.grad.add_(out)  # add_ promotes the wire dtype inside the kernel
         u.rs_pending.clear()
 
@@ -378,7 +381,7 @@ class FSDPRuntime(ParamProvider):
         H, I = self.cfg.hidden_size, self.cfg.intermediate_size
         if u.full_grad is None:
             if self.bf16_grads:  # every segment is written (not accumulated) once per micro-step
-                u.full_grad = torch.empty(u.padded, dtype=torch.bfloat16, device=self.device)
+                u.full_grad = torch.empty(u.padded, dtype=self.reduce_dtype, device=self.device)
                 if u.padded > u.numel:
                     u.full_grad[u.numel:].zero_()
                 u.norm_grad = torch.zeros(2 * H, dtype=torch.float32, device=self.device)
@@ -386,7 +389,7 @@ class FSDPRuntime(ParamProvider):
                 u.full_grad = torch.zeros(u.padded, dtype=torch.float32, device=self.device)
         p = f"layers.{i}."
         g = u.full_grad
-        if g.dtype == torch.bfloat16:
+        if g.dtype in (torch.bfloat16, torch.float16):
             ln1, ln2 = u.norm_grad[:H], u.norm_grad[H:]
         else:
             ln1 = self._view(u, g, p + "input_layernorm.weight")
@@ -451,7 +454,7 @@ class FSDPRuntime(ParamProvider):
 
     def post_backward(self, uid):
         u = self.units[uid]
-        if u.full_grad is not None and u.full_grad.dtype == torch.bfloat16 and uid != "head":
+        if u.full_grad is not None and u.full_grad.dtype in (torch.bfloat16, torch.float16) and uid != "head":
             # the norm-weight gradients (fp32 side buffer) into the bf16 send buffer
             H = self.cfg.hidden_size
             p = f"layers.{uid}."

@@ -169,10 +169,17 @@ class DistributedTrainer:
         total = torch.zeros((), dtype=torch.float32, device=self.device)
         # micro-step pipelining (engine.train_window): from the second step on, so the
         # first one runs the GEMM autotuning on a quiet GPU
-        pipelined = (self.use_engine and chains > 1 and cfg.pipeline_micro_steps
-                     and self.loss_scale is None and self._engine_warm
+        window_ok = (self.use_engine and chains > 1 and cfg.pipeline_micro_steps
+                     and self.loss_scale is None
                      and (self.device.type != "cuda" or getattr(self.model.engine.gemm, "stream_safe", False))
                      and os.environ.get("DLT_PIPELINE", "1") != "0")
+        pipelined = window_ok and self._engine_warm
+        # first step: the GEMM races time on a quiet GPU, so no stream pipelining -- but
+        # when the window would run ffbb, its single-stream form (same block order, same
+        # dY slot ring) keeps the first step's memory at the steady state's
+        serial = (window_ok and not self._engine_warm and self.device.type == "cuda"
+                  and self.model.engine.window_schedule(chains, cfg.defer_wgrad)[1] == "ffbb")
+        pipelined = pipelined or serial
         if pipelined:
             ids_l = [input_ids[m * chain_bs:(m + 1) * chain_bs] for m in range(chains)]
             from ..models.engine import shift_targets
@@ -187,7 +194,7 @@ class DistributedTrainer:
                 ids_l, tg_l, dloss, recompute=bool(self.model.gradient_checkpointing),
                 before_last=(lambda: self.ddp.require_sync(True)) if self.ddp is not None else None,
                 sync_hook=self.ddp.require_sync if self.ddp is not None else None,
-                defer=cfg.defer_wgrad)
+                defer=cfg.defer_wgrad, serial=serial)
             range_pop()
             for loss in losses:
                 total += (loss / chains).detach().float()

@@ -191,8 +191,9 @@ def test_pipelined_window_matches_sequential_gpu(recompute):
         assert torch.equal(g1[n], g2[n]), (n, (g1[n] - g2[n]).abs().max().item())
 
 
-@pytest.mark.parametrize("recompute,ring", [(False, "0"), (True, "0"), (False, "2"), (True, "2")])
-def test_window_ffbb_matches_sequential_gpu(recompute, ring, monkeypatch):
+@pytest.mark.parametrize("recompute,ring,serial", [(False, "0", False), (True, "0", False), (False, "2", False),
+                                                   (True, "2", False), (False, "2", True)])
+def test_window_ffbb_matches_sequential_gpu(recompute, ring, serial, monkeypatch):
     """Two-chain window F0 || F1 | B0 || B1 (DLT_WINDOW_SCHED=ffbb: both forwards, then both
     backwards concurrently, B1 one block behind B0 with per-buffer waits) == the sequential
     schedule: same losses, bit-identical gradients -- with one dY slot per layer (ring 0)
@@ -217,7 +218,8 @@ def test_window_ffbb_matches_sequential_gpu(recompute, ring, monkeypatch):
         seq.append(loss.item())
     flags = []
     win = e2.train_window([data[j] for j in range(GA)], [shift_targets(data[j]) for j in range(GA)],
-                          torch.full((), 1.0 / GA, device=DEV), recompute=recompute, sync_hook=flags.append)
+                          torch.full((), 1.0 / GA, device=DEV), recompute=recompute, sync_hook=flags.append,
+                          serial=serial)
     torch.cuda.synchronize()
     assert flags and flags[0] is False and flags[-1] is True
     for a, b in zip(seq, win):
@@ -686,7 +688,7 @@ def test_precision_modes_match_fp32_reference(mp):
             tr = FSDPTrainer(cfg, FSDPTrainingConfig(batch_size=2, gradient_accumulation_steps=4, warmup_steps=1,
                                                      learning_rate=3e-3),
                              FSDPConfig(mixed_precision=mp, activation_checkpointing=False))
-        ref_loss = _fp32_reference_loss(cfg, data, 15)
+        ref_loss = _fp32_reference_loss(cfg, data, tr.training_config.seed)
         losses = [tr.train_step({"input_ids": data})["loss"] for _ in range(6)]
         assert all(math.isfinite(x) for x in losses), (kind, losses)
         assert abs(losses[0] - ref_loss) < tol * ref_loss, (kind, mp, losses[0], ref_loss)

@@ -668,7 +668,8 @@ int main(int argc, char** argv) {
                              {"nt", run_bf16<128>},      {"ntrow", run_bf16<132>},   {"np", run_bf16<256>},
                              {"nprow", run_bf16<260>},   {"d4", run_bf16<512 | (4 << 24)>},
                              {"d8", run_bf16<512 | (8 << 24)>}, {"d13", run_bf16<512 | (13 << 24)>},
-                             {"d20", run_bf16<512 | (20 << 24)>}, {"lt", run_bf16<1024>}};
+                             {"d20", run_bf16<512 | (20 << 24)>}, {"lt", run_bf16<1024>}, {"xb", run_bf16<12>},
+                             {"xblt", run_bf16<1036>}};
   std::string only = (argc > 1 && strcmp(argv[1], "all")) ? std::string(",") + argv[1] + "," : "all";
   std::vector<int> shp;
   for (int i = 2; i < argc; ++i) shp.push_back(atoi(argv[i]));
