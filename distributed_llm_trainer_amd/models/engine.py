@@ -624,6 +624,13 @@ class GPTEngine:
             nf_scaled = st.nf * (dloss * inv_ce)
             if nf_out is not None:
                 nf_scaled = nf_out.copy_(nf_scaled)
+        if nf_out is not None:
+            # the window's lm_head weight gradient (the last backward, side stream) reads
+            # every micro-step's nf slot: "nf" marks this one written, chained through the
+            # previous backwards' marks (they run on other streams, a backward apart)
+            if prev is not None and "nf" in prev:
+                torch.cuda.current_stream().wait_event(prev["nf"])
+            mark("nf")
         head_ev = None
         head_add = None  # the window's lm_head weight gradient, added after the scatter-adds
         head_late = None  # overlapped backwards: the per-micro-step head wgrad waits for "embed"
@@ -647,7 +654,7 @@ class GPTEngine:
                 gm.wgrad_acc(head_add, lg_all, nf_all)
             if side is not None:
                 ev = torch.cuda.Event()
-                ev.record()
+                ev.record()  # after this backward's nf mark, which follows every earlier one
                 side.wait_event(ev)
                 for e in ready or ():
                     side.wait_event(e)

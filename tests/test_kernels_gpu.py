@@ -821,3 +821,30 @@ def test_fp16_norm_swiglu_ce_scale_vs_fp32():
     sc = torch.full((), 0.25, device=DEV)
     z = hip.scale_bf16(d, sc, mul=2.0)
     assert z.dtype == torch.float16 and torch.equal(z, (d.float() * 0.5).half())
+
+
+@pytest.mark.parametrize("cap", [8, 64, 192])
+def test_gemm_persistent_multi_tile_matches(cap):
+    """The persistent hand GEMMs with a capped grid (the ffbb window runs them on 192
+    workgroups): every workgroup walks several tiles and prefetches the next tile's
+    K-tiles, so the forward (K-major B) and the data-gradient (reduction-major B) forms
+    must give bit-identical outputs to the one-tile-per-workgroup launches, and match
+    the fp32 product."""
+    torch.manual_seed(cap)
+    M = 4096
+    x = (torch.rand(M, 768, device=DEV) * 2 - 1).bfloat16()
+    w = ((torch.rand(2304, 768, device=DEV) * 2 - 1) / 768 ** 0.5).bfloat16()
+    dy = (torch.rand(M, 2304, device=DEV) * 2 - 1).bfloat16()
+    prev = hip.gemm_grid_cap(0)
+    try:
+        y_full = hip.gemm_bf16(x, w)
+        dx_full = hip.gemm_dgrad(dy, w)
+        hip.gemm_grid_cap(cap)
+        y_cap = hip.gemm_bf16(x, w)
+        dx_cap = hip.gemm_dgrad(dy, w)
+    finally:
+        hip.gemm_grid_cap(prev)
+    torch.cuda.synchronize()
+    assert _relerr(dx_full, dy.float() @ w.float()) < 8e-3
+    assert torch.equal(y_cap, y_full), (y_cap.float() - y_full.float()).abs().max().item()
+    assert torch.equal(dx_cap, dx_full), (dx_cap.float() - dx_full.float()).abs().max().item()

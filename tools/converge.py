@@ -22,13 +22,14 @@ def main():
     ap.add_argument("--lr", type=float, default=6e-4)
     ap.add_argument("--eager", action="store_true", help="reference-style eager autocast model instead of the engine")
     ap.add_argument("--log", type=int, default=10)
+    ap.add_argument("--seed", type=int, default=1234, help="trainer seed (model init + dropout streams)")
     a = ap.parse_args()
     from distributed_llm_trainer_amd.models.config import GPTConfig
     from distributed_llm_trainer_amd.training.configs import TrainingConfig
     from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
     cfg = GPTConfig.gpt2_small()
     tc = TrainingConfig(batch_size=8, gradient_accumulation_steps=4, max_steps=a.steps, warmup_steps=20,
-                        learning_rate=a.lr, mixed_precision="bf16")
+                        learning_rate=a.lr, mixed_precision="bf16", seed=a.seed)
     tr = DistributedTrainer(cfg, tc, use_engine=not a.eager)
     if a.eager:  # the reference path: torch modules under bf16 autocast
         tr.autocast_ctx = torch.autocast(device_type="cuda", dtype=torch.bfloat16)
@@ -42,7 +43,7 @@ def main():
         if step % a.log == 0 or step == a.steps - 1:
             out.append({"step": step, "loss": float(loss)})
             print(json.dumps(out[-1]), flush=True)
-    print(json.dumps({"path": "eager" if a.eager else "engine", "seconds": round(time.time() - t0, 1),
+    print(json.dumps({"path": "eager" if a.eager else "engine", "seed": a.seed, "seconds": round(time.time() - t0, 1),
                       "first": out[0]["loss"], "last": out[-1]["loss"]}), flush=True)
 
 
