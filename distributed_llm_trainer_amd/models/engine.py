@@ -618,6 +618,10 @@ class GPTEngine:
         dnf = gm.linear_dgrad(st.dlogits, hw.lm_head)
         nf_out = self._sb(st, "head", "nf", M, H, dev)
         inv_ce = 1.0 / st.ce_scale  # the pre-scaled CE gradient (fp16), see ce_grad_scale
+        if prev is None and mine is not None and _TEST_DELAY_FIRST_BWD:
+            # race test hook (DLT_TEST_DELAY_FIRST_BWD=cycles): the first overlapped backward
+            # writes its nf slot late, so a reader that does not wait for it sees stale data
+            torch.cuda._sleep(_TEST_DELAY_FIRST_BWD)
         if st.nf.dtype in (torch.bfloat16, torch.float16):
             nf_scaled = ops.scale_bf16(st.nf, dloss, out=nf_out, mul=inv_ce)
         else:
@@ -1046,6 +1050,9 @@ class GPTEngine:
         if overlap:  # the optimizer (current stream) must see every backward's gradients
             main.wait_stream(pipe)
         return losses
+
+
+_TEST_DELAY_FIRST_BWD = int(os.environ.get("DLT_TEST_DELAY_FIRST_BWD", "0"))
 
 
 def _wgrad(gm, dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:

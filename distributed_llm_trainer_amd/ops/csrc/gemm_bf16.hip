@@ -574,12 +574,14 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
           *reinterpret_cast<uint2*>(srow + 32 + lq * 4) = sp[2];
         }
         bf16_t* crow = C + (size_t)row * ldc + n0;
-        if (EPI == GB_EPI_STORE && !BT && (flags & 1024)) {
+        if (EPI != GB_EPI_SWIGLU_BWD && !BT && (flags & 1024)) {
           // LDS-transposed stores: the lane's three 16-byte chunks (8 consecutive columns
           // each) go to the wave's staging block, then every store instruction writes
-          // 5.33 whole 192-byte row segments (12 lanes per row, consecutive lanes on
-          // consecutive 16 bytes) instead of 16 rows x 64 bytes.  Wave-local: the wave
-          // reads back only what it wrote (LDS operations of one wave stay in order).
+          // 5.33 whole row segments (12 lanes per row, consecutive lanes on consecutive
+          // 16 bytes) instead of 16 rows x 64 bytes.  Staging column chunk c holds columns
+          // gb_ncol(wn, c / 2) + (c % 2) * 8: one 192-byte run per row for STORE, the gate
+          // and up 96-byte runs for SWIGLU, the head-pair map for ROPE.  Wave-local: the
+          // wave reads back only what it wrote (LDS operations of one wave stay in order).
           bf16_t* stg = lds + 2 * Cf::BUF + wid * (16 * GB_STG_ROW);
 #pragma unroll
           for (int p = 0; p < NT / 2; ++p) {
@@ -593,12 +595,20 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
             const int chunk = 4 * p + 2 * (lq & 1) + (lq >> 1);
             *reinterpret_cast<gb_u32x4_t*>(stg + l16 * GB_STG_ROW + chunk * 8) = gb_u32x4_t{x[0], x[1], y[0], y[1]};
           }
-          bf16_t* cblk = C + (size_t)(m0 + wm * 64 + mt * 16) * ldc + n0 + wn * 96;
+          bf16_t* cblk = C + (size_t)(m0 + wm * 64 + mt * 16) * ldc + n0;
+          // write-through (sc1, flags & 2048) stores: the C lines leave the XCD's L2
+          // instead of displacing the operand panels the next K-iterations read
+          // (profiles/r4_gemm_forward.md section 5)
+          const auto rs = __builtin_amdgcn_make_buffer_rsrc(cblk, 0, 16 * ldc * 2, 0x00020000);
 #pragma unroll
           for (int i = 0; i < 3; ++i) {
             const int e = i * 64 + lane, r = e / 12, c = e - r * 12;
+            const int col = gb_ncol<BN, EPI>(wn, c >> 1, ep.I) + (c & 1) * 8;
             const gb_u32x4_t v = *reinterpret_cast<const gb_u32x4_t*>(stg + r * GB_STG_ROW + c * 8);
-            *reinterpret_cast<gb_u32x4_t*>(cblk + (size_t)r * ldc + c * 8) = v;
+            if (flags & 2048)
+              __builtin_amdgcn_raw_buffer_store_b128(v, rs, (r * ldc + col) * 2, 0, 16);
+            else
+              *reinterpret_cast<gb_u32x4_t*>(cblk + (size_t)r * ldc + col) = v;
           }
           continue;
         }

@@ -743,10 +743,12 @@ def gemm_wgrad_sk(dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, shares: i
 # (multiple of 8) workgroups (A/B knobs for overlapped schedules)
 # Production flags (round 4): 1024 = LDS-transposed C stores (whole 192-byte row
 # segments per store instruction: the plain epilogue's cycles -26 %), 12 = XCD row-band
-# tile walk (an XCD keeps its A panels in its L2); tools/cpp/gemm_stamps.cpp and
-# profiles/r4_gemm_forward.md.  DLT_GEMM_FLAGS=n replaces them (bits 256 / 1024 / 12).
-_GB_DEFAULT_FLAGS = 1024 | 12
-_GB_FLAGS = (int(os.environ.get("DLT_GEMM_FLAGS", str(_GB_DEFAULT_FLAGS))) & (256 | 1024 | 12)) | \
+# tile walk (an XCD keeps its A panels in its L2), 2048 = write-through (sc1) C stores
+# (the C lines leave the XCD's L2 instead of evicting the operand panels: lm_head forward
+# later K-iterations 6461 -> 4909 cycles); tools/cpp/gemm_stamps.cpp and
+# profiles/r4_gemm_forward.md.  DLT_GEMM_FLAGS=n replaces them (bits 256 / 1024 / 2048 / 12).
+_GB_DEFAULT_FLAGS = 2048 | 1024 | 12
+_GB_FLAGS = (int(os.environ.get("DLT_GEMM_FLAGS", str(_GB_DEFAULT_FLAGS))) & (256 | 1024 | 2048 | 12)) | \
     ((min(int(os.environ.get("DLT_GEMM_GRID", "0")), 2040) // 8) << 16)
 
 

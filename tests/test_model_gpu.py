@@ -731,15 +731,19 @@ def test_engine_gpt2_small_grads_vs_fp32_eager(act):
     assert worst[0] < bound, worst
 
 
-@pytest.mark.parametrize("dgrad", ["1", "0"])
-def test_window_ffbb_hand_kernels_match_sequential_gpu(dgrad, monkeypatch):
+@pytest.mark.parametrize("dgrad,delay", [("1", 0), ("0", 0), ("1", 20_000_000)])
+def test_window_ffbb_hand_kernels_match_sequential_gpu(dgrad, delay, monkeypatch):
     """The ffbb window at shapes every hand-written kernel tiles (hidden 384, 3H 1152,
     2I 3072, vocab 1152, 1024-token chains): the hand forward / data-gradient / weight-
     gradient GEMMs on two concurrent chains (grid capped at 192 workgroups) must give
-    the sequential schedule's gradients bit for bit."""
+    the sequential schedule's gradients bit for bit.  delay: the first backward is held
+    back by a spin kernel before it writes its lm_head-gradient (nf) slot -- the race of
+    round 3 (the window's head weight gradient did not wait for that write)."""
+    from distributed_llm_trainer_amd.models import engine as engine_mod
     from distributed_llm_trainer_amd.models.engine import shift_targets
     monkeypatch.setenv("DLT_WINDOW_SCHED", "ffbb")
     monkeypatch.setenv("DLT_GEMM_DGRAD", dgrad)
+    monkeypatch.setattr(engine_mod, "_TEST_DELAY_FIRST_BWD", delay)
     cfg = GPTConfig(vocab_size=1152, hidden_size=384, num_layers=4, num_heads=6, intermediate_size=1536,
                     max_seq_len=256, dropout=0.1, attention_dropout=0.1)
     torch.manual_seed(16)

@@ -190,9 +190,12 @@ static int epi_main(int M, int H, int I, int S) {
     std::vector<float> ref((size_t)nr * N);
     CK(hipMemcpyAsync(ref.data(), R, ref.size() * 4, hipMemcpyDeviceToHost, st));
     CK(hipStreamSynchronize(st));
+    // EPI_FLAGS=n: k_gemm_bf16 flags of the fused and plain launches (1036 = LDS-transposed
+    // stores + row bands, 3084 = the same with write-through stores)
+    const int ef = getenv("EPI_FLAGS") ? atoi(getenv("EPI_FLAGS")) : 0;
     auto fused = [&]() {
-      if (which == 0) return dlt_gemm_bf16_qkv_rope(A, B, C, M, H, K, S, dc, ds, 0, st);
-      return dlt_gemm_bf16_gu_swiglu(A, B, C, Sb, M, I, K, 0, st);
+      if (which == 0) return dlt_gemm_bf16_qkv_rope(A, B, C, M, H, K, S, dc, ds, ef, st);
+      return dlt_gemm_bf16_gu_swiglu(A, B, C, Sb, M, I, K, ef, st);
     };
     auto unfused = [&]() {
       int rc = run_blas(A, B, C2, M, N, K, st);
@@ -246,8 +249,8 @@ static int epi_main(int M, int H, int I, int S) {
       }
     }
     const float tf = time_us(fused, st), tu = time_us(unfused, st);
-    const float tp = time_us([&]() { return dlt_gemm_bf16_tn(A, B, C, M, N, K, K, K, N, 0, st); }, st);
-    printf("  plain bf16 %.1f us\n", tp);
+    const float tp = time_us([&]() { return dlt_gemm_bf16_tn(A, B, C, M, N, K, K, K, N, ef, st); }, st);
+    printf("  plain bf16 %.1f us (flags %d)\n", tp, ef);
     printf("%s M=%d N=%d K=%d: fused %.1f us | hipBLASLt + %s %.1f us | err %.1e%s%.1e\n",
            which == 0 ? "qkv+rope" : "gu+swiglu", M, N, K, tf, which == 0 ? "rope" : "swiglu", tu, e1 / m1,
            which == 1 ? " s err " : "", which == 1 ? e2 / m2 : 0.0);
@@ -669,7 +672,8 @@ int main(int argc, char** argv) {
                              {"nprow", run_bf16<260>},   {"d4", run_bf16<512 | (4 << 24)>},
                              {"d8", run_bf16<512 | (8 << 24)>}, {"d13", run_bf16<512 | (13 << 24)>},
                              {"d20", run_bf16<512 | (20 << 24)>}, {"lt", run_bf16<1024>}, {"xb", run_bf16<12>},
-                             {"xblt", run_bf16<1036>}};
+                             {"xblt", run_bf16<1036>}, {"sc1", run_bf16<3072>},
+                             {"xbsc1", run_bf16<3084>}};
   std::string only = (argc > 1 && strcmp(argv[1], "all")) ? std::string(",") + argv[1] + "," : "all";
   std::vector<int> shp;
   for (int i = 2; i < argc; ++i) shp.push_back(atoi(argv[i]));
