@@ -53,6 +53,9 @@ constexpr int GB_BK = 64;
 // land on disjoint banks)
 constexpr int GB_STG_ROW = 104;
 constexpr int GB_STG = 8 * 16 * GB_STG_ROW;
+// SWIGLU: s is staged in its own per-wave 16 x 48 block (rows padded to 56 elements)
+constexpr int GB_SSTG_ROW = 56;
+constexpr int GB_SSTG = 8 * 16 * GB_SSTG_ROW;
 
 __device__ __forceinline__ int gb_swz(int row, int chunk) { return row * GB_BK + ((chunk ^ ((row >> 1) & 7)) << 3); }
 
@@ -168,7 +171,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
   using Cf = GbCfg<BN>;
   constexpr int TS = EPI == GB_EPI_SWIGLU ? 96 : BN;  // tile stride in B rows
   constexpr int NT = Cf::NT, NH = Cf::NH;
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * Cf::BUF + GB_STG];
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * Cf::BUF + GB_STG + (EPI == GB_EPI_SWIGLU ? GB_SSTG : 0)];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int half = wid >> 2;                  // stagger group (waves w and w+4 share a SIMD)
@@ -548,10 +551,14 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
         uint2 pk[NT];
 #pragma unroll
         for (int t = 0; t < NT; ++t) pk[t] = gb_pack(acc[t][mt]);
+        // staged (LDS-transposed) stores: flag 1024; always for SWIGLU (its two stores
+        // per lane otherwise write 16 rows x 32 + 8 bytes each)
+        const bool lt = EPI == GB_EPI_SWIGLU || (EPI != GB_EPI_SWIGLU_BWD && !BT && (flags & 1024));
         if constexpr (EPI == GB_EPI_SWIGLU) {
-          // s = silu(g) * u on the bf16-rounded gate/up values (the packs stored as gu);
-          // n-tiles 0/1 of s are paired for 16-byte stores, n-tile 2 stores 8 bytes per lane
           uint2 sp[3];
+          // s = silu(g) * u on the bf16-rounded gate/up values (the packs stored as gu);
+          // without the staged stores n-tiles 0/1 of s are paired for 16-byte stores and
+          // n-tile 2 stores 8 bytes per lane
 #pragma unroll
           for (int t = 0; t < 3; ++t) {
             float g[4], u[4];
@@ -562,19 +569,26 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
             for (int e = 0; e < 4; ++e) sv[e] = g[e] * dlt_sigmoid(g[e]) * u[e];
             sp[t] = gb_pack(sv);
           }
-          bf16_t* srow = ep.s_out + (size_t)row * ep.ld_s + (size_t)tn * 96 + wn * 48;
-          uint32_t x[2] = {sp[0].x, sp[0].y}, y[2] = {sp[1].x, sp[1].y};
+          if (lt) {
+            bf16_t* sstg = lds + 2 * Cf::BUF + GB_STG + wid * (16 * GB_SSTG_ROW);
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            auto sw = __builtin_amdgcn_permlane16_swap(x[h], y[h], false, false);
-            x[h] = sw[0];
-            y[h] = sw[1];
+            for (int t = 0; t < 3; ++t)
+              *reinterpret_cast<uint2*>(sstg + l16 * GB_SSTG_ROW + t * 16 + lq * 4) = sp[t];
+          } else {
+            bf16_t* srow = ep.s_out + (size_t)row * ep.ld_s + (size_t)tn * 96 + wn * 48;
+            uint32_t x[2] = {sp[0].x, sp[0].y}, y[2] = {sp[1].x, sp[1].y};
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              auto sw = __builtin_amdgcn_permlane16_swap(x[h], y[h], false, false);
+              x[h] = sw[0];
+              y[h] = sw[1];
+            }
+            *reinterpret_cast<uint4*>(srow + (lq & 1) * 16 + (lq >> 1) * 8) = uint4{x[0], x[1], y[0], y[1]};
+            *reinterpret_cast<uint2*>(srow + 32 + lq * 4) = sp[2];
           }
-          *reinterpret_cast<uint4*>(srow + (lq & 1) * 16 + (lq >> 1) * 8) = uint4{x[0], x[1], y[0], y[1]};
-          *reinterpret_cast<uint2*>(srow + 32 + lq * 4) = sp[2];
         }
         bf16_t* crow = C + (size_t)row * ldc + n0;
-        if (EPI != GB_EPI_SWIGLU_BWD && !BT && (flags & 1024)) {
+        if (lt) {
           // LDS-transposed stores: the lane's three 16-byte chunks (8 consecutive columns
           // each) go to the wave's staging block, then every store instruction writes
           // 5.33 whole row segments (12 lanes per row, consecutive lanes on consecutive
@@ -609,6 +623,23 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
               __builtin_amdgcn_raw_buffer_store_b128(v, rs, (r * ldc + col) * 2, 0, 16);
             else
               *reinterpret_cast<gb_u32x4_t*>(cblk + (size_t)r * ldc + col) = v;
+          }
+          if constexpr (EPI == GB_EPI_SWIGLU) {
+            // s [16 rows x 48 columns] from its staging block: 96-byte row runs
+            const bf16_t* sstg = lds + 2 * Cf::BUF + GB_STG + wid * (16 * GB_SSTG_ROW);
+            bf16_t* sblk = ep.s_out + (size_t)(m0 + wm * 64 + mt * 16) * ep.ld_s + (size_t)tn * 96 + wn * 48;
+            const auto rss = __builtin_amdgcn_make_buffer_rsrc(sblk, 0, 16 * ep.ld_s * 2, 0x00020000);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+              const int e = i * 64 + lane, r = e / 6, c = e - r * 6;
+              if (i == 0 || lane < 32) {
+                const gb_u32x4_t v = *reinterpret_cast<const gb_u32x4_t*>(sstg + r * GB_SSTG_ROW + c * 8);
+                if (flags & 2048)
+                  __builtin_amdgcn_raw_buffer_store_b128(v, rss, (r * ep.ld_s + c * 8) * 2, 0, 16);
+                else
+                  *reinterpret_cast<gb_u32x4_t*>(sblk + (size_t)r * ep.ld_s + c * 8) = v;
+              }
+            }
           }
           continue;
         }

@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "gemm_bf16.hip"
@@ -53,7 +54,17 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&C, (size_t)M * N * 2));
   k_fill<<<1024, 256, 0, st>>>(A, (size_t)M * K, 1);
   k_fill<<<1024, 256, 0, st>>>(B, (size_t)N * K, 2);
-  const int ntiles = (M / 256) * (N / 192);
+  // EPI=rope (N = 3H, RoPE epilogue, S = 1024) | swiglu (N = 2I, SwiGLU epilogue) | plain
+  const char* epi = getenv("EPI") ? getenv("EPI") : "plain";
+  const int mode = !strcmp(epi, "rope") ? 1 : !strcmp(epi, "swiglu") ? 2 : 0;
+  float* tab = nullptr;
+  bf16_t* Sb = nullptr;
+  if (mode == 1) {
+    CK(hipMalloc(&tab, 1024 * 32 * 4));
+    CK(hipMemset(tab, 0, 1024 * 32 * 4));
+  }
+  if (mode == 2) CK(hipMalloc(&Sb, (size_t)M * (N / 2) * 2));
+  const int ntiles = (M / 256) * (mode == 2 ? N / 192 : N / 192);
   const int G = gb_grid(ntiles);
   unsigned long long* buf;
   CK(hipMalloc(&buf, (size_t)G * 8 * 8 * 8));
@@ -61,7 +72,7 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  printf("M=%d N=%d K=%d tiles=%d grid=%d\n", M, N, K, ntiles, G);
+  printf("M=%d N=%d K=%d tiles=%d grid=%d epilogue %s\n", M, N, K, ntiles, G, epi);
   for (int a = 4; a < argc; ++a) {
     const int flags = atoi(argv[a]);
     // warm: ~1.5 s of launches
@@ -69,7 +80,14 @@ int main(int argc, char** argv) {
     int iters = 0;
     CK(hipEventRecord(e0, st));
     while (ms < 1500.f) {
-      for (int i = 0; i < 50; ++i) dlt_gemm_bf16_tn(A, B, C, M, N, K, K, K, N, flags, st);
+      for (int i = 0; i < 50; ++i) {
+        if (mode == 1)
+          dlt_gemm_bf16_qkv_rope(A, B, C, M, N / 3, K, 1024, tab, tab, flags, st);
+        else if (mode == 2)
+          dlt_gemm_bf16_gu_swiglu(A, B, C, Sb, M, N / 2, K, flags, st);
+        else
+          dlt_gemm_bf16_tn(A, B, C, M, N, K, K, K, N, flags, st);
+      }
       iters += 50;
       CK(hipEventRecord(e1, st));
       CK(hipEventSynchronize(e1));
