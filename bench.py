@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--mode", default="ddp", choices=["ddp", "fsdp"])
     ap.add_argument("--sharding", default="FULL_SHARD")
     ap.add_argument("--no_ac", action="store_true", help="FSDP: disable activation checkpointing")
+    ap.add_argument("--cpu_offload", action="store_true",
+                    help="FSDP: fp32 master shards + AdamW on the host (pinned), reduced grads staged D2H")
     ap.add_argument("--model_override", default="",
                     help="rehearsal only: comma-separated GPTConfig overrides (e.g. hidden_size=64,num_layers=2); "
                          "the JSON line then names a custom model and vs_baseline is null")
@@ -92,7 +94,8 @@ def main():
         from distributed_llm_trainer_amd.training.fsdp_trainer import FSDPTrainer
         tc = FSDPTrainingConfig(batch_size=args.batch_size, gradient_accumulation_steps=args.grad_accum,
                                 max_steps=100000, micro_step_fusion=args.fusion)
-        fc = FSDPConfig(sharding_strategy=args.sharding, activation_checkpointing=not args.no_ac)
+        fc = FSDPConfig(sharding_strategy=args.sharding, activation_checkpointing=not args.no_ac,
+                        cpu_offload=args.cpu_offload)
         trainer = FSDPTrainer(cfg, tc, fc)
     dev = trainer.device
     world = trainer.world_size
@@ -158,7 +161,8 @@ def main():
                        "parallelism": f"{args.mode}{world}", "micro_batch": args.batch_size,
                        "grad_accum": args.grad_accum,
                        "micro_step_fusion": trainer.fusion_factor(args.grad_accum, args.batch_size, args.seq_len),
-                       **({"memory_lean": True} if args.memory_lean else {})},
+                       **({"memory_lean": True} if args.memory_lean else {}),
+                       **({"cpu_offload": True} if args.cpu_offload else {})},
             "peak_gb_per_gpu": round(peak, 3), "final_loss": round(loss, 4),
             "vs_baseline_linear": None if overrides else round(tps / (12500.0 * world), 3),
         }

@@ -164,6 +164,10 @@ class _StepState:
     nf: Any = None
     dlogits: Any = None
     ce_scale: float = 1.0
+    head_key: int = 0   # which per-stream lm_head buffers (chunk logits, fp32 wgrad) it uses
+    head_rows: Any = None  # the lm_head row chunks [(r0, r1), ...] (chunked head)
+    dnf: Any = None     # early head: d(final norm output), computed in the forward
+    head_acc: Any = None  # chunked head: this micro-step's fp32 lm_head weight gradient
     d_last: Any = None  # bf16 d of last layer (input of final norm)
 
 
@@ -195,6 +199,32 @@ class GPTEngine:
         # dY-operand slot ring (ffbb window, see _window_ffbb): 0 = one slot per layer
         self._ring = 0
         self._ring_done = {}
+        # with the dY ring on, the SwiGLU output s (the down projection's weight-gradient
+        # operand) joins it too: the backward's swiglu_bwd rewrites it (same bits) and the
+        # forward's copy is a temporary -- R slots instead of one [2M, I] slot per layer
+        # (-1.8 GB at the headline shape).  DLT_S_RING=0: per-layer s slots from the forward.
+        self.s_ring = os.environ.get("DLT_S_RING", "1") != "0"
+        # lm_head + cross-entropy in row chunks (head_chunks > 0; 0 = the window's logits
+        # stay resident for ONE lm_head weight-gradient GEMM over all its rows, on the
+        # side stream during the backward).  Per micro-step, for each chunk of rows:
+        # logits GEMM, CE (gradient in place), the lm_head data gradient and the weight
+        # gradient into a private fp32 buffer, added to the tied embedding gradient after
+        # the micro-step's embedding scatter-add.  In train_window (dloss known up front)
+        # the forward runs all of it ("early head") through ONE [M / chunks, V] logits
+        # buffer instead of a [GA * M, V] window slot: headline peak 21.4 -> 19.0 GB, but
+        # -3.5 % tok/s (the lm_head weight gradient no longer overlaps the backward;
+        # profiles/r4_memory.md), so it is the memory-lean modes' choice (the DDP trainer
+        # sets 2 with --memory_lean).  DLT_HEAD_CHUNKS=n overrides.
+        env_chunks = os.environ.get("DLT_HEAD_CHUNKS")
+        self.head_chunks_env = env_chunks is not None
+        self.head_chunks = max(0, int(env_chunks)) if env_chunks is not None else 0
+        # ... and the micro-steps of a window share ONE chunk logits buffer (DLT_HEAD_SHARE,
+        # default on): a micro-step's early head waits for the previous one's (a device-side
+        # event wait; the other chain's layers keep the GPU busy meanwhile)
+        self.head_share = os.environ.get("DLT_HEAD_SHARE", "1") != "0"
+        self._head_lg = {}   # head_key (0 when shared) -> chunk logits buffer
+        self._head_lg_ev = None  # shared buffer: the last early head's completion event
+        self._head_accs = {}  # head_key -> fp32 [V, H] weight-gradient buffer
         self._side = None  # weight-gradient side stream (lazily created)
         self._mask_side = None  # attention keep-bit side stream
         self._pipe = None  # second compute stream of train_window
@@ -263,6 +293,8 @@ class GPTEngine:
     ROLES = ("qkv", "o", "gu", "down", "head")
 
     def _deferred(self, st, role: str) -> bool:
+        if role == "head" and self.head_chunks > 0:
+            return False  # the chunked head computes its weight gradient per micro-step
         return st.defer and role in self.defer_roles
 
     def _sb(self, st, layer, name: str, M: int, N: int, device):
@@ -275,9 +307,17 @@ class GPTEngine:
     # slot buffers written by the backward (the dY operands of the deferred weight gradients)
     _DY_SLOTS = frozenset(("dqkv", "da", "dgu", "dd"))
 
+    def _ring_name(self, name: str) -> bool:
+        return name in self._DY_SLOTS or (name == "s" and self.s_ring)
+
+    def _s_in_ring(self, st) -> bool:
+        """The SwiGLU output lives in the slot ring (written by the backward), not in a
+        per-layer slot from the forward."""
+        return bool(self._ring) and self.s_ring and self._deferred(st, "down")
+
     def _slot_buf(self, st, layer, name: str, M: int, N: int, device):
         # ffbb ring: the dY operands of layer i live in ring slot i % R (see _window_ffbb)
-        key = (("ring", layer % self._ring), name) if self._ring and name in self._DY_SLOTS else (layer, name)
+        key = (("ring", layer % self._ring), name) if self._ring and self._ring_name(name) else (layer, name)
         buf = self._slots.get(key)
         if buf is None or buf.shape != (self.acc_slots * M, N) or buf.device != device:
             if buf is not None and buf.is_cuda:
@@ -289,9 +329,45 @@ class GPTEngine:
         return buf[st.slot * M:(st.slot + 1) * M], buf
 
     def release_slots(self) -> None:
-        if any(b.is_cuda for b in self._slots.values()):
+        bufs = list(self._slots.values()) + list(self._head_lg.values()) + list(self._head_accs.values())
+        if any(b.is_cuda for b in bufs):
             torch.cuda.synchronize()
         self._slots.clear()
+        self._head_lg.clear()
+        self._head_accs.clear()
+        self._head_lg_ev = None
+
+    # ---------------------------------------------------------------- chunked head
+    def _head_rows(self, M: int, nseg: int):
+        """Row chunks of the lm_head (never straddling a loss segment)."""
+        seg = M // nseg
+        per = max(1, self.head_chunks // nseg)
+        while per > 1 and seg % per:
+            per -= 1
+        step = seg // per
+        return [(k * seg + j * step, k * seg + (j + 1) * step) for k in range(nseg) for j in range(per)]
+
+    def _head_buf(self, cache: dict, key, shape, dtype, device):
+        buf = cache.get(key)
+        if buf is None or tuple(buf.shape) != tuple(shape) or buf.dtype != dtype or buf.device != device:
+            if buf is not None and buf.is_cuda:
+                torch.cuda.synchronize(buf.device)  # shared across streams without record_stream
+            buf = torch.empty(shape, dtype=dtype, device=device)
+            cache[key] = buf
+        return buf
+
+    def _nf_scaled(self, nf, dloss, inv_ce, out=None):
+        if nf.dtype in (torch.bfloat16, torch.float16):
+            return self.ops.scale_bf16(nf, dloss, out=out, mul=inv_ce)
+        r = nf * (dloss * inv_ce)
+        return out.copy_(r) if out is not None else r
+
+    def _head_chunk_bwd(self, dl, w, dnf_out, acc, nfs, first: bool) -> None:
+        """One row chunk of the lm_head backward: dnf rows = dl @ E, acc (+)= dl^T @ nfs."""
+        self.gemm.linear_dgrad(dl, w, out=dnf_out)
+        if first:
+            acc.zero_()
+        self.gemm.wgrad_acc(acc, dl, nfs)
 
     # ---------------------------------------------------------------- helpers
     def rope(self, S: int, device):
@@ -397,12 +473,16 @@ class GPTEngine:
         x2, n2, rstd2 = ops.add_dropout_rmsnorm_fwd(x, a, w.ln2, self.eps, ph, k_resid, self.act_dtype,
                                                     y_out=sb("n2", H))
         del a
+        s_ring = self._s_in_ring(st)  # s is a temporary: the backward refills its ring slot
+        s_slot = None if s_ring else sb("s", I)
         if hasattr(gm, "linear_swiglu"):  # gate/up GEMM with SwiGLU in its epilogue (when faster)
-            gu, s = gm.linear_swiglu(n2, w.wgu, ops, s_out=sb("s", I))
+            gu, s = gm.linear_swiglu(n2, w.wgu, ops, s_out=s_slot)
         else:
             gu = gm.linear(n2, w.wgu)
-            s = ops.swiglu_fwd(gu, out=sb("s", I))
+            s = ops.swiglu_fwd(gu, out=s_slot)
         d_out = gm.linear(s, w.wdown)
+        if s_ring:
+            s = None
         if save:
             c = _LayerCache(x=x, rstd1=rstd1, n1=n1, q=q, k=k, v=v, o=o, lse=lse,
                             x2=x2, rstd2=rstd2, n2=n2, gu=gu, s=s)
@@ -457,14 +537,17 @@ class GPTEngine:
         del qkv
         _, n2, rstd2 = ops.add_dropout_rmsnorm_fwd(c.x2, None, w.ln2, self.eps, 0.0, 0, self.act_dtype,
                                                    y_out=sb("n2", H))
+        s_ring = self._s_in_ring(st)  # the backward writes s into its ring slot
         if c.gu is not None:  # gate/up output kept by the forward (_ac_keep)
             gu = c.gu
-            s = ops.swiglu_fwd(gu, out=sb("s", I))
+            s = None if s_ring else ops.swiglu_fwd(gu, out=sb("s", I))
         elif hasattr(gm, "linear_swiglu"):
-            gu, s = gm.linear_swiglu(n2, w.wgu, ops, s_out=sb("s", I))
+            gu, s = gm.linear_swiglu(n2, w.wgu, ops, s_out=None if s_ring else sb("s", I))
         else:
             gu = gm.linear(n2, w.wgu)
-            s = ops.swiglu_fwd(gu, out=sb("s", I))
+            s = None if s_ring else ops.swiglu_fwd(gu, out=sb("s", I))
+        if s_ring:
+            s = None
         return _LayerCache(x=c.x, rstd1=rstd1, n1=n1, q=q, k=k, v=v, o=c.o, lse=c.lse,
                            x2=c.x2, rstd2=rstd2, n2=n2, gu=gu, s=s)
 
@@ -475,11 +558,13 @@ class GPTEngine:
         return _drain(self._forward_gen(ids, targets, train, recompute, return_logits, need_backward))
 
     def _forward_gen(self, ids, targets, train, recompute=False, return_logits=False, need_backward=None,
-                     acc=None):
+                     acc=None, head_dloss=None):
         """Generator form of :meth:`forward`: yields after every block so the window
         scheduler (:meth:`train_window`) can interleave it with another micro-step's
         backward; the return value is forward's tuple.  ``acc`` = (slot, n_slots,
-        defer) overrides the engine-global accumulation state."""
+        defer) overrides the engine-global accumulation state.  ``head_dloss`` (the
+        backward's dloss, known up front in train_window): run the chunked lm_head
+        backward here ("early head", see head_chunks)."""
         B, S = ids.shape
         if need_backward is None:
             need_backward = torch.is_grad_enabled()
@@ -493,6 +578,7 @@ class GPTEngine:
         slot, n_slots, defer = acc if acc is not None else (self.acc_slot, self.acc_slots, self.defer)
         if need_bwd and defer:
             st.slot, st.defer, st.last = slot, True, slot == n_slots - 1
+        st.head_key = slot % 2  # micro-steps of a window alternate between two streams by parity
         prov = self.provider
         ph = self.p_hidden if train else 0.0
 
@@ -516,28 +602,64 @@ class GPTEngine:
         loss, logits = None, None
         V, Vp = self.cfg.vocab_size, hw.lm_head.shape[0]
         if targets is not None:
-            # [M, Vp]; with deferred weight gradients the logits (-> dlogits) of every
-            # micro-step of the window stay resident for ONE lm_head wgrad GEMM
-            lg_out = self._sb(st, "head", "lg", B * S, Vp, nf.device)
-            lg = self.gemm.linear(nf, hw.lm_head, out=lg_out)
+            rows = B * S
             nseg = self.loss_segments if (train and B % self.loss_segments == 0) else 1
+            # fused micro-steps: per-segment normalisation (see set_loss_segments); the
+            # gradient of (1/nseg) * mean_k: the CE kernel divides by its count argument
+            segs = [(k * rows // nseg, (k + 1) * rows // nseg) for k in range(nseg)]
             if nseg == 1:
-                n_valid = (targets != -100).sum()
-                row_loss = self.ops.cross_entropy_fwd_bwd(lg, targets, V, n_valid, self.ce_grad_scale)
-                loss = row_loss.sum() / n_valid.clamp(min=1).float()
-            else:  # fused micro-steps: per-segment normalisation (see set_loss_segments)
-                rows = (B // nseg) * S
-                seg_losses = []
-                for k in range(nseg):
-                    tk = targets[k * rows:(k + 1) * rows]
-                    nv = (tk != -100).sum()
-                    # gradient of (1/nseg) * mean_k: the kernel divides by its count argument
-                    rl = self.ops.cross_entropy_fwd_bwd(lg[k * rows:(k + 1) * rows], tk, V, nv * nseg,
-                                                        self.ce_grad_scale)
-                    seg_losses.append(rl.sum() / nv.clamp(min=1).float())
-                loss = torch.stack(seg_losses).mean()
+                nvs = [(targets != -100).sum()]
+                norms = nvs
+            else:
+                nvs = [(targets[a:b] != -100).sum() for a, b in segs]
+                norms = [nv * nseg for nv in nvs]
+            chunked = need_bwd and self.head_chunks > 0
+            if chunked:
+                st.head_rows = self._head_rows(rows, nseg)
+            if chunked and head_dloss is not None:
+                # early head: per row chunk, logits -> CE (gradient in place) -> the lm_head
+                # data gradient and weight gradient, through one chunk-sized logits buffer
+                H = self.cfg.hidden_size
+                rc = max(b - a for a, b in st.head_rows)
+                lg_buf = self._head_buf(self._head_lg, 0 if self.head_share else st.head_key, (rc, Vp), nf.dtype,
+                                        nf.device)
+                if self.head_share and self._head_lg_ev is not None:
+                    torch.cuda.current_stream().wait_event(self._head_lg_ev)
+                hacc = self._head_buf(self._head_accs, st.head_key, tuple(hw.lm_head.shape), torch.float32,
+                                      nf.device)
+                dnf = torch.empty(rows, H, dtype=nf.dtype, device=nf.device)
+                nfs = self._nf_scaled(nf, head_dloss.reshape(()).float(), 1.0 / self.ce_grad_scale)
+                parts = []
+                for ci, (a, b) in enumerate(st.head_rows):
+                    lg = self.gemm.linear(nf[a:b], hw.lm_head, out=lg_buf[:b - a])
+                    parts.append(self.ops.cross_entropy_fwd_bwd(lg, targets[a:b], V, norms[a * nseg // rows],
+                                                                self.ce_grad_scale))
+                    self._head_chunk_bwd(lg, hw.lm_head, dnf[a:b], hacc, nfs[a:b], ci == 0)
+                del nfs
+                if self.head_share and lg_buf.is_cuda:
+                    self._head_lg_ev = torch.cuda.Event()
+                    self._head_lg_ev.record()
+                row_loss = parts[0] if len(parts) == 1 else torch.cat(parts)
+                st.dnf, st.head_acc = dnf, hacc
+            else:
+                # [M, Vp]; with the window-deferred head (head_chunks 0) the logits
+                # (-> dlogits) of every micro-step stay resident for ONE lm_head wgrad GEMM
+                lg_out = self._sb(st, "head", "lg", rows, Vp, nf.device)
+                lg = self.gemm.linear(nf, hw.lm_head, out=lg_out)
+                if nseg == 1:
+                    row_loss = self.ops.cross_entropy_fwd_bwd(lg, targets, V, norms[0], self.ce_grad_scale)
+                else:
+                    row_loss = torch.cat([self.ops.cross_entropy_fwd_bwd(lg[a:b], targets[a:b], V, norms[k],
+                                                                         self.ce_grad_scale)
+                                          for k, (a, b) in enumerate(segs)])
+                if need_bwd:
+                    st.dlogits = lg  # now holds ce_grad_scale * d(mean loss)/d(logits)
+            if nseg == 1:
+                loss = row_loss.sum() / nvs[0].clamp(min=1).float()
+            else:
+                loss = torch.stack([row_loss[a:b].sum() / nvs[k].clamp(min=1).float()
+                                    for k, (a, b) in enumerate(segs)]).mean()
             if need_bwd:
-                st.dlogits = lg  # now holds ce_grad_scale * d(mean loss)/d(logits)
                 st.ce_scale = self.ce_grad_scale
                 st.xf, st.rstdf, st.nf = xf, rstdf, nf
         if return_logits or targets is None:
@@ -608,66 +730,76 @@ class GPTEngine:
         prov.pre_backward("head")
         hw, hg = prov.head(), prov.head_grads()
         M, H, I = B * S, cfg.hidden_size, cfg.intermediate_size
-        dev = st.dlogits.device
+        dev = st.nf.device
         # deferred roles: one GEMM over the window at the last micro-step (side stream);
         # the others (defer_roles) run in every micro-step's own backward, inline
         dfr = {r: self._deferred(st, r) for r in self.ROLES}
         win = st.last and any(dfr.values())  # this backward runs the window's deferred GEMMs
         side = self._wgrad_stream(dev) if win else None
-        # lm_head: dnf = dlogits @ E ; dE += dlogits^T @ (nf * dloss)
-        dnf = gm.linear_dgrad(st.dlogits, hw.lm_head)
-        nf_out = self._sb(st, "head", "nf", M, H, dev)
         inv_ce = 1.0 / st.ce_scale  # the pre-scaled CE gradient (fp16), see ce_grad_scale
-        if prev is None and mine is not None and _TEST_DELAY_FIRST_BWD:
-            # race test hook (DLT_TEST_DELAY_FIRST_BWD=cycles): the first overlapped backward
-            # writes its nf slot late, so a reader that does not wait for it sees stale data
-            torch.cuda._sleep(_TEST_DELAY_FIRST_BWD)
-        if st.nf.dtype in (torch.bfloat16, torch.float16):
-            nf_scaled = ops.scale_bf16(st.nf, dloss, out=nf_out, mul=inv_ce)
-        else:
-            nf_scaled = st.nf * (dloss * inv_ce)
-            if nf_out is not None:
-                nf_scaled = nf_out.copy_(nf_scaled)
-        if nf_out is not None:
-            # the window's lm_head weight gradient (the last backward, side stream) reads
-            # every micro-step's nf slot: "nf" marks this one written, chained through the
-            # previous backwards' marks (they run on other streams, a backward apart)
-            if prev is not None and "nf" in prev:
-                torch.cuda.current_stream().wait_event(prev["nf"])
-            mark("nf")
         head_ev = None
         head_add = None  # the window's lm_head weight gradient, added after the scatter-adds
         head_late = None  # overlapped backwards: the per-micro-step head wgrad waits for "embed"
-        if not dfr["head"]:
-            if prev is not None:
-                head_late = (st.dlogits, nf_scaled)
-            else:
-                gm.wgrad_acc(hg.embed, st.dlogits, nf_scaled)
-        elif st.last:
-            # ONE [Vp, H] wgrad GEMM over all GA*M rows of the window (K = 32768 instead
-            # of 4 x 8192), on the weight-gradient stream so it overlaps the layer
-            # backward.  It goes to its own buffer, added into the embedding gradient
-            # after the last scatter-add (head_done): the same order in every schedule
-            # (sequential, pipelined, overlapped), so it may run whenever its operands exist.
-            lg_all = self._slot_buf(st, "head", "lg", M, hw.lm_head.shape[0], dev)[1]
-            nf_all = self._slot_buf(st, "head", "nf", M, H, dev)[1]
-            head_add = self._head_wgrad_buf(hg.embed)
+        head_acc = None  # chunked head: this micro-step's lm_head weight gradient (fp32)
+        if st.dnf is not None:
+            # early head (train_window): the forward already ran the lm_head backward
+            dnf, head_acc = st.dnf, st.head_acc
+            st.dnf = st.head_acc = None
+        elif st.head_rows is not None:
+            # chunked head from the kept logits (autograd path): the same chunk GEMMs, in
+            # the same order, as the early head -- the same bits
+            dnf = torch.empty(M, H, dtype=st.nf.dtype, device=dev)
+            head_acc = self._head_buf(self._head_accs, st.head_key, tuple(hw.lm_head.shape), torch.float32, dev)
+            nfs = self._nf_scaled(st.nf, dloss, inv_ce)
+            for ci, (a, b) in enumerate(st.head_rows):
+                self._head_chunk_bwd(st.dlogits[a:b], hw.lm_head, dnf[a:b], head_acc, nfs[a:b], ci == 0)
+            del nfs
+        else:
+            # lm_head: dnf = dlogits @ E ; dE += dlogits^T @ (nf * dloss)
+            dnf = gm.linear_dgrad(st.dlogits, hw.lm_head)
+            nf_out = self._sb(st, "head", "nf", M, H, dev)
+            if prev is None and mine is not None and _TEST_DELAY_FIRST_BWD:
+                # race test hook (DLT_TEST_DELAY_FIRST_BWD=cycles): the first overlapped backward
+                # writes its nf slot late, so a reader that does not wait for it sees stale data
+                torch.cuda._sleep(_TEST_DELAY_FIRST_BWD)
+            nf_scaled = self._nf_scaled(st.nf, dloss, inv_ce, out=nf_out)
+            if nf_out is not None:
+                # the window's lm_head weight gradient (the last backward, side stream) reads
+                # every micro-step's nf slot: "nf" marks this one written, chained through the
+                # previous backwards' marks (they run on other streams, a backward apart)
+                if prev is not None and "nf" in prev:
+                    torch.cuda.current_stream().wait_event(prev["nf"])
+                mark("nf")
+            if not dfr["head"]:
+                if prev is not None:
+                    head_late = (st.dlogits, nf_scaled)
+                else:
+                    gm.wgrad_acc(hg.embed, st.dlogits, nf_scaled)
+            elif st.last:
+                # ONE [Vp, H] wgrad GEMM over all GA*M rows of the window (K = 32768 instead
+                # of 4 x 8192), on the weight-gradient stream so it overlaps the layer
+                # backward.  It goes to its own buffer, added into the embedding gradient
+                # after the last scatter-add (head_done): the same order in every schedule
+                # (sequential, pipelined, overlapped), so it may run whenever its operands exist.
+                lg_all = self._slot_buf(st, "head", "lg", M, hw.lm_head.shape[0], dev)[1]
+                nf_all = self._slot_buf(st, "head", "nf", M, H, dev)[1]
+                head_add = self._head_wgrad_buf(hg.embed)
 
-            def issue_head():
-                head_add.zero_()
-                gm.wgrad_acc(head_add, lg_all, nf_all)
-            if side is not None:
-                ev = torch.cuda.Event()
-                ev.record()  # after this backward's nf mark, which follows every earlier one
-                side.wait_event(ev)
-                for e in ready or ():
-                    side.wait_event(e)
-                with torch.cuda.stream(side):
+                def issue_head():
+                    head_add.zero_()
+                    gm.wgrad_acc(head_add, lg_all, nf_all)
+                if side is not None:
+                    ev = torch.cuda.Event()
+                    ev.record()  # after this backward's nf mark, which follows every earlier one
+                    side.wait_event(ev)
+                    for e in ready or ():
+                        side.wait_event(e)
+                    with torch.cuda.stream(side):
+                        issue_head()
+                        head_ev = torch.cuda.Event()
+                        head_ev.record()
+                else:
                     issue_head()
-                    head_ev = torch.cuda.Event()
-                    head_ev.record()
-            else:
-                issue_head()
         st.dlogits = None
         key_last = self._keys(st.micro, L - 1)[2]
         # The side stream lags the dgrad chain by a few layers' worth of weight-gradient
@@ -691,6 +823,8 @@ class GPTEngine:
             ops.embedding_bwd(st.ids, g_x2n if early_head else g_x2, hg.embed)
             if head_add is not None:
                 hg.embed.add_(head_add)
+            if head_acc is not None:
+                hg.embed.add_(head_acc)
             mark("embed")
             prov.post_backward("head")
 
@@ -726,11 +860,14 @@ class GPTEngine:
             w, gr = prov.layer(i), prov.layer_grads(i)
             k_attn, k_resid, k_mlp = self._keys(st.micro, i)
             # MLP
+            # s ring: the SwiGLU backward also rewrites s (the down wgrad operand) into
+            # layer i's ring slot, from the same gu with the forward's arithmetic
+            s_kw = {"s_out": sb(i, "s", I)} if self._s_in_ring(st) else {}
             if hasattr(gm, "linear_dgrad_swiglu"):  # down dgrad with the SwiGLU backward in its epilogue (when faster)
-                dgu = gm.linear_dgrad_swiglu(g_d, w.wdown, c.gu, ops, out=sb(i, "dgu", 2 * I))
+                dgu = gm.linear_dgrad_swiglu(g_d, w.wdown, c.gu, ops, out=sb(i, "dgu", 2 * I), **s_kw)
             else:
                 ds = gm.linear_dgrad(g_d, w.wdown)
-                dgu = ops.swiglu_bwd(c.gu, ds, out=sb(i, "dgu", 2 * I))
+                dgu = ops.swiglu_bwd(c.gu, ds, out=sb(i, "dgu", 2 * I), **s_kw)
                 del ds
             dn2 = gm.linear_dgrad(dgu, w.wgu)
             dx2, da = ops.rmsnorm_bwd(dn2, c.x2, c.rstd2, w.ln2, g_x2, gr.ln2, ph, k_resid,
@@ -884,7 +1021,7 @@ class GPTEngine:
         self._ring = ring if 2 <= ring < self.cfg.num_layers else 0
         self._ring_done = {}
         if self._ring:  # per-layer dY slots of an earlier schedule would only hold memory
-            for key in [k for k in self._slots if k[1] in self._DY_SLOTS and not isinstance(k[0], tuple)]:
+            for key in [k for k in self._slots if self._ring_name(k[1]) and not isinstance(k[0], tuple)]:
                 del self._slots[key]
         try:
             return self._window_ffbb_body(micro_ids, micro_targets, dloss, recompute, defer, sync_hook, before_last,
@@ -902,7 +1039,7 @@ class GPTEngine:
         ready: List[Any] = []
         # forwards: chain 0 first in every round (micro-step numbering = dropout streams)
         gens = [self._forward_gen(micro_ids[k], micro_targets[k], True, recompute, need_backward=True,
-                                  acc=(k, 2, defer)) for k in range(2)]
+                                  acc=(k, 2, defer), head_dloss=dloss) for k in range(2)]
         live = [0, 1]
         while live:
             for k in list(live):
@@ -1013,7 +1150,7 @@ class GPTEngine:
 
         def fwd(k):
             return self._forward_gen(micro_ids[k], micro_targets[k], True, recompute, need_backward=True,
-                                     acc=(k, GA, defer))
+                                     acc=(k, GA, defer), head_dloss=dloss)
 
         losses: List[Any] = [None] * GA
         states: List[Any] = [None] * GA
@@ -1089,7 +1226,9 @@ class _TorchGemm:
         return torch.matmul(x, w.t())
 
     @staticmethod
-    def linear_dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
+        if out is not None:
+            return torch.matmul(dy, w, out=out)
         return torch.matmul(dy, w)
 
     @staticmethod

@@ -335,9 +335,13 @@ __global__ __launch_bounds__(256) void k_swiglu_fwd(const bf16_t* __restrict__ g
   }
 }
 
+// s_out (optional): also writes s = silu(g) * u with the forward's exact arithmetic
+// (k_swiglu_fwd, same bits) -- the engine's ffbb window keeps s only in a short slot ring
+// filled here instead of one [M, I] slot per layer from the forward.
 template <int HK = 0>
 __global__ __launch_bounds__(256) void k_swiglu_bwd(const bf16_t* __restrict__ gu, const bf16_t* __restrict__ da,
-                                                    bf16_t* __restrict__ dgu, int M, int I) {
+                                                    bf16_t* __restrict__ dgu, bf16_t* __restrict__ s_out, int M,
+                                                    int I) {
   const int q = I >> 3;
   const size_t total = (size_t)M * q;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
@@ -346,16 +350,18 @@ __global__ __launch_bounds__(256) void k_swiglu_bwd(const bf16_t* __restrict__ g
     const u16x8 g = *reinterpret_cast<const u16x8*>(gu + m * 2 * I + c);
     const u16x8 u = *reinterpret_cast<const u16x8*>(gu + m * 2 * I + I + c);
     const u16x8 d = *reinterpret_cast<const u16x8*>(da + m * I + c);
-    u16x8 og, ou;
+    u16x8 og, ou, os;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const float gv = h2f<HK>(g.v[e]), uv = h2f<HK>(u.v[e]), dv = h2f<HK>(d.v[e]);
       const float sg = sigmoidf_(gv);
       og.v[e] = f2h<HK>(dv * uv * sg * (1.f + gv * (1.f - sg)));
       ou.v[e] = f2h<HK>(dv * gv * sg);
+      os.v[e] = f2h<HK>(gv * sg * uv);
     }
     *reinterpret_cast<u16x8*>(dgu + m * 2 * I + c) = og;
     *reinterpret_cast<u16x8*>(dgu + m * 2 * I + I + c) = ou;
+    if (s_out) *reinterpret_cast<u16x8*>(s_out + m * I + c) = os;
   }
 }
 
@@ -388,9 +394,10 @@ DLT_API int dlt_swiglu_fwd(const bf16_t* gu, bf16_t* a, int M, int I, int hk, hi
   DLT_CHECK_LAUNCH();
 }
 
-DLT_API int dlt_swiglu_bwd(const bf16_t* gu, const bf16_t* da, bf16_t* dgu, int M, int I, int hk, hipStream_t st) {
+DLT_API int dlt_swiglu_bwd(const bf16_t* gu, const bf16_t* da, bf16_t* dgu, bf16_t* s_out, int M, int I, int hk,
+                           hipStream_t st) {
   if (I % 8) return -1;
-  DLT_HK_DISPATCH(hk, k_swiglu_bwd<HKC><<<ew_blocks((size_t)M * (I / 8)), 256, 0, st>>>(gu, da, dgu, M, I));
+  DLT_HK_DISPATCH(hk, k_swiglu_bwd<HKC><<<ew_blocks((size_t)M * (I / 8)), 256, 0, st>>>(gu, da, dgu, s_out, M, I));
   DLT_CHECK_LAUNCH();
 }
 

@@ -431,11 +431,12 @@ class HipGemm:
         return dx
 
     def linear_dgrad_swiglu(self, dd: torch.Tensor, wdown: torch.Tensor, gu: torch.Tensor, ops,
-                            out: torch.Tensor = None) -> torch.Tensor:
+                            out: torch.Tensor = None, s_out: torch.Tensor = None) -> torch.Tensor:
         """dgu[M, 2I]: the down projection's data gradient ds = dd @ Wdown and the SwiGLU
         backward against the kept gu, fused in one hand-written kernel
         (``hip.gemm_down_swiglu_bwd``) or as ``linear_dgrad`` + ``ops.swiglu_bwd`` --
-        raced once per shape (kind "dswiglu")."""
+        raced once per shape (kind "dswiglu").  ``s_out``: also (re)writes the SwiGLU
+        output s = silu(g) * u there (the forward's bits; engine s ring)."""
         from . import hip
         M, H = dd.shape
         I = wdown.shape[1]
@@ -443,10 +444,15 @@ class HipGemm:
 
         def unfused():
             ds = self.linear_dgrad(dd, wdown)
-            ops.swiglu_bwd(gu, ds, out=dgu)
+            if s_out is not None:
+                ops.swiglu_bwd(gu, ds, out=dgu, s_out=s_out)
+            else:
+                ops.swiglu_bwd(gu, ds, out=dgu)
 
         def fused():
             hip.gemm_down_swiglu_bwd(dd, wdown, gu, out=dgu)
+            if s_out is not None:
+                ops.swiglu_fwd(gu, out=s_out)
         ok = (self._dgrad_on and hip.gemm_bf16_fits(M, I, H) and tuple(gu.shape) == (M, 2 * I)
               and self._hand_ok(gu, dgu))
         if ok and self._fused_pick("dswiglu", dd, wdown, fused, unfused, key=("dswiglu", M, I, H)):

@@ -44,7 +44,7 @@ _SIGS = {
     "dlt_rope_qkv_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                          c_int, c_int, c_void_p],
     "dlt_swiglu_fwd": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
-    "dlt_swiglu_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
+    "dlt_swiglu_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "dlt_cross_entropy_fwd_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int,
                                   c_void_p],
     "dlt_sumsq": [c_void_p, c_int64, c_void_p, c_void_p, c_void_p],
@@ -590,14 +590,18 @@ def swiglu_fwd(gu, out=None):
     return out
 
 
-def swiglu_bwd(gu, da, out=None):
+def swiglu_bwd(gu, da, out=None, s_out=None):
+    """dgu = SwiGLU backward; ``s_out``: also writes s = silu(g) * u (the forward's bits)."""
     M, twoI = gu.shape
     hk = _req_act(gu, gu.dtype, "swiglu_bwd.gu")
     _req(da, gu.dtype, "swiglu_bwd.da", M * twoI // 2)
     if out is None:
         out = torch.empty_like(gu)
     _req(out, gu.dtype, "swiglu_bwd.out", M * twoI)
-    _chk(lib().dlt_swiglu_bwd(_p(gu), _p(da), _p(out), M, twoI // 2, hk, _stream()), "swiglu_bwd")
+    if s_out is not None:
+        _req(s_out, gu.dtype, "swiglu_bwd.s_out", M * twoI // 2)
+    _chk(lib().dlt_swiglu_bwd(_p(gu), _p(da), _p(out), _p(s_out) if s_out is not None else None, M, twoI // 2, hk,
+                              _stream()), "swiglu_bwd")
     return out
 
 

@@ -239,8 +239,11 @@ def swiglu_fwd(gu: torch.Tensor, out=None) -> torch.Tensor:
     return r
 
 
-def swiglu_bwd(gu: torch.Tensor, da: torch.Tensor, out=None) -> torch.Tensor:
+def swiglu_bwd(gu: torch.Tensor, da: torch.Tensor, out=None, s_out=None) -> torch.Tensor:
+    """``s_out``: also writes s = silu(g) * u (as swiglu_fwd)."""
     i = gu.shape[-1] // 2
+    if s_out is not None:
+        swiglu_fwd(gu, out=s_out)
     g, u = gu[:, :i].float(), gu[:, i:].float()
     d = da.float()
     sg = torch.sigmoid(g)

@@ -86,6 +86,7 @@ class FlatUnit:
         self.full_grad: Optional[torch.Tensor] = None   # full fp32 grads during backward
         self.ag_work = None
         self.rs_pending = []
+        self.host_bufs = []      # cpu_offload: pinned staging buffers, one per pending reduce
         self.refs = 0            # chains (forward / backward of a micro-step) using `full`
         self.ready_ev = None     # HIP event: `full` is complete (recorded after the gather wait)
         self.norm_grad = None    # bf16-gradient mode: fp32 ln1 | ln2 gradients of the micro-step
@@ -151,6 +152,7 @@ class FSDPRuntime(ParamProvider):
         self.max_prefetch = 2 if limit_all_gathers else 1 << 30
         self._prefetched = set()
         self._rep_stream = None  # HYBRID_SHARD: replicate all-reduces off the compute stream
+        self._d2h_stream = None  # cpu_offload: reduced shards copied to pinned host buffers
         self.units: Dict[object, FlatUnit] = {}
         self._build_units(model)
         self._free_module_params(model)
@@ -314,7 +316,7 @@ class FSDPRuntime(ParamProvider):
             work = None
             if self.dist and (self.world > 1 or self.force):
                 work = dist.all_reduce(t, group=self.pg if self.strategy != "NO_SHARD" else None, async_op=True)
-            u.rs_pending.append((work, t, None))
+            u.rs_pending.append(self._stage_host(u, work, t, None))
         else:
             src = g if self.reduce_dtype == torch.float32 else g.to(self.reduce_dtype)
             out = torch.empty(u.shard, dtype=src.dtype, device=self.device)
@@ -333,11 +335,44 @@ class FSDPRuntime(ParamProvider):
                 else:
                     work.wait()
                     work = dist.all_reduce(out, group=self.rep_pg, async_op=True)
-            u.rs_pending.append((work, out, src))
+            u.rs_pending.append(self._stage_host(u, work, out, src))
         u.full_grad = None
 
+    def _stage_host(self, u: FlatUnit, work, out: torch.Tensor, src):
+        """cpu_offload: copy the reduced shard to a pinned host buffer as soon as its
+        collective completes -- on a copy stream that waits for it on the device, so the
+        D2H transfer overlaps the rest of the backward instead of a blocking ``.cpu()`` per
+        unit in finish(), which then only waits for the copy and adds on the host.
+        Returns the rs_pending entry (work, out, src, host, event)."""
+        if not (self.cpu_offload and out.is_cuda):
+            return (work, out, src, None, None)
+        if self._d2h_stream is None:
+            self._d2h_stream = torch.cuda.Stream(self.device)
+        k = len(u.rs_pending)
+        n = min(out.numel(), u.shard)
+        while len(u.host_bufs) <= k:
+            u.host_bufs.append(None)
+        host = u.host_bufs[k]
+        if host is None or host.numel() != n or host.dtype != out.dtype:
+            host = torch.empty(n, dtype=out.dtype, pin_memory=True)
+            u.host_bufs[k] = host
+        cur = torch.cuda.current_stream(self.device)
+        self._d2h_stream.wait_stream(cur)  # `out` / the collective were issued from here
+        with torch.cuda.stream(self._d2h_stream):
+            if work is not None:
+                work.wait()  # device-side: the copy stream waits for the collective
+            host.copy_(out[:n], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        out.record_stream(self._d2h_stream)
+        return (None, out, src, host, ev)
+
     def _finish_reduce(self, u: FlatUnit):
-        for work, out, _src in u.rs_pending:
+        for work, out, _src, host, ev in u.rs_pending:
+            if host is not None:  # cpu_offload: the staged D2H copy (see _stage_host)
+                ev.synchronize()
+                u.grad.add_(host)
+                continue
             if work is not None:
                 work.wait()
             if out.numel() != u.shard:  # NO_SHARD: full buffer == shard

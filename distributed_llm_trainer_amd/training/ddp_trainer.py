@@ -115,6 +115,8 @@ class DistributedTrainer:
             act = self.dtype if self.device.type == "cuda" else None
             eng = self.model.enable_engine(seed=self.training_config.seed + 1000003 * self.rank, act_dtype=act)
             eng.defer_roles = parse_defer_roles(self.training_config.defer_roles)
+            if "head" not in eng.defer_roles and not eng.head_chunks_env:
+                eng.head_chunks = 2  # memory-lean: chunked lm_head run in the forwards (GPTEngine)
             self.store = self.model.store
         else:
             self.store = FlatParamStore(self.model, self.device, compute_dtype=torch.float32)

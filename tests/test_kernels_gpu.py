@@ -142,6 +142,11 @@ def test_swiglu():
     _close(hip.swiglu_fwd(gu), ref.swiglu_fwd(gu), 3e-2, 1e-2, "swiglu fwd")
     da = torch.randn(M, I, device=DEV).bfloat16()
     _close(hip.swiglu_bwd(gu, da), ref.swiglu_bwd(gu, da), 3e-2, 1e-2, "swiglu bwd")
+    # the optional s output (engine s ring) carries exactly the forward kernel's bits
+    s_out = torch.empty(M, I, device=DEV, dtype=torch.bfloat16)
+    dgu = hip.swiglu_bwd(gu, da, s_out=s_out)
+    assert torch.equal(s_out, hip.swiglu_fwd(gu))
+    assert torch.equal(dgu, hip.swiglu_bwd(gu, da))
 
 
 def test_cross_entropy():

@@ -191,17 +191,20 @@ def test_pipelined_window_matches_sequential_gpu(recompute):
         assert torch.equal(g1[n], g2[n]), (n, (g1[n] - g2[n]).abs().max().item())
 
 
-@pytest.mark.parametrize("recompute,ring,serial", [(False, "0", False), (True, "0", False), (False, "2", False),
-                                                   (True, "2", False), (False, "2", True)])
-def test_window_ffbb_matches_sequential_gpu(recompute, ring, serial, monkeypatch):
+@pytest.mark.parametrize("recompute,ring,serial,sring", [(False, "0", False, "1"), (True, "0", False, "1"),
+                                                         (False, "2", False, "1"), (True, "2", False, "1"),
+                                                         (False, "2", True, "1"), (False, "2", False, "0")])
+def test_window_ffbb_matches_sequential_gpu(recompute, ring, serial, sring, monkeypatch):
     """Two-chain window F0 || F1 | B0 || B1 (DLT_WINDOW_SCHED=ffbb: both forwards, then both
     backwards concurrently, B1 one block behind B0 with per-buffer waits) == the sequential
     schedule: same losses, bit-identical gradients -- with one dY slot per layer (ring 0)
     and with the dY operands in a 2-slot ring (reused while the other backward and the
-    side-stream weight gradients are still running)."""
+    side-stream weight gradients are still running); with the SwiGLU output s in that
+    ring (rewritten by the backward, DLT_S_RING=1) or in per-layer slots from the forward."""
     from distributed_llm_trainer_amd.models.engine import shift_targets
     monkeypatch.setenv("DLT_WINDOW_SCHED", "ffbb")
     monkeypatch.setenv("DLT_SLOT_RING", ring)
+    monkeypatch.setenv("DLT_S_RING", sring)
     torch.manual_seed(6)
     base = GPT(_cfg(0.1)).to(DEV)
     m1, m2 = copy.deepcopy(base), copy.deepcopy(base)
@@ -731,18 +734,22 @@ def test_engine_gpt2_small_grads_vs_fp32_eager(act):
     assert worst[0] < bound, worst
 
 
-@pytest.mark.parametrize("dgrad,delay", [("1", 0), ("0", 0), ("1", 20_000_000)])
-def test_window_ffbb_hand_kernels_match_sequential_gpu(dgrad, delay, monkeypatch):
+@pytest.mark.parametrize("dgrad,delay,chunks", [("1", 0, "2"), ("0", 0, "2"), ("1", 0, "0"), ("1", 20_000_000, "0"),
+                                                ("1", 0, "4")])
+def test_window_ffbb_hand_kernels_match_sequential_gpu(dgrad, delay, chunks, monkeypatch):
     """The ffbb window at shapes every hand-written kernel tiles (hidden 384, 3H 1152,
     2I 3072, vocab 1152, 1024-token chains): the hand forward / data-gradient / weight-
     gradient GEMMs on two concurrent chains (grid capped at 192 workgroups) must give
-    the sequential schedule's gradients bit for bit.  delay: the first backward is held
-    back by a spin kernel before it writes its lm_head-gradient (nf) slot -- the race of
-    round 3 (the window's head weight gradient did not wait for that write)."""
+    the sequential schedule's gradients bit for bit -- with the chunked lm_head (run in
+    the window's forwards, "early head") and with the round-3 window-deferred head
+    (chunks 0).  delay (window head): the first backward is held back by a spin kernel
+    before it writes its lm_head-gradient (nf) slot -- the race of round 3 (the window's
+    head weight gradient did not wait for that write)."""
     from distributed_llm_trainer_amd.models import engine as engine_mod
     from distributed_llm_trainer_amd.models.engine import shift_targets
     monkeypatch.setenv("DLT_WINDOW_SCHED", "ffbb")
     monkeypatch.setenv("DLT_GEMM_DGRAD", dgrad)
+    monkeypatch.setenv("DLT_HEAD_CHUNKS", chunks)
     monkeypatch.setattr(engine_mod, "_TEST_DELAY_FIRST_BWD", delay)
     cfg = GPTConfig(vocab_size=1152, hidden_size=384, num_layers=4, num_heads=6, intermediate_size=1536,
                     max_seq_len=256, dropout=0.1, attention_dropout=0.1)

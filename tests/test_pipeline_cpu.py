@@ -20,13 +20,17 @@ def tiny(**kw):
     return GPTConfig(**d)
 
 
-@pytest.mark.parametrize("GA,recompute", [(2, False), (3, False), (4, True)])
-def test_train_window_matches_sequential(GA, recompute):
+@pytest.mark.parametrize("GA,recompute,chunks", [(2, False, 0), (3, False, 0), (4, True, 0), (2, False, 2),
+                                                  (3, True, 1), (2, False, 3)])
+def test_train_window_matches_sequential(GA, recompute, chunks):
+    """chunks > 0: the chunked lm_head (GPTEngine.head_chunks) -- run in the window's
+    forwards ("early head") vs from the kept logits in the sequential backward."""
     torch.manual_seed(11)
     m1 = GPT(tiny())
     m2 = copy.deepcopy(m1)
     e1 = m1.enable_engine(seed=5)
     e2 = m2.enable_engine(seed=5)
+    e1.head_chunks = e2.head_chunks = chunks
     m1.gradient_checkpointing = m2.gradient_checkpointing = recompute
     m1.train()
     m2.train()
@@ -174,13 +178,17 @@ def test_fsdp_trainer_pipelined_matches_sequential(strategy, sync_every):
         assert torch.allclose(res[0][1][k], res[1][1][k], atol=1e-7, rtol=1e-6), k
 
 
-@pytest.mark.parametrize("F,pipe", [(2, True), (2, False), (4, True)])
-def test_micro_step_fusion_matches_unfused(F, pipe):
+@pytest.mark.parametrize("F,pipe,chunks", [(2, True, None), (2, False, None), (4, True, None), (2, True, "2"),
+                                           (4, True, "1")])
+def test_micro_step_fusion_matches_unfused(F, pipe, chunks, monkeypatch):
     """micro_step_fusion=F executes F micro-steps as one chain of F*batch rows: the
     trainer step equals the unfused GA average (dropout off: fused chains draw other
-    dropout streams by design).  Ragged ignore_index counts: the next test."""
+    dropout streams by design).  Ragged ignore_index counts: the next test.  chunks:
+    the chunked lm_head (DLT_HEAD_CHUNKS; per-segment chunks when fewer are asked)."""
     from distributed_llm_trainer_amd.training.configs import TrainingConfig
     from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
+    if chunks is not None:
+        monkeypatch.setenv("DLT_HEAD_CHUNKS", chunks)
     torch.manual_seed(14)
     data = torch.randint(0, 256, (8, 32))
     res = []

@@ -398,7 +398,7 @@ static int dgrad_main(std::vector<int> shp) {
     auto fused = [&]() { return dlt_gemm_bf16_down_swiglu_bwd(dd, Wd, gu, dgu, M, I, H, 0, st); };
     auto unfused = [&]() {
       int rc = run_blas_nn(dd, Wd, ds, M, I, H, st);
-      return rc ? rc : dlt_swiglu_bwd(gu, ds, dgu2, M, I, 0, st);
+      return rc ? rc : dlt_swiglu_bwd(gu, ds, dgu2, nullptr, M, I, 0, st);
     };
     CK(hipMemsetAsync(dgu, 0xff, (size_t)M * 2 * I * 2, st));
     if (fused()) {
