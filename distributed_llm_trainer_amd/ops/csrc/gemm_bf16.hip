@@ -661,25 +661,32 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
             const bf16_t* grow = ep.gu_in + (size_t)row * ep.ld_s + n0 + col;
             const gb_u32x4_t gv = *reinterpret_cast<const gb_u32x4_t*>(grow);
             const gb_u32x4_t uv = *reinterpret_cast<const gb_u32x4_t*>(grow + ep.I);
-            gb_u32x4_t og, ou;
+            gb_u32x4_t og, ou, os;
+            const bool want_s = ep.s_out != nullptr;  // uniform
 #pragma unroll
             for (int h = 0; h < 4; ++h) {
               float d[2] = {__uint_as_float(cv[h] << 16), __uint_as_float(cv[h] & 0xffff0000u)};
               float g[2] = {__uint_as_float(gv[h] << 16), __uint_as_float(gv[h] & 0xffff0000u)};
               float u[2] = {__uint_as_float(uv[h] << 16), __uint_as_float(uv[h] & 0xffff0000u)};
-              floatx4_t r;
+              floatx4_t r, sv;
 #pragma unroll
               for (int e = 0; e < 2; ++e) {
                 const float sg = dlt_sigmoid(g[e]);
                 r[e] = d[e] * u[e] * sg * (1.f + g[e] * (1.f - sg));
                 r[2 + e] = d[e] * g[e] * sg;
+                sv[e] = g[e] * sg * u[e];  // s = silu(g) * u: k_swiglu_fwd's arithmetic, same bits
+                sv[2 + e] = 0.f;
               }
               const uint2 pr = gb_pack(r);  // (dg0, dg1), (du0, du1)
               og[h] = pr.x;
               ou[h] = pr.y;
+              os[h] = gb_pack(sv).x;
             }
             *reinterpret_cast<gb_u32x4_t*>(crow + col) = og;
             *reinterpret_cast<gb_u32x4_t*>(crow + ep.I + col) = ou;
+            // s_out (engine s ring): the down weight gradient's operand, rewritten from the
+            // kept gu as k_swiglu_bwd's s_out does -- no separate k_swiglu_fwd pass
+            if (want_s) *reinterpret_cast<gb_u32x4_t*>(ep.s_out + (size_t)row * ep.I + n0 + col) = os;
           } else {
             gb_u32x4_t* cp = reinterpret_cast<gb_u32x4_t*>(crow + col);
             if (flags & 128)  // nontemporal (streaming) C stores
@@ -778,11 +785,11 @@ DLT_API int dlt_gemm_bf16_nn(const bf16_t* dY, const bf16_t* W, bf16_t* dX, int 
 
 // Down-projection data gradient fused with the SwiGLU backward: ds = dd[M, H] . Wdown[H, I]
 // (bf16-rounded) and dgu[M, 2I] from ds and the kept gu[M, 2I] (k_swiglu_bwd's math).
-DLT_API int dlt_gemm_bf16_down_swiglu_bwd(const bf16_t* dd, const bf16_t* Wdown, const bf16_t* gu, bf16_t* dgu, int M,
-                                          int I, int H, int flags, hipStream_t st) {
+DLT_API int dlt_gemm_bf16_down_swiglu_bwd(const bf16_t* dd, const bf16_t* Wdown, const bf16_t* gu, bf16_t* dgu,
+                                          bf16_t* s_out, int M, int I, int H, int flags, hipStream_t st) {
   if (!gb_shape_ok(M, I, H, H, I, 2 * I) || I % 192) return -1;
   const int ntiles = (M / 256) * (I / 192);
-  GbEpi ep{nullptr, nullptr, 1, 0, nullptr, 2 * I, I, gu};
+  GbEpi ep{nullptr, nullptr, 1, 0, s_out, 2 * I, I, gu};  // s_out (optional): s [M, I], row stride I
   k_gemm_bf16<192, GB_EPI_SWIGLU_BWD, true>
       <<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(dd, Wdown, dgu, M, I, H, H, I, 2 * I, flags, ep);
   DLT_CHECK_LAUNCH();

@@ -450,11 +450,9 @@ class HipGemm:
                 ops.swiglu_bwd(gu, ds, out=dgu)
 
         def fused():
-            hip.gemm_down_swiglu_bwd(dd, wdown, gu, out=dgu)
-            if s_out is not None:
-                ops.swiglu_fwd(gu, out=s_out)
+            hip.gemm_down_swiglu_bwd(dd, wdown, gu, out=dgu, s_out=s_out)
         ok = (self._dgrad_on and hip.gemm_bf16_fits(M, I, H) and tuple(gu.shape) == (M, 2 * I)
-              and self._hand_ok(gu, dgu))
+              and self._hand_ok(gu, dgu) and (s_out is None or self._hand_ok(s_out)))
         if ok and self._fused_pick("dswiglu", dd, wdown, fused, unfused, key=("dswiglu", M, I, H)):
             fused()
         else:

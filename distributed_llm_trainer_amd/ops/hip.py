@@ -64,7 +64,8 @@ _SIGS = {
                                c_void_p],
     "dlt_gemm_bf16_gu_swiglu": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
     "dlt_gemm_bf16_nn": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
-    "dlt_gemm_bf16_down_swiglu_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
+    "dlt_gemm_bf16_down_swiglu_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                      c_void_p],
     "dlt_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                      c_uint32, c_uint32, c_float, c_int, c_int, c_void_p],
     "dlt_attn_dropout_mask": [c_void_p, c_int, c_int, c_int, c_uint32, c_uint32, c_void_p],
@@ -850,10 +851,13 @@ def gemm_dgrad(dy: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = 
 
 
 def gemm_down_swiglu_bwd(dd: torch.Tensor, wdown: torch.Tensor, gu: torch.Tensor,
-                         out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+                         out: Optional[torch.Tensor] = None, s_out: Optional[torch.Tensor] = None
+                         ) -> Optional[torch.Tensor]:
     """dgu[M, 2I] = SwiGLU backward of ds = dd[M, H] @ Wdown[H, I] (bf16-rounded) against
     the kept gu[M, 2I] -- the down projection's data gradient and ``swiglu_bwd`` in one
-    kernel (same math and roundings as the unfused pair).  None if it does not tile."""
+    kernel (same math and roundings as the unfused pair).  ``s_out`` [M, I] (optional):
+    also writes s = silu(g) * u with the forward's bits (``swiglu_bwd``'s s_out).  None
+    if it does not tile."""
     M, H = dd.shape
     I = wdown.shape[1]
     if not gemm_bf16_fits(M, I, H) or wdown.shape[0] != H or tuple(gu.shape) != (M, 2 * I):
@@ -863,8 +867,10 @@ def gemm_down_swiglu_bwd(dd: torch.Tensor, wdown: torch.Tensor, gu: torch.Tensor
     _req(gu, torch.bfloat16, "gemm_down_swiglu_bwd.gu")
     c = torch.empty(M, 2 * I, dtype=torch.bfloat16, device=dd.device) if out is None else out
     _req(c, torch.bfloat16, "gemm_down_swiglu_bwd.out", M * 2 * I)
-    _chk(lib().dlt_gemm_bf16_down_swiglu_bwd(_p(dd), _p(wdown), _p(gu), _p(c), M, I, H, _GB_FLAGS, _stream()),
-         "gemm_down_swiglu_bwd")
+    if s_out is not None:
+        _req(s_out, torch.bfloat16, "gemm_down_swiglu_bwd.s_out", M * I)
+    _chk(lib().dlt_gemm_bf16_down_swiglu_bwd(_p(dd), _p(wdown), _p(gu), _p(c), _p(s_out), M, I, H, _GB_FLAGS,
+                                             _stream()), "gemm_down_swiglu_bwd")
     return c
 
 

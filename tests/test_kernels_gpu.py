@@ -607,6 +607,12 @@ def test_gemm_down_swiglu_bwd_vs_fp32():
     assert _relerr(dgu, want) < 1.5e-2, _relerr(dgu, want)
     ref_k = hip.swiglu_bwd(gu, (dd.float() @ wd.float()).bfloat16())
     assert _relerr(dgu, ref_k.float()) < 1.5e-2
+    # s_out: s = silu(g) * u with the forward kernel's exact bits (the engine's s ring),
+    # the dgu output unchanged by it
+    s = torch.full((M, I), float("nan"), dtype=torch.bfloat16, device=DEV)
+    dgu2 = hip.gemm_down_swiglu_bwd(dd, wd, gu, s_out=s)
+    assert torch.equal(dgu2, dgu)
+    assert torch.equal(s, hip.swiglu_fwd(gu))
 
 
 def test_planner_dgrad_races_match_library():

@@ -395,10 +395,10 @@ static int dgrad_main(std::vector<int> shp) {
     std::vector<bf16_t> hgu((size_t)nr * 2 * I), got((size_t)nr * 2 * I);
     CK(hipMemcpyAsync(ref.data(), R, ref.size() * 4, hipMemcpyDeviceToHost, st));
     CK(hipMemcpyAsync(hgu.data(), gu + (size_t)r0 * 2 * I, hgu.size() * 2, hipMemcpyDeviceToHost, st));
-    auto fused = [&]() { return dlt_gemm_bf16_down_swiglu_bwd(dd, Wd, gu, dgu, M, I, H, 0, st); };
+    auto fused = [&]() { return dlt_gemm_bf16_down_swiglu_bwd(dd, Wd, gu, dgu, ds, M, I, H, 0, st); };  // + s into ds
     auto unfused = [&]() {
       int rc = run_blas_nn(dd, Wd, ds, M, I, H, st);
-      return rc ? rc : dlt_swiglu_bwd(gu, ds, dgu2, nullptr, M, I, 0, st);
+      return rc ? rc : dlt_swiglu_bwd(gu, ds, dgu2, ds, M, I, 0, st);  // + s (in place over ds, as the s ring)
     };
     CK(hipMemsetAsync(dgu, 0xff, (size_t)M * 2 * I * 2, st));
     if (fused()) {
