@@ -774,3 +774,17 @@ def test_window_ffbb_hand_kernels_match_sequential_gpu(dgrad, delay, chunks, mon
     g1, g2 = _grads(m1), _grads(m2)
     for n in g1:
         assert torch.equal(g1[n], g2[n]), (n, (g1[n] - g2[n]).abs().max().item(), rep)
+
+
+def test_window_ffbb_forced_fused_epilogues_match_sequential_gpu(monkeypatch):
+    """As test_window_ffbb_hand_kernels_match_sequential_gpu with every fused-epilogue race
+    forced to the hand-written kernel (QKV + RoPE, gate/up + SwiGLU, every data gradient,
+    down dgrad + SwiGLU backward): the ffbb window's s ring is then refilled by the fused
+    down-dgrad epilogue (s_out) while the sequential schedule keeps the forward's s -- the
+    gradients match bit for bit only if both produce the same s bits."""
+    from distributed_llm_trainer_amd.ops import gemm as gemm_mod
+
+    def forced(self, kind, x, w, fused, unfused, key=None):
+        return self._hand_ok(x, w)
+    monkeypatch.setattr(gemm_mod.HipGemm, "_fused_pick", forced)
+    test_window_ffbb_hand_kernels_match_sequential_gpu("1", 0, "0", monkeypatch)
