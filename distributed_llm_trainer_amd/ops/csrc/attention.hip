@@ -487,6 +487,18 @@ __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const b
 // ~1.1 resident waves per SIMD on average at B16).  Round 1 measured one item per
 // workgroup in the NATURAL order 1.8x slower than the pairing (equal-length items
 // stacked on a CU); longest-first does not stack them.
+// Forward diagnostics (tools/cpp/attn_fwd_timing.cpp, -DDLT_ATTN_FWD_TIMING only): per
+// wave, the shader cycles inside the tile compute and inside the per-tile DMA wait +
+// barrier, and the tile count, written by lane 0 with vector stores.
+#ifdef DLT_ATTN_FWD_TIMING
+__device__ unsigned long long* g_attn_ftim;
+#define FWD_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define FWD_ACC(c, w) (f_comp += (c), f_wait += (w), ++f_tiles)
+#else
+#define FWD_T(v) ((void)0)
+#define FWD_ACC(c, w) ((void)0)
+#endif
+
 template <bool DROP, int HK = 0>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_attn_fwd(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
                                                     const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
@@ -507,6 +519,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   using B1 = std::integral_constant<int, 1>;
   using UNM = std::integral_constant<bool, false>;
   using MSK = std::integral_constant<bool, true>;
+#ifdef DLT_ATTN_FWD_TIMING
+  unsigned long long f_comp = 0, f_wait = 0, f_tiles = 0;
+  const unsigned long long f_t0 = __builtin_amdgcn_s_memtime();
+#endif
 
 #pragma unroll 1
   for (int it = 0; it < 2; ++it) {
@@ -540,6 +556,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     auto step = [&](auto bufc, auto maskc, int kb) {
       constexpr int BUF = decltype(bufc)::value;
       constexpr bool MASKED = decltype(maskc)::value;
+      FWD_T(ta);
       const bool more = kb + 1 < nkv;
       if (more) {  // next tile straight into the other buffer (read by nobody since the last barrier)
         bf16_t* Kn = lds + (BUF ^ 1) * 2 * KVB * HD;
@@ -555,7 +572,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       else if (k0 <= q0 + 31)
         fwd_tile<true, DROP, HK>(fs, Kt, Vt, qf, k0, qa, S, lane, c_log2, mw_cur);
       mw_cur = mw_next;
+      FWD_T(tb);
       tile_barrier();
+      FWD_T(tc);
+      FWD_ACC(tb - ta, tc - tb);
     };
     const int nfull = min(qb, nkv);
     int kb = 0;
@@ -588,6 +608,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       store_row16(orow, w, h);
     }
   }
+#ifdef DLT_ATTN_FWD_TIMING
+  const unsigned long long f_t1 = __builtin_amdgcn_s_memtime();
+  if (lane == 0) {
+    unsigned long long* r = g_attn_ftim + ((size_t)blockIdx.x * 2 + wid) * 6;
+    r[0] = f_t0; r[1] = f_t1; r[2] = f_comp; r[3] = f_wait; r[4] = f_tiles;
+  }
+#endif
 }
 
 // ============================================================================ backward
