@@ -60,6 +60,9 @@ def main():
                          "(dummy mode: uniform ids from a counter hash, pinned ring, H2D on a side stream), so "
                          "the input pipeline is inside the timed region as in the reference; resident: 4 "
                          "pre-made device batches reused")
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"],
+                    help="DDP: TrainingConfig.mixed_precision (the headline is bf16; fp16 = the HIP kernels "
+                         "instantiated for IEEE half + dynamic loss scaling, fp32 = the reference/debug mode)")
     ap.add_argument("--dropout", type=float, default=None,
                     help="ablation only: override dropout/attention_dropout (reference config: 0.1)")
     args = ap.parse_args()
@@ -86,7 +89,7 @@ def main():
         from distributed_llm_trainer_amd.training.configs import TrainingConfig
         from distributed_llm_trainer_amd.training.ddp_trainer import LEAN_DEFER_ROLES, DistributedTrainer
         tc = TrainingConfig(batch_size=args.batch_size, gradient_accumulation_steps=args.grad_accum,
-                            max_steps=100000, mixed_precision="bf16", micro_step_fusion=args.fusion,
+                            max_steps=100000, mixed_precision=args.precision, micro_step_fusion=args.fusion,
                             defer_roles=LEAN_DEFER_ROLES if args.memory_lean else "all")
         trainer = DistributedTrainer(cfg, tc)
     else:
@@ -151,7 +154,7 @@ def main():
             "metric": "tokens/sec", "value": round(tps, 1), "unit": "tokens/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 3),
             "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": round(tps / base, 3) if base else None, "dtype": "bf16", "data": "synthetic",
+            "vs_baseline": round(tps / base, 3) if base else None, "dtype": args.precision if args.mode == "ddp" else "bf16", "data": "synthetic",
             "input_pipeline": "native loader (fresh batch per step, in the timed loop)" if loader is not None
             else "resident batches",
             "config": {"model": f"GPT-2 124M (gpt2_{args.model_size} preset, {cfg.num_parameters():,} params, "

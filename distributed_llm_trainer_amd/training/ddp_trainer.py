@@ -131,7 +131,7 @@ class DistributedTrainer:
                                               c.weight_decay, split_no_decay=True)
 
     def fusion_factor(self, GA: int, micro_bs: int, seq_len: int) -> int:
-        gpu_engine = self.use_engine and self.device.type == "cuda" and self.loss_scale is None
+        gpu_engine = self.use_engine and self.device.type == "cuda"
         return micro_step_fusion(self.training_config.micro_step_fusion, GA, micro_bs, seq_len, gpu_engine)
 
     def chains_per_step(self) -> int:
@@ -172,7 +172,6 @@ class DistributedTrainer:
         # micro-step pipelining (engine.train_window): from the second step on, so the
         # first one runs the GEMM autotuning on a quiet GPU
         window_ok = (self.use_engine and chains > 1 and cfg.pipeline_micro_steps
-                     and self.loss_scale is None
                      and (self.device.type != "cuda" or getattr(self.model.engine.gemm, "stream_safe", False))
                      and os.environ.get("DLT_PIPELINE", "1") != "0")
         pipelined = window_ok and self._engine_warm
@@ -188,7 +187,8 @@ class DistributedTrainer:
             tg_l = [shift_targets(x) for x in ids_l]
             if self.ddp is not None:
                 self.ddp.require_sync(False)
-            dloss = torch.full((), 1.0 / chains, dtype=torch.float32, device=self.device)
+            # fp16: the backward seed carries the loss scale, as (loss * scale).backward() does
+            dloss = torch.full((), (self.loss_scale or 1.0) / chains, dtype=torch.float32, device=self.device)
             range_push("window")
             # defer_wgrad=False: each chain's weight gradients run in its own backward, so no
             # [GA*M, N] slot buffers and no window-wide dlogits are kept (defer_roles: per role)

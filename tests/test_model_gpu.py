@@ -788,3 +788,25 @@ def test_window_ffbb_forced_fused_epilogues_match_sequential_gpu(monkeypatch):
         return self._hand_ok(x, w)
     monkeypatch.setattr(gemm_mod.HipGemm, "_fused_pick", forced)
     test_window_ffbb_hand_kernels_match_sequential_gpu("1", 0, "0", monkeypatch)
+
+
+def test_ddp_trainer_fp16_pipelined_window_matches_sequential_gpu():
+    """--mixed_precision fp16 runs the pipelined micro-step window and micro-step fusion
+    too (the window's backward seed carries the dynamic loss scale): same losses and
+    bit-identical parameters and loss scale as the sequential micro-step loop."""
+    from distributed_llm_trainer_amd.training.configs import TrainingConfig
+    from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
+    data = torch.randint(0, 1000, (8, 256), device=DEV, generator=torch.Generator(DEV).manual_seed(11))
+    res = []
+    for pipe in (False, True):
+        torch.manual_seed(3)
+        tc = TrainingConfig(batch_size=2, gradient_accumulation_steps=4, warmup_steps=1, learning_rate=1e-3,
+                            mixed_precision="fp16", pipeline_micro_steps=pipe)
+        tr = DistributedTrainer(_cfg(0.1), tc)
+        assert tr.dtype == torch.float16 and tr.loss_scale is not None
+        losses = [tr.train_step({"input_ids": data})["loss"] for _ in range(3)]
+        res.append((losses, tr.store.flat.detach().clone(), tr.loss_scale))
+    assert all(math.isfinite(x) for x in res[1][0])
+    assert res[0][0] == res[1][0], (res[0][0], res[1][0])
+    assert res[0][2] == res[1][2]
+    assert torch.equal(res[0][1], res[1][1]), (res[0][1] - res[1][1]).abs().max().item()
