@@ -55,6 +55,9 @@ def main():
     ap.add_argument("--memory_lean", action="store_true",
                     help="the trainer's --memory_lean (TrainingConfig.defer_roles='qkv,o'): gate/up, down "
                          "and lm_head weight gradients per chain, lower peak memory")
+    ap.add_argument("--defer_roles", default=None,
+                    help="DDP: TrainingConfig.defer_roles override ('none' = no weight gradient deferred to the "
+                         "window: per-chain weight gradients, no slot buffers)")
     ap.add_argument("--data", default="loader", choices=["loader", "resident"],
                     help="loader (default): every timed step takes a fresh batch from the native C++ loader "
                          "(dummy mode: uniform ids from a counter hash, pinned ring, H2D on a side stream), so "
@@ -90,7 +93,9 @@ def main():
         from distributed_llm_trainer_amd.training.ddp_trainer import LEAN_DEFER_ROLES, DistributedTrainer
         tc = TrainingConfig(batch_size=args.batch_size, gradient_accumulation_steps=args.grad_accum,
                             max_steps=100000, mixed_precision=args.precision, micro_step_fusion=args.fusion,
-                            defer_roles=LEAN_DEFER_ROLES if args.memory_lean else "all")
+                            defer_roles=(args.defer_roles if args.defer_roles not in (None, "none") else
+                                         LEAN_DEFER_ROLES if args.memory_lean else "all"),
+                            defer_wgrad=args.defer_roles != "none")
         trainer = DistributedTrainer(cfg, tc)
     else:
         from distributed_llm_trainer_amd.training.configs import FSDPConfig, FSDPTrainingConfig
@@ -165,6 +170,7 @@ def main():
                        "grad_accum": args.grad_accum,
                        "micro_step_fusion": trainer.fusion_factor(args.grad_accum, args.batch_size, args.seq_len),
                        **({"memory_lean": True} if args.memory_lean else {}),
+                       **({"defer_roles": args.defer_roles} if args.defer_roles else {}),
                        **({"cpu_offload": True} if args.cpu_offload else {})},
             "peak_gb_per_gpu": round(peak, 3), "final_loss": round(loss, 4),
             "vs_baseline_linear": None if overrides else round(tps / (12500.0 * world), 3),

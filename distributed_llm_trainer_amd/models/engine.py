@@ -193,7 +193,7 @@ class GPTEngine:
         # deferred weight gradients (see set_accumulation)
         self.acc_slot, self.acc_slots, self.defer = 0, 1, False
         # which weight gradients a deferred window defers (the others run per micro-step):
-        # all by default; the memory-lean mode keeps only the small-operand ones (qkv, o)
+        # all by default; the memory-lean mode defers none (per-chain weight gradients)
         self.defer_roles = frozenset(self.ROLES)
         self._slots = {}
         # dY-operand slot ring (ffbb window, see _window_ffbb): 0 = one slot per layer

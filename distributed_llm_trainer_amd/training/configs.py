@@ -47,7 +47,7 @@ class TrainingConfig:
     adam_eps: float = 1e-8
     defer_wgrad: bool = True           # one weight-grad GEMM per layer per optimizer step
     # which weight gradients defer_wgrad defers: "all", or a comma list of qkv / o / gu / down
-    # / head (the others run in each micro-step chain's backward); --memory_lean: "qkv,o"
+    # / head, or "none" (the others run in each micro-step chain's backward); --memory_lean: "none"
     defer_roles: str = "all"
     pipeline_micro_steps: bool = True  # overlap fwd(k+1) with bwd(k) on two HIP streams (engine path)
     # execute F consecutive micro-steps as one forward/backward chain of F*batch_size rows

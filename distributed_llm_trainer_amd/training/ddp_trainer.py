@@ -290,14 +290,20 @@ class DistributedTrainer:
 
 
 # --------------------------------------------------------------------------- CLI
-LEAN_DEFER_ROLES = "qkv,o"
+# --memory_lean: no weight gradient deferred to the window -- every chain runs its own
+# (no [GA*M, N] slot buffers), the lm_head in row chunks in the forwards: 11.9 GB at the
+# headline shape vs 14.9 GB deferring qkv / o ("qkv,o", the round-3 choice), -0.7 %
+# (profiles/r4_memory_lean.md)
+LEAN_DEFER_ROLES = "none"
 
 
 def parse_defer_roles(text: str) -> frozenset:
-    """TrainingConfig.defer_roles -> the engine's role set ("all" or a comma list)."""
+    """TrainingConfig.defer_roles -> the engine's role set ("all", "none" or a comma list)."""
     from ..models.engine import GPTEngine
     if text.strip() in ("", "all"):
         return frozenset(GPTEngine.ROLES)
+    if text.strip() == "none":
+        return frozenset()
     roles = frozenset(r.strip() for r in text.split(",") if r.strip())
     bad = roles - set(GPTEngine.ROLES)
     if bad:
@@ -333,9 +339,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--metrics_jsonl", type=str, default=None)
     p.add_argument("--no_final_save", action="store_true")
     p.add_argument("--memory_lean", action="store_true",
-                   help="defer only the small-operand weight gradients (qkv, o) to the end of the accumulation "
-                        "window; gate/up, down and lm_head run in each micro-step chain's own backward (no "
-                        "[GA*M, 2I] slot buffers, no window-wide dlogits): ~2/3 of the peak memory")
+                   help="no weight gradient deferred to the end of the accumulation window: every micro-step "
+                        "chain runs its own (no [GA*M, N] slot buffers, no window-wide dlogits; lm_head in row "
+                        "chunks): ~56 %% of the default peak memory at -3 %% tok/s")
     return p
 
 

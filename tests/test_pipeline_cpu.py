@@ -94,7 +94,8 @@ def test_trainer_memory_lean_matches_deferred(recompute):
     torch.manual_seed(14)
     data = torch.randint(0, 256, (8, 32))
     res = []
-    variants = [(True, "all"), (True, LEAN_DEFER_ROLES), (True, "gu,head"), (True, "down"), (False, "all")]
+    variants = [(True, "all"), (True, LEAN_DEFER_ROLES), (True, "qkv,o"), (True, "gu,head"), (True, "down"),
+                (False, "all")]
     for defer, roles in variants:
         tc = TrainingConfig(batch_size=2, gradient_accumulation_steps=4, warmup_steps=2, max_steps=10,
                             defer_wgrad=defer, defer_roles=roles)
@@ -107,6 +108,8 @@ def test_trainer_memory_lean_matches_deferred(recompute):
         if not defer:
             assert not slots  # nothing deferred, no slot buffers
         elif roles == LEAN_DEFER_ROLES:
+            assert not slots, slots  # --memory_lean defers nothing
+        elif roles == "qkv,o":
             assert slots == {"n1", "dqkv", "o", "da"}, slots
     for losses, flat in res[1:]:
         for a, b in zip(res[0][0], losses):
