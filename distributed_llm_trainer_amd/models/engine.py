@@ -199,11 +199,14 @@ class GPTEngine:
         # dY-operand slot ring (ffbb window, see _window_ffbb): 0 = one slot per layer
         self._ring = 0
         self._ring_done = {}
-        # with the dY ring on, the SwiGLU output s (the down projection's weight-gradient
-        # operand) joins it too: the backward's swiglu_bwd rewrites it (same bits) and the
-        # forward's copy is a temporary -- R slots instead of one [2M, I] slot per layer
-        # (-1.8 GB at the headline shape).  DLT_S_RING=0: per-layer s slots from the forward.
-        self.s_ring = os.environ.get("DLT_S_RING", "1") != "0"
+        # DLT_S_RING=1: with the dY ring on, the SwiGLU output s (the down projection's
+        # weight-gradient operand) joins it too -- the backward rewrites it (same bits; the
+        # fused down-dgrad epilogue's s_out) and the forward's copy is a temporary: R slots
+        # instead of one [2M, I] slot per layer, -1.8 GB at the headline shape.  Off by
+        # default since the SwiGLU backward moved into the down-dgrad GEMM epilogue, where
+        # the extra s stores cost the step 1.2-1.5 % (785.2k vs 797.1k tok/s, three same-box
+        # pairs; profiles/r4_memory_lean.md)
+        self.s_ring = os.environ.get("DLT_S_RING", "0") == "1"
         # lm_head + cross-entropy in row chunks (head_chunks > 0; 0 = the window's logits
         # stay resident for ONE lm_head weight-gradient GEMM over all its rows, on the
         # side stream during the backward).  Per micro-step, for each chunk of rows:

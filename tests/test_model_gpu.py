@@ -789,6 +789,7 @@ def test_window_ffbb_forced_fused_epilogues_match_sequential_gpu(monkeypatch):
     def forced(self, kind, x, w, fused, unfused, key=None):
         return self._hand_ok(x, w)
     monkeypatch.setattr(gemm_mod.HipGemm, "_fused_pick", forced)
+    monkeypatch.setenv("DLT_S_RING", "1")
     test_window_ffbb_hand_kernels_match_sequential_gpu("1", 0, "0", monkeypatch)
 
 

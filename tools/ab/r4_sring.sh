@@ -1,9 +1,11 @@
-# round 4: SwiGLU output in the dY slot ring (DLT_S_RING): correctness + memory / throughput A/B
+# round 4, end: SwiGLU output kept per layer from the forward (DLT_S_RING=0) vs rewritten into the ring by the
+# fused down-dgrad epilogue (default); with the fused epilogue off for comparison
 set -o pipefail
-cd $GRAFT_REPO_ROOT
+cd "${GRAFT_REPO_ROOT:-.}"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests/test_model_gpu.py tests/test_kernels_gpu.py -x -v --timeout 300 --timeout-method thread \
-  -k "ffbb or test_swiglu or precision or dswiglu" > gpurun_out/r4_sring_t.log 2>&1 || { tail -60 gpurun_out/r4_sring_t.log; exit 1; }
-grep -E 'PASS|FAIL|ERROR' gpurun_out/r4_sring_t.log | grep -v PASSED | tail; tail -2 gpurun_out/r4_sring_t.log
-REPS=2 STEPS=20 VARIANTS="sring:DLT_S_RING=1 nosring:DLT_S_RING=0 ring2:DLT_SLOT_RING=2" bash tools/ab/r3b_env_ab.sh
+run() { n=$1; shift; timeout -k 10 300 env "$@" python bench.py --steps 20 --warmup 3 > gpurun_out/sr_$n.log 2> gpurun_out/sr_$n.err || { tail -20 gpurun_out/sr_$n.err; exit 1; }; echo "$n $(grep -o '"value": [0-9.]*' gpurun_out/sr_$n.log) $(grep -o '"peak_gb_per_gpu": [0-9.]*' gpurun_out/sr_$n.log)"; }
+for rep in 1 2 3; do
+  run ring.$rep DLT_S_RING=1 && run noring.$rep DLT_S_RING=0 &&
+  run noring_nodsw.$rep DLT_S_RING=0 DLT_GEMM_PLAN=tools/ab/plan_nodsw.json || exit 1
+done
