@@ -31,6 +31,10 @@
 //
 // Requirements (launcher-checked): Nr % 128 == 0 (a last half tile when Nr % 256 == 128),
 // Nc % 192 == 0, T % 128 == 0, 16-byte aligned rows.
+//
+// HK: operand format, 0 = bf16, 1 = IEEE half (--mixed_precision fp16).  Staging and the
+// transposed reads move 16-bit words either way; only the MFMA differs
+// (v_mfma_f32_16x16x32_f16, same shape and rate).
 #include "common.h"
 
 // shared token-major staging / transposed-read helpers (also used by the dgrad form of
@@ -41,6 +45,15 @@
 // loop over K-tiles [kt0, kt0 + nk) (nk even >= 2), epilogue into dst (row stride ldd;
 // accumulate: dst += acc, else dst = acc).  Ends with every wave past its last LDS read,
 // so a workgroup may run segments back to back (stream-K).
+template <int HK>
+__device__ __forceinline__ floatx4_t gw_mfma(const bf16x8_t& a, const bf16x8_t& b, const floatx4_t& c) {
+  if constexpr (HK == 0) return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c, 0,
+                                                  0, 0);
+}
+
+template <int HK>
 __device__ __forceinline__ void gw_segment(bf16_t* lds, const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X,
                                            int r0, int c0, int kt0, int nk, bool half_tile, int ldy, int ldx,
                                            float* __restrict__ dst, int ldd, bool accumulate) {
@@ -163,8 +176,7 @@ __device__ __forceinline__ void gw_segment(bf16_t* lds, const bf16_t* __restrict
       for (int nt = 0; nt < 3; ++nt)
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt)
-          acc[qn * 3 + nt][qm * 2 + mt] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nt][s], fa[mt][s], acc[qn * 3 + nt][qm * 2 + mt], 0, 0, 0);
+          acc[qn * 3 + nt][qm * 2 + mt] = gw_mfma<HK>(fb[nt][s], fa[mt][s], acc[qn * 3 + nt][qm * 2 + mt]);
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -262,6 +274,7 @@ __device__ __forceinline__ void gw_segment(bf16_t* lds, const bf16_t* __restrict
   }
 }
 
+template <int HK>
 __global__ __launch_bounds__(512, 1) void k_gemm_wgrad(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X,
                                                        float* __restrict__ out, int T, int Nr, int Nc, int ldy,
                                                        int ldx, int splits, int accumulate) {
@@ -287,7 +300,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_wgrad(const bf16_t* __restrict_
   const int npair = T / (2 * GW_BK);
   const int p0 = (int)(((long)split * npair) / splits), p1 = (int)(((long)(split + 1) * npair) / splits);
   float* const dst = out + (accumulate ? 0 : (size_t)split * Nr * Nc) + (size_t)r0 * Nc + c0;
-  gw_segment(lds, dY, X, r0, c0, 2 * p0, 2 * (p1 - p0), half_tile, ldy, ldx, dst, Nc, accumulate != 0);
+  gw_segment<HK>(lds, dY, X, r0, c0, 2 * p0, 2 * (p1 - p0), half_tile, ldy, ldx, dst, Nc, accumulate != 0);
 }
 
 // ---------------------------------------------------------------- stream-K (round 3)
@@ -314,6 +327,7 @@ struct GwSk {
   }
 };
 
+template <int HK>
 __global__ __launch_bounds__(512, 1) void k_gemm_wgrad_sk(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X,
                                                           float* __restrict__ dW, float* __restrict__ part, int Nr,
                                                           int Nc, int ldy, int ldx, GwSk sk) {
@@ -333,7 +347,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_wgrad_sk(const bf16_t* __restri
     const bool whole = p0 == 0 && p1 == sk.npair;
     float* dst = whole ? dW + (size_t)r0 * Nc + c0
                        : part + (((size_t)c * sk.Gc + g) * sk.maxseg + (rt - rt_first)) * (256 * 192);
-    gw_segment(lds, dY, X, r0, c0, 2 * p0, 2 * (p1 - p0), r0 + 256 > Nr, ldy, ldx, dst, whole ? Nc : 192, whole);
+    gw_segment<HK>(lds, dY, X, r0, c0, 2 * p0, 2 * (p1 - p0), r0 + 256 > Nr, ldy, ldx, dst, whole ? Nc : 192, whole);
     i += p1 - p0;
   }
 }
@@ -397,13 +411,15 @@ DLT_API long dlt_gemm_wgrad_sk_scratch(int T, int Nr, int Nc, int Gc) {
 
 // dW[Nr, Nc] (fp32) += dY[T, Nr]^T . X[T, Nc], stream-K over Gc shares per column tile
 // (Gc <= 0: 256 / column tiles, one workgroup per CU); `part` holds
-// dlt_gemm_wgrad_sk_scratch() floats.  Deterministic (fixed-order fixup).
+// dlt_gemm_wgrad_sk_scratch() floats.  Deterministic (fixed-order fixup).  hk: operand
+// format (0 bf16, 1 fp16).
 DLT_API int dlt_gemm_wgrad_sk(const bf16_t* dY, const bf16_t* X, float* dW, float* part, int T, int Nr, int Nc,
-                              int ldy, int ldx, int Gc, hipStream_t st) {
+                              int ldy, int ldx, int Gc, int hk, hipStream_t st) {
   if (T <= 0 || T % 128 || Nr % 128 || Nc % 192 || (ldy | ldx) % 8 || !dW || !part) return -1;
   const GwSk sk = gw_sk_plan(T, Nr, Nc, Gc);
   const int ntc = Nc / 192;
-  k_gemm_wgrad_sk<<<((sk.Gc + 7) / 8) * 8 * ntc, 512, 0, st>>>(dY, X, dW, part, Nr, Nc, ldy, ldx, sk);
+  DLT_HK_DISPATCH(hk, k_gemm_wgrad_sk<HKC><<<((sk.Gc + 7) / 8) * 8 * ntc, 512, 0, st>>>(dY, X, dW, part, Nr, Nc, ldy,
+                                                                                      ldx, sk));
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   k_wgrad_sk_fix<<<dim3(GW_FIX_SPLIT, sk.nrt * ntc), 256, 0, st>>>(part, dW, Nr, Nc, sk);
@@ -412,13 +428,14 @@ DLT_API int dlt_gemm_wgrad_sk(const bf16_t* dY, const bf16_t* X, float* dW, floa
 
 // dW[Nr, Nc] (fp32) += dY[T, Nr]^T . X[T, Nc].  splits == 1: accumulated in place; splits
 // > 1: the fp32 partials go to `part` [splits, Nr, Nc] (the caller sums them into dW in a
-// fixed order).  Returns -1 (nothing launched) for shapes outside the tiling.
+// fixed order).  Returns -1 (nothing launched) for shapes outside the tiling.  hk:
+// operand format (0 bf16, 1 fp16).
 DLT_API int dlt_gemm_wgrad(const bf16_t* dY, const bf16_t* X, float* dW, float* part, int T, int Nr, int Nc, int ldy,
-                           int ldx, int splits, hipStream_t st) {
+                           int ldx, int splits, int hk, hipStream_t st) {
   if (T <= 0 || T % 128 || Nr % 128 || Nc % 192 || (ldy | ldx) % 8 || splits < 1 || splits > T / 128) return -1;
   if (splits > 1 && part == nullptr) return -1;
   const int units = ((Nr + 255) / 256) * splits;  // (row tile, split) pairs, padded to 8s
-  k_gemm_wgrad<<<((units + 7) / 8) * 8 * (Nc / 192), 512, 0, st>>>(dY, X, splits > 1 ? part : dW, T, Nr, Nc, ldy, ldx, splits,
-                                               splits > 1 ? 0 : 1);
+  DLT_HK_DISPATCH(hk, k_gemm_wgrad<HKC><<<((units + 7) / 8) * 8 * (Nc / 192), 512, 0, st>>>(
+                          dY, X, splits > 1 ? part : dW, T, Nr, Nc, ldy, ldx, splits, splits > 1 ? 0 : 1));
   DLT_CHECK_LAUNCH();
 }

@@ -303,6 +303,14 @@ class HipGemm:
         so a dtype check must precede every cached hand-written pick)."""
         return all(t.dtype == torch.bfloat16 and t.is_contiguous() for t in ts)
 
+    @staticmethod
+    def _wgrad_hand_ok(dy, x, to16: bool = False) -> bool:
+        """Operands the hand-written weight-gradient kernels take: bf16, or fp16 into an
+        fp32 accumulator (the kernels are instantiated for both operand formats; the
+        16-bit-output route sums its partials with a bf16-only kernel)."""
+        ok = dy.dtype == x.dtype and dy.is_contiguous() and x.is_contiguous()
+        return ok and (dy.dtype == torch.bfloat16 or (dy.dtype == torch.float16 and not to16))
+
     def _can_race(self, x, w) -> bool:
         return (self._race and x.is_contiguous() and w.is_contiguous() and x.dtype == torch.bfloat16
                 and w.dtype == torch.bfloat16 and not torch.cuda.is_current_stream_capturing())
@@ -544,8 +552,7 @@ class HipGemm:
         # library split-K: skinny outputs only (its [s, N, K] fp32 scratch)
         cands = [s for s in self.SPLITK_CANDIDATES if M % (s * 8) == 0 and (N * K) % 4 == 0
                  and N * K <= 4096 * 4096]
-        hand = (self._hand_wgrad and x.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16
-                and hip.wgrad_fits(M, N, K) and x.is_contiguous() and dy.is_contiguous())
+        hand = self._hand_wgrad and self._wgrad_hand_ok(dy, x, to_bf16) and hip.wgrad_fits(M, N, K)
         if hand:  # whole rounds of 256 workgroups, plus a few fixed depths (sweep in
             # profiles/r3_wgrad.md: the best split is shape-specific, 5..16 here); the
             # split partials ([s, N, K] fp32) stay under ~1 GB
@@ -584,11 +591,11 @@ class HipGemm:
         self._splitk[key] = choice
         return choice
 
-    def _resolve(self, s, dy, x):
+    def _resolve(self, s, dy, x, to16=False):
         """A recorded hand-written pick (-s) falls back to the library when the operands
         do not suit the kernel or DLT_WGRAD_HAND=0: split-K x s if the tokens divide,
         else the plain accumulate GEMM."""
-        if s < 0 and not (self._hand_wgrad and self._hand_ok(dy, x)):
+        if s < 0 and not (self._hand_wgrad and self._wgrad_hand_ok(dy, x, to16)):
             s = -s if self._splitk_on and -s in self.SPLITK_CANDIDATES and dy.shape[0] % (-s * 8) == 0 else 1
         return s
 
@@ -602,7 +609,7 @@ class HipGemm:
         dw2 = dw.view(N, K)
         if dw2.dtype not in (torch.bfloat16, torch.float16) or dw2.dtype != dy.dtype or not dw2.is_contiguous():
             raise ValueError("wgrad_set output must be contiguous bf16 / fp16 (the operands' dtype)")
-        s = self._resolve(self._pick_splitk(dw2, dy, x, to_bf16=True), dy, x)
+        s = self._resolve(self._pick_splitk(dw2, dy, x, to_bf16=True), dy, x, True)
         self._run_wgrad(dw2, dy, x, s, True)
 
     def wgrad_acc(self, dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:

@@ -55,9 +55,10 @@ _SIGS = {
                       c_float, c_float, c_float, c_void_p, c_void_p],
     "dlt_cast_bf16": [c_void_p, c_void_p, c_int64, c_int, c_void_p],
     "dlt_add_bf16_f32": [c_void_p, c_void_p, c_int64, c_int, c_void_p],
-    "dlt_gemm_wgrad": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "dlt_gemm_wgrad": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                       c_void_p],
     "dlt_gemm_wgrad_sk": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
-                          c_void_p],
+                          c_int, c_void_p],
     "dlt_scale_bf16": [c_void_p, c_void_p, ctypes.c_long, c_void_p, c_float, c_int, c_void_p],
     "dlt_gemm_bf16_tn": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "dlt_gemm_bf16_qkv_rope": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
@@ -689,8 +690,8 @@ def gemm_wgrad(dw: Optional[torch.Tensor], dy: torch.Tensor, x: torch.Tensor, sp
     (csrc/gemm_wgrad.hip).  splits == 0 picks the CU-filling split; with splits > 1 the
     fp32 partials go to `part` ([splits, Nr, Nc], allocated if None) and are summed into
     dw in fixed split order (deterministic).  dw = None with splits > 1: only the
-    partials are written (the caller reduces them, e.g. straight into bf16).  Returns
-    False (nothing launched) when the shape does not tile."""
+    partials are written (the caller reduces them, e.g. straight into bf16).  dy / x:
+    both bf16 or both fp16.  Returns False (nothing launched) when the shape does not tile."""
     T, Nr = dy.shape
     Nc = x.shape[1]
     if not wgrad_fits(T, Nr, Nc) or dy.stride(1) != 1 or x.stride(1) != 1 or dy.stride(0) % 8 or x.stride(0) % 8:
@@ -701,19 +702,23 @@ def gemm_wgrad(dw: Optional[torch.Tensor], dy: torch.Tensor, x: torch.Tensor, sp
             raise ValueError("gemm_wgrad: partials-only mode needs splits > 1 and an fp32 part buffer")
     else:
         _req(dw, torch.float32, "wgrad.dw", Nr * Nc)
-    if dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16 or x.shape[0] != T:
-        raise ValueError("gemm_wgrad: bf16 dy[T,Nr] / x[T,Nc] expected")
+    if dy.dtype not in _WG_HK or x.dtype != dy.dtype or x.shape[0] != T:
+        raise ValueError("gemm_wgrad: bf16 / fp16 dy[T,Nr] / x[T,Nc] of one dtype expected")
     if splits <= 0:
         splits = wgrad_splits(T, Nr, Nc)
     splits = min(splits, T // 128)
     if splits > 1 and (part is None or part.numel() < splits * Nr * Nc):
         part = torch.empty(splits * Nr * Nc, device=dw.device, dtype=torch.float32)
     _chk(lib().dlt_gemm_wgrad(_p(dy), _p(x), _p(dw) if dw is not None else None, _p(part) if splits > 1 else None,
-                              T, Nr, Nc, dy.stride(0), x.stride(0), splits, _stream()), "gemm_wgrad")
+                              T, Nr, Nc, dy.stride(0), x.stride(0), splits, _WG_HK[dy.dtype], _stream()),
+         "gemm_wgrad")
     if splits > 1 and dw is not None:
         _chk(lib().dlt_splitk_acc(_p(part), _p(dw), Nr * Nc, splits, _stream()), "splitk_acc")
     return True
 
+
+# operand format of the weight-gradient kernels (HK template parameter)
+_WG_HK = {torch.bfloat16: 0, torch.float16: 1}
 
 # DLT_WGRAD_SK_SHARES=n: n shares per column tile instead of 256 / column tiles (A/B knob)
 _SK_SHARES = int(os.environ.get("DLT_WGRAD_SK_SHARES", "0"))
@@ -732,13 +737,13 @@ def gemm_wgrad_sk(dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, shares: i
     if not wgrad_fits(T, Nr, Nc) or dy.stride(1) != 1 or x.stride(1) != 1 or dy.stride(0) % 8 or x.stride(0) % 8:
         return False
     _req(dw, torch.float32, "wgrad_sk.dw", Nr * Nc)
-    if dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16 or x.shape[0] != T:
-        raise ValueError("gemm_wgrad_sk: bf16 dy[T,Nr] / x[T,Nc] expected")
+    if dy.dtype not in _WG_HK or x.dtype != dy.dtype or x.shape[0] != T:
+        raise ValueError("gemm_wgrad_sk: bf16 / fp16 dy[T,Nr] / x[T,Nc] of one dtype expected")
     shares = shares or _SK_SHARES
     n = int(lib().dlt_gemm_wgrad_sk_scratch(T, Nr, Nc, shares))
     part = torch.empty(n, device=dw.device, dtype=torch.float32)
     _chk(lib().dlt_gemm_wgrad_sk(_p(dy), _p(x), _p(dw), _p(part), T, Nr, Nc, dy.stride(0), x.stride(0), shares,
-                                 _stream()), "gemm_wgrad_sk")
+                                 _WG_HK[dy.dtype], _stream()), "gemm_wgrad_sk")
     return True
 
 

@@ -467,6 +467,35 @@ def test_gemm_wgrad_stream_k(T, Nr, Nc, shares):
     assert not hip.gemm_wgrad_sk(base, dy[:, :64], x), "untileable shape must be refused"
 
 
+@pytest.mark.parametrize("T,Nr,Nc", [(2048, 768, 384), (4096, 2304, 768), (2048, 384, 192)])
+def test_gemm_wgrad_kernels_fp16(T, Nr, Nc):
+    """The weight-gradient kernels instantiated for IEEE-half operands
+    (v_mfma_f32_16x16x32_f16; --mixed_precision fp16): split-K, in-place and stream-K
+    forms vs the fp32 reference, and the planner's hand-written route for fp16 operands
+    into an fp32 accumulator."""
+    from distributed_llm_trainer_amd.ops import gemm
+    torch.manual_seed(6)
+    dy = torch.randn(T, Nr, device=DEV).half()
+    x = torch.randn(T, Nc, device=DEV).half()
+    base = torch.randn(Nr, Nc, device=DEV)
+    ref = base + dy.float().t() @ x.float()
+    for splits in (1, 3):
+        dw = base.clone()
+        assert hip.gemm_wgrad(dw, dy, x, splits)
+        _close(dw, ref, 1e-3 * T ** 0.5, 1e-4, f"fp16 wgrad splits={splits}")
+    dw = base.clone()
+    assert hip.gemm_wgrad_sk(dw, dy, x, 0)
+    _close(dw, ref, 1e-3 * T ** 0.5, 1e-4, "fp16 wgrad stream-K")
+    with pytest.raises(ValueError):
+        hip.gemm_wgrad(base.clone(), dy, x.bfloat16(), 1)  # mixed operand formats
+    g = gemm.HipGemm()
+    assert g._wgrad_hand_ok(dy, x) and not g._wgrad_hand_ok(dy, x, to16=True)
+    for s in (-1, -3, g.STREAMK):
+        dw = base.clone()
+        g._run_wgrad(dw, dy, x, s, False)
+        _close(dw, ref, 1e-3 * T ** 0.5, 1e-4, f"fp16 planner route {s}")
+
+
 def test_planner_stream_k_route():
     """The planner's stream-K pick (splitk value STREAMK) runs the stream-K kernel for an
     fp32 accumulator and falls back to the split kernel for a bf16 output."""

@@ -469,8 +469,8 @@ static int wgrad_main(std::vector<int> shp) {
     const size_t nscr = S < 0 ? (size_t)dlt_gemm_wgrad_sk_scratch(T, Nr, Nc, Gc) : (size_t)S * Nr * Nc;
     CK(hipMalloc(&part, nscr * 4));
     auto hand = [&]() {
-      if (S < 0) return dlt_gemm_wgrad_sk(dY, X, dW, part, T, Nr, Nc, Nr, Nc, Gc, st);
-      int rc = dlt_gemm_wgrad(dY, X, dW, part, T, Nr, Nc, Nr, Nc, S, st);
+      if (S < 0) return dlt_gemm_wgrad_sk(dY, X, dW, part, T, Nr, Nc, Nr, Nc, Gc, 0, st);
+      int rc = dlt_gemm_wgrad(dY, X, dW, part, T, Nr, Nc, Nr, Nc, S, 0, st);
       if (rc == 0 && S > 1) rc = dlt_splitk_acc(part, dW, (long)Nr * Nc, S, st);
       return rc;
     };
@@ -508,7 +508,7 @@ static int wgrad_main(std::vector<int> shp) {
       float* p2;
       CK(hipMalloc(&p2, (size_t)4 * Nr * Nc * 4));
       CK(hipMemsetAsync(dW2, 0, (size_t)Nr * Nc * 4, st));
-      if (dlt_gemm_wgrad(dY, X, dW2, p2, T, Nr, Nc, Nr, Nc, 4, st) || dlt_splitk_acc(p2, dW2, (long)Nr * Nc, 4, st)) return 1;
+      if (dlt_gemm_wgrad(dY, X, dW2, p2, T, Nr, Nc, Nr, Nc, 4, 0, st) || dlt_splitk_acc(p2, dW2, (long)Nr * Nc, 4, st)) return 1;
       CK(hipMemcpyAsync(split.data(), dW2, split.size() * 4, hipMemcpyDeviceToHost, st));
       CK(hipStreamSynchronize(st));
       CK(hipFree(p2));
