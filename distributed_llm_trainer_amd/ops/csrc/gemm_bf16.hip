@@ -146,6 +146,13 @@ typedef uint32_t gb_u32x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint2 gb_pack(const floatx4_t& v) {
   return __builtin_bit_cast(uint2, __builtin_convertvector(v, gb_bf16x4_t));
 }
+// the plain store epilogue's pack for IEEE-half output (HK = 1, --mixed_precision fp16)
+typedef _Float16 gb_f16x4_t __attribute__((ext_vector_type(4)));
+template <int HK>
+__device__ __forceinline__ uint2 gb_pack_hk(const floatx4_t& v) {
+  if constexpr (HK == 0) return gb_pack(v);
+  else return __builtin_bit_cast(uint2, __builtin_convertvector(v, gb_f16x4_t));
+}
 __device__ __forceinline__ void gb_unpack(uint2 p, float (&f)[4]) {
   f[0] = __uint_as_float(p.x << 16);
   f[1] = __uint_as_float(p.x & 0xffff0000u);
@@ -161,13 +168,15 @@ __device__ __forceinline__ void gb_unpack(uint2 p, float (&f)[4]) {
 // swizzle and read with ds_read_b64_tr_b16 (gemm_common.h, as k_gemm_wgrad reads its
 // token-major operands).  Same unit sizes and DMA counts per wave, so the 8-phase
 // schedule and its counted waits are unchanged.
-template <int BN, int EPI, bool BT = false>
+// HK: operand / output format, 0 = bf16, 1 = IEEE half (plain store epilogue only).
+template <int BN, int EPI, bool BT = false, int HK = 0>
 __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                       bf16_t* __restrict__ C, int M, int N, int K, int lda, int ldb,
                                                       int ldc, int flags, GbEpi ep) {
   static_assert(EPI == GB_EPI_STORE || BN == 192, "pair epilogues need the 192-column tile");
   static_assert(!BT || (BN == 192 && (EPI == GB_EPI_STORE || EPI == GB_EPI_SWIGLU_BWD)),
                 "the reduction-major B form is the 192-column data-gradient kernel");
+  static_assert(HK == 0 || EPI == GB_EPI_STORE, "the fused epilogues are bf16-only");
   using Cf = GbCfg<BN>;
   constexpr int TS = EPI == GB_EPI_SWIGLU ? 96 : BN;  // tile stride in B rows
   constexpr int NT = Cf::NT, NH = Cf::NH;
@@ -365,8 +374,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
       for (int nt = 0; nt < NH; ++nt)
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt)
-          acc[qn * NH + nt][qm * 2 + mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              fb[nt][s], fa[mt][s], acc[qn * NH + nt][qm * 2 + mt], 0, 0, 0);
+          acc[qn * NH + nt][qm * 2 + mt] = gw_mfma<HK>(fb[nt][s], fa[mt][s], acc[qn * NH + nt][qm * 2 + mt]);
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -550,7 +558,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
         const int row = m0 + wm * 64 + mt * 16 + l16;
         uint2 pk[NT];
 #pragma unroll
-        for (int t = 0; t < NT; ++t) pk[t] = gb_pack(acc[t][mt]);
+        for (int t = 0; t < NT; ++t) pk[t] = gb_pack_hk<HK>(acc[t][mt]);
         // staged (LDS-transposed) stores: flag 1024; always for SWIGLU (its two stores
         // per lane otherwise write 16 rows x 32 + 8 bytes each)
         const bool lt = EPI == GB_EPI_SWIGLU || (EPI != GB_EPI_SWIGLU_BWD && !BT && (flags & 1024));
@@ -773,13 +781,14 @@ DLT_API int dlt_gemm_bf16_qkv_rope(const bf16_t* A, const bf16_t* W, bf16_t* C, 
 
 // Data gradient dX[M, Nout] = dY[M, Nred] . W[Nred, Nout] with W read as stored (the
 // input gradients of every projection: q/k/v, o, gate/up, down and the tied lm_head).
+// hk: operand / output format (0 bf16, 1 fp16).
 DLT_API int dlt_gemm_bf16_nn(const bf16_t* dY, const bf16_t* W, bf16_t* dX, int M, int Nout, int Nred, int ldy,
-                             int ldw, int ldx, int flags, hipStream_t st) {
+                             int ldw, int ldx, int flags, int hk, hipStream_t st) {
   if (!gb_shape_ok(M, Nout, Nred, ldy, ldw, ldx) || Nout % 192) return -1;
   const int ntiles = (M / 256) * (Nout / 192);
   GbEpi ep{};
-  k_gemm_bf16<192, GB_EPI_STORE, true>
-      <<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(dY, W, dX, M, Nout, Nred, ldy, ldw, ldx, flags, ep);
+  DLT_HK_DISPATCH(hk, k_gemm_bf16<192, GB_EPI_STORE, true, HKC><<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(
+                          dY, W, dX, M, Nout, Nred, ldy, ldw, ldx, flags, ep));
   DLT_CHECK_LAUNCH();
 }
 

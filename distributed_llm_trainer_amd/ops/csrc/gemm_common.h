@@ -11,6 +11,16 @@ typedef __attribute__((address_space(3))) void* gw_lds_vptr_t;
 typedef short gw_sx8_t __attribute__((ext_vector_type(8)));
 typedef const __attribute__((address_space(1))) void* gw_gbl_cvptr_t;
 
+// 16x16x32 MFMA on 16-bit operand fragments: HK = 0 bf16, 1 IEEE half (same shape, rate
+// and fragment layout -- the staging and transposed reads move 16-bit words either way)
+template <int HK>
+__device__ __forceinline__ floatx4_t gw_mfma(const bf16x8_t& a, const bf16x8_t& b, const floatx4_t& c) {
+  if constexpr (HK == 0) return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c, 0,
+                                                  0, 0);
+}
+
 namespace {
 
 constexpr int GW_BK = 64;

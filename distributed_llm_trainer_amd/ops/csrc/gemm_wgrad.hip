@@ -46,14 +46,6 @@
 // accumulate: dst += acc, else dst = acc).  Ends with every wave past its last LDS read,
 // so a workgroup may run segments back to back (stream-K).
 template <int HK>
-__device__ __forceinline__ floatx4_t gw_mfma(const bf16x8_t& a, const bf16x8_t& b, const floatx4_t& c) {
-  if constexpr (HK == 0) return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-  else
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c, 0,
-                                                  0, 0);
-}
-
-template <int HK>
 __device__ __forceinline__ void gw_segment(bf16_t* lds, const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X,
                                            int r0, int c0, int kt0, int nk, bool half_tile, int ldy, int ldx,
                                            float* __restrict__ dst, int ldd, bool accumulate) {

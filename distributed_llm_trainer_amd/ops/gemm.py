@@ -304,6 +304,13 @@ class HipGemm:
         return all(t.dtype == torch.bfloat16 and t.is_contiguous() for t in ts)
 
     @staticmethod
+    def _hand16_ok(*ts) -> bool:
+        """Operands of the kernels instantiated for both 16-bit formats (the data-gradient
+        GEMM): all bf16 or all fp16, contiguous."""
+        return (ts[0].dtype in (torch.bfloat16, torch.float16)
+                and all(t.dtype == ts[0].dtype and t.is_contiguous() for t in ts))
+
+    @staticmethod
     def _wgrad_hand_ok(dy, x, to16: bool = False) -> bool:
         """Operands the hand-written weight-gradient kernels take: bf16, or fp16 into an
         fp32 accumulator (the kernels are instantiated for both operand formats; the
@@ -430,7 +437,7 @@ class HipGemm:
         M, N = dy.shape
         K = w.shape[1]
         dx = torch.empty(M, K, dtype=dy.dtype, device=dy.device) if out is None else out
-        ok = self._dgrad_on and self._race and hip.gemm_bf16_fits(M, K, N) and self._hand_ok(dy, w, dx)
+        ok = self._dgrad_on and self._race and hip.gemm_bf16_fits(M, K, N) and self._hand16_ok(dy, w, dx)
         if ok and self._fused_pick("dgrad", dy, w, lambda: hip.gemm_dgrad(dy, w, out=dx),
                                    lambda: self._lib_dgrad(dy, w, dx), key=("dgrad", M, K, N)):
             hip.gemm_dgrad(dy, w, out=dx)

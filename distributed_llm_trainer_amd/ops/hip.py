@@ -64,7 +64,8 @@ _SIGS = {
     "dlt_gemm_bf16_qkv_rope": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                                c_void_p],
     "dlt_gemm_bf16_gu_swiglu": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
-    "dlt_gemm_bf16_nn": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "dlt_gemm_bf16_nn": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                         c_void_p],
     "dlt_gemm_bf16_down_swiglu_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                       c_void_p],
     "dlt_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
@@ -840,18 +841,21 @@ def gemm_gu_swiglu(x: torch.Tensor, wgu: torch.Tensor, gu_out: Optional[torch.Te
 def gemm_dgrad(dy: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
     """dX[M, Nout] = dY[M, Nred] @ W[Nred, Nout] with W read as stored (the data gradient
     of a projection y = x @ W^T) by the hand-written persistent MFMA kernel in its
-    reduction-major-B form.  None (nothing launched) when the shape does not tile
-    (M % 256, Nout % 192, Nred % 128)."""
+    reduction-major-B form; bf16 or fp16 (all three tensors one dtype).  None (nothing
+    launched) when the shape does not tile (M % 256, Nout % 192, Nred % 128)."""
     M, Nred = dy.shape
     Nout = w.shape[1]
     if not gemm_bf16_fits(M, Nout, Nred) or w.shape[0] != Nred:
         return None
-    _req(dy, torch.bfloat16, "gemm_dgrad.dy")
-    _req(w, torch.bfloat16, "gemm_dgrad.w")
-    c = torch.empty(M, Nout, dtype=torch.bfloat16, device=dy.device) if out is None else out
-    _req(c, torch.bfloat16, "gemm_dgrad.out", M * Nout)
-    _chk(lib().dlt_gemm_bf16_nn(_p(dy), _p(w), _p(c), M, Nout, Nred, Nred, Nout, Nout, _GB_FLAGS, _stream()),
-         "gemm_dgrad")
+    dt = dy.dtype
+    if dt not in _WG_HK:
+        raise ValueError("gemm_dgrad: bf16 / fp16 operands expected")
+    _req(dy, dt, "gemm_dgrad.dy")
+    _req(w, dt, "gemm_dgrad.w")
+    c = torch.empty(M, Nout, dtype=dt, device=dy.device) if out is None else out
+    _req(c, dt, "gemm_dgrad.out", M * Nout)
+    _chk(lib().dlt_gemm_bf16_nn(_p(dy), _p(w), _p(c), M, Nout, Nred, Nred, Nout, Nout, _GB_FLAGS, _WG_HK[dt],
+                                _stream()), "gemm_dgrad")
     return c
 
 

@@ -618,6 +618,28 @@ def test_gemm_dgrad_vs_fp32(M, Nout, Nred):
     assert _relerr(r, want) < 8e-3, _relerr(r, want)
 
 
+@pytest.mark.parametrize("M,Nout,Nred", [(512, 768, 2304), (1024, 3072, 768), (512, 768, 50304)])
+def test_gemm_dgrad_fp16_vs_fp32(M, Nout, Nred):
+    """The data-gradient kernel instantiated for IEEE half (k_gemm_bf16<192, 0, true, 1>,
+    v_mfma_f32_16x16x32_f16, fp16 output) against the fp32 product, and the planner's
+    dgrad route for fp16 operands (hand-written when the shape is pinned or raced so)."""
+    from distributed_llm_trainer_amd.ops import gemm
+    torch.manual_seed(Nred + 1)
+    dy = (torch.rand(M, Nred, device=DEV) * 2 - 1).half()
+    w = ((torch.rand(Nred, Nout, device=DEV) * 2 - 1) / Nred ** 0.5).half()
+    r = hip.gemm_dgrad(dy, w)
+    assert r.dtype == torch.float16
+    want = dy.float() @ w.float()
+    assert torch.isfinite(r.float()).all()
+    assert _relerr(r, want) < 2e-3, _relerr(r, want)
+    g = gemm.HipGemm()
+    assert g._hand16_ok(dy, w, r) and not g._hand16_ok(dy, w.bfloat16(), r)
+    r2 = g.linear_dgrad(dy, w)
+    assert _relerr(r2, want) < 2e-3
+    with pytest.raises(ValueError):
+        hip.gemm_dgrad(dy.float(), w.float())
+
+
 def test_gemm_down_swiglu_bwd_vs_fp32():
     """Down-projection dgrad with the SwiGLU backward in the epilogue == the fp32 product
     rounded to bf16 (what the unfused dgrad writes) through k_swiglu_bwd's math, and ==

@@ -344,7 +344,7 @@ static int dgrad_main(std::vector<int> shp) {
     for (int v = 0; v < 3; ++v) {
       auto fn = [&]() {
         if (v == 2) return run_blas_nn(A, W, C, M, N, K, st);
-        return dlt_gemm_bf16_nn(A, W, C, M, N, K, K, N, N, v == 1 ? 1 : 0, st);
+        return dlt_gemm_bf16_nn(A, W, C, M, N, K, K, N, N, v == 1 ? 1 : 0, 0, st);
       };
       CK(hipMemsetAsync(C, 0xff, (size_t)M * N * 2, st));
       int rc = fn();
@@ -422,7 +422,7 @@ static int dgrad_main(std::vector<int> shp) {
       }
     const float tf = time_us(fused, st), tu = time_us(unfused, st);
     const float tb = time_us([&]() { return run_blas_nn(dd, Wd, ds, M, I, H, st); }, st);
-    const float th = time_us([&]() { return dlt_gemm_bf16_nn(dd, Wd, ds, M, I, H, H, I, I, 0, st); }, st);
+    const float th = time_us([&]() { return dlt_gemm_bf16_nn(dd, Wd, ds, M, I, H, H, I, I, 0, 0, st); }, st);
     printf("down dgrad + swiglu_bwd: fused %.1f us | hipBLASLt + k_swiglu_bwd %.1f us (dgrad alone %.1f, hand dgrad "
            "alone %.1f) | err %.1e\n",
            tf, tu, tb, th, mref > 0 ? e / mref : 0.0);
