@@ -19,6 +19,7 @@ REF = {("ddp", "small", 1): 12500, ("ddp", "small", 2): 24100, ("ddp", "small", 
 CONFIGS = {
     "ddp_small": ["--model_size", "small", "--batch_size", "8", "--grad_accum", "4"],
     "ddp_small_lean": ["--model_size", "small", "--batch_size", "8", "--grad_accum", "4", "--memory_lean"],
+    "ddp_small_fp16": ["--model_size", "small", "--batch_size", "8", "--grad_accum", "4", "--precision", "fp16"],
     "fsdp_small": ["--mode", "fsdp", "--model_size", "small", "--batch_size", "8", "--grad_accum", "4"],
     "ddp_medium": ["--model_size", "medium", "--batch_size", "4", "--grad_accum", "8"],
     "fsdp_medium": ["--mode", "fsdp", "--model_size", "medium", "--batch_size", "4", "--grad_accum", "8"],
