@@ -1,4 +1,4 @@
-# round 4, end: AdamW with 4 float4 groups per thread (DLT_ADAMW_U=4) vs 2 -- standalone, then the step
+# round 4, end: AdamW with 4 float4 groups per thread (DLT_ADAMW_U=4, a knob of the reverted variant; the shipped kernel ignores it) vs 2 -- standalone, then the step
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
