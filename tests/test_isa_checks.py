@@ -64,3 +64,39 @@ def test_attention_counted_lds_waits_have_no_smem_in_flight(tmp_path, kread_asm)
         assert asm.count("lgkmcnt(4)") > 0, "the asm K-row reads' counted wait is gone"
     assert counted > 0
     assert not bad, f"SMEM load inside a counted LDS wait window: {bad[:5]}"
+
+
+def _kernel_bodies(asm: str, pattern: str):
+    """name -> instruction lines of every kernel whose symbol matches ``pattern``."""
+    lines = asm.split("\n")
+    out = {}
+    for i, ln in enumerate(lines):
+        m = re.match(r"^(_Z\w+):", ln)
+        if m and re.search(pattern, m.group(1)):
+            j = i + 1
+            while j < len(lines) and not lines[j].startswith(".Lfunc_end"):
+                j += 1
+            out[m.group(1)] = [t.strip() for t in lines[i + 1:j] if t.startswith("\t")]
+    return out
+
+
+@pytest.mark.skipif(shutil.which("hipcc") is None and not os.path.exists("/opt/rocm/bin/hipcc"),
+                    reason="hipcc not available")
+@pytest.mark.parametrize("src,pattern", [("gemm_wgrad.hip", r"k_gemm_wgrad"),
+                                         ("gemm_bf16.hip", r"k_gemm_bf16ILi192ELi0ELb1ELi")])
+def test_gemm_operand_format_instantiations_use_their_mfma(tmp_path, src, pattern):
+    """The weight- and data-gradient GEMMs are instantiated per 16-bit operand format
+    (template HK: 0 = bf16, 1 = fp16).  Each instantiation must issue only its own MFMA
+    (v_mfma_f32_16x16x32_bf16 / _f16) -- a mix-up would run fp16 bits through the bf16
+    datapath (or the reverse) without any shape error."""
+    asm = _device_asm(os.path.join(kbuild.CSRC, src), tmp_path)
+    bodies = _kernel_bodies(asm, pattern)
+    hk = {k: re.search(r"[IE]Li([01])EEv", k).group(1) for k in bodies}  # the last template argument
+    assert set(hk.values()) == {"0", "1"}, sorted(bodies)
+    for name, ins in bodies.items():
+        fmt = "f16" if hk[name] == "1" else "bf16"
+        other = "bf16" if fmt == "f16" else "f16"
+        mf = [t for t in ins if t.startswith("v_mfma")]
+        assert mf, name
+        assert all(f"x32_{fmt} " in t for t in mf), (name, [t for t in mf if f"x32_{fmt} " not in t][:3])
+        assert not any(f"x32_{other} " in t for t in mf), name

@@ -218,3 +218,22 @@ def test_deferred_wgrad_matches_per_micro_step(recompute):
         (l2 / 3).backward()
     for (n, p1), (_, p2) in zip(m1.named_parameters(), m2.named_parameters()):
         assert torch.allclose(p1.grad, p2.grad, atol=1e-6, rtol=1e-4), n
+
+
+def test_gemm_planner_operand_format_gating():
+    """HipGemm routes a GEMM to a hand-written kernel only for operand formats that kernel
+    is instantiated for: weight gradients bf16, or fp16 into an fp32 accumulator (the
+    16-bit-output route sums with a bf16-only kernel); data gradients all-bf16 or all-fp16."""
+    import torch
+    from distributed_llm_trainer_amd.ops import gemm
+    g = gemm.HipGemm
+    h = torch.zeros(8, 8, dtype=torch.float16)
+    b = torch.zeros(8, 8, dtype=torch.bfloat16)
+    f = torch.zeros(8, 8)
+    assert g._wgrad_hand_ok(b, b) and g._wgrad_hand_ok(b, b, True)
+    assert g._wgrad_hand_ok(h, h) and not g._wgrad_hand_ok(h, h, True)
+    assert not g._wgrad_hand_ok(h, b) and not g._wgrad_hand_ok(f, f)
+    assert not g._wgrad_hand_ok(b.t(), b)  # non-contiguous
+    assert g._hand16_ok(b, b, b) and g._hand16_ok(h, h, h)
+    assert not g._hand16_ok(h, b, h) and not g._hand16_ok(f, f, f)
+    assert g._hand_ok(b, b) and not g._hand_ok(h, h)  # the fused epilogues stay bf16-only
