@@ -86,7 +86,8 @@ class DistributedTrainer:
         # reference ddp_trainer.py:129-152: bf16 autocast, fp16 autocast + GradScaler, or
         # fp32.  Here every mode runs the fused engine with fp32 master weights and a
         # compute-dtype shadow: bf16 and fp16 on the HIP kernels (fp16: the same kernels
-        # instantiated for IEEE half, hipBLASLt fp16 GEMMs, dynamic loss scaling -- 2^16,
+        # instantiated for IEEE half, the hand weight / data gradient GEMMs in fp16 and
+        # hipBLASLt fp16 forward GEMMs, dynamic loss scaling -- 2^16,
         # x0.5 and skip on inf/nan, x2 after 2000 good steps: GradScaler defaults); fp32
         # (the reference / debug mode) with PyTorch ops on the GPU + hipBLASLt GEMMs
         if cuda and mp == "bf16":

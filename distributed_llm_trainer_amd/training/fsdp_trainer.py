@@ -58,7 +58,7 @@ class FSDPTrainer:
         # bf16, bf16), fp16 -> all fp16, otherwise none).  Master shards are always fp32;
         # the gathered compute copy, the activations and the reduce-scatter wire take the
         # policy dtype.  bf16 and fp16 run the HIP kernels (fp16: IEEE-half instances,
-        # hipBLASLt fp16 GEMMs); fp32 (reference / debug mode) runs the same schedule with
+        # hand weight / data gradient GEMMs, hipBLASLt fp16 forwards); fp32 (reference / debug mode) runs the same schedule with
         # PyTorch ops on the GPU + hipBLASLt GEMMs (GPT.enable_engine).  fp16 adds a
         # dynamic loss scale the reference lacks (Q11): the global grad sumsq is
         # all-reduced anyway for clipping, so an inf/nan on ANY rank's shard skips the step
