@@ -853,8 +853,16 @@ class GPTEngine:
                 # i-1's dd (slot (i-1) % R); their previous occupants are layers i+R and
                 # i-1+R, whose window weight gradients were issued (side stream, in layer
                 # order) by the last backward before this block was issued
-                ev = self._ring_done.get(i - 1 + self._ring)
-                if ev is not None:
+                j = i - 1 + self._ring
+                if j < L and any(self._deferred(st, self._SLOT_ROLE[n]) for n in self._DY_SLOTS):
+                    # the window's last backward records it after issuing layer j's
+                    # weight gradients; B1 runs one block behind B0 and R >= 2, so it must
+                    # exist by now -- a missing event means the issue order changed and
+                    # this block would overwrite operands still being read
+                    ev = self._ring_done.get(j)
+                    if ev is None:
+                        raise RuntimeError(f"dY ring: layer {j}'s weight gradients not issued before layer {i} "
+                                           "reuses its slot (window issue order changed?)")
                     torch.cuda.current_stream().wait_event(ev)
             c = st.caches[i]
             if st.recompute:

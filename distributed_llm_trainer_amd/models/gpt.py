@@ -246,6 +246,9 @@ class GPT(nn.Module):
         With the engine enabled this uses the KV-cached decoder in
         ``eval/decode.py`` (one token per step instead of a full re-forward)."""
         self.eval()
+        flush = getattr(getattr(self.engine, "provider", None), "flush_pending", None)
+        if flush is not None:  # a recorded (lazy) optimizer step: the decoder reads every unit
+            flush()
         if self.engine is not None:
             from ..eval.decode import kv_cached_generate
             return kv_cached_generate(self, input_ids, max_new_tokens, temperature, top_k)

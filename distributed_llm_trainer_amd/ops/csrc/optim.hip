@@ -108,8 +108,10 @@ __device__ __forceinline__ uint16_t to_shadow(float x) {
   }
 }
 
-template <bool NTM, int OCC = 1, bool F16 = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void k_adamw(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+// ZG: the gradient is zeroed in the same pass (the lazy per-unit optimizer step of the
+// flat store: the next micro-steps accumulate into it right after; no separate memset)
+template <bool NTM, int OCC = 1, bool F16 = false, bool ZG = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void k_adamw(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                                                float* __restrict__ v, bf16_t* __restrict__ shadow, int64_t n, float lr,
                                                float b1, float b2, float eps, float wd, float step_size,
                                                float inv_bc2_sqrt, const float* __restrict__ gscale_ptr) {
@@ -146,16 +148,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
     const float4 g0 = ld4<NTM>(g, i), g1 = ld4<NTM>(g, j);
     const float4 m0 = ld4<NTM>(m, i), m1 = ld4<NTM>(m, j);
     const float4 v0 = ld4<NTM>(v, i), v1 = ld4<NTM>(v, j);
+    if constexpr (ZG) {
+      st4<NTM>(g, i, make_float4(0.f, 0.f, 0.f, 0.f));
+      st4<NTM>(g, j, make_float4(0.f, 0.f, 0.f, 0.f));
+    }
     upd(i, p0, g0, m0, v0);
     upd(j, p1, g1, m1, v1);
   }
-  if (i < n4)
-    upd(i, reinterpret_cast<const float4*>(p)[i], reinterpret_cast<const float4*>(g)[i],
-        reinterpret_cast<const float4*>(m)[i], reinterpret_cast<const float4*>(v)[i]);
+  if (i < n4) {
+    const float4 g0 = reinterpret_cast<const float4*>(g)[i];
+    if constexpr (ZG) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    upd(i, reinterpret_cast<const float4*>(p)[i], g0, reinterpret_cast<const float4*>(m)[i],
+        reinterpret_cast<const float4*>(v)[i]);
+  }
   if (blockIdx.x == 0) {
     for (int64_t i = (n4 << 2) + threadIdx.x; i < n; i += blockDim.x) {
       float pp = p[i], mm = m[i], vv = v[i];
-      adam_elem(pp, g[i] * gs, mm, vv, lr, b1, b2, eps, wd, step_size, inv_bc2_sqrt);
+      const float gi = g[i];
+      if constexpr (ZG) g[i] = 0.f;
+      adam_elem(pp, gi * gs, mm, vv, lr, b1, b2, eps, wd, step_size, inv_bc2_sqrt);
       p[i] = pp; m[i] = mm; v[i] = vv;
       if (shadow) shadow[i] = to_shadow<F16>(pp);
     }
@@ -189,7 +200,7 @@ DLT_API int dlt_clip_coef(const float* sumsq, float* out, float norm_mul, float 
   DLT_CHECK_LAUNCH();
 }
 
-DLT_API int dlt_adamw(float* p, const float* g, float* m, float* v, bf16_t* shadow, int64_t n, float lr, float b1,
+DLT_API int dlt_adamw(float* p, float* g, float* m, float* v, bf16_t* shadow, int64_t n, float lr, float b1,
                       float b2, float eps, float wd, float step_size, float inv_bc2_sqrt, const float* gscale,
                       hipStream_t st) {
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return -1;
@@ -219,13 +230,38 @@ DLT_API int dlt_adamw(float* p, const float* g, float* m, float* v, bf16_t* shad
 }
 
 // AdamW with an fp16 shadow (the engine's --mixed_precision fp16 weights)
-DLT_API int dlt_adamw_f16(float* p, const float* g, float* m, float* v, bf16_t* shadow, int64_t n, float lr, float b1,
+DLT_API int dlt_adamw_f16(float* p, float* g, float* m, float* v, bf16_t* shadow, int64_t n, float lr, float b1,
                           float b2, float eps, float wd, float step_size, float inv_bc2_sqrt, const float* gscale,
                           hipStream_t st) {
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return -1;
   if (shadow && ((uintptr_t)shadow & 7)) return -1;
   k_adamw<false, 1, true><<<flat_blocks(n), 256, 0, st>>>(p, g, m, v, shadow, n, lr, b1, b2, eps, wd, step_size,
                                                           inv_bc2_sqrt, gscale);
+  DLT_CHECK_LAUNCH();
+}
+
+// AdamW with options (flags): bit 0 = fp16 shadow (else bf16 or none), bit 1 = zero the
+// gradient in the same pass (the flat store's lazy per-unit step); bf16 runs the
+// production build (nontemporal, eight waves per SIMD: dlt_adamw's defaults)
+DLT_API int dlt_adamw_ex(float* p, float* g, float* m, float* v, bf16_t* shadow, int64_t n, float lr, float b1,
+                         float b2, float eps, float wd, float step_size, float inv_bc2_sqrt, const float* gscale,
+                         int flags, hipStream_t st) {
+  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return -1;
+  if (shadow && ((uintptr_t)shadow & 7)) return -1;
+  const bool f16 = flags & 1, zg = flags & 2;
+  const int nb = flat_blocks(n);
+  if (f16 && zg)
+    k_adamw<false, 1, true, true><<<nb, 256, 0, st>>>(p, g, m, v, shadow, n, lr, b1, b2, eps, wd, step_size,
+                                                      inv_bc2_sqrt, gscale);
+  else if (f16)
+    k_adamw<false, 1, true><<<nb, 256, 0, st>>>(p, g, m, v, shadow, n, lr, b1, b2, eps, wd, step_size,
+                                                inv_bc2_sqrt, gscale);
+  else if (zg)
+    k_adamw<true, 8, false, true><<<nb, 256, 0, st>>>(p, g, m, v, shadow, n, lr, b1, b2, eps, wd, step_size,
+                                                      inv_bc2_sqrt, gscale);
+  else
+    k_adamw<true, 8><<<nb, 256, 0, st>>>(p, g, m, v, shadow, n, lr, b1, b2, eps, wd, step_size, inv_bc2_sqrt,
+                                         gscale);
   DLT_CHECK_LAUNCH();
 }
 

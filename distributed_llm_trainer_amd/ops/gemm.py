@@ -137,9 +137,10 @@ def load_plan(path: str, shipped: bool = False) -> None:
 
 
 def _splitk_key(text: str):
-    """'MxNxK' -> (M, N, K); 'MxNxKxbf16' -> (M, N, K, 'bf16') (the bf16-output race)."""
+    """'MxNxK' -> (M, N, K); 'MxNxKxbf16' -> (M, N, K, 'bf16') (the 16-bit-output races,
+    'bf16' / 'fp16')."""
     parts = text.split("x")
-    return tuple(p if p == "bf16" else int(p) for p in parts)
+    return tuple(p if p in ("bf16", "fp16") else int(p) for p in parts)
 
 
 def export_plan() -> dict:
@@ -312,15 +313,15 @@ class HipGemm:
 
     @staticmethod
     def _wgrad_hand_ok(dy, x, to16: bool = False) -> bool:
-        """Operands the hand-written weight-gradient kernels take: bf16, or fp16 into an
-        fp32 accumulator (the kernels are instantiated for both operand formats; the
-        16-bit-output route sums its partials with a bf16-only kernel)."""
+        """Operands the hand-written weight-gradient kernels take: bf16 or fp16, one format
+        (the kernels are instantiated for both; the 16-bit-output route sums its fp32
+        partials into the operands' format with hip.splitk_sum_bf16, which takes both)."""
         ok = dy.dtype == x.dtype and dy.is_contiguous() and x.is_contiguous()
-        return ok and (dy.dtype == torch.bfloat16 or (dy.dtype == torch.float16 and not to16))
+        return ok and dy.dtype in (torch.bfloat16, torch.float16)
 
-    def _can_race(self, x, w) -> bool:
-        return (self._race and x.is_contiguous() and w.is_contiguous() and x.dtype == torch.bfloat16
-                and w.dtype == torch.bfloat16 and not torch.cuda.is_current_stream_capturing())
+    def _can_race(self, x, w, dtypes=(torch.bfloat16,)) -> bool:
+        return (self._race and x.is_contiguous() and w.is_contiguous() and x.dtype in dtypes
+                and w.dtype == x.dtype and not torch.cuda.is_current_stream_capturing())
 
     def _pick(self, x, w, y):
         from . import hip
@@ -353,13 +354,14 @@ class HipGemm:
         """Race a hand-written kernel (``fused``) against its library equivalent once
         per key; kinds "rope" / "swiglu" / "dswiglu" are fused epilogues
         (``DLT_GEMM_FUSED=0`` turns them off), "dgrad" the plain data-gradient GEMM."""
-        on = self._fuse if kind != "dgrad" else True
-        if not (on and self._hand_ok(x, w)):
+        plain = kind.startswith("dgrad")  # the data-gradient kernel (bf16 and fp16 instances)
+        on = self._fuse if not plain else True
+        if not (on and (self._hand16_ok(x, w) if plain else self._hand_ok(x, w))):
             return False
         key = key or (kind, x.shape[0], w.shape[0], x.shape[1])
         choice = self._choice.get(key)
         if choice is None:
-            if not self._can_race(x, w):
+            if not self._can_race(x, w, (torch.bfloat16, torch.float16) if plain else (torch.bfloat16,)):
                 return False  # not recorded: decided again when racing is possible
             choice = _time_of(fused, inner=3) < self.RACE_MARGIN * _time_of(unfused, inner=3)
             self._choice[key] = choice
@@ -414,10 +416,10 @@ class HipGemm:
         out = {f"M{k[0]}xN{k[1]}xK{k[2]}": ("hipBLASLt" if c is None else "hand-written gemm_bf16")
                for k, c in self._choice.items() if len(k) == 3}
         out.update({f"{k[0]} M{k[1]}xN{k[2]}xK{k[3]}": (("hand-written gemm_dgrad" if c else "hipBLASLt")
-                                                       if k[0] == "dgrad" else
+                                                       if k[0].startswith("dgrad") else
                                                        ("fused gemm_bf16" if c else "unfused (linear + kernel)"))
                     for k, c in self._choice.items() if len(k) == 4})
-        out.update({f"wgrad{' (bf16 out)' if len(key) == 4 else ''} M{key[0]}xN{key[1]}xK{key[2]}":
+        out.update({f"wgrad{f' ({key[3]} out)' if len(key) == 4 else ''} M{key[0]}xN{key[1]}xK{key[2]}":
                     ("hand-written gemm_wgrad stream-K" if s == self.STREAMK else
                      f"hand-written gemm_wgrad x{-s}" if s < 0 else
                      f"hipBLASLt split-K x{s}" if s > 1 else "hipBLASLt plain")
@@ -438,8 +440,11 @@ class HipGemm:
         K = w.shape[1]
         dx = torch.empty(M, K, dtype=dy.dtype, device=dy.device) if out is None else out
         ok = self._dgrad_on and self._race and hip.gemm_bf16_fits(M, K, N) and self._hand16_ok(dy, w, dx)
-        if ok and self._fused_pick("dgrad", dy, w, lambda: hip.gemm_dgrad(dy, w, out=dx),
-                                   lambda: self._lib_dgrad(dy, w, dx), key=("dgrad", M, K, N)):
+        # bf16 and fp16 race separately (kind "dgrad" / "dgrad16"): one format's pick must
+        # not decide the other's
+        kind = "dgrad" if dy.dtype == torch.bfloat16 else "dgrad16"
+        if ok and self._fused_pick(kind, dy, w, lambda: hip.gemm_dgrad(dy, w, out=dx),
+                                   lambda: self._lib_dgrad(dy, w, dx), key=(kind, M, K, N)):
             hip.gemm_dgrad(dy, w, out=dx)
         else:
             self._lib_dgrad(dy, w, dx)
@@ -466,7 +471,7 @@ class HipGemm:
 
         def fused():
             hip.gemm_down_swiglu_bwd(dd, wdown, gu, out=dgu, s_out=s_out)
-        ok = (self._dgrad_on and hip.gemm_bf16_fits(M, I, H) and tuple(gu.shape) == (M, 2 * I)
+        ok = (self._dgrad_on and self._race and hip.gemm_bf16_fits(M, I, H) and tuple(gu.shape) == (M, 2 * I)
               and self._hand_ok(gu, dgu) and (s_out is None or self._hand_ok(s_out)))
         if ok and self._fused_pick("dswiglu", dd, wdown, fused, unfused, key=("dswiglu", M, I, H)):
             fused()
@@ -553,7 +558,8 @@ class HipGemm:
         from . import hip
         M, N = dy.shape
         K = x.shape[1]
-        key = (M, N, K, "bf16") if to_bf16 else (M, N, K)
+        # 16-bit outputs race per format ("bf16" / "fp16" key suffix)
+        key = (M, N, K, "bf16" if dw2.dtype == torch.bfloat16 else "fp16") if to_bf16 else (M, N, K)
         if key in self._splitk:
             return self._splitk[key]
         # library split-K: skinny outputs only (its [s, N, K] fp32 scratch)

@@ -51,6 +51,8 @@ _SIGS = {
     "dlt_clip_coef": [c_void_p, c_void_p, c_float, c_float, c_float, c_void_p],
     "dlt_adamw": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float, c_float,
                   c_float, c_float, c_float, c_void_p, c_void_p],
+    "dlt_adamw_ex": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float, c_float,
+                     c_float, c_float, c_float, c_void_p, c_int, c_void_p],
     "dlt_adamw_f16": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float, c_float,
                       c_float, c_float, c_float, c_void_p, c_void_p],
     "dlt_cast_bf16": [c_void_p, c_void_p, c_int64, c_int, c_void_p],
@@ -643,7 +645,10 @@ def clip_coef(sumsq_t: torch.Tensor, out: torch.Tensor, norm_mul: float, max_nor
     _chk(lib().dlt_clip_coef(_p(sumsq_t), _p(out), norm_mul, max_norm, scale_mul, _stream()), "clip_coef")
 
 
-def adamw_flat(param, grad, exp_avg, exp_avg_sq, shadow, lr, beta1, beta2, eps, wd, step, gscale):
+def adamw_flat(param, grad, exp_avg, exp_avg_sq, shadow, lr, beta1, beta2, eps, wd, step, gscale,
+               zero_grad: bool = False):
+    """One fused AdamW pass over flat fp32 buffers (+ the 16-bit shadow); ``zero_grad``:
+    the gradient is zeroed in the same pass."""
     n = param.numel()
     for t, nm in ((param, "param"), (grad, "grad"), (exp_avg, "exp_avg"), (exp_avg_sq, "exp_avg_sq")):
         _req(t, torch.float32, "adamw." + nm, n)
@@ -651,7 +656,13 @@ def adamw_flat(param, grad, exp_avg, exp_avg_sq, shadow, lr, beta1, beta2, eps, 
         raise ValueError("adamw.shadow must be bf16 or fp16 of the same numel")
     bc1 = 1.0 - beta1 ** step
     bc2 = 1.0 - beta2 ** step
-    fn = lib().dlt_adamw_f16 if (shadow is not None and shadow.dtype == torch.float16) else lib().dlt_adamw
+    f16 = shadow is not None and shadow.dtype == torch.float16
+    if zero_grad:
+        _chk(lib().dlt_adamw_ex(_p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), _p(shadow), n, lr, beta1, beta2,
+                                eps, wd, lr / bc1, 1.0 / math.sqrt(bc2), _p(gscale), (1 if f16 else 0) | 2,
+                                _stream()), "adamw")
+        return
+    fn = lib().dlt_adamw_f16 if f16 else lib().dlt_adamw
     _chk(fn(_p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), _p(shadow), n, lr, beta1, beta2, eps, wd,
             lr / bc1, 1.0 / math.sqrt(bc2), _p(gscale), _stream()), "adamw")
 
@@ -761,6 +772,14 @@ def gemm_wgrad_sk(dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, shares: i
 _GB_DEFAULT_FLAGS = 2048 | 1024 | 12
 _GB_FLAGS = (int(os.environ.get("DLT_GEMM_FLAGS", str(_GB_DEFAULT_FLAGS))) & (256 | 1024 | 2048 | 12)) | \
     ((min(int(os.environ.get("DLT_GEMM_GRID", "0")), 2040) // 8) << 16)
+# extra flag bits for the FORWARD projection GEMMs only (plain / RoPE / SwiGLU epilogues):
+# DLT_GEMM_FWD_FLAGS=256 runs them one tile per workgroup (grid = tiles) while the data
+# gradients keep the persistent grid (A/B knob for the two-chain window)
+_GB_FWD_EXTRA = int(os.environ.get("DLT_GEMM_FWD_FLAGS", "0")) & 256
+
+
+def _fwd_flags() -> int:
+    return _GB_FLAGS | _GB_FWD_EXTRA
 
 
 def gemm_grid_cap(n: int) -> int:
@@ -791,7 +810,7 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = No
     _req(b, torch.bfloat16, "gemm_bf16.b")
     c = torch.empty(M, N, dtype=torch.bfloat16, device=a.device) if out is None else out
     _req(c, torch.bfloat16, "gemm_bf16.c", M * N)
-    _chk(lib().dlt_gemm_bf16_tn(_p(a), _p(b), _p(c), M, N, K, K, K, N, _GB_FLAGS, _stream()), "gemm_bf16")
+    _chk(lib().dlt_gemm_bf16_tn(_p(a), _p(b), _p(c), M, N, K, K, K, N, _fwd_flags(), _stream()), "gemm_bf16")
     return c
 
 
@@ -813,7 +832,7 @@ def gemm_qkv_rope(x: torch.Tensor, wqkv: torch.Tensor, S: int, cos: torch.Tensor
     _req(sin, torch.float32, "gemm_qkv_rope.sin", cos.numel())
     c = torch.empty(M, N, dtype=torch.bfloat16, device=x.device) if out is None else out
     _req(c, torch.bfloat16, "gemm_qkv_rope.out", M * N)
-    _chk(lib().dlt_gemm_bf16_qkv_rope(_p(x), _p(wqkv), _p(c), M, H, K, S, _p(cos), _p(sin), _GB_FLAGS, _stream()),
+    _chk(lib().dlt_gemm_bf16_qkv_rope(_p(x), _p(wqkv), _p(c), M, H, K, S, _p(cos), _p(sin), _fwd_flags(), _stream()),
          "gemm_qkv_rope")
     return c
 
@@ -834,7 +853,7 @@ def gemm_gu_swiglu(x: torch.Tensor, wgu: torch.Tensor, gu_out: Optional[torch.Te
     s = torch.empty(M, I, dtype=torch.bfloat16, device=x.device) if s_out is None else s_out
     _req(gu, torch.bfloat16, "gemm_gu_swiglu.gu", M * I2)
     _req(s, torch.bfloat16, "gemm_gu_swiglu.s", M * I)
-    _chk(lib().dlt_gemm_bf16_gu_swiglu(_p(x), _p(wgu), _p(gu), _p(s), M, I, K, _GB_FLAGS, _stream()), "gemm_gu_swiglu")
+    _chk(lib().dlt_gemm_bf16_gu_swiglu(_p(x), _p(wgu), _p(gu), _p(s), M, I, K, _fwd_flags(), _stream()), "gemm_gu_swiglu")
     return gu, s
 
 

@@ -112,6 +112,8 @@ class FlatParamStore(ParamProvider):
         else:
             self.shadow = self.flat.to(compute_dtype)
         self._build_views()
+        # readers of the module's state see the weights of the last optimizer step
+        model.register_state_dict_pre_hook(lambda *args, **kw: self.flush_pending())
 
     # ----------------------------------------------------------------- views
     def _build_views(self):
@@ -152,6 +154,34 @@ class FlatParamStore(ParamProvider):
         self._hgrads = HeadGrads(embed=self.grad[e.offset:e.offset + Vp * H].view(Vp, H),
                                  norm=vec(self.grad, "norm.weight"))
 
+    def unit_ranges(self) -> Dict[object, List[Tuple[int, int]]]:
+        """The flat ranges of each forward unit, in forward order: "head" (embedding / tied
+        lm_head + the final norm; the embedding is read first) and layer i (its weights and
+        its two norm weights).  Together they cover the buffer exactly once (the lazy
+        optimizer step updates one unit at a time, training/optim.py LazyStep)."""
+        lay, H = self.layout, self.cfg.hidden_size
+        bn = lay.by_name
+        fn = bn["norm.weight"]
+        units: Dict[object, List[Tuple[int, int]]] = {"head": [(lay.embed_offset, lay.decay_end),
+                                                               (fn.offset, fn.offset + fn.numel)]}
+        for i, (a, b) in enumerate(lay.layer_bounds):
+            n1 = bn[f"layers.{i}.input_layernorm.weight"]
+            n2 = bn[f"layers.{i}.post_attention_layernorm.weight"]
+            assert n2.offset == n1.offset + H
+            units[i] = [(a, b), (n1.offset, n2.offset + H)]
+        return units
+
+    # pending lazy optimizer step (training/optim.py LazyStep): each unit's update is
+    # launched by pre_forward(unit) of the next forward
+    pending = None
+
+    def flush_pending(self) -> None:
+        """Apply every not-yet-applied unit of a pending lazy optimizer step, ordered before
+        the current stream's later work (checkpoints, eval, state_dict readers)."""
+        if self.pending is not None:
+            self.pending.ensure_all()
+            self.pending = None
+
     def refresh_shadow(self) -> None:
         """Re-derive the bf16 shadow from the fp32 master (after load / external edits)."""
         if self.shadow is not self.flat:
@@ -190,6 +220,8 @@ class FlatParamStore(ParamProvider):
     hooks: Optional[object] = None
 
     def pre_forward(self, unit):
+        if self.pending is not None:
+            self.pending.ensure(unit)
         if self.hooks is not None:
             self.hooks.pre_forward(unit)
 

@@ -55,6 +55,12 @@ class TrainingConfig:
     # 0 = auto (GPU engine: largest F with F*batch_size*seq <= 16384 tokens and >= 2
     # chains left to pipeline), 1 = off
     micro_step_fusion: int = 0
+    # engine path: record the optimizer step and apply it unit by unit where the next
+    # forward first needs each unit ("inline": on that chain's stream; "stream": on a
+    # stream of its own; "off": the reference's end-of-step update, weights final when
+    # train_step returns).  Readers outside a forward flush it (save, state_dict, eval):
+    # DistributedTrainer.flush_optimizer.  See training/optim.py LazyStep.
+    lazy_optimizer: str = "inline"
 
 
 @dataclass

@@ -238,12 +238,20 @@ class DistributedTrainer:
                 self._good_steps += 1
                 if self._good_steps % 2000 == 0:
                     self.loss_scale *= 2.0
-        if not skip:
-            self.optimizer.step(scale)
-            if not self.use_engine:
-                self.store.refresh_shadow()
+        lazy = self._lazy_mode()
+        if not skip and lazy != "off":
+            # recorded, applied per unit by the next forward's pre_forward hooks (which
+            # also zero each unit's gradient): the update overlaps the next step's compute
+            if self.store.pending is not None and not self.store.pending.complete:
+                self.store.flush_pending()
+            self.store.pending = self.optimizer.step_lazy(scale, self.store.unit_ranges(), mode=lazy)
+        else:
+            if not skip:
+                self.optimizer.step(scale)
+                if not self.use_engine:
+                    self.store.refresh_shadow()
+            self.optimizer.zero_grad(set_to_none=True)
         self._last_norm = scale[0]
-        self.optimizer.zero_grad(set_to_none=True)
         self._grads_zeroed = True
         if not cfg.lr_schedule_fix:  # reference order: LR for the *next* step set after this one
             lr = self.get_lr(self.global_step)
@@ -260,8 +268,29 @@ class DistributedTrainer:
             out["loss_global"] = global_mean_loss(total, self.world_size)
         return out
 
+    def _lazy_mode(self) -> str:
+        """The optimizer-step mode of TrainingConfig.lazy_optimizer (engine path only;
+        DLT_LAZY_OPT overrides): "inline", "stream" or "off"."""
+        mode = os.environ.get("DLT_LAZY_OPT") or getattr(self.training_config, "lazy_optimizer", "inline")
+        mode = {"0": "off", "1": "inline", "": "off"}.get(str(mode), str(mode))
+        if mode not in ("inline", "stream", "off"):
+            raise ValueError(f"lazy_optimizer must be inline / stream / off, got {mode!r}")
+        return mode if self.use_engine else "off"
+
+    def flush_optimizer(self) -> None:
+        """Apply a recorded (lazy) optimizer step now: after this the parameters, the
+        16-bit shadow and the zeroed gradients are what the reference's end-of-step
+        ``optimizer.step(); zero_grad()`` leaves (``ddp_trainer.py:352-358``)."""
+        self.store.flush_pending()
+
+    def flat_params(self) -> torch.Tensor:
+        """The flat fp32 master weights after every recorded optimizer step is applied."""
+        self.flush_optimizer()
+        return self.store.flat
+
     # ------------------------------------------------------------ checkpoints
     def save_checkpoint(self, path: str):
+        self.flush_optimizer()
         if not self.is_main_process:
             return
         payload = {
@@ -275,6 +304,7 @@ class DistributedTrainer:
         ckpt.save_checkpoint(path, payload)
 
     def load_checkpoint(self, path: str):
+        self.flush_optimizer()
         c = ckpt.load_checkpoint(path, map_location="cpu")
         ckpt.load_model_state(self.model, c["model"])
         self.store.refresh_shadow()

@@ -85,16 +85,31 @@ class FlatAdamW:
         for (a, b, _), g in zip(self.regions, self.param_groups):
             if b <= a:
                 continue
-            lr, (b1, b2), eps, wd = g["lr"], g["betas"], g["eps"], g["weight_decay"]
-            if self.is_cuda:
-                from ..ops import hip
-                hip.adamw_flat(self.flat[a:b], self.grad[a:b], self.exp_avg[a:b], self.exp_avg_sq[a:b],
-                               None if self.shadow is None else self.shadow[a:b], lr, b1, b2, eps, wd,
-                               self.step_count, sc)
-            else:
-                ref.adamw_step(self.flat[a:b], self.grad[a:b], self.exp_avg[a:b], self.exp_avg_sq[a:b],
-                               None if self.shadow is None else self.shadow[a:b], lr, b1, b2, eps, wd,
-                               self.step_count, sc[1])
+            self._apply_range(a, b, (g["lr"], tuple(g["betas"]), g["eps"], g["weight_decay"]), self.step_count, sc,
+                              zero_grad=False)
+
+    def step_lazy(self, scale: Optional[torch.Tensor], units: Dict[object, List[Tuple[int, int]]],
+                  mode: str = "inline") -> "LazyStep":
+        """Record this step instead of running it: each unit's AdamW (and its gradient
+        zeroing) is launched when the unit is next needed -- the engine's pre_forward hook
+        of the next step (see :class:`LazyStep`).  Same per-element arithmetic, hyper-
+        parameters snapshotted now, so the weights come out bitwise as :meth:`step`'s."""
+        self.step_count += 1
+        return LazyStep(self, scale if scale is not None else self._ones, units, mode)
+
+    def _apply_range(self, a: int, b: int, hp, step: int, sc: torch.Tensor, zero_grad: bool) -> None:
+        """AdamW over flat[a:b] with one group's hyperparameters ``hp`` = (lr, (b1, b2), eps, wd)."""
+        lr, (b1, b2), eps, wd = hp
+        sh = None if self.shadow is None else self.shadow[a:b]
+        if self.is_cuda:
+            from ..ops import hip
+            hip.adamw_flat(self.flat[a:b], self.grad[a:b], self.exp_avg[a:b], self.exp_avg_sq[a:b], sh, lr, b1, b2,
+                           eps, wd, step, sc, zero_grad=zero_grad)
+        else:
+            ref.adamw_step(self.flat[a:b], self.grad[a:b], self.exp_avg[a:b], self.exp_avg_sq[a:b], sh, lr, b1, b2,
+                           eps, wd, step, sc[1])
+            if zero_grad:
+                self.grad[a:b].zero_()
 
     def zero_grad(self, set_to_none: bool = True) -> None:
         # grads are persistent flat views; "set_to_none" semantics = zero the buffer
@@ -138,6 +153,95 @@ class FlatAdamW:
                     steps.append(int(stp.item() if torch.is_tensor(stp) else stp))
         if steps:
             self.step_count = max(steps)
+
+
+class LazyStep:
+    """A recorded optimizer step, applied unit by unit where the next forward needs it.
+
+    The reference steps every parameter at the end of the step (``ddp_trainer.py:352-356``),
+    a memory-bound pass with nothing to overlap (1.03 ms of a 41 ms step alone on the
+    GPU, profiles/r4_step_breakdown_final.md).  Here the trainer records the step (clip
+    scale, lr, betas, eps, wd, step count) and the flat store's ``pre_forward(unit)`` hook
+    launches that unit's AdamW -- which also zeroes its gradient -- right before the
+    unit's first use in the next forward:
+
+    * ``inline``: on the stream of the first chain that reaches the unit; the other
+      chain's stream waits for an event.  In the two-chain ``ffbb`` window a unit's
+      update runs beside the other chain's previous layer.
+    * ``stream``: every unit is issued at once, in forward order, on a stream of its own
+      (one event per unit), so the updates run ahead beside the forward of both chains.
+
+    Anything that reads the weights outside a training forward (checkpoint save, eval,
+    decode, ``state_dict``) calls :meth:`ensure_all` first (the trainer does; the store's
+    ``flush_pending``).  Units are disjoint flat ranges (:meth:`FlatParamStore.unit_ranges`).
+    """
+
+    def __init__(self, opt: FlatAdamW, scale: torch.Tensor, units: Dict[object, List[Tuple[int, int]]], mode: str):
+        self.opt = opt
+        self.step = opt.step_count
+        self.scale = scale.detach().clone()  # the next step's compute_scale reuses the buffer
+        self.hp = [(g["lr"], tuple(g["betas"]), g["eps"], g["weight_decay"]) for g in opt.param_groups]
+        self.units = {u: list(r) for u, r in units.items()}
+        self.mode = mode if opt.is_cuda else "inline"
+        self.events: Dict[object, object] = {}
+        self.done = set()
+        self._stream = None
+        covered = sorted(x for r in self.units.values() for x in r)
+        pos = 0
+        for a, b in covered:
+            if a != pos:
+                raise ValueError(f"lazy optimizer units leave [{pos}, {a}) of the flat buffer uncovered")
+            pos = b
+        if pos != opt.flat.numel():
+            raise ValueError("lazy optimizer units do not cover the flat buffer")
+
+    def _launch(self, unit) -> None:
+        for (a, b) in self.units[unit]:
+            for (ra, rb, _), hp in zip(self.opt.regions, self.hp):
+                lo, hi = max(a, ra), min(b, rb)
+                if hi > lo:
+                    self.opt._apply_range(lo, hi, hp, self.step, self.scale, zero_grad=True)
+        self.done.add(unit)
+
+    def _issue_all_on_stream(self) -> None:
+        cur = torch.cuda.current_stream()
+        if self._stream is None:
+            self._stream = torch.cuda.Stream(cur.device)
+        self._stream.wait_stream(cur)  # after the step's clip scale and the gradient all-reduces
+        with torch.cuda.stream(self._stream):
+            for u in self.units:
+                self._launch(u)
+                ev = torch.cuda.Event()
+                ev.record()
+                self.events[u] = ev
+
+    def ensure(self, unit) -> None:
+        """Make ``unit``'s update visible to the current stream (launching it if needed)."""
+        if unit not in self.units:
+            return
+        if self.mode == "stream":
+            if not self.events:
+                self._issue_all_on_stream()
+            torch.cuda.current_stream().wait_event(self.events[unit])
+            return
+        if unit in self.done:
+            ev = self.events.get(unit)
+            if ev is not None:
+                torch.cuda.current_stream().wait_event(ev)
+            return
+        self._launch(unit)
+        if self.opt.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+            self.events[unit] = ev
+
+    def ensure_all(self) -> None:
+        for u in self.units:
+            self.ensure(u)
+
+    @property
+    def complete(self) -> bool:
+        return len(self.done) == len(self.units)
 
 
 def flat_store_optimizer(store, lr: float, betas, eps: float, weight_decay: float,

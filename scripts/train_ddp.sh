@@ -11,7 +11,8 @@ if [ -z "${HIP_VISIBLE_DEVICES:-}" ]; then
   export HIP_VISIBLE_DEVICES=$(seq -s, 0 $((NUM_GPUS - 1)))
 fi
 echo "Training GPT-2 ${MODEL_SIZE} with DDP on ${NUM_GPUS} MI355X GPU(s) (HIP_VISIBLE_DEVICES=${HIP_VISIBLE_DEVICES})"
-python3 -m distributed_llm_trainer_amd.ops.build
+maybe_build
 python3 -m torch.distributed.run --standalone --local-addr 127.0.0.1 --nproc_per_node="${NUM_GPUS}" \
   src/training/ddp_trainer.py --model_size "${MODEL_SIZE}" --batch_size 8 --max_steps 1000 \
   --mixed_precision bf16 "$@"
+echo "Training complete!"

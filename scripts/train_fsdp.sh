@@ -11,7 +11,8 @@ if [ -z "${HIP_VISIBLE_DEVICES:-}" ]; then
   export HIP_VISIBLE_DEVICES=$(seq -s, 0 $((NUM_GPUS - 1)))
 fi
 echo "Training GPT-2 ${MODEL_SIZE} with FSDP on ${NUM_GPUS} MI355X GPU(s)"
-python3 -m distributed_llm_trainer_amd.ops.build
+maybe_build
 python3 -m torch.distributed.run --standalone --local-addr 127.0.0.1 --nproc_per_node="${NUM_GPUS}" \
   src/training/fsdp_trainer.py --model_size "${MODEL_SIZE}" --batch_size 4 --max_steps 1000 \
   --sharding FULL_SHARD "$@"
+echo "Training complete!"

@@ -30,7 +30,7 @@ def _ddp_worker(rank, world, steps, bucket_mb, fusion=1, GA=2):
     losses = []
     for s in range(steps):
         losses.append(tr.train_step({"input_ids": _data(s, rank, n=2 * GA)})["loss"])
-    return tr.store.flat.clone(), losses, len(tr.ddp.buckets)
+    return tr.flat_params().clone(), losses, len(tr.ddp.buckets)
 
 
 def _single_worker_equiv(steps, world, GA=2):
@@ -45,7 +45,7 @@ def _single_worker_equiv(steps, world, GA=2):
     for s in range(steps):
         batch = torch.cat([_data(s, r, n=2 * GA) for r in range(world)], dim=0)
         tr.train_step({"input_ids": batch})
-    return tr.store.flat.clone()
+    return tr.flat_params().clone()
 
 
 @pytest.mark.parametrize("bucket_mb", [0.05, 64.0])
@@ -331,7 +331,7 @@ def _forced_worker(rank, world, mode, strategy="FULL_SHARD"):
     for s in range(2):
         tr.train_step({"input_ids": _data(s, 0, n=8)})
     launched = tr.ddp.launched if mode == "ddp" else 0
-    sd = tr._full_state() if mode != "ddp" else {"flat": tr.store.flat.detach().cpu().clone()}
+    sd = tr._full_state() if mode != "ddp" else {"flat": tr.flat_params().detach().cpu().clone()}
     return {k: v.detach().float().cpu() for k, v in sd.items() if "rotary" not in k}, launched
 
 

@@ -45,14 +45,14 @@ def _ddp(rank, world, single):
                         max_steps=100, learning_rate=1e-3, bucket_cap_mb=1.0)
     tr = DistributedTrainer(GPTConfig(**TINY), tc)
     assert tr.use_engine and (tr.device.type == "cuda" or _cpu_dry_run())
-    init = tr.store.flat.detach().float().cpu().clone()
+    init = tr.flat_params().detach().float().cpu().clone()
     norms = []
     for s in range(STEPS):
         batch = torch.cat([_data(s, r) for r in range(world)]) if single else _data(s, rank)
         tr.train_step({"input_ids": batch})
         norms.append(float(tr._last_norm))
     nb = len(tr.ddp.buckets) if tr.ddp is not None else 0
-    return init, tr.store.flat.detach().float().cpu().clone(), norms, nb
+    return init, tr.flat_params().detach().float().cpu().clone(), norms, nb
 
 
 def _fsdp(rank, world, single, strategy):
@@ -127,7 +127,7 @@ def _forced(rank, world, mode):
             g = torch.Generator().manual_seed(77 + s)
             tr.train_step({"input_ids": torch.randint(0, HANDCFG["vocab_size"], (4, 256), generator=g)})
         rep = gemm.race_report()
-        return {"flat": tr.store.flat.detach().float().cpu().clone()}, (tr.ddp.launched, rep)
+        return {"flat": tr.flat_params().detach().float().cpu().clone()}, (tr.ddp.launched, rep)
     if mode.startswith("ddp"):
         from distributed_llm_trainer_amd.training.configs import TrainingConfig
         from distributed_llm_trainer_amd.training.ddp_trainer import LEAN_DEFER_ROLES, DistributedTrainer
@@ -145,7 +145,7 @@ def _forced(rank, world, mode):
     for s in range(STEPS):
         tr.train_step({"input_ids": torch.cat([_data(s, 0), _data(s, 1)])})
     launched = tr.ddp.launched if mode.startswith("ddp") else -1
-    sd = tr._full_state() if mode == "fsdp" else {"flat": tr.store.flat}
+    sd = tr._full_state() if mode == "fsdp" else {"flat": tr.flat_params()}
     return {k: v.detach().float().cpu().clone() for k, v in sd.items() if "rotary" not in k}, launched
 
 

@@ -222,8 +222,9 @@ def test_deferred_wgrad_matches_per_micro_step(recompute):
 
 def test_gemm_planner_operand_format_gating():
     """HipGemm routes a GEMM to a hand-written kernel only for operand formats that kernel
-    is instantiated for: weight gradients bf16, or fp16 into an fp32 accumulator (the
-    16-bit-output route sums with a bf16-only kernel); data gradients all-bf16 or all-fp16."""
+    is instantiated for: weight gradients bf16 or fp16 (fp32 accumulator or a 16-bit output
+    of the operands' format: splitk_sum_bf16 takes both); data gradients all-bf16 or
+    all-fp16."""
     import torch
     from distributed_llm_trainer_amd.ops import gemm
     g = gemm.HipGemm
@@ -231,9 +232,38 @@ def test_gemm_planner_operand_format_gating():
     b = torch.zeros(8, 8, dtype=torch.bfloat16)
     f = torch.zeros(8, 8)
     assert g._wgrad_hand_ok(b, b) and g._wgrad_hand_ok(b, b, True)
-    assert g._wgrad_hand_ok(h, h) and not g._wgrad_hand_ok(h, h, True)
+    assert g._wgrad_hand_ok(h, h) and g._wgrad_hand_ok(h, h, True)
     assert not g._wgrad_hand_ok(h, b) and not g._wgrad_hand_ok(f, f)
     assert not g._wgrad_hand_ok(b.t(), b)  # non-contiguous
     assert g._hand16_ok(b, b, b) and g._hand16_ok(h, h, h)
     assert not g._hand16_ok(h, b, h) and not g._hand16_ok(f, f, f)
     assert g._hand_ok(b, b) and not g._hand_ok(h, h)  # the fused epilogues stay bf16-only
+
+
+def test_gemm_planner_routes_fp16_dgrad_to_the_hand_kernel(monkeypatch):
+    """The fp16 data gradient races (and, when faster, runs) the hand-written kernel under
+    its own plan key "dgrad16", separate from the bf16 pick (round-4 advisor finding: the
+    bf16-only race gate sent every fp16 dgrad to hipBLASLt)."""
+    import torch
+    from distributed_llm_trainer_amd.ops import gemm, hip
+    g = object.__new__(gemm.HipGemm)
+    g._choice, g._splitk = {}, {}
+    g._race = g._fuse = g._dgrad_on = g._hand_wgrad = g._splitk_on = True
+    calls = []
+    monkeypatch.setattr(hip, "gemm_bf16_fits", lambda M, N, K: True)
+    monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: False)
+    monkeypatch.setattr(hip, "gemm_dgrad", lambda dy, w, out=None: calls.append(("hand", dy.dtype)) or out)
+    monkeypatch.setattr(gemm.HipGemm, "_lib_dgrad", lambda self, dy, w, dx: calls.append(("lib", dy.dtype)))
+    times = iter([1.0, 2.0, 2.0, 1.0])  # fp16: hand faster; bf16: library faster
+    monkeypatch.setattr(gemm, "_time_of", lambda fn, reps=3, inner=5: next(times))
+    for dt in (torch.float16, torch.bfloat16):
+        dy = torch.zeros(256, 128, dtype=dt)
+        w = torch.zeros(128, 192, dtype=dt)
+        calls.clear()
+        g.linear_dgrad(dy, w)
+        assert calls == ([("hand", dt)] if dt == torch.float16 else [("lib", dt)]), (dt, calls)
+    assert g._choice == {("dgrad16", 256, 192, 128): True, ("dgrad", 256, 192, 128): False}
+    # pinned choices replay without racing; an fp16 pick never decides the bf16 route
+    calls.clear()
+    g.linear_dgrad(torch.zeros(256, 128, dtype=torch.float16), torch.zeros(128, 192, dtype=torch.float16))
+    assert calls == [("hand", torch.float16)]

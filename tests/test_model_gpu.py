@@ -413,9 +413,35 @@ def test_training_is_bitwise_reproducible():
         tr = DistributedTrainer(_cfg(0.1), tc)
         assert tr.use_engine
         losses = [tr.train_step({"input_ids": data})["loss"] for _ in range(3)]
-        res.append((losses, tr.store.flat.detach().clone()))
+        res.append((losses, tr.flat_params().detach().clone()))
     assert res[0][0] == res[1][0], (res[0][0], res[1][0])
     assert torch.equal(res[0][1], res[1][1]), (res[0][1] - res[1][1]).abs().max().item()
+
+
+@pytest.mark.parametrize("fusion", [0, 1])
+def test_lazy_optimizer_modes_bitwise_gpu(fusion):
+    """The recorded optimizer step applied per unit in the next forward -- on the first
+    chain's stream ("inline") or on a stream of its own ("stream") -- trains bitwise like
+    the end-of-step update ("off"), in the two-chain ffbb window (fusion 0: 2 chains of 2
+    micro-steps) and the GA-4 fb window (fusion 1), dropout on."""
+    from distributed_llm_trainer_amd.training.configs import TrainingConfig
+    from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
+    data = [torch.randint(0, 1000, (8, 256), device=DEV, generator=torch.Generator(DEV).manual_seed(9 + s))
+            for s in range(4)]
+    res = []
+    for mode in ("off", "inline", "stream"):
+        torch.manual_seed(3)
+        tc = TrainingConfig(batch_size=2, gradient_accumulation_steps=4, warmup_steps=1, learning_rate=1e-3,
+                            micro_step_fusion=fusion, lazy_optimizer=mode)
+        tr = DistributedTrainer(_cfg(0.1), tc)
+        losses = [tr.train_step({"input_ids": d})["loss"] for d in data]
+        res.append((losses, tr.flat_params().detach().clone(), tr.optimizer.exp_avg_sq.detach().clone(),
+                    float(tr.store.grad.abs().max())))
+    for losses, flat, v, gmax in res[1:]:
+        assert losses == res[0][0], (res[0][0], losses)
+        assert torch.equal(flat, res[0][1]), (flat - res[0][1]).abs().max().item()
+        assert torch.equal(v, res[0][2])
+        assert gmax == 0.0
 
 
 def test_memory_lean_deferral_matches_default_gpu():
@@ -432,7 +458,7 @@ def test_memory_lean_deferral_matches_default_gpu():
                             defer_wgrad=defer, defer_roles=roles)
         tr = DistributedTrainer(_cfg(0.1), tc)
         losses = [tr.train_step({"input_ids": data})["loss"] for _ in range(3)]
-        res.append((losses, tr.store.flat.detach().clone()))
+        res.append((losses, tr.flat_params().detach().clone()))
     for losses, flat in res[1:]:
         assert all(abs(a - b) < 2e-3 for a, b in zip(res[0][0], losses)), (res[0][0], losses)
         # AdamW normalises each update, so elements with near-zero gradients can differ by
@@ -470,7 +496,7 @@ def test_checkpoint_resume_is_exact_gpu(tmp_path):
     c.load_checkpoint(path)
     lb += [c.train_step({"input_ids": data[s]})["loss"] for s in range(2, 4)]
     assert la == lb, (la, lb)
-    assert torch.equal(a.store.flat, c.store.flat), (a.store.flat - c.store.flat).abs().max().item()
+    assert torch.equal(a.flat_params(), c.flat_params()), (a.flat_params() - c.flat_params()).abs().max().item()
 
 
 def _fsdp_run(strategy="FULL_SHARD", offload=False, steps=3):
@@ -808,7 +834,7 @@ def test_ddp_trainer_fp16_pipelined_window_matches_sequential_gpu():
         tr = DistributedTrainer(_cfg(0.1), tc)
         assert tr.dtype == torch.float16 and tr.loss_scale is not None
         losses = [tr.train_step({"input_ids": data})["loss"] for _ in range(3)]
-        res.append((losses, tr.store.flat.detach().clone(), tr.loss_scale))
+        res.append((losses, tr.flat_params().detach().clone(), tr.loss_scale))
     assert all(math.isfinite(x) for x in res[1][0])
     assert res[0][0] == res[1][0], (res[0][0], res[1][0])
     assert res[0][2] == res[1][2]

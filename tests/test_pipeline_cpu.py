@@ -78,7 +78,7 @@ def test_trainer_pipelined_step_matches_sequential():
                             pipeline_micro_steps=pipe)
         tr = DistributedTrainer(tiny(), tc)
         losses = [tr.train_step({"input_ids": data})["loss"] for _ in range(3)]
-        res.append((losses, tr.store.flat.clone()))
+        res.append((losses, tr.flat_params().clone()))
     assert res[0][0] == res[1][0]
     assert torch.allclose(res[0][1], res[1][1], atol=1e-7, rtol=1e-6)
 
@@ -103,7 +103,7 @@ def test_trainer_memory_lean_matches_deferred(recompute):
         cfg.gradient_checkpointing = recompute
         tr = DistributedTrainer(cfg, tc)
         losses = [tr.train_step({"input_ids": data})["loss"] for _ in range(3)]
-        res.append((losses, tr.store.flat.clone()))
+        res.append((losses, tr.flat_params().clone()))
         slots = {name for (_, name) in tr.model.engine._slots}
         if not defer:
             assert not slots  # nothing deferred, no slot buffers
@@ -201,7 +201,7 @@ def test_micro_step_fusion_matches_unfused(F, pipe, chunks, monkeypatch):
         tr = DistributedTrainer(tiny(dropout=0.0, attention_dropout=0.0), tc)
         assert tr.fusion_factor(4, 2, 32) == fuse
         losses = [tr.train_step({"input_ids": data})["loss"] for _ in range(3)]
-        res.append((losses, tr.store.flat.clone()))
+        res.append((losses, tr.flat_params().clone()))
     for a, b in zip(res[0][0], res[1][0]):
         assert abs(a - b) < 1e-5 * max(1.0, abs(a)), (a, b)
     assert torch.allclose(res[0][1], res[1][1], atol=1e-6, rtol=1e-5)
@@ -286,3 +286,44 @@ def test_wgrad_set_and_acc_contracts():
     assert (db.float() - ref_).norm() / ref_.norm() < 2e-2
     with pytest.raises(ValueError):
         g.wgrad_acc(db, dy.bfloat16(), x.bfloat16())
+
+
+def test_lazy_optimizer_step_matches_end_of_step_update(tmp_path):
+    """The recorded optimizer step (TrainingConfig.lazy_optimizer: each unit's AdamW +
+    gradient zeroing launched by the next forward's pre_forward hook) trains bitwise like
+    the reference's end-of-step update: same losses, weights, AdamW moments; state_dict,
+    checkpoints and generation flush a pending step first."""
+    from distributed_llm_trainer_amd.training.configs import TrainingConfig
+    from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
+    torch.manual_seed(15)
+    data = [torch.randint(0, 256, (8, 32)) for _ in range(4)]
+    res = []
+    for mode in ("off", "inline"):
+        tc = TrainingConfig(batch_size=2, gradient_accumulation_steps=4, warmup_steps=2, max_steps=10,
+                            lazy_optimizer=mode)
+        tr = DistributedTrainer(tiny(), tc)
+        losses = [tr.train_step({"input_ids": d})["loss"] for d in data]
+        if mode == "inline":
+            assert tr.store.pending is not None and not tr.store.pending.complete
+            sd = tr.model.state_dict()  # the state_dict pre-hook flushes the pending step
+            assert tr.store.pending is None
+            assert float(tr.store.grad.abs().max()) == 0.0  # gradients zeroed by the unit updates
+        else:
+            sd = tr.model.state_dict()
+        res.append((losses, tr.flat_params().clone(), tr.optimizer.exp_avg.clone(), tr.optimizer.exp_avg_sq.clone(),
+                    {k: v.clone() for k, v in sd.items()}))
+    (l0, f0, m0, v0, s0), (l1, f1, m1, v1, s1) = res
+    assert l0 == l1
+    assert torch.equal(f0, f1) and torch.equal(m0, m1) and torch.equal(v0, v1)
+    assert all(torch.equal(s0[k], s1[k]) for k in s0)
+    # a checkpoint taken with a step pending holds the updated weights
+    tc = TrainingConfig(batch_size=2, gradient_accumulation_steps=4, warmup_steps=2, max_steps=10,
+                        lazy_optimizer="inline", checkpoint_dir=str(tmp_path))
+    tr = DistributedTrainer(tiny(), tc)
+    for d in data:
+        tr.train_step({"input_ids": d})
+    tr.save_checkpoint(str(tmp_path / "c.pt"))
+    from distributed_llm_trainer_amd.utils.checkpoint import load_checkpoint
+    c = load_checkpoint(str(tmp_path / "c.pt"))
+    assert torch.equal(c["model"]["norm.weight"], s0["norm.weight"])
+    assert torch.equal(c["model"]["layers.1.mlp.down_proj.weight"], s0["layers.1.mlp.down_proj.weight"])
