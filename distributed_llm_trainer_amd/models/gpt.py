@@ -182,19 +182,13 @@ class GPT(nn.Module):
             from ..parallel.flat import FlatParamStore
             provider = FlatParamStore(self, dev, compute_dtype=compute_dtype)
             self.store = provider
-        torch_ops_on_gpu = False
         if ops is None:
-            if dev.type == "cuda" and act_dtype not in (torch.bfloat16, torch.float16):
-                # fp32 models (--mixed_precision fp32, the reference/debug mode): the HIP
-                # kernels move 16-bit activations, so the engine's schedule runs with
-                # PyTorch ops on the GPU and hipBLASLt fp32 GEMMs.  bf16 and fp16 run the
-                # HIP kernels (instantiated for both formats, csrc/common.h HK).
-                ops = ops_mod.CPU_OPS
-                torch_ops_on_gpu = True
-            else:
-                ops = ops_mod.for_device(dev, head_dim=self.config.head_dim)
+            # bf16 / fp16 run the 16-bit HIP kernels (csrc/common.h HK), fp32 (the
+            # reference / debug mode, --mixed_precision fp32) the fp32 ones (csrc/fp32.hip);
+            # GEMMs go through the planner (hipBLASLt fp32 GEMMs in fp32 mode)
+            ops = ops_mod.for_device(dev, head_dim=self.config.head_dim, act_dtype=act_dtype)
         gemm = None
-        if dev.type == "cuda" and (ops.backend == "hip" or torch_ops_on_gpu):
+        if dev.type == "cuda" and ops.backend == "hip":
             import os
             from ..ops import gemm as gemm_mod
             if os.environ.get("DLT_GEMM", "planner") == "planner" and gemm_mod.available():
@@ -205,6 +199,13 @@ class GPT(nn.Module):
 
     def forward(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
                 labels: Optional[torch.Tensor] = None):
+        """(logits [B, S, V], loss or None), as the reference (``gpt.py:388-455``).
+
+        Divergence on the engine path: a TRAINING forward with labels (``self.training``
+        and grad enabled) returns ``(None, loss)`` -- the fused lm_head + cross-entropy
+        turns the logits buffer into dloss/dlogits in place, so full [B, S, V] logits are
+        never materialised for the caller.  Eval mode, ``torch.no_grad()`` or a call
+        without labels returns the logits as the reference does."""
         if self.engine is not None:
             return self._engine_forward(input_ids, labels)
         h = self.embed_tokens(input_ids)

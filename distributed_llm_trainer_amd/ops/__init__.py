@@ -43,27 +43,33 @@ def hip_ops():
     return ns
 
 
-# the attention-side ops whose HIP kernels are specialised for head_dim 64
+# the attention-side ops whose HIP kernels are specialised for head_dims 64 / 128
 _ATTN_FUNCS = ("rope_qkv_fwd", "rope_qkv_bwd", "attention_fwd", "attention_bwd", "rope_qk_inplace",
                "attention_fwd_packed", "attention_bwd_packed")
 
 
-def for_device(device, head_dim: int = 64) -> types.SimpleNamespace:
-    """Op namespace for ``device``.  On the GPU every op is a HIP kernel, except that a
-    model whose head_dim is not 64 (the reference allows any ``hidden % heads == 0``,
-    ``config.py:38-39``) runs RoPE + attention through the PyTorch reference ops ON THE
-    GPU (``attn_backend == "reference"``, with a one-time warning) while the norms,
-    SwiGLU, cross-entropy, embedding, optimizer and GEMMs stay native."""
+def for_device(device, head_dim: int = 64, act_dtype=torch.bfloat16) -> types.SimpleNamespace:
+    """Op namespace for ``device``.  On the GPU every op is a HIP kernel: bf16 / fp16
+    activations on the 16-bit kernels, fp32 (``--mixed_precision fp32``) on the fp32
+    kernels (``csrc/fp32.hip``; the ``hip`` wrappers dispatch on the tensor dtype).  The
+    attention kernels take head_dim 64 and 128 in every precision; a model with another
+    head_dim (the reference allows any ``hidden % heads == 0``, ``config.py:38-39``) runs
+    RoPE + attention through the PyTorch reference ops ON THE GPU (``attn_backend ==
+    "reference"``, with a one-time warning) while the norms, SwiGLU, cross-entropy,
+    embedding, optimizer and GEMMs stay native."""
     dev = torch.device(device)
     if dev.type == "cuda":
         if os.environ.get("DLT_ALLOW_REFERENCE_ON_GPU") == "1":
             return _namespace(reference, "reference")
         ns = hip_ops()
         ns.attn_backend = "hip"
-        if head_dim != 64:
+        from .hip import ATTN_HEAD_DIMS
+        from .hip_f32 import ATTN_HEAD_DIMS as F32_HEAD_DIMS
+        native_hd = F32_HEAD_DIMS if act_dtype == torch.float32 else ATTN_HEAD_DIMS
+        if head_dim not in native_hd:
             import warnings
-            warnings.warn(f"head_dim {head_dim}: the HIP attention kernels are specialised for head_dim 64; "
-                          "RoPE + attention run as PyTorch ops on the GPU for this model")
+            warnings.warn(f"head_dim {head_dim}: the HIP attention kernels take head_dim {native_hd} for "
+                          f"{act_dtype} activations; RoPE + attention run as PyTorch ops on the GPU for this model")
             for f in _ATTN_FUNCS:
                 setattr(ns, f, getattr(reference, f))
             ns.attn_backend = "reference"

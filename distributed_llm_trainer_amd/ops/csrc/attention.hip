@@ -1,4 +1,5 @@
-// Causal flash attention (head_dim 64) with in-kernel dropout for gfx950 MFMA.
+// Causal flash attention (head_dim 64 or 128: template parameter D) with in-kernel
+// dropout for gfx950 MFMA.
 //
 // Replaces the reference's naive attention (gpt.py:230-234: Q@K^T, triu mask,
 // fp32 softmax, bernoulli dropout, @V -- a [B,nh,S,S] score tensor per layer) and
@@ -38,7 +39,6 @@
 
 #include <type_traits>
 
-#define HD 64
 #define KVB 64     // keys per staged tile (fwd / dQ)
 #define RB 64      // rows (queries for fwd / dQ, keys for dK/dV) per work item: 2 waves x 32
 #define QSTEP 64   // queries per staged tile (dK/dV)
@@ -48,29 +48,37 @@
 typedef __attribute__((address_space(3))) shortx4_t lds_shortx4_t;
 typedef short shortx8_t __attribute__((ext_vector_type(8)));
 
-// LDS tile: [64 rows][64 bf16] = 128-B rows; 16-B chunk c of row r is stored at
-// chunk c ^ ((r >> 1) & 7): conflict-free ds_read_b128 row-fragment reads.
+// LDS tile: [64 rows][D bf16].  D = 64: 128-B rows, 16-B chunk c of row r stored at
+// chunk c ^ ((r >> 1) & 7) -- row pairs fill the 64 banks, so 16 consecutive rows of a
+// ds_read_b128 row-fragment read are conflict-free.  D = 128: 256-B rows (every row
+// starts at bank 0), chunk c ^ (r & 15) gives 16 consecutive rows 16 distinct chunks.
+template <int D>
+__device__ __forceinline__ int swz_x(int row) { return D == 64 ? ((row >> 1) & 7) : (row & 15); }
+template <int D>
 __device__ __forceinline__ int swz_off(int row, int col) {
-  return row * HD + ((((col >> 3) ^ ((row >> 1) & 7))) << 3) + (col & 7);
+  return row * D + ((((col >> 3) ^ swz_x<D>(row))) << 3) + (col & 7);
 }
 
+template <int D>
 __device__ __forceinline__ bf16x8_t lds_row8(const bf16_t* T, int row, int col) {
-  return *reinterpret_cast<const bf16x8_t*>(T + swz_off(row, col));
+  return *reinterpret_cast<const bf16x8_t*>(T + swz_off<D>(row, col));
 }
 
+template <int D>
 __device__ __forceinline__ shortx4_t lds_tr4(const bf16_t* T, int row, int col) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_shortx4_t*)(T + swz_off(row, col)));
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_shortx4_t*)(T + swz_off<D>(row, col)));
 }
 
 // A operand A[d][k] (k = rows of T) in the permuted k order that matches accumulator
 // registers 8s..8s+7 used as the B operand: element j of lane-half h <-> row
 // 16*kk + 8*(j>>2) + 4*h + (j&3)  (cdna_hip_programming.md §3).
+template <int D>
 __device__ __forceinline__ bf16x8_t tr_frag(const bf16_t* T, int kk, int dt, int lane) {
   const int h = lane >> 5, i = lane & 15;
   const int col = 32 * dt + 16 * ((lane >> 4) & 1) + 4 * (i & 3);
   const int r1 = 16 * kk + 4 * h + (i >> 2);
-  const shortx4_t a = lds_tr4(T, r1, col);
-  const shortx4_t b = lds_tr4(T, r1 + 8, col);
+  const shortx4_t a = lds_tr4<D>(T, r1, col);
+  const shortx4_t b = lds_tr4<D>(T, r1 + 8, col);
   shortx8_t c = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
   return __builtin_bit_cast(bf16x8_t, c);
 }
@@ -82,27 +90,30 @@ __device__ __forceinline__ bf16x8_t tr_frag(const bf16_t* T, int kk, int dt, int
 // check; the protocol that makes them safe is explicit: every tile step ends with
 // `s_waitcnt vmcnt(0)` + barrier (tile_barrier), so a tile is complete before any
 // wave reads it, and tr_wait() retires the reads before their registers are used.
+template <int D>
 __device__ __forceinline__ shortx4_t lds_tr4_asm(const bf16_t* T, int row, int col) {
   shortx4_t r;
-  const uint32_t addr = (uint32_t)(uintptr_t)(T + swz_off(row, col));
+  const uint32_t addr = (uint32_t)(uintptr_t)(T + swz_off<D>(row, col));
   asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr));
   return r;
 }
+template <int D>
 __device__ __forceinline__ bf16x8_t tr_frag_asm(const bf16_t* T, int kk, int dt, int lane) {
   const int h = lane >> 5, i = lane & 15;
   const int col = 32 * dt + 16 * ((lane >> 4) & 1) + 4 * (i & 3);
   const int r1 = 16 * kk + 4 * h + (i >> 2);
-  const shortx4_t a = lds_tr4_asm(T, r1, col);
-  const shortx4_t b = lds_tr4_asm(T, r1 + 8, col);
+  const shortx4_t a = lds_tr4_asm<D>(T, r1, col);
+  const shortx4_t b = lds_tr4_asm<D>(T, r1 + 8, col);
   shortx8_t c = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
   return __builtin_bit_cast(bf16x8_t, c);
 }
 // Row-fragment read through inline asm (see lds_tr4_asm for the protocol), so several
 // reads can be in flight under one counted wait (the intrinsic form drew one
 // lgkmcnt(0) per MFMA pair).
+template <int D>
 __device__ __forceinline__ bf16x8_t lds_row8_asm(const bf16_t* T, int row, int col) {
   bf16x8_t r;
-  const uint32_t addr = (uint32_t)(uintptr_t)(T + swz_off(row, col));
+  const uint32_t addr = (uint32_t)(uintptr_t)(T + swz_off<D>(row, col));
   asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(addr));
   return r;
 }
@@ -110,6 +121,22 @@ __device__ __forceinline__ bf16x8_t lds_row8_asm(const bf16_t* T, int row, int c
 // load is issued inside a tile step).
 __device__ __forceinline__ void lgkm_wait4(bf16x8_t& a, bf16x8_t& b, bf16x8_t& c, bf16x8_t& d) {
   asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d)::"memory");
+}
+// D = 128 forms: the oldest eight of sixteen reads retired; pin4 keeps four more
+// fragments' consumers below the preceding wait (volatile asm stays in order).
+__device__ __forceinline__ void lgkm_wait8(bf16x8_t& a, bf16x8_t& b, bf16x8_t& c, bf16x8_t& d) {
+  asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d)::"memory");
+}
+__device__ __forceinline__ void pin4(bf16x8_t& a, bf16x8_t& b, bf16x8_t& c, bf16x8_t& d) {
+  asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+}
+// Retire every outstanding LDS read, holding the consumers of all N fragments below it.
+template <int N>
+__device__ __forceinline__ void tr_wait_all(bf16x8_t (&f)[N]) {
+  static_assert(N % 4 == 0, "groups of four");
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3])::"memory");
+#pragma unroll
+  for (int j = 4; j < N; j += 4) pin4(f[j], f[j + 1], f[j + 2], f[j + 3]);
 }
 __device__ __forceinline__ float max16(const floatx16_t& a) {
   const float m0 = fmaxf(fmaxf(a[0], a[1]), a[2]), m1 = fmaxf(fmaxf(a[3], a[4]), a[5]);
@@ -179,65 +206,44 @@ __device__ __forceinline__ floatx16_t zero16() {
   return z;
 }
 
-// Register-staged tile copy: 64 rows x 64 cols bf16; 4 x 16 B per thread of a
-// 128-thread block.  Rows beyond S are CLAMPED to row S-1, not zero-filled: a
-// zero-fill select right after the load would force an immediate vmcnt wait and
-// serialise the prefetch with the tile compute.  Every tile that can reach past S
-// runs the masked tile kind, which zeroes those rows' probabilities, and the clamped
-// data is finite, so it never contributes.  `rstride` = row stride in elements.
-typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-struct Stage4 { u32x4_t c0, c1, c2, c3; };  // vector members: stays in VGPRs (no scratch alloca)
-// 128 threads: thread t moves 16-B chunk (t & 7) of rows (t >> 3) + {0, 16, 32, 48}.
-__device__ __forceinline__ void stage_load(Stage4& st, const bf16_t* __restrict__ base, int row0, int S,
-                                           int rstride, int tid) {
-  const int r = tid >> 3, ch = tid & 7;
-  const bf16_t* p = base + ch * 8;
-  st.c0 = *reinterpret_cast<const u32x4_t*>(p + (size_t)min(row0 + r, S - 1) * rstride);
-  st.c1 = *reinterpret_cast<const u32x4_t*>(p + (size_t)min(row0 + r + 16, S - 1) * rstride);
-  st.c2 = *reinterpret_cast<const u32x4_t*>(p + (size_t)min(row0 + r + 32, S - 1) * rstride);
-  st.c3 = *reinterpret_cast<const u32x4_t*>(p + (size_t)min(row0 + r + 48, S - 1) * rstride);
-}
-__device__ __forceinline__ void stage_store(const Stage4& st, bf16_t* T, int tid) {
-  const int r = tid >> 3, ch = tid & 7;
-  *reinterpret_cast<u32x4_t*>(T + swz_off(r, ch * 8)) = st.c0;
-  *reinterpret_cast<u32x4_t*>(T + swz_off(r + 16, ch * 8)) = st.c1;
-  *reinterpret_cast<u32x4_t*>(T + swz_off(r + 32, ch * 8)) = st.c2;
-  *reinterpret_cast<u32x4_t*>(T + swz_off(r + 48, ch * 8)) = st.c3;
-}
-
 // Direct global->LDS tile copy (global_load_lds_dwordx4, no staging registers): one
-// wave-instruction writes 1 KiB = 8 rows contiguously (lane l -> row l/8, 16-B slot
-// l%8), so the XOR swizzle is applied on the SOURCE address: slot s of row r holds
-// global chunk s ^ ((r >> 1) & 7), exactly the image swz_off() reads.  64 rows =
-// 8 instructions, 4 per wave of the 2-wave workgroup.  Completion is tracked by
-// vmcnt; the __syncthreads() that ends every tile step waits for it.
+// wave-instruction writes 1 KiB = 1024 / (2D) rows contiguously (lane l -> row
+// l / (D/8), 16-B slot l % (D/8)), so the XOR swizzle is applied on the SOURCE
+// address: slot s of row r holds global chunk s ^ swz_x(r), exactly the image
+// swz_off() reads.  64 rows = 8 (D = 64) or 16 (D = 128) instructions, split over the
+// 2 waves.  Completion is tracked by vmcnt; the __syncthreads() that ends every tile
+// step waits for it.
 typedef __attribute__((address_space(3))) void* lds_vptr_t;
 typedef const __attribute__((address_space(1))) void* gbl_cvptr_t;
+template <int D>
 __device__ __forceinline__ void glds_tile(const bf16_t* __restrict__ base, int row0, int S, int rstride, bf16_t* T,
                                           int wid, int lane) {
   // 32-bit offsets (a head's rows span < 4 GB) on the wave-uniform base: the DMA takes
   // the saddr form and no 64-bit address arithmetic runs per tile (fwd / dQ).
+  constexpr int CPR = D / 8, RPI = 64 / CPR, NI = 32 / RPI;  // chunks / row, rows / instr, instr / wave
   const char* b = reinterpret_cast<const char*>(base);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int rr = (wid * 4 + j) * 8;  // first row of this 1 KiB piece (wave-uniform)
-    const int row = rr + (lane >> 3);
-    const int c = (lane & 7) ^ ((row >> 1) & 7);
+  for (int j = 0; j < NI; ++j) {
+    const int rr = (wid * NI + j) * RPI;  // first row of this 1 KiB piece (wave-uniform)
+    const int row = rr + lane / CPR;
+    const int c = (lane % CPR) ^ swz_x<D>(row);
     const uint32_t off = (uint32_t)(min(row0 + row, S - 1) * rstride + c * 8) * 2u;
-    __builtin_amdgcn_global_load_lds((gbl_cvptr_t)(b + off), (lds_vptr_t)(T + rr * HD), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((gbl_cvptr_t)(b + off), (lds_vptr_t)(T + rr * D), 16, 0, 0);
   }
 }
 // The same copy with 64-bit row addressing: fewer live registers in dK/dV, which stages
 // two operands with different row strides and sits at the VGPR limit.
+template <int D>
 __device__ __forceinline__ void glds_tile64(const bf16_t* __restrict__ base, int row0, int S, int rstride, bf16_t* T,
                                             int wid, int lane) {
+  constexpr int CPR = D / 8, RPI = 64 / CPR, NI = 32 / RPI;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int rr = (wid * 4 + j) * 8;
-    const int row = rr + (lane >> 3);
-    const int c = (lane & 7) ^ ((row >> 1) & 7);
+  for (int j = 0; j < NI; ++j) {
+    const int rr = (wid * NI + j) * RPI;
+    const int row = rr + lane / CPR;
+    const int c = (lane % CPR) ^ swz_x<D>(row);
     const bf16_t* g = base + (size_t)min(row0 + row, S - 1) * rstride + c * 8;
-    __builtin_amdgcn_global_load_lds((gbl_cvptr_t)g, (lds_vptr_t)(T + rr * HD), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((gbl_cvptr_t)g, (lds_vptr_t)(T + rr * D), 16, 0, 0);
   }
 }
 
@@ -363,9 +369,10 @@ __device__ __forceinline__ float xhalf_sum(float x) {
 // lands there; own g = 2m + 1 stays in the high lanes' vsrc -- leaves lane h holding
 // dims 16m + 8h + [0, 8): 4 dwordx4 stores per row instead of 8 dwordx2 (the epilogue's
 // store issue is the tail of every work item).
-__device__ __forceinline__ void store_row16(bf16_t* __restrict__ row, const uint2 (&w)[2][4], int h) {
+template <int D>
+__device__ __forceinline__ void store_row16(bf16_t* __restrict__ row, const uint2 (&w)[D / 32][4], int h) {
 #pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
+  for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
       const auto rx = __builtin_amdgcn_permlane32_swap(w[dt][2 * m].x, w[dt][2 * m + 1].x, false, false);
@@ -380,14 +387,16 @@ __device__ __forceinline__ void store_row16(bf16_t* __restrict__ row, const uint
 // rescale after a row's first tile is skipped.
 #define RESCALE_LOG2 8.0f
 
+template <int D>
 struct FwdState {
-  floatx16_t o[2];
+  floatx16_t o[D / 32];
   float m, l;  // running max (raw score units) and per-lane partial row sum
 };
 
-template <bool MASK, bool DROP, int HK = 0>
-__device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const bf16_t* Vt, const bf16x8_t (&qf)[4],
-                                         int k0, int qa, int S, int lane, float c_log2, uint2 mw) {
+template <bool MASK, bool DROP, int HK, int D>
+__device__ __forceinline__ void fwd_tile(FwdState<D>& fs, const bf16_t* Kt, const bf16_t* Vt,
+                                         const bf16x8_t (&qf)[D / 16], int k0, int qa, int S, int lane, float c_log2,
+                                         uint2 mw) {
   // One 64-key tile as ONE online-softmax step: S = K.Q^T of both 32-key halves first
   // (two independent MFMA chains), one row max / rescale decision for the tile, then
   // per half exp -> dropout -> P.V; the second half's softmax VALU runs while the
@@ -398,33 +407,39 @@ __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const b
   // so no vmcnt wait lands inside the tile); this lane-half's 16 bits per half-tile
   // sit at (i&3) + 8(i>>2)
   const uint32_t words[2] = {mw.x >> (4 * h), mw.y >> (4 * h)};
+  constexpr int NS = D / 16;  // 16-dim contraction steps of S = K.Q^T
   floatx16_t sacc[2];
   {
-    bf16x8_t kf[2][4];
+    bf16x8_t kf[2][NS];
 #if DLT_ATTN_KREAD_ASM
-    // all eight K fragments in flight at once, one counted wait per half
+    // all K fragments of the tile in flight at once, one counted wait per half
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) kf[t][s] = lds_row8_asm(Kt, 32 * t + ql, 16 * s + 8 * h);
-    lgkm_wait4(kf[0][0], kf[0][1], kf[0][2], kf[0][3]);
+      for (int s = 0; s < NS; ++s) kf[t][s] = lds_row8_asm<D>(Kt, 32 * t + ql, 16 * s + 8 * h);
+    if constexpr (D == 64) {
+      lgkm_wait4(kf[0][0], kf[0][1], kf[0][2], kf[0][3]);
+    } else {
+      lgkm_wait8(kf[0][0], kf[0][1], kf[0][2], kf[0][3]);
+      pin4(kf[0][4], kf[0][5], kf[0][6], kf[0][7]);
+    }
     sacc[0] = zero16();
 #pragma unroll
-    for (int s = 0; s < 4; ++s) sacc[0] = mfma<HK>(kf[0][s], qf[s], sacc[0]);
-    tr_wait(kf[1][0], kf[1][1], kf[1][2], kf[1][3]);
+    for (int s = 0; s < NS; ++s) sacc[0] = mfma<HK>(kf[0][s], qf[s], sacc[0]);
+    tr_wait_all(kf[1]);
     sacc[1] = zero16();
 #pragma unroll
-    for (int s = 0; s < 4; ++s) sacc[1] = mfma<HK>(kf[1][s], qf[s], sacc[1]);
+    for (int s = 0; s < NS; ++s) sacc[1] = mfma<HK>(kf[1][s], qf[s], sacc[1]);
 #else
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      kf[0][s] = lds_row8(Kt, ql, 16 * s + 8 * h);
-      kf[1][s] = lds_row8(Kt, 32 + ql, 16 * s + 8 * h);
+    for (int s = 0; s < NS; ++s) {
+      kf[0][s] = lds_row8<D>(Kt, ql, 16 * s + 8 * h);
+      kf[1][s] = lds_row8<D>(Kt, 32 + ql, 16 * s + 8 * h);
     }
     sacc[0] = zero16();
     sacc[1] = zero16();
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < NS; ++s) {
       sacc[0] = mfma<HK>(kf[0][s], qf[s], sacc[0]);
       sacc[1] = mfma<HK>(kf[1][s], qf[s], sacc[1]);
     }
@@ -447,7 +462,7 @@ __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const b
     fs.m = m_new;
     fs.l *= alpha;
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
+    for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
       for (int i = 0; i < 16; ++i) fs.o[dt][i] *= alpha;
   }
@@ -455,11 +470,11 @@ __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const b
   float l0 = 0.f, l1 = 0.f;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    bf16x8_t vf[2][2];
+    bf16x8_t vf[2][D / 32];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt) vf[kk][dt] = tr_frag_asm(Vt, 2 * t + kk, dt, lane);
+      for (int dt = 0; dt < D / 32; ++dt) vf[kk][dt] = tr_frag_asm<D>(Vt, 2 * t + kk, dt, lane);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const float p = fast_exp2(fmaf(sacc[t][i], c_log2, nmc));
@@ -468,12 +483,17 @@ __device__ __forceinline__ void fwd_tile(FwdState& fs, const bf16_t* Kt, const b
       if (DROP) sacc[t][i] = keep_and(p, keep_ones(words[t], (i & 3) + 8 * (i >> 2)));  // 1/(1-p) at the end
       else sacc[t][i] = p;
     }
-    tr_wait(vf[0][0], vf[0][1], vf[1][0], vf[1][1]);
+    if constexpr (D == 64) {
+      tr_wait(vf[0][0], vf[0][1], vf[1][0], vf[1][1]);
+    } else {
+      tr_wait(vf[0][0], vf[0][1], vf[0][2], vf[0][3]);
+      pin4(vf[1][0], vf[1][1], vf[1][2], vf[1][3]);
+    }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const bf16x8_t pb = acc_frag<HK>(sacc[t], kk);
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt) fs.o[dt] = mfma<HK>(vf[kk][dt], pb, fs.o[dt]);
+      for (int dt = 0; dt < D / 32; ++dt) fs.o[dt] = mfma<HK>(vf[kk][dt], pb, fs.o[dt]);
     }
   }
   fs.l += l0 + l1;
@@ -499,13 +519,16 @@ __device__ unsigned long long* g_attn_ftim;
 #define FWD_ACC(c, w) ((void)0)
 #endif
 
-template <bool DROP, int HK = 0>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_attn_fwd(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
+// D = 128 doubles the O accumulators and Q / K / V fragments: 256 VGPRs would spill,
+// so its instantiation may take the whole 512-register file (one wave per SIMD).
+#define ATTN_WAVES(D) __attribute__((amdgpu_waves_per_eu(D == 64 ? 2 : 1, 2)))
+template <bool DROP, int HK, int D>
+__global__ __launch_bounds__(NT) ATTN_WAVES(D) void k_attn_fwd(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
                                                     const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
                                                     float* __restrict__ lse, const uint32_t* __restrict__ mask,
                                                     int S, int nh, float c_log2, float dscale, long in_bs,
                                                     int in_hs, int in_rs, int xcd_map) {
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * 2 * KVB * HD];  // [buf][K|V][64][64]
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * 2 * KVB * D];  // [buf][K|V][64][D]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, ql = lane & 31;
@@ -532,19 +555,20 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     const int qa = q0 + ql;
     const uint32_t* mrow = mask ? mask + (size_t)bh * W * S + min(qa, S - 1) : nullptr;  // word j at mrow[j*S]
 
-    bf16x8_t qf[4];
+    bf16x8_t qf[D / 16];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) qf[s] = load_row8(q + hin + (size_t)min(qa, S - 1) * in_rs + 16 * s + 8 * h, qa < S);
+    for (int s = 0; s < D / 16; ++s)
+      qf[s] = load_row8(q + hin + (size_t)min(qa, S - 1) * in_rs + 16 * s + 8 * h, qa < S);
 
-    FwdState fs;
-    fs.o[0] = zero16();
-    fs.o[1] = zero16();
+    FwdState<D> fs;
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt) fs.o[dt] = zero16();
     fs.m = -INFINITY;
     fs.l = 0.f;
 
     const int nkv = (min(S, qb * RB + RB) + KVB - 1) / KVB;  // = qb + 1 except at a ragged end
-    glds_tile(k + hin, 0, S, in_rs, lds, wid, lane);
-    glds_tile(v + hin, 0, S, in_rs, lds + KVB * HD, wid, lane);
+    glds_tile<D>(k + hin, 0, S, in_rs, lds, wid, lane);
+    glds_tile<D>(v + hin, 0, S, in_rs, lds + KVB * D, wid, lane);
     __syncthreads();
 
     // One K/V tile per step.  BUF is a compile-time LDS buffer index and MASKED a
@@ -559,18 +583,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       FWD_T(ta);
       const bool more = kb + 1 < nkv;
       if (more) {  // next tile straight into the other buffer (read by nobody since the last barrier)
-        bf16_t* Kn = lds + (BUF ^ 1) * 2 * KVB * HD;
-        glds_tile(k + hin, (kb + 1) * KVB, S, in_rs, Kn, wid, lane);
-        glds_tile(v + hin, (kb + 1) * KVB, S, in_rs, Kn + KVB * HD, wid, lane);
+        bf16_t* Kn = lds + (BUF ^ 1) * 2 * KVB * D;
+        glds_tile<D>(k + hin, (kb + 1) * KVB, S, in_rs, Kn, wid, lane);
+        glds_tile<D>(v + hin, (kb + 1) * KVB, S, in_rs, Kn + KVB * D, wid, lane);
         if (DROP) mw_next = make_uint2(mrow[(size_t)(2 * (kb + 1)) * S], 2 * (kb + 1) + 1 < W ? mrow[(size_t)(2 * (kb + 1) + 1) * S] : 0u);
       }
-      const bf16_t* Kt = lds + BUF * 2 * KVB * HD;
-      const bf16_t* Vt = Kt + KVB * HD;
+      const bf16_t* Kt = lds + BUF * 2 * KVB * D;
+      const bf16_t* Vt = Kt + KVB * D;
       const int k0 = kb * KVB;
       if (!MASKED)
-        fwd_tile<false, DROP, HK>(fs, Kt, Vt, qf, k0, qa, S, lane, c_log2, mw_cur);
+        fwd_tile<false, DROP, HK, D>(fs, Kt, Vt, qf, k0, qa, S, lane, c_log2, mw_cur);
       else if (k0 <= q0 + 31)
-        fwd_tile<true, DROP, HK>(fs, Kt, Vt, qf, k0, qa, S, lane, c_log2, mw_cur);
+        fwd_tile<true, DROP, HK, D>(fs, Kt, Vt, qf, k0, qa, S, lane, c_log2, mw_cur);
       mw_cur = mw_next;
       FWD_T(tb);
       tile_barrier();
@@ -594,10 +618,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     const float inv_l = (DROP ? dscale : 1.f) / l_tot;
     if (qa < S) {
       if (h == 0) lse[(size_t)bh * S + qa] = fs.m * (c_log2 / LOG2E) + __logf(l_tot);
-      bf16_t* orow = o + (((size_t)b * S + qa) * nh + head) * HD;
-      uint2 w[2][4];
+      bf16_t* orow = o + (((size_t)b * S + qa) * nh + head) * D;
+      uint2 w[D / 32][4];
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
+      for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           u16x4 t;
@@ -605,7 +629,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
           for (int e = 0; e < 4; ++e) t.v[e] = f2h<HK>(fs.o[dt][4 * g + e] * inv_l);
           w[dt][g] = __builtin_bit_cast(uint2, t);
         }
-      store_row16(orow, w, h);
+      store_row16<D>(orow, w, h);
     }
   }
 #ifdef DLT_ATTN_FWD_TIMING
@@ -623,35 +647,41 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 // position `pos` is applied first: the partner of dim j < 32 is j + 32, i.e. the same
 // register of the other dt -- the rotation needs no data exchange.  (Replaces the
 // separate repack kernel that read dq/dk back and wrote the packed [M, 3H] gradient.)
-template <int HK = 0>
-__device__ __forceinline__ void store_head_row(bf16_t* __restrict__ dst, const floatx16_t (&a)[2], float sc, int h,
+template <int HK, int D>
+__device__ __forceinline__ void store_head_row(bf16_t* __restrict__ dst, const floatx16_t (&a)[D / 32], float sc, int h,
                                                const float* __restrict__ cosT, const float* __restrict__ sinT,
                                                int pos) {
-  uint2 w[2][4];
+  // dims of a[dt] element 4g + e: 32 dt + 8 g + 4 h + e; the RoPE partner of dim j < D/2
+  // is j + D/2, register 4g + e of a[dt + D/64]
+  constexpr int HP = D / 64;
+  uint2 w[D / 32][4];
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    u16x4 w0, w1;
-    if (cosT) {
-      const float4 c4 = *reinterpret_cast<const float4*>(cosT + pos * (HD / 2) + 8 * g + 4 * h);
-      const float4 s4 = *reinterpret_cast<const float4*>(sinT + pos * (HD / 2) + 8 * g + 4 * h);
-      const float cc[4] = {c4.x, c4.y, c4.z, c4.w}, ss[4] = {s4.x, s4.y, s4.z, s4.w};
+  for (int g = 0; g < 4; ++g)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float x1 = a[0][4 * g + e] * sc, x2 = a[1][4 * g + e] * sc;
-        w0.v[e] = f2h<HK>(fmaf(x1, cc[e], x2 * ss[e]));
-        w1.v[e] = f2h<HK>(fmaf(x2, cc[e], -x1 * ss[e]));
+    for (int dt = 0; dt < HP; ++dt) {
+      u16x4 w0, w1;
+      if (cosT) {
+        const int ti = pos * (D / 2) + 32 * dt + 8 * g + 4 * h;
+        const float4 c4 = *reinterpret_cast<const float4*>(cosT + ti);
+        const float4 s4 = *reinterpret_cast<const float4*>(sinT + ti);
+        const float cc[4] = {c4.x, c4.y, c4.z, c4.w}, ss[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float x1 = a[dt][4 * g + e] * sc, x2 = a[dt + HP][4 * g + e] * sc;
+          w0.v[e] = f2h<HK>(fmaf(x1, cc[e], x2 * ss[e]));
+          w1.v[e] = f2h<HK>(fmaf(x2, cc[e], -x1 * ss[e]));
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          w0.v[e] = f2h<HK>(a[dt][4 * g + e] * sc);
+          w1.v[e] = f2h<HK>(a[dt + HP][4 * g + e] * sc);
+        }
       }
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        w0.v[e] = f2h<HK>(a[0][4 * g + e] * sc);
-        w1.v[e] = f2h<HK>(a[1][4 * g + e] * sc);
-      }
+      w[dt][g] = __builtin_bit_cast(uint2, w0);
+      w[dt + HP][g] = __builtin_bit_cast(uint2, w1);
     }
-    w[0][g] = __builtin_bit_cast(uint2, w0);
-    w[1][g] = __builtin_bit_cast(uint2, w1);
-  }
-  store_row16(dst, w, h);
+  store_row16<D>(dst, w, h);
 }
 
 // Per-wave timestamps for tools/cpp/attn_timing.cpp (only with -DDLT_ATTN_TIMING):
@@ -670,17 +700,17 @@ __device__ unsigned long long* g_attn_tim;
 // ---------------------------------------------------------------- dK / dV
 // One workgroup per 128 keys (32 per wave); sweep query tiles of 64 (two 32-row
 // sub-tiles).  Accumulators: S and dP with queries in registers, keys on lanes.
-template <bool MASK, bool DROP, int HK = 0>
-__device__ __forceinline__ void dkdv_subtile(floatx16_t (&dka)[2], floatx16_t (&dva)[2], const bf16_t* Qt,
+template <bool MASK, bool DROP, int HK, int D>
+__device__ __forceinline__ void dkdv_subtile(floatx16_t (&dka)[D / 32], floatx16_t (&dva)[D / 32], const bf16_t* Qt,
                                              const bf16_t* Dt, const float* rl, const float* rd,
-                                             uint32_t mw, const bf16x8_t (&kf)[4], const bf16x8_t (&vf)[4],
+                                             uint32_t mw, const bf16x8_t (&kf)[D / 16], const bf16x8_t (&vf)[D / 16],
                                              int qs, int ka, int S, int lane, float c_log2, float dscale) {
   const int h = lane >> 5, kl = lane & 31;
   floatx16_t sacc = zero16(), pacc = zero16();
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    sacc = mfma<HK>(lds_row8(Qt, kl, 16 * s + 8 * h), kf[s], sacc);
-    pacc = mfma<HK>(lds_row8(Dt, kl, 16 * s + 8 * h), vf[s], pacc);
+  for (int s = 0; s < D / 16; ++s) {
+    sacc = mfma<HK>(lds_row8<D>(Qt, kl, 16 * s + 8 * h), kf[s], sacc);
+    pacc = mfma<HK>(lds_row8<D>(Dt, kl, 16 * s + 8 * h), vf[s], pacc);
   }
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
@@ -717,17 +747,17 @@ __device__ __forceinline__ void dkdv_subtile(floatx16_t (&dka)[2], floatx16_t (&
     const bf16x8_t pb = acc_frag<HK>(sacc, s);
     const bf16x8_t sb = acc_frag<HK>(pacc, s);
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt) {
-      dva[dt] = mfma<HK>(tr_frag(Dt, s, dt, lane), pb, dva[dt]);
-      dka[dt] = mfma<HK>(tr_frag(Qt, s, dt, lane), sb, dka[dt]);
+    for (int dt = 0; dt < D / 32; ++dt) {
+      dva[dt] = mfma<HK>(tr_frag<D>(Dt, s, dt, lane), pb, dva[dt]);
+      dka[dt] = mfma<HK>(tr_frag<D>(Qt, s, dt, lane), sb, dka[dt]);
     }
   }
 }
 
 // Work items: 64 keys (2 waves x 32); a workgroup processes the pair of key blocks
 // (p, nrb-1-p) -- equal work per workgroup (see the forward).
-template <bool DROP, int HK = 0>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_attn_bwd_dkdv(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
+template <bool DROP, int HK, int D>
+__global__ __launch_bounds__(NT) ATTN_WAVES(D) void k_attn_bwd_dkdv(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
                                                          const bf16_t* __restrict__ v,
                                                          const bf16_t* __restrict__ dout,
                                                          const float* __restrict__ lse,
@@ -739,9 +769,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
                                                          const float* __restrict__ cosT,
                                                          const float* __restrict__ sinT, int xcd_map) {
   // one LDS object (avoids hipcc's extra vmcnt waits with several __shared__ arrays)
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * QSTEP * HD * 2 + 2 * 2 * QSTEP * 4];
-  bf16_t* lds = reinterpret_cast<bf16_t*>(smem);                              // [buf][Q|dO][64][64]
-  float* rowc = reinterpret_cast<float*>(smem + 2 * 2 * QSTEP * HD * 2);      // [buf][lse2|delta][64]
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * QSTEP * D * 2 + 2 * 2 * QSTEP * 4];
+  bf16_t* lds = reinterpret_cast<bf16_t*>(smem);                              // [buf][Q|dO][64][D]
+  float* rowc = reinterpret_cast<float*>(smem + 2 * 2 * QSTEP * D * 2);       // [buf][lse2|delta][64]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, kl = lane & 31;
@@ -752,10 +782,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const int b = bh / nh, head = bh % nh;
   const size_t hin = (size_t)b * in_bs + (size_t)head * in_hs;     // q / k / v
   const size_t hout = (size_t)b * out_bs + (size_t)head * out_hs;  // dk / dv
-  const int rstride = nh * HD;
+  const int rstride = nh * D;
   const int W = (S + 31) >> 5;
   const int nqt = (S + QSTEP - 1) / QSTEP;
-  const bf16_t* dob = dout + ((size_t)b * S * nh + head) * HD;
+  const bf16_t* dob = dout + ((size_t)b * S * nh + head) * D;
   using UNM = std::integral_constant<bool, false>;
   using MSK = std::integral_constant<bool, true>;
 
@@ -768,21 +798,23 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     // this lane's key column of the transposed keep-bit mask: one word per 32 queries
     const uint32_t* mcol = DROP ? maskT + (size_t)bh * W * S + min(ka, S - 1) : nullptr;  // word j at mcol[j*S]
 
-    bf16x8_t kf[4], vf[4];
+    bf16x8_t kf[D / 16], vf[D / 16];
     const int kc = min(ka, S - 1);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < D / 16; ++s) {
       kf[s] = load_row8(k + hin + (size_t)kc * in_rs + 16 * s + 8 * h, ka < S);
       vf[s] = load_row8(v + hin + (size_t)kc * in_rs + 16 * s + 8 * h, ka < S);
     }
-    floatx16_t dka[2] = {zero16(), zero16()}, dva[2] = {zero16(), zero16()};
+    floatx16_t dka[D / 32], dva[D / 32];
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt) dka[dt] = dva[dt] = zero16();
 
     const int qt_begin = kblk;  // the 64-query tile holding this item's diagonal
     float rl = 0.f, rd = 0.f;
     uint2 mw_cur = make_uint2(0u, 0u), mw_next = make_uint2(0u, 0u);
     auto load_rows = [&](int t, int buf) {  // Q / dO tiles by LDS-DMA, row stats via registers
-      glds_tile64(q + hin, t * QSTEP, S, in_rs, lds + buf * 2 * QSTEP * HD, wid, lane);
-      glds_tile64(dob, t * QSTEP, S, rstride, lds + buf * 2 * QSTEP * HD + QSTEP * HD, wid, lane);
+      glds_tile64<D>(q + hin, t * QSTEP, S, in_rs, lds + buf * 2 * QSTEP * D, wid, lane);
+      glds_tile64<D>(dob, t * QSTEP, S, rstride, lds + buf * 2 * QSTEP * D + QSTEP * D, wid, lane);
       if (DROP) {  // this lane's two 32-query keep words of tile t (consumed one tile later)
         const int w0 = (t * QSTEP) >> 5;
         mw_next = make_uint2(mcol[(size_t)w0 * S], (w0 + 1 < W) ? mcol[(size_t)(w0 + 1) * S] : 0u);
@@ -815,22 +847,22 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       const bool more = t + 1 < nqt;
       const uint32_t mw0 = mw_cur.x, mw1 = mw_cur.y;
       if (more) load_rows(t + 1, cur ^ 1);
-      const bf16_t* Qt = lds + cur * 2 * QSTEP * HD;
-      const bf16_t* Dt = Qt + QSTEP * HD;
+      const bf16_t* Qt = lds + cur * 2 * QSTEP * D;
+      const bf16_t* Dt = Qt + QSTEP * D;
       const float* rlp = rowc + cur * 2 * QSTEP;
       const float* rdp = rlp + QSTEP;
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
         const int qs = t * QSTEP + 32 * qt;
-        const bf16_t* Qs = Qt + 32 * qt * HD;
-        const bf16_t* Ds = Dt + 32 * qt * HD;
+        const bf16_t* Qs = Qt + 32 * qt * D;
+        const bf16_t* Ds = Dt + 32 * qt * D;
         const uint32_t mw = (qt ? mw1 : mw0) >> (4 * h);
         if (!MASKED)
-          dkdv_subtile<false, DROP, HK>(dka, dva, Qs, Ds, rlp + 32 * qt, rdp + 32 * qt, mw, kf, vf, qs, ka, S, lane,
-                                    c_log2, dscale);
+          dkdv_subtile<false, DROP, HK, D>(dka, dva, Qs, Ds, rlp + 32 * qt, rdp + 32 * qt, mw, kf, vf, qs, ka, S,
+                                           lane, c_log2, dscale);
         else if (qs + 31 >= k0)
-          dkdv_subtile<true, DROP, HK>(dka, dva, Qs, Ds, rlp + 32 * qt, rdp + 32 * qt, mw, kf, vf, qs, ka, S, lane,
-                                   c_log2, dscale);
+          dkdv_subtile<true, DROP, HK, D>(dka, dva, Qs, Ds, rlp + 32 * qt, rdp + 32 * qt, mw, kf, vf, qs, ka, S,
+                                          lane, c_log2, dscale);
       }
       if (more) store_rows(cur ^ 1);
       mw_cur = mw_next;
@@ -845,8 +877,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     ATTN_STAMP(3);
 
     if (ka < S) {
-      store_head_row<HK>(dk + hout + (size_t)ka * out_rs, dka, scale, h, cosT, sinT, ka);
-      store_head_row<HK>(dv + hout + (size_t)ka * out_rs, dva, DROP ? dscale : 1.f, h, nullptr, nullptr, 0);
+      store_head_row<HK, D>(dk + hout + (size_t)ka * out_rs, dka, scale, h, cosT, sinT, ka);
+      store_head_row<HK, D>(dv + hout + (size_t)ka * out_rs, dva, DROP ? dscale : 1.f, h, nullptr, nullptr, 0);
     }
 #ifdef DLT_ATTN_TIMING
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -857,10 +889,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 }
 
 // ---------------------------------------------------------------------- dQ
-template <bool MASK, bool DROP, int HK = 0>
-__device__ __forceinline__ void dq_tile(floatx16_t (&dqa)[2], const bf16_t* Kt, const bf16_t* Vt,
-                                        const bf16x8_t (&qf)[4], const bf16x8_t (&df)[4], int k0, int qa, int S,
-                                        int lane, float c_log2, float nl2, float dl, float dscale, uint2 mw) {
+template <bool MASK, bool DROP, int HK, int D>
+__device__ __forceinline__ void dq_tile(floatx16_t (&dqa)[D / 32], const bf16_t* Kt, const bf16_t* Vt,
+                                        const bf16x8_t (&qf)[D / 16], const bf16x8_t (&df)[D / 16], int k0, int qa,
+                                        int S, int lane, float c_log2, float nl2, float dl, float dscale, uint2 mw) {
+  constexpr int NS = D / 16;
   const int h = lane >> 5, ql = lane & 31;
   floatx16_t sacc[2], pacc[2];
 #pragma unroll
@@ -869,22 +902,27 @@ __device__ __forceinline__ void dq_tile(floatx16_t (&dqa)[2], const bf16_t* Kt, 
     pacc[t] = zero16();
 #if DLT_ATTN_KREAD_ASM
     // the half-tile's K and V fragments in flight at once, one counted wait each
-    bf16x8_t kf[4], vf[4];
+    bf16x8_t kf[NS], vf[NS];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) kf[s] = lds_row8_asm(Kt, 32 * t + ql, 16 * s + 8 * h);
+    for (int s = 0; s < NS; ++s) kf[s] = lds_row8_asm<D>(Kt, 32 * t + ql, 16 * s + 8 * h);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) vf[s] = lds_row8_asm(Vt, 32 * t + ql, 16 * s + 8 * h);
-    lgkm_wait4(kf[0], kf[1], kf[2], kf[3]);
+    for (int s = 0; s < NS; ++s) vf[s] = lds_row8_asm<D>(Vt, 32 * t + ql, 16 * s + 8 * h);
+    if constexpr (D == 64) {
+      lgkm_wait4(kf[0], kf[1], kf[2], kf[3]);
+    } else {
+      lgkm_wait8(kf[0], kf[1], kf[2], kf[3]);
+      pin4(kf[4], kf[5], kf[6], kf[7]);
+    }
 #pragma unroll
-    for (int s = 0; s < 4; ++s) sacc[t] = mfma<HK>(kf[s], qf[s], sacc[t]);
-    tr_wait(vf[0], vf[1], vf[2], vf[3]);
+    for (int s = 0; s < NS; ++s) sacc[t] = mfma<HK>(kf[s], qf[s], sacc[t]);
+    tr_wait_all(vf);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) pacc[t] = mfma<HK>(vf[s], df[s], pacc[t]);
+    for (int s = 0; s < NS; ++s) pacc[t] = mfma<HK>(vf[s], df[s], pacc[t]);
 #else
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      sacc[t] = mfma<HK>(lds_row8(Kt, 32 * t + ql, 16 * s + 8 * h), qf[s], sacc[t]);
-      pacc[t] = mfma<HK>(lds_row8(Vt, 32 * t + ql, 16 * s + 8 * h), df[s], pacc[t]);
+    for (int s = 0; s < NS; ++s) {
+      sacc[t] = mfma<HK>(lds_row8<D>(Kt, 32 * t + ql, 16 * s + 8 * h), qf[s], sacc[t]);
+      pacc[t] = mfma<HK>(lds_row8<D>(Vt, 32 * t + ql, 16 * s + 8 * h), df[s], pacc[t]);
     }
 #endif
   }
@@ -912,12 +950,12 @@ __device__ __forceinline__ void dq_tile(floatx16_t (&dqa)[2], const bf16_t* Kt, 
   for (int kk = 0; kk < 4; ++kk) {
     const bf16x8_t sb = acc_frag<HK>(pacc[kk >> 1], kk & 1);
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt) dqa[dt] = mfma<HK>(tr_frag(Kt, kk, dt, lane), sb, dqa[dt]);
+    for (int dt = 0; dt < D / 32; ++dt) dqa[dt] = mfma<HK>(tr_frag<D>(Kt, kk, dt, lane), sb, dqa[dt]);
   }
 }
 
-template <bool DROP, int HK = 0>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_attn_bwd_dq(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
+template <bool DROP, int HK, int D>
+__global__ __launch_bounds__(NT) ATTN_WAVES(D) void k_attn_bwd_dq(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
                                                        const bf16_t* __restrict__ v, const bf16_t* __restrict__ dout,
                                                        const bf16_t* __restrict__ o,
                                                        const float* __restrict__ lse,
@@ -927,7 +965,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
                                                        long in_bs, int in_hs, int in_rs, long out_bs, int out_hs,
                                                        int out_rs, const float* __restrict__ cosT,
                                                        const float* __restrict__ sinT, int xcd_map) {
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * 2 * KVB * HD];
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * 2 * KVB * D];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, ql = lane & 31;
@@ -953,11 +991,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     const int qc = min(qa, S - 1);
     const uint32_t* mrow = mask ? mask + (size_t)bh * W * S + qc : nullptr;  // word j at mrow[j*S]
 
-    bf16x8_t qf[4], df[4];
-    const size_t orow = (((size_t)b * S + qc) * nh + head) * HD;
+    bf16x8_t qf[D / 16], df[D / 16];
+    const size_t orow = (((size_t)b * S + qc) * nh + head) * D;
     float dsum = 0.f;  // Delta = rowsum(dO * O), computed here (this kernel runs before dK/dV)
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < D / 16; ++s) {
       qf[s] = load_row8(q + hin + (size_t)qc * in_rs + 16 * s + 8 * h, qok);
       df[s] = load_row8(dout + orow + 16 * s + 8 * h, qok);
       const bf16x8_t of = load_row8(o + orow + 16 * s + 8 * h, qok);
@@ -967,11 +1005,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     const float nl2 = qok ? -lse[(size_t)bh * S + qc] * LOG2E : 0.f;
     const float dl = xhalf_sum(dsum);
     if (qok && h == 0) delta[(size_t)bh * S + qa] = dl;
-    floatx16_t dqa[2] = {zero16(), zero16()};
+    floatx16_t dqa[D / 32];
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt) dqa[dt] = zero16();
 
     const int nkv = (min(S, qb * RB + RB) + KVB - 1) / KVB;
-    glds_tile(k + hin, 0, S, in_rs, lds, wid, lane);
-    glds_tile(v + hin, 0, S, in_rs, lds + KVB * HD, wid, lane);
+    glds_tile<D>(k + hin, 0, S, in_rs, lds, wid, lane);
+    glds_tile<D>(v + hin, 0, S, in_rs, lds + KVB * D, wid, lane);
     __syncthreads();
 
     // Same loop structure as the forward: straight-line unmasked tiles (static LDS
@@ -983,18 +1023,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       constexpr bool MASKED = decltype(maskc)::value;
       const bool more = kb + 1 < nkv;
       if (more) {  // next tile straight into the other buffer (read by nobody since the last barrier)
-        bf16_t* Kn = lds + (BUF ^ 1) * 2 * KVB * HD;
-        glds_tile(k + hin, (kb + 1) * KVB, S, in_rs, Kn, wid, lane);
-        glds_tile(v + hin, (kb + 1) * KVB, S, in_rs, Kn + KVB * HD, wid, lane);
+        bf16_t* Kn = lds + (BUF ^ 1) * 2 * KVB * D;
+        glds_tile<D>(k + hin, (kb + 1) * KVB, S, in_rs, Kn, wid, lane);
+        glds_tile<D>(v + hin, (kb + 1) * KVB, S, in_rs, Kn + KVB * D, wid, lane);
         if (DROP) mw_next = make_uint2(mrow[(size_t)(2 * (kb + 1)) * S], 2 * (kb + 1) + 1 < W ? mrow[(size_t)(2 * (kb + 1) + 1) * S] : 0u);
       }
-      const bf16_t* Kt = lds + BUF * 2 * KVB * HD;
-      const bf16_t* Vt = Kt + KVB * HD;
+      const bf16_t* Kt = lds + BUF * 2 * KVB * D;
+      const bf16_t* Vt = Kt + KVB * D;
       const int k0 = kb * KVB;
       if (!MASKED)
-        dq_tile<false, DROP, HK>(dqa, Kt, Vt, qf, df, k0, qa, S, lane, c_log2, nl2, dl, dscale, mw_cur);
+        dq_tile<false, DROP, HK, D>(dqa, Kt, Vt, qf, df, k0, qa, S, lane, c_log2, nl2, dl, dscale, mw_cur);
       else if (k0 <= q0 + 31)
-        dq_tile<true, DROP, HK>(dqa, Kt, Vt, qf, df, k0, qa, S, lane, c_log2, nl2, dl, dscale, mw_cur);
+        dq_tile<true, DROP, HK, D>(dqa, Kt, Vt, qf, df, k0, qa, S, lane, c_log2, nl2, dl, dscale, mw_cur);
       mw_cur = mw_next;
       tile_barrier();
     };
@@ -1010,12 +1050,24 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     } else if (kb < nkv) {
       step(B0{}, MSK{}, kb);
     }
-    if (qok) store_head_row<HK>(dq + hout + (size_t)qa * out_rs, dqa, scale, h, cosT, sinT, qa);
+    if (qok) store_head_row<HK, D>(dq + hout + (size_t)qa * out_rs, dqa, scale, h, cosT, sinT, qa);
   }
 }
 
 // ============================================================================ launchers
 #include <cstdlib>
+// head_dim dispatch: HDC = 64 or 128 inside the body
+#define DLT_HD_DISPATCH(hd, ...) \
+  do {                           \
+    if ((hd) == 128) {           \
+      constexpr int HDC = 128;   \
+      __VA_ARGS__;               \
+    } else {                     \
+      constexpr int HDC = 64;    \
+      __VA_ARGS__;               \
+    }                            \
+  } while (0)
+static inline bool attn_hd_ok(int hd) { return hd == 64 || hd == 128; }
 // XCD-aware work map on by default; DLT_ATTN_XCD=0 restores the natural order (A/B).
 static int xcd_map_enabled() {
   static int v = -1;
@@ -1054,7 +1106,7 @@ DLT_API int dlt_attn_dropout_mask(uint32_t* mask, int B, int nh, int S, uint32_t
 DLT_API int dlt_attn_fwd_ex(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, uint32_t* mask,
                             int B, int nh, int S, int hd, float scale, uint32_t key, uint32_t thr, float dscale,
                             int gen_mask, long in_bs, int in_hs, int in_rs, int hk, hipStream_t st) {
-  if (hd != HD || S <= 0 || in_rs % 8 || in_hs % 8 || in_bs % 8) return -1;
+  if (!attn_hd_ok(hd) || S <= 0 || in_rs % 8 || in_hs % 8 || in_bs % 8) return -1;
   if (thr && !mask) return -2;  // dropout needs the keep-bit buffer
   const int nrb = (S + RB - 1) / RB;
   const int xm = xcd_map_enabled();
@@ -1065,11 +1117,11 @@ DLT_API int dlt_attn_fwd_ex(const bf16_t* q, const bf16_t* k, const bf16_t* v, b
       const int rc = dlt_attn_dropout_mask(mask, B, nh, S, key, thr, st);
       if (rc) return rc;
     }
-    DLT_HK_DISPATCH(hk, k_attn_fwd<true, HKC><<<grid, NT, 0, st>>>(q, k, v, o, lse, mask, S, nh, c_log2, dscale,
-                                                                  in_bs, in_hs, in_rs, xm));
+    DLT_HD_DISPATCH(hd, DLT_HK_DISPATCH(hk, k_attn_fwd<true, HKC, HDC><<<grid, NT, 0, st>>>(
+                                                q, k, v, o, lse, mask, S, nh, c_log2, dscale, in_bs, in_hs, in_rs, xm)));
   } else {
-    DLT_HK_DISPATCH(hk, k_attn_fwd<false, HKC><<<grid, NT, 0, st>>>(q, k, v, o, lse, nullptr, S, nh, c_log2, dscale,
-                                                                   in_bs, in_hs, in_rs, xm));
+    DLT_HD_DISPATCH(hd, DLT_HK_DISPATCH(hk, k_attn_fwd<false, HKC, HDC><<<grid, NT, 0, st>>>(
+                                                q, k, v, o, lse, nullptr, S, nh, c_log2, dscale, in_bs, in_hs, in_rs, xm)));
   }
   DLT_CHECK_LAUNCH();
 }
@@ -1078,7 +1130,7 @@ DLT_API int dlt_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16
                          int B, int nh, int S, int hd, float scale, uint32_t key, uint32_t thr, float dscale,
                          int gen_mask, int hk, hipStream_t st) {
   return dlt_attn_fwd_ex(q, k, v, o, lse, mask, B, nh, S, hd, scale, key, thr, dscale, gen_mask,
-                         (long)nh * S * HD, S * HD, HD, hk, st);
+                         (long)nh * S * hd, S * hd, hd, hk, st);
 }
 
 // dq/dk/dv use the (out_bs, out_hs, out_rs) layout; with cosT/sinT ([>= S, 32] fp32)
@@ -1089,7 +1141,8 @@ DLT_API int dlt_attn_bwd_ex(const bf16_t* q, const bf16_t* k, const bf16_t* v, c
                             bf16_t* dv, int B, int nh, int S, int hd, float scale, float dscale, long in_bs,
                             int in_hs, int in_rs, long out_bs, int out_hs, int out_rs, const float* cosT,
                             const float* sinT, int hk, hipStream_t st) {
-  if (hd != HD || S <= 0 || in_rs % 8 || in_hs % 8 || in_bs % 8 || out_rs % 4 || out_hs % 4 || out_bs % 4) return -1;
+  if (!attn_hd_ok(hd) || S <= 0 || in_rs % 8 || in_hs % 8 || in_bs % 8 || out_rs % 4 || out_hs % 4 || out_bs % 4)
+    return -1;
   if ((cosT == nullptr) != (sinT == nullptr)) return -3;
   const float c_log2 = scale * LOG2E;
   const int nrb = (S + RB - 1) / RB;
@@ -1099,19 +1152,19 @@ DLT_API int dlt_attn_bwd_ex(const bf16_t* q, const bf16_t* k, const bf16_t* v, c
   // dK/dV then reads.
   if (mask) {
     const uint32_t* maskT = mask + (size_t)B * nh * S * ((S + 31) / 32);
-    DLT_HK_DISPATCH(hk, k_attn_bwd_dq<true, HKC><<<gq, NT, 0, st>>>(
+    DLT_HD_DISPATCH(hd, DLT_HK_DISPATCH(hk, k_attn_bwd_dq<true, HKC, HDC><<<gq, NT, 0, st>>>(
                             q, k, v, dout, o, lse, delta_ws, mask, dq, S, nh, c_log2, scale, dscale, in_bs, in_hs,
-                            in_rs, out_bs, out_hs, out_rs, cosT, sinT, xm));
-    DLT_HK_DISPATCH(hk, k_attn_bwd_dkdv<true, HKC><<<gk, NT, 0, st>>>(
+                            in_rs, out_bs, out_hs, out_rs, cosT, sinT, xm)));
+    DLT_HD_DISPATCH(hd, DLT_HK_DISPATCH(hk, k_attn_bwd_dkdv<true, HKC, HDC><<<gk, NT, 0, st>>>(
                             q, k, v, dout, lse, delta_ws, maskT, dk, dv, S, nh, c_log2, scale, dscale, in_bs, in_hs,
-                            in_rs, out_bs, out_hs, out_rs, cosT, sinT, xm));
+                            in_rs, out_bs, out_hs, out_rs, cosT, sinT, xm)));
   } else {
-    DLT_HK_DISPATCH(hk, k_attn_bwd_dq<false, HKC><<<gq, NT, 0, st>>>(
+    DLT_HD_DISPATCH(hd, DLT_HK_DISPATCH(hk, k_attn_bwd_dq<false, HKC, HDC><<<gq, NT, 0, st>>>(
                             q, k, v, dout, o, lse, delta_ws, mask, dq, S, nh, c_log2, scale, dscale, in_bs, in_hs,
-                            in_rs, out_bs, out_hs, out_rs, cosT, sinT, xm));
-    DLT_HK_DISPATCH(hk, k_attn_bwd_dkdv<false, HKC><<<gk, NT, 0, st>>>(
+                            in_rs, out_bs, out_hs, out_rs, cosT, sinT, xm)));
+    DLT_HD_DISPATCH(hd, DLT_HK_DISPATCH(hk, k_attn_bwd_dkdv<false, HKC, HDC><<<gk, NT, 0, st>>>(
                             q, k, v, dout, lse, delta_ws, mask, dk, dv, S, nh, c_log2, scale, dscale, in_bs, in_hs,
-                            in_rs, out_bs, out_hs, out_rs, cosT, sinT, xm));
+                            in_rs, out_bs, out_hs, out_rs, cosT, sinT, xm)));
   }
   DLT_CHECK_LAUNCH();
 }
@@ -1119,7 +1172,7 @@ DLT_API int dlt_attn_bwd_ex(const bf16_t* q, const bf16_t* k, const bf16_t* v, c
 DLT_API int dlt_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,
                          const float* lse, const uint32_t* mask, float* delta_ws, bf16_t* dq, bf16_t* dk, bf16_t* dv,
                          int B, int nh, int S, int hd, float scale, float dscale, int hk, hipStream_t st) {
-  const long bs = (long)nh * S * HD;
-  return dlt_attn_bwd_ex(q, k, v, o, dout, lse, mask, delta_ws, dq, dk, dv, B, nh, S, hd, scale, dscale, bs, S * HD,
-                         HD, bs, S * HD, HD, nullptr, nullptr, hk, st);
+  const long bs = (long)nh * S * hd;
+  return dlt_attn_bwd_ex(q, k, v, o, dout, lse, mask, delta_ws, dq, dk, dv, B, nh, S, hd, scale, dscale, bs, S * hd,
+                         hd, bs, S * hd, hd, nullptr, nullptr, hk, st);
 }

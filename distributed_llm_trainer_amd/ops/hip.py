@@ -22,7 +22,7 @@ from . import rng
 _LIB = None
 # DLT_KERNEL_DEBUG=1 loads the bounds-checked build (ops/build.py --debug);
 # DLT_KERNEL_LIB=<file in ops/> loads another build of the same sources (same-box A/B
-# of a kernel change: tools/ab/ab_kernels.sh)
+# of a kernel change: tools/ab/kernels_ab.sh)
 _LIBPATH = os.path.join(os.path.dirname(os.path.abspath(__file__)),
                         "_dlt_kernels_debug.so" if os.environ.get("DLT_KERNEL_DEBUG") == "1"
                         else os.path.basename(os.environ.get("DLT_KERNEL_LIB", "_dlt_kernels.so")))
@@ -108,7 +108,8 @@ def lib():
                 "`python -m distributed_llm_trainer_amd.ops.build` (or __graft_entry__.build()).")
         import torch  # noqa: F401  (load torch's HIP runtime first so the .so binds to it)
         L = ctypes.CDLL(_LIBPATH)
-        for name, argt in _SIGS.items():
+        from . import hip_f32
+        for name, argt in {**_SIGS, **hip_f32.SIGS}.items():
             fn = getattr(L, name)
             fn.argtypes = argt
             fn.restype = c_int
@@ -339,6 +340,9 @@ def _norm_weight(weight: torch.Tensor, H: int, name: str, act=torch.bfloat16):
 
 
 def add_dropout_rmsnorm_fwd(resid, delta, weight, eps, p, key, out_dtype=torch.bfloat16, y_out=None):
+    if out_dtype == torch.float32:
+        from . import hip_f32
+        return hip_f32.add_dropout_rmsnorm_fwd(resid, delta, weight, eps, p, key, y_out=y_out)
     src = resid if resid is not None else delta
     M, H = src.shape
     if out_dtype not in _HK:
@@ -366,6 +370,10 @@ def add_dropout_rmsnorm_fwd(resid, delta, weight, eps, p, key, out_dtype=torch.b
 
 def rmsnorm_bwd(dy, x, rstd, weight, dres, dweight, p_prev, key_prev, dy_scale=None, want_ddelta=True,
                 ddelta_out=None, dy_mul: float = 1.0):
+    if dy.dtype == torch.float32:
+        from . import hip_f32
+        return hip_f32.rmsnorm_bwd(dy, x, rstd, weight, dres, dweight, p_prev, key_prev, dy_scale, want_ddelta, ddelta_out,
+                                   dy_mul)
     M, H = x.shape
     act = dy.dtype
     hk = _req_act(dy, act, "rmsnorm_bwd.dy", M * H)
@@ -395,6 +403,9 @@ def rmsnorm_bwd(dy, x, rstd, weight, dres, dweight, p_prev, key_prev, dy_scale=N
 
 # ------------------------------------------------------------------- RoPE
 def rope_qkv_fwd(qkv, B, S, nh, cos, sin):
+    if qkv.dtype == torch.float32:
+        from . import hip_f32
+        return hip_f32.rope_qkv_fwd(qkv, B, S, nh, cos, sin)
     M, threeH = qkv.shape
     hd = threeH // (3 * nh)
     if M != B * S or hd * 3 * nh != threeH:
@@ -411,6 +422,9 @@ def rope_qkv_fwd(qkv, B, S, nh, cos, sin):
 
 
 def rope_qkv_bwd(dq, dk, dv, cos, sin, out=None):
+    if dk.dtype == torch.float32:
+        from . import hip_f32
+        return hip_f32.rope_qkv_bwd(dq, dk, dv, cos, sin, out=out)
     B, nh, S, hd = dk.shape
     act = dk.dtype
     for t, n in ((dk, "dk"), (dv, "dv")):
@@ -429,6 +443,9 @@ def rope_qkv_bwd(dq, dk, dv, cos, sin, out=None):
 
 def rope_qk_inplace(qkv, B, S, nh, cos, sin):
     """Rotate the q and k column blocks of the packed [B*S, 3H] QKV in place."""
+    if qkv.dtype == torch.float32:
+        from . import hip_f32
+        return hip_f32.rope_qk_inplace(qkv, B, S, nh, cos, sin)
     M, threeH = qkv.shape
     hd = threeH // (3 * nh)
     if M != B * S or hd * 3 * nh != threeH or hd % 16:
@@ -452,6 +469,10 @@ class AttnAux(tuple):
     [0] = bits by (key word, query), [1] = bits by (query word, key); word-major)."""
 
 
+# head dims of the 16-bit MFMA attention kernels (template parameter D of attention.hip)
+ATTN_HEAD_DIMS = (64, 128)
+
+
 def attention_dropout_mask(B, nh, S, p, key, device=None):
     """Keep-bit masks [2, B*nh, ceil(S/32), S] for attention dropout (None if p == 0).
     Data-independent, so the engine builds them on a side stream ahead of time."""
@@ -467,13 +488,16 @@ def attention_fwd(q, k, v, p, key, causal=True, store_mask=True, out=None, mask=
     """Returns (o [B*S, nh*hd] bf16, aux).  With dropout on, the keep bits are written
     to a bitmask consumed by attention_bwd (no re-hashing in the backward); pass
     ``mask`` from ``attention_dropout_mask`` to skip generating it here."""
+    if q.dtype == torch.float32:
+        from . import hip_f32
+        return hip_f32.attention_fwd(q, k, v, p, key, causal, store_mask=store_mask, out=out, mask=mask)
     if not causal:
         raise NotImplementedError("only causal attention is implemented (the model is a causal LM)")
     B, nh, S, hd = q.shape
     for t, n in ((q, "q"), (k, "k"), (v, "v")):
         hk = _req_act(t, q.dtype, "attn." + n, B * nh * S * hd)
-    if hd != 64:
-        raise NotImplementedError(f"attention kernel is specialised for head_dim 64 (got {hd})")
+    if hd not in ATTN_HEAD_DIMS:
+        raise NotImplementedError(f"attention kernels take head_dim {ATTN_HEAD_DIMS} (got {hd})")
     o = torch.empty(B * S, nh * hd, dtype=q.dtype, device=q.device) if out is None else out
     _req(o, q.dtype, "attn.o", B * S * nh * hd)
     lse = torch.empty(B, nh, S, dtype=torch.float32, device=q.device)
@@ -499,8 +523,8 @@ def _packed_dims(qkv, B, S, nh):
     hd = threeH // (3 * nh)
     if M != B * S or hd * 3 * nh != threeH:
         raise ValueError("packed attention: qkv must be [B*S, 3*nh*hd]")
-    if hd != 64:
-        raise NotImplementedError(f"attention kernel is specialised for head_dim 64 (got {hd})")
+    if hd not in ATTN_HEAD_DIMS:
+        raise NotImplementedError(f"attention kernels take head_dim {ATTN_HEAD_DIMS} (got {hd})")
     _req_act(qkv, qkv.dtype, "attn.qkv")
     return M, nh * hd, hd
 
@@ -508,6 +532,9 @@ def _packed_dims(qkv, B, S, nh):
 def attention_fwd_packed(qkv, B, S, nh, p, key, out=None, mask=None, store_mask=True):
     """Causal attention reading q/k/v straight from the packed (roped) [B*S, 3H] QKV.
     Returns (o [B*S, H] bf16, aux) like :func:`attention_fwd`."""
+    if qkv.dtype == torch.float32:
+        from . import hip_f32
+        return hip_f32.attention_fwd_packed(qkv, B, S, nh, p, key, out=out, mask=mask, store_mask=store_mask)
     M, H, hd = _packed_dims(qkv, B, S, nh)
     hk = _HK[qkv.dtype]
     o = torch.empty(M, H, dtype=qkv.dtype, device=qkv.device) if out is None else out
@@ -533,6 +560,9 @@ def attention_bwd_packed(qkv, o, do, aux, p, key, B, S, nh, cos, sin, out=None):
     """Backward of :func:`attention_fwd_packed` + the in-place RoPE: returns dqkv
     [B*S, 3H] (gradient w.r.t. the pre-rotation QKV GEMM output); dq/dk/dv are written
     into it by the attention kernels with the inverse rotation in their epilogue."""
+    if qkv.dtype == torch.float32:
+        from . import hip_f32
+        return hip_f32.attention_bwd_packed(qkv, o, do, aux, p, key, B, S, nh, cos, sin, out=out)
     M, H, hd = _packed_dims(qkv, B, S, nh)
     hk = _HK[qkv.dtype]
     for t, nm in ((o, "o"), (do, "do")):
@@ -560,6 +590,9 @@ def attention_bwd_packed(qkv, o, do, aux, p, key, B, S, nh, cos, sin, out=None):
 
 
 def attention_bwd(q, k, v, o, do, aux, p, key, causal=True):
+    if q.dtype == torch.float32:
+        from . import hip_f32
+        return hip_f32.attention_bwd(q, k, v, o, do, aux, p, key, causal)
     B, nh, S, hd = q.shape
     n = B * nh * S * hd
     for t, nm in ((q, "q"), (k, "k"), (v, "v"), (o, "o"), (do, "do")):
@@ -586,6 +619,9 @@ def attention_bwd(q, k, v, o, do, aux, p, key, causal=True):
 
 # ----------------------------------------------------------------- SwiGLU
 def swiglu_fwd(gu, out=None):
+    if gu.dtype == torch.float32:
+        from . import hip_f32
+        return hip_f32.swiglu_fwd(gu, out=out)
     M, twoI = gu.shape
     hk = _req_act(gu, gu.dtype, "swiglu.gu")
     if out is None:
@@ -597,6 +633,9 @@ def swiglu_fwd(gu, out=None):
 
 def swiglu_bwd(gu, da, out=None, s_out=None):
     """dgu = SwiGLU backward; ``s_out``: also writes s = silu(g) * u (the forward's bits)."""
+    if gu.dtype == torch.float32:
+        from . import hip_f32
+        return hip_f32.swiglu_bwd(gu, da, out=out, s_out=s_out)
     M, twoI = gu.shape
     hk = _req_act(gu, gu.dtype, "swiglu_bwd.gu")
     _req(da, gu.dtype, "swiglu_bwd.da", M * twoI // 2)
@@ -615,6 +654,9 @@ def cross_entropy_fwd_bwd(logits, targets, vocab, n_valid, grad_scale: float = 1
     """Per-row loss; the logits buffer (bf16 or fp16) is overwritten by
     grad_scale * (softmax - onehot) / n_valid (fp16: grad_scale = the loss scale, so the
     gradient does not underflow)."""
+    if logits.dtype == torch.float32:
+        from . import hip_f32
+        return hip_f32.cross_entropy_fwd_bwd(logits, targets, vocab, n_valid, grad_scale)
     M, Vp = logits.shape
     hk = _req_act(logits, logits.dtype, "ce.logits")
     targets = targets.contiguous()
@@ -770,16 +812,20 @@ def gemm_wgrad_sk(dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, shares: i
 # later K-iterations 6461 -> 4909 cycles); tools/cpp/gemm_stamps.cpp and
 # profiles/r4_gemm_forward.md.  DLT_GEMM_FLAGS=n replaces them (bits 256 / 1024 / 2048 / 12).
 _GB_DEFAULT_FLAGS = 2048 | 1024 | 12
-_GB_FLAGS = (int(os.environ.get("DLT_GEMM_FLAGS", str(_GB_DEFAULT_FLAGS))) & (256 | 1024 | 2048 | 12)) | \
+_GB_FLAG_BITS = 256 | 512 | 1024 | 2048 | 4096 | 12 | (0xff << 24)  # (512 + bits 24-31: start-delay ablation)
+_GB_FLAGS = (int(os.environ.get("DLT_GEMM_FLAGS", str(_GB_DEFAULT_FLAGS))) & _GB_FLAG_BITS) | \
     ((min(int(os.environ.get("DLT_GEMM_GRID", "0")), 2040) // 8) << 16)
-# extra flag bits for the FORWARD projection GEMMs only (plain / RoPE / SwiGLU epilogues):
-# DLT_GEMM_FWD_FLAGS=256 runs them one tile per workgroup (grid = tiles) while the data
-# gradients keep the persistent grid (A/B knob for the two-chain window)
-_GB_FWD_EXTRA = int(os.environ.get("DLT_GEMM_FWD_FLAGS", "0")) & 256
+# launch flags of the FORWARD projection GEMMs only (plain / RoPE / SwiGLU epilogues),
+# A/B knob for the two-chain window: DLT_GEMM_FWD_FLAGS=n replaces their flag bits (e.g.
+# 256 | 3084: one tile per workgroup, grid = tiles) while the data gradients keep
+# DLT_GEMM_FLAGS; the grid cap of gemm_grid_cap applies to both
+_GB_FWD_OVERRIDE = os.environ.get("DLT_GEMM_FWD_FLAGS")
 
 
 def _fwd_flags() -> int:
-    return _GB_FLAGS | _GB_FWD_EXTRA
+    if _GB_FWD_OVERRIDE is None:
+        return _GB_FLAGS
+    return (int(_GB_FWD_OVERRIDE) & _GB_FLAG_BITS) | (_GB_FLAGS & (0xff << 16))
 
 
 def gemm_grid_cap(n: int) -> int:
@@ -789,7 +835,7 @@ def gemm_grid_cap(n: int) -> int:
     change.  The ``ffbb`` window sets 192: the other chain's kernels keep 64 CUs."""
     global _GB_FLAGS
     prev = 8 * ((_GB_FLAGS >> 16) & 0xff)
-    _GB_FLAGS = (_GB_FLAGS & 0xffff) | ((min(max(int(n), 0), 2040) // 8) << 16)
+    _GB_FLAGS = (_GB_FLAGS & ~(0xff << 16)) | ((min(max(int(n), 0), 2040) // 8) << 16)
     return prev
 
 
@@ -906,6 +952,9 @@ def scale_bf16(x: torch.Tensor, scale: torch.Tensor, out: Optional[torch.Tensor]
                mul: float = 1.0) -> torch.Tensor:
     """y = x * scale * mul with a device scalar (no host sync) and a host factor, x bf16
     or fp16; falls back for odd sizes."""
+    if x.dtype == torch.float32:
+        from . import hip_f32
+        return hip_f32.scale(x, scale, out=out, mul=mul)
     hk = _req_act(x, x.dtype, "scale_bf16.x")
     s = scale.reshape(1).float().contiguous()
     if x.numel() % 8:

@@ -1,0 +1,294 @@
+"""fp32-activation wrappers (``csrc/fp32.hip``) behind the op functions of ``ops/hip.py``.
+
+``hip.<op>`` hands over here when its activation tensor is fp32: the engine's
+``--mixed_precision fp32`` mode (the reference's fp32 path, ``ddp_trainer.py:137-139``)
+then runs HIP kernels for every non-GEMM op, as bf16 / fp16 do; the GEMMs are hipBLASLt
+fp32.  Same semantics and dropout bits as ``ops/reference.py``; attention supports
+head_dim 64 and 128.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+
+from . import rng
+
+c_void_p, c_int, c_float, c_uint32, c_long = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_uint32, ctypes.c_long
+
+SIGS = {
+    "dlt_f32_norm_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_uint32,
+                         c_uint32, c_float, c_void_p],
+    "dlt_f32_norm_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_void_p, c_float, c_int, c_int, c_uint32, c_uint32, c_float, c_void_p],
+    "dlt_f32_rope": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_long, c_long, c_long, c_long,
+                     c_long, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_int, c_void_p],
+    "dlt_f32_swiglu_fwd": [c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "dlt_f32_swiglu_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "dlt_f32_cross_entropy": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p],
+    "dlt_f32_scale": [c_void_p, c_void_p, c_long, c_void_p, c_float, c_void_p],
+    "dlt_f32_attn_fwd": [c_void_p, c_void_p, c_void_p, c_long, c_long, c_long, c_void_p, c_void_p, c_void_p, c_int,
+                         c_int, c_int, c_int, c_float, c_float, c_void_p],
+    "dlt_f32_attn_bwd": [c_void_p, c_void_p, c_void_p, c_long, c_long, c_long, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_long, c_long, c_int, c_int, c_int, c_int,
+                         c_float, c_float, c_void_p],
+}
+
+ATTN_HEAD_DIMS = (64, 128)
+
+
+def _h():
+    from . import hip
+    return hip
+
+
+def _req32(t: torch.Tensor, name: str, numel=None):
+    _h()._req(t, torch.float32, name, numel)
+
+
+def _chk(rc, name):
+    _h()._chk(rc, name)
+
+
+def _p(t):
+    return _h()._p(t)
+
+
+def _st():
+    return _h()._stream()
+
+
+def _lib():
+    return _h().lib()
+
+
+# ---------------------------------------------------------------- RMSNorm
+def add_dropout_rmsnorm_fwd(resid, delta, weight, eps, p, key, y_out=None):
+    src = resid if resid is not None else delta
+    M, H = src.shape
+    for t, n in ((resid, "resid"), (delta, "delta")):
+        if t is not None:
+            _req32(t, "rmsnorm_f32." + n, M * H)
+    w = weight.float().contiguous()
+    if w.numel() != H:
+        raise ValueError("rmsnorm_f32.weight: expected H elements")
+    y = torch.empty(M, H, dtype=torch.float32, device=src.device) if y_out is None else y_out
+    _req32(y, "rmsnorm_f32.y", M * H)
+    rstd = torch.empty(M, dtype=torch.float32, device=src.device)
+    if delta is None:
+        x, xo = resid, None
+    else:
+        x = torch.empty(M, H, dtype=torch.float32, device=src.device)
+        xo = x
+    thr = rng.keep_threshold(p)
+    dscale = 1.0 / (1.0 - p) if thr else 1.0
+    _chk(_lib().dlt_f32_norm_fwd(_p(resid), _p(delta), _p(w), _p(xo), _p(y), _p(rstd), M, H, float(eps),
+                                 key & 0xFFFFFFFF, thr, dscale, _st()), "f32_norm_fwd")
+    return x, y, rstd
+
+
+def rmsnorm_bwd(dy, x, rstd, weight, dres, dweight, p_prev, key_prev, dy_scale=None, want_ddelta=True,
+                ddelta_out=None, dy_mul: float = 1.0):
+    M, H = x.shape
+    _req32(dy, "rmsnorm_bwd_f32.dy", M * H)
+    _req32(x, "rmsnorm_bwd_f32.x", M * H)
+    _req32(rstd, "rmsnorm_bwd_f32.rstd", M)
+    if dres is not None:
+        _req32(dres, "rmsnorm_bwd_f32.dres", M * H)
+    _req32(dweight, "rmsnorm_bwd_f32.dweight", H)
+    w = weight.float().contiguous()
+    scale_t = dy_scale.reshape(1).float().contiguous() if dy_scale is not None else None
+    dx = torch.empty(M, H, dtype=torch.float32, device=x.device)
+    dd = None
+    if want_ddelta:
+        dd = torch.empty(M, H, dtype=torch.float32, device=x.device) if ddelta_out is None else ddelta_out
+        _req32(dd, "rmsnorm_bwd_f32.ddelta", M * H)
+    thr = rng.keep_threshold(p_prev)
+    dscale = 1.0 / (1.0 - p_prev) if thr else 1.0
+    nb = min(1024, (M + 3) // 4)
+    ws = torch.empty(max(nb, 1) * H, dtype=torch.float32, device=x.device)
+    _chk(_lib().dlt_f32_norm_bwd(_p(dy), _p(x), _p(rstd), _p(w), _p(dres), _p(dx), _p(dd), _p(dweight), _p(ws),
+                                 _p(scale_t), float(dy_mul), M, H, key_prev & 0xFFFFFFFF, thr, dscale, _st()),
+         "f32_norm_bwd")
+    return dx, dd
+
+
+# ------------------------------------------------------------------- RoPE
+def rope_qk_inplace(qkv, B, S, nh, cos, sin, sign: float = 1.0):
+    M, threeH = qkv.shape
+    hd = threeH // (3 * nh)
+    _req32(qkv, "rope_qk_f32.qkv")
+    H = nh * hd
+    base = qkv.data_ptr()
+    ptr = [ctypes.c_void_p(base + j * H * 4) for j in range(3)]
+    st = (S * threeH, threeH, hd)
+    if cos.shape[0] < S or cos.shape[1] != hd // 2 or sin.shape != cos.shape:
+        raise ValueError("rope tables too short")
+    c, s = cos.contiguous(), sin.contiguous()
+    _chk(_lib().dlt_f32_rope(*ptr, *ptr, *st, *st, _p(c), _p(s), B, S, nh, hd, float(sign), 2, _st()), "f32_rope_qk")
+    return qkv
+
+
+def rope_qkv_fwd(qkv, B, S, nh, cos, sin):
+    M, threeH = qkv.shape
+    hd = threeH // (3 * nh)
+    _req32(qkv, "rope_qkv_f32.qkv")
+    q = torch.empty(B, nh, S, hd, dtype=torch.float32, device=qkv.device)
+    k, v = torch.empty_like(q), torch.empty_like(q)
+    H = nh * hd
+    src = [ctypes.c_void_p(qkv.data_ptr() + j * H * 4) for j in range(3)]
+    c, s = cos.contiguous(), sin.contiguous()
+    if c.shape[0] < S or c.shape[1] != hd // 2:
+        raise ValueError("rope tables too short")
+    _chk(_lib().dlt_f32_rope(*src, _p(q), _p(k), _p(v), S * threeH, threeH, hd, nh * S * hd, hd, S * hd, _p(c), _p(s),
+                             B, S, nh, hd, 1.0, 3, _st()), "f32_rope_qkv")
+    return q, k, v
+
+
+def rope_qkv_bwd(dq, dk, dv, cos, sin, out=None):
+    B, nh, S, hd = dk.shape
+    for t, n in ((dq, "dq"), (dk, "dk"), (dv, "dv")):
+        _req32(t.contiguous(), "rope_bwd_f32." + n)
+    dq, dk, dv = dq.contiguous(), dk.contiguous(), dv.contiguous()
+    H = nh * hd
+    if out is None:
+        out = torch.empty(B * S, 3 * H, dtype=torch.float32, device=dk.device)
+    _req32(out, "rope_bwd_f32.out", B * S * 3 * H)
+    dst = [ctypes.c_void_p(out.data_ptr() + j * H * 4) for j in range(3)]
+    c, s = cos.contiguous(), sin.contiguous()
+    _chk(_lib().dlt_f32_rope(_p(dq), _p(dk), _p(dv), *dst, nh * S * hd, hd, S * hd, S * 3 * H, 3 * H, hd, _p(c), _p(s),
+                             B, S, nh, hd, -1.0, 3, _st()), "f32_rope_qkv_bwd")
+    return out
+
+
+# -------------------------------------------------------------- attention
+def _check_hd(hd):
+    if hd not in ATTN_HEAD_DIMS:
+        raise NotImplementedError(f"fp32 attention kernels take head_dim 64 or 128 (got {hd})")
+
+
+def _mask(B, nh, S, p, key, device, mask=None):
+    thr = rng.keep_threshold(p)
+    if not thr:
+        return None, 1.0
+    if mask is None:
+        mask = _h().attention_dropout_mask(B, nh, S, p, key, device=device)
+    return mask, 1.0 / (1.0 - p)
+
+
+def _fwd(qp, kp, vp, strides, B, nh, S, hd, p, key, device, out, mask, store_mask=True):
+    _check_hd(hd)
+    o = torch.empty(B * S, nh * hd, dtype=torch.float32, device=device) if out is None else out
+    _req32(o, "attn_f32.o", B * S * nh * hd)
+    lse = torch.empty(B, nh, S, dtype=torch.float32, device=device)
+    mask, dscale = _mask(B, nh, S, p, key, device, mask)
+    _chk(_lib().dlt_f32_attn_fwd(qp, kp, vp, *strides, _p(o), _p(lse), _p(mask), B, nh, S, hd, 1.0 / math.sqrt(hd),
+                                 dscale, _st()), "f32_attn_fwd")
+    # store_mask=False: the keep bits only live for this call (the backward regenerates them)
+    return o, _h().AttnAux((lse, mask if store_mask else None))
+
+
+def attention_fwd(q, k, v, p, key, causal=True, store_mask=True, out=None, mask=None):
+    if not causal:
+        raise NotImplementedError("only causal attention is implemented (the model is a causal LM)")
+    B, nh, S, hd = q.shape
+    for t, n in ((q, "q"), (k, "k"), (v, "v")):
+        _req32(t, "attn_f32." + n, B * nh * S * hd)
+    return _fwd(_p(q), _p(k), _p(v), (nh * S * hd, S * hd, hd), B, nh, S, hd, p, key, q.device, out, mask,
+                store_mask)
+
+
+def attention_fwd_packed(qkv, B, S, nh, p, key, out=None, mask=None, store_mask=True):
+    M, threeH = qkv.shape
+    hd = threeH // (3 * nh)
+    if M != B * S or hd * 3 * nh != threeH:
+        raise ValueError("packed attention: qkv must be [B*S, 3*nh*hd]")
+    _req32(qkv, "attn_f32.qkv")
+    H = nh * hd
+    ptr = [ctypes.c_void_p(qkv.data_ptr() + j * H * 4) for j in range(3)]
+    return _fwd(*ptr, (S * threeH, hd, threeH), B, nh, S, hd, p, key, qkv.device, out, mask, store_mask)
+
+
+def _bwd(qp, kp, vp, strides, o, do, aux, B, nh, S, hd, p, key, device, gp, gstrides):
+    _check_hd(hd)
+    lse, mask = aux if isinstance(aux, tuple) else (aux, None)
+    _req32(lse, "attn_bwd_f32.lse", B * nh * S)
+    _req32(o, "attn_bwd_f32.o", B * S * nh * hd)
+    _req32(do, "attn_bwd_f32.do", B * S * nh * hd)
+    mask, dscale = _mask(B, nh, S, p, key, device, mask)
+    delta = torch.empty(B, nh, S, dtype=torch.float32, device=device)
+    _chk(_lib().dlt_f32_attn_bwd(qp, kp, vp, *strides, _p(o), _p(do), _p(lse), _p(mask), _p(delta), *gp, *gstrides,
+                                 B, nh, S, hd, 1.0 / math.sqrt(hd), dscale, _st()), "f32_attn_bwd")
+
+
+def attention_bwd(q, k, v, o, do, aux, p, key, causal=True):
+    B, nh, S, hd = q.shape
+    for t, n in ((q, "q"), (k, "k"), (v, "v")):
+        _req32(t, "attn_bwd_f32." + n, B * nh * S * hd)
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    st = (nh * S * hd, S * hd, hd)
+    _bwd(_p(q), _p(k), _p(v), st, o, do, aux, B, nh, S, hd, p, key, q.device, (_p(dq), _p(dk), _p(dv)), st)
+    return dq, dk, dv
+
+
+def attention_bwd_packed(qkv, o, do, aux, p, key, B, S, nh, cos, sin, out=None):
+    """dqkv [B*S, 3H] (pre-RoPE): the attention backward writes raw dq / dk / dv into the
+    packed layout, then the inverse rotation runs in place on the q and k blocks."""
+    M, threeH = qkv.shape
+    hd = threeH // (3 * nh)
+    _req32(qkv, "attn_bwd_f32.qkv")
+    H = nh * hd
+    dqkv = torch.empty(M, threeH, dtype=torch.float32, device=qkv.device) if out is None else out
+    _req32(dqkv, "attn_bwd_f32.dqkv", M * threeH)
+    src = [ctypes.c_void_p(qkv.data_ptr() + j * H * 4) for j in range(3)]
+    dst = [ctypes.c_void_p(dqkv.data_ptr() + j * H * 4) for j in range(3)]
+    st = (S * threeH, hd, threeH)
+    _bwd(*src, st, o, do, aux, B, nh, S, hd, p, key, qkv.device, dst, st)
+    rope_qk_inplace(dqkv, B, S, nh, cos, sin, sign=-1.0)
+    return dqkv
+
+
+# ----------------------------------------------------------------- SwiGLU
+def swiglu_fwd(gu, out=None):
+    M, twoI = gu.shape
+    _req32(gu, "swiglu_f32.gu")
+    out = torch.empty(M, twoI // 2, dtype=torch.float32, device=gu.device) if out is None else out
+    _req32(out, "swiglu_f32.out", M * twoI // 2)
+    _chk(_lib().dlt_f32_swiglu_fwd(_p(gu), _p(out), M, twoI // 2, _st()), "f32_swiglu_fwd")
+    return out
+
+
+def swiglu_bwd(gu, da, out=None, s_out=None):
+    M, twoI = gu.shape
+    _req32(gu, "swiglu_bwd_f32.gu")
+    _req32(da, "swiglu_bwd_f32.da", M * twoI // 2)
+    out = torch.empty_like(gu) if out is None else out
+    _req32(out, "swiglu_bwd_f32.out", M * twoI)
+    if s_out is not None:
+        _req32(s_out, "swiglu_bwd_f32.s_out", M * twoI // 2)
+    _chk(_lib().dlt_f32_swiglu_bwd(_p(gu), _p(da), _p(out), _p(s_out), M, twoI // 2, _st()), "f32_swiglu_bwd")
+    return out
+
+
+# ------------------------------------------------------------ cross-entropy
+def cross_entropy_fwd_bwd(logits, targets, vocab, n_valid, grad_scale: float = 1.0):
+    M, Vp = logits.shape
+    _req32(logits, "ce_f32.logits")
+    targets = targets.contiguous()
+    if targets.dtype != torch.int64 or targets.numel() != M:
+        raise ValueError("ce.targets must be int64 [M]")
+    nv = n_valid.reshape(1).to(torch.int64).contiguous()
+    loss = torch.empty(M, dtype=torch.float32, device=logits.device)
+    _chk(_lib().dlt_f32_cross_entropy(_p(logits), _p(targets), _p(nv), _p(loss), M, Vp, vocab, float(grad_scale),
+                                      _st()), "f32_cross_entropy")
+    return loss
+
+
+def scale(x, s, out=None, mul: float = 1.0):
+    s = s.reshape(1).float().contiguous()
+    _req32(x, "scale_f32.x")
+    y = torch.empty_like(x) if out is None else out
+    _req32(y, "scale_f32.out", x.numel())
+    _chk(_lib().dlt_f32_scale(_p(x), _p(y), x.numel(), _p(s), float(mul), _st()), "f32_scale")
+    return y

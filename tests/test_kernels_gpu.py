@@ -198,19 +198,23 @@ def test_adamw_and_norm():
     _close(sh, p.bfloat16(), 0.0, 0.0, "shadow")
 
 
-def _attn_inputs(B, nh, S, seed):
+def _attn_inputs(B, nh, S, seed, hd=64):
     torch.manual_seed(seed)
-    q = torch.randn(B, nh, S, 64, device=DEV).bfloat16()
-    k = torch.randn(B, nh, S, 64, device=DEV).bfloat16()
-    v = torch.randn(B, nh, S, 64, device=DEV).bfloat16()
+    q = torch.randn(B, nh, S, hd, device=DEV).bfloat16()
+    k = torch.randn(B, nh, S, hd, device=DEV).bfloat16()
+    v = torch.randn(B, nh, S, hd, device=DEV).bfloat16()
     return q, k, v
 
 
-@pytest.mark.parametrize("S", [64, 128, 200, 1024, 2100])
+# head_dim 128 (template D = 128 of attention.hip) on a subset of the sequence lengths
+_ATTN_FWD_CASES = [(S, 64) for S in (64, 128, 200, 1024, 2100)] + [(S, 128) for S in (64, 200, 1024)]
+
+
+@pytest.mark.parametrize("S,hd", _ATTN_FWD_CASES)
 @pytest.mark.parametrize("p", [0.0, 0.1])
-def test_attention_fwd(S, p):
+def test_attention_fwd(S, hd, p):
     B, nh = 2, 3
-    q, k, v = _attn_inputs(B, nh, S, 10 + S)
+    q, k, v = _attn_inputs(B, nh, S, 10 + S, hd)
     key = rng.site_key(1, 2, 3, rng.SITE_ATTN)
     o, aux = hip.attention_fwd(q, k, v, p, key)
     lse = aux[0]
@@ -248,9 +252,10 @@ def test_attention_fwd_identity_asymmetric():
 
 @pytest.mark.parametrize("S", [64, 192, 1024])
 @pytest.mark.parametrize("p", [0.0, 0.1])
-def test_attention_bwd(S, p):
+@pytest.mark.parametrize("hd", [64, 128])
+def test_attention_bwd(S, p, hd):
     B, nh = 2, 3
-    q, k, v = _attn_inputs(B, nh, S, 20 + S)
+    q, k, v = _attn_inputs(B, nh, S, 20 + S, hd)
     key = rng.site_key(4, 5, 6, rng.SITE_ATTN)
     o, lse = ref.attention_fwd(q, k, v, p, key)
     do = torch.randn_like(o.float()).bfloat16()
@@ -278,11 +283,12 @@ def test_rope_qk_inplace():
 
 @pytest.mark.parametrize("S", [64, 200, 1024])
 @pytest.mark.parametrize("p", [0.0, 0.1])
-def test_attention_packed_fwd_bwd(S, p):
+@pytest.mark.parametrize("hd", [64, 128])
+def test_attention_packed_fwd_bwd(S, p, hd):
     """Attention straight on the packed QKV (strided q/k/v) with the inverse RoPE in the
     backward epilogue == the split path (RoPE copy kernel, head-major attention, repack)."""
     torch.manual_seed(32 + S)
-    B, nh, hd = 2, 3, 64
+    B, nh = 2, 3
     H = nh * hd
     raw = torch.randn(B * S, 3 * H, device=DEV).bfloat16()
     cos, sin = hip.rope_tables(hd, 1024, device=DEV)
@@ -557,11 +563,20 @@ def test_gemm_bf16(M, N, K):
     assert hip.gemm_bf16(a[:, :K - 64].contiguous(), b[:, :K - 64].contiguous()) is None  # K % 128
 
 
+@pytest.fixture(params=[0, 4096], ids=["stage-in-loop", "epilogue-first"])
+def gemm_late_flag(request, monkeypatch):
+    """Runs a test with and without flags bit 4096 (epilogue-first staging of the next
+    tile: the LATE instances of the RoPE / SwiGLU-backward GEMMs)."""
+    monkeypatch.setattr(hip, "_GB_FLAGS", (hip._GB_FLAGS & ~4096) | request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("B,S,nh,K", [(16, 1024, 12, 768), (4, 256, 25, 1600 // 128 * 128), (2, 512, 16, 1024)])
-def test_gemm_qkv_rope(B, S, nh, K):
+def test_gemm_qkv_rope(B, S, nh, K, gemm_late_flag):
     """QKV GEMM with NeoX RoPE on q/k in the epilogue == fp32 GEMM -> bf16 -> RoPE (the
     unfused GEMM + rope_qk_inplace math), at GPT-2 small (nh 12), an xl-like head count
-    (nh 25, packed stride 3*25*64 = 4800) and medium (nh 16)."""
+    (nh 25, packed stride 3*25*64 = 4800) and medium (nh 16); both staging schedules
+    (the persistent grid walks 3 tiles per workgroup at the first shape)."""
     torch.manual_seed(nh)
     M, H = B * S, nh * 64
     x = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
@@ -640,12 +655,14 @@ def test_gemm_dgrad_fp16_vs_fp32(M, Nout, Nred):
         hip.gemm_dgrad(dy.float(), w.float())
 
 
-def test_gemm_down_swiglu_bwd_vs_fp32():
+@pytest.mark.parametrize("M", [512, 16384])
+def test_gemm_down_swiglu_bwd_vs_fp32(M, gemm_late_flag):
     """Down-projection dgrad with the SwiGLU backward in the epilogue == the fp32 product
     rounded to bf16 (what the unfused dgrad writes) through k_swiglu_bwd's math, and ==
-    hip.swiglu_bwd on the library dgrad within bf16 rounding."""
+    hip.swiglu_bwd on the library dgrad within bf16 rounding.  M 16384: 4 tiles per
+    persistent workgroup (the epilogue-first staging's cross-tile path)."""
     torch.manual_seed(7)
-    M, H, I = 512, 768, 3072
+    H, I = 768, 3072
     dd = (torch.rand(M, H, device=DEV) * 2 - 1).bfloat16()
     wd = ((torch.rand(H, I, device=DEV) * 2 - 1) / H ** 0.5).bfloat16()
     gu = (torch.randn(M, 2 * I, device=DEV) * 2).bfloat16()

@@ -595,18 +595,20 @@ def test_fused_decode_falls_back_beyond_lds():
     assert out.shape == (1, 20)
 
 
-def test_head_dim_128_trains_on_gpu():
-    """A YAML-style config with head_dim 128 (the reference accepts any hidden % heads
-    == 0): the engine runs RoPE + attention as PyTorch ops on the GPU and everything else
-    native, and its gradients match the all-reference-ops engine (verdict r2: it raised)."""
-    cfg = GPTConfig(vocab_size=1000, hidden_size=256, num_layers=2, num_heads=2, max_seq_len=256,
+@pytest.mark.parametrize("hidden,heads,backend", [(256, 2, "hip"), (256, 8, "reference")])
+def test_head_dim_128_trains_on_gpu(hidden, heads, backend):
+    """YAML-style configs with head_dim 128 (the MFMA attention kernels' D = 128
+    instantiation) and head_dim 32 (no HIP attention kernel: RoPE + attention run as
+    PyTorch ops on the GPU, everything else native) -- the reference accepts any hidden %
+    heads == 0.  Gradients match the all-reference-ops engine (verdict r2: it raised)."""
+    cfg = GPTConfig(vocab_size=1000, hidden_size=hidden, num_layers=2, num_heads=heads, max_seq_len=256,
                     dropout=0.1, attention_dropout=0.1)
-    assert cfg.head_dim == 128
+    assert cfg.head_dim == hidden // heads
     torch.manual_seed(13)
     base = GPT(cfg).to(DEV)
     m1, m2 = copy.deepcopy(base), copy.deepcopy(base)
     e1 = m1.enable_engine(seed=6)
-    assert e1.ops.attn_backend == "reference" and e1.ops.backend == "hip"
+    assert e1.ops.attn_backend == backend and e1.ops.backend == "hip"
     m2.enable_engine(seed=6, ops=ops.CPU_OPS)
     ids = torch.randint(0, 1000, (2, 256), device=DEV)
     _, l1 = m1(ids, labels=ids)
