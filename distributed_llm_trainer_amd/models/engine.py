@@ -682,6 +682,7 @@ class GPTEngine:
         if not getattr(self.provider, "side_stream_hooks", False) or not getattr(self.gemm, "stream_safe", False):
             return None
         if self._side is None:
+            _queue_pad(dev)
             self._side = torch.cuda.Stream(dev)
         return self._side
 
@@ -1201,6 +1202,25 @@ class GPTEngine:
 
 
 _TEST_DELAY_FIRST_BWD = int(os.environ.get("DLT_TEST_DELAY_FIRST_BWD", "0"))
+
+_QUEUE_PAD = []  # streams that exist only to shift the engine streams' hardware queues
+
+
+def _queue_pad(dev) -> None:
+    """A/B knob (DLT_QUEUE_PAD=n): before the engine's first side stream is created, n
+    streams each dispatch one empty kernel, so the HIP runtime's round-robin assignment of
+    hardware queues (at a stream's first dispatch) gives the engine's weight-gradient and
+    pipeline streams queues n later (profiles/r4_stream_queues.md: the two-chain window
+    collapses when a communicator's streams shift them)."""
+    n = int(os.environ.get("DLT_QUEUE_PAD", "0"))
+    if n <= 0 or _QUEUE_PAD or torch.device(dev).type != "cuda":
+        return
+    for _ in range(n):
+        st = torch.cuda.Stream(dev)
+        with torch.cuda.stream(st):
+            torch.cuda._sleep(1)
+        _QUEUE_PAD.append(st)
+    torch.cuda.synchronize(dev)
 
 
 def _wgrad(gm, dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:

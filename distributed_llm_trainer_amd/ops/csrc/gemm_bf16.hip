@@ -140,6 +140,18 @@ __device__ __forceinline__ int gb_bmap(int r, int I) {
   return gb_ncol<BN, EPI>(r / (BN / 2), (r % (BN / 2)) >> 4, I) + (r & 15);
 }
 
+// One 16-byte-per-lane LDS-DMA piece issued from inline asm: the compiler's wait pass does
+// not see it.  For an LDS-DMA it knows about, that pass waits vmcnt(0) before the first use
+// of ANY older load's result (it does not count LDS-DMA in order with the loads), which
+// turned the epilogue-first staging's gu / cos-sin waits into waits for the whole next-tile
+// prefetch.  Invisible pieces only ever make the compiler's counted waits stricter (it
+// counts fewer younger operations than are in flight), never unsafe; the code that reads
+// the staged LDS waits for them with its own counted s_waitcnt.
+__device__ __forceinline__ void gb_dma_asm(const void* g, const void* lds) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)lds);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0) : "memory", "m0");
+}
+
 // 4 fp32 -> 4 bf16 (RNE) as two v_cvt_pk_bf16_f32; and back (exact)
 typedef __bf16 gb_bf16x4_t __attribute__((ext_vector_type(4)));
 typedef uint32_t gb_u32x4_t __attribute__((ext_vector_type(4)));
@@ -169,7 +181,8 @@ __device__ __forceinline__ void gb_unpack(uint2 p, float (&f)[4]) {
 // token-major operands).  Same unit sizes and DMA counts per wave, so the 8-phase
 // schedule and its counted waits are unchanged.
 // HK: operand / output format, 0 = bf16, 1 = IEEE half (plain store epilogue only).
-template <int BN, int EPI, bool BT = false, int HK = 0>
+// LATE (ROPE / SWIGLU_BWD only): epilogue-first staging of the next tile, see the loop.
+template <int BN, int EPI, bool BT = false, int HK = 0, bool LATE = false>
 __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                       bf16_t* __restrict__ C, int M, int N, int K, int lda, int ldb,
                                                       int ldc, int flags, GbEpi ep) {
@@ -177,6 +190,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
   static_assert(!BT || (BN == 192 && (EPI == GB_EPI_STORE || EPI == GB_EPI_SWIGLU_BWD)),
                 "the reduction-major B form is the 192-column data-gradient kernel");
   static_assert(HK == 0 || EPI == GB_EPI_STORE, "the fused epilogues are bf16-only");
+  static_assert(!LATE || EPI == GB_EPI_ROPE || EPI == GB_EPI_SWIGLU_BWD, "epilogue-first staging: loading epilogues");
   using Cf = GbCfg<BN>;
   constexpr int TS = EPI == GB_EPI_SWIGLU ? 96 : BN;  // tile stride in B rows
   constexpr int NT = Cf::NT, NH = Cf::NH;
@@ -286,26 +300,56 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
     }
   }
 
+  // (LATE kernels: every piece from inline asm, gb_dma_asm -- with any compiler-visible
+  // LDS-DMA possibly in flight at the K-loop exit, the compiler made the epilogue's first
+  // load use wait vmcnt(0); the K-loop's own counted waits + barriers are what orders
+  // the LDS images, in every variant)
   auto stA = [&](const bf16_t* g, int q, bf16_t* img) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-      __builtin_amdgcn_global_load_lds((gb_gbl_cvptr_t)((const char*)g + oa[q][j]),
-                                       (gb_lds_vptr_t)(img + gb_arow<BN>(q, wid * 2 + j) * GB_BK), 16, 0, 0);
+    for (int j = 0; j < 2; ++j) {
+      if constexpr (LATE)
+        gb_dma_asm((const char*)g + oa[q][j], img + gb_arow<BN>(q, wid * 2 + j) * GB_BK);
+      else
+        __builtin_amdgcn_global_load_lds((gb_gbl_cvptr_t)((const char*)g + oa[q][j]),
+                                         (gb_lds_vptr_t)(img + gb_arow<BN>(q, wid * 2 + j) * GB_BK), 16, 0, 0);
+    }
   };
   auto stB0 = [&](const bf16_t* g, bf16_t* img) {
 #pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      bf16_t* dst = img + (BT ? (wid * 2 + j) * 512 : gb_brow<BN>(0, wid * 2 + j) * GB_BK);
+      if constexpr (LATE)
+        gb_dma_asm((const char*)g + ob0[j], dst);
+      else
+        __builtin_amdgcn_global_load_lds((gb_gbl_cvptr_t)((const char*)g + ob0[j]), (gb_lds_vptr_t)dst, 16, 0, 0);
+    }
+  };
+  // the same units from inline asm (LATE staging: gb_dma_asm)
+  auto stA_asm = [&](const bf16_t* g, int q, bf16_t* img) {
+#pragma unroll
     for (int j = 0; j < 2; ++j)
-      __builtin_amdgcn_global_load_lds(
-          (gb_gbl_cvptr_t)((const char*)g + ob0[j]),
-          (gb_lds_vptr_t)(img + (BT ? (wid * 2 + j) * 512 : gb_brow<BN>(0, wid * 2 + j) * GB_BK)), 16, 0, 0);
+      gb_dma_asm((const char*)g + oa[q][j], img + gb_arow<BN>(q, wid * 2 + j) * GB_BK);
+  };
+  auto stB0_asm = [&](const bf16_t* g, bf16_t* img) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      gb_dma_asm((const char*)g + ob0[j], img + (BT ? (wid * 2 + j) * 512 : gb_brow<BN>(0, wid * 2 + j) * GB_BK));
+  };
+  auto stB1_asm = [&](const bf16_t* g, bf16_t* img) {
+#pragma unroll
+    for (int j = 0; j < Cf::B1_DMA; ++j)
+      gb_dma_asm((const char*)g + ob1[j],
+                 img + (BT ? GW_IMG_A + wid * 512 : gb_brow<BN>(1, wid * Cf::B1_DMA + j) * GB_BK));
   };
   auto stB1 = [&](const bf16_t* g, bf16_t* img) {
 #pragma unroll
-    for (int j = 0; j < Cf::B1_DMA; ++j)
-      __builtin_amdgcn_global_load_lds(
-          (gb_gbl_cvptr_t)((const char*)g + ob1[j]),
-          (gb_lds_vptr_t)(img + (BT ? GW_IMG_A + wid * 512 : gb_brow<BN>(1, wid * Cf::B1_DMA + j) * GB_BK)), 16, 0,
-          0);
+    for (int j = 0; j < Cf::B1_DMA; ++j) {
+      bf16_t* dst = img + (BT ? GW_IMG_A + wid * 512 : gb_brow<BN>(1, wid * Cf::B1_DMA + j) * GB_BK);
+      if constexpr (LATE)
+        gb_dma_asm((const char*)g + ob1[j], dst);
+      else
+        __builtin_amdgcn_global_load_lds((gb_gbl_cvptr_t)((const char*)g + ob1[j]), (gb_lds_vptr_t)dst, 16, 0, 0);
+    }
   };
   // operand pointer of K-tile kt (relative): A and the K-major B advance along the row,
   // the reduction-major B by whole rows
@@ -404,6 +448,20 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), d = (uint64_t)((uint32_t)flags >> 24) << 10;
     while (__builtin_amdgcn_s_memtime() - t0 < d) __builtin_amdgcn_s_sleep(2);
   }
+  // the next tile's first K-tiles, as the kernel prologue stages them (epilogue-first
+  // staging, flags & 4096): K-tile 0 whole into buffer 0, A0 / B0 of K-tile 1 into buffer 1
+  auto stage_next_of = [&](int t) {
+    const bf16_t* Ab = abase(t);
+    const bf16_t* Bb = bbase(t);
+    __builtin_amdgcn_sched_barrier(0);  // the epilogue's loads stay older than these
+    stA_asm(Ab, 0, A0i);
+    stB0_asm(Bb, B0i);
+    stB1_asm(Bb, B0i);
+    stA_asm(Ab, 1, A0i);
+    stA_asm(Ab + GB_BK, 0, A1i);
+    stB0_asm(bk(Bb, 1), B1i);
+    __builtin_amdgcn_sched_barrier(0);
+  };
   // prologue: K-tile 0 of the first tile complete in buffer 0, units A0/B0 of K-tile 1
   // in flight (their steady-state slots are phases 7 and 8)
   {
@@ -420,6 +478,16 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
     if (half == 1) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 one barrier behind
   }
 
+  // LATE: epilogues that READ global memory (RoPE: cos/sin tables; SwiGLU backward: the
+  // kept gu) issue those loads first and only then the next tile's first K-tiles
+  // ("epilogue-first staging"; the launcher selects it with flags & 4096): vmcnt retires
+  // in issue order, so with the next tile's DMA staged in the last K-iteration (the plain
+  // epilogue's schedule) every epilogue load waited for that whole prefetch (RoPE
+  // epilogue 9.3k vs 3.1k cycles, profiles/r4_gemm_forward.md section 5).  The next
+  // tile's K-tile 0 then lands during the epilogue's arithmetic and stores.  Compile-time,
+  // and the staging is issued on every tile (the last one re-stages its own operands,
+  // never read), so the compiler's waits see one instruction count on every path (a
+  // conditional staging made them vmcnt(0) at the join).
   for (int r = 0;; ++r) {
     const int next = tile_of(r + 1);
     const bool has_next = next < tend;
@@ -427,6 +495,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
     const bf16_t* const Bb = bbase(tile);
     const bf16_t* const An = has_next ? abase(next) : Ab;
     const bf16_t* const Bn = has_next ? bbase(next) : Bb;
+    auto stage_next = [&]() { stage_next_of(has_next ? next : tile); };
 #pragma unroll
     for (int a = 0; a < NT; ++a)
 #pragma unroll
@@ -439,7 +508,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
       // the K-tiles staged in this iteration: kt+1 (rest of it), kt+2, kt+3 -- the last
       // two belong to the next tile at the end of this one
       const bool inner = kt + 2 < nk;
-      const bool more = inner || has_next;
+      const bool more = inner || (has_next && !LATE);
       const bf16_t* const A2 = inner ? Ab + (kt + 2) * GB_BK : An;
       const bf16_t* const B2 = inner ? bk(Bb, kt + 2) : Bn;
       // ---- phase 1: buffer 0, q0 ; stage B1 of K-tile kt+1
@@ -534,14 +603,19 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
             sn[mt][u] = *reinterpret_cast<const float4*>(ep.sinT + (size_t)pos * 32 + j);
           }
         }
+        if constexpr (LATE) stage_next();
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
           for (int t = 0; t < 3; ++t) {
             const int P = wn * 48 + t * 16 + lq * 4;
-            if (n0 + (P >> 5) * 64 < ep.rot_cols) {
+            if (LATE || n0 + (P >> 5) * 64 < ep.rot_cols) {
+              // LATE: branch-free (cos 1 / sin 0 on the v heads) -- a branch here made the
+              // compiler wait for every outstanding load, the next tile's DMA included
+              const bool rot = !LATE || n0 + (P >> 5) * 64 < ep.rot_cols;
               const float4 c4 = cs[mt][t & 1], s4 = sn[mt][t & 1];
-              const float cc[4] = {c4.x, c4.y, c4.z, c4.w}, ss[4] = {s4.x, s4.y, s4.z, s4.w};
+              const float cc[4] = {rot ? c4.x : 1.f, rot ? c4.y : 1.f, rot ? c4.z : 1.f, rot ? c4.w : 1.f};
+              const float ss[4] = {rot ? s4.x : 0.f, rot ? s4.y : 0.f, rot ? s4.z : 0.f, rot ? s4.w : 0.f};
               float x1[4], x2[4];
               gb_unpack(gb_pack(acc[t][mt]), x1);  // the bf16 GEMM output the unfused path rotates
               gb_unpack(gb_pack(acc[t + 3][mt]), x2);
@@ -553,6 +627,32 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
             }
           }
       }
+      // SWIGLU_BWD: the lane's kept gate / up values for all 4 m-tiles (8 consecutive
+      // columns per pair p: the same columns its permlane-swapped ds values land on)
+      // Buffer loads / stores over the tile's 256 rows: ONE per-lane byte offset (row
+      // l16 of the wave's first m-tile, the lane's column base) for all 24 + 24 accesses,
+      // the m-tile (and the up half) in the SGPR offset, the pair p in the immediate --
+      // 64-bit row pointers per access pushed the preloading kernel into spills.
+      gb_u32x4_t gv[EPI == GB_EPI_SWIGLU_BWD ? 4 : 1][NT / 2], uv[EPI == GB_EPI_SWIGLU_BWD ? 4 : 1][NT / 2];
+      [[maybe_unused]] __amdgpu_buffer_rsrc_t rs_gu, rs_c;
+      [[maybe_unused]] int sw_voff = 0;
+      if constexpr (EPI == GB_EPI_SWIGLU_BWD) {
+        rs_gu = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(ep.gu_in) + (size_t)m0 * ep.ld_s, 0,
+                                                  GB_BM * ep.ld_s * 2, 0x00020000);
+        rs_c = __builtin_amdgcn_make_buffer_rsrc(C + (size_t)m0 * ldc, 0, GB_BM * ldc * 2, 0x00020000);
+        // column of pair p: wn * 96 + (2p + (lq & 1)) * 16 + (lq >> 1) * 8 (the STORE map)
+        sw_voff = ((wm * 64 + l16) * ep.ld_s + n0 + wn * (BN / 2) + (lq & 1) * 16 + (lq >> 1) * 8) * 2;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int p = 0; p < NT / 2; ++p) {
+            const int so = mt * 16 * ep.ld_s * 2;
+            gv[mt][p] = __builtin_bit_cast(gb_u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs_gu, sw_voff + p * 64, so, 0));
+            uv[mt][p] = __builtin_bit_cast(gb_u32x4_t,
+                                           __builtin_amdgcn_raw_buffer_load_b128(rs_gu, sw_voff + p * 64, so + ep.I * 2, 0));
+          }
+        if constexpr (LATE) stage_next();
+      }
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
         const int row = m0 + wm * 64 + mt * 16 + l16;
@@ -561,7 +661,9 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
         for (int t = 0; t < NT; ++t) pk[t] = gb_pack_hk<HK>(acc[t][mt]);
         // staged (LDS-transposed) stores: flag 1024; always for SWIGLU (its two stores
         // per lane otherwise write 16 rows x 32 + 8 bytes each)
-        const bool lt = EPI == GB_EPI_SWIGLU || (EPI != GB_EPI_SWIGLU_BWD && !BT && (flags & 1024));
+        // (LATE RoPE: row-per-lane permlane stores -- the staging ds_writes would make the
+        // compiler drain the next tile's in-flight LDS-DMA first)
+        const bool lt = EPI == GB_EPI_SWIGLU || (EPI != GB_EPI_SWIGLU_BWD && !BT && !LATE && (flags & 1024));
         if constexpr (EPI == GB_EPI_SWIGLU) {
           uint2 sp[3];
           // s = silu(g) * u on the bf16-rounded gate/up values (the packs stored as gu);
@@ -666,16 +768,14 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
           if constexpr (EPI == GB_EPI_SWIGLU_BWD) {
             // 8 consecutive ds values (bf16-rounded, as the unfused kernel reads them)
             // against the kept gate / up values of the same columns; C = dgu [M, 2I]
-            const bf16_t* grow = ep.gu_in + (size_t)row * ep.ld_s + n0 + col;
-            const gb_u32x4_t gv = *reinterpret_cast<const gb_u32x4_t*>(grow);
-            const gb_u32x4_t uv = *reinterpret_cast<const gb_u32x4_t*>(grow + ep.I);
             gb_u32x4_t og, ou, os;
             const bool want_s = ep.s_out != nullptr;  // uniform
 #pragma unroll
             for (int h = 0; h < 4; ++h) {
               float d[2] = {__uint_as_float(cv[h] << 16), __uint_as_float(cv[h] & 0xffff0000u)};
-              float g[2] = {__uint_as_float(gv[h] << 16), __uint_as_float(gv[h] & 0xffff0000u)};
-              float u[2] = {__uint_as_float(uv[h] << 16), __uint_as_float(uv[h] & 0xffff0000u)};
+              const uint32_t gw = gv[mt][p][h], uw = uv[mt][p][h];
+              float g[2] = {__uint_as_float(gw << 16), __uint_as_float(gw & 0xffff0000u)};
+              float u[2] = {__uint_as_float(uw << 16), __uint_as_float(uw & 0xffff0000u)};
               floatx4_t r, sv;
 #pragma unroll
               for (int e = 0; e < 2; ++e) {
@@ -690,8 +790,11 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
               ou[h] = pr.y;
               os[h] = gb_pack(sv).x;
             }
-            *reinterpret_cast<gb_u32x4_t*>(crow + col) = og;
-            *reinterpret_cast<gb_u32x4_t*>(crow + ep.I + col) = ou;
+            // dgu has gu's layout (ldc == ld_s): the load offsets address it too
+            const int so = mt * 16 * ldc * 2;
+            __builtin_amdgcn_raw_buffer_store_b128(og, rs_c, sw_voff + p * 64, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(ou, rs_c, sw_voff + p * 64,
+                                                   so + ep.I * 2, 0);
             // s_out (engine s ring): the down weight gradient's operand, rewritten from the
             // kept gu as k_swiglu_bwd's s_out does -- no separate k_swiglu_fwd pass
             if (want_s) *reinterpret_cast<gb_u32x4_t*>(ep.s_out + (size_t)row * ep.I + n0 + col) = os;
@@ -705,6 +808,27 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
         }
       }
       if (flags & 32) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (LATE) {
+        // younger than K-tile 0's DMA: K-tile 1's A0 / B0 units (4 instructions) and the
+        // epilogue's stores (ROPE: 12 per wave, STORE-form permlane or staged; SWIGLU_BWD:
+        // 24, +12 with s_out) -- counted so the stores keep draining into the next tile
+        // (tests/test_isa_checks.py checks these counts in the ISA)
+        if constexpr (EPI == GB_EPI_ROPE) {
+          asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        } else if constexpr (EPI == GB_EPI_SWIGLU_BWD) {
+          if (ep.s_out != nullptr)
+            asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(28)" ::: "memory");
+        }
+        // barrier alignment: at loop exit waves 4-7 are one barrier behind waves 0-3, so
+        // waves 0-3 pass one barrier that pairs with the others' last loop barrier, then
+        // all meet behind every wave's staging (the kernel prologue's state), and waves
+        // 4-7 fall one barrier behind again
+        if (half == 0) __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_barrier();
+        if (half == 1) __builtin_amdgcn_s_barrier();
+      }
     }
 #ifdef GB_STAMPS
     {
@@ -718,6 +842,9 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
     if (!has_next) break;
     tile = next;
   }
+  // LATE: the last tile re-staged its own operands; no LDS-DMA may still be writing the
+  // workgroup's LDS when it is released
+  if constexpr (LATE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (half == 0) __builtin_amdgcn_s_barrier();  // equal barrier counts for both halves
 #ifdef GB_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -775,7 +902,11 @@ DLT_API int dlt_gemm_bf16_qkv_rope(const bf16_t* A, const bf16_t* W, bf16_t* C, 
   if (!gb_shape_ok(M, N, K, K, K, N) || N % 192 || H % 64 || S <= 0) return -1;
   GbEpi ep{cosT, sinT, S, 2 * H, nullptr, 0, 0};
   const int ntiles = (M / 256) * (N / 192);
-  k_gemm_bf16<192, GB_EPI_ROPE><<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(A, W, C, M, N, K, K, K, N, flags, ep);
+  if (flags & 4096)  // epilogue-first staging of the next tile
+    k_gemm_bf16<192, GB_EPI_ROPE, false, 0, true>
+        <<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(A, W, C, M, N, K, K, K, N, flags, ep);
+  else
+    k_gemm_bf16<192, GB_EPI_ROPE><<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(A, W, C, M, N, K, K, K, N, flags, ep);
   DLT_CHECK_LAUNCH();
 }
 
@@ -799,8 +930,12 @@ DLT_API int dlt_gemm_bf16_down_swiglu_bwd(const bf16_t* dd, const bf16_t* Wdown,
   if (!gb_shape_ok(M, I, H, H, I, 2 * I) || I % 192) return -1;
   const int ntiles = (M / 256) * (I / 192);
   GbEpi ep{nullptr, nullptr, 1, 0, s_out, 2 * I, I, gu};  // s_out (optional): s [M, I], row stride I
-  k_gemm_bf16<192, GB_EPI_SWIGLU_BWD, true>
-      <<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(dd, Wdown, dgu, M, I, H, H, I, 2 * I, flags, ep);
+  if (flags & 4096)  // epilogue-first staging of the next tile
+    k_gemm_bf16<192, GB_EPI_SWIGLU_BWD, true, 0, true>
+        <<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(dd, Wdown, dgu, M, I, H, H, I, 2 * I, flags, ep);
+  else
+    k_gemm_bf16<192, GB_EPI_SWIGLU_BWD, true>
+        <<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(dd, Wdown, dgu, M, I, H, H, I, 2 * I, flags, ep);
   DLT_CHECK_LAUNCH();
 }
 

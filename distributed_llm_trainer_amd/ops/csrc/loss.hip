@@ -13,7 +13,7 @@
 // Vp <= 57344: 1024 threads x 7 16-byte chunks, held to 64 VGPRs (8 waves per SIMD,
 // two rows per CU in flight): 320 us vs 346 us per 8192 x 50304 call for 512 threads
 // x 13 chunks (94 VGPRs, five waves per SIMD), bench step -0.1 to -0.2 ms
-// (tools/ab/ab_ce.sh; DLT_CE_THREADS=512 selects the older shape).  Rows too long for
+// (round-2 harness ab_ce.sh, in git history; DLT_CE_THREADS=512 selects the older shape).  Rows too long for
 // registers fall back to k_ce_fwd_bwd (online max/sum pass + gradient pass).
 #include "common.h"
 #include <cstdlib>

@@ -128,6 +128,20 @@ def _forced(rank, world, mode):
             tr.train_step({"input_ids": torch.randint(0, HANDCFG["vocab_size"], (4, 256), generator=g)})
         rep = gemm.race_report()
         return {"flat": tr.flat_params().detach().float().cpu().clone()}, (tr.ddp.launched, rep)
+    if mode == "fsdp_hand":
+        from distributed_llm_trainer_amd.training.configs import FSDPConfig, FSDPTrainingConfig
+        from distributed_llm_trainer_amd.training.fsdp_trainer import FSDPTrainer
+        from distributed_llm_trainer_amd.ops import gemm
+        tc = FSDPTrainingConfig(batch_size=2, gradient_accumulation_steps=2, warmup_steps=1, max_steps=100,
+                                learning_rate=1e-3)
+        tr = FSDPTrainer(GPTConfig(**HANDCFG), tc, FSDPConfig(sharding_strategy="FULL_SHARD"))
+        assert tr.device.type == "cuda" and dist.get_backend() == "nccl"
+        for s in range(STEPS):
+            g = torch.Generator().manual_seed(77 + s)
+            tr.train_step({"input_ids": torch.randint(0, HANDCFG["vocab_size"], (4, 256), generator=g)})
+        rep = gemm.race_report()
+        sd = {k: v.detach().float().cpu().clone() for k, v in tr._full_state().items() if "rotary" not in k}
+        return sd, (1 if tr.runtime.force else 0, rep)
     if mode.startswith("ddp"):
         from distributed_llm_trainer_amd.training.configs import TrainingConfig
         from distributed_llm_trainer_amd.training.ddp_trainer import LEAN_DEFER_ROLES, DistributedTrainer
@@ -149,19 +163,20 @@ def _forced(rank, world, mode):
     return {k: v.detach().float().cpu().clone() for k, v in sd.items() if "rotary" not in k}, launched
 
 
-def test_rccl_forced_collectives_with_hand_kernels(tmp_path):
+@pytest.mark.parametrize("mode", ["ddp_hand", "fsdp_hand"])
+def test_rccl_forced_collectives_with_hand_kernels(tmp_path, mode):
     """The forced-collectives rehearsal with the SHIPPED kernel choices: every GEMM role
     races hand-written vs library as in production (first run, plan written), the second
     run replays that plan with DLT_FORCE_COLLECTIVES=1, so the hand wgrad / stream-K /
-    dgrad kernels on the weight-gradient stream feed the RCCL bucket all-reduces.  A
-    1-rank sum is the identity: parameters equal bit for bit."""
+    dgrad kernels feed the RCCL bucket all-reduces (DDP) or the unit all-gathers and
+    reduce-scatters (FSDP).  A 1-rank sum is the identity: parameters equal bit for bit."""
     plan = str(tmp_path / "plan.json")
     env = {"DLT_FORCE_CPU": None, "DLT_BACKEND": "nccl", "DLT_GEMM_PLAN": plan}
-    a, (_, rep) = run_multiprocess(_forced, world=1, args=("ddp_hand",), env=env, timeout=300)[0]
+    a, (_, rep) = run_multiprocess(_forced, world=1, args=(mode,), env=env, timeout=300)[0]
     assert os.path.exists(plan)
-    b, (launched, rep_b) = run_multiprocess(_forced, world=1, args=("ddp_hand",),
+    b, (launched, rep_b) = run_multiprocess(_forced, world=1, args=(mode,),
                                             env={**env, "DLT_FORCE_COLLECTIVES": "1"}, timeout=300)[0]
-    assert launched > 2
+    assert launched > (2 if mode == "ddp_hand" else 0)
     assert rep == rep_b
     # the hand-written kernels are among the choices (shapes tile by construction)
     assert any("hand-written" in v or "fused gemm_bf16" in v for v in rep.values()), rep

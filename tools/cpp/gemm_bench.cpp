@@ -426,7 +426,37 @@ static int dgrad_main(std::vector<int> shp) {
     printf("down dgrad + swiglu_bwd: fused %.1f us | hipBLASLt + k_swiglu_bwd %.1f us (dgrad alone %.1f, hand dgrad "
            "alone %.1f) | err %.1e\n",
            tf, tu, tb, th, mref > 0 ? e / mref : 0.0);
-    fflush(stdout);
+    // production flags (3084) vs epilogue-first staging (| 4096), with / without the s output;
+    // each variant checked against the flags-0 result bit for bit first
+    // DSW_FLAGS="f1,f2,...": the launch flags to compare (default: production 3084 and
+    // epilogue-first staging 7180)
+    std::vector<int> fls;
+    if (const char* e = getenv("DSW_FLAGS")) {
+      for (const char* c = e; *c;) {
+        fls.push_back(atoi(c));
+        while (*c && *c != ',') ++c;
+        if (*c == ',') ++c;
+      }
+    } else {
+      fls = {3084, 3084 | 4096};
+    }
+    for (int fl : fls) {
+      for (int ws = 0; ws < 2; ++ws) {
+        auto f = [&]() { return dlt_gemm_bf16_down_swiglu_bwd(dd, Wd, gu, dgu2, ws ? ds : nullptr, M, I, H, fl, st); };
+        CK(hipMemsetAsync(dgu2, 0xff, (size_t)M * 2 * I * 2, st));
+        if (f()) {
+          printf("flags %d launch failed\n", fl);
+          return 1;
+        }
+        CK(hipStreamSynchronize(st));
+        std::vector<bf16_t> a((size_t)M * 2 * I), b((size_t)M * 2 * I);
+        CK(hipMemcpy(a.data(), dgu, a.size() * 2, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(b.data(), dgu2, b.size() * 2, hipMemcpyDeviceToHost));
+        const bool same = !memcmp(a.data(), b.data(), a.size() * 2);
+        printf("  fused flags %d s_out %d: %.1f us  %s\n", fl, ws, time_us(f, st), same ? "bit-equal" : "MISMATCH");
+        fflush(stdout);
+      }
+    }
   }
   return 0;
 }
