@@ -153,6 +153,7 @@ def main():
     elapsed, peak = float(t[0]), float(t[1])
     tokens = args.steps * B * args.seq_len * world
     tps = tokens / elapsed
+    eng = getattr(getattr(trainer, "model", None), "engine", None)
     if trainer.is_main_process:
         base = None if overrides else BASELINE_TPS.get(world)
         out = {
@@ -173,6 +174,7 @@ def main():
                        **({"defer_roles": args.defer_roles} if args.defer_roles else {}),
                        **({"cpu_offload": True} if args.cpu_offload else {})},
             "peak_gb_per_gpu": round(peak, 3), "final_loss": round(loss, 4),
+            **({"window": eng.last_window, "stream_placement": eng.queue_placement} if eng is not None else {}),
             "vs_baseline_linear": None if overrides else round(tps / (12500.0 * world), 3),
         }
         print(json.dumps(out), flush=True)

@@ -231,6 +231,8 @@ class GPTEngine:
         self._side = None  # weight-gradient side stream (lazily created)
         self._mask_side = None  # attention keep-bit side stream
         self._pipe = None  # second compute stream of train_window
+        self.queue_placement = None  # how the side streams were placed (_place_streams)
+        self.last_window = None  # schedule of the last train_window ("ffbb" | "fb")
         # attention straight on the packed [M, 3H] QKV GEMM output (RoPE in place,
         # inverse RoPE in the backward epilogue); DLT_PACKED_QKV=0 -> split q/k/v copies
         self.packed_qkv = (hasattr(ops, "attention_fwd_packed")
@@ -677,14 +679,85 @@ class GPTEngine:
 
         Only with a provider whose gradient hooks are stream-safe (the flat store /
         DDP runtime) and a GEMM backend with per-stream workspaces."""
-        if dev.type != "cuda" or os.environ.get("DLT_WGRAD_STREAM", "1") == "0":
+        if not self._side_wanted(dev):
             return None
-        if not getattr(self.provider, "side_stream_hooks", False) or not getattr(self.gemm, "stream_safe", False):
-            return None
-        if self._side is None:
-            _queue_pad(dev)
-            self._side = torch.cuda.Stream(dev)
+        self._place_streams(dev)
         return self._side
+
+    def _side_wanted(self, dev) -> bool:
+        return (dev.type == "cuda" and os.environ.get("DLT_WGRAD_STREAM", "1") != "0"
+                and getattr(self.provider, "side_stream_hooks", False) and getattr(self.gemm, "stream_safe", False))
+
+    def _place_streams(self, dev) -> None:
+        """Create the weight-gradient and pipeline streams, each on a hardware queue that
+        dispatches independently of the current stream's and of each other's.
+
+        HIP binds a stream to a hardware queue at its first dispatch, round-robin, and a
+        queue that shares a command-processor pipe with another cannot dispatch while the
+        other's kernel is still placing workgroups -- a big GEMM holds the pipe for most of
+        its run, so two chains on such queues serialise (the ffbb window fell from 800k to
+        693k tok/s when a communicator's streams shifted the engine's queues, and to 696k
+        with one idle stream created first: profiles/r5_stream_queues.md).  So each new
+        stream is probed: a long many-workgroup kernel on an already placed stream, a
+        one-workgroup kernel on the candidate; if the candidate's kernel cannot finish
+        before the long one does, the candidate is parked (its queue stays taken) and the
+        next stream, bound to the next queue, is tried.  DLT_QUEUE_PAD=n instead creates n
+        idle streams first and skips the probe; DLT_QUEUE_PROBE=0 skips both."""
+        if self._pipe is not None:
+            return
+        want_side = self._side_wanted(dev)
+        pad = os.environ.get("DLT_QUEUE_PAD")
+        if pad is not None or os.environ.get("DLT_QUEUE_PROBE", "1") == "0":
+            _queue_pad(dev, int(pad or 0))
+            self._side = torch.cuda.Stream(dev) if want_side else None
+            self._pipe = torch.cuda.Stream(dev)
+            self.queue_placement = {"probe": False, "pads": int(pad or 0), "verified": False}
+            return
+        main = torch.cuda.current_stream(dev)
+        big = torch.zeros(64 << 20, dtype=torch.float32, device=dev)  # 256 MiB: ~16k workgroups per pass
+        tiny = torch.zeros(8, dtype=torch.float32, device=dev)
+
+        def fresh():
+            st = torch.cuda.Stream(dev)
+            with torch.cuda.stream(st):
+                tiny.add_(0.0)  # first dispatch: binds the hardware queue
+            return st
+
+        def blocked(a, b) -> bool:
+            votes = 0
+            for _ in range(3):
+                e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+                with torch.cuda.stream(a):
+                    e0.record()
+                    big.add_(1.0)
+                    big.add_(1.0)
+                    e2.record()
+                b.wait_event(e0)
+                with torch.cuda.stream(b):
+                    tiny.add_(1.0)
+                    e1.record()
+                torch.cuda.synchronize(dev)
+                votes += e0.elapsed_time(e1) > 0.5 * e0.elapsed_time(e2)
+            return votes >= 2
+
+        torch.cuda.synchronize(dev)
+        placed, parked, verified = [main], 0, True
+        chosen = []
+        for _ in range(2 if want_side else 1):
+            for attempt in range(4):
+                st = fresh()
+                if not any(blocked(p, st) for p in placed):
+                    break
+                if attempt == 3:
+                    verified = False  # keep the last candidate anyway
+                    break
+                _QUEUE_PAD.append(st)
+                parked += 1
+            placed.append(st)
+            chosen.append(st)
+        self._side, self._pipe = (chosen[0], chosen[1]) if want_side else (None, chosen[0])
+        del big, tiny
+        self.queue_placement = {"probe": True, "pads": parked, "verified": verified}
 
     def _head_wgrad_buf(self, like: torch.Tensor) -> torch.Tensor:
         """Persistent fp32 buffer for the window's lm_head weight gradient."""
@@ -983,17 +1056,22 @@ class GPTEngine:
         (the memory-lean modes keep fb: both forwards' activations live at once cost ~5 GB;
         FSDP's per-micro-step weight gradients: measured no faster, 1.5x the memory), the
         model is GPT-2-small-sized (small +0.9-1.1 %, medium -1.3 %: its larger GEMMs fill
-        the GPU alone, two forwards only contend) and no gradient collective runs (with the
-        DDP bucket all-reduces in flight ffbb measured 692-697k vs fb 775-777k tok/s on one
-        forced RCCL rank: the RCCL kernels starve for CUs next to three busy streams).
-        ``DLT_WINDOW_SCHED=fb|ffbb`` overrides (profiles/r3_window_ffbb.md)."""
+        the GPU alone, two forwards only contend).  With gradient collectives it also needs
+        the side streams' placement verified (_place_streams): a communicator's streams
+        shift the engine's hardware queues, and ffbb on two queues of one pipe measured
+        693k vs fb 789k tok/s on one forced RCCL rank (797.5-798.0k placed, no communicator
+        800-801k: profiles/r5_stream_queues.md).  ``DLT_WINDOW_SCHED=fb|ffbb`` overrides
+        (profiles/r3_window_ffbb.md)."""
         overlap = (cuda and GA > 1 and getattr(self.provider, "overlap_backward_ok", False)
                    and os.environ.get("DLT_BWD_OVERLAP", "1") != "0")
         hooks = getattr(self.provider, "hooks", None)
         comm = bool(getattr(hooks, "collectives", False) or getattr(self.provider, "collectives", False))
-        sched = os.environ.get("DLT_WINDOW_SCHED",
-                               "ffbb" if (defer and self.defer_roles == frozenset(self.ROLES)
-                                          and self.cfg.hidden_size <= 768 and not comm) else "fb")
+        eligible = (overlap and GA == 2 and defer and self.defer_roles == frozenset(self.ROLES)
+                    and self.cfg.hidden_size <= 768)
+        if eligible and comm and "DLT_WINDOW_SCHED" not in os.environ:
+            self._place_streams(torch.device("cuda", torch.cuda.current_device()))
+            eligible = bool(self.queue_placement and self.queue_placement["verified"])
+        sched = os.environ.get("DLT_WINDOW_SCHED", "ffbb" if eligible else "fb")
         if not (overlap and GA == 2 and sched == "ffbb"):
             sched = "fb"
         return overlap, sched
@@ -1010,8 +1088,7 @@ class GPTEngine:
         if serial:
             p0 = main
         else:
-            if self._pipe is None:
-                self._pipe = torch.cuda.Stream(dev)
+            self._place_streams(dev)
             p0 = self._pipe
         self.rope(micro_ids[0].shape[1], dev)
         self._wgrad_stream(dev)  # created before the fork
@@ -1132,6 +1209,7 @@ class GPTEngine:
         dev = micro_ids[0].device
         cuda = dev.type == "cuda"
         overlap, sched = self.window_schedule(GA, defer, cuda)
+        self.last_window = sched
         prog: List[dict] = [dict() for _ in range(GA)]
         if sched == "ffbb":
             return self._window_ffbb(micro_ids, micro_targets, dloss, recompute, defer, sync_hook, before_last,
@@ -1148,8 +1226,7 @@ class GPTEngine:
             # stream is idle by then.  Two streams in flight at any time, never three.
             pipe = self._wgrad_stream(dev)
             if pipe is None:
-                if self._pipe is None:
-                    self._pipe = torch.cuda.Stream(dev)
+                self._place_streams(dev)
                 pipe = self._pipe
             self.rope(micro_ids[0].shape[1], dev)  # lazily-built shared state: before the fork
             pipe.wait_stream(main)
@@ -1206,13 +1283,11 @@ _TEST_DELAY_FIRST_BWD = int(os.environ.get("DLT_TEST_DELAY_FIRST_BWD", "0"))
 _QUEUE_PAD = []  # streams that exist only to shift the engine streams' hardware queues
 
 
-def _queue_pad(dev) -> None:
-    """A/B knob (DLT_QUEUE_PAD=n): before the engine's first side stream is created, n
-    streams each dispatch one empty kernel, so the HIP runtime's round-robin assignment of
-    hardware queues (at a stream's first dispatch) gives the engine's weight-gradient and
-    pipeline streams queues n later (profiles/r4_stream_queues.md: the two-chain window
-    collapses when a communicator's streams shift them)."""
-    n = int(os.environ.get("DLT_QUEUE_PAD", "0"))
+def _queue_pad(dev, n: int) -> None:
+    """DLT_QUEUE_PAD=n (A/B knob, replaces the probe of Engine._place_streams): before the
+    engine's side streams are created, n streams each dispatch one empty kernel, so the
+    HIP runtime's round-robin assignment of hardware queues (at a stream's first dispatch)
+    gives the engine's weight-gradient and pipeline streams queues n later."""
     if n <= 0 or _QUEUE_PAD or torch.device(dev).type != "cuda":
         return
     for _ in range(n):

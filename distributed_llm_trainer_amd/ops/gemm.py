@@ -119,10 +119,11 @@ def load_plan(path: str, shipped: bool = False) -> None:
             if rc != 0:
                 raise RuntimeError(f"dlt_gemm_pin failed ({rc})")
             _PINNED["hipblaslt"][tuple(v[:-1])] = line
-    # "tn": forward-projection race ("bf16" = hand-written, null = hipBLASLt; the round-2
-    # integer tile configs of the retired gemm_tn kernels read as "library");
+    # "tn": forward-projection race ("bf16" = the persistent hand-written kernel, "tn4" =
+    # the four-wave one-tile-per-workgroup hand-written kernel, null = hipBLASLt; the
+    # round-2 integer tile configs of the retired gemm_tn kernels read as "library");
     # "fused": "kind:MxNxK" -> fused epilogue picked (older keys without a kind are ignored)
-    _PINNED["tn"] = {tuple(int(x) for x in k.split("x")): ("bf16" if c == "bf16" else None)
+    _PINNED["tn"] = {tuple(int(x) for x in k.split("x")): (c if c in ("bf16", "tn4") else None)
                      for k, c in plan.get("tn", {}).items()}
     for k, c in plan.get("fused", {}).items():
         if ":" in k:
@@ -324,16 +325,27 @@ class HipGemm:
                 and w.dtype == x.dtype and not torch.cuda.is_current_stream_capturing())
 
     def _pick(self, x, w, y):
+        """Forward projection race, once per shape: hipBLASLt (None), the persistent
+        hand-written kernel ("bf16") or the four-wave one (\"tn4\"); a hand-written pick
+        must beat the library by RACE_MARGIN.  The shipped plan pins the in-step winners."""
         from . import hip
         key = (x.shape[0], w.shape[0], x.shape[1])
         if key in self._choice:
             return self._choice[key]
+        if not self._can_race(x, w):
+            return None  # not recorded: decided when a bf16 call can race (fp16 replays pins)
         choice = None
-        if self._can_race(x, w) and hip.gemm_bf16_fits(*key):
-            t_lib = _time_of(lambda: self._lib_linear(x, w, y))
-            t_hand = _time_of(lambda: hip.gemm_bf16(x, w, out=y))
-            if t_hand < self.RACE_MARGIN * t_lib:
-                choice = "bf16"
+        t_lib = _time_of(lambda: self._lib_linear(x, w, y))
+        best = self.RACE_MARGIN * t_lib
+        cands = []
+        if hip.gemm_bf16_fits(*key):
+            cands.append(("bf16", lambda: hip.gemm_bf16(x, w, out=y)))
+        if hip.gemm_tn4_fits(*key) and os.environ.get("DLT_GEMM_TN4", "1") != "0":
+            cands.append(("tn4", lambda: hip.gemm_tn4(x, w, out=y)))
+        for name, fn in cands:
+            t = _time_of(fn)
+            if t < best:
+                best, choice = t, name
         self._choice[key] = choice
         return choice
 
@@ -343,11 +355,13 @@ class HipGemm:
         if out is not None and (out.shape != (M, N) or not out.is_contiguous() or out.dtype != x.dtype):
             raise ValueError("linear: out must be a contiguous [M, N] tensor of the input dtype")
         y = torch.empty(M, N, dtype=x.dtype, device=x.device) if out is None else out
-        if self._race and self._hand_ok(x, w) and self._pick(x, w, y) == "bf16":
-            from . import hip
-            hip.gemm_bf16(x, w, out=y)
-        else:
-            self._lib_linear(x, w, y)
+        pick = self._pick(x, w, y) if self._race and self._hand16_ok(x, w) else None
+        from . import hip
+        if pick == "bf16" and x.dtype == torch.bfloat16 and hip.gemm_bf16(x, w, out=y) is not None:
+            return y
+        if pick == "tn4" and hip.gemm_tn4(x, w, out=y) is not None:
+            return y
+        self._lib_linear(x, w, y)
         return y
 
     def _fused_pick(self, kind, x, w, fused, unfused, key=None) -> bool:

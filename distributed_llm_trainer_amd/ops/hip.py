@@ -63,6 +63,7 @@ _SIGS = {
                           c_int, c_void_p],
     "dlt_scale_bf16": [c_void_p, c_void_p, ctypes.c_long, c_void_p, c_float, c_int, c_void_p],
     "dlt_gemm_bf16_tn": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "dlt_gemm_tn4": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "dlt_gemm_bf16_qkv_rope": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                                c_void_p],
     "dlt_gemm_bf16_gu_swiglu": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
@@ -857,6 +858,27 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = No
     c = torch.empty(M, N, dtype=torch.bfloat16, device=a.device) if out is None else out
     _req(c, torch.bfloat16, "gemm_bf16.c", M * N)
     _chk(lib().dlt_gemm_bf16_tn(_p(a), _p(b), _p(c), M, N, K, K, K, N, _fwd_flags(), _stream()), "gemm_bf16")
+    return c
+
+
+def gemm_tn4_fits(M: int, N: int, K: int) -> bool:
+    """Shapes the four-wave forward GEMM (csrc/gemm_tn4.hip) tiles."""
+    return M > 0 and N > 0 and K > 0 and M % 256 == 0 and K % 32 == 0 and N % 8 == 0
+
+
+def gemm_tn4(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """C[M,N] = A[M,K] @ B[N,K]^T (bf16 or fp16 in/out, fp32 accumulate) with the
+    four-wave 256 x 256 one-tile-per-workgroup MFMA kernel.  Returns None (nothing
+    launched) when the shape does not tile (M % 256, K % 32, N % 8)."""
+    M, K = a.shape
+    N = b.shape[0]
+    if not gemm_tn4_fits(M, N, K) or b.shape[1] != K:
+        return None
+    hk = _req_act(a, a.dtype, "gemm_tn4.a")
+    _req(b, a.dtype, "gemm_tn4.b")
+    c = torch.empty(M, N, dtype=a.dtype, device=a.device) if out is None else out
+    _req(c, a.dtype, "gemm_tn4.c", M * N)
+    _chk(lib().dlt_gemm_tn4(_p(a), _p(b), _p(c), M, N, K, K, K, N, hk, _stream()), "gemm_tn4")
     return c
 
 

@@ -495,11 +495,17 @@ def test_gemm_wgrad_kernels_fp16(T, Nr, Nc):
     with pytest.raises(ValueError):
         hip.gemm_wgrad(base.clone(), dy, x.bfloat16(), 1)  # mixed operand formats
     g = gemm.HipGemm()
-    assert g._wgrad_hand_ok(dy, x) and not g._wgrad_hand_ok(dy, x, to16=True)
+    # fp16 operands take the hand route into an fp32 accumulator AND into a 16-bit output
+    # (FSDP's fp16 reduce buffers; the partial sum kernel dispatches on the format)
+    assert g._wgrad_hand_ok(dy, x) and g._wgrad_hand_ok(dy, x, to16=True)
     for s in (-1, -3, g.STREAMK):
         dw = base.clone()
         g._run_wgrad(dw, dy, x, s, False)
         _close(dw, ref, 1e-3 * T ** 0.5, 1e-4, f"fp16 planner route {s}")
+    for s in (-1, -3):
+        out = torch.empty(Nr, Nc, device=DEV, dtype=torch.float16)
+        g._run_wgrad(out, dy, x, s, True)
+        _close(out.float(), ref - base, 2e-3 * T ** 0.5, 2e-3, f"fp16 16-bit-output route {s}")
 
 
 def test_planner_stream_k_route():
@@ -561,6 +567,28 @@ def test_gemm_bf16(M, N, K):
     assert _relerr(c, want) < 8e-3
     _close(c, want, 8e-3 * want.abs().max().item(), 8e-3, "gemm_bf16")
     assert hip.gemm_bf16(a[:, :K - 64].contiguous(), b[:, :K - 64].contiguous()) is None  # K % 128
+
+
+# the five forward projections at the headline chain (M = 16384), a ragged last column
+# tile (N % 256 = 128: the 50304-row lm_head), a grid that is not a multiple of 8 XCDs,
+# and small shapes
+@pytest.mark.parametrize("M,N,K", [(16384, 2304, 768), (16384, 768, 768), (16384, 768, 3072), (4096, 6144, 768),
+                                   (2048, 50304, 768), (768, 1280, 512), (256, 264, 64), (1280, 640, 128), (512, 512, 64)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_gemm_tn4(M, N, K, dtype):
+    """Four-wave one-tile-per-workgroup MFMA GEMM C = A B^T (csrc/gemm_tn4.hip) vs fp32
+    torch, bf16 and fp16 operands: every element within 16-bit output rounding, every
+    tile written exactly once (a poisoned output must be fully overwritten)."""
+    torch.manual_seed(M + N + K)
+    a = (torch.rand(M, K, device=DEV) * 2 - 1).to(dtype)
+    b = (torch.rand(N, K, device=DEV) * 2 - 1).to(dtype)
+    c = torch.full((M, N), float("nan"), device=DEV, dtype=dtype)
+    assert hip.gemm_tn4(a, b, out=c) is not None
+    want = a.float() @ b.float().t()
+    assert not torch.isnan(c).any(), "unwritten output"
+    assert _relerr(c, want) < 8e-3
+    _close(c, want, 8e-3 * want.abs().max().item(), 8e-3, "gemm_tn4")
+    assert hip.gemm_tn4(a[:, :K - 16].contiguous(), b[:, :K - 16].contiguous()) is None  # K % 32 (BK 32 or 64)
 
 
 @pytest.fixture(params=[0, 4096], ids=["stage-in-loop", "epilogue-first"])

@@ -119,6 +119,48 @@ def test_generate_kv_cache_gpu():
             (lg[0, -1].max() - lg[0, -1][g[0, 17 + t]]).abs().item() < 0.05
 
 
+def _dispatch_blocked(a, b, big, tiny):
+    """Does a one-workgroup kernel on stream b wait for a long many-workgroup kernel on
+    stream a (hardware queues on one command-processor pipe)?"""
+    e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    with torch.cuda.stream(a):
+        e0.record()
+        for _ in range(4):
+            big.add_(1.0)
+        e2.record()
+    b.wait_event(e0)
+    with torch.cuda.stream(b):
+        tiny.add_(1.0)
+        e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) > 0.5 * e0.elapsed_time(e2)
+
+
+def test_side_streams_dispatch_independently():
+    """Engine._place_streams: after placement the pipeline stream's kernels dispatch while
+    a long kernel runs on the current stream, even when another stream took a hardware
+    queue first (as a communicator's streams do; profiles/r5_stream_queues.md)."""
+    torch.manual_seed(3)
+    m = GPT(_cfg(0.0)).to(DEV)
+    e = m.enable_engine(seed=1)
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        torch.zeros(1, device=DEV).add_(1.0)  # binds a queue before the engine's streams
+    e._place_streams(torch.device(DEV))
+    assert e.queue_placement["probe"] and e.queue_placement["verified"], e.queue_placement
+    big = torch.zeros(64 << 20, device=DEV)
+    tiny = torch.zeros(8, device=DEV)
+    main = torch.cuda.current_stream()
+    others = [x for x in (e._side, e._pipe) if x is not None]
+    for o in others:
+        assert sum(_dispatch_blocked(main, o, big, tiny) for _ in range(3)) <= 1
+    # the engine still trains on the placed streams (the window uses them)
+    ids = torch.randint(0, 1000, (2, 256), device=DEV)
+    _, loss = m(ids, labels=ids)
+    loss.backward()
+    assert torch.isfinite(loss)
+
+
 def test_deferred_wgrad_gpu():
     """hipBLASLt wgrad over the whole accumulation window == per-micro-step wgrads."""
     torch.manual_seed(2)

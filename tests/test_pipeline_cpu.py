@@ -237,8 +237,9 @@ def test_fused_loss_segments_normalise_per_micro_step():
 
 def test_window_schedule_choice(monkeypatch):
     """Two-chain window schedule: ffbb only with overlapped backwards, two chains, every
-    weight gradient deferred, a GPT-2-small-sized model and no gradient collectives in
-    flight; fb otherwise (profiles/r3_window_ffbb.md)."""
+    weight gradient deferred, a GPT-2-small-sized model, and with gradient collectives in
+    flight only on verified stream placement; fb otherwise (profiles/r3_window_ffbb.md,
+    r5_stream_queues.md)."""
     import types
     monkeypatch.delenv("DLT_WINDOW_SCHED", raising=False)
     monkeypatch.delenv("DLT_BWD_OVERLAP", raising=False)
@@ -253,8 +254,19 @@ def test_window_schedule_choice(monkeypatch):
     e.defer_roles = frozenset(("qkv", "o"))                               # memory-lean
     assert e.window_schedule(2, True, cuda=True) == (True, "fb")
     e.defer_roles = frozenset(e.ROLES)
-    e.provider.hooks = types.SimpleNamespace(collectives=True)            # DDP buckets in flight
+    # DDP buckets in flight: ffbb only once the side streams' hardware queues are verified
+    # to dispatch independently (Engine._place_streams; stubbed here, no GPU)
+    placement = {"verified": False}
+
+    def fake_place(dev):
+        e.queue_placement = dict(placement)
+    monkeypatch.setattr(e, "_place_streams", fake_place)
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: 0)  # no GPU here: only the index is read
+    e.provider.hooks = types.SimpleNamespace(collectives=True)
     assert e.window_schedule(2, True, cuda=True) == (True, "fb")
+    placement["verified"] = True
+    assert e.window_schedule(2, True, cuda=True) == (True, "ffbb")
+    placement["verified"] = False
     e.provider.hooks = types.SimpleNamespace(collectives=False)
     monkeypatch.setenv("DLT_BWD_OVERLAP", "0")
     assert e.window_schedule(2, True, cuda=True) == (False, "fb")
