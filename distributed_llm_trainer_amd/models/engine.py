@@ -697,18 +697,23 @@ class GPTEngine:
         other's kernel is still placing workgroups -- a big GEMM holds the pipe for most of
         its run, so two chains on such queues serialise (the ffbb window fell from 800k to
         693k tok/s when a communicator's streams shifted the engine's queues, and to 696k
-        with one idle stream created first: profiles/r5_stream_queues.md).  So each new
-        stream is probed: a long many-workgroup kernel on an already placed stream, a
-        one-workgroup kernel on the candidate; if the candidate's kernel cannot finish
-        before the long one does, the candidate is parked (its queue stays taken) and the
-        next stream, bound to the next queue, is tried.  DLT_QUEUE_PAD=n instead creates n
-        idle streams first and skips the probe; DLT_QUEUE_PROBE=0 skips both."""
+        with one idle stream created first: profiles/r5_stream_queues.md).
+        DLT_QUEUE_PROBE=1 probes each new stream: a long many-workgroup kernel on an
+        already placed stream, a one-workgroup kernel on the candidate; if the candidate's
+        kernel cannot finish before the long one does, the candidate is parked (its queue
+        stays taken) and the next stream, bound to the next queue, is tried.  Opt-in: on a
+        forced RCCL rank the probe found no blocked pair, yet ffbb still collapsed (706k)
+        and binding the side streams before the communicator's first collective cost fb
+        9 % (718k vs 789k), so by default the streams stay unbound until their first use
+        and collectives keep the fb window.  DLT_QUEUE_PAD=n creates n idle streams first
+        (forced RCCL rank, ffbb: 797k with n = 3)."""
         if self._pipe is not None:
             return
         want_side = self._side_wanted(dev)
         pad = os.environ.get("DLT_QUEUE_PAD")
-        if pad is not None or os.environ.get("DLT_QUEUE_PROBE", "1") == "0":
+        if pad is not None or os.environ.get("DLT_QUEUE_PROBE", "0") != "1":
             _queue_pad(dev, int(pad or 0))
+            # created unbound: each binds its hardware queue at its first dispatch
             self._side = torch.cuda.Stream(dev) if want_side else None
             self._pipe = torch.cuda.Stream(dev)
             self.queue_placement = {"probe": False, "pads": int(pad or 0), "verified": False}
@@ -1056,12 +1061,12 @@ class GPTEngine:
         (the memory-lean modes keep fb: both forwards' activations live at once cost ~5 GB;
         FSDP's per-micro-step weight gradients: measured no faster, 1.5x the memory), the
         model is GPT-2-small-sized (small +0.9-1.1 %, medium -1.3 %: its larger GEMMs fill
-        the GPU alone, two forwards only contend).  With gradient collectives it also needs
-        the side streams' placement verified (_place_streams): a communicator's streams
-        shift the engine's hardware queues, and ffbb on two queues of one pipe measured
-        693k vs fb 789k tok/s on one forced RCCL rank (797.5-798.0k placed, no communicator
-        800-801k: profiles/r5_stream_queues.md).  ``DLT_WINDOW_SCHED=fb|ffbb`` overrides
-        (profiles/r3_window_ffbb.md)."""
+        the GPU alone, two forwards only contend).  With gradient collectives it is fb: a
+        communicator's streams shift the engine's hardware queues, and ffbb measured 693k
+        vs fb 789k tok/s on one forced RCCL rank (797.5-798.0k with DLT_QUEUE_PAD=3, no
+        communicator 800-801k: profiles/r5_stream_queues.md); only a placement verified by
+        the opt-in probe (DLT_QUEUE_PROBE=1, _place_streams) lifts that.
+        ``DLT_WINDOW_SCHED=fb|ffbb`` overrides (profiles/r3_window_ffbb.md)."""
         overlap = (cuda and GA > 1 and getattr(self.provider, "overlap_backward_ok", False)
                    and os.environ.get("DLT_BWD_OVERLAP", "1") != "0")
         hooks = getattr(self.provider, "hooks", None)
@@ -1069,8 +1074,10 @@ class GPTEngine:
         eligible = (overlap and GA == 2 and defer and self.defer_roles == frozenset(self.ROLES)
                     and self.cfg.hidden_size <= 768)
         if eligible and comm and "DLT_WINDOW_SCHED" not in os.environ:
-            self._place_streams(torch.device("cuda", torch.cuda.current_device()))
-            eligible = bool(self.queue_placement and self.queue_placement["verified"])
+            eligible = False
+            if os.environ.get("DLT_QUEUE_PROBE") == "1":
+                self._place_streams(torch.device("cuda", torch.cuda.current_device()))
+                eligible = bool(self.queue_placement and self.queue_placement["verified"])
         sched = os.environ.get("DLT_WINDOW_SCHED", "ffbb" if eligible else "fb")
         if not (overlap and GA == 2 and sched == "ffbb"):
             sched = "fb"

@@ -3,6 +3,7 @@ running the PyTorch reference ops on the GPU (identical dropout masks) and (b) t
 eager autocast model (dropout off)."""
 import copy
 import math
+import os
 
 import pytest
 import torch
@@ -143,10 +144,14 @@ def test_side_streams_dispatch_independently():
     torch.manual_seed(3)
     m = GPT(_cfg(0.0)).to(DEV)
     e = m.enable_engine(seed=1)
+    os.environ["DLT_QUEUE_PROBE"] = "1"  # opt-in (the default leaves the streams unbound)
     st = torch.cuda.Stream()
     with torch.cuda.stream(st):
         torch.zeros(1, device=DEV).add_(1.0)  # binds a queue before the engine's streams
-    e._place_streams(torch.device(DEV))
+    try:
+        e._place_streams(torch.device(DEV))
+    finally:
+        del os.environ["DLT_QUEUE_PROBE"]
     assert e.queue_placement["probe"] and e.queue_placement["verified"], e.queue_placement
     big = torch.zeros(64 << 20, device=DEV)
     tiny = torch.zeros(8, device=DEV)

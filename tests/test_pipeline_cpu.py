@@ -254,8 +254,9 @@ def test_window_schedule_choice(monkeypatch):
     e.defer_roles = frozenset(("qkv", "o"))                               # memory-lean
     assert e.window_schedule(2, True, cuda=True) == (True, "fb")
     e.defer_roles = frozenset(e.ROLES)
-    # DDP buckets in flight: ffbb only once the side streams' hardware queues are verified
-    # to dispatch independently (Engine._place_streams; stubbed here, no GPU)
+    # DDP buckets in flight: fb, and ffbb only with the opt-in placement probe verifying
+    # the side streams' hardware queues (Engine._place_streams; stubbed here, no GPU)
+    monkeypatch.setenv("DLT_QUEUE_PROBE", "1")
     placement = {"verified": False}
 
     def fake_place(dev):
@@ -266,6 +267,8 @@ def test_window_schedule_choice(monkeypatch):
     assert e.window_schedule(2, True, cuda=True) == (True, "fb")
     placement["verified"] = True
     assert e.window_schedule(2, True, cuda=True) == (True, "ffbb")
+    monkeypatch.delenv("DLT_QUEUE_PROBE")
+    assert e.window_schedule(2, True, cuda=True) == (True, "fb")             # default: no probe
     placement["verified"] = False
     e.provider.hooks = types.SimpleNamespace(collectives=False)
     monkeypatch.setenv("DLT_BWD_OVERLAP", "0")
