@@ -727,19 +727,20 @@ __device__ __forceinline__ void dkdv_subtile(floatx16_t (&dka)[D / 32], floatx16
         const int qa = qs + r;
         p = (ka > qa || qa >= S || ka >= S) ? 0.f : p;
       }
-      float dp = pacc[i];
-      float pd = p;
-      float dps = dp;
+      const float dp = pacc[i];
       if (DROP) {
+        // dS = P o (s M o dP - Delta) = s (Pd o dP - P Delta / s) with Pd = M o P: the
+        // dropped P that dV needs anyway, so the mask is applied once (4 VALU per
+        // element instead of 5); rd holds Delta / s and s = 1/(1-p) is folded into the
+        // dK and dV epilogues
         const uint32_t ones = keep_ones(mw, 8 * g + e);  // maskT word >> 4h: query qs + r
-        pd = keep_and(p, ones);  // 1/(1-p) folded into the dV epilogue
-        dp = keep_and(dp, ones);
-        dps = fmaf(dp, dscale, -dv[e]);
+        const float pd = keep_and(p, ones);
+        sacc[i] = pd;                          // dropped P -> dV
+        pacc[i] = fmaf(pd, dp, -(p * dv[e]));  // dS / s   -> dK
       } else {
-        dps = dp - dv[e];
+        sacc[i] = p;
+        pacc[i] = p * (dp - dv[e]);
       }
-      sacc[i] = pd;        // dropped P  -> dV
-      pacc[i] = p * dps;   // dS         -> dK
     }
   }
 #pragma unroll
@@ -786,6 +787,7 @@ __global__ __launch_bounds__(NT) ATTN_WAVES(D) void k_attn_bwd_dkdv(const bf16_t
   const int W = (S + 31) >> 5;
   const int nqt = (S + QSTEP - 1) / QSTEP;
   const bf16_t* dob = dout + ((size_t)b * S * nh + head) * D;
+  const float inv_dscale = 1.f / dscale;
   using UNM = std::integral_constant<bool, false>;
   using MSK = std::integral_constant<bool, true>;
 
@@ -823,7 +825,7 @@ __global__ __launch_bounds__(NT) ATTN_WAVES(D) void k_attn_bwd_dkdv(const bf16_t
         const int qq = min(t * QSTEP + tid, S - 1);
         const bool ok = t * QSTEP + tid < S;
         rl = ok ? lse[(size_t)bh * S + qq] * LOG2E : 0.f;
-        rd = ok ? delta[(size_t)bh * S + qq] : 0.f;
+        rd = ok ? delta[(size_t)bh * S + qq] * (DROP ? inv_dscale : 1.f) : 0.f;  // Delta / s (dkdv_subtile)
       }
     };
     auto store_rows = [&](int buf) {
@@ -877,7 +879,7 @@ __global__ __launch_bounds__(NT) ATTN_WAVES(D) void k_attn_bwd_dkdv(const bf16_t
     ATTN_STAMP(3);
 
     if (ka < S) {
-      store_head_row<HK, D>(dk + hout + (size_t)ka * out_rs, dka, scale, h, cosT, sinT, ka);
+      store_head_row<HK, D>(dk + hout + (size_t)ka * out_rs, dka, DROP ? scale * dscale : scale, h, cosT, sinT, ka);
       store_head_row<HK, D>(dv + hout + (size_t)ka * out_rs, dva, DROP ? dscale : 1.f, h, nullptr, nullptr, 0);
     }
 #ifdef DLT_ATTN_TIMING
