@@ -20,6 +20,10 @@ CONFIGS = {
     "ddp_small": ["--model_size", "small", "--batch_size", "8", "--grad_accum", "4"],
     "ddp_small_lean": ["--model_size", "small", "--batch_size", "8", "--grad_accum", "4", "--memory_lean"],
     "ddp_small_fp16": ["--model_size", "small", "--batch_size", "8", "--grad_accum", "4", "--precision", "fp16"],
+    "ddp_small_fp32": ["--model_size", "small", "--batch_size", "8", "--grad_accum", "4", "--precision", "fp32"],
+    # head_dim 128 (6 heads of the small model's 768): the D = 128 MFMA attention kernels
+    "ddp_small_hd128": ["--model_size", "small", "--batch_size", "8", "--grad_accum", "4",
+                        "--model_override", "num_heads=6"],
     "fsdp_small": ["--mode", "fsdp", "--model_size", "small", "--batch_size", "8", "--grad_accum", "4"],
     "ddp_medium": ["--model_size", "medium", "--batch_size", "4", "--grad_accum", "8"],
     "fsdp_medium": ["--mode", "fsdp", "--model_size", "medium", "--batch_size", "4", "--grad_accum", "8"],
