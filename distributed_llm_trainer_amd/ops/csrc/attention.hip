@@ -184,7 +184,12 @@ __device__ __forceinline__ uint32_t keep_ones(uint32_t word, int bit) {
   asm("" : "+v"(m));
   return m;
 }
-__device__ __forceinline__ float keep_and(float x, uint32_t ones) { return __uint_as_float(__float_as_uint(x) & ones); }
+__device__ __forceinline__ float keep_and(float x, uint32_t ones) {
+#ifdef DLT_ATTN_NOSEL  // diagnostic upper bound only (tools/ab): drops nothing, wrong numerics
+  return x;
+#endif
+  return __uint_as_float(__float_as_uint(x) & ones);
+}
 
 template <int HK = 0>
 __device__ __forceinline__ floatx16_t mfma(const bf16x8_t& a, const bf16x8_t& b, const floatx16_t& c) {
