@@ -271,36 +271,86 @@ __device__ __forceinline__ bf16x8_t load_row8(const bf16_t* __restrict__ p, bool
 // Only causal 32x32 tiles (key word <= query band) exist.  One half-wave per tile:
 // lane l hashes row q = 32r + l (16 hashes -> its row word), then a 5-stage butterfly
 // bit transpose gives lane j the column word of key 32w + j.
-// Pure VALU at full occupancy (~3-4 us per layer at B8 nh12 S1024), so the MFMA
-// kernels only test bits instead of hashing at 2 waves/SIMD.
+// Pure VALU, so the MFMA kernels only test bits instead of hashing at 2 waves/SIMD.
+// Instruction budget (S % 32 == 0, the fast path): 11 VALU per hash -- the pair index
+// is one xor (the row word's 16 pair indices differ from its first only in their low
+// 4 bits), and each keep bit is the carry of (16 random bits in the high half) +
+// (65536 - thr) << 16, shifted into the word by v_addc (no compare / select / or per
+// bit); the transpose is branch-free (ds_swizzle + alignbit + bfi per stage).  Round 4
+// form: ~32 VALU per hash (compare + s_nop + select per bit, divergent transpose).
+
+// word = 2 * word + carry(v + c16): shifts in keep = (high 16 bits of v) >= thr at bit 0
+// (c16 = (65536 - thr) << 16; the low half of c16 is zero, so v's low half never carries)
+__device__ __forceinline__ uint32_t keep_shift_in(uint32_t word, uint32_t v, uint32_t c16) {
+  uint32_t sum;  // discarded: only the carry is used
+  asm("v_add_co_u32 %1, vcc, %2, %3\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc"
+      : "+v"(word), "=&v"(sum)
+      : "s"(c16), "v"(v)
+      : "vcc");
+  return word;
+}
+// (x ^ (x >> 16)) << 16: the low 16 bits of lowbias32's last step, in the high half
+__device__ __forceinline__ uint32_t lo16_hi(uint32_t x) {
+  uint32_t z;
+  asm("v_xor_b32_sdwa %0, %1, %1 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1"
+      : "=v"(z)
+      : "v"(x));
+  return z;
+}
+// lane l ^ d within 32-lane groups (ds_swizzle bitmask mode: and 0x1f, xor d)
+template <int d>
+__device__ __forceinline__ uint32_t swz_xor(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1f | (d << 10));
+}
+template <int d>
+__device__ __forceinline__ uint32_t bt_stage(uint32_t col, int l) {
+  // lanes with bit d clear keep the m-bits of their word and take the partner's m-bits
+  // shifted up by d (rotl d, the wrapped bits land in m and are dropped); lanes with
+  // bit d set keep ~m and take the partner's ~m-bits shifted down (rotr d)
+  constexpr uint32_t m = d == 16 ? 0x0000FFFFu : d == 8 ? 0x00FF00FFu : d == 4 ? 0x0F0F0F0Fu : d == 2 ? 0x33333333u
+                                                                                               : 0x55555555u;
+  const uint32_t y = swz_xor<d>(col);
+  const bool up = (l & d) == 0;
+  const uint32_t r = __builtin_amdgcn_alignbit(y, y, up ? 32 - d : d);
+  const uint32_t keep = up ? m : ~m;
+  return (col & keep) | (r & ~keep);
+}
+
 __global__ __launch_bounds__(256) void k_dropout_bits(uint32_t* __restrict__ mask, uint32_t* __restrict__ maskT,
                                                       int BH, int S, uint32_t key, uint32_t thr) {
   const int W = (S + 31) >> 5;  // words per row == number of 32-row bands
   const int bh = blockIdx.y;
-  const int lane = threadIdx.x & 63, l = lane & 31, half = lane >> 5;
-  const int tile = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + half;  // one tile per half-wave
+  const int lane = threadIdx.x & 63, l = lane & 31;
+  const int tile = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);  // one tile per half-wave
   const int ntiles = W * (W + 1) / 2;
   const bool active = tile < ntiles;
-  // tile -> (band r, word w <= r): band r starts at tile r(r+1)/2
-  int r = active ? (int)((sqrtf(8.f * (float)tile + 1.f) - 1.f) * 0.5f) : 0;
-  if (active) {
-    while ((r + 1) * (r + 2) / 2 <= tile) ++r;
-    while (r > 0 && r * (r + 1) / 2 > tile) --r;
-  }
-  const int w = active ? tile - r * (r + 1) / 2 : 0;
+  // tile -> (band r, word w <= r): band r starts at tile r(r+1)/2; the float root is
+  // within one of r for any realistic S, corrected once each way without loops
+  int r = (int)((sqrtf(8.f * (float)tile + 1.f) - 1.f) * 0.5f);
+  r += ((r + 1) * (r + 2) / 2 <= tile) ? 1 : 0;
+  r -= (r * (r + 1) / 2 > tile) ? 1 : 0;
+  const int w = tile - r * (r + 1) / 2;
   const int q = r * 32 + l;
   const uint32_t kbh = lowbias32(key + (uint32_t)bh * 0x9E3779B9u);
   uint32_t word = 0;
   if (active && q < S) {
     const uint32_t base = (uint32_t)q * (uint32_t)S + (uint32_t)(w * 32);
-    const int nk = min(32, S - w * 32);
-    if ((base & 1u) == 0 && nk == 32) {
+    if ((S & 31) == 0) {
+      // base % 32 == 0: pair index base/2 + m has m in the 4 low bits, which base/2 lacks
+      const uint32_t kx = kbh ^ (base >> 1);
+      const uint32_t c16 = (65536u - thr) << 16;
 #pragma unroll
-      for (int j = 0; j < 32; j += 2) {
-        const uint32_t hsh = lowbias32(kbh ^ ((base + j) >> 1));
-        word |= ((uint32_t)((hsh & 0xffffu) >= thr) << j) | ((uint32_t)((hsh >> 16) >= thr) << (j + 1));
+      for (int m = 15; m >= 0; --m) {  // bits shift in from the top element down
+        uint32_t x = kx ^ (uint32_t)m;
+        x ^= x >> 16;
+        x *= 0x7feb352du;
+        x ^= x >> 15;
+        x *= 0x846ca68bu;
+        word = keep_shift_in(word, x, c16);            // element 2m + 1: high 16 bits
+        word = keep_shift_in(word, lo16_hi(x), c16);  // element 2m: low 16 bits
       }
     } else {
+      const int nk = min(32, S - w * 32);
       for (int j = 0; j < nk; ++j) {
         const uint32_t flat = base + (uint32_t)j;
         const uint32_t hsh = lowbias32(kbh ^ (flat >> 1));
@@ -311,15 +361,14 @@ __global__ __launch_bounds__(256) void k_dropout_bits(uint32_t* __restrict__ mas
     mask[((size_t)bh * W + w) * S + q] = word;  // word-major: the half-wave's 32 rows are contiguous
   }
   // 32x32 bit transpose within each half-wave (lane l holds row l; afterwards lane j
-  // holds column j): 5 butterfly stages, each one lane^d exchange + 4 bit ops.
+  // holds column j).  Every lane runs it (inactive lanes carry zeros) so the swizzles see
+  // a full group.
   uint32_t col = word;
-#pragma unroll
-  for (int d = 16; d >= 1; d >>= 1) {
-    const uint32_t m = d == 16 ? 0x0000FFFFu : d == 8 ? 0x00FF00FFu : d == 4 ? 0x0F0F0F0Fu : d == 2 ? 0x33333333u
-                                                                                                   : 0x55555555u;
-    const uint32_t y = (uint32_t)__shfl_xor((int)col, d, 64);
-    col = (l & d) ? ((col & ~m) | ((y >> d) & m)) : ((col & m) | ((y & m) << d));
-  }
+  col = bt_stage<16>(col, l);
+  col = bt_stage<8>(col, l);
+  col = bt_stage<4>(col, l);
+  col = bt_stage<2>(col, l);
+  col = bt_stage<1>(col, l);
   const int kk = w * 32 + l;
   if (active && kk < S) maskT[((size_t)bh * W + r) * S + kk] = col;
 }
