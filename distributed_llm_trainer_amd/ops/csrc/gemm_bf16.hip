@@ -165,6 +165,17 @@ __device__ __forceinline__ uint2 gb_pack_hk(const floatx4_t& v) {
   if constexpr (HK == 0) return gb_pack(v);
   else return __builtin_bit_cast(uint2, __builtin_convertvector(v, gb_f16x4_t));
 }
+// two 16-bit values of one dword (low half first) as floats, in the operand format
+template <int HK>
+__device__ __forceinline__ void gb_unpack2(uint32_t w, float (&f)[2]) {
+  if constexpr (HK == 0) {
+    f[0] = __uint_as_float(w << 16);
+    f[1] = __uint_as_float(w & 0xffff0000u);
+  } else {
+    f[0] = (float)__builtin_bit_cast(_Float16, (uint16_t)(w & 0xffffu));
+    f[1] = (float)__builtin_bit_cast(_Float16, (uint16_t)(w >> 16));
+  }
+}
 __device__ __forceinline__ void gb_unpack(uint2 p, float (&f)[4]) {
   f[0] = __uint_as_float(p.x << 16);
   f[1] = __uint_as_float(p.x & 0xffff0000u);
@@ -189,7 +200,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
   static_assert(EPI == GB_EPI_STORE || BN == 192, "pair epilogues need the 192-column tile");
   static_assert(!BT || (BN == 192 && (EPI == GB_EPI_STORE || EPI == GB_EPI_SWIGLU_BWD)),
                 "the reduction-major B form is the 192-column data-gradient kernel");
-  static_assert(HK == 0 || EPI == GB_EPI_STORE, "the fused epilogues are bf16-only");
+  static_assert(HK == 0 || EPI == GB_EPI_STORE || EPI == GB_EPI_SWIGLU_BWD,
+                "the RoPE / SwiGLU forward epilogues are bf16-only");
   static_assert(!LATE || EPI == GB_EPI_ROPE || EPI == GB_EPI_SWIGLU_BWD, "epilogue-first staging: loading epilogues");
   using Cf = GbCfg<BN>;
   constexpr int TS = EPI == GB_EPI_SWIGLU ? 96 : BN;  // tile stride in B rows
@@ -772,10 +784,10 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
             const bool want_s = ep.s_out != nullptr;  // uniform
 #pragma unroll
             for (int h = 0; h < 4; ++h) {
-              float d[2] = {__uint_as_float(cv[h] << 16), __uint_as_float(cv[h] & 0xffff0000u)};
-              const uint32_t gw = gv[mt][p][h], uw = uv[mt][p][h];
-              float g[2] = {__uint_as_float(gw << 16), __uint_as_float(gw & 0xffff0000u)};
-              float u[2] = {__uint_as_float(uw << 16), __uint_as_float(uw & 0xffff0000u)};
+              float d[2], g[2], u[2];
+              gb_unpack2<HK>(cv[h], d);
+              gb_unpack2<HK>(gv[mt][p][h], g);
+              gb_unpack2<HK>(uv[mt][p][h], u);
               floatx4_t r, sv;
 #pragma unroll
               for (int e = 0; e < 2; ++e) {
@@ -785,10 +797,10 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
                 sv[e] = g[e] * sg * u[e];  // s = silu(g) * u: k_swiglu_fwd's arithmetic, same bits
                 sv[2 + e] = 0.f;
               }
-              const uint2 pr = gb_pack(r);  // (dg0, dg1), (du0, du1)
+              const uint2 pr = gb_pack_hk<HK>(r);  // (dg0, dg1), (du0, du1)
               og[h] = pr.x;
               ou[h] = pr.y;
-              os[h] = gb_pack(sv).x;
+              os[h] = gb_pack_hk<HK>(sv).x;
             }
             // dgu has gu's layout (ldc == ld_s): the load offsets address it too
             const int so = mt * 16 * ldc * 2;
@@ -883,14 +895,16 @@ static inline bool gb_shape_ok(int M, int N, int K, int lda, int ldb, int ldc) {
   return M > 0 && N > 0 && M % 256 == 0 && K % 128 == 0 && K >= 128 && (lda | ldb | ldc) % 8 == 0;
 }
 
-// C = A . B^T (bf16).  Only the 192-column tile is instantiated: the 256-column one
-// needs 256 accumulator + fragment VGPRs per lane and spills at 8 waves per CU.
+// C = A . B^T (bf16, or IEEE half with hk = 1).  Only the 192-column tile is
+// instantiated: the 256-column one needs 256 accumulator + fragment VGPRs per lane and
+// spills at 8 waves per CU.
 DLT_API int dlt_gemm_bf16_tn(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K, int lda, int ldb,
-                             int ldc, int flags, hipStream_t st) {
+                             int ldc, int flags, int hk, hipStream_t st) {
   if (!gb_shape_ok(M, N, K, lda, ldb, ldc) || N % 192) return -1;
   const int ntiles = (M / 256) * (N / 192);
   GbEpi ep{};
-  k_gemm_bf16<192, GB_EPI_STORE><<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, ep);
+  DLT_HK_DISPATCH(hk, k_gemm_bf16<192, GB_EPI_STORE, false, HKC><<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(
+                          A, B, C, M, N, K, lda, ldb, ldc, flags, ep));
   DLT_CHECK_LAUNCH();
 }
 
@@ -924,18 +938,22 @@ DLT_API int dlt_gemm_bf16_nn(const bf16_t* dY, const bf16_t* W, bf16_t* dX, int 
 }
 
 // Down-projection data gradient fused with the SwiGLU backward: ds = dd[M, H] . Wdown[H, I]
-// (bf16-rounded) and dgu[M, 2I] from ds and the kept gu[M, 2I] (k_swiglu_bwd's math).
+// (rounded to the activation format) and dgu[M, 2I] from ds and the kept gu[M, 2I]
+// (k_swiglu_bwd's math).  hk: activation format (0 bf16, 1 IEEE half).
 DLT_API int dlt_gemm_bf16_down_swiglu_bwd(const bf16_t* dd, const bf16_t* Wdown, const bf16_t* gu, bf16_t* dgu,
-                                          bf16_t* s_out, int M, int I, int H, int flags, hipStream_t st) {
+                                          bf16_t* s_out, int M, int I, int H, int flags, int hk, hipStream_t st) {
   if (!gb_shape_ok(M, I, H, H, I, 2 * I) || I % 192) return -1;
   const int ntiles = (M / 256) * (I / 192);
   GbEpi ep{nullptr, nullptr, 1, 0, s_out, 2 * I, I, gu};  // s_out (optional): s [M, I], row stride I
-  if (flags & 4096)  // epilogue-first staging of the next tile
-    k_gemm_bf16<192, GB_EPI_SWIGLU_BWD, true, 0, true>
-        <<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(dd, Wdown, dgu, M, I, H, H, I, 2 * I, flags, ep);
-  else
-    k_gemm_bf16<192, GB_EPI_SWIGLU_BWD, true>
-        <<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(dd, Wdown, dgu, M, I, H, H, I, 2 * I, flags, ep);
+  if (flags & 4096) {  // epilogue-first staging of the next tile
+    DLT_HK_DISPATCH(hk, k_gemm_bf16<192, GB_EPI_SWIGLU_BWD, true, HKC, true>
+                            <<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(dd, Wdown, dgu, M, I, H, H, I, 2 * I,
+                                                                           flags, ep));
+  } else {
+    DLT_HK_DISPATCH(hk, k_gemm_bf16<192, GB_EPI_SWIGLU_BWD, true, HKC>
+                            <<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(dd, Wdown, dgu, M, I, H, H, I, 2 * I,
+                                                                           flags, ep));
+  }
   DLT_CHECK_LAUNCH();
 }
 

@@ -292,6 +292,14 @@ class HipGemm:
         self._hand_wgrad = os.environ.get("DLT_WGRAD_HAND", "1") != "0"
         self._fuse = os.environ.get("DLT_GEMM_FUSED", "1") != "0"
         self._dgrad_on = os.environ.get("DLT_GEMM_DGRAD", "1") != "0"
+        # fp16 activations on the hand-written forward (the plan's shape pins) and fused
+        # down-dgrad + SwiGLU-backward kernels (both instantiated for IEEE half and
+        # tested): DLT_GEMM_FP16_HAND=1 ("fwd" / "dswiglu": only one of the two).  Off by
+        # default: --precision fp16 steps measured 744-749k with them vs 744-756k on
+        # hipBLASLt + the unfused SwiGLU backward (tools/ab/r5_fp16hand.sh, same box)
+        _f16 = os.environ.get("DLT_GEMM_FP16_HAND", "0")
+        self._fp16_hand = _f16 in ("1", "fwd")
+        self._fp16_dswiglu = _f16 in ("1", "dswiglu")
         _INSTANCES.append(weakref.ref(self))
 
     def _lib_linear(self, x, w, y):
@@ -357,7 +365,7 @@ class HipGemm:
         y = torch.empty(M, N, dtype=x.dtype, device=x.device) if out is None else out
         pick = self._pick(x, w, y) if self._race and self._hand16_ok(x, w) else None
         from . import hip
-        if pick == "bf16" and x.dtype == torch.bfloat16 and hip.gemm_bf16(x, w, out=y) is not None:
+        if pick == "bf16" and (x.dtype == torch.bfloat16 or self._fp16_hand) and hip.gemm_bf16(x, w, out=y) is not None:
             return y
         if pick == "tn4" and hip.gemm_tn4(x, w, out=y) is not None:
             return y
@@ -369,13 +377,14 @@ class HipGemm:
         per key; kinds "rope" / "swiglu" / "dswiglu" are fused epilogues
         (``DLT_GEMM_FUSED=0`` turns them off), "dgrad" the plain data-gradient GEMM."""
         plain = kind.startswith("dgrad")  # the data-gradient kernel (bf16 and fp16 instances)
+        both16 = plain or kind == "dswiglu16"  # kernels instantiated for both 16-bit formats
         on = self._fuse if not plain else True
-        if not (on and (self._hand16_ok(x, w) if plain else self._hand_ok(x, w))):
+        if not (on and (self._hand16_ok(x, w) if both16 else self._hand_ok(x, w))):
             return False
         key = key or (kind, x.shape[0], w.shape[0], x.shape[1])
         choice = self._choice.get(key)
         if choice is None:
-            if not self._can_race(x, w, (torch.bfloat16, torch.float16) if plain else (torch.bfloat16,)):
+            if not self._can_race(x, w, (torch.bfloat16, torch.float16) if both16 else (torch.bfloat16,)):
                 return False  # not recorded: decided again when racing is possible
             choice = _time_of(fused, inner=3) < self.RACE_MARGIN * _time_of(unfused, inner=3)
             self._choice[key] = choice
@@ -485,9 +494,12 @@ class HipGemm:
 
         def fused():
             hip.gemm_down_swiglu_bwd(dd, wdown, gu, out=dgu, s_out=s_out)
+        # bf16 and fp16 race separately (kind "dswiglu" / "dswiglu16")
+        kind = "dswiglu" if dd.dtype == torch.bfloat16 else "dswiglu16"
         ok = (self._dgrad_on and self._race and hip.gemm_bf16_fits(M, I, H) and tuple(gu.shape) == (M, 2 * I)
-              and self._hand_ok(gu, dgu) and (s_out is None or self._hand_ok(s_out)))
-        if ok and self._fused_pick("dswiglu", dd, wdown, fused, unfused, key=("dswiglu", M, I, H)):
+              and (dd.dtype == torch.bfloat16 or self._fp16_dswiglu)
+              and self._hand16_ok(dd, wdown, gu, dgu, *(() if s_out is None else (s_out,))))
+        if ok and self._fused_pick(kind, dd, wdown, fused, unfused, key=(kind, M, I, H)):
             fused()
         else:
             unfused()

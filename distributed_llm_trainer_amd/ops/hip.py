@@ -62,7 +62,8 @@ _SIGS = {
     "dlt_gemm_wgrad_sk": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                           c_int, c_void_p],
     "dlt_scale_bf16": [c_void_p, c_void_p, ctypes.c_long, c_void_p, c_float, c_int, c_void_p],
-    "dlt_gemm_bf16_tn": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "dlt_gemm_bf16_tn": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                         c_void_p],
     "dlt_gemm_tn4": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "dlt_gemm_bf16_qkv_rope": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                                c_void_p],
@@ -70,7 +71,7 @@ _SIGS = {
     "dlt_gemm_bf16_nn": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                          c_void_p],
     "dlt_gemm_bf16_down_swiglu_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                                      c_void_p],
+                                      c_int, c_void_p],
     "dlt_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                      c_uint32, c_uint32, c_float, c_int, c_int, c_void_p],
     "dlt_attn_dropout_mask": [c_void_p, c_int, c_int, c_int, c_uint32, c_uint32, c_void_p],
@@ -846,18 +847,20 @@ def gemm_bf16_fits(M: int, N: int, K: int) -> bool:
 
 
 def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
-    """C[M,N] = A[M,K] @ B[N,K]^T (bf16 in/out, fp32 accumulate) with the hand-written
-    persistent MFMA kernel.  Returns None (nothing launched) when the shape does not
-    tile (M % 256, N % 192, K % 128)."""
+    """C[M,N] = A[M,K] @ B[N,K]^T (bf16 or fp16 in/out, one format; fp32 accumulate) with
+    the hand-written persistent MFMA kernel.  Returns None (nothing launched) when the
+    shape does not tile (M % 256, N % 192, K % 128)."""
     M, K = a.shape
     N = b.shape[0]
     if not gemm_bf16_fits(M, N, K) or b.shape[1] != K:
         return None
-    _req(a, torch.bfloat16, "gemm_bf16.a")
-    _req(b, torch.bfloat16, "gemm_bf16.b")
-    c = torch.empty(M, N, dtype=torch.bfloat16, device=a.device) if out is None else out
-    _req(c, torch.bfloat16, "gemm_bf16.c", M * N)
-    _chk(lib().dlt_gemm_bf16_tn(_p(a), _p(b), _p(c), M, N, K, K, K, N, _fwd_flags(), _stream()), "gemm_bf16")
+    dt = a.dtype if a.dtype in _WG_HK else torch.bfloat16
+    _req(a, dt, "gemm_bf16.a")
+    _req(b, dt, "gemm_bf16.b")
+    c = torch.empty(M, N, dtype=dt, device=a.device) if out is None else out
+    _req(c, dt, "gemm_bf16.c", M * N)
+    _chk(lib().dlt_gemm_bf16_tn(_p(a), _p(b), _p(c), M, N, K, K, K, N, _fwd_flags(), _WG_HK[dt], _stream()),
+         "gemm_bf16")
     return c
 
 
@@ -958,15 +961,16 @@ def gemm_down_swiglu_bwd(dd: torch.Tensor, wdown: torch.Tensor, gu: torch.Tensor
     I = wdown.shape[1]
     if not gemm_bf16_fits(M, I, H) or wdown.shape[0] != H or tuple(gu.shape) != (M, 2 * I):
         return None
-    _req(dd, torch.bfloat16, "gemm_down_swiglu_bwd.dd")
-    _req(wdown, torch.bfloat16, "gemm_down_swiglu_bwd.w")
-    _req(gu, torch.bfloat16, "gemm_down_swiglu_bwd.gu")
-    c = torch.empty(M, 2 * I, dtype=torch.bfloat16, device=dd.device) if out is None else out
-    _req(c, torch.bfloat16, "gemm_down_swiglu_bwd.out", M * 2 * I)
+    dt = dd.dtype if dd.dtype in _WG_HK else torch.bfloat16  # bf16 or fp16, one format for all
+    _req(dd, dt, "gemm_down_swiglu_bwd.dd")
+    _req(wdown, dt, "gemm_down_swiglu_bwd.w")
+    _req(gu, dt, "gemm_down_swiglu_bwd.gu")
+    c = torch.empty(M, 2 * I, dtype=dt, device=dd.device) if out is None else out
+    _req(c, dt, "gemm_down_swiglu_bwd.out", M * 2 * I)
     if s_out is not None:
-        _req(s_out, torch.bfloat16, "gemm_down_swiglu_bwd.s_out", M * I)
+        _req(s_out, dt, "gemm_down_swiglu_bwd.s_out", M * I)
     _chk(lib().dlt_gemm_bf16_down_swiglu_bwd(_p(dd), _p(wdown), _p(gu), _p(c), _p(s_out), M, I, H, _GB_FLAGS,
-                                             _stream()), "gemm_down_swiglu_bwd")
+                                             _WG_HK[dt], _stream()), "gemm_down_swiglu_bwd")
     return c
 
 

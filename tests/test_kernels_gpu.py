@@ -553,16 +553,20 @@ def _relerr(got, want):
 
 # the model's forward-projection shapes at the fused-chain size (M = 16384 rows), a
 # medium-size projection, and small multi-round / partial-round grids
-@pytest.mark.parametrize("M,N,K", [(16384, 2304, 768), (16384, 768, 768), (16384, 768, 3072), (16384, 6144, 768),
-                                   (4096, 3072, 1024), (512, 384, 256), (2560, 1152, 384)])
-def test_gemm_bf16(M, N, K):
+@pytest.mark.parametrize("M,N,K,dtype", [(16384, 2304, 768, torch.bfloat16), (16384, 768, 768, torch.bfloat16),
+                                         (16384, 768, 3072, torch.bfloat16), (16384, 6144, 768, torch.bfloat16),
+                                         (4096, 3072, 1024, torch.bfloat16), (512, 384, 256, torch.bfloat16),
+                                         (2560, 1152, 384, torch.bfloat16), (16384, 2304, 768, torch.float16),
+                                         (2560, 1152, 384, torch.float16)])
+def test_gemm_bf16(M, N, K, dtype):
     """Persistent hand-written MFMA GEMM C = A B^T (csrc/gemm_bf16.hip) vs fp32 torch:
-    every element within bf16 output rounding (relative to the tensor's max)."""
+    every element within 16-bit output rounding (relative to the tensor's max); bf16 and
+    IEEE-half operands (the --precision fp16 instantiation)."""
     torch.manual_seed(M + N + K)
-    a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
-    b = (torch.rand(N, K, device=DEV) * 2 - 1).bfloat16()
+    a = (torch.rand(M, K, device=DEV) * 2 - 1).to(dtype)
+    b = (torch.rand(N, K, device=DEV) * 2 - 1).to(dtype)
     c = hip.gemm_bf16(a, b)
-    assert c is not None
+    assert c is not None and c.dtype == dtype
     want = a.float() @ b.float().t()
     assert _relerr(c, want) < 8e-3
     _close(c, want, 8e-3 * want.abs().max().item(), 8e-3, "gemm_bf16")
@@ -683,29 +687,32 @@ def test_gemm_dgrad_fp16_vs_fp32(M, Nout, Nred):
         hip.gemm_dgrad(dy.float(), w.float())
 
 
-@pytest.mark.parametrize("M", [512, 16384])
-def test_gemm_down_swiglu_bwd_vs_fp32(M, gemm_late_flag):
+@pytest.mark.parametrize("M,dtype", [(512, torch.bfloat16), (16384, torch.bfloat16), (512, torch.float16),
+                                     (16384, torch.float16)])
+def test_gemm_down_swiglu_bwd_vs_fp32(M, dtype, gemm_late_flag):
     """Down-projection dgrad with the SwiGLU backward in the epilogue == the fp32 product
-    rounded to bf16 (what the unfused dgrad writes) through k_swiglu_bwd's math, and ==
-    hip.swiglu_bwd on the library dgrad within bf16 rounding.  M 16384: 4 tiles per
-    persistent workgroup (the epilogue-first staging's cross-tile path)."""
+    rounded to the activation format (what the unfused dgrad writes) through
+    k_swiglu_bwd's math, and == hip.swiglu_bwd on the library dgrad within 16-bit
+    rounding; bf16 and IEEE half.  M 16384: 4 tiles per persistent workgroup (the
+    epilogue-first staging's cross-tile path)."""
     torch.manual_seed(7)
     H, I = 768, 3072
-    dd = (torch.rand(M, H, device=DEV) * 2 - 1).bfloat16()
-    wd = ((torch.rand(H, I, device=DEV) * 2 - 1) / H ** 0.5).bfloat16()
-    gu = (torch.randn(M, 2 * I, device=DEV) * 2).bfloat16()
+    dd = (torch.rand(M, H, device=DEV) * 2 - 1).to(dtype)
+    wd = ((torch.rand(H, I, device=DEV) * 2 - 1) / H ** 0.5).to(dtype)
+    gu = (torch.randn(M, 2 * I, device=DEV) * 2).to(dtype)
     dgu = hip.gemm_down_swiglu_bwd(dd, wd, gu)
-    ds = (dd.float() @ wd.float()).bfloat16().float()
+    assert dgu.dtype == dtype
+    ds = (dd.float() @ wd.float()).to(dtype).float()
     g, u = gu.float()[:, :I], gu.float()[:, I:]
     sg = torch.sigmoid(g)
     want = torch.cat([ds * u * sg * (1 + g * (1 - sg)), ds * g * sg], dim=1)
     assert torch.isfinite(dgu.float()).all()
     assert _relerr(dgu, want) < 1.5e-2, _relerr(dgu, want)
-    ref_k = hip.swiglu_bwd(gu, (dd.float() @ wd.float()).bfloat16())
+    ref_k = hip.swiglu_bwd(gu, (dd.float() @ wd.float()).to(dtype))
     assert _relerr(dgu, ref_k.float()) < 1.5e-2
     # s_out: s = silu(g) * u with the forward kernel's exact bits (the engine's s ring),
     # the dgu output unchanged by it
-    s = torch.full((M, I), float("nan"), dtype=torch.bfloat16, device=DEV)
+    s = torch.full((M, I), float("nan"), dtype=dtype, device=DEV)
     dgu2 = hip.gemm_down_swiglu_bwd(dd, wd, gu, s_out=s)
     assert torch.equal(dgu2, dgu)
     assert torch.equal(s, hip.swiglu_fwd(gu))

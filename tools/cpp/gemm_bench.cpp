@@ -53,7 +53,7 @@ typedef int (*launch_fn)(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, h
 
 template <int FLAGS>
 static int run_bf16(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K, hipStream_t s) {
-  return dlt_gemm_bf16_tn(A, B, C, M, N, K, K, K, N, FLAGS, s);
+  return dlt_gemm_bf16_tn(A, B, C, M, N, K, K, K, N, FLAGS, 0, s);
 }
 
 // hipBLASLt reference (system ROCm 7.2 library, best of the first 24 heuristic candidates,
@@ -249,7 +249,7 @@ static int epi_main(int M, int H, int I, int S) {
       }
     }
     const float tf = time_us(fused, st), tu = time_us(unfused, st);
-    const float tp = time_us([&]() { return dlt_gemm_bf16_tn(A, B, C, M, N, K, K, K, N, ef, st); }, st);
+    const float tp = time_us([&]() { return dlt_gemm_bf16_tn(A, B, C, M, N, K, K, K, N, ef, 0, st); }, st);
     printf("  plain bf16 %.1f us (flags %d)\n", tp, ef);
     printf("%s M=%d N=%d K=%d: fused %.1f us | hipBLASLt + %s %.1f us | err %.1e%s%.1e\n",
            which == 0 ? "qkv+rope" : "gu+swiglu", M, N, K, tf, which == 0 ? "rope" : "swiglu", tu, e1 / m1,
@@ -395,7 +395,7 @@ static int dgrad_main(std::vector<int> shp) {
     std::vector<bf16_t> hgu((size_t)nr * 2 * I), got((size_t)nr * 2 * I);
     CK(hipMemcpyAsync(ref.data(), R, ref.size() * 4, hipMemcpyDeviceToHost, st));
     CK(hipMemcpyAsync(hgu.data(), gu + (size_t)r0 * 2 * I, hgu.size() * 2, hipMemcpyDeviceToHost, st));
-    auto fused = [&]() { return dlt_gemm_bf16_down_swiglu_bwd(dd, Wd, gu, dgu, ds, M, I, H, 0, st); };  // + s into ds
+    auto fused = [&]() { return dlt_gemm_bf16_down_swiglu_bwd(dd, Wd, gu, dgu, ds, M, I, H, 0, 0, st); };  // + s into ds
     auto unfused = [&]() {
       int rc = run_blas_nn(dd, Wd, ds, M, I, H, st);
       return rc ? rc : dlt_swiglu_bwd(gu, ds, dgu2, ds, M, I, 0, st);  // + s (in place over ds, as the s ring)
@@ -442,7 +442,7 @@ static int dgrad_main(std::vector<int> shp) {
     }
     for (int fl : fls) {
       for (int ws = 0; ws < 2; ++ws) {
-        auto f = [&]() { return dlt_gemm_bf16_down_swiglu_bwd(dd, Wd, gu, dgu2, ws ? ds : nullptr, M, I, H, fl, st); };
+        auto f = [&]() { return dlt_gemm_bf16_down_swiglu_bwd(dd, Wd, gu, dgu2, ws ? ds : nullptr, M, I, H, fl, 0, st); };
         CK(hipMemsetAsync(dgu2, 0xff, (size_t)M * 2 * I * 2, st));
         if (f()) {
           printf("flags %d launch failed\n", fl);

@@ -86,7 +86,7 @@ int main(int argc, char** argv) {
         else if (mode == 2)
           dlt_gemm_bf16_gu_swiglu(A, B, C, Sb, M, N / 2, K, flags, st);
         else
-          dlt_gemm_bf16_tn(A, B, C, M, N, K, K, K, N, flags, st);
+          dlt_gemm_bf16_tn(A, B, C, M, N, K, K, K, N, flags, 0, st);
       }
       iters += 50;
       CK(hipEventRecord(e1, st));
