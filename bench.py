@@ -175,6 +175,8 @@ def main():
                        **({"cpu_offload": True} if args.cpu_offload else {})},
             "peak_gb_per_gpu": round(peak, 3), "final_loss": round(loss, 4),
             **({"window": eng.last_window, "stream_placement": eng.queue_placement} if eng is not None else {}),
+            **({"window_choice": {"decided": eng.window_auto["decided"], "step_ms": eng.window_auto["ms"]}}
+               if eng is not None and eng.window_auto is not None else {}),
             "vs_baseline_linear": None if overrides else round(tps / (12500.0 * world), 3),
         }
         print(json.dumps(out), flush=True)

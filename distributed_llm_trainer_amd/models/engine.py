@@ -233,6 +233,7 @@ class GPTEngine:
         self._pipe = None  # second compute stream of train_window
         self.queue_placement = None  # how the side streams were placed (_place_streams)
         self.last_window = None  # schedule of the last train_window ("ffbb" | "fb")
+        self.window_auto = None  # trial state of the timed fb / ffbb choice under collectives
         # attention straight on the packed [M, 3H] QKV GEMM output (RoPE in place,
         # inverse RoPE in the backward epilogue); DLT_PACKED_QKV=0 -> split q/k/v copies
         self.packed_qkv = (hasattr(ops, "attention_fwd_packed")
@@ -711,6 +712,8 @@ class GPTEngine:
             return
         want_side = self._side_wanted(dev)
         pad = os.environ.get("DLT_QUEUE_PAD")
+        if pad is None and self.window_auto is not None:
+            pad = "3"  # the timed fb / ffbb choice (window_schedule): ffbb's measured placement
         if pad is not None or os.environ.get("DLT_QUEUE_PROBE", "0") != "1":
             _queue_pad(dev, int(pad or 0))
             # created unbound: each binds its hardware queue at its first dispatch
@@ -1061,11 +1064,12 @@ class GPTEngine:
         (the memory-lean modes keep fb: both forwards' activations live at once cost ~5 GB;
         FSDP's per-micro-step weight gradients: measured no faster, 1.5x the memory), the
         model is GPT-2-small-sized (small +0.9-1.1 %, medium -1.3 %: its larger GEMMs fill
-        the GPU alone, two forwards only contend).  With gradient collectives it is fb: a
-        communicator's streams shift the engine's hardware queues, and ffbb measured 693k
-        vs fb 789k tok/s on one forced RCCL rank (797.5-798.0k with DLT_QUEUE_PAD=3, no
-        communicator 800-801k: profiles/r5_stream_queues.md); only a placement verified by
-        the opt-in probe (DLT_QUEUE_PROBE=1, _place_streams) lifts that.
+        the GPU alone, two forwards only contend).  With gradient collectives a
+        communicator's streams shift the engine's hardware queues (ffbb 693k vs fb 789k tok/s
+        on one forced RCCL rank as placed by default, 797.5-798.0k with three idle streams
+        created first: profiles/r5_stream_queues.md), so the schedule is chosen by timing
+        (_auto_window / _auto_enter, default; DLT_WINDOW_AUTO=0 keeps fb, DLT_QUEUE_PROBE=1
+        uses the opt-in placement probe instead).
         ``DLT_WINDOW_SCHED=fb|ffbb`` overrides (profiles/r3_window_ffbb.md)."""
         overlap = (cuda and GA > 1 and getattr(self.provider, "overlap_backward_ok", False)
                    and os.environ.get("DLT_BWD_OVERLAP", "1") != "0")
@@ -1073,15 +1077,65 @@ class GPTEngine:
         comm = bool(getattr(hooks, "collectives", False) or getattr(self.provider, "collectives", False))
         eligible = (overlap and GA == 2 and defer and self.defer_roles == frozenset(self.ROLES)
                     and self.cfg.hidden_size <= 768)
+        auto = None
         if eligible and comm and "DLT_WINDOW_SCHED" not in os.environ:
             eligible = False
             if os.environ.get("DLT_QUEUE_PROBE") == "1":
                 self._place_streams(torch.device("cuda", torch.cuda.current_device()))
                 eligible = bool(self.queue_placement and self.queue_placement["verified"])
-        sched = os.environ.get("DLT_WINDOW_SCHED", "ffbb" if eligible else "fb")
+            elif os.environ.get("DLT_WINDOW_AUTO", "1") != "0":
+                auto = self._auto_window()
+        sched = auto or os.environ.get("DLT_WINDOW_SCHED", "ffbb" if eligible else "fb")
         if not (overlap and GA == 2 and sched == "ffbb"):
             sched = "fb"
         return overlap, sched
+
+    # Timed choice between the fb and ffbb windows under gradient collectives (default;
+    # DLT_WINDOW_AUTO=0 keeps fb).  With collectives ffbb depends on which hardware queues
+    # the communicator's streams leave the engine's (profiles/r5_stream_queues.md): on one
+    # forced RCCL rank it ran 693k tok/s as placed by default and 797.5-798.0k with three
+    # idle streams created ahead of the engine's (DLT_QUEUE_PAD=3, the default here), fb
+    # 787-790k -- unknown on a multi-GPU node.  So the first pipelined windows run fb,
+    # ffbb, fb, ffbb; at the entry of the next window each schedule's best step time (GPU
+    # events at consecutive window entries, i.e. the whole step) is max-reduced over the
+    # ranks and every rank keeps the faster schedule -- the same decision everywhere, taken
+    # at the same point of the collective sequence.
+    _AUTO_TRIALS = ("fb", "ffbb", "fb", "ffbb")
+
+    def _auto_window(self) -> str:
+        """The schedule of the next window while the choice is open, then the decision."""
+        a = self.window_auto
+        if a is None:
+            a = self.window_auto = {"events": [], "decided": None, "ms": None}
+        if a["decided"] is not None:
+            return a["decided"]
+        return self._AUTO_TRIALS[min(len(a["events"]), len(self._AUTO_TRIALS) - 1)]
+
+    def _auto_enter(self, dev) -> bool:
+        """Window entry while the timed choice is open: stamp it; after the last trial,
+        decide.  True when the decision was just taken (the caller re-reads the schedule)."""
+        a = self.window_auto
+        if a is None or a["decided"] is not None or dev.type != "cuda":
+            return False
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream(dev))
+        a["events"].append(ev)
+        n = len(self._AUTO_TRIALS)
+        if len(a["events"]) <= n:
+            return False
+        ev.synchronize()
+        t = [a["events"][i].elapsed_time(a["events"][i + 1]) for i in range(n)]
+        best = [min(t[i] for i in range(n) if self._AUTO_TRIALS[i] == k) for k in ("fb", "ffbb")]
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            v = torch.tensor(best, dtype=torch.float32, device=dev if dist.get_backend() == "nccl" else "cpu")
+            dist.all_reduce(v, op=dist.ReduceOp.MAX)
+            best = v.tolist()
+        fb, ffbb = (float(x) for x in best)
+        a["decided"] = "ffbb" if ffbb < fb else "fb"
+        a["ms"] = {"fb": round(fb, 3), "ffbb": round(ffbb, 3)}
+        a["events"] = []
+        return True
 
     def _window_ffbb(self, micro_ids, micro_targets, dloss, recompute, defer, sync_hook, before_last,
                      serial=False):
@@ -1216,6 +1270,8 @@ class GPTEngine:
         dev = micro_ids[0].device
         cuda = dev.type == "cuda"
         overlap, sched = self.window_schedule(GA, defer, cuda)
+        if not serial and self._auto_enter(dev):
+            overlap, sched = self.window_schedule(GA, defer, cuda)
         self.last_window = sched
         prog: List[dict] = [dict() for _ in range(GA)]
         if sched == "ffbb":

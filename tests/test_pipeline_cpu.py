@@ -235,6 +235,53 @@ def test_fused_loss_segments_normalise_per_micro_step():
         assert torch.allclose(p1.grad, p2.grad, atol=1e-6, rtol=1e-5), n
 
 
+def test_window_auto_choice(monkeypatch):
+    """Under gradient collectives the window schedule is chosen by timing: the first four
+    pipelined windows run fb, ffbb, fb, ffbb; at the next entry the faster schedule's best
+    whole-step time wins and is kept (stubbed GPU events; the max over ranks is the
+    identity on one rank)."""
+    import types
+    for k in ("DLT_WINDOW_SCHED", "DLT_BWD_OVERLAP", "DLT_QUEUE_PROBE", "DLT_WINDOW_AUTO"):
+        monkeypatch.delenv(k, raising=False)
+    e = GPT(tiny()).enable_engine(seed=1)
+    e.provider.hooks = types.SimpleNamespace(collectives=True)
+
+    def run(step_ms):
+        stamps = iter([sum(step_ms[:i]) for i in range(len(step_ms) + 1)] + [1e9] * 8)
+
+        class Ev:
+            def __init__(self, enable_timing=False):
+                self.t = None
+
+            def record(self, stream=None):
+                self.t = next(stamps)
+
+            def synchronize(self):
+                pass
+
+            def elapsed_time(self, other):
+                return other.t - self.t
+        monkeypatch.setattr(torch.cuda, "Event", Ev)
+        monkeypatch.setattr(torch.cuda, "current_stream", lambda dev=None: None)
+        dev = types.SimpleNamespace(type="cuda")
+        e.window_auto = None
+        seq = []
+        for _ in range(7):
+            _, s = e.window_schedule(2, True, cuda=True)
+            if e._auto_enter(dev):
+                _, s = e.window_schedule(2, True, cuda=True)
+            seq.append(s)
+        return seq
+    # first windows of each kind carry one-time costs: the best of two decides
+    assert run([45.0, 44.0, 41.6, 41.2, 40.0, 40.0]) == ["fb", "ffbb", "fb", "ffbb", "ffbb", "ffbb", "ffbb"]
+    assert e.window_auto["decided"] == "ffbb" and e.window_auto["ms"] == {"fb": 41.6, "ffbb": 41.2}
+    assert run([45.0, 47.0, 41.6, 46.0, 40.0, 40.0]) == ["fb", "ffbb", "fb", "ffbb", "fb", "fb", "fb"]
+    monkeypatch.setenv("DLT_WINDOW_AUTO", "0")
+    e.window_auto = None
+    assert e.window_schedule(2, True, cuda=True) == (True, "fb")
+    assert e.window_auto is None
+
+
 def test_window_schedule_choice(monkeypatch):
     """Two-chain window schedule: ffbb only with overlapped backwards, two chains, every
     weight gradient deferred, a GPT-2-small-sized model, and with gradient collectives in
@@ -268,7 +315,7 @@ def test_window_schedule_choice(monkeypatch):
     placement["verified"] = True
     assert e.window_schedule(2, True, cuda=True) == (True, "ffbb")
     monkeypatch.delenv("DLT_QUEUE_PROBE")
-    assert e.window_schedule(2, True, cuda=True) == (True, "fb")             # default: no probe
+    assert e.window_schedule(2, True, cuda=True) == (True, "fb")             # default: first timed trial
     placement["verified"] = False
     e.provider.hooks = types.SimpleNamespace(collectives=False)
     monkeypatch.setenv("DLT_BWD_OVERLAP", "0")

@@ -3,7 +3,7 @@
 mkdir -p gpurun_out
 set -o pipefail
 export DLT_BACKEND=gloo DLT_SHARE_GPU=1
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 3 --warmup 1 > gpurun_out/mr_ddp.log 2>&1 && \
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 6 --warmup 1 > gpurun_out/mr_ddp.log 2>&1 && \
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 3 --warmup 1 --mode fsdp > gpurun_out/mr_fsdp.log 2>&1 && \
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 4 --steps 2 --warmup 1 > gpurun_out/mr_ddp4.log 2>&1
 rc=$?
