@@ -128,6 +128,21 @@ def _forced(rank, world, mode):
             tr.train_step({"input_ids": torch.randint(0, HANDCFG["vocab_size"], (4, 256), generator=g)})
         rep = gemm.race_report()
         return {"flat": tr.flat_params().detach().float().cpu().clone()}, (tr.ddp.launched, rep)
+    if mode == "ddp_auto":
+        # enough steps for the timed fb / ffbb choice (first step unpipelined, four trial
+        # windows, the decision at the next window's entry)
+        from distributed_llm_trainer_amd.training.configs import TrainingConfig
+        from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
+        tc = TrainingConfig(batch_size=2, gradient_accumulation_steps=2, warmup_steps=1, max_steps=100,
+                            learning_rate=1e-3, bucket_cap_mb=2.0)
+        tr = DistributedTrainer(GPTConfig(**HANDCFG), tc)
+        assert tr.device.type == "cuda" and dist.get_backend() == "nccl"
+        for s in range(7):
+            g = torch.Generator().manual_seed(77 + s)
+            tr.train_step({"input_ids": torch.randint(0, HANDCFG["vocab_size"], (4, 256), generator=g)})
+        eng = tr.model.engine
+        auto = dict(eng.window_auto) if eng.window_auto is not None else None
+        return {"flat": tr.flat_params().detach().float().cpu().clone()}, (eng.last_window, auto)
     if mode == "fsdp_hand":
         from distributed_llm_trainer_amd.training.configs import FSDPConfig, FSDPTrainingConfig
         from distributed_llm_trainer_amd.training.fsdp_trainer import FSDPTrainer
@@ -180,6 +195,22 @@ def test_rccl_forced_collectives_with_hand_kernels(tmp_path, mode):
     assert rep == rep_b
     # the hand-written kernels are among the choices (shapes tile by construction)
     assert any("hand-written" in v or "fused gemm_bf16" in v for v in rep.values()), rep
+    for k in a:
+        assert torch.equal(a[k], b[k]), (k, (a[k] - b[k]).abs().max().item())
+
+
+def test_rccl_forced_collectives_timed_window_choice():
+    """Under forced RCCL collectives the window schedule is chosen by timing (four trial
+    windows fb / ffbb, then the faster one): the decision is taken and recorded, and the
+    parameters equal bit for bit those of the run without a communicator (ffbb throughout:
+    every schedule runs the same kernels in the same accumulation order)."""
+    env = {"DLT_FORCE_CPU": None, "DLT_BACKEND": "nccl"}
+    a, (win_a, auto_a) = run_multiprocess(_forced, world=1, args=("ddp_auto",), env=env, timeout=300)[0]
+    b, (win_b, auto_b) = run_multiprocess(_forced, world=1, args=("ddp_auto",),
+                                          env={**env, "DLT_FORCE_COLLECTIVES": "1"}, timeout=300)[0]
+    assert auto_a is None and win_a == "ffbb"
+    assert auto_b is not None and auto_b["decided"] in ("fb", "ffbb") and win_b == auto_b["decided"], auto_b
+    assert set(auto_b["ms"]) == {"fb", "ffbb"}
     for k in a:
         assert torch.equal(a[k], b[k]), (k, (a[k] - b[k]).abs().max().item())
 
