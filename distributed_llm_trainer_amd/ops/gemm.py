@@ -296,7 +296,7 @@ class HipGemm:
         # down-dgrad + SwiGLU-backward kernels (both instantiated for IEEE half and
         # tested): DLT_GEMM_FP16_HAND=1 ("fwd" / "dswiglu": only one of the two).  Off by
         # default: --precision fp16 steps measured 744-749k with them vs 744-756k on
-        # hipBLASLt + the unfused SwiGLU backward (tools/ab/r5_fp16hand.sh, same box)
+        # hipBLASLt + the unfused SwiGLU backward (tools/ab/r5/r5_fp16hand.sh, same box)
         _f16 = os.environ.get("DLT_GEMM_FP16_HAND", "0")
         self._fp16_hand = _f16 in ("1", "fwd")
         self._fp16_dswiglu = _f16 in ("1", "dswiglu")

@@ -3,5 +3,5 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 V="lib:DLT_X=0"
-for r in qkv o gu down head; do V="$V $r:DLT_GEMM_PLAN=tools/ab/plan_r5_one_$r.json"; done
+for r in qkv o gu down head; do V="$V $r:DLT_GEMM_PLAN=tools/ab/r5/plan_r5_one_$r.json"; done
 VARIANTS="$V" REPS=3 bash tools/ab/env_ab.sh

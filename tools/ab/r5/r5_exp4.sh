@@ -12,7 +12,7 @@ runc() { n=$1; shift; timeout -k 10 300 env $R "$@" python bench.py --steps 20 -
 runc cfb MASTER_PORT=29631 && runc cffbb MASTER_PORT=29632 DLT_WINDOW_SCHED=ffbb && \
   runc cffbbhp MASTER_PORT=29633 DLT_WINDOW_SCHED=ffbb TORCH_NCCL_HIGH_PRIORITY=1 && \
   runc cfbhp MASTER_PORT=29634 TORCH_NCCL_HIGH_PRIORITY=1 && runc plain MASTER_PORT=29635 DLT_FORCE_COLLECTIVES=0 || exit 1
-H=tools/ab/plan_r5_fwdhand.json
+H=tools/ab/r5/plan_r5_fwdhand.json
 run() { n=$1; shift; timeout -k 10 300 env "$@" python bench.py --steps 20 --warmup 3 > gpurun_out/e4_$n.log 2> gpurun_out/e4_$n.err || { tail -20 gpurun_out/e4_$n.err; exit 1; }; show gpurun_out/e4_$n.log $n; }
 for rep in 1 2; do
   run lib.$rep DLT_X=0 && run hand.$rep DLT_GEMM_PLAN=$H && run handgrp.$rep DLT_GEMM_PLAN=$H DLT_GEMM_FWD_FLAGS=3072 && \

@@ -11,8 +11,8 @@ runc pad0 MASTER_PORT=29641 && runc pad1 MASTER_PORT=29642 DLT_QUEUE_PAD=1 && ru
   runc pad3 MASTER_PORT=29644 DLT_QUEUE_PAD=3 || exit 1
 run() { n=$1; shift; timeout -k 10 300 env "$@" python bench.py --steps 20 --warmup 3 > gpurun_out/e5_$n.log 2> gpurun_out/e5_$n.err || { tail -20 gpurun_out/e5_$n.err; exit 1; }; show gpurun_out/e5_$n.log $n; }
 for rep in 1 2; do
-  run lib.$rep DLT_X=0 && run od.$rep DLT_GEMM_PLAN=tools/ab/plan_r5_od.json && \
-    run od1t.$rep DLT_GEMM_PLAN=tools/ab/plan_r5_od.json DLT_GEMM_FWD_FLAGS=3340 && \
-    run odq1t.$rep DLT_GEMM_PLAN=tools/ab/plan_r5_odq.json DLT_GEMM_FWD_FLAGS=3340 && \
+  run lib.$rep DLT_X=0 && run od.$rep DLT_GEMM_PLAN=tools/ab/r5/plan_r5_od.json && \
+    run od1t.$rep DLT_GEMM_PLAN=tools/ab/r5/plan_r5_od.json DLT_GEMM_FWD_FLAGS=3340 && \
+    run odq1t.$rep DLT_GEMM_PLAN=tools/ab/r5/plan_r5_odq.json DLT_GEMM_FWD_FLAGS=3340 && \
     run desync.$rep DLT_GEMM_FLAGS=201330188 || exit 1
 done

@@ -12,6 +12,6 @@ cat gpurun_out/e9_iso.log
 show() { python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d['ms_per_step'], d['peak_gb_per_gpu'], d['final_loss'])" "$1" "$2"; }
 run() { n=$1; shift; timeout -k 10 300 env "$@" python bench.py --steps 20 --warmup 3 > gpurun_out/e9_$n.log 2> gpurun_out/e9_$n.err || { tail -20 gpurun_out/e9_$n.err; exit 1; }; show gpurun_out/e9_$n.log $n; }
 for rep in 1 2; do
-  run lib.$rep DLT_X=0 && run all.$rep DLT_GEMM_PLAN=tools/ab/plan_r5_tn4all.json && \
-    run noh.$rep DLT_GEMM_PLAN=tools/ab/plan_r5_tn4noh.json && run od.$rep DLT_GEMM_PLAN=tools/ab/plan_r5_tn4od.json || exit 1
+  run lib.$rep DLT_X=0 && run all.$rep DLT_GEMM_PLAN=tools/ab/r5/plan_r5_tn4all.json && \
+    run noh.$rep DLT_GEMM_PLAN=tools/ab/r5/plan_r5_tn4noh.json && run od.$rep DLT_GEMM_PLAN=tools/ab/r5/plan_r5_tn4od.json || exit 1
 done

@@ -4,7 +4,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 mkdir -p gpurun_out
-H=tools/ab/plan_r5_fwdhand.json
+H=tools/ab/r5/plan_r5_fwdhand.json
 run() { n=$1; shift; timeout -k 10 300 env "$@" python bench.py --steps 20 --warmup 3 > gpurun_out/f5_$n.log 2> gpurun_out/f5_$n.err || { tail -20 gpurun_out/f5_$n.err; exit 1; }; python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d['ms_per_step'], d['peak_gb_per_gpu'])" gpurun_out/f5_$n.log $n; }
 for rep in 1 2; do
   run lib.$rep DLT_X=0 &&
