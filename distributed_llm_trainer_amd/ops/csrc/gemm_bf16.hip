@@ -77,8 +77,9 @@ __device__ __forceinline__ int gb_arow(int q, int g) { return (g >> 2) * 64 + q 
 template <int BN>
 __device__ __forceinline__ int gb_brow(int q, int g) {
   if (q == 0) return (g >> 3) * (BN / 2) + (g & 7) * 8;
-  constexpr int per = (BN / 2 - 64) / 8;  // groups per N half in unit 1
-  return (g / per) * (BN / 2) + 64 + (g % per) * 8;
+  constexpr int per = (BN / 2 - 64) / 8;  // groups per N half in unit 1 (none at BN = 128)
+  if constexpr (per == 0) return 0;
+  else return (g / per) * (BN / 2) + 64 + (g % per) * 8;
 }
 
 }  // namespace
@@ -198,8 +199,9 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
                                                       bf16_t* __restrict__ C, int M, int N, int K, int lda, int ldb,
                                                       int ldc, int flags, GbEpi ep) {
   static_assert(EPI == GB_EPI_STORE || BN == 192, "pair epilogues need the 192-column tile");
-  static_assert(!BT || (BN == 192 && (EPI == GB_EPI_STORE || EPI == GB_EPI_SWIGLU_BWD)),
-                "the reduction-major B form is the 192-column data-gradient kernel");
+  static_assert(!BT || (BN == 192 && (EPI == GB_EPI_STORE || EPI == GB_EPI_SWIGLU_BWD)) ||
+                    (BN == 128 && EPI == GB_EPI_STORE),
+                "the reduction-major B form is the 192- (or plain 128-) column data-gradient kernel");
   static_assert(HK == 0 || EPI == GB_EPI_STORE || EPI == GB_EPI_SWIGLU_BWD,
                 "the RoPE / SwiGLU forward epilogues are bf16-only");
   static_assert(!LATE || EPI == GB_EPI_ROPE || EPI == GB_EPI_SWIGLU_BWD, "epilogue-first staging: loading epilogues");
@@ -275,7 +277,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
   bf16_t* const B1i = lds + Cf::BUF + Cf::IMG_A;
 
   // per-lane source offsets (bytes, relative to the tile's first row at column kt*BK)
-  uint32_t oa[2][2], ob0[2], ob1[Cf::B1_DMA];
+  uint32_t oa[2][2], ob0[2], ob1[Cf::B1_DMA > 0 ? Cf::B1_DMA : 1];
 #pragma unroll
   for (int q = 0; q < 2; ++q)
 #pragma unroll
@@ -292,9 +294,9 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
     for (int j = 0; j < 2; ++j) {
       const int e = (wid * 2 + j) * 64 + lane;
       const int t = e >> 4, lc = (e & 15) ^ (2 * gw_v256(t));
-      ob0[j] = (uint32_t)(t * ldb + gw_b0map(lc * 8)) * 2u;
+      ob0[j] = (uint32_t)(t * ldb + gw_b0map<BN>(lc * 8)) * 2u;
     }
-    {
+    if constexpr (Cf::B1_DMA > 0) {
       const int e = wid * 64 + lane;
       const int t = e >> 3, lc = (e & 7) ^ (2 * gw_v128(t));
       ob1[0] = (uint32_t)(t * ldb + gw_b1map(lc * 8)) * 2u;
@@ -391,7 +393,14 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
     for (int j = 0; j < 2; ++j) kb1[j] = L128.base + L128.koff(2 * wn + j);
   }
   auto read_b = [&](const bf16_t* img, int qn, bf16x8_t (&fb)[NH][2]) {
-    if constexpr (BT) {
+    if constexpr (BT && BN == 128) {
+      // n-half qn: n-tiles 2qn, 2qn + 1, both from B0 (the image holds the tile's columns)
+      const uint32_t i0 = (uint32_t)(uintptr_t)img;
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int nt = 0; nt < NH; ++nt) fb[nt][s] = gw_frag<256>(i0 + kb0[qn * NH + nt], s);
+    } else if constexpr (BT) {
       // n-half 0: n-tiles 0..2 (B0); n-half 1: n-tile 3 (B0) and 4..5 (B1)
       const uint32_t i0 = (uint32_t)(uintptr_t)img, i1 = i0 + GW_IMG_A * 2;
 #pragma unroll
@@ -414,7 +423,11 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
     }
   };
   auto mma = [&](int qm, int qn, bf16x8_t (&fb)[NH][2]) {
-    if constexpr (BT) {
+    if constexpr (BT && NH == 2) {
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(fa[0][0]), "+v"(fa[0][1]), "+v"(fa[1][0]), "+v"(fa[1][1]), "+v"(fb[0][0]), "+v"(fb[0][1]),
+                     "+v"(fb[1][0]), "+v"(fb[1][1])::"memory");
+    } else if constexpr (BT) {
       // the transposed reads are asm (invisible to the compiler's lgkmcnt tracking): the
       // fragments are in/out operands of the wait so no MFMA is scheduled above it
       asm volatile("s_waitcnt lgkmcnt(0)"
@@ -675,7 +688,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
         // per lane otherwise write 16 rows x 32 + 8 bytes each)
         // (LATE RoPE: row-per-lane permlane stores -- the staging ds_writes would make the
         // compiler drain the next tile's in-flight LDS-DMA first)
-        const bool lt = EPI == GB_EPI_SWIGLU || (EPI != GB_EPI_SWIGLU_BWD && !BT && !LATE && (flags & 1024));
+        const bool lt = EPI == GB_EPI_SWIGLU || (EPI != GB_EPI_SWIGLU_BWD && !BT && !LATE && BN == 192 && (flags & 1024));
         if constexpr (EPI == GB_EPI_SWIGLU) {
           uint2 sp[3];
           // s = silu(g) * u on the bf16-rounded gate/up values (the packs stored as gu);
@@ -900,11 +913,17 @@ static inline bool gb_shape_ok(int M, int N, int K, int lda, int ldb, int ldc) {
 // spills at 8 waves per CU.
 DLT_API int dlt_gemm_bf16_tn(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K, int lda, int ldb,
                              int ldc, int flags, int hk, hipStream_t st) {
-  if (!gb_shape_ok(M, N, K, lda, ldb, ldc) || N % 192) return -1;
-  const int ntiles = (M / 256) * (N / 192);
+  if (!gb_shape_ok(M, N, K, lda, ldb, ldc) || (N % 192 && N % 128)) return -1;
   GbEpi ep{};
-  DLT_HK_DISPATCH(hk, k_gemm_bf16<192, GB_EPI_STORE, false, HKC><<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(
-                          A, B, C, M, N, K, lda, ldb, ldc, flags, ep));
+  if (N % 192 == 0) {
+    const int ntiles = (M / 256) * (N / 192);
+    DLT_HK_DISPATCH(hk, k_gemm_bf16<192, GB_EPI_STORE, false, HKC><<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(
+                            A, B, C, M, N, K, lda, ldb, ldc, flags, ep));
+  } else {  // 256 x 128 tiles (hidden sizes such as 1024)
+    const int ntiles = (M / 256) * (N / 128);
+    DLT_HK_DISPATCH(hk, k_gemm_bf16<128, GB_EPI_STORE, false, HKC><<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(
+                            A, B, C, M, N, K, lda, ldb, ldc, flags, ep));
+  }
   DLT_CHECK_LAUNCH();
 }
 
@@ -929,11 +948,17 @@ DLT_API int dlt_gemm_bf16_qkv_rope(const bf16_t* A, const bf16_t* W, bf16_t* C, 
 // hk: operand / output format (0 bf16, 1 fp16).
 DLT_API int dlt_gemm_bf16_nn(const bf16_t* dY, const bf16_t* W, bf16_t* dX, int M, int Nout, int Nred, int ldy,
                              int ldw, int ldx, int flags, int hk, hipStream_t st) {
-  if (!gb_shape_ok(M, Nout, Nred, ldy, ldw, ldx) || Nout % 192) return -1;
-  const int ntiles = (M / 256) * (Nout / 192);
+  if (!gb_shape_ok(M, Nout, Nred, ldy, ldw, ldx) || (Nout % 192 && Nout % 128)) return -1;
   GbEpi ep{};
-  DLT_HK_DISPATCH(hk, k_gemm_bf16<192, GB_EPI_STORE, true, HKC><<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(
-                          dY, W, dX, M, Nout, Nred, ldy, ldw, ldx, flags, ep));
+  if (Nout % 192 == 0) {
+    const int ntiles = (M / 256) * (Nout / 192);
+    DLT_HK_DISPATCH(hk, k_gemm_bf16<192, GB_EPI_STORE, true, HKC><<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(
+                            dY, W, dX, M, Nout, Nred, ldy, ldw, ldx, flags, ep));
+  } else {  // 256 x 128 tiles
+    const int ntiles = (M / 256) * (Nout / 128);
+    DLT_HK_DISPATCH(hk, k_gemm_bf16<128, GB_EPI_STORE, true, HKC><<<gb_launch_grid(ntiles, flags), 512, 0, st>>>(
+                            dY, W, dX, M, Nout, Nred, ldy, ldw, ldx, flags, ep));
+  }
   DLT_CHECK_LAUNCH();
 }
 

@@ -36,7 +36,9 @@ __device__ __forceinline__ int gw_v128(int t) { return ((t >> 1) & 1) | (((t >> 
 //   A unit q: image col j -> dW row wm*64 + q*32 + (j & 31), wm = j / 32
 //   B0: image col j -> dW col (j / 64) * 96 + (j & 63);  B1: j -> (j / 32) * 96 + 64 + (j & 31)
 __device__ __forceinline__ int gw_amap(int q, int j) { return (j >> 5) * 64 + q * 32 + (j & 31); }
-__device__ __forceinline__ int gw_b0map(int j) { return (j >> 6) * 96 + (j & 63); }
+//   (BN = 128 column tiles: B0 holds all 128 columns, image col j -> dW col j; no B1)
+template <int BN = 192>
+__device__ __forceinline__ int gw_b0map(int j) { return (j >> 6) * (BN / 2) + (j & 63); }
 __device__ __forceinline__ int gw_b1map(int j) { return (j >> 5) * 96 + 64 + (j & 31); }
 
 // LDS byte offset of (token row t, column col) in an image with 256- or 128-byte rows

@@ -30,7 +30,8 @@
 // the kernel adds straight into dW.
 //
 // Requirements (launcher-checked): Nr % 128 == 0 (a last half tile when Nr % 256 == 128),
-// Nc % 192 == 0, T % 128 == 0, 16-byte aligned rows.
+// Nc % 192 == 0 (or Nc % 128 == 0: the 256 x 128 column-tile instance, BN = 128, for
+// hidden sizes such as 1024), T % 128 == 0, 16-byte aligned rows.
 //
 // HK: operand format, 0 = bf16, 1 = IEEE half (--mixed_precision fp16).  Staging and the
 // transposed reads move 16-bit words either way; only the MFMA differs
@@ -45,10 +46,15 @@
 // loop over K-tiles [kt0, kt0 + nk) (nk even >= 2), epilogue into dst (row stride ldd;
 // accumulate: dst += acc, else dst = acc).  Ends with every wave past its last LDS read,
 // so a workgroup may run segments back to back (stream-K).
-template <int HK>
+// BN: dW tile columns, 192 (6 n-tiles per wave: B0 + B1) or 128 (4 per wave, B0 only; the
+// 8-phase schedule's counted waits hold unchanged with an empty B1 unit -- every wait
+// leaves exactly the next K-tile's A0 / B0 units in flight either way).
+template <int HK, int BN = 192>
 __device__ __forceinline__ void gw_segment(bf16_t* lds, const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X,
                                            int r0, int c0, int kt0, int nk, bool half_tile, int ldy, int ldx,
                                            float* __restrict__ dst, int ldd, bool accumulate) {
+  static_assert(BN == 192 || BN == 128, "dW column tile of 192 or 128");
+  constexpr int NT = BN / 32, NH = NT / 2;  // n-tiles per wave / per quadrant
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int half = wid >> 2;
@@ -81,7 +87,7 @@ __device__ __forceinline__ void gw_segment(bf16_t* lds, const bf16_t* __restrict
       if (half_tile) col &= 127;
       oa[q][j] = (uint32_t)(t * ldy + col) * 2u;
     }
-    ob0[j] = (uint32_t)(t * ldx + gw_b0map(lc * 8)) * 2u;
+    ob0[j] = (uint32_t)(t * ldx + gw_b0map<BN>(lc * 8)) * 2u;
   }
   {
     const int e = wid * 64 + lane;
@@ -106,17 +112,19 @@ __device__ __forceinline__ void gw_segment(bf16_t* lds, const bf16_t* __restrict
                                        (gw_lds_vptr_t)(lds + eB0(b) + (wid * 2 + j) * 512), 16, 0, 0);
   };
   auto stB1 = [&](int kt, int b) {
-    const char* g = (const char*)(Bb + (size_t)kt * GW_BK * ldx);
-    __builtin_amdgcn_global_load_lds((gw_gbl_cvptr_t)(g + ob1),
-                                     (gw_lds_vptr_t)(lds + eB1(b) + wid * 512), 16, 0, 0);
+    if constexpr (BN == 192) {
+      const char* g = (const char*)(Bb + (size_t)kt * GW_BK * ldx);
+      __builtin_amdgcn_global_load_lds((gw_gbl_cvptr_t)(g + ob1),
+                                       (gw_lds_vptr_t)(lds + eB1(b) + wid * 512), 16, 0, 0);
+    }
   };
 
-  floatx4_t acc[6][4];
+  floatx4_t acc[NT][4];
 #pragma unroll
-  for (int a = 0; a < 6; ++a)
+  for (int a = 0; a < NT; ++a)
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = floatx4_t{0.f, 0.f, 0.f, 0.f};
-  bf16x8_t fa[2][2], fb0[3][2], fb1[3][2];
+  bf16x8_t fa[2][2], fb0[NH][2], fb1[NH][2];
 
   GwLane<256> L256;
   GwLane<128> L128;
@@ -138,11 +146,15 @@ __device__ __forceinline__ void gw_segment(bf16_t* lds, const bf16_t* __restrict
 #pragma unroll
       for (int s = 0; s < 2; ++s) fa[mt][s] = gw_frag<256>(imgA(b, qm) + ka[mt], s);
   };
-  // n-half 0: n-tiles 0..2 (B0); n-half 1: n-tile 3 (B0) and 4..5 (B1)
-  auto read_b = [&](int b, int qn, bf16x8_t (&fb)[3][2]) {
+  // BN 192: n-half 0: n-tiles 0..2 (B0); n-half 1: n-tile 3 (B0) and 4..5 (B1)
+  // BN 128: n-half qn: n-tiles 2qn, 2qn + 1, both from B0
+  auto read_b = [&](int b, int qn, bf16x8_t (&fb)[NH][2]) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      if (qn == 0) {
+      if constexpr (BN == 128) {
+#pragma unroll
+        for (int nt = 0; nt < NH; ++nt) fb[nt][s] = gw_frag<256>(imgB0(b) + kb0[qn * NH + nt], s);
+      } else if (qn == 0) {
 #pragma unroll
         for (int nt = 0; nt < 3; ++nt) fb[nt][s] = gw_frag<256>(imgB0(b) + kb0[nt], s);
       } else {
@@ -154,21 +166,26 @@ __device__ __forceinline__ void gw_segment(bf16_t* lds, const bf16_t* __restrict
   };
   // retire this wave's transposed reads (asm, invisible to the compiler's lgkmcnt
   // tracking: the fragments are in/out operands so no MFMA is scheduled above the wait)
-  auto lds_wait = [&](bf16x8_t (&fb)[3][2]) {
-    asm volatile("s_waitcnt lgkmcnt(0)"
-                 : "+v"(fa[0][0]), "+v"(fa[0][1]), "+v"(fa[1][0]), "+v"(fa[1][1]), "+v"(fb[0][0]), "+v"(fb[0][1]),
-                   "+v"(fb[1][0]), "+v"(fb[1][1]), "+v"(fb[2][0]), "+v"(fb[2][1])::"memory");
+  auto lds_wait = [&](bf16x8_t (&fb)[NH][2]) {
+    if constexpr (NH == 3)
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(fa[0][0]), "+v"(fa[0][1]), "+v"(fa[1][0]), "+v"(fa[1][1]), "+v"(fb[0][0]), "+v"(fb[0][1]),
+                     "+v"(fb[1][0]), "+v"(fb[1][1]), "+v"(fb[2][0]), "+v"(fb[2][1])::"memory");
+    else
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(fa[0][0]), "+v"(fa[0][1]), "+v"(fa[1][0]), "+v"(fa[1][1]), "+v"(fb[0][0]), "+v"(fb[0][1]),
+                     "+v"(fb[1][0]), "+v"(fb[1][1])::"memory");
   };
-  auto mma = [&](int qm, int qn, bf16x8_t (&fb)[3][2]) {
+  auto mma = [&](int qm, int qn, bf16x8_t (&fb)[NH][2]) {
     lds_wait(fb);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int nt = 0; nt < 3; ++nt)
+      for (int nt = 0; nt < NH; ++nt)
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt)
-          acc[qn * 3 + nt][qm * 2 + mt] = gw_mfma<HK>(fb[nt][s], fa[mt][s], acc[qn * 3 + nt][qm * 2 + mt]);
+          acc[qn * NH + nt][qm * 2 + mt] = gw_mfma<HK>(fb[nt][s], fa[mt][s], acc[qn * NH + nt][qm * 2 + mt]);
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -245,13 +262,13 @@ __device__ __forceinline__ void gw_segment(bf16_t* lds, const bf16_t* __restrict
   if (half == 0) __builtin_amdgcn_s_barrier();
 
   // epilogue: acc[nt][mt] = D[n][m]: lane owns tile row wm*64 + mt*16 + l16 and the 4
-  // consecutive columns wn*96 + nt*16 + lq*4 .. +3 (one float4)
+  // consecutive columns wn*BN/2 + nt*16 + lq*4 .. +3 (one float4)
   if (half_tile && wm >= 2) return;  // rows past Nr (wave-uniform; no barrier follows in this segment)
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) {
-    float* row = dst + (size_t)(wm * 64 + mt * 16 + l16) * ldd + wn * 96 + lq * 4;
+    float* row = dst + (size_t)(wm * 64 + mt * 16 + l16) * ldd + wn * (BN / 2) + lq * 4;
 #pragma unroll
-    for (int nt = 0; nt < 6; ++nt) {
+    for (int nt = 0; nt < NT; ++nt) {
       float4* p = reinterpret_cast<float4*>(row + nt * 16);
       float4 v = {acc[nt][mt][0], acc[nt][mt][1], acc[nt][mt][2], acc[nt][mt][3]};
       if (accumulate) {
@@ -266,7 +283,7 @@ __device__ __forceinline__ void gw_segment(bf16_t* lds, const bf16_t* __restrict
   }
 }
 
-template <int HK>
+template <int HK, int BN = 192>
 __global__ __launch_bounds__(512, 1) void k_gemm_wgrad(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X,
                                                        float* __restrict__ out, int T, int Nr, int Nc, int ldy,
                                                        int ldx, int splits, int accumulate) {
@@ -278,13 +295,13 @@ __global__ __launch_bounds__(512, 1) void k_gemm_wgrad(const bf16_t* __restrict_
   // all on XCD u % 8 and dispatched together, so the slab is fetched from HBM once, not
   // ntc times (the 3.3 GB dlogits slab of the lm_head gradient was read 4x before).
   // The grid is padded to whole groups of 8 units; padding workgroups exit at once.
-  const int ntc = Nc / 192;
+  const int ntc = Nc / BN;
   const int nunits = ((Nr + 255) / 256) * splits;
   const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3;
   const int u = (q / ntc) * 8 + xcd;
   if (u >= nunits) return;  // padding (uniform over the workgroup, before any barrier)
   const int split = u % splits;
-  const int r0 = (u / splits) * 256, c0 = (q % ntc) * 192;
+  const int r0 = (u / splits) * 256, c0 = (q % ntc) * BN;
   // Nr % 256 == 128 (the 50304-row lm_head / embedding gradient): the last row tile has
   // 128 valid dW rows -- its other half re-reads valid columns (no out-of-bounds reads
   // at the end of dY) and stores nothing (wm >= 2 is wave-uniform)
@@ -292,7 +309,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_wgrad(const bf16_t* __restrict_
   const int npair = T / (2 * GW_BK);
   const int p0 = (int)(((long)split * npair) / splits), p1 = (int)(((long)(split + 1) * npair) / splits);
   float* const dst = out + (accumulate ? 0 : (size_t)split * Nr * Nc) + (size_t)r0 * Nc + c0;
-  gw_segment<HK>(lds, dY, X, r0, c0, 2 * p0, 2 * (p1 - p0), half_tile, ldy, ldx, dst, Nc, accumulate != 0);
+  gw_segment<HK, BN>(lds, dY, X, r0, c0, 2 * p0, 2 * (p1 - p0), half_tile, ldy, ldx, dst, Nc, accumulate != 0);
 }
 
 // ---------------------------------------------------------------- stream-K (round 3)
@@ -319,16 +336,16 @@ struct GwSk {
   }
 };
 
-template <int HK>
+template <int HK, int BN = 192>
 __global__ __launch_bounds__(512, 1) void k_gemm_wgrad_sk(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X,
                                                           float* __restrict__ dW, float* __restrict__ part, int Nr,
                                                           int Nc, int ldy, int ldx, GwSk sk) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * GW_BUF];
-  const int ntc = Nc / 192;
+  const int ntc = Nc / BN;
   const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3;
   const int c = q % ntc, g = (q / ntc) * 8 + xcd;
   if (g >= sk.Gc) return;  // padding (uniform, before any barrier)
-  const int c0 = c * 192;
+  const int c0 = c * BN;
   const long e = sk.s_of(g + 1);
   long i = sk.s_of(g);
   const int rt_first = (int)(i / sk.npair);
@@ -338,8 +355,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm_wgrad_sk(const bf16_t* __restri
     const int r0 = rt * 256;
     const bool whole = p0 == 0 && p1 == sk.npair;
     float* dst = whole ? dW + (size_t)r0 * Nc + c0
-                       : part + (((size_t)c * sk.Gc + g) * sk.maxseg + (rt - rt_first)) * (256 * 192);
-    gw_segment<HK>(lds, dY, X, r0, c0, 2 * p0, 2 * (p1 - p0), r0 + 256 > Nr, ldy, ldx, dst, whole ? Nc : 192, whole);
+                       : part + (((size_t)c * sk.Gc + g) * sk.maxseg + (rt - rt_first)) * (256 * BN);
+    gw_segment<HK, BN>(lds, dY, X, r0, c0, 2 * p0, 2 * (p1 - p0), r0 + 256 > Nr, ldy, ldx, dst, whole ? Nc : BN, whole);
     i += p1 - p0;
   }
 }
@@ -348,10 +365,11 @@ __global__ __launch_bounds__(512, 1) void k_gemm_wgrad_sk(const bf16_t* __restri
 // increasing g.  Grid: (GW_FIX_SPLIT, tiles); each block sums 1/GW_FIX_SPLIT of the tile.
 // The slot index of every share is computed once per block (64-bit divisions) into LDS.
 constexpr int GW_FIX_SPLIT = 48;
+template <int BN = 192>
 __global__ __launch_bounds__(256) void k_wgrad_sk_fix(const float* __restrict__ part, float* __restrict__ dW, int Nr,
                                                       int Nc, GwSk sk) {
   __shared__ int jt[256];
-  const int ntc = Nc / 192;
+  const int ntc = Nc / BN;
   const int tile = blockIdx.y, rt = tile / ntc, c = tile - rt * ntc;
   const long i0 = (long)rt * sk.npair, i1 = i0 + sk.npair - 1;
   const int g_lo = sk.g_of(i0), g_hi = sk.g_of(i1);
@@ -360,16 +378,16 @@ __global__ __launch_bounds__(256) void k_wgrad_sk_fix(const float* __restrict__ 
   for (int t = threadIdx.x; t < nsh && t < 256; t += 256) jt[t] = rt - (int)(sk.s_of(g_lo + t) / sk.npair);
   __syncthreads();
   const int rows = min(256, Nr - rt * 256);
-  const float4* pc = reinterpret_cast<const float4*>(part) + ((size_t)c * sk.Gc + g_lo) * sk.maxseg * (256 * 192 / 4);
-  const size_t gstride = (size_t)sk.maxseg * (256 * 192 / 4);  // float4s between consecutive shares' slot 0
-  for (int k = blockIdx.x * 256 + threadIdx.x; k < 256 * 192 / 4; k += gridDim.x * 256) {
-    const int r = (k * 4) / 192, col = (k * 4) % 192;
+  const float4* pc = reinterpret_cast<const float4*>(part) + ((size_t)c * sk.Gc + g_lo) * sk.maxseg * (256 * BN / 4);
+  const size_t gstride = (size_t)sk.maxseg * (256 * BN / 4);  // float4s between consecutive shares' slot 0
+  for (int k = blockIdx.x * 256 + threadIdx.x; k < 256 * BN / 4; k += gridDim.x * 256) {
+    const int r = (k * 4) / BN, col = (k * 4) % BN;
     if (r >= rows) break;  // k grows with r: the rest of this thread's elements are past Nr too
-    float4* d = reinterpret_cast<float4*>(dW + (size_t)(rt * 256 + r) * Nc + c * 192 + col);
+    float4* d = reinterpret_cast<float4*>(dW + (size_t)(rt * 256 + r) * Nc + c * BN + col);
     float4 a = *d;
     for (int t = 0; t < nsh; ++t) {
       const int j = t < 256 ? jt[t] : rt - (int)(sk.s_of(g_lo + t) / sk.npair);
-      const float4 p = pc[t * gstride + (size_t)j * (256 * 192 / 4) + k];
+      const float4 p = pc[t * gstride + (size_t)j * (256 * BN / 4) + k];
       a.x += p.x;
       a.y += p.y;
       a.z += p.z;
@@ -379,12 +397,15 @@ __global__ __launch_bounds__(256) void k_wgrad_sk_fix(const float* __restrict__ 
   }
 }
 
+// dW column tile of a shape: 192 when it divides Nc, else 128 (0 = neither tiles)
+static inline int gw_bn(int Nc) { return Nc % 192 == 0 ? 192 : (Nc % 128 == 0 ? 128 : 0); }
+
 static inline GwSk gw_sk_plan(int T, int Nr, int Nc, int Gc_req) {
   GwSk sk{};
   sk.npair = T / 128;
   sk.nrt = (Nr + 255) / 256;
   sk.Wc = sk.nrt * sk.npair;
-  const int ntc = Nc / 192;
+  const int ntc = Nc / gw_bn(Nc);
   int Gc = Gc_req > 0 ? Gc_req : 256 / ntc;
   Gc = Gc < 1 ? 1 : (Gc > sk.Wc ? sk.Wc : Gc);
   sk.Gc = Gc;
@@ -396,9 +417,10 @@ static inline GwSk gw_sk_plan(int T, int Nr, int Nc, int Gc_req) {
 
 // Floats of scratch the stream-K weight gradient needs (0 = shape does not tile).
 DLT_API long dlt_gemm_wgrad_sk_scratch(int T, int Nr, int Nc, int Gc) {
-  if (T <= 0 || T % 128 || Nr % 128 || Nc % 192) return 0;
+  if (T <= 0 || T % 128 || Nr % 128 || !gw_bn(Nc)) return 0;
+  const int bn = gw_bn(Nc);
   const GwSk sk = gw_sk_plan(T, Nr, Nc, Gc);
-  return (long)(Nc / 192) * sk.Gc * sk.maxseg * 256 * 192;
+  return (long)(Nc / bn) * sk.Gc * sk.maxseg * 256 * bn;
 }
 
 // dW[Nr, Nc] (fp32) += dY[T, Nr]^T . X[T, Nc], stream-K over Gc shares per column tile
@@ -407,14 +429,20 @@ DLT_API long dlt_gemm_wgrad_sk_scratch(int T, int Nr, int Nc, int Gc) {
 // format (0 bf16, 1 fp16).
 DLT_API int dlt_gemm_wgrad_sk(const bf16_t* dY, const bf16_t* X, float* dW, float* part, int T, int Nr, int Nc,
                               int ldy, int ldx, int Gc, int hk, hipStream_t st) {
-  if (T <= 0 || T % 128 || Nr % 128 || Nc % 192 || (ldy | ldx) % 8 || !dW || !part) return -1;
+  const int bn = gw_bn(Nc);
+  if (T <= 0 || T % 128 || Nr % 128 || !bn || (ldy | ldx) % 8 || !dW || !part) return -1;
   const GwSk sk = gw_sk_plan(T, Nr, Nc, Gc);
-  const int ntc = Nc / 192;
-  DLT_HK_DISPATCH(hk, k_gemm_wgrad_sk<HKC><<<((sk.Gc + 7) / 8) * 8 * ntc, 512, 0, st>>>(dY, X, dW, part, Nr, Nc, ldy,
-                                                                                      ldx, sk));
+  const int ntc = Nc / bn;
+  const int grid = ((sk.Gc + 7) / 8) * 8 * ntc;
+  if (bn == 192) {
+    DLT_HK_DISPATCH(hk, k_gemm_wgrad_sk<HKC, 192><<<grid, 512, 0, st>>>(dY, X, dW, part, Nr, Nc, ldy, ldx, sk));
+  } else {
+    DLT_HK_DISPATCH(hk, k_gemm_wgrad_sk<HKC, 128><<<grid, 512, 0, st>>>(dY, X, dW, part, Nr, Nc, ldy, ldx, sk));
+  }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  k_wgrad_sk_fix<<<dim3(GW_FIX_SPLIT, sk.nrt * ntc), 256, 0, st>>>(part, dW, Nr, Nc, sk);
+  if (bn == 192) k_wgrad_sk_fix<192><<<dim3(GW_FIX_SPLIT, sk.nrt * ntc), 256, 0, st>>>(part, dW, Nr, Nc, sk);
+  else k_wgrad_sk_fix<128><<<dim3(GW_FIX_SPLIT, sk.nrt * ntc), 256, 0, st>>>(part, dW, Nr, Nc, sk);
   DLT_CHECK_LAUNCH();
 }
 
@@ -424,10 +452,17 @@ DLT_API int dlt_gemm_wgrad_sk(const bf16_t* dY, const bf16_t* X, float* dW, floa
 // operand format (0 bf16, 1 fp16).
 DLT_API int dlt_gemm_wgrad(const bf16_t* dY, const bf16_t* X, float* dW, float* part, int T, int Nr, int Nc, int ldy,
                            int ldx, int splits, int hk, hipStream_t st) {
-  if (T <= 0 || T % 128 || Nr % 128 || Nc % 192 || (ldy | ldx) % 8 || splits < 1 || splits > T / 128) return -1;
+  const int bn = gw_bn(Nc);
+  if (T <= 0 || T % 128 || Nr % 128 || !bn || (ldy | ldx) % 8 || splits < 1 || splits > T / 128) return -1;
   if (splits > 1 && part == nullptr) return -1;
   const int units = ((Nr + 255) / 256) * splits;  // (row tile, split) pairs, padded to 8s
-  DLT_HK_DISPATCH(hk, k_gemm_wgrad<HKC><<<((units + 7) / 8) * 8 * (Nc / 192), 512, 0, st>>>(
-                          dY, X, splits > 1 ? part : dW, T, Nr, Nc, ldy, ldx, splits, splits > 1 ? 0 : 1));
+  const int grid = ((units + 7) / 8) * 8 * (Nc / bn);
+  if (bn == 192) {
+    DLT_HK_DISPATCH(hk, k_gemm_wgrad<HKC, 192><<<grid, 512, 0, st>>>(dY, X, splits > 1 ? part : dW, T, Nr, Nc, ldy,
+                                                                    ldx, splits, splits > 1 ? 0 : 1));
+  } else {
+    DLT_HK_DISPATCH(hk, k_gemm_wgrad<HKC, 128><<<grid, 512, 0, st>>>(dY, X, splits > 1 ? part : dW, T, Nr, Nc, ldy,
+                                                                    ldx, splits, splits > 1 ? 0 : 1));
+  }
   DLT_CHECK_LAUNCH();
 }

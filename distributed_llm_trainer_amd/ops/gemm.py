@@ -405,7 +405,7 @@ class HipGemm:
 
         def fused():
             hip.gemm_qkv_rope(x, w, S, cos, sin, out=y)
-        ok = (w.shape[0] == 3 * nh * 64 and hip.gemm_bf16_fits(M, w.shape[0], x.shape[1]) and M % S == 0
+        ok = (w.shape[0] == 3 * nh * 64 and hip.gemm_bf16_fits192(M, w.shape[0], x.shape[1]) and M % S == 0
               and cos.dtype == torch.float32 and cos.is_contiguous() and sin.is_contiguous())
         if ok and self._fused_pick("rope", x, w, fused, unfused):
             fused()
@@ -428,7 +428,7 @@ class HipGemm:
 
         def fused():
             hip.gemm_gu_swiglu(x, w, gu_out=gu, s_out=s)
-        ok = I2 % 192 == 0 and hip.gemm_bf16_fits(M, I2, x.shape[1]) and s.is_contiguous()
+        ok = I2 % 192 == 0 and hip.gemm_bf16_fits192(M, I2, x.shape[1]) and s.is_contiguous()
         if ok and self._fused_pick("swiglu", x, w, fused, unfused):
             fused()
         else:
@@ -496,7 +496,7 @@ class HipGemm:
             hip.gemm_down_swiglu_bwd(dd, wdown, gu, out=dgu, s_out=s_out)
         # bf16 and fp16 race separately (kind "dswiglu" / "dswiglu16")
         kind = "dswiglu" if dd.dtype == torch.bfloat16 else "dswiglu16"
-        ok = (self._dgrad_on and self._race and hip.gemm_bf16_fits(M, I, H) and tuple(gu.shape) == (M, 2 * I)
+        ok = (self._dgrad_on and self._race and hip.gemm_bf16_fits192(M, I, H) and tuple(gu.shape) == (M, 2 * I)
               and (dd.dtype == torch.bfloat16 or self._fp16_dswiglu)
               and self._hand16_ok(dd, wdown, gu, dgu, *(() if s_out is None else (s_out,))))
         if ok and self._fused_pick(kind, dd, wdown, fused, unfused, key=(kind, M, I, H)):
@@ -595,7 +595,7 @@ class HipGemm:
         if hand:  # whole rounds of 256 workgroups, plus a few fixed depths (sweep in
             # profiles/r3_wgrad.md: the best split is shape-specific, 5..16 here); the
             # split partials ([s, N, K] fp32) stay under ~1 GB
-            tiles = ((N + 255) // 256) * (K // 192)
+            tiles = ((N + 255) // 256) * (K // hip.wgrad_bn(K))
             hs = {max(1, (256 * r) // tiles) for r in (1, 2, 3)} | {2, 3, 4, 8, 16}
             cands += [-h for h in sorted(hs) if h <= min(64, M // 128) and (h == 1 or h * N * K * 4 <= 1 << 30)]
             if not to_bf16:  # stream-K (fp32 accumulate only)

@@ -727,16 +727,26 @@ def cast_bf16(x: torch.Tensor, y: torch.Tensor) -> None:
 
 
 # ---------------------------------------------------------------- wgrad GEMM
+# the 256 x 128 tile forms of the hand GEMMs (hidden sizes 192 does not divide, e.g. the
+# medium model's 1024); DLT_GEMM_BN128=0 leaves such shapes to hipBLASLt
+_BN128 = os.environ.get("DLT_GEMM_BN128", "1") != "0"
+
+
+def wgrad_bn(Nc: int) -> int:
+    """dW column tile of the weight-gradient kernel: 192, else 128 (e.g. hidden 1024), else 0."""
+    return 192 if Nc % 192 == 0 else (128 if _BN128 and Nc % 128 == 0 else 0)
+
+
 def wgrad_fits(T: int, Nr: int, Nc: int) -> bool:
-    """Shapes the 256 x 192 weight-gradient kernel tiles (T in 128-token pairs; a last
-    half row tile when Nr % 256 == 128)."""
-    return T > 0 and T % 128 == 0 and Nr % 128 == 0 and Nc % 192 == 0
+    """Shapes the 256 x 192 (or 256 x 128) weight-gradient kernel tiles (T in 128-token
+    pairs; a last half row tile when Nr % 256 == 128)."""
+    return T > 0 and T % 128 == 0 and Nr % 128 == 0 and wgrad_bn(Nc) > 0
 
 
 def wgrad_splits(T: int, Nr: int, Nc: int, target: int = 256) -> int:
     """Split-K factor that brings tiles x splits closest to `target` workgroups (one per
     CU), capped by the number of 128-token pairs."""
-    tiles = ((Nr + 255) // 256) * (Nc // 192)
+    tiles = ((Nr + 255) // 256) * (Nc // wgrad_bn(Nc))
     return max(1, min(T // 128, (target + tiles // 2) // tiles))
 
 
@@ -842,8 +852,14 @@ def gemm_grid_cap(n: int) -> int:
 
 
 def gemm_bf16_fits(M: int, N: int, K: int) -> bool:
-    """Shapes the persistent 256 x 192 MFMA kernel tiles exactly."""
-    return M > 0 and M % 256 == 0 and N % 192 == 0 and K % 128 == 0 and K >= 128
+    """Shapes the persistent MFMA kernel tiles exactly: 256 x 192 tiles, or 256 x 128 when
+    192 does not divide N (plain store / data-gradient forms only)."""
+    return M > 0 and M % 256 == 0 and (N % 192 == 0 or (_BN128 and N % 128 == 0)) and K % 128 == 0 and K >= 128
+
+
+def gemm_bf16_fits192(M: int, N: int, K: int) -> bool:
+    """Shapes the fused-epilogue forms (RoPE, SwiGLU, SwiGLU backward) tile: 256 x 192 only."""
+    return gemm_bf16_fits(M, N, K) and N % 192 == 0
 
 
 def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
@@ -894,7 +910,7 @@ def gemm_qkv_rope(x: torch.Tensor, wqkv: torch.Tensor, S: int, cos: torch.Tensor
     M, K = x.shape
     N = wqkv.shape[0]
     H = N // 3
-    if (not gemm_bf16_fits(M, N, K) or N % 3 or H % 64 or wqkv.shape[1] != K or M % S
+    if (not gemm_bf16_fits192(M, N, K) or N % 3 or H % 64 or wqkv.shape[1] != K or M % S
             or cos.shape[-1] != 32 or cos.shape[0] < S):
         return None
     _req(x, torch.bfloat16, "gemm_qkv_rope.x")
@@ -916,7 +932,7 @@ def gemm_gu_swiglu(x: torch.Tensor, wgu: torch.Tensor, gu_out: Optional[torch.Te
     M, K = x.shape
     I2 = wgu.shape[0]
     I = I2 // 2
-    if not gemm_bf16_fits(M, I2, K) or I2 % 2 or I % 96 or wgu.shape[1] != K:
+    if not gemm_bf16_fits192(M, I2, K) or I2 % 2 or I % 96 or wgu.shape[1] != K:
         return None
     _req(x, torch.bfloat16, "gemm_gu_swiglu.x")
     _req(wgu, torch.bfloat16, "gemm_gu_swiglu.w")
@@ -959,7 +975,7 @@ def gemm_down_swiglu_bwd(dd: torch.Tensor, wdown: torch.Tensor, gu: torch.Tensor
     if it does not tile."""
     M, H = dd.shape
     I = wdown.shape[1]
-    if not gemm_bf16_fits(M, I, H) or wdown.shape[0] != H or tuple(gu.shape) != (M, 2 * I):
+    if not gemm_bf16_fits192(M, I, H) or wdown.shape[0] != H or tuple(gu.shape) != (M, 2 * I):
         return None
     dt = dd.dtype if dd.dtype in _WG_HK else torch.bfloat16  # bf16 or fp16, one format for all
     _req(dd, dt, "gemm_down_swiglu_bwd.dd")

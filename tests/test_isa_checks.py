@@ -91,8 +91,10 @@ def test_gemm_operand_format_instantiations_use_their_mfma(tmp_path, src, patter
     datapath (or the reverse) without any shape error."""
     asm = _device_asm(os.path.join(kbuild.CSRC, src), tmp_path)
     bodies = _kernel_bodies(asm, pattern)
-    # HK is the last int template argument (k_gemm_bf16 has a bool LATE after it)
-    hk = {k: re.findall(r"Li(\d+)E", k)[-1] for k in bodies}
+    # HK: the first int template argument of k_gemm_wgrad<HK, BN>, the last int one of
+    # k_gemm_bf16<BN, EPI, BT, HK, LATE> (a bool LATE after it)
+    pick = 0 if "wgrad" in pattern else -1
+    hk = {k: re.findall(r"Li(\d+)E", k)[pick] for k in bodies}
     assert set(hk.values()) == {"0", "1"}, sorted(bodies)
     for name, ins in bodies.items():
         fmt = "f16" if hk[name] == "1" else "bf16"

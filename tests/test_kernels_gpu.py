@@ -430,11 +430,12 @@ def test_gemm_plan_pin_roundtrip(tmp_path):
 
 
 @pytest.mark.parametrize("T,Nr,Nc", [(1024, 256, 192), (2048, 768, 384), (4096, 2304, 768), (1024, 384, 192),
-                                     (2048, 50304, 768)])
+                                     (2048, 50304, 768), (2048, 1024, 1024), (2048, 384, 128), (1024, 1024, 4096)])
 def test_gemm_wgrad_kernel(T, Nr, Nc):
     """Hand-written weight-gradient GEMM (in-place and split-K + fixed-order sum) vs
     the fp32 torch reference; split-K results are bitwise repeatable.  Nr % 256 == 128
-    (384; the 50304-row lm_head gradient) runs a last half row tile."""
+    (384; the 50304-row lm_head gradient) runs a last half row tile.  Nc % 192 != 0
+    (1024, 128, 4096: the medium model's hidden sizes) runs the 256 x 128 column tile."""
     torch.manual_seed(0)
     dy = torch.randn(T, Nr, device=DEV).bfloat16()
     x = torch.randn(T, Nc, device=DEV).bfloat16()
@@ -453,7 +454,8 @@ def test_gemm_wgrad_kernel(T, Nr, Nc):
 
 
 @pytest.mark.parametrize("T,Nr,Nc,shares", [(32768, 6144, 768, 0), (4096, 2304, 768, 0), (2048, 384, 192, 5),
-                                            (8192, 50304, 768, 0), (1024, 256, 192, 3), (4096, 768, 3072, 7)])
+                                            (8192, 50304, 768, 0), (1024, 256, 192, 3), (4096, 768, 3072, 7),
+                                            (4096, 1024, 1024, 0), (2048, 384, 128, 5)])
 def test_gemm_wgrad_stream_k(T, Nr, Nc, shares):
     """Stream-K weight gradient (k_gemm_wgrad_sk + the fixed-order fixup): accumulates
     into dw like the split-K kernel, matches the fp32 reference on the whole output
@@ -473,7 +475,7 @@ def test_gemm_wgrad_stream_k(T, Nr, Nc, shares):
     assert not hip.gemm_wgrad_sk(base, dy[:, :64], x), "untileable shape must be refused"
 
 
-@pytest.mark.parametrize("T,Nr,Nc", [(2048, 768, 384), (4096, 2304, 768), (2048, 384, 192)])
+@pytest.mark.parametrize("T,Nr,Nc", [(2048, 768, 384), (4096, 2304, 768), (2048, 384, 192), (2048, 1024, 1024)])
 def test_gemm_wgrad_kernels_fp16(T, Nr, Nc):
     """The weight-gradient kernels instantiated for IEEE-half operands
     (v_mfma_f32_16x16x32_f16; --mixed_precision fp16): split-K, in-place and stream-K
@@ -557,7 +559,8 @@ def _relerr(got, want):
                                          (16384, 768, 3072, torch.bfloat16), (16384, 6144, 768, torch.bfloat16),
                                          (4096, 3072, 1024, torch.bfloat16), (512, 384, 256, torch.bfloat16),
                                          (2560, 1152, 384, torch.bfloat16), (16384, 2304, 768, torch.float16),
-                                         (2560, 1152, 384, torch.float16)])
+                                         (2560, 1152, 384, torch.float16), (4096, 1024, 1024, torch.bfloat16),
+                                         (2048, 4096, 1024, torch.bfloat16), (2560, 1280, 384, torch.float16)])
 def test_gemm_bf16(M, N, K, dtype):
     """Persistent hand-written MFMA GEMM C = A B^T (csrc/gemm_bf16.hip) vs fp32 torch:
     every element within 16-bit output rounding (relative to the tensor's max); bf16 and
@@ -647,17 +650,19 @@ def test_gemm_gu_swiglu(M, I, K):
 
 
 @pytest.mark.parametrize("M,Nout,Nred", [(512, 768, 2304), (512, 768, 768), (256, 768, 6144), (512, 3072, 768),
-                                          (256, 768, 50304), (256, 1600, 4800), (512, 192, 128)])
+                                          (256, 768, 50304), (256, 1600, 4800), (512, 192, 128), (512, 1024, 1024),
+                                          (256, 1024, 4096), (256, 4096, 1024), (512, 128, 256)])
 def test_gemm_dgrad_vs_fp32(M, Nout, Nred):
     """Data gradient dX = dY @ W (W[Nred, Nout] read as stored) on the hand-written
     reduction-major-B kernel against the fp32 product -- every dgrad role of the step
-    (q/k/v 2304, o 768, gate/up 6144, down 768 -> 3072, lm_head 50304) plus shapes that do
-    not tile (None, nothing launched)."""
+    (q/k/v 2304, o 768, gate/up 6144, down 768 -> 3072, lm_head 50304), the 256 x 128
+    column tile (Nout 1024 / 4096 / 128: the medium model) plus shapes that do not tile
+    (None, nothing launched)."""
     torch.manual_seed(Nred)
     dy = (torch.rand(M, Nred, device=DEV) * 2 - 1).bfloat16()
     w = ((torch.rand(Nred, Nout, device=DEV) * 2 - 1) / Nred ** 0.5).bfloat16()
     r = hip.gemm_dgrad(dy, w)
-    if Nout % 192:
+    if Nout % 192 and Nout % 128:
         assert r is None
         return
     want = dy.float() @ w.float()
