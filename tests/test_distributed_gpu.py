@@ -199,12 +199,13 @@ def test_rccl_forced_collectives_with_hand_kernels(tmp_path, mode):
         assert torch.equal(a[k], b[k]), (k, (a[k] - b[k]).abs().max().item())
 
 
-def test_rccl_forced_collectives_timed_window_choice():
+def test_rccl_forced_collectives_timed_window_choice(tmp_path):
     """Under forced RCCL collectives the window schedule is chosen by timing (four trial
     windows fb / ffbb, then the faster one): the decision is taken and recorded, and the
     parameters equal bit for bit those of the run without a communicator (ffbb throughout:
-    every schedule runs the same kernels in the same accumulation order)."""
-    env = {"DLT_FORCE_CPU": None, "DLT_BACKEND": "nccl"}
+    every schedule runs the same kernels in the same accumulation order; the second run
+    replays the first one's GEMM plan, so both use the same kernel per shape)."""
+    env = {"DLT_FORCE_CPU": None, "DLT_BACKEND": "nccl", "DLT_GEMM_PLAN": str(tmp_path / "plan.json")}
     a, (win_a, auto_a) = run_multiprocess(_forced, world=1, args=("ddp_auto",), env=env, timeout=300)[0]
     b, (win_b, auto_b) = run_multiprocess(_forced, world=1, args=("ddp_auto",),
                                           env={**env, "DLT_FORCE_COLLECTIVES": "1"}, timeout=300)[0]
