@@ -4,12 +4,13 @@
 ``--mixed_precision fp32`` mode (the reference's fp32 path, ``ddp_trainer.py:137-139``)
 then runs HIP kernels for every non-GEMM op, as bf16 / fp16 do; the GEMMs are hipBLASLt
 fp32.  Same semantics and dropout bits as ``ops/reference.py``; attention supports
-head_dim 64 and 128.
+head_dim 64 and 128 (the flash kernels; the GEMM formulation takes any head_dim <= 256).
 """
 from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import torch
 
@@ -33,9 +34,20 @@ SIGS = {
     "dlt_f32_attn_bwd": [c_void_p, c_void_p, c_void_p, c_long, c_long, c_long, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_long, c_long, c_int, c_int, c_int, c_int,
                          c_float, c_float, c_void_p],
+    "dlt_f32_attn_softmax": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_void_p],
+    "dlt_f32_attn_dsoftmax": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                              c_float, c_float, c_void_p],
 }
 
 ATTN_HEAD_DIMS = (64, 128)
+
+# fp32 attention: "gemm" -- the dense [S, S] score matrix of every (b, h) through batched
+# hipBLASLt fp32 GEMMs (MFMA) around two row kernels; "flash" -- the lane-per-query VALU
+# kernels (no [S, S] buffer); "auto" -- gemm while S <= 4096 and its two score buffers fit
+# in GEMM_ATTN_BYTES.  The causal half the GEMMs compute for nothing is cheaper than the
+# flash kernels' LDS-broadcast-bound FMAs (profiles/r5_fp32_attention.md).
+ATTN_IMPL = os.environ.get("DLT_F32_ATTN", "auto")
+GEMM_ATTN_BYTES = 16 << 30
 
 
 def _h():
@@ -177,6 +189,55 @@ def _mask(B, nh, S, p, key, device, mask=None):
     return mask, 1.0 / (1.0 - p)
 
 
+def _use_gemm(B, nh, S, hd):
+    if ATTN_IMPL not in ("auto", "gemm", "flash"):
+        raise ValueError(f"DLT_F32_ATTN={ATTN_IMPL!r}: expected auto, gemm or flash")
+    if ATTN_IMPL == "flash":
+        return False
+    fits = S <= 4096 and hd <= 256 and 2 * B * nh * S * S * 4 <= GEMM_ATTN_BYTES
+    if ATTN_IMPL == "gemm" and not fits:
+        raise ValueError(f"fp32 GEMM attention: S={S}, hd={hd}, B*nh={B * nh} exceeds its limits")
+    return fits
+
+
+def _heads(t, B, S, nh, hd):
+    """[B*S, nh*hd]-rowed view (row stride may exceed nh*hd) -> [B, nh, S, hd] view."""
+    return t.as_strided((B, nh, S, hd), (S * t.stride(0), hd, t.stride(0), 1))
+
+
+def _gemm_fwd(q4, k4, v4, B, nh, S, hd, p, key, device, out, mask, store_mask):
+    o = torch.empty(B * S, nh * hd, dtype=torch.float32, device=device) if out is None else out
+    _req32(o, "attn_f32.o", B * S * nh * hd)
+    lse = torch.empty(B, nh, S, dtype=torch.float32, device=device)
+    mask, dscale = _mask(B, nh, S, p, key, device, mask)
+    sc = torch.matmul(q4, k4.transpose(-1, -2))
+    _chk(_lib().dlt_f32_attn_softmax(_p(sc), _p(lse), _p(mask), B * nh, S, 1.0 / math.sqrt(hd), dscale, _st()),
+         "f32_attn_softmax")
+    o4 = torch.matmul(sc, v4)
+    del sc
+    _heads(o, B, S, nh, hd).copy_(o4)
+    return o, _h().AttnAux((lse, mask if store_mask else None))
+
+
+def _gemm_bwd(q4, k4, v4, o, do, aux, B, nh, S, hd, p, key, device):
+    """(dq, dk, dv) as contiguous [B, nh, S, hd]."""
+    lse, mask = aux if isinstance(aux, tuple) else (aux, None)
+    _req32(lse, "attn_bwd_f32.lse", B * nh * S)
+    _req32(o, "attn_bwd_f32.o", B * S * nh * hd)
+    _req32(do, "attn_bwd_f32.do", B * S * nh * hd)
+    mask, dscale = _mask(B, nh, S, p, key, device, mask)
+    do4 = _heads(do, B, S, nh, hd)
+    sc = torch.matmul(q4, k4.transpose(-1, -2))
+    dp = torch.matmul(do4, v4.transpose(-1, -2))
+    _chk(_lib().dlt_f32_attn_dsoftmax(_p(sc), _p(dp), _p(lse), _p(o), _p(do), _p(mask), B, nh, S, hd,
+                                      1.0 / math.sqrt(hd), dscale, _st()), "f32_attn_dsoftmax")
+    dv = torch.matmul(sc.transpose(-1, -2), do4)
+    del sc
+    dq = torch.matmul(dp, k4)
+    dk = torch.matmul(dp.transpose(-1, -2), q4)
+    return dq, dk, dv
+
+
 def _fwd(qp, kp, vp, strides, B, nh, S, hd, p, key, device, out, mask, store_mask=True):
     _check_hd(hd)
     o = torch.empty(B * S, nh * hd, dtype=torch.float32, device=device) if out is None else out
@@ -195,6 +256,8 @@ def attention_fwd(q, k, v, p, key, causal=True, store_mask=True, out=None, mask=
     B, nh, S, hd = q.shape
     for t, n in ((q, "q"), (k, "k"), (v, "v")):
         _req32(t, "attn_f32." + n, B * nh * S * hd)
+    if _use_gemm(B, nh, S, hd):
+        return _gemm_fwd(q, k, v, B, nh, S, hd, p, key, q.device, out, mask, store_mask)
     return _fwd(_p(q), _p(k), _p(v), (nh * S * hd, S * hd, hd), B, nh, S, hd, p, key, q.device, out, mask,
                 store_mask)
 
@@ -206,6 +269,9 @@ def attention_fwd_packed(qkv, B, S, nh, p, key, out=None, mask=None, store_mask=
         raise ValueError("packed attention: qkv must be [B*S, 3*nh*hd]")
     _req32(qkv, "attn_f32.qkv")
     H = nh * hd
+    if _use_gemm(B, nh, S, hd):
+        q4, k4, v4 = (_heads(qkv[:, j * H:(j + 1) * H], B, S, nh, hd) for j in range(3))
+        return _gemm_fwd(q4, k4, v4, B, nh, S, hd, p, key, qkv.device, out, mask, store_mask)
     ptr = [ctypes.c_void_p(qkv.data_ptr() + j * H * 4) for j in range(3)]
     return _fwd(*ptr, (S * threeH, hd, threeH), B, nh, S, hd, p, key, qkv.device, out, mask, store_mask)
 
@@ -226,6 +292,8 @@ def attention_bwd(q, k, v, o, do, aux, p, key, causal=True):
     B, nh, S, hd = q.shape
     for t, n in ((q, "q"), (k, "k"), (v, "v")):
         _req32(t, "attn_bwd_f32." + n, B * nh * S * hd)
+    if _use_gemm(B, nh, S, hd):
+        return _gemm_bwd(q, k, v, o, do, aux, B, nh, S, hd, p, key, q.device)
     dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
     st = (nh * S * hd, S * hd, hd)
     _bwd(_p(q), _p(k), _p(v), st, o, do, aux, B, nh, S, hd, p, key, q.device, (_p(dq), _p(dk), _p(dv)), st)
@@ -241,6 +309,11 @@ def attention_bwd_packed(qkv, o, do, aux, p, key, B, S, nh, cos, sin, out=None):
     H = nh * hd
     dqkv = torch.empty(M, threeH, dtype=torch.float32, device=qkv.device) if out is None else out
     _req32(dqkv, "attn_bwd_f32.dqkv", M * threeH)
+    if _use_gemm(B, nh, S, hd):
+        q4, k4, v4 = (_heads(qkv[:, j * H:(j + 1) * H], B, S, nh, hd) for j in range(3))
+        for j, g in enumerate(_gemm_bwd(q4, k4, v4, o, do, aux, B, nh, S, hd, p, key, qkv.device)):
+            _heads(dqkv[:, j * H:(j + 1) * H], B, S, nh, hd).copy_(g)
+        return rope_qk_inplace(dqkv, B, S, nh, cos, sin, sign=-1.0)
     src = [ctypes.c_void_p(qkv.data_ptr() + j * H * 4) for j in range(3)]
     dst = [ctypes.c_void_p(dqkv.data_ptr() + j * H * 4) for j in range(3)]
     st = (S * threeH, hd, threeH)

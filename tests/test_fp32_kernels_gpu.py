@@ -79,10 +79,14 @@ def test_f32_swiglu_ce_scale():
     assert torch.allclose(hip.scale_bf16(x, torch.tensor(0.25, device=DEV), mul=2.0), x * 0.5)
 
 
-@pytest.mark.parametrize("hd,S,p", [(64, 256, 0.0), (64, 200, 0.1), (128, 160, 0.1)])
-def test_f32_attention_packed_vs_reference(hd, S, p):
-    """fp32 flash attention fwd + bwd (packed QKV, inverse RoPE of the gradient) against
-    the fp32 reference with the same dropout keep bits; ragged S (not a tile multiple)."""
+@pytest.mark.parametrize("impl", ["flash", "gemm"])
+@pytest.mark.parametrize("hd,S,p", [(64, 256, 0.0), (64, 200, 0.1), (128, 160, 0.1), (64, 1100, 0.1)])
+def test_f32_attention_packed_vs_reference(hd, S, p, impl, monkeypatch):
+    """fp32 attention fwd + bwd (packed QKV, inverse RoPE of the gradient) against the fp32
+    reference with the same dropout keep bits; ragged S (not a tile multiple), both the
+    flash kernels and the GEMM formulation (S 1100: 5 keys per softmax thread)."""
+    from distributed_llm_trainer_amd.ops import hip_f32
+    monkeypatch.setattr(hip_f32, "ATTN_IMPL", impl)
     torch.manual_seed(hd + S)
     B, nh = 2, 3
     H = nh * hd
@@ -99,9 +103,12 @@ def test_f32_attention_packed_vs_reference(hd, S, p):
     assert _rel(g, gr) < 5e-5, _rel(g, gr)
 
 
-def test_f32_attention_head_major():
+@pytest.mark.parametrize("impl,hd", [("flash", 64), ("gemm", 64), ("gemm", 96)])
+def test_f32_attention_head_major(impl, hd, monkeypatch):
+    from distributed_llm_trainer_amd.ops import hip_f32
+    monkeypatch.setattr(hip_f32, "ATTN_IMPL", impl)
     torch.manual_seed(9)
-    B, nh, S, hd = 2, 2, 130, 64
+    B, nh, S = 2, 2, 130
     q, k, v = (torch.randn(B, nh, S, hd, device=DEV) for _ in range(3))
     o, aux = hip.attention_fwd(q, k, v, 0.1, 99)
     orf, lser = ref.attention_fwd(q, k, v, 0.1, 99)

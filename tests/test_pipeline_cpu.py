@@ -389,3 +389,22 @@ def test_lazy_optimizer_step_matches_end_of_step_update(tmp_path):
     c = load_checkpoint(str(tmp_path / "c.pt"))
     assert torch.equal(c["model"]["norm.weight"], s0["norm.weight"])
     assert torch.equal(c["model"]["layers.1.mlp.down_proj.weight"], s0["layers.1.mlp.down_proj.weight"])
+
+
+def test_f32_attention_impl_choice(monkeypatch):
+    """fp32 attention picks the GEMM formulation while its two [B*nh, S, S] score buffers fit
+    and S <= 4096, else the flash kernels; a forced "gemm" beyond the limits is an error."""
+    from distributed_llm_trainer_amd.ops import hip_f32
+    monkeypatch.setattr(hip_f32, "ATTN_IMPL", "auto")
+    assert hip_f32._use_gemm(16, 12, 1024, 64)
+    assert not hip_f32._use_gemm(1, 12, 8192, 64)  # rows longer than the softmax kernel takes
+    assert not hip_f32._use_gemm(256, 32, 2048, 128)  # 2 x 128 GiB of scores
+    assert not hip_f32._use_gemm(2, 2, 64, 512)
+    monkeypatch.setattr(hip_f32, "ATTN_IMPL", "flash")
+    assert not hip_f32._use_gemm(16, 12, 1024, 64)
+    monkeypatch.setattr(hip_f32, "ATTN_IMPL", "gemm")
+    with pytest.raises(ValueError):
+        hip_f32._use_gemm(1, 12, 8192, 64)
+    monkeypatch.setattr(hip_f32, "ATTN_IMPL", "bogus")
+    with pytest.raises(ValueError):
+        hip_f32._use_gemm(1, 1, 64, 64)
