@@ -157,19 +157,40 @@ __global__ __launch_bounds__(256) void k_f32_norm_bwd(const float* __restrict__ 
     ws[(size_t)blockIdx.x * H + c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
 }
 
-// dw[c] += sum_b ws[b][c] in block order (deterministic)
-__global__ __launch_bounds__(256) void k_f32_colsum(const float* __restrict__ ws, float* __restrict__ dw, int nb, int H) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= H) return;
-  float s = 0.f;
-  for (int b = 0; b < nb; ++b) s += ws[(size_t)b * H + c];
-  dw[c] += s;
+// dw[c] += sum_b ws[b][c] in a fixed order (deterministic): 64 columns per workgroup, lane =
+// column; wave w of 16 sums rows w, w+16, ... into 4 interleaved accumulators (four loads in
+// flight per lane), then the 16 wave sums combine in LDS in wave order.
+__global__ __launch_bounds__(1024) void k_f32_colsum(const float* __restrict__ ws, float* __restrict__ dw, int nb, int H) {
+  __shared__ float part[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (c < H) {
+    int b = w;
+    for (; b + 48 < nb; b += 64) {
+      a0 += ws[(size_t)b * H + c];
+      a1 += ws[(size_t)(b + 16) * H + c];
+      a2 += ws[(size_t)(b + 32) * H + c];
+      a3 += ws[(size_t)(b + 48) * H + c];
+    }
+    for (; b < nb; b += 16) a0 += ws[(size_t)b * H + c];
+  }
+  part[w][lane] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (w == 0 && c < H) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += part[i][lane];
+    dw[c] += s;
+  }
 }
 
 // ------------------------------------------------------------------- RoPE
 // For tensor t in {q, k, v} (t < 2 rotated, sign -1 = inverse rotation), element (b, s, h, j):
 //   src at src_t + b*sb + s*sr + h*sh + j, dst likewise with the d* strides.
-// In place is allowed (same pointer and strides).  One thread per (row, head, pair j).
+// In place is allowed (same pointer and strides).  Grid x: (head, pair j) of a row, one
+// thread each; grid y strides over the B*S rows (no 64-bit index division per element).
+// cosT == nullptr: a plain layout copy of the ntens tensors (no rotation).
 struct F32QKV {
   const float* src[3];
   float* dst[3];
@@ -180,18 +201,17 @@ __global__ __launch_bounds__(256) void k_f32_rope(F32QKV a, const float* __restr
                                                   const float* __restrict__ sinT, int B, int S, int nh, int hd,
                                                   float sign, int ntens) {
   const int half = hd >> 1;
-  const long n = (long)B * S * nh * half;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const int j = (int)(i % half);
-    const long r = i / half;
-    const int h = (int)(r % nh);
-    const long bs = r / nh;
-    const int s = (int)(bs % S), b = (int)(bs / S);
-    const float c = cosT[(size_t)s * half + j], sn = sign * sinT[(size_t)s * half + j];
+  const int t0 = blockIdx.x * 256 + threadIdx.x;
+  if (t0 >= nh * half) return;
+  const int h = t0 / half, j = t0 - h * half;
+  for (int r = blockIdx.y; r < B * S; r += gridDim.y) {
+    const int b = r / S, s = r - b * S;
+    const bool rot = cosT != nullptr;
+    const float c = rot ? cosT[(size_t)s * half + j] : 1.f, sn = rot ? sign * sinT[(size_t)s * half + j] : 0.f;
     const long so = b * a.sb + s * a.sr + h * a.sh + j, dof = b * a.db + s * a.dr + h * a.dh + j;
     for (int t = 0; t < ntens; ++t) {
       const float x1 = a.src[t][so], x2 = a.src[t][so + half];
-      if (t < 2) {
+      if (t < 2 && rot) {
         a.dst[t][dof] = x1 * c - x2 * sn;
         a.dst[t][dof + half] = x2 * c + x1 * sn;
       } else {
@@ -203,26 +223,71 @@ __global__ __launch_bounds__(256) void k_f32_rope(F32QKV a, const float* __restr
 }
 
 // ----------------------------------------------------------------- SwiGLU
-__global__ __launch_bounds__(256) void k_f32_swiglu_fwd(const float* __restrict__ gu, float* __restrict__ s, int M, int I) {
-  const long n = (long)M * I;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const long m = i / I, j = i - m * I;
-    const float g = gu[m * 2 * I + j], u = gu[m * 2 * I + I + j];
-    s[i] = g * dlt_sigmoid(g) * u;
+// Grid x: V consecutive columns per thread (V = 4: float4 accesses, I % 4 == 0); grid y
+// strides over the rows.
+template <int V>
+struct F32Vec {
+  float v[V];
+};
+
+template <int V>
+__device__ __forceinline__ F32Vec<V> f32_ldv(const float* p) {
+  F32Vec<V> r;
+  if constexpr (V == 4) {
+    const float4 t = *reinterpret_cast<const float4*>(p);
+    r.v[0] = t.x; r.v[1] = t.y; r.v[2] = t.z; r.v[3] = t.w;
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) r.v[i] = p[i];
+  }
+  return r;
+}
+
+template <int V>
+__device__ __forceinline__ void f32_stv(float* p, const F32Vec<V>& r) {
+  if constexpr (V == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(r.v[0], r.v[1], r.v[2], r.v[3]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) p[i] = r.v[i];
   }
 }
 
+template <int V>
+__global__ __launch_bounds__(256) void k_f32_swiglu_fwd(const float* __restrict__ gu, float* __restrict__ s, int M, int I) {
+  const int j = (blockIdx.x * 256 + threadIdx.x) * V;
+  if (j >= I) return;
+  for (int m = blockIdx.y; m < M; m += gridDim.y) {
+    const float* row = gu + (size_t)m * 2 * I;
+    const F32Vec<V> g = f32_ldv<V>(row + j), u = f32_ldv<V>(row + I + j);
+    F32Vec<V> o;
+#pragma unroll
+    for (int i = 0; i < V; ++i) o.v[i] = g.v[i] * dlt_sigmoid(g.v[i]) * u.v[i];
+    f32_stv<V>(s + (size_t)m * I + j, o);
+  }
+}
+
+template <int V>
 __global__ __launch_bounds__(256) void k_f32_swiglu_bwd(const float* __restrict__ gu, const float* __restrict__ da,
                                                         float* __restrict__ dgu, float* __restrict__ s_out, int M,
                                                         int I) {
-  const long n = (long)M * I;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const long m = i / I, j = i - m * I;
-    const float g = gu[m * 2 * I + j], u = gu[m * 2 * I + I + j], d = da[i];
-    const float sg = dlt_sigmoid(g);
-    dgu[m * 2 * I + j] = d * u * sg * (1.f + g * (1.f - sg));
-    dgu[m * 2 * I + I + j] = d * g * sg;
-    if (s_out) s_out[i] = g * sg * u;
+  const int j = (blockIdx.x * 256 + threadIdx.x) * V;
+  if (j >= I) return;
+  for (int m = blockIdx.y; m < M; m += gridDim.y) {
+    const float* row = gu + (size_t)m * 2 * I;
+    const F32Vec<V> g = f32_ldv<V>(row + j), u = f32_ldv<V>(row + I + j), d = f32_ldv<V>(da + (size_t)m * I + j);
+    F32Vec<V> dg, du, so;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      const float sg = dlt_sigmoid(g.v[i]);
+      dg.v[i] = d.v[i] * u.v[i] * sg * (1.f + g.v[i] * (1.f - sg));
+      du.v[i] = d.v[i] * g.v[i] * sg;
+      so.v[i] = g.v[i] * sg * u.v[i];
+    }
+    float* drow = dgu + (size_t)m * 2 * I;
+    f32_stv<V>(drow + j, dg);
+    f32_stv<V>(drow + I + j, du);
+    if (s_out) f32_stv<V>(s_out + (size_t)m * I + j, so);
   }
 }
 
@@ -231,6 +296,7 @@ __global__ __launch_bounds__(256) void k_f32_swiglu_bwd(const float* __restrict_
 // sum per thread, then block combine), loss = lse - logit[target], and the row is
 // overwritten by grad_scale * (softmax - onehot) / n_valid (padding columns and ignored
 // rows: zero).
+template <int V>
 __global__ __launch_bounds__(256) void k_f32_ce_row(float* __restrict__ logits, const long* __restrict__ targets,
                                                     const long* __restrict__ n_valid, float* __restrict__ loss, int Vp,
                                                     int vocab, float grad_scale) {
@@ -239,7 +305,21 @@ __global__ __launch_bounds__(256) void k_f32_ce_row(float* __restrict__ logits, 
   float* lg = logits + (size_t)row * Vp;
   const long tg = targets[row];
   float m = -INFINITY, l = 0.f;
-  for (int c = tid; c < vocab; c += 256) {
+  // V-wide groups (one rescale per group), then the scalar tail of vocab % V columns
+  const int nvg = vocab / V;
+  for (int c = tid; c < nvg; c += 256) {
+    const F32Vec<V> x = f32_ldv<V>(lg + c * V);
+    float mx = x.v[0];
+#pragma unroll
+    for (int i = 1; i < V; ++i) mx = fmaxf(mx, x.v[i]);
+    if (mx > m) {
+      l *= __expf(m - mx);
+      m = mx;
+    }
+#pragma unroll
+    for (int i = 0; i < V; ++i) l += __expf(x.v[i] - m);
+  }
+  for (int c = nvg * V + tid; c < vocab; c += 256) {
     const float v = lg[c];
     if (v > m) {
       l = l * __expf(m - v) + 1.f;
@@ -271,10 +351,14 @@ __global__ __launch_bounds__(256) void k_f32_ce_row(float* __restrict__ logits, 
   if (tid == 0) loss[row] = valid ? lse - lg[tg] : 0.f;
   __syncthreads();  // the target logit is read before any thread overwrites it
   const float gs = valid ? grad_scale / nv : 0.f;
-  for (int c = tid; c < Vp; c += 256) {
-    float gv = 0.f;
-    if (c < vocab && valid) gv = (__expf(lg[c] - lse) - (c == tg ? 1.f : 0.f)) * gs;
-    lg[c] = gv;
+  for (int c0 = tid * V; c0 < Vp; c0 += 256 * V) {
+    F32Vec<V> g = f32_ldv<V>(lg + c0);
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      const int c = c0 + i;
+      g.v[i] = (c < vocab && valid) ? (__expf(g.v[i] - lse) - (c == tg ? 1.f : 0.f)) * gs : 0.f;
+    }
+    f32_stv<V>(lg + c0, g);
   }
 }
 
@@ -694,33 +778,44 @@ DLT_API int dlt_f32_norm_bwd(const float* dy, const float* x, const float* rstd,
   nb = (M + rpb - 1) / rpb;
   F32_NT_DISPATCH(nt, k_f32_norm_bwd<NTC><<<nb, 256, 0, st>>>(dy, x, rstd, w, dres, dx, ddelta, ws, scale, dy_mul, M, H,
                                                               rpb, key, thr, dscale));
-  k_f32_colsum<<<(H + 255) / 256, 256, 0, st>>>(ws, dweight, nb, H);
+  k_f32_colsum<<<(H + 63) / 64, 1024, 0, st>>>(ws, dweight, nb, H);
   DLT_CHECK_LAUNCH();
 }
 
 DLT_API int dlt_f32_rope(const float* sq, const float* sk, const float* sv, float* dq, float* dk, float* dv, long sb,
                          long sr, long sh, long db, long dr, long dh, const float* cosT, const float* sinT, int B, int S,
                          int nh, int hd, float sign, int ntens, hipStream_t st) {
-  if (hd % 2 || ntens < 2 || ntens > 3) return -1;
+  if (hd % 2 || ntens < 1 || ntens > 3 || (cosT && ntens < 2)) return -1;
   F32QKV a{{sq, sk, sv}, {dq, dk, dv}, sb, sr, sh, db, dr, dh};
-  k_f32_rope<<<f32_blocks((long)B * S * nh * (hd / 2)), 256, 0, st>>>(a, cosT, sinT, B, S, nh, hd, sign, ntens);
+  if ((long)B * S > 0x7fffffffL) return -1;
+  const dim3 grid((nh * (hd / 2) + 255) / 256, B * S < 65535 ? B * S : 65535);
+  k_f32_rope<<<grid, 256, 0, st>>>(a, cosT, sinT, B, S, nh, hd, sign, ntens);
   DLT_CHECK_LAUNCH();
 }
 
+static inline bool f32_al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+static inline dim3 f32_rows_grid(int cols, int M) {
+  return dim3((cols + 255) / 256, M < 65535 ? (M < 1 ? 1 : M) : 65535);
+}
+
 DLT_API int dlt_f32_swiglu_fwd(const float* gu, float* s, int M, int I, hipStream_t st) {
-  k_f32_swiglu_fwd<<<f32_blocks((long)M * I), 256, 0, st>>>(gu, s, M, I);
+  if (I % 4 == 0 && f32_al16(gu) && f32_al16(s)) k_f32_swiglu_fwd<4><<<f32_rows_grid(I / 4, M), 256, 0, st>>>(gu, s, M, I);
+  else k_f32_swiglu_fwd<1><<<f32_rows_grid(I, M), 256, 0, st>>>(gu, s, M, I);
   DLT_CHECK_LAUNCH();
 }
 
 DLT_API int dlt_f32_swiglu_bwd(const float* gu, const float* da, float* dgu, float* s_out, int M, int I, hipStream_t st) {
-  k_f32_swiglu_bwd<<<f32_blocks((long)M * I), 256, 0, st>>>(gu, da, dgu, s_out, M, I);
+  if (I % 4 == 0 && f32_al16(gu) && f32_al16(da) && f32_al16(dgu) && f32_al16(s_out)) k_f32_swiglu_bwd<4><<<f32_rows_grid(I / 4, M), 256, 0, st>>>(gu, da, dgu, s_out, M, I);
+  else k_f32_swiglu_bwd<1><<<f32_rows_grid(I, M), 256, 0, st>>>(gu, da, dgu, s_out, M, I);
   DLT_CHECK_LAUNCH();
 }
 
 DLT_API int dlt_f32_cross_entropy(float* logits, const long* targets, const long* n_valid, float* loss, int M, int Vp,
                                   int vocab, float grad_scale, hipStream_t st) {
   if (M <= 0) return 0;
-  k_f32_ce_row<<<M, 256, 0, st>>>(logits, targets, n_valid, loss, Vp, vocab, grad_scale);
+  if (Vp % 4 == 0 && f32_al16(logits)) k_f32_ce_row<4><<<M, 256, 0, st>>>(logits, targets, n_valid, loss, Vp, vocab, grad_scale);
+  else k_f32_ce_row<1><<<M, 256, 0, st>>>(logits, targets, n_valid, loss, Vp, vocab, grad_scale);
   DLT_CHECK_LAUNCH();
 }
 

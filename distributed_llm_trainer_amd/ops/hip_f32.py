@@ -48,6 +48,7 @@ ATTN_HEAD_DIMS = (64, 128)
 # flash kernels' LDS-broadcast-bound FMAs (profiles/r5_fp32_attention.md).
 ATTN_IMPL = os.environ.get("DLT_F32_ATTN", "auto")
 GEMM_ATTN_BYTES = 16 << 30
+BMM_PLANNER = os.environ.get("DLT_F32_BMM", "torch") == "planner"
 
 
 def _h():
@@ -200,9 +201,49 @@ def _use_gemm(B, nh, S, hd):
     return fits
 
 
-def _heads(t, B, S, nh, hd):
-    """[B*S, nh*hd]-rowed view (row stride may exceed nh*hd) -> [B, nh, S, hd] view."""
-    return t.as_strided((B, nh, S, hd), (S * t.stride(0), hd, t.stride(0), 1))
+def _relayout(src, sstr, B, S, nh, hd, device, dst=None, dstr=None):
+    """Strided copy of len(src) tensors (element (b, s, h, d) at ptr + b*st[0] + s*st[1] +
+    h*st[2] + d) into head-major [n, B, nh, S, hd] (k_f32_rope without rotation), or into
+    ``dst`` pointers with strides ``dstr``."""
+    n = len(src)
+    out = None
+    if dst is None:
+        out = torch.empty(n, B, nh, S, hd, dtype=torch.float32, device=device)
+        dst, dstr = [_p(out[j]) for j in range(n)], (nh * S * hd, hd, S * hd)
+    pad = [None] * (3 - n)
+    _chk(_lib().dlt_f32_rope(*src, *pad, *dst, *pad, *sstr, *dstr, None, None, B, S, nh, hd, 1.0, n, _st()),
+         "f32_relayout")
+    return out
+
+
+def _bmm(kind, a, b):
+    """Batched row-major products over contiguous [..., r, c] operands: "nt" a @ b^T,
+    "nn" a @ b, "tn" a^T @ b.  torch.matmul (hipBLASLt's heuristic pick) by default;
+    BMM_PLANNER routes them through the autotuned planner of ops/gemm.py instead -- its
+    per-shape races run while the other chain's kernels share the GPU and picked slower
+    kernels in the step (profiles/r5_fp32_attention.md)."""
+    from . import gemm
+    if not (BMM_PLANNER and gemm.available()):
+        a2 = a.transpose(-1, -2) if kind == "tn" else a
+        return torch.matmul(a2, b.transpose(-1, -2) if kind == "nt" else b)
+    *lead, ra, ca = a.shape
+    rb, cb = b.shape[-2:]
+    bt = a.numel() // (ra * ca)
+    M, K = (ca, ra) if kind == "tn" else (ra, ca)
+    N = rb if kind == "nt" else cb
+    c = torch.empty(*lead, M, N, dtype=torch.float32, device=a.device)
+    sa, sb, sc = ra * ca, rb * cb, M * N
+    if kind == "nt":    # C^T = op_T(B_c) . A_c
+        gemm._gemm_batched(1, 0, N, M, K, b, cb, sb, a, ca, sa, c, N, sc, bt)
+    elif kind == "nn":  # C^T = B_c . A_c
+        gemm._gemm_batched(0, 0, N, M, K, b, cb, sb, a, ca, sa, c, N, sc, bt)
+    else:               # C^T = B_c . op_T(A_c)
+        gemm._gemm_batched(0, 1, N, M, K, b, cb, sb, a, ca, sa, c, N, sc, bt)
+    return c
+
+
+def _packed_ptrs(t, n, H):
+    return [ctypes.c_void_p(t.data_ptr() + j * H * 4) for j in range(n)]
 
 
 def _gemm_fwd(q4, k4, v4, B, nh, S, hd, p, key, device, out, mask, store_mask):
@@ -210,12 +251,12 @@ def _gemm_fwd(q4, k4, v4, B, nh, S, hd, p, key, device, out, mask, store_mask):
     _req32(o, "attn_f32.o", B * S * nh * hd)
     lse = torch.empty(B, nh, S, dtype=torch.float32, device=device)
     mask, dscale = _mask(B, nh, S, p, key, device, mask)
-    sc = torch.matmul(q4, k4.transpose(-1, -2))
+    sc = _bmm("nt", q4, k4)
     _chk(_lib().dlt_f32_attn_softmax(_p(sc), _p(lse), _p(mask), B * nh, S, 1.0 / math.sqrt(hd), dscale, _st()),
          "f32_attn_softmax")
-    o4 = torch.matmul(sc, v4)
+    o4 = _bmm("nn", sc, v4)
     del sc
-    _heads(o, B, S, nh, hd).copy_(o4)
+    _relayout([_p(o4)], (nh * S * hd, hd, S * hd), B, S, nh, hd, device, [_p(o)], (S * nh * hd, nh * hd, hd))
     return o, _h().AttnAux((lse, mask if store_mask else None))
 
 
@@ -226,15 +267,15 @@ def _gemm_bwd(q4, k4, v4, o, do, aux, B, nh, S, hd, p, key, device):
     _req32(o, "attn_bwd_f32.o", B * S * nh * hd)
     _req32(do, "attn_bwd_f32.do", B * S * nh * hd)
     mask, dscale = _mask(B, nh, S, p, key, device, mask)
-    do4 = _heads(do, B, S, nh, hd)
-    sc = torch.matmul(q4, k4.transpose(-1, -2))
-    dp = torch.matmul(do4, v4.transpose(-1, -2))
+    do4 = _relayout([_p(do)], (S * nh * hd, nh * hd, hd), B, S, nh, hd, device)[0]
+    sc = _bmm("nt", q4, k4)
+    dp = _bmm("nt", do4, v4)
     _chk(_lib().dlt_f32_attn_dsoftmax(_p(sc), _p(dp), _p(lse), _p(o), _p(do), _p(mask), B, nh, S, hd,
                                       1.0 / math.sqrt(hd), dscale, _st()), "f32_attn_dsoftmax")
-    dv = torch.matmul(sc.transpose(-1, -2), do4)
+    dv = _bmm("tn", sc, do4)
     del sc
-    dq = torch.matmul(dp, k4)
-    dk = torch.matmul(dp.transpose(-1, -2), q4)
+    dq = _bmm("nn", dp, k4)
+    dk = _bmm("tn", dp, q4)
     return dq, dk, dv
 
 
@@ -270,7 +311,7 @@ def attention_fwd_packed(qkv, B, S, nh, p, key, out=None, mask=None, store_mask=
     _req32(qkv, "attn_f32.qkv")
     H = nh * hd
     if _use_gemm(B, nh, S, hd):
-        q4, k4, v4 = (_heads(qkv[:, j * H:(j + 1) * H], B, S, nh, hd) for j in range(3))
+        q4, k4, v4 = _relayout(_packed_ptrs(qkv, 3, H), (S * threeH, threeH, hd), B, S, nh, hd, qkv.device)
         return _gemm_fwd(q4, k4, v4, B, nh, S, hd, p, key, qkv.device, out, mask, store_mask)
     ptr = [ctypes.c_void_p(qkv.data_ptr() + j * H * 4) for j in range(3)]
     return _fwd(*ptr, (S * threeH, hd, threeH), B, nh, S, hd, p, key, qkv.device, out, mask, store_mask)
@@ -310,10 +351,10 @@ def attention_bwd_packed(qkv, o, do, aux, p, key, B, S, nh, cos, sin, out=None):
     dqkv = torch.empty(M, threeH, dtype=torch.float32, device=qkv.device) if out is None else out
     _req32(dqkv, "attn_bwd_f32.dqkv", M * threeH)
     if _use_gemm(B, nh, S, hd):
-        q4, k4, v4 = (_heads(qkv[:, j * H:(j + 1) * H], B, S, nh, hd) for j in range(3))
-        for j, g in enumerate(_gemm_bwd(q4, k4, v4, o, do, aux, B, nh, S, hd, p, key, qkv.device)):
-            _heads(dqkv[:, j * H:(j + 1) * H], B, S, nh, hd).copy_(g)
-        return rope_qk_inplace(dqkv, B, S, nh, cos, sin, sign=-1.0)
+        q4, k4, v4 = _relayout(_packed_ptrs(qkv, 3, H), (S * threeH, threeH, hd), B, S, nh, hd, qkv.device)
+        dq, dk, dv = _gemm_bwd(q4, k4, v4, o, do, aux, B, nh, S, hd, p, key, qkv.device)
+        del q4, k4, v4
+        return rope_qkv_bwd(dq, dk, dv, cos, sin, out=dqkv)
     src = [ctypes.c_void_p(qkv.data_ptr() + j * H * 4) for j in range(3)]
     dst = [ctypes.c_void_p(dqkv.data_ptr() + j * H * 4) for j in range(3)]
     st = (S * threeH, hd, threeH)
