@@ -35,8 +35,8 @@ def main():
     delta = torch.randn(M, H, device=dev)
     w = torch.ones(H, device=dev)
     key = rng.site_key(1, 0, 0, rng.SITE_RESID)
-    row("norm fwd", timeit(lambda: hip.add_dropout_rmsnorm_fwd(resid, delta, w, 1e-5, 0.1, key)), M * H * 16)
-    x, y, rstd = hip.add_dropout_rmsnorm_fwd(resid, delta, w, 1e-5, 0.1, key)
+    row("norm fwd", timeit(lambda: hip.add_dropout_rmsnorm_fwd(resid, delta, w, 1e-5, 0.1, key, out_dtype=torch.float32)), M * H * 16)
+    x, y, rstd = hip.add_dropout_rmsnorm_fwd(resid, delta, w, 1e-5, 0.1, key, out_dtype=torch.float32)
     dy, dres, dw = torch.randn(M, H, device=dev), torch.randn(M, H, device=dev), torch.zeros(H, device=dev)
     row("norm bwd (+colsum)", timeit(lambda: hip.rmsnorm_bwd(dy, x, rstd, w, dres, dw, 0.1, key)), M * H * 20)
     gu, da = torch.randn(M, 2 * I, device=dev), torch.randn(M, I, device=dev)
