@@ -103,10 +103,13 @@ def test_f32_attention_packed_vs_reference(hd, S, p, impl, monkeypatch):
     assert _rel(g, gr) < 5e-5, _rel(g, gr)
 
 
-@pytest.mark.parametrize("impl,hd", [("flash", 64), ("gemm", 64), ("gemm", 96)])
+@pytest.mark.parametrize("impl,hd", [("flash", 64), ("gemm", 64), ("gemm", 96), ("gemm-planner", 64)])
 def test_f32_attention_head_major(impl, hd, monkeypatch):
+    """Head-major fp32 attention vs the reference: flash kernels, the GEMM formulation
+    (torch.matmul products; "gemm-planner": the autotuned planner's batched GEMMs)."""
     from distributed_llm_trainer_amd.ops import hip_f32
-    monkeypatch.setattr(hip_f32, "ATTN_IMPL", impl)
+    monkeypatch.setattr(hip_f32, "ATTN_IMPL", impl.split("-")[0])
+    monkeypatch.setattr(hip_f32, "BMM_PLANNER", impl.endswith("planner"))
     torch.manual_seed(9)
     B, nh, S = 2, 2, 130
     q, k, v = (torch.randn(B, nh, S, hd, device=DEV) for _ in range(3))
