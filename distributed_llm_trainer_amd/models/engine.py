@@ -453,7 +453,7 @@ class GPTEngine:
         if mask is not None:
             torch.cuda.current_stream().wait_event(mask_ev)
         kw = {"mask": mask} if mask is not None else {}
-        if pa > 0.0 and getattr(ops, "backend", "") == "hip" and getattr(ops, "attn_backend", "hip") == "hip":
+        if pa > 0.0 and getattr(ops, "backend", "") == "hip" and getattr(ops, "attn_backend", "hip") in ("hip", "gemm"):
             # keep this layer's keep bits for the backward only within the memory budget.
             # The masks (two layouts, 1 bit per causal score: 8 * B * nh * S * ceil(S/32) B)
             # grow with S^2, the saved block input (M * H * 4 B) with S: under activation

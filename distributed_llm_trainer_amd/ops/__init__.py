@@ -52,11 +52,13 @@ def for_device(device, head_dim: int = 64, act_dtype=torch.bfloat16) -> types.Si
     """Op namespace for ``device``.  On the GPU every op is a HIP kernel: bf16 / fp16
     activations on the 16-bit kernels, fp32 (``--mixed_precision fp32``) on the fp32
     kernels (``csrc/fp32.hip``; the ``hip`` wrappers dispatch on the tensor dtype).  The
-    attention kernels take head_dim 64 and 128 in every precision; a model with another
-    head_dim (the reference allows any ``hidden % heads == 0``, ``config.py:38-39``) runs
-    RoPE + attention through the PyTorch reference ops ON THE GPU (``attn_backend ==
-    "reference"``, with a one-time warning) while the norms, SwiGLU, cross-entropy,
-    embedding, optimizer and GEMMs stay native."""
+    flash attention kernels take head_dim 64 and 128 in every precision; a model with
+    another head_dim (the reference allows any ``hidden % heads == 0``, ``config.py:38-39``)
+    runs attention through the fp32 GEMM formulation (``ops/attn_gemm.py``: hipBLASLt fp32
+    GEMMs + HIP row kernels, ``attn_backend == "gemm"``, with a one-time warning) and its
+    RoPE on the HIP kernel when that takes the head_dim (16-bit: head_dim % 16 == 0; fp32:
+    even), else as PyTorch ops on the GPU; the norms, SwiGLU, cross-entropy, embedding,
+    optimizer and GEMMs stay native."""
     dev = torch.device(device)
     if dev.type == "cuda":
         if os.environ.get("DLT_ALLOW_REFERENCE_ON_GPU") == "1":
@@ -68,10 +70,17 @@ def for_device(device, head_dim: int = 64, act_dtype=torch.bfloat16) -> types.Si
         native_hd = F32_HEAD_DIMS if act_dtype == torch.float32 else ATTN_HEAD_DIMS
         if head_dim not in native_hd:
             import warnings
-            warnings.warn(f"head_dim {head_dim}: the HIP attention kernels take head_dim {native_hd} for "
-                          f"{act_dtype} activations; RoPE + attention run as PyTorch ops on the GPU for this model")
+
+            from . import attn_gemm
+            rope_native = head_dim % (2 if act_dtype == torch.float32 else 16) == 0
+            warnings.warn(f"head_dim {head_dim}: the HIP flash attention kernels take head_dim {native_hd}; attention "
+                          f"runs as fp32 GEMMs + HIP row kernels for this model (RoPE: "
+                          f"{'HIP kernel' if rope_native else 'PyTorch ops'})")
             for f in _ATTN_FUNCS:
-                setattr(ns, f, getattr(reference, f))
-            ns.attn_backend = "reference"
+                if not f.startswith("rope"):
+                    setattr(ns, f, getattr(attn_gemm, f))
+                elif not rope_native:
+                    setattr(ns, f, getattr(reference, f))
+            ns.attn_backend = "gemm"
         return ns
     return CPU_OPS

@@ -138,3 +138,28 @@ def test_fp32_training_runs_hip_kernels():
     data = torch.randint(0, 1000, (4, 256), device=DEV, generator=torch.Generator(DEV).manual_seed(1))
     losses = [tr.train_step({"input_ids": data})["loss"] for _ in range(5)]
     assert all(l == l for l in losses) and losses[-1] < losses[0], losses
+
+
+@pytest.mark.parametrize("dt,hd", [(torch.bfloat16, 48), (torch.float16, 80), (torch.float32, 32)])
+def test_attn_gemm_odd_head_dims_vs_reference(dt, hd):
+    """ops/attn_gemm.py (head_dims without a flash kernel): 16-bit / fp32 packed QKV
+    through the fp32 GEMM formulation against the PyTorch reference attention (also fp32
+    arithmetic on the same inputs, same keep bits), forward + backward + inverse RoPE."""
+    from distributed_llm_trainer_amd.ops import attn_gemm
+    torch.manual_seed(hd)
+    B, nh, S, p = 2, 3, 200, 0.1
+    H = nh * hd
+    qkv = (torch.randn(B * S, 3 * H, device=DEV) * 0.5).to(dt)
+    cos, sin = hip.rope_tables(hd, S, device=DEV)
+    assert attn_gemm.fits(B, nh, S, hd)
+    o, aux = attn_gemm.attention_fwd_packed(qkv, B, S, nh, p, 77)
+    orf, lser = ref.attention_fwd_packed(qkv, B, S, nh, p, 77)
+    assert o.dtype == dt
+    tol = 2e-5 if dt == torch.float32 else 1e-2
+    assert _rel(o, orf) < tol, _rel(o, orf)
+    assert _rel(aux[0], lser) < 2e-5
+    do = torch.randn(B * S, H, device=DEV).to(dt)
+    g = attn_gemm.attention_bwd_packed(qkv, o, do, aux, p, 77, B, S, nh, cos, sin)
+    gr = ref.attention_bwd_packed(qkv, orf, do, lser, p, 77, B, S, nh, cos, sin)
+    assert g.dtype == dt and g.shape == qkv.shape
+    assert _rel(g, gr) < (5e-5 if dt == torch.float32 else 2e-2), _rel(g, gr)
