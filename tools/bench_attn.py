@@ -30,12 +30,14 @@ def main():
     ap.add_argument("--p", type=float, default=0.1)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--packed", action="store_true", help="attention on the packed [B*S, 3H] QKV (engine default)")
+    ap.add_argument("--dtype", default="bf16", choices=("bf16", "fp16"))
     a = ap.parse_args()
+    dt = torch.bfloat16 if a.dtype == "bf16" else torch.float16
     torch.manual_seed(0)
-    q, k, v = (torch.randn(a.B, a.nh, a.S, 64, device="cuda").bfloat16() for _ in range(3))
+    q, k, v = (torch.randn(a.B, a.nh, a.S, 64, device="cuda").to(dt) for _ in range(3))
     key = rng.site_key(1, 2, 3, rng.SITE_ATTN)
     if a.packed:
-        qkv = torch.randn(a.B * a.S, 3 * a.nh * 64, device="cuda").bfloat16()
+        qkv = torch.randn(a.B * a.S, 3 * a.nh * 64, device="cuda").to(dt)
         cos, sin = hip.rope_tables(64, a.S, device="cuda")
         o, aux = hip.attention_fwd_packed(qkv, a.B, a.S, a.nh, a.p, key)
         do = torch.randn_like(o)
