@@ -8,6 +8,7 @@ last kernel end) vs the summed kernel time -> GPU idle (launch gaps).
 usage: python tools/step_profile.py run_kernel_trace.csv [micro_steps]
 """
 import csv
+import os
 import re
 import sys
 from collections import defaultdict
@@ -84,7 +85,7 @@ def main(path, micro=4):
     print()
     print("| kernel | ms/step | launches | avg us |")
     print("|---|---:|---:|---:|")
-    for n, (t, k) in sorted(names.items(), key=lambda kv: -kv[1][0])[:25]:
+    for n, (t, k) in sorted(names.items(), key=lambda kv: -kv[1][0])[:int(os.environ.get("STEP_PROFILE_TOP", "25"))]:
         print(f"| `{n.replace('|', '/')}` | {t / 1e3:.3f} | {k} | {t / k:.1f} |")
 
 
