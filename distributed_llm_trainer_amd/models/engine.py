@@ -46,10 +46,9 @@ other leaves idle.  The reference runs the micro-steps strictly one after the ot
 from __future__ import annotations
 
 import contextlib
-import math
 import os
 from dataclasses import dataclass, field
-from typing import Any, Callable, Dict, List, Optional
+from typing import Any, Callable, List, Optional
 
 import torch
 

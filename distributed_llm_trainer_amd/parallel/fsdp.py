@@ -36,7 +36,6 @@ full-size fp32 unit gradients across micro-steps and reduce-scatters once.
 """
 from __future__ import annotations
 
-import math
 import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple

@@ -11,7 +11,7 @@ reference behaviour (e.g. ``seed``), or enable MI355X-specific knobs
 """
 from __future__ import annotations
 
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Optional
 
 

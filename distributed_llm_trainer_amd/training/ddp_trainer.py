@@ -27,7 +27,6 @@ import argparse
 import contextlib
 import json
 import os
-import sys
 import time
 from typing import Optional
 

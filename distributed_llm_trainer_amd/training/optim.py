@@ -19,7 +19,6 @@ reference's ``optimizer.state_dict()``.
 """
 from __future__ import annotations
 
-import math
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
