@@ -1,25 +1,96 @@
 """Attention for head_dims without a flash kernel (not 64 / 128), on native kernels.
 
 The reference accepts any ``hidden % heads == 0`` (``config.py:38-39``); the MFMA flash
-kernels exist for head_dim 64 and 128.  Any other head_dim runs the GEMM formulation of
-``hip_f32``: q / k / v widened to fp32, the six S x S x hd products as batched hipBLASLt
-fp32 GEMMs around the ``k_f32_attn_softmax`` / ``_dsoftmax`` row kernels (same dropout
-keep bits as every other path), the result narrowed back to the activation dtype.  That
-is the arithmetic of the PyTorch reference attention (``reference.py:180-227``: fp32
-scores, fp32 softmax), with HIP kernels in place of the ATen masking / softmax / dropout
-over the [S, S] matrix.  Rows longer than 4096 keys, or score buffers over
-``hip_f32.GEMM_ATTN_BYTES``, use the reference ops (the same choice is made for a
-forward and its backward, from the shapes alone).
+kernels exist for head_dim 64 and 128.  Any other head_dim runs attention as batched
+hipBLASLt GEMMs over the dense [S, S] scores around the row kernels of
+``csrc/attn_gemm.hip`` (causal softmax / its backward, the same dropout keep bits as every
+other path):
+
+* 16-bit activations, head_dim % 16 == 0: 16-bit MFMA GEMMs (through the autotuned planner,
+  ``ops/gemm.py``) with fp32 scores and dO·Vᵀ, P / Pd / dS rounded to 16 bits as operands
+  -- the flash kernels' arithmetic; q / k / v / dO reach the head-major layout through
+  ``k_relayout16`` and the gradient leaves through the 16-bit inverse-RoPE kernel.
+* otherwise: q / k / v widened to fp32 and ``hip_f32``'s fp32 formulation, the result
+  narrowed back -- the arithmetic of the PyTorch reference attention
+  (``reference.py:180-227``: fp32 scores, fp32 softmax).
+
+Rows longer than 4096 keys, or score buffers over ``hip_f32.GEMM_ATTN_BYTES``, use the
+reference ops.  A forward and its backward make the same choice (from the shapes and the
+dtype alone).
 """
 from __future__ import annotations
+
+import math
 
 import torch
 
 from . import hip_f32, reference
 
+_HK = {torch.bfloat16: 0, torch.float16: 1}
+
 
 def fits(B: int, nh: int, S: int, hd: int) -> bool:
-    return hd % 2 == 0 and hd <= 256 and S <= 4096 and 2 * B * nh * S * S * 4 <= hip_f32.GEMM_ATTN_BYTES
+    """Shapes the GEMM formulation takes (its live score buffers: 8-12 B per score)."""
+    return hd % 2 == 0 and hd <= 256 and S <= 4096 and 3 * B * nh * S * S * 4 <= hip_f32.GEMM_ATTN_BYTES
+
+
+def use16(dtype, B: int, nh: int, S: int, hd: int) -> bool:
+    """16-bit GEMMs (vs fp32 widening) for these operands."""
+    from . import gemm
+    return dtype in _HK and hd % 16 == 0 and fits(B, nh, S, hd) and gemm.available()
+
+
+def _relayout16(src, sstr, dst, dstr, B, S, nh, hd, n, sts=0, dts=0):
+    hip_f32._chk(hip_f32._lib().dlt_relayout16(hip_f32._p(src), hip_f32._p(dst), *sstr, *dstr, sts, dts, B, S, nh, hd, n,
+                                               hip_f32._st()), "relayout16")
+
+
+def _heads16(t, B, S, nh, hd, n):
+    """The n [B*S, nh*hd] column blocks of t (row stride t.stride(0)) -> [n, B, nh, S, hd]."""
+    H, ld = nh * hd, t.stride(0)
+    out = torch.empty(n, B, nh, S, hd, dtype=t.dtype, device=t.device)
+    _relayout16(t, (S * ld, ld, hd), out, (nh * S * hd, hd, S * hd), B, S, nh, hd, n, H, B * nh * S * hd)
+    return out
+
+
+def _fwd16(q4, k4, v4, B, nh, S, hd, p, key, out, mask, store_mask):
+    dt, dev = q4.dtype, q4.device
+    H = nh * hd
+    lse = torch.empty(B, nh, S, dtype=torch.float32, device=dev)
+    mask, dscale = hip_f32._mask(B, nh, S, p, key, dev, mask)
+    sc = hip_f32._bmm("nt", q4, k4, torch.float32)
+    pm = torch.empty(B, nh, S, S, dtype=dt, device=dev)
+    hip_f32._chk(hip_f32._lib().dlt_attn16_softmax(hip_f32._p(sc), hip_f32._p(pm), hip_f32._p(lse), hip_f32._p(mask),
+                                                   B * nh, S, 1.0 / math.sqrt(hd), dscale, _HK[dt], hip_f32._st()),
+                 "attn16_softmax")
+    del sc
+    o4 = hip_f32._bmm("nn", pm, v4)
+    del pm
+    o = torch.empty(B * S, H, dtype=dt, device=dev) if out is None else out
+    if o.dtype != dt or not o.is_contiguous() or o.numel() != B * S * H:
+        raise ValueError("attn_gemm: out must be a contiguous [B*S, H] tensor of the activation dtype")
+    _relayout16(o4, (nh * S * hd, hd, S * hd), o, (S * H, H, hd), B, S, nh, hd, 1)
+    return o, hip_f32._h().AttnAux((lse, mask if store_mask else None))
+
+
+def _bwd16(q4, k4, v4, o, do, aux, B, nh, S, hd, p, key):
+    """(dq, dk, dv) as contiguous [B, nh, S, hd] in the activation dtype."""
+    dt, dev = q4.dtype, q4.device
+    lse, mask = aux if isinstance(aux, tuple) else (aux, None)
+    o, do = o.contiguous(), do.contiguous()
+    mask, dscale = hip_f32._mask(B, nh, S, p, key, dev, mask)
+    do4 = _heads16(do, B, S, nh, hd, 1)[0]
+    sc = hip_f32._bmm("nt", q4, k4, torch.float32)
+    dp = hip_f32._bmm("nt", do4, v4, torch.float32)
+    pd = torch.empty(B, nh, S, S, dtype=dt, device=dev)
+    ds = torch.empty_like(pd)
+    hip_f32._chk(hip_f32._lib().dlt_attn16_dsoftmax(
+        hip_f32._p(sc), hip_f32._p(dp), hip_f32._p(pd), hip_f32._p(ds), hip_f32._p(lse), hip_f32._p(o), hip_f32._p(do),
+        hip_f32._p(mask), B, nh, S, hd, 1.0 / math.sqrt(hd), dscale, _HK[dt], hip_f32._st()), "attn16_dsoftmax")
+    del sc, dp
+    dv = hip_f32._bmm("tn", pd, do4)
+    del pd
+    return hip_f32._bmm("nn", ds, k4), hip_f32._bmm("tn", ds, q4), dv
 
 
 def _f32(t: torch.Tensor) -> torch.Tensor:
@@ -42,6 +113,9 @@ def _heads32(qkv, B, S, nh, hd):
 
 def attention_fwd_packed(qkv, B, S, nh, p, key, out=None, mask=None, store_mask=True):
     hd = qkv.shape[1] // (3 * nh)
+    if use16(qkv.dtype, B, nh, S, hd):
+        q4, k4, v4 = _heads16(qkv, B, S, nh, hd, 3)
+        return _fwd16(q4, k4, v4, B, nh, S, hd, p, key, out, mask, store_mask)
     if not fits(B, nh, S, hd):
         return reference.attention_fwd_packed(qkv, B, S, nh, p, key, out=out, mask=mask)
     q4, k4, v4 = _heads32(qkv, B, S, nh, hd)
@@ -52,6 +126,12 @@ def attention_fwd_packed(qkv, B, S, nh, p, key, out=None, mask=None, store_mask=
 
 def attention_bwd_packed(qkv, o, do, aux, p, key, B, S, nh, cos, sin, out=None):
     hd = qkv.shape[1] // (3 * nh)
+    if use16(qkv.dtype, B, nh, S, hd):
+        from . import hip
+        q4, k4, v4 = _heads16(qkv, B, S, nh, hd, 3)
+        dq, dk, dv = _bwd16(q4, k4, v4, o, do, aux, B, nh, S, hd, p, key)
+        del q4, k4, v4
+        return hip.rope_qkv_bwd(dq, dk, dv, cos, sin, out=out)
     if not fits(B, nh, S, hd):
         return reference.attention_bwd_packed(qkv, o, do, aux, p, key, B, S, nh, cos, sin, out=out)
     q4, k4, v4 = _heads32(qkv, B, S, nh, hd)
@@ -65,6 +145,8 @@ def attention_fwd(q, k, v, p, key, causal=True, store_mask=True, out=None, mask=
     if not causal:
         raise NotImplementedError("only causal attention is implemented (the model is a causal LM)")
     B, nh, S, hd = q.shape
+    if use16(q.dtype, B, nh, S, hd):
+        return _fwd16(q.contiguous(), k.contiguous(), v.contiguous(), B, nh, S, hd, p, key, out, mask, store_mask)
     if not fits(B, nh, S, hd):
         return reference.attention_fwd(q, k, v, p, key, causal, out=out)
     o32 = out if out is not None and out.dtype == torch.float32 else None
@@ -74,6 +156,8 @@ def attention_fwd(q, k, v, p, key, causal=True, store_mask=True, out=None, mask=
 
 def attention_bwd(q, k, v, o, do, aux, p, key, causal=True):
     B, nh, S, hd = q.shape
+    if use16(q.dtype, B, nh, S, hd):
+        return _bwd16(q.contiguous(), k.contiguous(), v.contiguous(), o, do, aux, B, nh, S, hd, p, key)
     if not fits(B, nh, S, hd):
         return reference.attention_bwd(q, k, v, o, do, aux, p, key, causal)
     g = hip_f32._gemm_bwd(_f32(q), _f32(k), _f32(v), _f32(o), _f32(do), aux, B, nh, S, hd, p, key, q.device)

@@ -12,10 +12,8 @@
 //     (forward, dQ) or per key (dK/dV), K/V (Q/dO) tiles staged through LDS and read as
 //     wave-wide broadcasts; head_dim 64 and 128; dropout from the keep-bit words of
 //     k_dropout_bits (attention.hip), so fp32 and 16-bit runs drop the same scores.
-//   * k_f32_attn_softmax / _dsoftmax   -- the row-wise middle of the GEMM formulation of
-//     the same attention (the default up to 4096 keys: the six S x S x hd products go to
-//     hipBLASLt's fp32 MFMA kernels, which keep the matrix cores fed where the lane-per-
-//     query flash kernels are LDS-broadcast bound)
+//     (the default fp32 attention up to 4096 keys is the GEMM formulation instead: its row
+//     kernels are in attn_gemm.hip)
 //
 // fp32 is the reference / debug precision here: these kernels are written for exactness
 // and simplicity, not tuned like the bf16 hot path.
@@ -625,119 +623,6 @@ __global__ __launch_bounds__(64) void k_f32_attn_bwd_dkdv(F32Attn a) {
   }
 }
 
-// ------------------------------------------------- attention through fp32 GEMMs
-// The fp32 MFMA path: Q·Kᵀ, P·V, dO·Vᵀ, Pᵀ·dO, dS·K and dSᵀ·Q run as batched hipBLASLt
-// fp32 GEMMs over the dense [S, S] score matrix of each (b, h) (hip_f32.py); these two
-// kernels are the row-wise middle.  One 256-thread block per (bh, q) row.  The lane-per-
-// query flash kernels above stay for rows longer than 4096 keys or when the [S, S] buffers
-// do not fit.
-__device__ __forceinline__ float f32_wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
-
-__device__ __forceinline__ float f32_wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
-// block-wide max / sum over the 4 waves, returned to every thread
-template <bool MAX>
-__device__ __forceinline__ float f32_block_reduce(float v, float* red) {
-  v = MAX ? f32_wave_max(v) : f32_wave_sum(v);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-  __syncthreads();
-  const float r = MAX ? fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])) : (red[0] + red[1]) + (red[2] + red[3]);
-  __syncthreads();  // red is reused by the next reduction
-  return r;
-}
-
-// forward: sc [BH*S, S] raw scores q·k -> in place keep * dscale * softmax(scale * s) over
-// keys <= q (zeros after q); lse [BH*S] natural log.  NE keys per thread (S <= 256 * NE).
-template <int NE>
-__global__ __launch_bounds__(256) void k_f32_attn_softmax(float* __restrict__ sc, float* __restrict__ lse,
-                                                          const uint32_t* __restrict__ mask, int S, float scale,
-                                                          float dscale) {
-  __shared__ float red[4];
-  const long row = blockIdx.x;
-  const int q = (int)(row % S);
-  const long bh = row / S;
-  float* r = sc + row * S;
-  const float c = scale * 1.44269504088896341f;
-  float x[NE];
-  float m = -INFINITY;
-#pragma unroll
-  for (int i = 0; i < NE; ++i) {
-    const int k = threadIdx.x + 256 * i;
-    x[i] = k <= q ? r[k] * c : -INFINITY;
-    m = fmaxf(m, x[i]);
-  }
-  m = f32_block_reduce<true>(m, red);  // finite: key 0 is always visible
-  float l = 0.f;
-#pragma unroll
-  for (int i = 0; i < NE; ++i) {
-    x[i] = exp2f(x[i] - m);
-    l += x[i];
-  }
-  l = f32_block_reduce<false>(l, red);
-  if (threadIdx.x == 0) lse[row] = (m + __log2f(l)) * 0.69314718055994531f;
-  const float inv = 1.f / l;
-  const uint32_t* mw = mask ? mask + bh * (long)((S + 31) >> 5) * S + q : nullptr;
-#pragma unroll
-  for (int i = 0; i < NE; ++i) {
-    const int k = threadIdx.x + 256 * i;
-    if (k >= S) break;
-    float p = 0.f;
-    if (k <= q) {
-      p = x[i] * inv;
-      if (mw) p = ((mw[(size_t)(k >> 5) * S] >> (k & 31)) & 1u) ? p * dscale : 0.f;
-    }
-    r[k] = p;
-  }
-}
-
-// backward: sc = recomputed scores q·k, dp = dO·vᵀ (the gradient of the dropped
-// probabilities), per (bh, q) row.  In place: sc <- the dropped probabilities (for
-// dV = Pdᵀ·dO), dp <- scale * p * (keep * dscale * dp - delta) (for dQ = dS·K, dK = dSᵀ·Q);
-// delta = rowsum(dO * O) from o / dO [B*S, nh*hd].
-__global__ __launch_bounds__(256) void k_f32_attn_dsoftmax(float* __restrict__ sc, float* __restrict__ dp,
-                                                           const float* __restrict__ lse, const float* __restrict__ o,
-                                                           const float* __restrict__ dO,
-                                                           const uint32_t* __restrict__ mask, int S, int nh, int hd,
-                                                           float scale, float dscale) {
-  __shared__ float red[4];
-  const long row = blockIdx.x;
-  const int q = (int)(row % S);
-  const long bh = row / S;
-  const long b = bh / nh, h = bh % nh;
-  const size_t orow = ((size_t)(b * S + q) * nh + h) * hd;
-  float dl = 0.f;
-  for (int d = threadIdx.x; d < hd; d += 256) dl = fmaf(o[orow + d], dO[orow + d], dl);
-  const float delta = f32_block_reduce<false>(dl, red);
-  const float ls = lse[row];
-  float* rs = sc + row * S;
-  float* rd = dp + row * S;
-  const uint32_t* mw = mask ? mask + bh * (long)((S + 31) >> 5) * S + q : nullptr;
-  for (int k = threadIdx.x; k < S; k += 256) {
-    float pd = 0.f, ds = 0.f;
-    if (k <= q) {
-      const float p = __expf(rs[k] * scale - ls);
-      float g = rd[k];
-      pd = p;
-      if (mw) {
-        const bool keep = (mw[(size_t)(k >> 5) * S] >> (k & 31)) & 1u;
-        pd = keep ? p * dscale : 0.f;
-        g = keep ? g * dscale : 0.f;
-      }
-      ds = p * (g - delta) * scale;
-    }
-    rs[k] = pd;
-    rd[k] = ds;
-  }
-}
-
 // ---------------------------------------------------------------- launchers
 static inline int f32_blocks(long n) {
   long b = (n + 255) / 256;
@@ -861,26 +746,3 @@ DLT_API int dlt_f32_attn_bwd(const float* q, const float* k, const float* v, lon
   DLT_CHECK_LAUNCH();
 }
 
-// sc [BH*S, S] in place; lse [BH*S]; S <= 4096
-DLT_API int dlt_f32_attn_softmax(float* sc, float* lse, const uint32_t* mask, int BH, int S, float scale, float dscale,
-                                 hipStream_t st) {
-  const long rows = (long)BH * S;
-  if (S <= 0 || S > 4096 || rows > 0x7fffffffL) return -1;
-  const int ne = (S + 255) / 256;
-  if (ne <= 1) k_f32_attn_softmax<1><<<rows, 256, 0, st>>>(sc, lse, mask, S, scale, dscale);
-  else if (ne <= 2) k_f32_attn_softmax<2><<<rows, 256, 0, st>>>(sc, lse, mask, S, scale, dscale);
-  else if (ne <= 4) k_f32_attn_softmax<4><<<rows, 256, 0, st>>>(sc, lse, mask, S, scale, dscale);
-  else if (ne <= 8) k_f32_attn_softmax<8><<<rows, 256, 0, st>>>(sc, lse, mask, S, scale, dscale);
-  else k_f32_attn_softmax<16><<<rows, 256, 0, st>>>(sc, lse, mask, S, scale, dscale);
-  DLT_CHECK_LAUNCH();
-}
-
-// sc / dp [B*nh*S, S] in place; o / dO [B*S, nh*hd]
-DLT_API int dlt_f32_attn_dsoftmax(float* sc, float* dp, const float* lse, const float* o, const float* dO,
-                                  const uint32_t* mask, int B, int nh, int S, int hd, float scale, float dscale,
-                                  hipStream_t st) {
-  const long rows = (long)B * nh * S;
-  if (S <= 0 || hd <= 0 || hd > 256 || rows > 0x7fffffffL) return -1;
-  k_f32_attn_dsoftmax<<<rows, 256, 0, st>>>(sc, dp, lse, o, dO, mask, S, nh, hd, scale, dscale);
-  DLT_CHECK_LAUNCH();
-}

@@ -37,6 +37,12 @@ SIGS = {
     "dlt_f32_attn_softmax": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_void_p],
     "dlt_f32_attn_dsoftmax": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                               c_float, c_float, c_void_p],
+    # 16-bit GEMM-formulated attention (csrc/attn_gemm.hip, used by ops/attn_gemm.py)
+    "dlt_attn16_softmax": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_int, c_void_p],
+    "dlt_attn16_dsoftmax": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                            c_int, c_int, c_float, c_float, c_int, c_void_p],
+    "dlt_relayout16": [c_void_p, c_void_p, c_long, c_long, c_long, c_long, c_long, c_long, c_long, c_long, c_int, c_int,
+                       c_int, c_int, c_int, c_void_p],
 }
 
 ATTN_HEAD_DIMS = (64, 128)
@@ -216,14 +222,17 @@ def _relayout(src, sstr, B, S, nh, hd, device, dst=None, dstr=None):
     return out
 
 
-def _bmm(kind, a, b):
+def _bmm(kind, a, b, out_dtype=None):
     """Batched row-major products over contiguous [..., r, c] operands: "nt" a @ b^T,
-    "nn" a @ b, "tn" a^T @ b.  torch.matmul (hipBLASLt's heuristic pick) by default;
-    BMM_PLANNER routes them through the autotuned planner of ops/gemm.py instead -- its
-    per-shape races run while the other chain's kernels share the GPU and picked slower
-    kernels in the step (profiles/r5_fp32_attention.md)."""
+    "nn" a @ b, "tn" a^T @ b, output in ``out_dtype`` (default: the operands').  fp32:
+    torch.matmul (hipBLASLt's heuristic pick) by default; BMM_PLANNER routes them through
+    the autotuned planner of ops/gemm.py instead -- its per-shape races run while the
+    other chain's kernels share the GPU and picked slower kernels in the step
+    (profiles/r5_fp32_attention.md).  16-bit operands always take the planner (fp32
+    scores from 16-bit operands are not a torch.matmul form)."""
     from . import gemm
-    if not (BMM_PLANNER and gemm.available()):
+    out_dtype = out_dtype or a.dtype
+    if a.dtype == torch.float32 and not (BMM_PLANNER and gemm.available()):
         a2 = a.transpose(-1, -2) if kind == "tn" else a
         return torch.matmul(a2, b.transpose(-1, -2) if kind == "nt" else b)
     *lead, ra, ca = a.shape
@@ -231,7 +240,7 @@ def _bmm(kind, a, b):
     bt = a.numel() // (ra * ca)
     M, K = (ca, ra) if kind == "tn" else (ra, ca)
     N = rb if kind == "nt" else cb
-    c = torch.empty(*lead, M, N, dtype=torch.float32, device=a.device)
+    c = torch.empty(*lead, M, N, dtype=out_dtype, device=a.device)
     sa, sb, sc = ra * ca, rb * cb, M * N
     if kind == "nt":    # C^T = op_T(B_c) . A_c
         gemm._gemm_batched(1, 0, N, M, K, b, cb, sb, a, ca, sa, c, N, sc, bt)

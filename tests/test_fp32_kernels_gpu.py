@@ -140,11 +140,13 @@ def test_fp32_training_runs_hip_kernels():
     assert all(l == l for l in losses) and losses[-1] < losses[0], losses
 
 
-@pytest.mark.parametrize("dt,hd", [(torch.bfloat16, 48), (torch.float16, 80), (torch.float32, 32)])
+@pytest.mark.parametrize("dt,hd", [(torch.bfloat16, 48), (torch.float16, 80), (torch.bfloat16, 40),
+                                   (torch.float32, 32)])
 def test_attn_gemm_odd_head_dims_vs_reference(dt, hd):
-    """ops/attn_gemm.py (head_dims without a flash kernel): 16-bit / fp32 packed QKV
-    through the fp32 GEMM formulation against the PyTorch reference attention (also fp32
-    arithmetic on the same inputs, same keep bits), forward + backward + inverse RoPE."""
+    """ops/attn_gemm.py (head_dims without a flash kernel) against the PyTorch reference
+    attention (fp32 arithmetic on the same inputs, same keep bits), forward + backward +
+    inverse RoPE: 16-bit GEMMs with fp32 scores for 16-bit head_dims % 16 == 0 (48, 80),
+    the fp32 formulation on widened inputs otherwise (40; fp32 32)."""
     from distributed_llm_trainer_amd.ops import attn_gemm
     torch.manual_seed(hd)
     B, nh, S, p = 2, 3, 200, 0.1
@@ -152,6 +154,7 @@ def test_attn_gemm_odd_head_dims_vs_reference(dt, hd):
     qkv = (torch.randn(B * S, 3 * H, device=DEV) * 0.5).to(dt)
     cos, sin = hip.rope_tables(hd, S, device=DEV)
     assert attn_gemm.fits(B, nh, S, hd)
+    assert attn_gemm.use16(dt, B, nh, S, hd) == (dt != torch.float32 and hd % 16 == 0)
     o, aux = attn_gemm.attention_fwd_packed(qkv, B, S, nh, p, 77)
     orf, lser = ref.attention_fwd_packed(qkv, B, S, nh, p, 77)
     assert o.dtype == dt
@@ -163,3 +166,21 @@ def test_attn_gemm_odd_head_dims_vs_reference(dt, hd):
     gr = ref.attention_bwd_packed(qkv, orf, do, lser, p, 77, B, S, nh, cos, sin)
     assert g.dtype == dt and g.shape == qkv.shape
     assert _rel(g, gr) < (5e-5 if dt == torch.float32 else 2e-2), _rel(g, gr)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_attn_gemm_16bit_head_major(dt):
+    """The head-major attn_gemm entry points on the 16-bit GEMM route (head_dim 96)."""
+    from distributed_llm_trainer_amd.ops import attn_gemm
+    torch.manual_seed(3)
+    B, nh, S, hd = 2, 2, 130, 96
+    q, k, v = ((torch.randn(B, nh, S, hd, device=DEV) * 0.5).to(dt) for _ in range(3))
+    assert attn_gemm.use16(dt, B, nh, S, hd)
+    o, aux = attn_gemm.attention_fwd(q, k, v, 0.1, 99)
+    orf, lser = ref.attention_fwd(q, k, v, 0.1, 99)
+    assert o.dtype == dt and _rel(o, orf) < 1e-2
+    do = torch.randn(B * S, nh * hd, device=DEV).to(dt)
+    got = attn_gemm.attention_bwd(q, k, v, o, do, aux, 0.1, 99)
+    want = ref.attention_bwd(q, k, v, orf, do, lser, 0.1, 99)
+    for a, b in zip(got, want):
+        assert a.dtype == dt and _rel(a, b) < 2e-2, _rel(a, b)
