@@ -45,6 +45,9 @@ def main():
     ap.add_argument("--mode", default="ddp", choices=["ddp", "fsdp"])
     ap.add_argument("--sharding", default="FULL_SHARD")
     ap.add_argument("--no_ac", action="store_true", help="FSDP: disable activation checkpointing")
+    ap.add_argument("--fsdp_defer_sync", action="store_true",
+                    help="FSDP: reduce-scatter once per optimizer step (full-size fp32 unit gradients kept "
+                         "across micro-steps, weight gradients deferred) instead of every micro-step")
     ap.add_argument("--cpu_offload", action="store_true",
                     help="FSDP: fp32 master shards + AdamW on the host (pinned), reduced grads staged D2H")
     ap.add_argument("--model_override", default="",
@@ -103,7 +106,7 @@ def main():
         tc = FSDPTrainingConfig(batch_size=args.batch_size, gradient_accumulation_steps=args.grad_accum,
                                 max_steps=100000, micro_step_fusion=args.fusion)
         fc = FSDPConfig(sharding_strategy=args.sharding, activation_checkpointing=not args.no_ac,
-                        cpu_offload=args.cpu_offload)
+                        cpu_offload=args.cpu_offload, sync_every_micro_step=not args.fsdp_defer_sync)
         trainer = FSDPTrainer(cfg, tc, fc)
     dev = trainer.device
     world = trainer.world_size
