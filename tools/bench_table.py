@@ -24,6 +24,9 @@ CONFIGS = {
     # head_dim 128 (6 heads of the small model's 768): the D = 128 MFMA attention kernels
     "ddp_small_hd128": ["--model_size", "small", "--batch_size", "8", "--grad_accum", "4",
                         "--model_override", "num_heads=6"],
+    # head_dim 96 (8 heads of 768): no flash kernel, attention as 16-bit GEMMs (ops/attn_gemm.py)
+    "ddp_small_hd96": ["--model_size", "small", "--batch_size", "8", "--grad_accum", "4",
+                       "--model_override", "num_heads=8"],
     "fsdp_small": ["--mode", "fsdp", "--model_size", "small", "--batch_size", "8", "--grad_accum", "4"],
     "ddp_medium": ["--model_size", "medium", "--batch_size", "4", "--grad_accum", "8"],
     "fsdp_medium": ["--mode", "fsdp", "--model_size", "medium", "--batch_size", "4", "--grad_accum", "8"],
