@@ -1,10 +1,15 @@
 """Attention for head_dims without a flash kernel (not 64 / 128), on native kernels.
 
 The reference accepts any ``hidden % heads == 0`` (``config.py:38-39``); the MFMA flash
-kernels exist for head_dim 64 and 128.  Any other head_dim runs attention as batched
-hipBLASLt GEMMs over the dense [S, S] scores around the row kernels of
-``csrc/attn_gemm.hip`` (causal softmax / its backward, the same dropout keep bits as every
-other path):
+kernels exist for head_dim 64 and 128.  Routes, first that applies:
+
+* 16-bit activations, head_dim < 128 (``PAD_FLASH``): the heads zero-padded to 64 / 128 and
+  the flash kernels run with the unpadded head_dim's score scale -- the zero columns add
+  nothing to q·k, P·V or the gradients, so this is exact; the padding costs
+  128 / head_dim in FLOPs (head_dim 96: 1.33x) plus the layout copies (``k_relayout16``).
+* else attention as batched hipBLASLt GEMMs over the dense [S, S] scores around the row
+  kernels of ``csrc/attn_gemm.hip`` (causal softmax / its backward, the same dropout keep
+  bits as every other path):
 
 * 16-bit activations, head_dim % 16 == 0: 16-bit MFMA GEMMs (through the autotuned planner,
   ``ops/gemm.py``) with fp32 scores and dO·Vᵀ, P / Pd / dS rounded to 16 bits as operands
@@ -21,12 +26,21 @@ dtype alone).
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
 from . import hip_f32, reference
 
 _HK = {torch.bfloat16: 0, torch.float16: 1}
+PAD_FLASH = os.environ.get("DLT_ATTN_PAD", "1") != "0"
+
+
+def pad_dim(dtype, hd: int):
+    """The flash head_dim a 16-bit head of ``hd`` is zero-padded to, or None."""
+    if not PAD_FLASH or dtype not in _HK or hd % 8:
+        return None
+    return 64 if hd < 64 else (128 if hd < 128 else None)
 
 
 def fits(B: int, nh: int, S: int, hd: int) -> bool:
@@ -51,6 +65,43 @@ def _heads16(t, B, S, nh, hd, n):
     out = torch.empty(n, B, nh, S, hd, dtype=t.dtype, device=t.device)
     _relayout16(t, (S * ld, ld, hd), out, (nh * S * hd, hd, S * hd), B, S, nh, hd, n, H, B * nh * S * hd)
     return out
+
+
+def _pad16(src, sstr, B, S, nh, hd, Dp, n, sts):
+    """n [b, s, h, d < hd] blocks of src -> zero-padded head-major [n, B, nh, S, Dp]."""
+    out = torch.zeros(n, B, nh, S, Dp, dtype=src.dtype, device=src.device)
+    _relayout16(src, sstr, out, (nh * S * Dp, Dp, S * Dp), B, S, nh, hd, n, sts, B * nh * S * Dp)
+    return out
+
+
+def _rows_padded(t, B, S, nh, hd, Dp):
+    """[B*S, nh*hd] -> zero-padded [B*S, nh*Dp]."""
+    out = torch.zeros(B * S, nh * Dp, dtype=t.dtype, device=t.device)
+    _relayout16(t.contiguous(), (S * nh * hd, nh * hd, hd), out, (S * nh * Dp, nh * Dp, Dp), B, S, nh, hd, 1)
+    return out
+
+
+def _fwd_pad(q4p, B, S, nh, hd, Dp, p, key, out, mask, store_mask, dt):
+    from . import hip
+    o_p, aux = hip.attention_fwd(q4p[0], q4p[1], q4p[2], p, key, True, store_mask=store_mask, mask=mask,
+                                 scale=1.0 / math.sqrt(hd))
+    H = nh * hd
+    o = torch.empty(B * S, H, dtype=dt, device=q4p.device) if out is None else out
+    if o.dtype != dt or not o.is_contiguous() or o.numel() != B * S * H:
+        raise ValueError("attn_gemm: out must be a contiguous [B*S, H] tensor of the activation dtype")
+    _relayout16(o_p, (S * nh * Dp, nh * Dp, Dp), o, (S * H, H, hd), B, S, nh, hd, 1)
+    return o, aux
+
+
+def _bwd_pad(q4p, o, do, aux, B, S, nh, hd, Dp, p, key):
+    """(dq, dk, dv) [3, B, nh, S, hd] from the padded flash backward."""
+    from . import hip
+    dq, dk, dv = hip.attention_bwd(q4p[0], q4p[1], q4p[2], _rows_padded(o, B, S, nh, hd, Dp),
+                                   _rows_padded(do, B, S, nh, hd, Dp), aux, p, key, scale=1.0 / math.sqrt(hd))
+    g = torch.empty(3, B, nh, S, hd, dtype=dq.dtype, device=dq.device)
+    for j, t in enumerate((dq, dk, dv)):
+        _relayout16(t, (nh * S * Dp, Dp, S * Dp), g[j], (nh * S * hd, hd, S * hd), B, S, nh, hd, 1)
+    return g
 
 
 def _fwd16(q4, k4, v4, B, nh, S, hd, p, key, out, mask, store_mask):
@@ -113,6 +164,11 @@ def _heads32(qkv, B, S, nh, hd):
 
 def attention_fwd_packed(qkv, B, S, nh, p, key, out=None, mask=None, store_mask=True):
     hd = qkv.shape[1] // (3 * nh)
+    Dp = pad_dim(qkv.dtype, hd)
+    if Dp:
+        ld = qkv.stride(0)
+        q4p = _pad16(qkv, (S * ld, ld, hd), B, S, nh, hd, Dp, 3, nh * hd)
+        return _fwd_pad(q4p, B, S, nh, hd, Dp, p, key, out, mask, store_mask, qkv.dtype)
     if use16(qkv.dtype, B, nh, S, hd):
         q4, k4, v4 = _heads16(qkv, B, S, nh, hd, 3)
         return _fwd16(q4, k4, v4, B, nh, S, hd, p, key, out, mask, store_mask)
@@ -126,6 +182,17 @@ def attention_fwd_packed(qkv, B, S, nh, p, key, out=None, mask=None, store_mask=
 
 def attention_bwd_packed(qkv, o, do, aux, p, key, B, S, nh, cos, sin, out=None):
     hd = qkv.shape[1] // (3 * nh)
+    Dp = pad_dim(qkv.dtype, hd)
+    if Dp:
+        from . import hip
+        ld = qkv.stride(0)
+        q4p = _pad16(qkv, (S * ld, ld, hd), B, S, nh, hd, Dp, 3, nh * hd)
+        g = _bwd_pad(q4p, o, do, aux, B, S, nh, hd, Dp, p, key)
+        del q4p
+        if hd % 16 == 0:
+            return hip.rope_qkv_bwd(g[0], g[1], g[2], cos, sin, out=out)
+        res = reference.rope_qkv_bwd(g[0], g[1], g[2], cos, sin)
+        return res if out is None else out.copy_(res)
     if use16(qkv.dtype, B, nh, S, hd):
         from . import hip
         q4, k4, v4 = _heads16(qkv, B, S, nh, hd, 3)
@@ -145,6 +212,11 @@ def attention_fwd(q, k, v, p, key, causal=True, store_mask=True, out=None, mask=
     if not causal:
         raise NotImplementedError("only causal attention is implemented (the model is a causal LM)")
     B, nh, S, hd = q.shape
+    Dp = pad_dim(q.dtype, hd)
+    if Dp:
+        hm = (nh * S * hd, hd, S * hd)
+        q4p = torch.stack([_pad16(t.contiguous(), hm, B, S, nh, hd, Dp, 1, 0)[0] for t in (q, k, v)])
+        return _fwd_pad(q4p, B, S, nh, hd, Dp, p, key, out, mask, store_mask, q.dtype)
     if use16(q.dtype, B, nh, S, hd):
         return _fwd16(q.contiguous(), k.contiguous(), v.contiguous(), B, nh, S, hd, p, key, out, mask, store_mask)
     if not fits(B, nh, S, hd):
@@ -156,6 +228,11 @@ def attention_fwd(q, k, v, p, key, causal=True, store_mask=True, out=None, mask=
 
 def attention_bwd(q, k, v, o, do, aux, p, key, causal=True):
     B, nh, S, hd = q.shape
+    Dp = pad_dim(q.dtype, hd)
+    if Dp:
+        hm = (nh * S * hd, hd, S * hd)
+        q4p = torch.stack([_pad16(t.contiguous(), hm, B, S, nh, hd, Dp, 1, 0)[0] for t in (q, k, v)])
+        return tuple(_bwd_pad(q4p, o, do, aux, B, S, nh, hd, Dp, p, key).unbind(0))
     if use16(q.dtype, B, nh, S, hd):
         return _bwd16(q.contiguous(), k.contiguous(), v.contiguous(), o, do, aux, B, nh, S, hd, p, key)
     if not fits(B, nh, S, hd):

@@ -486,12 +486,16 @@ def attention_dropout_mask(B, nh, S, p, key, device=None):
     return mask
 
 
-def attention_fwd(q, k, v, p, key, causal=True, store_mask=True, out=None, mask=None):
+def attention_fwd(q, k, v, p, key, causal=True, store_mask=True, out=None, mask=None, scale=None):
     """Returns (o [B*S, nh*hd] bf16, aux).  With dropout on, the keep bits are written
     to a bitmask consumed by attention_bwd (no re-hashing in the backward); pass
-    ``mask`` from ``attention_dropout_mask`` to skip generating it here."""
+    ``mask`` from ``attention_dropout_mask`` to skip generating it here.  ``scale``:
+    the score scale (default 1/sqrt(hd); ops/attn_gemm.py runs zero-padded heads with
+    the unpadded head_dim's)."""
     if q.dtype == torch.float32:
         from . import hip_f32
+        if scale is not None:
+            raise NotImplementedError("fp32 attention: the score scale is 1/sqrt(head_dim)")
         return hip_f32.attention_fwd(q, k, v, p, key, causal, store_mask=store_mask, out=out, mask=mask)
     if not causal:
         raise NotImplementedError("only causal attention is implemented (the model is a causal LM)")
@@ -515,7 +519,8 @@ def attention_fwd(q, k, v, p, key, causal=True, store_mask=True, out=None, mask=
         # [0] row layout (lane = query), [1] transposed (lane = key) -- see attention.hip;
         # with store_mask=False it only lives for this call (the backward regenerates it)
         mask = torch.empty(2, B * nh, (S + 31) // 32, S, dtype=torch.int32, device=q.device)
-    _chk(lib().dlt_attn_fwd(_p(q), _p(k), _p(v), _p(o), _p(lse), _p(mask), B, nh, S, hd, 1.0 / math.sqrt(hd),
+    _chk(lib().dlt_attn_fwd(_p(q), _p(k), _p(v), _p(o), _p(lse), _p(mask), B, nh, S, hd,
+                            1.0 / math.sqrt(hd) if scale is None else float(scale),
                             key & 0xFFFFFFFF, thr, dscale, gen, hk, _stream()), "attn_fwd")
     return o, AttnAux((lse, mask if (store_mask or gen == 0) else None))
 
@@ -591,9 +596,11 @@ def attention_bwd_packed(qkv, o, do, aux, p, key, B, S, nh, cos, sin, out=None):
     return dqkv
 
 
-def attention_bwd(q, k, v, o, do, aux, p, key, causal=True):
+def attention_bwd(q, k, v, o, do, aux, p, key, causal=True, scale=None):
     if q.dtype == torch.float32:
         from . import hip_f32
+        if scale is not None:
+            raise NotImplementedError("fp32 attention: the score scale is 1/sqrt(head_dim)")
         return hip_f32.attention_bwd(q, k, v, o, do, aux, p, key, causal)
     B, nh, S, hd = q.shape
     n = B * nh * S * hd
@@ -615,7 +622,8 @@ def attention_bwd(q, k, v, o, do, aux, p, key, causal=True):
     dv = torch.empty_like(v)
     dscale = 1.0 / (1.0 - p) if thr else 1.0
     _chk(lib().dlt_attn_bwd(_p(q), _p(k), _p(v), _p(o), _p(do), _p(lse), _p(mask), _p(delta), _p(dq), _p(dk), _p(dv),
-                            B, nh, S, hd, 1.0 / math.sqrt(hd), dscale, hk, _stream()), "attn_bwd")
+                            B, nh, S, hd, 1.0 / math.sqrt(hd) if scale is None else float(scale), dscale, hk,
+                            _stream()), "attn_bwd")
     return dq, dk, dv
 
 

@@ -140,20 +140,24 @@ def test_fp32_training_runs_hip_kernels():
     assert all(l == l for l in losses) and losses[-1] < losses[0], losses
 
 
-@pytest.mark.parametrize("dt,hd", [(torch.bfloat16, 48), (torch.float16, 80), (torch.bfloat16, 40),
-                                   (torch.float32, 32)])
-def test_attn_gemm_odd_head_dims_vs_reference(dt, hd):
+@pytest.mark.parametrize("dt,hd,pad", [(torch.bfloat16, 48, True), (torch.float16, 80, True), (torch.bfloat16, 40, True),
+                                       (torch.bfloat16, 48, False), (torch.float16, 80, False),
+                                       (torch.bfloat16, 40, False), (torch.bfloat16, 160, True), (torch.float32, 32, True)])
+def test_attn_gemm_odd_head_dims_vs_reference(dt, hd, pad, monkeypatch):
     """ops/attn_gemm.py (head_dims without a flash kernel) against the PyTorch reference
     attention (fp32 arithmetic on the same inputs, same keep bits), forward + backward +
-    inverse RoPE: 16-bit GEMMs with fp32 scores for 16-bit head_dims % 16 == 0 (48, 80),
-    the fp32 formulation on widened inputs otherwise (40; fp32 32)."""
+    inverse RoPE, on every route: 16-bit heads zero-padded onto the flash kernels (pad,
+    head_dim < 128), 16-bit GEMMs with fp32 scores (head_dim % 16 == 0: 48, 80, 160), the
+    fp32 formulation on widened inputs (40 without padding; fp32 32)."""
     from distributed_llm_trainer_amd.ops import attn_gemm
+    monkeypatch.setattr(attn_gemm, "PAD_FLASH", pad)
     torch.manual_seed(hd)
     B, nh, S, p = 2, 3, 200, 0.1
     H = nh * hd
     qkv = (torch.randn(B * S, 3 * H, device=DEV) * 0.5).to(dt)
     cos, sin = hip.rope_tables(hd, S, device=DEV)
     assert attn_gemm.fits(B, nh, S, hd)
+    assert (attn_gemm.pad_dim(dt, hd) is not None) == (pad and dt != torch.float32 and hd < 128)
     assert attn_gemm.use16(dt, B, nh, S, hd) == (dt != torch.float32 and hd % 16 == 0)
     o, aux = attn_gemm.attention_fwd_packed(qkv, B, S, nh, p, 77)
     orf, lser = ref.attention_fwd_packed(qkv, B, S, nh, p, 77)
@@ -168,10 +172,12 @@ def test_attn_gemm_odd_head_dims_vs_reference(dt, hd):
     assert _rel(g, gr) < (5e-5 if dt == torch.float32 else 2e-2), _rel(g, gr)
 
 
-@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
-def test_attn_gemm_16bit_head_major(dt):
-    """The head-major attn_gemm entry points on the 16-bit GEMM route (head_dim 96)."""
+@pytest.mark.parametrize("dt,pad", [(torch.bfloat16, False), (torch.float16, False), (torch.bfloat16, True)])
+def test_attn_gemm_16bit_head_major(dt, pad, monkeypatch):
+    """The head-major attn_gemm entry points at head_dim 96: 16-bit GEMM route, and the
+    zero-padded flash route."""
     from distributed_llm_trainer_amd.ops import attn_gemm
+    monkeypatch.setattr(attn_gemm, "PAD_FLASH", pad)
     torch.manual_seed(3)
     B, nh, S, hd = 2, 2, 130, 96
     q, k, v = ((torch.randn(B, nh, S, hd, device=DEV) * 0.5).to(dt) for _ in range(3))

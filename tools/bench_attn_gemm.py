@@ -1,6 +1,6 @@
 """Attention for a head_dim without a flash kernel (default: bf16, head_dim 96, B16 nh8
-S1024): fwd + bwd time of the 16-bit GEMM route, the fp32-widened route and the PyTorch
-reference ops, with the head_dim-64 flash kernels at the same FLOPs per token for scale."""
+S1024): fwd + bwd time of the zero-padded flash route, the 16-bit GEMM route, the
+fp32-widened route and the PyTorch reference ops, with the head_dim-64 flash kernels at the same FLOPs per token for scale."""
 import argparse
 import os
 import sys
@@ -42,13 +42,16 @@ def main():
         o, aux = mod.attention_fwd_packed(qkv, B, S, nh, 0.1, 5)
         mod.attention_bwd_packed(qkv, o, do, aux, 0.1, 5, B, S, nh, cos, sin)
     fl = 4 * B * nh * S * S / 2 * hd * 3.5  # causal fwd + bwd (2.5x) FLOPs
+    tpad = timeit(lambda: step(attn_gemm))
+    attn_gemm.PAD_FLASH = False
     t16 = timeit(lambda: step(attn_gemm))
     use16 = attn_gemm.use16
     attn_gemm.use16 = lambda *x: False
     t32 = timeit(lambda: step(attn_gemm))
     attn_gemm.use16 = use16
     tref = timeit(lambda: step(reference), 3)
-    print(f"hd {hd}: 16-bit GEMMs {t16:8.1f} us ({fl / t16 / 1e6:6.1f} TF/s)  fp32-widened {t32:8.1f} us  "
+    print(f"hd {hd}: zero-padded flash {tpad:8.1f} us ({fl / tpad / 1e6:6.1f} TF/s)  "
+          f"16-bit GEMMs {t16:8.1f} us ({fl / t16 / 1e6:6.1f} TF/s)  fp32-widened {t32:8.1f} us  "
           f"reference ops {tref:8.1f} us", flush=True)
     nh64 = H // 64
     q64 = (torch.randn(B * S, 3 * nh64 * 64, device="cuda") * 0.5).bfloat16()
