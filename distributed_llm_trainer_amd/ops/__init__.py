@@ -54,9 +54,9 @@ def for_device(device, head_dim: int = 64, act_dtype=torch.bfloat16) -> types.Si
     kernels (``csrc/fp32.hip``; the ``hip`` wrappers dispatch on the tensor dtype).  The
     flash attention kernels take head_dim 64 and 128 in every precision; a model with
     another head_dim (the reference allows any ``hidden % heads == 0``, ``config.py:38-39``)
-    runs attention as GEMMs over the dense scores around HIP row kernels (``ops/attn_gemm.py``:
-    16-bit MFMA GEMMs with fp32 scores, or fp32 GEMMs on widened inputs;
-    ``attn_backend == "gemm"``, with a one-time warning) and its
+    runs attention on native kernels (``ops/attn_gemm.py``, ``attn_backend == "gemm"``, with
+    a one-time warning): 16-bit heads under 128 zero-padded onto the flash kernels, else
+    GEMMs over the dense scores around HIP row kernels) and its
     RoPE on the HIP kernel when that takes the head_dim (16-bit: head_dim % 16 == 0; fp32:
     even), else as PyTorch ops on the GPU; the norms, SwiGLU, cross-entropy, embedding,
     optimizer and GEMMs stay native."""
@@ -75,7 +75,7 @@ def for_device(device, head_dim: int = 64, act_dtype=torch.bfloat16) -> types.Si
             from . import attn_gemm
             rope_native = head_dim % (2 if act_dtype == torch.float32 else 16) == 0
             warnings.warn(f"head_dim {head_dim}: the HIP flash attention kernels take head_dim {native_hd}; attention "
-                          f"runs as batched GEMMs + HIP row kernels for this model (RoPE: "
+                          f"runs zero-padded on them or as batched GEMMs + HIP row kernels for this model (RoPE: "
                           f"{'HIP kernel' if rope_native else 'PyTorch ops'})")
             for f in _ATTN_FUNCS:
                 if not f.startswith("rope"):
