@@ -56,8 +56,7 @@ def for_device(device, head_dim: int = 64, act_dtype=torch.bfloat16) -> types.Si
     another head_dim (the reference allows any ``hidden % heads == 0``, ``config.py:38-39``)
     runs attention on native kernels (``ops/attn_gemm.py``, ``attn_backend == "gemm"``, with
     a one-time warning): 16-bit heads under 128 zero-padded onto the flash kernels, else
-    GEMMs over the dense scores around HIP row kernels) and its
-    RoPE on the HIP kernel when that takes the head_dim (16-bit: head_dim % 16 == 0; fp32:
+    GEMMs over the dense scores around HIP row kernels.  Its RoPE runs on the HIP kernel when that takes the head_dim (16-bit: head_dim % 16 == 0; fp32:
     even), else as PyTorch ops on the GPU; the norms, SwiGLU, cross-entropy, embedding,
     optimizer and GEMMs stay native."""
     dev = torch.device(device)
