@@ -408,3 +408,17 @@ def test_f32_attention_impl_choice(monkeypatch):
     monkeypatch.setattr(hip_f32, "ATTN_IMPL", "bogus")
     with pytest.raises(ValueError):
         hip_f32._use_gemm(1, 1, 64, 64)
+
+
+def test_attn_gemm_routes(monkeypatch):
+    """Head dims without a flash kernel: 16-bit heads under 128 (multiple of 8) pad to 64 / 128;
+    fp32, head_dim >= 128 and DLT_ATTN_PAD=0 do not pad; the GEMM formulation's shape limits."""
+    from distributed_llm_trainer_amd.ops import attn_gemm
+    monkeypatch.setattr(attn_gemm, "PAD_FLASH", True)
+    assert attn_gemm.pad_dim(torch.bfloat16, 32) == 64 and attn_gemm.pad_dim(torch.float16, 48) == 64
+    assert attn_gemm.pad_dim(torch.bfloat16, 96) == 128 and attn_gemm.pad_dim(torch.bfloat16, 80) == 128
+    assert attn_gemm.pad_dim(torch.bfloat16, 160) is None and attn_gemm.pad_dim(torch.float32, 96) is None
+    assert attn_gemm.pad_dim(torch.bfloat16, 36) is None  # not a multiple of 8
+    monkeypatch.setattr(attn_gemm, "PAD_FLASH", False)
+    assert attn_gemm.pad_dim(torch.bfloat16, 96) is None
+    assert attn_gemm.fits(16, 12, 1024, 96) and not attn_gemm.fits(1, 1, 8192, 96) and not attn_gemm.fits(1, 1, 64, 258)
