@@ -226,9 +226,8 @@ def _bmm(kind, a, b, out_dtype=None):
     """Batched row-major products over contiguous [..., r, c] operands: "nt" a @ b^T,
     "nn" a @ b, "tn" a^T @ b, output in ``out_dtype`` (default: the operands').  fp32:
     torch.matmul (hipBLASLt's heuristic pick) by default; BMM_PLANNER routes them through
-    the autotuned planner of ops/gemm.py instead -- its per-shape races run while the
-    other chain's kernels share the GPU and picked slower kernels in the step
-    (profiles/r5_fp32_attention.md).  16-bit operands always take the planner (fp32
+    the autotuned planner of ops/gemm.py instead (within 1 % of torch.matmul in the fp32
+    step, tools/ab/README.md).  16-bit operands always take the planner (fp32
     scores from 16-bit operands are not a torch.matmul form)."""
     from . import gemm
     out_dtype = out_dtype or a.dtype
