@@ -10,7 +10,9 @@
 // arithmetic: fp32 scores and softmax, P and dS rounded to 16 bits as MFMA operands.
 //
 //   * k_attn_softmax<NE, OT>   -- causal mask, softmax, lse (natural log) and dropout from
-//     the keep-bit words of k_dropout_bits (attention.hip), one 256-thread block per row
+//     the keep-bit words of k_dropout_bits (attention.hip), one 256-thread block per row;
+//     k_attn_softmax_w / k_attn_dsoftmax_w: one wave per row, 4 rows per workgroup, float4
+//     score accesses and wave-only reductions (no LDS, no barrier), for S % 4 == 0
 //   * k_attn_dsoftmax<OT>      -- P from lse, delta = rowsum(dO * O), the dropped P (for
 //     dV) and scale * dS (for dQ / dK)
 //   * k_relayout16             -- 16-bit [b, s, h, d] strided copy (packed QKV <-> head-major)
@@ -155,6 +157,127 @@ __global__ __launch_bounds__(256) void k_attn_dsoftmax(const float* sc, const fl
   }
 }
 
+// 4 consecutive values at p (float4 for fp32, one 8-byte store for 16-bit)
+template <int OT>
+__device__ __forceinline__ void a_st4(typename ATy<OT>::T* p, const float (&v)[4]) {
+  if constexpr (OT == 0) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    uint2 w;
+    w.x = (uint32_t)f2h<OT - 1>(v[0]) | ((uint32_t)f2h<OT - 1>(v[1]) << 16);
+    w.y = (uint32_t)f2h<OT - 1>(v[2]) | ((uint32_t)f2h<OT - 1>(v[3]) << 16);
+    *reinterpret_cast<uint2*>(p) = w;
+  }
+}
+
+// k_attn_softmax with one wave per row: lane l owns columns 4l + 256i (i < NV, S <= 256 NV,
+// S % 4 == 0); the 4 columns of a group share one keep-bit word.
+template <int NV, int OT>
+__global__ __launch_bounds__(256) void k_attn_softmax_w(const float* sc, typename ATy<OT>::T* pout,
+                                                        float* __restrict__ lse, const uint32_t* __restrict__ mask,
+                                                        long rows, int S, float scale, float dscale) {
+  const long row = blockIdx.x * 4L + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int lane = threadIdx.x & 63;
+  const int q = (int)(row % S);
+  const long bh = row / S;
+  const float* r = sc + row * S;
+  const float c = scale * 1.44269504088896341f;
+  float x[NV][4];
+  float m = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c0 = 4 * lane + 256 * i;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c0 <= q) v = *reinterpret_cast<const float4*>(r + c0);  // c0 <= q < S: the group is in the row
+    const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      x[i][e] = c0 + e <= q ? vv[e] * c : -INFINITY;
+      m = fmaxf(m, x[i][e]);
+    }
+  }
+  m = wave_max(m);  // finite: key 0 is always visible
+  float l = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      x[i][e] = exp2f(x[i][e] - m);
+      l += x[i][e];
+    }
+  l = wave_sum(l);
+  if (lane == 0) lse[row] = (m + __log2f(l)) * 0.69314718055994531f;
+  const float inv = 1.f / l;
+  const uint32_t* mw = mask ? mask + bh * (long)((S + 31) >> 5) * S + q : nullptr;
+  typename ATy<OT>::T* po = pout + row * S;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c0 = 4 * lane + 256 * i;
+    if (c0 >= S) break;
+    float p[4] = {0.f, 0.f, 0.f, 0.f};
+    if (c0 <= q) {
+      const uint32_t w = mw ? mw[(size_t)(c0 >> 5) * S] >> (c0 & 31) : ~0u;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float pe = x[i][e] * inv;
+        p[e] = mw ? (((w >> e) & 1u) ? pe * dscale : 0.f) : pe;
+      }
+    }
+    a_st4<OT>(po + c0, p);
+  }
+}
+
+// k_attn_dsoftmax with one wave per row (S % 4 == 0)
+template <int OT>
+__global__ __launch_bounds__(256) void k_attn_dsoftmax_w(const float* sc, const float* dp, typename ATy<OT>::T* pd_out,
+                                                         typename ATy<OT>::T* ds_out, const float* __restrict__ lse,
+                                                         const typename ATy<OT>::T* __restrict__ o,
+                                                         const typename ATy<OT>::T* __restrict__ dO,
+                                                         const uint32_t* __restrict__ mask, long rows, int S, int nh,
+                                                         int hd, float scale, float dscale) {
+  const long row = blockIdx.x * 4L + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int lane = threadIdx.x & 63;
+  const int q = (int)(row % S);
+  const long bh = row / S;
+  const long b = bh / nh, h = bh % nh;
+  const size_t orow = ((size_t)(b * S + q) * nh + h) * hd;
+  float dl = 0.f;
+  for (int d = lane; d < hd; d += 64) dl = fmaf(a_ld<OT>(o, orow + d), a_ld<OT>(dO, orow + d), dl);
+  const float delta = wave_sum(dl);
+  const float ls = lse[row];
+  const float* rs = sc + row * S;
+  const float* rd = dp + row * S;
+  typename ATy<OT>::T* wp = pd_out + row * S;
+  typename ATy<OT>::T* wd = ds_out + row * S;
+  const uint32_t* mw = mask ? mask + bh * (long)((S + 31) >> 5) * S + q : nullptr;
+  for (int c0 = 4 * lane; c0 < S; c0 += 256) {
+    float pd[4] = {0.f, 0.f, 0.f, 0.f}, ds[4] = {0.f, 0.f, 0.f, 0.f};
+    if (c0 <= q) {
+      const float4 s4 = *reinterpret_cast<const float4*>(rs + c0), g4 = *reinterpret_cast<const float4*>(rd + c0);
+      const float sv[4] = {s4.x, s4.y, s4.z, s4.w}, gv[4] = {g4.x, g4.y, g4.z, g4.w};
+      const uint32_t w = mw ? mw[(size_t)(c0 >> 5) * S] >> (c0 & 31) : ~0u;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (c0 + e > q) break;
+        const float p = __expf(sv[e] * scale - ls);
+        float g = gv[e];
+        float pe = p;
+        if (mw) {
+          const bool keep = (w >> e) & 1u;
+          pe = keep ? p * dscale : 0.f;
+          g = keep ? g * dscale : 0.f;
+        }
+        pd[e] = pe;
+        ds[e] = p * (g - delta) * scale;
+      }
+    }
+    a_st4<OT>(wp + c0, pd);
+    a_st4<OT>(wd + c0, ds);
+  }
+}
+
 // 16-bit strided copy of ntens tensors: element (b, s, h, d) of tensor t at
 // src + t*sts + b*sb + s*sr + h*sh + d -> dst + t*dts + b*db + s*dr + h*dh + d.  Grid x:
 // (head, chunk of V elements) of a row, grid y strides over the B*S rows.  V = 8: 16-byte
@@ -180,6 +303,16 @@ __global__ __launch_bounds__(256) void k_relayout16(const uint16_t* __restrict__
   }
 }
 
+// DLT_ATTN_ROW_WAVE=0: the block-per-row kernels for every S (A/B)
+static bool row_w_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DLT_ATTN_ROW_WAVE");
+    v = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  return v == 1;
+}
+
 template <int OT>
 static int softmax_launch(float* sc, void* pout, float* lse, const uint32_t* mask, int BH, int S, float scale,
                           float dscale, hipStream_t st) {
@@ -188,6 +321,15 @@ static int softmax_launch(float* sc, void* pout, float* lse, const uint32_t* mas
   using T = typename ATy<OT>::T;
   T* po = static_cast<T*>(pout);
   const int ne = (S + 255) / 256;
+  if (S % 4 == 0 && row_w_enabled()) {  // wave per row (the 16-bit rows are 8-byte aligned: S % 4 == 0)
+    const unsigned nb = (unsigned)((rows + 3) / 4);
+    if (ne <= 1) k_attn_softmax_w<1, OT><<<nb, 256, 0, st>>>(sc, po, lse, mask, rows, S, scale, dscale);
+    else if (ne <= 2) k_attn_softmax_w<2, OT><<<nb, 256, 0, st>>>(sc, po, lse, mask, rows, S, scale, dscale);
+    else if (ne <= 4) k_attn_softmax_w<4, OT><<<nb, 256, 0, st>>>(sc, po, lse, mask, rows, S, scale, dscale);
+    else if (ne <= 8) k_attn_softmax_w<8, OT><<<nb, 256, 0, st>>>(sc, po, lse, mask, rows, S, scale, dscale);
+    else k_attn_softmax_w<16, OT><<<nb, 256, 0, st>>>(sc, po, lse, mask, rows, S, scale, dscale);
+    return 0;
+  }
   if (ne <= 1) k_attn_softmax<1, OT><<<rows, 256, 0, st>>>(sc, po, lse, mask, S, scale, dscale);
   else if (ne <= 2) k_attn_softmax<2, OT><<<rows, 256, 0, st>>>(sc, po, lse, mask, S, scale, dscale);
   else if (ne <= 4) k_attn_softmax<4, OT><<<rows, 256, 0, st>>>(sc, po, lse, mask, S, scale, dscale);
@@ -203,6 +345,12 @@ static int dsoftmax_launch(const float* sc, const float* dp, void* pd_out, void*
   const long rows = (long)B * nh * S;
   if (S <= 0 || hd <= 0 || hd > 256 || rows > 0x7fffffffL) return -1;
   using T = typename ATy<OT>::T;
+  if (S % 4 == 0 && row_w_enabled()) {
+    k_attn_dsoftmax_w<OT><<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(
+        sc, dp, static_cast<T*>(pd_out), static_cast<T*>(ds_out), lse, static_cast<const T*>(o),
+        static_cast<const T*>(dO), mask, rows, S, nh, hd, scale, dscale);
+    return 0;
+  }
   k_attn_dsoftmax<OT><<<rows, 256, 0, st>>>(sc, dp, static_cast<T*>(pd_out), static_cast<T*>(ds_out), lse,
                                             static_cast<const T*>(o), static_cast<const T*>(dO), mask, S, nh, hd, scale,
                                             dscale);
