@@ -109,13 +109,22 @@ def _fwd16(q4, k4, v4, B, nh, S, hd, p, key, out, mask, store_mask):
     H = nh * hd
     lse = torch.empty(B, nh, S, dtype=torch.float32, device=dev)
     mask, dscale = hip_f32._mask(B, nh, S, p, key, dev, mask)
-    sc = hip_f32._bmm("nt", q4, k4, torch.float32)
+    T, BH = hip_f32.attn_blocks(S), B * nh
+    if T > 1:
+        sc = torch.empty(B, nh, S, S, dtype=torch.float32, device=dev)
+        hip_f32.blocked_scores(q4.reshape(BH, S, hd), k4.reshape(BH, S, hd), sc.view(BH, S, S), T, S, hd)
+    else:
+        sc = hip_f32._bmm("nt", q4, k4, torch.float32)
     pm = torch.empty(B, nh, S, S, dtype=dt, device=dev)
     hip_f32._chk(hip_f32._lib().dlt_attn16_softmax(hip_f32._p(sc), hip_f32._p(pm), hip_f32._p(lse), hip_f32._p(mask),
-                                                   B * nh, S, 1.0 / math.sqrt(hd), dscale, _HK[dt], hip_f32._st()),
-                 "attn16_softmax")
+                                                   BH, S, 1.0 / math.sqrt(hd), dscale, S // T if T > 1 else 0,
+                                                   _HK[dt], hip_f32._st()), "attn16_softmax")
     del sc
-    o4 = hip_f32._bmm("nn", pm, v4)
+    if T > 1:
+        o4 = torch.empty(B, nh, S, hd, dtype=dt, device=dev)
+        hip_f32.blocked_rows(pm.view(BH, S, S), v4.reshape(BH, S, hd), o4.view(BH, S, hd), T, S, hd)
+    else:
+        o4 = hip_f32._bmm("nn", pm, v4)
     del pm
     o = torch.empty(B * S, H, dtype=dt, device=dev) if out is None else out
     if o.dtype != dt or not o.is_contiguous() or o.numel() != B * S * H:
@@ -131,14 +140,30 @@ def _bwd16(q4, k4, v4, o, do, aux, B, nh, S, hd, p, key):
     o, do = o.contiguous(), do.contiguous()
     mask, dscale = hip_f32._mask(B, nh, S, p, key, dev, mask)
     do4 = _heads16(do, B, S, nh, hd, 1)[0]
-    sc = hip_f32._bmm("nt", q4, k4, torch.float32)
-    dp = hip_f32._bmm("nt", do4, v4, torch.float32)
+    T, BH = hip_f32.attn_blocks(S), B * nh
+    q3, k3, v3, do3 = (t.reshape(BH, S, hd) for t in (q4, k4, v4, do4))
+    if T > 1:
+        sc = torch.empty(B, nh, S, S, dtype=torch.float32, device=dev)
+        dp = torch.empty_like(sc)
+        hip_f32.blocked_scores(q3, k3, sc.view(BH, S, S), T, S, hd)
+        hip_f32.blocked_scores(do3, v3, dp.view(BH, S, S), T, S, hd)
+    else:
+        sc = hip_f32._bmm("nt", q4, k4, torch.float32)
+        dp = hip_f32._bmm("nt", do4, v4, torch.float32)
     pd = torch.empty(B, nh, S, S, dtype=dt, device=dev)
     ds = torch.empty_like(pd)
     hip_f32._chk(hip_f32._lib().dlt_attn16_dsoftmax(
         hip_f32._p(sc), hip_f32._p(dp), hip_f32._p(pd), hip_f32._p(ds), hip_f32._p(lse), hip_f32._p(o), hip_f32._p(do),
-        hip_f32._p(mask), B, nh, S, hd, 1.0 / math.sqrt(hd), dscale, _HK[dt], hip_f32._st()), "attn16_dsoftmax")
+        hip_f32._p(mask), B, nh, S, hd, 1.0 / math.sqrt(hd), dscale, S // T if T > 1 else 0, _HK[dt],
+        hip_f32._st()), "attn16_dsoftmax")
     del sc, dp
+    if T > 1:
+        dq, dk, dv = (torch.empty(B, nh, S, hd, dtype=dt, device=dev) for _ in range(3))
+        hip_f32.blocked_cols(pd.view(BH, S, S), do3, dv.view(BH, S, hd), T, S, hd)
+        del pd
+        hip_f32.blocked_rows(ds.view(BH, S, S), k3, dq.view(BH, S, hd), T, S, hd)
+        hip_f32.blocked_cols(ds.view(BH, S, S), q3, dk.view(BH, S, hd), T, S, hd)
+        return dq, dk, dv
     dv = hip_f32._bmm("tn", pd, do4)
     del pd
     return hip_f32._bmm("nn", ds, k4), hip_f32._bmm("tn", ds, q4), dv

@@ -72,11 +72,12 @@ __device__ __forceinline__ float ag_block_reduce(float v, float* red) {
 template <int NE, int OT>
 __global__ __launch_bounds__(256) void k_attn_softmax(const float* sc, typename ATy<OT>::T* pout,
                                                       float* __restrict__ lse, const uint32_t* __restrict__ mask,
-                                                      int S, float scale, float dscale) {
+                                                      int S, float scale, float dscale, int Lb) {
   __shared__ float red[4];
   const long row = blockIdx.x;
   const int q = (int)(row % S);
   const long bh = row / S;
+  const int wl = Lb > 0 ? min(S, (q / Lb + 1) * Lb) : S;  // columns the blocked GEMMs read
   const float* r = sc + row * S;
   const float c = scale * 1.44269504088896341f;
   float x[NE];
@@ -102,7 +103,7 @@ __global__ __launch_bounds__(256) void k_attn_softmax(const float* sc, typename 
 #pragma unroll
   for (int i = 0; i < NE; ++i) {
     const int k = threadIdx.x + 256 * i;
-    if (k >= S) break;
+    if (k >= wl) break;
     float p = 0.f;
     if (k <= q) {
       p = x[i] * inv;
@@ -123,7 +124,7 @@ __global__ __launch_bounds__(256) void k_attn_dsoftmax(const float* sc, const fl
                                                        const typename ATy<OT>::T* __restrict__ o,
                                                        const typename ATy<OT>::T* __restrict__ dO,
                                                        const uint32_t* __restrict__ mask, int S, int nh, int hd,
-                                                       float scale, float dscale) {
+                                                       float scale, float dscale, int Lb) {
   __shared__ float red[4];
   const long row = blockIdx.x;
   const int q = (int)(row % S);
@@ -139,7 +140,8 @@ __global__ __launch_bounds__(256) void k_attn_dsoftmax(const float* sc, const fl
   typename ATy<OT>::T* wp = pd_out + row * S;
   typename ATy<OT>::T* wd = ds_out + row * S;
   const uint32_t* mw = mask ? mask + bh * (long)((S + 31) >> 5) * S + q : nullptr;
-  for (int k = threadIdx.x; k < S; k += 256) {
+  const int wl = Lb > 0 ? min(S, (q / Lb + 1) * Lb) : S;
+  for (int k = threadIdx.x; k < wl; k += 256) {
     float pd = 0.f, ds = 0.f;
     if (k <= q) {
       const float p = __expf(rs[k] * scale - ls);
@@ -175,7 +177,7 @@ __device__ __forceinline__ void a_st4(typename ATy<OT>::T* p, const float (&v)[4
 template <int NV, int OT>
 __global__ __launch_bounds__(256) void k_attn_softmax_w(const float* sc, typename ATy<OT>::T* pout,
                                                         float* __restrict__ lse, const uint32_t* __restrict__ mask,
-                                                        long rows, int S, float scale, float dscale) {
+                                                        long rows, int S, float scale, float dscale, int Lb) {
   const long row = blockIdx.x * 4L + (threadIdx.x >> 6);
   if (row >= rows) return;
   const int lane = threadIdx.x & 63;
@@ -214,7 +216,7 @@ __global__ __launch_bounds__(256) void k_attn_softmax_w(const float* sc, typenam
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c0 = 4 * lane + 256 * i;
-    if (c0 >= S) break;
+    if (c0 >= (Lb > 0 ? min(S, (q / Lb + 1) * Lb) : S)) break;
     float p[4] = {0.f, 0.f, 0.f, 0.f};
     if (c0 <= q) {
       const uint32_t w = mw ? mw[(size_t)(c0 >> 5) * S] >> (c0 & 31) : ~0u;
@@ -235,7 +237,7 @@ __global__ __launch_bounds__(256) void k_attn_dsoftmax_w(const float* sc, const 
                                                          const typename ATy<OT>::T* __restrict__ o,
                                                          const typename ATy<OT>::T* __restrict__ dO,
                                                          const uint32_t* __restrict__ mask, long rows, int S, int nh,
-                                                         int hd, float scale, float dscale) {
+                                                         int hd, float scale, float dscale, int Lb) {
   const long row = blockIdx.x * 4L + (threadIdx.x >> 6);
   if (row >= rows) return;
   const int lane = threadIdx.x & 63;
@@ -252,7 +254,8 @@ __global__ __launch_bounds__(256) void k_attn_dsoftmax_w(const float* sc, const 
   typename ATy<OT>::T* wp = pd_out + row * S;
   typename ATy<OT>::T* wd = ds_out + row * S;
   const uint32_t* mw = mask ? mask + bh * (long)((S + 31) >> 5) * S + q : nullptr;
-  for (int c0 = 4 * lane; c0 < S; c0 += 256) {
+  const int wl = Lb > 0 ? min(S, (q / Lb + 1) * Lb) : S;
+  for (int c0 = 4 * lane; c0 < wl; c0 += 256) {
     float pd[4] = {0.f, 0.f, 0.f, 0.f}, ds[4] = {0.f, 0.f, 0.f, 0.f};
     if (c0 <= q) {
       const float4 s4 = *reinterpret_cast<const float4*>(rs + c0), g4 = *reinterpret_cast<const float4*>(rd + c0);
@@ -315,68 +318,70 @@ static bool row_w_enabled() {
 
 template <int OT>
 static int softmax_launch(float* sc, void* pout, float* lse, const uint32_t* mask, int BH, int S, float scale,
-                          float dscale, hipStream_t st) {
+                          float dscale, int Lb, hipStream_t st) {
   const long rows = (long)BH * S;
-  if (S <= 0 || S > 4096 || rows > 0x7fffffffL) return -1;
+  if (S <= 0 || S > 4096 || rows > 0x7fffffffL || Lb < 0 || Lb % 4) return -1;
   using T = typename ATy<OT>::T;
   T* po = static_cast<T*>(pout);
   const int ne = (S + 255) / 256;
   if (S % 4 == 0 && row_w_enabled()) {  // wave per row (the 16-bit rows are 8-byte aligned: S % 4 == 0)
     const unsigned nb = (unsigned)((rows + 3) / 4);
-    if (ne <= 1) k_attn_softmax_w<1, OT><<<nb, 256, 0, st>>>(sc, po, lse, mask, rows, S, scale, dscale);
-    else if (ne <= 2) k_attn_softmax_w<2, OT><<<nb, 256, 0, st>>>(sc, po, lse, mask, rows, S, scale, dscale);
-    else if (ne <= 4) k_attn_softmax_w<4, OT><<<nb, 256, 0, st>>>(sc, po, lse, mask, rows, S, scale, dscale);
-    else if (ne <= 8) k_attn_softmax_w<8, OT><<<nb, 256, 0, st>>>(sc, po, lse, mask, rows, S, scale, dscale);
-    else k_attn_softmax_w<16, OT><<<nb, 256, 0, st>>>(sc, po, lse, mask, rows, S, scale, dscale);
+    if (ne <= 1) k_attn_softmax_w<1, OT><<<nb, 256, 0, st>>>(sc, po, lse, mask, rows, S, scale, dscale, Lb);
+    else if (ne <= 2) k_attn_softmax_w<2, OT><<<nb, 256, 0, st>>>(sc, po, lse, mask, rows, S, scale, dscale, Lb);
+    else if (ne <= 4) k_attn_softmax_w<4, OT><<<nb, 256, 0, st>>>(sc, po, lse, mask, rows, S, scale, dscale, Lb);
+    else if (ne <= 8) k_attn_softmax_w<8, OT><<<nb, 256, 0, st>>>(sc, po, lse, mask, rows, S, scale, dscale, Lb);
+    else k_attn_softmax_w<16, OT><<<nb, 256, 0, st>>>(sc, po, lse, mask, rows, S, scale, dscale, Lb);
     return 0;
   }
-  if (ne <= 1) k_attn_softmax<1, OT><<<rows, 256, 0, st>>>(sc, po, lse, mask, S, scale, dscale);
-  else if (ne <= 2) k_attn_softmax<2, OT><<<rows, 256, 0, st>>>(sc, po, lse, mask, S, scale, dscale);
-  else if (ne <= 4) k_attn_softmax<4, OT><<<rows, 256, 0, st>>>(sc, po, lse, mask, S, scale, dscale);
-  else if (ne <= 8) k_attn_softmax<8, OT><<<rows, 256, 0, st>>>(sc, po, lse, mask, S, scale, dscale);
-  else k_attn_softmax<16, OT><<<rows, 256, 0, st>>>(sc, po, lse, mask, S, scale, dscale);
+  if (ne <= 1) k_attn_softmax<1, OT><<<rows, 256, 0, st>>>(sc, po, lse, mask, S, scale, dscale, Lb);
+  else if (ne <= 2) k_attn_softmax<2, OT><<<rows, 256, 0, st>>>(sc, po, lse, mask, S, scale, dscale, Lb);
+  else if (ne <= 4) k_attn_softmax<4, OT><<<rows, 256, 0, st>>>(sc, po, lse, mask, S, scale, dscale, Lb);
+  else if (ne <= 8) k_attn_softmax<8, OT><<<rows, 256, 0, st>>>(sc, po, lse, mask, S, scale, dscale, Lb);
+  else k_attn_softmax<16, OT><<<rows, 256, 0, st>>>(sc, po, lse, mask, S, scale, dscale, Lb);
   return 0;
 }
 
 template <int OT>
 static int dsoftmax_launch(const float* sc, const float* dp, void* pd_out, void* ds_out, const float* lse,
                            const void* o, const void* dO, const uint32_t* mask, int B, int nh, int S, int hd,
-                           float scale, float dscale, hipStream_t st) {
+                           float scale, float dscale, int Lb, hipStream_t st) {
   const long rows = (long)B * nh * S;
-  if (S <= 0 || hd <= 0 || hd > 256 || rows > 0x7fffffffL) return -1;
+  if (S <= 0 || hd <= 0 || hd > 256 || rows > 0x7fffffffL || Lb < 0 || Lb % 4) return -1;
   using T = typename ATy<OT>::T;
   if (S % 4 == 0 && row_w_enabled()) {
     k_attn_dsoftmax_w<OT><<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(
         sc, dp, static_cast<T*>(pd_out), static_cast<T*>(ds_out), lse, static_cast<const T*>(o),
-        static_cast<const T*>(dO), mask, rows, S, nh, hd, scale, dscale);
+        static_cast<const T*>(dO), mask, rows, S, nh, hd, scale, dscale, Lb);
     return 0;
   }
   k_attn_dsoftmax<OT><<<rows, 256, 0, st>>>(sc, dp, static_cast<T*>(pd_out), static_cast<T*>(ds_out), lse,
                                             static_cast<const T*>(o), static_cast<const T*>(dO), mask, S, nh, hd, scale,
-                                            dscale);
+                                            dscale, Lb);
   return 0;
 }
 
+// Lb (every entry point): the row-block size of blocked causal GEMMs -- a row q only
+// writes the columns below the end of its block, (q / Lb + 1) * Lb; 0: the whole row.
 // fp32: sc [BH*S, S] in place; lse [BH*S]; S <= 4096
 DLT_API int dlt_f32_attn_softmax(float* sc, float* lse, const uint32_t* mask, int BH, int S, float scale, float dscale,
-                                 hipStream_t st) {
-  if (softmax_launch<0>(sc, sc, lse, mask, BH, S, scale, dscale, st)) return -1;
+                                 int Lb, hipStream_t st) {
+  if (softmax_launch<0>(sc, sc, lse, mask, BH, S, scale, dscale, Lb, st)) return -1;
   DLT_CHECK_LAUNCH();
 }
 
 // fp32: sc / dp [B*nh*S, S] in place; o / dO [B*S, nh*hd]
 DLT_API int dlt_f32_attn_dsoftmax(float* sc, float* dp, const float* lse, const float* o, const float* dO,
                                   const uint32_t* mask, int B, int nh, int S, int hd, float scale, float dscale,
-                                  hipStream_t st) {
-  if (dsoftmax_launch<0>(sc, dp, sc, dp, lse, o, dO, mask, B, nh, S, hd, scale, dscale, st)) return -1;
+                                  int Lb, hipStream_t st) {
+  if (dsoftmax_launch<0>(sc, dp, sc, dp, lse, o, dO, mask, B, nh, S, hd, scale, dscale, Lb, st)) return -1;
   DLT_CHECK_LAUNCH();
 }
 
 // 16-bit (hk 0 bf16, 1 fp16): fp32 scores sc -> P into pout [BH*S, S]
 DLT_API int dlt_attn16_softmax(const float* sc, void* pout, float* lse, const uint32_t* mask, int BH, int S,
-                               float scale, float dscale, int hk, hipStream_t st) {
-  const int rc = hk ? softmax_launch<2>(const_cast<float*>(sc), pout, lse, mask, BH, S, scale, dscale, st)
-                    : softmax_launch<1>(const_cast<float*>(sc), pout, lse, mask, BH, S, scale, dscale, st);
+                               float scale, float dscale, int Lb, int hk, hipStream_t st) {
+  const int rc = hk ? softmax_launch<2>(const_cast<float*>(sc), pout, lse, mask, BH, S, scale, dscale, Lb, st)
+                    : softmax_launch<1>(const_cast<float*>(sc), pout, lse, mask, BH, S, scale, dscale, Lb, st);
   if (rc) return -1;
   DLT_CHECK_LAUNCH();
 }
@@ -384,9 +389,9 @@ DLT_API int dlt_attn16_softmax(const float* sc, void* pout, float* lse, const ui
 // 16-bit: fp32 sc / dp -> pd / ds [B*nh*S, S] (16-bit); o / dO [B*S, nh*hd] 16-bit
 DLT_API int dlt_attn16_dsoftmax(const float* sc, const float* dp, void* pd_out, void* ds_out, const float* lse,
                                 const void* o, const void* dO, const uint32_t* mask, int B, int nh, int S, int hd,
-                                float scale, float dscale, int hk, hipStream_t st) {
-  const int rc = hk ? dsoftmax_launch<2>(sc, dp, pd_out, ds_out, lse, o, dO, mask, B, nh, S, hd, scale, dscale, st)
-                    : dsoftmax_launch<1>(sc, dp, pd_out, ds_out, lse, o, dO, mask, B, nh, S, hd, scale, dscale, st);
+                                float scale, float dscale, int Lb, int hk, hipStream_t st) {
+  const int rc = hk ? dsoftmax_launch<2>(sc, dp, pd_out, ds_out, lse, o, dO, mask, B, nh, S, hd, scale, dscale, Lb, st)
+                    : dsoftmax_launch<1>(sc, dp, pd_out, ds_out, lse, o, dO, mask, B, nh, S, hd, scale, dscale, Lb, st);
   if (rc) return -1;
   DLT_CHECK_LAUNCH();
 }

@@ -34,13 +34,14 @@ SIGS = {
     "dlt_f32_attn_bwd": [c_void_p, c_void_p, c_void_p, c_long, c_long, c_long, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_long, c_long, c_int, c_int, c_int, c_int,
                          c_float, c_float, c_void_p],
-    "dlt_f32_attn_softmax": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_void_p],
+    "dlt_f32_attn_softmax": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_int, c_void_p],
     "dlt_f32_attn_dsoftmax": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                              c_float, c_float, c_void_p],
+                              c_float, c_float, c_int, c_void_p],
     # 16-bit GEMM-formulated attention (csrc/attn_gemm.hip, used by ops/attn_gemm.py)
-    "dlt_attn16_softmax": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_int, c_void_p],
+    "dlt_attn16_softmax": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_int, c_int,
+                           c_void_p],
     "dlt_attn16_dsoftmax": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
-                            c_int, c_int, c_float, c_float, c_int, c_void_p],
+                            c_int, c_int, c_float, c_float, c_int, c_int, c_void_p],
     "dlt_relayout16": [c_void_p, c_void_p, c_long, c_long, c_long, c_long, c_long, c_long, c_long, c_long, c_int, c_int,
                        c_int, c_int, c_int, c_void_p],
 }
@@ -55,6 +56,7 @@ ATTN_HEAD_DIMS = (64, 128)
 ATTN_IMPL = os.environ.get("DLT_F32_ATTN", "auto")
 GEMM_ATTN_BYTES = 16 << 30
 BMM_PLANNER = os.environ.get("DLT_F32_BMM", "torch") == "planner"
+ATTN_BLOCKS = int(os.environ.get("DLT_ATTN_BLOCKS", "4"))
 
 
 def _h():
@@ -250,6 +252,48 @@ def _bmm(kind, a, b, out_dtype=None):
     return c
 
 
+def attn_blocks(S: int) -> int:
+    """Row blocks T of the causal GEMMs (``DLT_ATTN_BLOCKS``, default 4; needs the planner):
+    query block i (S/T rows) multiplies only the keys below its end, so the products do
+    (T+1)/(2T) of the dense work (T = 4: 62.5 %) and the row kernels write only the columns
+    the next products read.  1 = dense."""
+    from . import gemm
+    T = ATTN_BLOCKS
+    while T > 1 and (S % (4 * T) or S // T < 64):
+        T //= 2
+    return T if T > 1 and gemm.available() else 1
+
+
+def _gb(kind, a, b, c, M, N, K, lda, ldb, ldc, sa, sb, scc, bt):
+    """One batched row-major product through the planner on (possibly offset) views:
+    "nt" C = A B^T, "nn" C = A B, "tn" C = A^T B; leading dims / batch strides explicit."""
+    from . import gemm
+    ta, tb = {"nt": (1, 0), "nn": (0, 0), "tn": (0, 1)}[kind]
+    gemm._gemm_batched(ta, tb, N, M, K, b, ldb, sb, a, lda, sa, c, ldc, scc, bt)
+
+
+def blocked_scores(x3, y3, out3, T, S, hd):
+    """out3[:, block i, :L_i] = x3[:, block i] @ y3[:, :L_i]^T (x3 / y3 [BH, S, hd], out3 [BH, S, S])."""
+    Sb, BH = S // T, x3.shape[0]
+    for i in range(T):
+        _gb("nt", x3[:, i * Sb:], y3, out3[:, i * Sb:], Sb, (i + 1) * Sb, hd, hd, hd, S, S * hd, S * hd, S * S, BH)
+
+
+def blocked_rows(p3, y3, out3, T, S, hd):
+    """out3[:, block i] = p3[:, block i, :L_i] @ y3[:, :L_i] (P.V, dS.K)."""
+    Sb, BH = S // T, p3.shape[0]
+    for i in range(T):
+        _gb("nn", p3[:, i * Sb:], y3, out3[:, i * Sb:], Sb, hd, (i + 1) * Sb, S, hd, hd, S * S, S * hd, S * hd, BH)
+
+
+def blocked_cols(p3, y3, out3, T, S, hd):
+    """out3[:, block j] = p3[:, j*Sb:, block j]^T @ y3[:, j*Sb:] (Pd^T.dO, dS^T.Q)."""
+    Sb, BH = S // T, p3.shape[0]
+    for j in range(T):
+        _gb("tn", p3[:, j * Sb:, j * Sb:], y3[:, j * Sb:], out3[:, j * Sb:], Sb, hd, S - j * Sb, S, hd, hd, S * S,
+            S * hd, S * hd, BH)
+
+
 def _packed_ptrs(t, n, H):
     return [ctypes.c_void_p(t.data_ptr() + j * H * 4) for j in range(n)]
 
@@ -259,10 +303,19 @@ def _gemm_fwd(q4, k4, v4, B, nh, S, hd, p, key, device, out, mask, store_mask):
     _req32(o, "attn_f32.o", B * S * nh * hd)
     lse = torch.empty(B, nh, S, dtype=torch.float32, device=device)
     mask, dscale = _mask(B, nh, S, p, key, device, mask)
-    sc = _bmm("nt", q4, k4)
-    _chk(_lib().dlt_f32_attn_softmax(_p(sc), _p(lse), _p(mask), B * nh, S, 1.0 / math.sqrt(hd), dscale, _st()),
-         "f32_attn_softmax")
-    o4 = _bmm("nn", sc, v4)
+    T, BH = attn_blocks(S), B * nh
+    if T > 1:
+        sc = torch.empty(B, nh, S, S, dtype=torch.float32, device=device)
+        blocked_scores(q4.view(BH, S, hd), k4.view(BH, S, hd), sc.view(BH, S, S), T, S, hd)
+    else:
+        sc = _bmm("nt", q4, k4)
+    _chk(_lib().dlt_f32_attn_softmax(_p(sc), _p(lse), _p(mask), BH, S, 1.0 / math.sqrt(hd), dscale,
+                                     S // T if T > 1 else 0, _st()), "f32_attn_softmax")
+    if T > 1:
+        o4 = torch.empty(B, nh, S, hd, dtype=torch.float32, device=device)
+        blocked_rows(sc.view(BH, S, S), v4.view(BH, S, hd), o4.view(BH, S, hd), T, S, hd)
+    else:
+        o4 = _bmm("nn", sc, v4)
     del sc
     _relayout([_p(o4)], (nh * S * hd, hd, S * hd), B, S, nh, hd, device, [_p(o)], (S * nh * hd, nh * hd, hd))
     return o, _h().AttnAux((lse, mask if store_mask else None))
@@ -276,10 +329,25 @@ def _gemm_bwd(q4, k4, v4, o, do, aux, B, nh, S, hd, p, key, device):
     _req32(do, "attn_bwd_f32.do", B * S * nh * hd)
     mask, dscale = _mask(B, nh, S, p, key, device, mask)
     do4 = _relayout([_p(do)], (S * nh * hd, nh * hd, hd), B, S, nh, hd, device)[0]
-    sc = _bmm("nt", q4, k4)
-    dp = _bmm("nt", do4, v4)
+    T, BH = attn_blocks(S), B * nh
+    if T > 1:
+        q3, k3, v3, do3 = (t.view(BH, S, hd) for t in (q4, k4, v4, do4))
+        sc = torch.empty(B, nh, S, S, dtype=torch.float32, device=device)
+        dp = torch.empty_like(sc)
+        blocked_scores(q3, k3, sc.view(BH, S, S), T, S, hd)
+        blocked_scores(do3, v3, dp.view(BH, S, S), T, S, hd)
+    else:
+        sc = _bmm("nt", q4, k4)
+        dp = _bmm("nt", do4, v4)
     _chk(_lib().dlt_f32_attn_dsoftmax(_p(sc), _p(dp), _p(lse), _p(o), _p(do), _p(mask), B, nh, S, hd,
-                                      1.0 / math.sqrt(hd), dscale, _st()), "f32_attn_dsoftmax")
+                                      1.0 / math.sqrt(hd), dscale, S // T if T > 1 else 0, _st()), "f32_attn_dsoftmax")
+    if T > 1:
+        dq, dk, dv = (torch.empty(B, nh, S, hd, dtype=torch.float32, device=device) for _ in range(3))
+        blocked_cols(sc.view(BH, S, S), do3, dv.view(BH, S, hd), T, S, hd)
+        del sc
+        blocked_rows(dp.view(BH, S, S), k3, dq.view(BH, S, hd), T, S, hd)
+        blocked_cols(dp.view(BH, S, S), q3, dk.view(BH, S, hd), T, S, hd)
+        return dq, dk, dv
     dv = _bmm("tn", sc, do4)
     del sc
     dq = _bmm("nn", dp, k4)

@@ -53,12 +53,12 @@ def main():
     mask = hip.attention_dropout_mask(B, nh, S, 0.1, 7, device=dev)
     L = hip_f32._lib()
     row("attn softmax", timeit(lambda: L.dlt_f32_attn_softmax(hip_f32._p(sc), hip_f32._p(lse), hip_f32._p(mask), B * nh, S,
-                                                              0.125, 1 / 0.9, hip_f32._st())), sc.numel() * 8)
+                                                              0.125, 1 / 0.9, 0, hip_f32._st())), sc.numel() * 8)
     dp = torch.randn_like(sc)
     o, do = torch.randn(M, H, device=dev), torch.randn(M, H, device=dev)
     row("attn dsoftmax", timeit(lambda: L.dlt_f32_attn_dsoftmax(hip_f32._p(sc), hip_f32._p(dp), hip_f32._p(lse),
                                                                 hip_f32._p(o), hip_f32._p(do), hip_f32._p(mask), B, nh, S,
-                                                                hd, 0.125, 1 / 0.9, hip_f32._st())), sc.numel() * 16)
+                                                                hd, 0.125, 1 / 0.9, 0, hip_f32._st())), sc.numel() * 16)
     q4 = torch.randn(B, nh, S, hd, device=dev)
     row("bmm q.k^T (B*nh x S x S x hd)", timeit(lambda: torch.matmul(q4, q4.transpose(-1, -2))),
         2 * B * nh * S * S * hd / 1e3 * 1e6 / 1e6)  # "TB/s" column = TFLOP/s here
