@@ -220,6 +220,21 @@ __global__ __launch_bounds__(256) void k_f32_rope(F32QKV a, const float* __restr
   }
 }
 
+// The copy mode of k_f32_rope with float4 accesses: 4 consecutive elements of a head row per
+// thread (hd % 4 == 0, every stride a multiple of 4 elements, 16-byte aligned bases).
+__global__ __launch_bounds__(256) void k_f32_relayout4(F32QKV a, int B, int S, int nh, int hd, int ntens) {
+  const int per = hd >> 2;
+  const int t0 = blockIdx.x * 256 + threadIdx.x;
+  if (t0 >= nh * per) return;
+  const int h = t0 / per, j = (t0 - h * per) * 4;
+  for (int r = blockIdx.y; r < B * S; r += gridDim.y) {
+    const int b = r / S, s = r - b * S;
+    const long so = b * a.sb + s * a.sr + h * a.sh + j, dof = b * a.db + s * a.dr + h * a.dh + j;
+    for (int t = 0; t < ntens; ++t)
+      *reinterpret_cast<float4*>(a.dst[t] + dof) = *reinterpret_cast<const float4*>(a.src[t] + so);
+  }
+}
+
 // ----------------------------------------------------------------- SwiGLU
 // Grid x: V consecutive columns per thread (V = 4: float4 accesses, I % 4 == 0); grid y
 // strides over the rows.
@@ -673,6 +688,16 @@ DLT_API int dlt_f32_rope(const float* sq, const float* sk, const float* sv, floa
   if (hd % 2 || ntens < 1 || ntens > 3 || (cosT && ntens < 2)) return -1;
   F32QKV a{{sq, sk, sv}, {dq, dk, dv}, sb, sr, sh, db, dr, dh};
   if ((long)B * S > 0x7fffffffL) return -1;
+  if (!cosT) {  // plain layout copy: float4 when every address lines up
+    bool v4 = hd % 4 == 0;
+    for (long x : {sb, sr, sh, db, dr, dh}) v4 = v4 && x % 4 == 0;
+    for (int t = 0; t < ntens; ++t) v4 = v4 && ((uintptr_t)a.src[t] & 15) == 0 && ((uintptr_t)a.dst[t] & 15) == 0;
+    if (v4) {
+      const dim3 g4((nh * (hd / 4) + 255) / 256, B * S < 65535 ? B * S : 65535);
+      k_f32_relayout4<<<g4, 256, 0, st>>>(a, B, S, nh, hd, ntens);
+      DLT_CHECK_LAUNCH();
+    }
+  }
   const dim3 grid((nh * (hd / 2) + 255) / 256, B * S < 65535 ? B * S : 65535);
   k_f32_rope<<<grid, 256, 0, st>>>(a, cosT, sinT, B, S, nh, hd, sign, ntens);
   DLT_CHECK_LAUNCH();
