@@ -1126,9 +1126,14 @@ class GPTEngine:
         t = [a["events"][i].elapsed_time(a["events"][i + 1]) for i in range(n)]
         best = [min(t[i] for i in range(n) if self._AUTO_TRIALS[i] == k) for k in ("fb", "ffbb")]
         import torch.distributed as dist
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            v = torch.tensor(best, dtype=torch.float32, device=dev if dist.get_backend() == "nccl" else "cpu")
-            dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        # over the gradient collectives' own group (the DDP runtime's pg; FSDP, whose shard
+        # and replica groups together span every rank: None = WORLD): every rank of that
+        # group takes the same pipelined-window path, so all of them reach this reduction
+        # at the same point of their collective sequence
+        pg = getattr(getattr(self.provider, "hooks", None), "pg", None)
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size(pg) > 1:
+            v = torch.tensor(best, dtype=torch.float32, device=dev if dist.get_backend(pg) == "nccl" else "cpu")
+            dist.all_reduce(v, op=dist.ReduceOp.MAX, group=pg)
             best = v.tolist()
         fb, ffbb = (float(x) for x in best)
         a["decided"] = "ffbb" if ffbb < fb else "fb"

@@ -467,12 +467,6 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16(const bf16_t* __restrict__
     return BT ? B + (size_t)tn * TS : B + (size_t)(tn * TS) * ldb;
   };
 
-  // flags & 512 (ablation only): the workgroups of odd XCD-slot rows start (flags >> 24) x
-  // 1024 shader cycles late, so their tile epilogues fall between the others'
-  if ((flags & 512) && ((bid >> 3) & 1)) {
-    const uint64_t t0 = __builtin_amdgcn_s_memtime(), d = (uint64_t)((uint32_t)flags >> 24) << 10;
-    while (__builtin_amdgcn_s_memtime() - t0 < d) __builtin_amdgcn_s_sleep(2);
-  }
   // the next tile's first K-tiles, as the kernel prologue stages them (epilogue-first
   // staging, flags & 4096): K-tile 0 whole into buffer 0, A0 / B0 of K-tile 1 into buffer 1
   auto stage_next_of = [&](int t) {
@@ -894,12 +888,18 @@ static inline int gb_grid(int ntiles) {
   return (g + 7) & ~7;
 }
 
-// flags & 256: one tile per workgroup (grid = tiles, a multiple of 8) instead of the
-// persistent grid -- frees CUs between tiles when other streams run kernels alongside
+// flags & 256: bounded persistence -- each workgroup walks at most T = max(1, (flags >> 24)
+// & 15) tiles (grid = ceil(tiles / T), a multiple of 8) instead of one workgroup per CU
+// for the whole launch: workgroups end every T tiles and hand their CU back to the
+// dispatcher, so kernels of another stream get CUs while the GEMM runs (a persistent grid
+// holds its CUs for the whole launch).  T = 1: one tile per workgroup.
 // flags >> 16 (A/B knob): cap the persistent grid at 8 * (flags >> 16) workgroups, so
 // kernels of the other stream keep the remaining CUs
 static inline int gb_launch_grid(int ntiles, int flags) {
-  if (flags & 256) return (ntiles + 7) & ~7;
+  if (flags & 256) {
+    const int t = ((flags >> 24) & 15) ? ((flags >> 24) & 15) : 1;
+    return ((ntiles + t - 1) / t + 7) & ~7;
+  }
   const int g = gb_grid(ntiles), cap = 8 * ((flags >> 16) & 0xff);
   return cap && cap < g ? cap : g;
 }

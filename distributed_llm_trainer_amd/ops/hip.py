@@ -822,8 +822,9 @@ def gemm_wgrad_sk(dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, shares: i
 
 
 # ------------------------------------------------- projection GEMMs (csrc/gemm_bf16.hip)
-# launch flags of the hand projection GEMMs; DLT_GEMM_FLAGS bit 256 = one tile per
-# workgroup instead of the persistent grid; DLT_GEMM_GRID=n caps the persistent grid at n
+# launch flags of the hand projection GEMMs; DLT_GEMM_FLAGS bit 256 = bounded persistence
+# (each workgroup walks at most (flags >> 24) & 15 tiles, default 1, grid = tiles / that)
+# instead of the persistent grid; DLT_GEMM_GRID=n caps the persistent grid at n
 # (multiple of 8) workgroups (A/B knobs for overlapped schedules)
 # Production flags (round 4): 1024 = LDS-transposed C stores (whole 192-byte row
 # segments per store instruction: the plain epilogue's cycles -26 %), 12 = XCD row-band
@@ -832,7 +833,7 @@ def gemm_wgrad_sk(dw: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, shares: i
 # later K-iterations 6461 -> 4909 cycles); tools/cpp/gemm_stamps.cpp and
 # profiles/r4_gemm_forward.md.  DLT_GEMM_FLAGS=n replaces them (bits 256 / 1024 / 2048 / 12).
 _GB_DEFAULT_FLAGS = 2048 | 1024 | 12
-_GB_FLAG_BITS = 256 | 512 | 1024 | 2048 | 4096 | 12 | (0xff << 24)  # (512 + bits 24-31: start-delay ablation)
+_GB_FLAG_BITS = 256 | 1024 | 2048 | 4096 | 12 | (0xf << 24)  # (256 + bits 24-27: tiles per workgroup)
 _GB_FLAGS = (int(os.environ.get("DLT_GEMM_FLAGS", str(_GB_DEFAULT_FLAGS))) & _GB_FLAG_BITS) | \
     ((min(int(os.environ.get("DLT_GEMM_GRID", "0")), 2040) // 8) << 16)
 # launch flags of the FORWARD projection GEMMs only (plain / RoPE / SwiGLU epilogues),

@@ -73,7 +73,10 @@ class DDPRuntime:
     # ------------------------------------------------------------------ init
     @torch.no_grad()
     def broadcast_parameters(self) -> None:
-        """Rank 0's weights win (one flat broadcast instead of DDP's per-bucket X2)."""
+        """Rank 0's weights win (one flat broadcast instead of DDP's per-bucket X2).  A
+        pending lazy optimizer step is applied first, so the broadcast carries final weights
+        and nothing is replayed on top of them afterwards."""
+        self.store.flush_pending()
         dist.broadcast(self.store.flat, src=0, group=self.pg)
         self.store.refresh_shadow()
 

@@ -112,8 +112,11 @@ class FlatParamStore(ParamProvider):
         else:
             self.shadow = self.flat.to(compute_dtype)
         self._build_views()
-        # readers of the module's state see the weights of the last optimizer step
+        # readers of the module's state see the weights of the last optimizer step, and a
+        # load replaces them only after that step is applied (a pending update replayed
+        # onto loaded weights would corrupt them with stale gradients and moments)
         model.register_state_dict_pre_hook(lambda *args, **kw: self.flush_pending())
+        model.register_load_state_dict_pre_hook(lambda *args, **kw: self.flush_pending())
 
     # ----------------------------------------------------------------- views
     def _build_views(self):
@@ -182,8 +185,20 @@ class FlatParamStore(ParamProvider):
             self.pending.ensure_all()
             self.pending = None
 
+    def discard_pending(self) -> None:
+        """Drop a pending lazy optimizer step without applying it (its not-yet-applied
+        units' gradients are zeroed, as the step would have done): the fp32 master was
+        overwritten externally and is the truth now."""
+        p = self.pending
+        if p is not None:
+            p.discard()
+            self.pending = None
+
     def refresh_shadow(self) -> None:
-        """Re-derive the bf16 shadow from the fp32 master (after load / external edits)."""
+        """Re-derive the bf16 shadow from the fp32 master (after load / external edits).
+        The master is taken as final: a still-pending lazy step is discarded, never
+        replayed on top of it (callers that want it applied flush before editing)."""
+        self.discard_pending()
         if self.shadow is not self.flat:
             self.shadow.copy_(self.flat)
 

@@ -22,6 +22,9 @@ def setup_distributed(require: bool = False, timeout_s: Optional[float] = None):
     """
     distributed = dist.is_initialized() or "RANK" in os.environ or require
     if distributed and not dist.is_initialized():
+        # RCCL's xGMI defaults, read when the communicator is created (parallel/comm_env.py)
+        from ..parallel import comm_env
+        comm_env.apply()
         backend = os.environ.get("DLT_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         t = timeout_s or float(os.environ.get("DLT_PG_TIMEOUT", "1800"))
         kw = dict(backend=backend, timeout=datetime.timedelta(seconds=t))

@@ -94,7 +94,19 @@ class FlatAdamW:
         of the next step (see :class:`LazyStep`).  Same per-element arithmetic, hyper-
         parameters snapshotted now, so the weights come out bitwise as :meth:`step`'s."""
         self.step_count += 1
-        return LazyStep(self, scale if scale is not None else self._ones, units, mode)
+        self._lazy = LazyStep(self, scale if scale is not None else self._ones, units, mode)
+        return self._lazy
+
+    # the last recorded lazy step (state_dict / load_state_dict apply it first, so the
+    # moments reported or replaced are those of step_count)
+    _lazy = None
+    # the stream of LazyStep's "stream" mode, created once and reused by every step
+    _lazy_stream = None
+
+    def flush_lazy(self) -> None:
+        if self._lazy is not None:
+            self._lazy.ensure_all()
+            self._lazy = None
 
     def _apply_range(self, a: int, b: int, hp, step: int, sc: torch.Tensor, zero_grad: bool) -> None:
         """AdamW over flat[a:b] with one group's hyperparameters ``hp`` = (lr, (b1, b2), eps, wd)."""
@@ -116,6 +128,7 @@ class FlatAdamW:
 
     # ------------------------------------------------------------- state dict
     def state_dict(self) -> Dict:
+        self.flush_lazy()
         state, groups, idx = {}, [], 0
         pm = self.param_map or [[("flat", a, b - a, (b - a,))] for (a, b, _) in self.regions]
         for g, plist in zip(self.param_groups, pm):
@@ -132,6 +145,7 @@ class FlatAdamW:
         return {"state": state, "param_groups": groups}
 
     def load_state_dict(self, sd: Dict) -> None:
+        self.flush_lazy()
         pm = self.param_map or [[("flat", a, b - a, (b - a,))] for (a, b, _) in self.regions]
         st = sd["state"]
         steps = []
@@ -205,7 +219,12 @@ class LazyStep:
     def _issue_all_on_stream(self) -> None:
         cur = torch.cuda.current_stream()
         if self._stream is None:
-            self._stream = torch.cuda.Stream(cur.device)
+            # one stream for every step (kept on the optimizer): a fresh torch.cuda.Stream
+            # per step cycles through PyTorch's stream pool and would periodically alias
+            # the engine's or RCCL's streams
+            if self.opt._lazy_stream is None or self.opt._lazy_stream.device != cur.device:
+                self.opt._lazy_stream = torch.cuda.Stream(cur.device)
+            self._stream = self.opt._lazy_stream
         self._stream.wait_stream(cur)  # after the step's clip scale and the gradient all-reduces
         with torch.cuda.stream(self._stream):
             for u in self.units:
@@ -237,6 +256,20 @@ class LazyStep:
     def ensure_all(self) -> None:
         for u in self.units:
             self.ensure(u)
+
+    def discard(self) -> None:
+        """Give the step up: units not yet updated only get their gradients zeroed (what
+        the update would also have done); units already launched stay applied."""
+        if self.mode == "stream" and self.events:
+            return  # every unit was issued with the first ensure
+        for u, ranges in self.units.items():
+            if u in self.done:
+                continue
+            for (a, b) in ranges:
+                self.opt.grad[a:b].zero_()
+            self.done.add(u)
+        if self.opt._lazy is self:
+            self.opt._lazy = None
 
     @property
     def complete(self) -> bool:

@@ -413,3 +413,119 @@ def test_fsdp_limit_all_gathers_bounds_prefetch():
         for uid in range(4):
             rt._prefetch(rt.units[uid])
         assert len(issued) == want, (limit, issued)
+
+
+def _count_worker(rank, world, mode, strategy="FULL_SHARD"):
+    """One warm step, then the collectives of one optimizer step (GA = 2 micro-steps),
+    counted by wrapping torch.distributed: [(name, numel, element size)]."""
+    import torch.distributed as dist
+    from distributed_llm_trainer_amd.models.config import GPTConfig
+    cfg = GPTConfig(**TINY)
+    if mode == "ddp":
+        from distributed_llm_trainer_amd.training.configs import TrainingConfig
+        from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
+        tc = TrainingConfig(batch_size=2, gradient_accumulation_steps=2, warmup_steps=1, max_steps=100,
+                            learning_rate=1e-2, bucket_cap_mb=0.05, micro_step_fusion=1)
+        tr = DistributedTrainer(cfg, tc)
+    else:
+        from distributed_llm_trainer_amd.training.configs import FSDPConfig, FSDPTrainingConfig
+        from distributed_llm_trainer_amd.training.fsdp_trainer import FSDPTrainer
+        tc = FSDPTrainingConfig(batch_size=2, gradient_accumulation_steps=2, warmup_steps=1, max_steps=100,
+                                learning_rate=1e-2, micro_step_fusion=1)
+        tr = FSDPTrainer(cfg, tc, FSDPConfig(sharding_strategy=strategy, reduce_dtype="fp32"))
+    tr.train_step({"input_ids": _data(0, rank, n=4)})
+    log = []
+    names = ("all_reduce", "all_gather_into_tensor", "reduce_scatter_tensor", "broadcast", "all_gather",
+             "reduce_scatter", "barrier")
+    orig = {n: getattr(dist, n) for n in names}
+
+    def wrap(n):
+        def f(*a, **kw):
+            # the full-size operand: all_gather_into_tensor's output, reduce_scatter_tensor's input
+            t = a[1] if n == "reduce_scatter_tensor" else (a[0] if a and torch.is_tensor(a[0]) else kw.get("tensor"))
+            log.append((n, t.numel() if torch.is_tensor(t) else 0, t.element_size() if torch.is_tensor(t) else 0))
+            return orig[n](*a, **kw)
+        return f
+    for n in names:
+        setattr(dist, n, wrap(n))
+    try:
+        tr.train_step({"input_ids": _data(1, rank, n=4)})
+    finally:
+        for n in names:
+            setattr(dist, n, orig[n])
+    if mode == "ddp":
+        return log, [b - a for a, b in tr.ddp.buckets], tr.store.flat.numel()
+    units = {str(uid): (u.padded, u.shard) for uid, u in tr.runtime.units.items()}
+    return log, units, cfg.num_layers
+
+
+def test_ddp_collective_pattern_per_step():
+    """SURVEY §2.4 X3/X4 on 2 gloo ranks: one optimizer step (2 micro-steps) issues one fp32
+    all-reduce per bucket -- only in the last micro-step (no_sync), covering the flat
+    gradient buffer exactly once -- plus the logged global loss (one scalar); no per-step
+    buffer broadcast (X3 is dropped by design) and nothing else."""
+    for log, buckets, total in run_multiprocess(_count_worker, world=2, args=("ddp",)):
+        ar = [x for x in log if x[0] == "all_reduce"]
+        assert len(log) == len(ar), log  # no broadcast / gather / reduce-scatter per step
+        big = [x for x in ar if x[1] > 1]
+        assert sorted(x[1] for x in big) == sorted(buckets) and len(buckets) > 2
+        assert sum(x[1] for x in big) == total and all(x[2] == 4 for x in big)
+        assert len(ar) - len(big) == 1  # the global-loss scalar
+
+
+@pytest.mark.parametrize("strategy", ["FULL_SHARD", "SHARD_GRAD_OP"])
+def test_fsdp_collective_pattern_per_step(strategy):
+    """SURVEY §2.4 X5-X8 on 2 gloo ranks, per optimizer step of 2 micro-steps: every
+    micro-step all-gathers each block for its forward (X5; the root unit once per step),
+    FULL_SHARD gathers each block again for its backward (X6; SHARD_GRAD_OP keeps the
+    forward's gather), reduce-scatters
+    every unit's gradient once (X7), and the step ends with one scalar all-reduce for the
+    gradient clip (X8) plus the logged global loss."""
+    for log, units, L in run_multiprocess(_count_worker, world=2, args=("fsdp", strategy)):
+        ag = [x for x in log if x[0] == "all_gather_into_tensor"]
+        rs = [x for x in log if x[0] == "reduce_scatter_tensor"]
+        ar = [x for x in log if x[0] == "all_reduce"]
+        assert len(ag) + len(rs) + len(ar) == len(log), log
+        full = {uid: p for uid, (p, _) in units.items()}
+        head, block = full["head"], full["0"]
+        # the root unit (embedding / tied lm_head / final norm) is gathered once and kept for
+        # the step (the reference's root FSDP unit is never resharded after forward); every
+        # block is gathered for each micro-step's forward and, under FULL_SHARD, again for
+        # its backward
+        per_block = 4 if strategy == "FULL_SHARD" else 2
+        assert [x[1] for x in ag].count(head) == 1
+        assert [x[1] for x in ag].count(block) == per_block * L and len(ag) == 1 + per_block * L
+        assert sorted(x[1] for x in rs) == sorted(2 * list(full.values()))  # every unit, every micro-step
+        assert [x[1] for x in ar] == [1, 1]  # clip sum of squares + the logged loss
+
+
+def test_comm_env_is_set_before_the_process_group(monkeypatch):
+    """parallel/comm_env.py: the RCCL xGMI defaults are exported before
+    init_process_group creates a communicator, and a user's own value wins."""
+    import torch.distributed as dist
+    from distributed_llm_trainer_amd.parallel import comm_env
+    from distributed_llm_trainer_amd.training import common
+    if dist.is_initialized():
+        pytest.skip("process group already initialised in this process")
+    for k in list(comm_env.COMMON) + list(comm_env.SINGLE_NODE):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("NCCL_DEBUG", "INFO")  # user-set: kept
+    monkeypatch.setenv("RANK", "0")
+    monkeypatch.setenv("WORLD_SIZE", "8")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    seen = {}
+
+    def fake_init(**kw):
+        seen.update({k: os.environ.get(k) for k in list(comm_env.COMMON) + list(comm_env.SINGLE_NODE)})
+        raise RuntimeError("stop")  # nothing to rendezvous with
+    monkeypatch.setattr(dist, "init_process_group", fake_init)
+    with pytest.raises(RuntimeError, match="stop"):
+        common.setup_distributed(require=True)
+    assert seen["NCCL_DEBUG"] == "INFO"
+    assert seen["NCCL_IB_DISABLE"] == "1" and seen["NCCL_MIN_NCHANNELS"] == "32"
+    assert seen["TORCH_NCCL_HIGH_PRIORITY"] == "1" and seen["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    # several nodes: no NCCL_IB_DISABLE
+    monkeypatch.delenv("NCCL_IB_DISABLE")
+    assert "NCCL_IB_DISABLE" not in comm_env.apply(world_size=16, local_world_size=8)
+    monkeypatch.setenv("DLT_COMM_ENV", "0")
+    assert comm_env.apply() == {}

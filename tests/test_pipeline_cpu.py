@@ -391,6 +391,66 @@ def test_lazy_optimizer_step_matches_end_of_step_update(tmp_path):
     assert torch.equal(c["model"]["layers.1.mlp.down_proj.weight"], s0["layers.1.mlp.down_proj.weight"])
 
 
+def test_lazy_optimizer_never_replays_onto_loaded_weights():
+    """Weights loaded (model.load_state_dict, utils.checkpoint.load_model_state) or written
+    into the master and re-derived (refresh_shadow) while a lazy optimizer step is pending
+    are final: the next forward must not apply the stale update on top of them.  The
+    optimizer's state_dict reports the moments of its step count (the pending step is
+    applied first)."""
+    from distributed_llm_trainer_amd.training.configs import TrainingConfig
+    from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
+    from distributed_llm_trainer_amd.utils.checkpoint import load_model_state
+    torch.manual_seed(16)
+    data = [torch.randint(0, 256, (8, 32)) for _ in range(3)]
+
+    def trained(mode):
+        tc = TrainingConfig(batch_size=2, gradient_accumulation_steps=4, warmup_steps=2, max_steps=10,
+                            lazy_optimizer=mode)
+        tr = DistributedTrainer(tiny(), tc)
+        for d in data[:2]:
+            tr.train_step({"input_ids": d})
+        return tr
+
+    ref_tr = trained("off")
+    ref_sd = {k: v.clone() for k, v in ref_tr.model.state_dict().items()}
+    ref_m = ref_tr.optimizer.exp_avg.clone()
+    # optimizer state_dict with a step pending: the moments of step_count
+    tr = trained("inline")
+    assert tr.store.pending is not None and not tr.store.pending.complete
+    osd = tr.optimizer.state_dict()
+    assert all(int(s["step"]) == ref_tr.optimizer.step_count for s in osd["state"].values())
+    assert torch.equal(tr.optimizer.exp_avg, ref_m)
+    # load_state_dict with a step pending, for both load entry points
+    other = {k: torch.randn_like(v) if v.dtype.is_floating_point else v for k, v in ref_sd.items()}
+    if "lm_head.weight" in other:  # tied: one tensor
+        other["lm_head.weight"] = other["embed_tokens.weight"]
+    for load in (lambda m, sd: m.load_state_dict(sd), load_model_state):
+        tr = trained("inline")
+        assert tr.store.pending is not None and not tr.store.pending.complete
+        load(tr.model, other)
+        tr.store.refresh_shadow()
+        tr.train_step({"input_ids": data[2]})  # its forward runs every unit's pre_forward hook
+        sd = tr.model.state_dict()  # flushes the step this train_step recorded: compare before
+        # the new step is applied: re-load and take the parameters straight from the store
+        tr2 = trained("inline")
+        load(tr2.model, other)
+        tr2.store.refresh_shadow()
+        tr2.train_step({"input_ids": data[2]})
+        for k in ("norm.weight", "layers.1.mlp.down_proj.weight", "embed_tokens.weight"):
+            seg = tr2.store.layout.by_name[k]
+            got = tr2.store.flat[seg.offset:seg.offset + seg.numel].view(seg.shape)
+            assert torch.equal(got, other[k].to(got.dtype)), k  # loaded weights untouched by the old step
+        assert set(sd) == set(other)
+    # external edit of the master + refresh_shadow: the edit is final, the pending step is dropped
+    tr = trained("inline")
+    edited = torch.randn_like(tr.store.flat)
+    tr.store.flat.copy_(edited)
+    tr.store.refresh_shadow()
+    assert tr.store.pending is None and float(tr.store.grad.abs().max()) == 0.0
+    tr.train_step({"input_ids": data[2]})
+    assert torch.equal(tr.store.flat, edited)
+
+
 def test_f32_attention_impl_choice(monkeypatch):
     """fp32 attention picks the GEMM formulation while its two [B*nh, S, S] score buffers fit
     and S <= 4096, else the flash kernels; a forced "gemm" beyond the limits is an error."""
