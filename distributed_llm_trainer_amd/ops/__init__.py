@@ -53,12 +53,13 @@ def for_device(device, head_dim: int = 64, act_dtype=torch.bfloat16) -> types.Si
     activations on the 16-bit kernels, fp32 (``--mixed_precision fp32``) on the fp32
     kernels (``csrc/fp32.hip``; the ``hip`` wrappers dispatch on the tensor dtype).  The
     flash attention kernels take head_dim 64 and 128 in every precision; a model with
-    another head_dim (the reference allows any ``hidden % heads == 0``, ``config.py:38-39``)
-    runs attention on native kernels (``ops/attn_gemm.py``, ``attn_backend == "gemm"``, with
-    a one-time warning): 16-bit heads under 128 zero-padded onto the flash kernels, else
-    GEMMs over the dense scores around HIP row kernels.  Its RoPE runs on the HIP kernel when that takes the head_dim (16-bit: head_dim % 16 == 0; fp32:
-    even), else as PyTorch ops on the GPU; the norms, SwiGLU, cross-entropy, embedding,
-    optimizer and GEMMs stay native."""
+    another head_dim (the reference allows any ``hidden % heads == 0``, ``config.py:38-39``,
+    with an even head_dim for its rotate_half) runs attention on native kernels
+    (``ops/attn_gemm.py``, ``attn_backend == "gemm"``, with a one-time warning): heads under
+    128 zero-padded onto the flash kernels, wider ones as GEMMs over the dense scores around
+    HIP row kernels.  Its RoPE runs on the 16-bit HIP kernel when that takes the head_dim
+    (% 16), else on the fp32 HIP kernel over the widened values.  No op falls back to
+    PyTorch reference ops on the GPU."""
     dev = torch.device(device)
     if dev.type == "cuda":
         if os.environ.get("DLT_ALLOW_REFERENCE_ON_GPU") == "1":
@@ -72,15 +73,17 @@ def for_device(device, head_dim: int = 64, act_dtype=torch.bfloat16) -> types.Si
             import warnings
 
             from . import attn_gemm
-            rope_native = head_dim % (2 if act_dtype == torch.float32 else 16) == 0
+            if head_dim % 2:
+                raise NotImplementedError(f"head_dim {head_dim}: RoPE (rotate_half) needs an even head_dim")
+            rope16 = act_dtype == torch.float32 or head_dim % 16 == 0
+            route = ("zero-padded onto the flash kernels" if attn_gemm.pad_dim(act_dtype, head_dim)
+                     else "batched GEMMs + HIP row kernels")
             warnings.warn(f"head_dim {head_dim}: the HIP flash attention kernels take head_dim {native_hd}; attention "
-                          f"runs zero-padded on them or as batched GEMMs + HIP row kernels for this model (RoPE: "
-                          f"{'HIP kernel' if rope_native else 'PyTorch ops'})")
+                          f"runs {route} for this model (RoPE: "
+                          f"{'HIP kernel' if rope16 else 'fp32 HIP kernel on widened values'})")
             for f in _ATTN_FUNCS:
-                if not f.startswith("rope"):
+                if not f.startswith("rope") or not rope16:
                     setattr(ns, f, getattr(attn_gemm, f))
-                elif not rope_native:
-                    setattr(ns, f, getattr(reference, f))
             ns.attn_backend = "gemm"
         return ns
     return CPU_OPS

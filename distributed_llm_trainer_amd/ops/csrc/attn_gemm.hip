@@ -12,7 +12,8 @@
 //   * k_attn_softmax<NE, OT>   -- causal mask, softmax, lse (natural log) and dropout from
 //     the keep-bit words of k_dropout_bits (attention.hip), one 256-thread block per row;
 //     k_attn_softmax_w / k_attn_dsoftmax_w: one wave per row, 4 rows per workgroup, float4
-//     score accesses and wave-only reductions (no LDS, no barrier), for S % 4 == 0
+//     score accesses and wave-only reductions (no LDS, no barrier), for S % 4 == 0;
+//     k_attn_softmax_long: rows of more than 4096 keys (three passes over the row)
 //   * k_attn_dsoftmax<OT>      -- P from lse, delta = rowsum(dO * O), the dropped P (for
 //     dV) and scale * dS (for dQ / dK)
 //   * k_relayout16             -- 16-bit [b, s, h, d] strided copy (packed QKV <-> head-major)
@@ -230,6 +231,41 @@ __global__ __launch_bounds__(256) void k_attn_softmax_w(const float* sc, typenam
   }
 }
 
+// k_attn_softmax for rows longer than the register-resident kernels above take (S > 4096
+// keys): one wave per row, three passes over the row in memory (max, sum, write), the same
+// arithmetic.  OT = 0: pout may be sc (each element is read and written by one lane).
+template <int OT>
+__global__ __launch_bounds__(256) void k_attn_softmax_long(const float* sc, typename ATy<OT>::T* pout,
+                                                           float* __restrict__ lse, const uint32_t* __restrict__ mask,
+                                                           long rows, int S, float scale, float dscale, int Lb) {
+  const long row = blockIdx.x * 4L + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int lane = threadIdx.x & 63;
+  const int q = (int)(row % S);
+  const long bh = row / S;
+  const float* r = sc + row * S;
+  const float c = scale * 1.44269504088896341f;
+  float m = -INFINITY;
+  for (int k = lane; k <= q; k += 64) m = fmaxf(m, r[k] * c);
+  m = wave_max(m);  // finite: key 0 is always visible
+  float l = 0.f;
+  for (int k = lane; k <= q; k += 64) l += exp2f(r[k] * c - m);
+  l = wave_sum(l);
+  if (lane == 0) lse[row] = (m + __log2f(l)) * 0.69314718055994531f;
+  const float inv = 1.f / l;
+  const uint32_t* mw = mask ? mask + bh * (long)((S + 31) >> 5) * S + q : nullptr;
+  typename ATy<OT>::T* po = pout + row * S;
+  const int wl = Lb > 0 ? min(S, (q / Lb + 1) * Lb) : S;
+  for (int k = lane; k < wl; k += 64) {
+    float p = 0.f;
+    if (k <= q) {
+      p = exp2f(r[k] * c - m) * inv;
+      if (mw) p = ((mw[(size_t)(k >> 5) * S] >> (k & 31)) & 1u) ? p * dscale : 0.f;
+    }
+    a_st<OT>(po, k, p);
+  }
+}
+
 // k_attn_dsoftmax with one wave per row (S % 4 == 0)
 template <int OT>
 __global__ __launch_bounds__(256) void k_attn_dsoftmax_w(const float* sc, const float* dp, typename ATy<OT>::T* pd_out,
@@ -320,9 +356,13 @@ template <int OT>
 static int softmax_launch(float* sc, void* pout, float* lse, const uint32_t* mask, int BH, int S, float scale,
                           float dscale, int Lb, hipStream_t st) {
   const long rows = (long)BH * S;
-  if (S <= 0 || S > 4096 || rows > 0x7fffffffL || Lb < 0 || Lb % 4) return -1;
+  if (S <= 0 || rows > 0x7fffffffL || Lb < 0 || Lb % 4) return -1;
   using T = typename ATy<OT>::T;
   T* po = static_cast<T*>(pout);
+  if (S > 4096) {  // rows longer than the register-resident kernels take
+    k_attn_softmax_long<OT><<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(sc, po, lse, mask, rows, S, scale, dscale, Lb);
+    return 0;
+  }
   const int ne = (S + 255) / 256;
   if (S % 4 == 0 && row_w_enabled()) {  // wave per row (the 16-bit rows are 8-byte aligned: S % 4 == 0)
     const unsigned nb = (unsigned)((rows + 3) / 4);
@@ -362,7 +402,7 @@ static int dsoftmax_launch(const float* sc, const float* dp, void* pd_out, void*
 
 // Lb (every entry point): the row-block size of blocked causal GEMMs -- a row q only
 // writes the columns below the end of its block, (q / Lb + 1) * Lb; 0: the whole row.
-// fp32: sc [BH*S, S] in place; lse [BH*S]; S <= 4096
+// fp32: sc [BH*S, S] in place; lse [BH*S]
 DLT_API int dlt_f32_attn_softmax(float* sc, float* lse, const uint32_t* mask, int BH, int S, float scale, float dscale,
                                  int Lb, hipStream_t st) {
   if (softmax_launch<0>(sc, sc, lse, mask, BH, S, scale, dscale, Lb, st)) return -1;

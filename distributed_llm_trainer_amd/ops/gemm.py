@@ -119,11 +119,11 @@ def load_plan(path: str, shipped: bool = False) -> None:
             if rc != 0:
                 raise RuntimeError(f"dlt_gemm_pin failed ({rc})")
             _PINNED["hipblaslt"][tuple(v[:-1])] = line
-    # "tn": forward-projection race ("bf16" = the persistent hand-written kernel, "tn4" =
-    # the four-wave one-tile-per-workgroup hand-written kernel, null = hipBLASLt; the
+    # "tn": forward-projection race ("bf16" = the persistent hand-written kernel, "fwd" =
+    # the one-tile-per-workgroup hand-written kernel, null = hipBLASLt; the
     # round-2 integer tile configs of the retired gemm_tn kernels read as "library");
     # "fused": "kind:MxNxK" -> fused epilogue picked (older keys without a kind are ignored)
-    _PINNED["tn"] = {tuple(int(x) for x in k.split("x")): (c if c in ("bf16", "tn4") else None)
+    _PINNED["tn"] = {tuple(int(x) for x in k.split("x")): (c if c in ("bf16", "fwd") else None)
                      for k, c in plan.get("tn", {}).items()}
     for k, c in plan.get("fused", {}).items():
         if ":" in k:
@@ -296,7 +296,7 @@ class HipGemm:
         # down-dgrad + SwiGLU-backward kernels (both instantiated for IEEE half and
         # tested): DLT_GEMM_FP16_HAND=1 ("fwd" / "dswiglu": only one of the two).  Off by
         # default: --precision fp16 steps measured 744-749k with them vs 744-756k on
-        # hipBLASLt + the unfused SwiGLU backward (tools/ab/r5/r5_fp16hand.sh, same box)
+        # hipBLASLt + the unfused SwiGLU backward (r5_fp16hand.sh in tools/ab/README.md, same box)
         _f16 = os.environ.get("DLT_GEMM_FP16_HAND", "0")
         self._fp16_hand = _f16 in ("1", "fwd")
         self._fp16_dswiglu = _f16 in ("1", "dswiglu")
@@ -334,7 +334,7 @@ class HipGemm:
 
     def _pick(self, x, w, y):
         """Forward projection race, once per shape: hipBLASLt (None), the persistent
-        hand-written kernel ("bf16") or the four-wave one (\"tn4\"); a hand-written pick
+        hand-written kernel ("bf16") or the one-tile-per-workgroup one ("fwd"); a hand-written pick
         must beat the library by RACE_MARGIN.  The shipped plan pins the in-step winners."""
         from . import hip
         key = (x.shape[0], w.shape[0], x.shape[1])
@@ -348,8 +348,8 @@ class HipGemm:
         cands = []
         if hip.gemm_bf16_fits(*key):
             cands.append(("bf16", lambda: hip.gemm_bf16(x, w, out=y)))
-        if hip.gemm_tn4_fits(*key) and os.environ.get("DLT_GEMM_TN4", "1") != "0":
-            cands.append(("tn4", lambda: hip.gemm_tn4(x, w, out=y)))
+        if hip.gemm_fwd_fits(*key) and os.environ.get("DLT_GEMM_FWD2", "1") != "0":
+            cands.append(("fwd", lambda: hip.gemm_fwd(x, w, out=y)))
         for name, fn in cands:
             t = _time_of(fn)
             if t < best:
@@ -367,7 +367,7 @@ class HipGemm:
         from . import hip
         if pick == "bf16" and (x.dtype == torch.bfloat16 or self._fp16_hand) and hip.gemm_bf16(x, w, out=y) is not None:
             return y
-        if pick == "tn4" and hip.gemm_tn4(x, w, out=y) is not None:
+        if pick == "fwd" and hip.gemm_fwd(x, w, out=y) is not None:
             return y
         self._lib_linear(x, w, y)
         return y

@@ -355,14 +355,16 @@ def _gemm_bwd(q4, k4, v4, o, do, aux, B, nh, S, hd, p, key, device):
     return dq, dk, dv
 
 
-def _fwd(qp, kp, vp, strides, B, nh, S, hd, p, key, device, out, mask, store_mask=True):
+def _fwd(qp, kp, vp, strides, B, nh, S, hd, p, key, device, out, mask, store_mask=True, scale=None):
+    """The VALU flash forward; ``scale`` overrides 1/sqrt(hd) (heads zero-padded to hd)."""
     _check_hd(hd)
     o = torch.empty(B * S, nh * hd, dtype=torch.float32, device=device) if out is None else out
     _req32(o, "attn_f32.o", B * S * nh * hd)
     lse = torch.empty(B, nh, S, dtype=torch.float32, device=device)
     mask, dscale = _mask(B, nh, S, p, key, device, mask)
-    _chk(_lib().dlt_f32_attn_fwd(qp, kp, vp, *strides, _p(o), _p(lse), _p(mask), B, nh, S, hd, 1.0 / math.sqrt(hd),
-                                 dscale, _st()), "f32_attn_fwd")
+    sc = 1.0 / math.sqrt(hd) if scale is None else float(scale)
+    _chk(_lib().dlt_f32_attn_fwd(qp, kp, vp, *strides, _p(o), _p(lse), _p(mask), B, nh, S, hd, sc, dscale, _st()),
+         "f32_attn_fwd")
     # store_mask=False: the keep bits only live for this call (the backward regenerates them)
     return o, _h().AttnAux((lse, mask if store_mask else None))
 
@@ -393,7 +395,7 @@ def attention_fwd_packed(qkv, B, S, nh, p, key, out=None, mask=None, store_mask=
     return _fwd(*ptr, (S * threeH, hd, threeH), B, nh, S, hd, p, key, qkv.device, out, mask, store_mask)
 
 
-def _bwd(qp, kp, vp, strides, o, do, aux, B, nh, S, hd, p, key, device, gp, gstrides):
+def _bwd(qp, kp, vp, strides, o, do, aux, B, nh, S, hd, p, key, device, gp, gstrides, scale=None):
     _check_hd(hd)
     lse, mask = aux if isinstance(aux, tuple) else (aux, None)
     _req32(lse, "attn_bwd_f32.lse", B * nh * S)
@@ -402,7 +404,8 @@ def _bwd(qp, kp, vp, strides, o, do, aux, B, nh, S, hd, p, key, device, gp, gstr
     mask, dscale = _mask(B, nh, S, p, key, device, mask)
     delta = torch.empty(B, nh, S, dtype=torch.float32, device=device)
     _chk(_lib().dlt_f32_attn_bwd(qp, kp, vp, *strides, _p(o), _p(do), _p(lse), _p(mask), _p(delta), *gp, *gstrides,
-                                 B, nh, S, hd, 1.0 / math.sqrt(hd), dscale, _st()), "f32_attn_bwd")
+                                 B, nh, S, hd, 1.0 / math.sqrt(hd) if scale is None else float(scale), dscale, _st()),
+         "f32_attn_bwd")
 
 
 def attention_bwd(q, k, v, o, do, aux, p, key, causal=True):

@@ -162,7 +162,8 @@ def _forced(rank, world, mode):
         from distributed_llm_trainer_amd.training.ddp_trainer import LEAN_DEFER_ROLES, DistributedTrainer
         tc = TrainingConfig(batch_size=2, gradient_accumulation_steps=4, warmup_steps=1, max_steps=100,
                             learning_rate=1e-3, bucket_cap_mb=1.0,
-                            defer_roles=LEAN_DEFER_ROLES if mode == "ddp_lean" else "all")
+                            defer_roles=LEAN_DEFER_ROLES if mode == "ddp_lean" else "all",
+                            reduce_dtype="bf16" if mode == "ddp_bf16" else "fp32")
         tr = DistributedTrainer(GPTConfig(**TINY), tc)
     else:
         from distributed_llm_trainer_amd.training.configs import FSDPConfig, FSDPTrainingConfig
@@ -232,3 +233,23 @@ def test_rccl_forced_collectives_one_rank(mode):
         assert launched > 2
     for k in a:
         assert torch.equal(a[k], b[k]), (k, (a[k] - b[k]).abs().max().item())
+
+
+def test_rccl_forced_bf16_wire_matches_fp32_wire():
+    """DDP with reduce_dtype bf16 (the gradient buckets cast to bf16 for the RCCL
+    all-reduce, summed, cast back into the fp32 accumulators) on one forced RCCL rank: every
+    bucket goes through the bf16 transport (so the parameters differ from the fp32 wire's
+    in the last bits) and the trained parameters stay within bf16 gradient rounding of the
+    fp32-wire run."""
+    env = {"DLT_FORCE_CPU": None, "DLT_BACKEND": "nccl", "DLT_GEMM_TUNE": "0", "DLT_WGRAD_SPLITK": "0",
+           "DLT_GEMM_TN": "0", "DLT_GEMM_FUSED": "0", "DLT_WGRAD_HAND": "0", "DLT_FORCE_COLLECTIVES": "1"}
+    a, la = run_multiprocess(_forced, world=1, args=("ddp",), env=env, timeout=240)[0]
+    b, lb = run_multiprocess(_forced, world=1, args=("ddp_bf16",), env=env, timeout=240)[0]
+    assert la == lb and la > 2
+    fa, fb = a["flat"], b["flat"]
+    assert not torch.equal(fa, fb)  # the bf16 transport ran
+    # AdamW normalises the update, so a bf16-rounded gradient moves each weight by at most
+    # ~lr per step either way; the parameters agree to well under one step's update
+    rel = ((fa - fb).norm() / fa.norm()).item()
+    assert rel < 1e-3, rel
+    assert (fa - fb).abs().max().item() < 3 * 1e-3 * STEPS

@@ -142,13 +142,15 @@ def test_fp32_training_runs_hip_kernels():
 
 @pytest.mark.parametrize("dt,hd,pad", [(torch.bfloat16, 48, True), (torch.float16, 80, True), (torch.bfloat16, 40, True),
                                        (torch.bfloat16, 48, False), (torch.float16, 80, False),
-                                       (torch.bfloat16, 40, False), (torch.bfloat16, 160, True), (torch.float32, 32, True)])
+                                       (torch.bfloat16, 40, False), (torch.bfloat16, 160, True), (torch.float32, 32, True),
+                                       (torch.float32, 32, False), (torch.bfloat16, 36, True), (torch.float32, 96, True)])
 def test_attn_gemm_odd_head_dims_vs_reference(dt, hd, pad, monkeypatch):
     """ops/attn_gemm.py (head_dims without a flash kernel) against the PyTorch reference
     attention (fp32 arithmetic on the same inputs, same keep bits), forward + backward +
-    inverse RoPE, on every route: 16-bit heads zero-padded onto the flash kernels (pad,
-    head_dim < 128), 16-bit GEMMs with fp32 scores (head_dim % 16 == 0: 48, 80, 160), the
-    fp32 formulation on widened inputs (40 without padding; fp32 32)."""
+    inverse RoPE, on every route: heads zero-padded onto the flash kernels (pad, head_dim
+    < 128: 16-bit MFMA and fp32 VALU flash kernels), 16-bit GEMMs with fp32 scores
+    (head_dim % 16 == 0: 48, 80, 160), the fp32 formulation on widened inputs (40 without
+    padding; fp32 32 without padding); 36: the widened fp32 RoPE."""
     from distributed_llm_trainer_amd.ops import attn_gemm
     monkeypatch.setattr(attn_gemm, "PAD_FLASH", pad)
     torch.manual_seed(hd)
@@ -157,10 +159,15 @@ def test_attn_gemm_odd_head_dims_vs_reference(dt, hd, pad, monkeypatch):
     qkv = (torch.randn(B * S, 3 * H, device=DEV) * 0.5).to(dt)
     cos, sin = hip.rope_tables(hd, S, device=DEV)
     assert attn_gemm.fits(B, nh, S, hd)
-    assert (attn_gemm.pad_dim(dt, hd) is not None) == (pad and dt != torch.float32 and hd < 128)
+    assert (attn_gemm.pad_dim(dt, hd) is not None) == (pad and hd < 128)
     assert attn_gemm.use16(dt, B, nh, S, hd) == (dt != torch.float32 and hd % 16 == 0)
     o, aux = attn_gemm.attention_fwd_packed(qkv, B, S, nh, p, 77)
     orf, lser = ref.attention_fwd_packed(qkv, B, S, nh, p, 77)
+    if hd % 16:  # the ops namespace's RoPE for this head_dim (widened onto the fp32 kernel)
+        qr = qkv.clone()
+        attn_gemm.rope_qk_inplace(qr, B, S, nh, cos, sin)
+        want = ref.rope_qk_inplace(qkv.clone(), B, S, nh, cos, sin)
+        assert _rel(qr, want) < (1e-6 if dt == torch.float32 else 8e-3)
     assert o.dtype == dt
     tol = 2e-5 if dt == torch.float32 else 1e-2
     assert _rel(o, orf) < tol, _rel(o, orf)
@@ -170,6 +177,34 @@ def test_attn_gemm_odd_head_dims_vs_reference(dt, hd, pad, monkeypatch):
     gr = ref.attention_bwd_packed(qkv, orf, do, lser, p, 77, B, S, nh, cos, sin)
     assert g.dtype == dt and g.shape == qkv.shape
     assert _rel(g, gr) < (5e-5 if dt == torch.float32 else 2e-2), _rel(g, gr)
+
+
+@pytest.mark.parametrize("dt,hd,S", [(torch.bfloat16, 40, 5000), (torch.float32, 40, 5000), (torch.bfloat16, 160, 4200)])
+def test_attn_long_rows_native_route(dt, hd, S, monkeypatch):
+    """Rows past the register-resident softmax (> 4096 keys) on head dims without a flash
+    kernel stay native: head_dim 40 (bf16 / fp32) zero-padded onto the flash kernels, head
+    dim 160 on the GEMM route with the long-row softmax kernel; the reference-op functions
+    are made to raise, so a silent fallback would fail the test."""
+    from distributed_llm_trainer_amd.ops import attn_gemm, reference
+    for name in ("attention_fwd_packed", "attention_bwd_packed", "attention_fwd", "attention_bwd", "rope_qkv_bwd",
+                 "rope_qk_inplace"):
+        monkeypatch.setattr(reference, name, lambda *a, **k: (_ for _ in ()).throw(AssertionError("reference op")))
+    torch.manual_seed(S)
+    B, nh, p = 1, 2, 0.1
+    H = nh * hd
+    assert (attn_gemm.pad_dim(dt, hd) is not None) == (hd < 128)
+    qkv = (torch.randn(B * S, 3 * H, device=DEV) * 0.5).to(dt)
+    cos, sin = hip.rope_tables(hd, S, device=DEV)
+    o, aux = attn_gemm.attention_fwd_packed(qkv, B, S, nh, p, 5)
+    do = torch.randn(B * S, H, device=DEV).to(dt)
+    g = attn_gemm.attention_bwd_packed(qkv, o, do, aux, p, 5, B, S, nh, cos, sin)
+    monkeypatch.undo()
+    orf, lser = ref.attention_fwd_packed(qkv, B, S, nh, p, 5)
+    gr = ref.attention_bwd_packed(qkv, orf, do, lser, p, 5, B, S, nh, cos, sin)
+    tol = (2e-5, 5e-5) if dt == torch.float32 else (1e-2, 2e-2)
+    assert _rel(o, orf) < tol[0], _rel(o, orf)
+    assert _rel(aux[0], lser) < 2e-5
+    assert _rel(g, gr) < tol[1], _rel(g, gr)
 
 
 @pytest.mark.parametrize("dt,pad", [(torch.bfloat16, False), (torch.float16, False), (torch.bfloat16, True)])

@@ -646,10 +646,10 @@ def test_fused_decode_falls_back_beyond_lds():
                                                    (320, 8, "gemm")])
 def test_head_dim_128_trains_on_gpu(hidden, heads, backend):
     """YAML-style configs with head_dim 128 (the MFMA attention kernels' D = 128
-    instantiation) and head_dims 32 / 48 / 40 (no flash kernel: attention through the fp32
-    GEMM formulation of ops/attn_gemm.py; RoPE on the HIP kernel for 32 / 48, PyTorch ops
-    for 40) -- the reference accepts any hidden % heads == 0.  Gradients match the
-    all-reference-ops engine (verdict r2: it raised)."""
+    instantiation) and head_dims 32 / 48 / 40 (no flash kernel: attention zero-padded onto
+    the flash kernels by ops/attn_gemm.py; RoPE on the 16-bit HIP kernel for 32 / 48, on the
+    fp32 HIP kernel over widened values for 40) -- the reference accepts any hidden % heads
+    == 0.  Gradients match the all-reference-ops engine (verdict r2: it raised)."""
     cfg = GPTConfig(vocab_size=1000, hidden_size=hidden, num_layers=2, num_heads=heads, max_seq_len=256,
                     dropout=0.1, attention_dropout=0.1)
     assert cfg.head_dim == hidden // heads
@@ -659,9 +659,9 @@ def test_head_dim_128_trains_on_gpu(hidden, heads, backend):
     e1 = m1.enable_engine(seed=6)
     assert e1.ops.attn_backend == backend and e1.ops.backend == "hip"
     if backend == "gemm":
-        from distributed_llm_trainer_amd.ops import attn_gemm, reference
+        from distributed_llm_trainer_amd.ops import attn_gemm
         assert e1.ops.attention_fwd_packed is attn_gemm.attention_fwd_packed
-        assert (e1.ops.rope_qk_inplace is reference.rope_qk_inplace) == (cfg.head_dim % 16 != 0)
+        assert (e1.ops.rope_qk_inplace is attn_gemm.rope_qk_inplace) == (cfg.head_dim % 16 != 0)
     m2.enable_engine(seed=6, ops=ops.CPU_OPS)
     ids = torch.randint(0, 1000, (2, 256), device=DEV)
     _, l1 = m1(ids, labels=ids)

@@ -471,14 +471,23 @@ def test_f32_attention_impl_choice(monkeypatch):
 
 
 def test_attn_gemm_routes(monkeypatch):
-    """Head dims without a flash kernel: 16-bit heads under 128 (multiple of 8) pad to 64 / 128;
-    fp32, head_dim >= 128 and DLT_ATTN_PAD=0 do not pad; the GEMM formulation's shape limits."""
+    """Head dims without a flash kernel: heads under 128 pad to 64 / 128 (16-bit: any
+    head_dim; fp32: even ones), head_dim >= 128 and DLT_ATTN_PAD=0 do not pad; the GEMM
+    formulation takes rows of any length and raises (no silent fallback) past its score
+    buffer budget."""
     from distributed_llm_trainer_amd.ops import attn_gemm
     monkeypatch.setattr(attn_gemm, "PAD_FLASH", True)
     assert attn_gemm.pad_dim(torch.bfloat16, 32) == 64 and attn_gemm.pad_dim(torch.float16, 48) == 64
     assert attn_gemm.pad_dim(torch.bfloat16, 96) == 128 and attn_gemm.pad_dim(torch.bfloat16, 80) == 128
-    assert attn_gemm.pad_dim(torch.bfloat16, 160) is None and attn_gemm.pad_dim(torch.float32, 96) is None
-    assert attn_gemm.pad_dim(torch.bfloat16, 36) is None  # not a multiple of 8
+    assert attn_gemm.pad_dim(torch.bfloat16, 160) is None and attn_gemm.pad_dim(torch.float32, 96) == 128
+    assert attn_gemm.pad_dim(torch.bfloat16, 36) == 64 and attn_gemm.pad_dim(torch.float32, 40) == 64
+    assert attn_gemm.pad_dim(torch.float32, 35) is None
     monkeypatch.setattr(attn_gemm, "PAD_FLASH", False)
     assert attn_gemm.pad_dim(torch.bfloat16, 96) is None
-    assert attn_gemm.fits(16, 12, 1024, 96) and not attn_gemm.fits(1, 1, 8192, 96) and not attn_gemm.fits(1, 1, 64, 258)
+    assert attn_gemm.fits(16, 12, 1024, 96) and attn_gemm.fits(1, 1, 8192, 96) and attn_gemm.fits(1, 1, 64, 258)
+    monkeypatch.setattr(attn_gemm, "GEMM_ROUTE_BYTES", 1 << 20)
+    assert not attn_gemm.fits(1, 1, 8192, 160)
+    with pytest.raises(NotImplementedError, match="DLT_ATTN_GEMM_GB"):
+        attn_gemm._need_fit(1, 1, 8192, 160)
+    import inspect
+    assert "reference." not in inspect.getsource(attn_gemm).split('"""', 2)[2]  # no reference-op route

@@ -1,6 +1,6 @@
 """Isolated timing of the forward projection GEMMs at the headline chain shape (M = 16384):
 hipBLASLt (the planner's library path) vs the persistent hand kernel (k_gemm_bf16) vs the
-four-wave one-tile-per-workgroup kernel (k_gemm_tn4).  Mean of --iters launches after
+one-tile-per-workgroup 256 x 128 kernel (k_gemm_fwd).  Mean of --iters launches after
 warmup, CUDA events.  usage: python tools/bench_gemm_fwd.py [--iters 50]"""
 import argparse
 import os
@@ -41,16 +41,16 @@ def main():
         row = [f"{name:8s} {M}x{N}x{K}:"]
         for label, fn in (("lib", lambda: g._lib_linear(a, b, y)),
                           ("bf16", (lambda: hip.gemm_bf16(a, b, out=y)) if hip.gemm_bf16_fits(M, N, K) else None),
-                          ("tn4", lambda: hip.gemm_tn4(a, b, out=y))):  # DLT_TN4_BK picks the stage depth
+                          ("fwd", lambda: hip.gemm_fwd(a, b, out=y))):
             if fn is None:
                 row.append(f"{label} -")
                 continue
             us = timed(fn, args.iters)
             row.append(f"{label} {us:7.1f} us {flops / us / 1e6:6.0f} TF")
         ref = (a.float() @ b.float().t())
-        hip.gemm_tn4(a, b, out=y)
+        hip.gemm_fwd(a, b, out=y)
         err = ((y.float() - ref).norm() / ref.norm()).item()
-        print(" | ".join(row) + f" | tn4 relerr {err:.1e}", flush=True)
+        print(" | ".join(row) + f" | fwd relerr {err:.1e}", flush=True)
 
 
 if __name__ == "__main__":
