@@ -823,6 +823,7 @@ class GPTEngine:
         inv_ce = 1.0 / st.ce_scale  # the pre-scaled CE gradient (fp16), see ce_grad_scale
         head_ev = None
         head_add = None  # the window's lm_head weight gradient, added after the scatter-adds
+        head_taken = False  # ... or by the DDP runtime after its own reduction (head_wgrad_ready)
         head_late = None  # overlapped backwards: the per-micro-step head wgrad waits for "embed"
         head_acc = None  # chunked head: this micro-step's lm_head weight gradient (fp32)
         if st.dnf is not None:
@@ -884,6 +885,11 @@ class GPTEngine:
                         head_ev.record()
                 else:
                     issue_head()
+                # a data-parallel provider may take the lm_head part over now (its own early
+                # all-reduce, added after the embedding part's reduction: parallel/ddp.py)
+                take = getattr(getattr(prov, "hooks", None), "head_wgrad_ready", None)
+                if take is not None and take(head_add, side):
+                    head_taken = True
         st.dlogits = None
         key_last = self._keys(st.micro, L - 1)[2]
         # The side stream lags the dgrad chain by a few layers' worth of weight-gradient
@@ -905,7 +911,7 @@ class GPTEngine:
             if head_late is not None:
                 gm.wgrad_acc(hg.embed, *head_late)
             ops.embedding_bwd(st.ids, g_x2n if early_head else g_x2, hg.embed)
-            if head_add is not None:
+            if head_add is not None and not head_taken:
                 hg.embed.add_(head_add)
             if head_acc is not None:
                 hg.embed.add_(head_acc)

@@ -22,6 +22,17 @@ differently, by design for an 8x MI355X xGMI full mesh:
   is applied inside the AdamW kernel together with the clip coefficient.
 * Optional ``reduce_dtype=torch.bfloat16`` halves the bytes on the wire (the fp32
   accumulation buffer is kept; bf16 is only the transport).
+* **Split head bucket.**  The tied embedding / lm_head gradient has two parts: the
+  lm_head weight gradient (dense [Vp, H], one GEMM at the START of the window's last
+  backward, ``GPTEngine`` deferred head) and the embedding scatter-add (at its END, only
+  the rows of tokens in the batch).  The engine hands the lm_head part over
+  (:meth:`head_wgrad_ready`): it is all-reduced right away, overlapped with the whole
+  layer backward, and added in :meth:`finish`.  The embedding part is reduced row-sparse:
+  the ranks agree on the union of their non-zero rows (one byte per row, MAX all-reduce)
+  and all-reduce only those rows -- dense when the union covers over half of the rows
+  (uniform random tokens at W = 8).  Before round 6 the whole 154 MB fp32 head bucket was
+  reduced after the embedding backward with nothing left to overlap
+  (``profiles/r5_comm_model.md``: 0.6-1.3 ms exposed at W = 8).
 """
 from __future__ import annotations
 
@@ -48,6 +59,14 @@ class DDPRuntime:
         self.force = dist.is_initialized() and self.world == 1 and os.environ.get("DLT_FORCE_COLLECTIVES") == "1"
         self.launched = 0
         self.handles: List[Tuple[object, Optional[torch.Tensor], int, int]] = []
+        # the lm_head part of the tied gradient taken over this step (head_wgrad_ready):
+        # (work, buffer, transport tensor or None), added into the grad in finish()
+        self.head_parts: List[Tuple[object, torch.Tensor, Optional[torch.Tensor]]] = []
+        # row-sparse embedding reductions in flight: (work, rows, index, a, b, H)
+        self.row_handles: List[Tuple[object, torch.Tensor, torch.Tensor, int, int, int]] = []
+        self.split_head = os.environ.get("DLT_DDP_SPLIT_HEAD", "1") != "0"
+        self.sparse_rows_max = float(os.environ.get("DLT_DDP_SPARSE_ROWS", "0.5"))  # union share for sparse
+        self.last_head = None  # how the last embedding bucket was reduced: "dense" / ("rows", U, Vp)
         lay = store.layout
         elem = store.grad.element_size()
         cap = max(1, int(bucket_cap_mb * 1024 * 1024 / elem))
@@ -65,6 +84,8 @@ class DDPRuntime:
             i = j - 1
         # embedding (tied lm_head) + all norm weights: final after the embedding bwd
         self.fire_at.setdefault("head", []).append((lay.embed_offset, lay.total))
+        self.embed_range = (lay.embed_offset, lay.decay_end)
+        self.hidden = store.cfg.hidden_size
         self.buckets = [b for v in self.fire_at.values() for b in v]
         if broadcast_init and (self.world > 1 or self.force):
             self.broadcast_parameters()
@@ -107,7 +128,53 @@ class DDPRuntime:
         if not self.sync or (self.world == 1 and not self.force):
             return
         for (a, b) in self.fire_at.get(unit, ()):
+            if unit == "head" and self.head_parts:
+                # the grad region holds only the embedding scatter-add (+ the norm weights)
+                ea, eb = self.embed_range
+                self._launch_rows(ea, eb, self.hidden)
+                if b > eb:
+                    self._launch(eb, b)
+            else:
+                self._launch(a, b)
+
+    def head_wgrad_ready(self, buf: torch.Tensor, stream=None) -> bool:
+        """The engine's lm_head weight gradient of this step's window ([Vp, H] fp32, a
+        buffer of its own, ``stream`` = where it was computed): all-reduce it now and add it
+        in :meth:`finish`.  Returns False (the engine adds it itself) when nothing is
+        reduced this micro-step or the split is off (``DLT_DDP_SPLIT_HEAD=0``)."""
+        if not (self.split_head and self.sync and (self.world > 1 or self.force)):
+            return False
+        ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+        with ctx:
+            self.launched += 1
+            if self.reduce_dtype != buf.dtype:
+                t = buf.to(self.reduce_dtype)
+                h = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+            else:
+                t = None
+                h = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+        self.head_parts.append((h, buf, t))
+        return True
+
+    def _launch_rows(self, a: int, b: int, H: int) -> None:
+        """All-reduce the rows of grad[a:b] (a [rows, H] matrix) that are non-zero on any
+        rank; rows zero on every rank stay zero (their sum).  One byte per row is MAX-
+        reduced first so every rank gathers the same rows (a host sync on the row count)."""
+        g = self.store.grad[a:b].view(-1, H)
+        touched = (g != 0).any(dim=1).to(torch.uint8)
+        dist.all_reduce(touched, op=dist.ReduceOp.MAX, group=self.pg)
+        idx = touched.nonzero().squeeze(1)
+        if idx.numel() > self.sparse_rows_max * g.shape[0]:
+            self.last_head = "dense"
             self._launch(a, b)
+            return
+        self.last_head = ("rows", int(idx.numel()), int(g.shape[0]))
+        self.launched += 1
+        rows = g.index_select(0, idx)
+        if self.reduce_dtype != rows.dtype:
+            rows = rows.to(self.reduce_dtype)
+        h = dist.all_reduce(rows, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+        self.row_handles.append((h, rows, idx, a, b, H))
 
     def _launch(self, a: int, b: int) -> None:
         self.launched += 1
@@ -129,7 +196,8 @@ class DDPRuntime:
         self.finish()
 
     def finish(self) -> None:
-        """Wait for every outstanding bucket (makes the current stream wait on RCCL)."""
+        """Wait for every outstanding bucket (makes the current stream wait on RCCL), then
+        add the reduced lm_head part of the tied gradient."""
         for (h, t, a, b) in self.handles:
             h.wait()
             if t is not None:
@@ -137,6 +205,23 @@ class DDPRuntime:
                     t.record_stream(torch.cuda.current_stream(t.device))
                 self.store.grad[a:b].copy_(t)
         self.handles.clear()
+        for (h, rows, idx, a, b, H) in self.row_handles:
+            h.wait()
+            g = self.store.grad[a:b].view(-1, H)
+            g.index_copy_(0, idx, rows.to(g.dtype))
+        self.row_handles.clear()
+        if self.head_parts:
+            ea, eb = self.embed_range
+            emb = self.store.grad[ea:eb].view_as(self.head_parts[0][1])
+            for (h, buf, t) in self.head_parts:
+                h.wait()
+                if t is not None:
+                    if t.is_cuda:
+                        t.record_stream(torch.cuda.current_stream(t.device))
+                    buf.copy_(t)
+                # the engine's order without collectives: embedding scatter-add, then + lm_head part
+                emb.add_(buf)
+            self.head_parts.clear()
 
     @property
     def collectives(self) -> bool:

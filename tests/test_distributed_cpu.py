@@ -454,23 +454,38 @@ def _count_worker(rank, world, mode, strategy="FULL_SHARD"):
         for n in names:
             setattr(dist, n, orig[n])
     if mode == "ddp":
-        return log, [b - a for a, b in tr.ddp.buckets], tr.store.flat.numel()
+        lay = tr.store.layout
+        info = dict(buckets=[b - a for a, b in tr.ddp.buckets], total=tr.store.flat.numel(), embed=lay.embed_offset,
+                    decay_end=lay.decay_end, H=cfg.hidden_size, Vp=cfg.vocab_size_padded, head=tr.ddp.last_head)
+        return log, info, None
     units = {str(uid): (u.padded, u.shard) for uid, u in tr.runtime.units.items()}
     return log, units, cfg.num_layers
 
 
 def test_ddp_collective_pattern_per_step():
-    """SURVEY §2.4 X3/X4 on 2 gloo ranks: one optimizer step (2 micro-steps) issues one fp32
-    all-reduce per bucket -- only in the last micro-step (no_sync), covering the flat
-    gradient buffer exactly once -- plus the logged global loss (one scalar); no per-step
-    buffer broadcast (X3 is dropped by design) and nothing else."""
-    for log, buckets, total in run_multiprocess(_count_worker, world=2, args=("ddp",)):
+    """SURVEY §2.4 X3/X4 on 2 gloo ranks: one optimizer step (2 micro-steps) issues its
+    gradient all-reduces only in the last micro-step (no_sync): one fp32 all-reduce per
+    layer bucket, the lm_head part of the tied gradient ([Vp, H], handed over by the engine
+    at the start of the last backward), the embedding part row-sparse (one byte per row
+    MAX-reduced, then only the union of non-zero rows -- or dense when the union exceeds
+    half the rows), the norm weights, plus the logged global loss (one scalar).  No
+    per-step buffer broadcast (X3 is dropped by design)."""
+    for log, d, _ in run_multiprocess(_count_worker, world=2, args=("ddp",)):
         ar = [x for x in log if x[0] == "all_reduce"]
         assert len(log) == len(ar), log  # no broadcast / gather / reduce-scatter per step
-        big = [x for x in ar if x[1] > 1]
-        assert sorted(x[1] for x in big) == sorted(buckets) and len(buckets) > 2
-        assert sum(x[1] for x in big) == total and all(x[2] == 4 for x in big)
-        assert len(ar) - len(big) == 1  # the global-loss scalar
+        H, Vp = d["H"], d["Vp"]
+        layer = [b for b in d["buckets"] if b <= d["embed"]]
+        sizes = [x[1] for x in ar]
+        # layer buckets first, in backward order, fp32, covering the layer region once
+        assert sum(x[1] for x in ar if x[1] in layer and x[2] == 4) >= d["embed"]
+        assert Vp * H in sizes  # the lm_head part (or a dense embedding part too)
+        assert [x for x in ar if x[2] == 1] == [("all_reduce", Vp, 1)]  # the union bitmap
+        head = d["head"]
+        assert head == "dense" or (head[0] == "rows" and 0 < head[1] <= Vp // 2 and head[2] == Vp), head
+        if head != "dense":
+            assert head[1] * H in sizes
+        assert d["total"] - d["decay_end"] in sizes  # the norm weights
+        assert sizes.count(1) == 1  # the global-loss scalar
 
 
 @pytest.mark.parametrize("strategy", ["FULL_SHARD", "SHARD_GRAD_OP"])
