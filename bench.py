@@ -58,6 +58,12 @@ def main():
     ap.add_argument("--memory_lean", action="store_true",
                     help="the trainer's --memory_lean (TrainingConfig.defer_roles='qkv,o'): gate/up, down "
                          "and lm_head weight gradients per chain, lower peak memory")
+    ap.add_argument("--memory_first", action="store_true",
+                    help="DDP: TrainingConfig.memory_first (lean + unfused micro-steps + SwiGLU output rewritten "
+                         "by the backward): the reference's per-GPU memory, lower tok/s")
+    ap.add_argument("--no_pipeline", action="store_true",
+                    help="DDP: TrainingConfig.pipeline_micro_steps=False (the micro-step chains run one after "
+                         "another: only one chain's activations live at a time)")
     ap.add_argument("--defer_roles", default=None,
                     help="DDP: TrainingConfig.defer_roles override ('none' = no weight gradient deferred to the "
                          "window: per-chain weight gradients, no slot buffers)")
@@ -98,7 +104,8 @@ def main():
                             max_steps=100000, mixed_precision=args.precision, micro_step_fusion=args.fusion,
                             defer_roles=(args.defer_roles if args.defer_roles not in (None, "none") else
                                          LEAN_DEFER_ROLES if args.memory_lean else "all"),
-                            defer_wgrad=args.defer_roles != "none")
+                            defer_wgrad=args.defer_roles != "none", pipeline_micro_steps=not args.no_pipeline,
+                            memory_first=args.memory_first)
         trainer = DistributedTrainer(cfg, tc)
     else:
         from distributed_llm_trainer_amd.training.configs import FSDPConfig, FSDPTrainingConfig
@@ -174,6 +181,8 @@ def main():
                        "grad_accum": args.grad_accum,
                        "micro_step_fusion": trainer.fusion_factor(args.grad_accum, args.batch_size, args.seq_len),
                        **({"memory_lean": True} if args.memory_lean else {}),
+                       **({"memory_first": True} if args.memory_first else {}),
+                       **({"pipeline_micro_steps": False} if args.no_pipeline else {}),
                        **({"defer_roles": args.defer_roles} if args.defer_roles else {}),
                        **({"cpu_offload": True} if args.cpu_offload else {})},
             "peak_gb_per_gpu": round(peak, 3), "final_loss": round(loss, 4),

@@ -206,6 +206,12 @@ class GPTEngine:
         # the extra s stores cost the step 1.2-1.5 % (785.2k vs 797.1k tok/s, three same-box
         # pairs; profiles/r4_memory_lean.md)
         self.s_ring = os.environ.get("DLT_S_RING", "0") == "1"
+        # memory-first (--memory_first): when the down projection's weight gradient runs in
+        # each micro-step's own backward (not deferred), the SwiGLU output s is not kept
+        # from the forward; the SwiGLU backward (fused into the down data gradient)
+        # rewrites it from the kept gu with the forward's arithmetic -- same bits -- for
+        # the down weight gradient (-100 MB per layer per 16k-token chain)
+        self.s_refill = os.environ.get("DLT_S_REFILL", "0") == "1"
         # lm_head + cross-entropy in row chunks (head_chunks > 0; 0 = the window's logits
         # stay resident for ONE lm_head weight-gradient GEMM over all its rows, on the
         # side stream during the backward).  Per micro-step, for each chunk of rows:
@@ -319,6 +325,10 @@ class GPTEngine:
         """The SwiGLU output lives in the slot ring (written by the backward), not in a
         per-layer slot from the forward."""
         return bool(self._ring) and self.s_ring and self._deferred(st, "down")
+
+    def _refill_s(self, st) -> bool:
+        """s is rewritten by the backward instead of kept (s_refill, see __init__)."""
+        return self.s_refill and not st.recompute and not self._deferred(st, "down")
 
     def _slot_buf(self, st, layer, name: str, M: int, N: int, device):
         # ffbb ring: the dY operands of layer i live in ring slot i % R (see _window_ffbb)
@@ -486,7 +496,7 @@ class GPTEngine:
             gu = gm.linear(n2, w.wgu)
             s = ops.swiglu_fwd(gu, out=s_slot)
         d_out = gm.linear(s, w.wdown)
-        if s_ring:
+        if s_ring or self._refill_s(st):
             s = None
         if save:
             c = _LayerCache(x=x, rstd1=rstd1, n1=n1, q=q, k=k, v=v, o=o, lse=lse,
@@ -961,6 +971,10 @@ class GPTEngine:
             # s ring: the SwiGLU backward also rewrites s (the down wgrad operand) into
             # layer i's ring slot, from the same gu with the forward's arithmetic
             s_kw = {"s_out": sb(i, "s", I)} if self._s_in_ring(st) else {}
+            s_new = None
+            if self._refill_s(st) and c.gu is not None:
+                s_new = torch.empty(M, I, dtype=c.gu.dtype, device=c.gu.device)
+                s_kw = {"s_out": s_new}
             if hasattr(gm, "linear_dgrad_swiglu"):  # down dgrad with the SwiGLU backward in its epilogue (when faster)
                 dgu = gm.linear_dgrad_swiglu(g_d, w.wdown, c.gu, ops, out=sb(i, "dgu", 2 * I), **s_kw)
             else:
@@ -1023,7 +1037,7 @@ class GPTEngine:
                 if side_ctx is not None:
                     side_ctx.__exit__(None, None, None)
                 if not dfr["down"]:
-                    _wgrad(gm, gr.wdown, g_d, c.s)
+                    _wgrad(gm, gr.wdown, g_d, c.s if s_new is None else s_new)
                 if not dfr["gu"]:
                     _wgrad(gm, gr.wgu, dgu, c.n2)
                 if not dfr["o"]:

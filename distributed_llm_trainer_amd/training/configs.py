@@ -55,6 +55,11 @@ class TrainingConfig:
     # 0 = auto (GPU engine: largest F with F*batch_size*seq <= 16384 tokens and >= 2
     # chains left to pipeline), 1 = off
     micro_step_fusion: int = 0
+    # --memory_first: the reference's per-GPU memory (8.2 GB at micro-batch 8) over speed --
+    # no weight gradient deferred (defer_roles "none", chunked lm_head), micro-steps run
+    # unfused (micro_step_fusion 0 -> 1), the SwiGLU output rewritten by the backward
+    # instead of kept (engine s_refill); profiles/r6_memory.md
+    memory_first: bool = False
     # engine path: record the optimizer step and apply it unit by unit where the next
     # forward first needs each unit ("inline": on that chain's stream; "stream": on a
     # stream of its own; "off": the reference's end-of-step update, weights final when

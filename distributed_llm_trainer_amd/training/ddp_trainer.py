@@ -114,6 +114,9 @@ class DistributedTrainer:
         if self.use_engine:
             act = self.dtype if self.device.type == "cuda" else None
             eng = self.model.enable_engine(seed=self.training_config.seed + 1000003 * self.rank, act_dtype=act)
+            if self.training_config.memory_first:
+                self.training_config.defer_roles = LEAN_DEFER_ROLES
+                eng.s_refill = True
             eng.defer_roles = parse_defer_roles(self.training_config.defer_roles)
             if "head" not in eng.defer_roles and not eng.head_chunks_env:
                 eng.head_chunks = 2  # memory-lean: chunked lm_head run in the forwards (GPTEngine)
@@ -132,7 +135,10 @@ class DistributedTrainer:
 
     def fusion_factor(self, GA: int, micro_bs: int, seq_len: int) -> int:
         gpu_engine = self.use_engine and self.device.type == "cuda"
-        return micro_step_fusion(self.training_config.micro_step_fusion, GA, micro_bs, seq_len, gpu_engine)
+        req = self.training_config.micro_step_fusion
+        if self.training_config.memory_first and req == 0:
+            req = 1  # one micro-step's activations per chain
+        return micro_step_fusion(req, GA, micro_bs, seq_len, gpu_engine)
 
     def chains_per_step(self) -> int:
         """Engine forwards per optimizer step (dropout streams are keyed by this count)."""
@@ -368,6 +374,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--profile", type=str, default=None, help="write a torch.profiler trace to this dir")
     p.add_argument("--metrics_jsonl", type=str, default=None)
     p.add_argument("--no_final_save", action="store_true")
+    p.add_argument("--memory_first", action="store_true",
+                   help="peak memory first: --memory_lean + unfused micro-steps + the SwiGLU output rewritten "
+                        "by the backward (TrainingConfig.memory_first; ~7 GB at the headline shape, "
+                        "profiles/r6_memory.md)")
     p.add_argument("--memory_lean", action="store_true",
                    help="no weight gradient deferred to the end of the accumulation window: every micro-step "
                         "chain runs its own (no [GA*M, N] slot buffers, no window-wide dlogits; lm_head in row "
@@ -403,6 +413,8 @@ def main(argv=None):
         model_config.max_seq_len = args.seq_len
     if args.memory_lean:
         tc.defer_roles = LEAN_DEFER_ROLES
+    if args.memory_first:
+        tc.memory_first = True
 
     trainer = DistributedTrainer(model_config, tc)
     if tc.resume_from:

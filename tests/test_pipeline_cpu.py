@@ -491,3 +491,22 @@ def test_attn_gemm_routes(monkeypatch):
         attn_gemm._need_fit(1, 1, 8192, 160)
     import inspect
     assert "reference." not in inspect.getsource(attn_gemm).split('"""', 2)[2]  # no reference-op route
+
+def test_memory_first_matches_memory_lean():
+    """TrainingConfig.memory_first (lean + unfused micro-steps + the SwiGLU output rewritten
+    by the backward instead of kept): same losses and weights as --memory_lean, bitwise on
+    the CPU ops (s is recomputed from the kept gu with the forward's arithmetic)."""
+    from distributed_llm_trainer_amd.training.configs import TrainingConfig
+    from distributed_llm_trainer_amd.training.ddp_trainer import LEAN_DEFER_ROLES, DistributedTrainer
+    torch.manual_seed(17)
+    data = [torch.randint(0, 256, (8, 32)) for _ in range(3)]
+    res = []
+    for first in (False, True):
+        tc = TrainingConfig(batch_size=2, gradient_accumulation_steps=4, warmup_steps=2, max_steps=10,
+                            defer_roles=LEAN_DEFER_ROLES, micro_step_fusion=1, memory_first=first)
+        tr = DistributedTrainer(tiny(), tc)
+        assert tr.model.engine.s_refill == first
+        losses = [tr.train_step({"input_ids": d})["loss"] for d in data]
+        res.append((losses, tr.flat_params().clone()))
+    assert res[0][0] == res[1][0]
+    assert torch.equal(res[0][1], res[1][1])
