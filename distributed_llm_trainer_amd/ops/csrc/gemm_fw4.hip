@@ -1,0 +1,356 @@
+// Forward projection GEMM, 4-wave 256 x 256 tile, one tile per workgroup (gfx950 / MI355X):
+//   C[M,N] = A[M,K] . B[N,K]^T   (both operands K-contiguous, fp32 accumulate)
+// -- the o, gate/up, down and lm_head forwards of /root/reference/src/models/gpt.py:239,
+// :278-281, :447.
+//
+// Why this shape (round 6).  In the two-chain training window a forward GEMM runs beside
+// the other chain's memory-bound kernels; a persistent grid starves them (profiles/
+// r6_gemm_fwd.md), so this kernel computes ONE tile per workgroup and hands its CU back
+// to the dispatcher after every tile.  Its main loop is built for the matrix pipe:
+//   * 256 threads = 4 waves (one per SIMD), each owning a 128 x 128 block of the tile:
+//     8 x 8 accumulators of v_mfma_f32_16x16x32_bf16 = all 256 AGPRs (the MFMAs are
+//     issued from inline asm with "+a" accumulators: the compiler's own MFMA selection
+//     splits 256 loop-carried accumulators over both register halves and copies them
+//     through v_accvgpr_read/write every iteration); 0.25 ds_read_b128 per MFMA;
+//   * BK = 32 stages in a ring of 4 x 32 KiB (A image, then B image): stage s + 4 is
+//     DMA'd into stage s's buffer while stage s computes, so three stages (96 KiB per CU)
+//     are in flight behind the one being consumed -- ~3 x 1000 cycles of L2 / MALL
+//     latency cover;
+//   * one barrier per stage: wait (counted vmcnt) for stage s + 1 and for this wave's
+//     fragment reads of stage s, barrier (every wave's reads of stage s's buffer are done,
+//     stage s + 1 visible), then 64 MFMAs on stage s's fragments with the 16 fragment
+//     reads of stage s + 1 and the 8 LDS-DMA pieces of stage s + 4 interleaved (two reads
+//     and one piece per 8-MFMA group); fragment registers alternate between two sets (the
+//     loop runs stages in pairs, the last four are peeled for the counted waits), so
+//     every instruction of the loop is inline asm in a fixed order;
+//   * LDS images with 64-byte rows (32 k): 16-byte chunk c of row r is stored at
+//     c ^ (2 * ((r >> 3) & 1)) -- a 16-lane group of ds_read_b128 (16 rows) covers all 64
+//     banks; the DMA is lane-linear on the LDS side, so the swizzle lives in the per-lane
+//     source offsets;
+//   * swapped product D = B_tile . A_tile^T, so a lane holds 4 consecutive columns of one
+//     output row; the epilogue stages each wave's 128 x 128 block in its own quarter of
+//     the ring (chunk-swizzled 256-byte rows) and stores whole row runs, 16 bytes a lane;
+//   * XCD row bands: block b runs on the XCD of b % 8 (round-robin dispatch; speed only):
+//     that XCD owns a band of tile rows and walks it column by column, so its A panels
+//     stay in its L2 and each B panel is fetched once per XCD.
+//
+// Requirements (launcher-checked): M % 256 == 0, N % 128 == 0, K % 64 == 0, K >= 128, rows
+// 16-byte aligned; a ragged last column tile (N % 256 == 128, the lm_head) clamps its B
+// rows and masks its stores.  HK: operand / output format, 0 = bf16, 1 = IEEE half.
+#include "common.h"
+
+#include <type_traits>
+#include <utility>
+
+namespace {
+
+constexpr int F4_BM = 256, F4_BN = 256, F4_BK = 64;
+constexpr int F4_IMG = 256 * F4_BK * 2;  // bytes of one operand image (32 KiB)
+constexpr int F4_BUF = 2 * F4_IMG;       // A image then B image (64 KiB)
+
+template <typename F, int... Is>
+__device__ __forceinline__ void f4_sfor_impl(F&& f, std::integer_sequence<int, Is...>) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+// compile-time loop: f(integral_constant<int, i>) for i = 0 .. N-1
+template <int N, typename F>
+__device__ __forceinline__ void f4_sfor(F&& f) {
+  f4_sfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+template <int HK>
+__device__ __forceinline__ void f4_mfma(floatx4_t& acc, const bf16x8_t& a, const bf16x8_t& b) {
+  if constexpr (HK == 0)
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+  else
+    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+template <int OFF>
+__device__ __forceinline__ void f4_read(bf16x8_t& dst, uint32_t addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%c2" : "=v"(dst) : "v"(addr), "i"(OFF));
+}
+
+// LDS-DMA of one 1 KiB piece (64 lanes x 16 B, lane-linear at the wave-uniform LDS byte
+// address lds) from SGPR base gbase + per-lane byte offset voff
+__device__ __forceinline__ void f4_dma(const void* gbase, uint32_t voff, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(gbase), "s"(lds)
+               : "memory");
+}
+
+typedef __bf16 f4_bf16x4_t __attribute__((ext_vector_type(4)));
+typedef _Float16 f4_f16x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t f4_u32x4_t __attribute__((ext_vector_type(4)));
+template <int HK>
+__device__ __forceinline__ uint2 f4_pack(const floatx4_t& v) {
+  if constexpr (HK == 0) return __builtin_bit_cast(uint2, __builtin_convertvector(v, f4_bf16x4_t));
+  else return __builtin_bit_cast(uint2, __builtin_convertvector(v, f4_f16x4_t));
+}
+
+struct F4Frags {
+  bf16x8_t a[8], b[8];  // m-tiles / n-tiles of one 32-deep stage
+};
+
+}  // namespace
+
+template <int HK, int SCHED>
+__global__ __launch_bounds__(256, 1) void k_gemm_fw4(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                     bf16_t* __restrict__ C, int M, int N, int K, int lda, int ldb,
+                                                     int ldc, int flags, unsigned long long* __restrict__ stamps) {
+  // diagnostic (stamps != nullptr, tools/bench_gemm_fwd.py --stamps): wave 0 records
+  // s_memrealtime (100 MHz) / s_memtime at start, after the prologue, after the main loop
+  // and after its stores landed, plus the hardware ids, into stamps[16 * blockIdx.x ..]
+  unsigned long long st_r[4], st_c[4];
+  const bool stamp = stamps != nullptr && threadIdx.x < 64;
+  if (stamp) { st_r[0] = __builtin_amdgcn_s_memrealtime(); st_c[0] = __builtin_amdgcn_s_memtime(); }
+  __shared__ __attribute__((aligned(16))) char lds[SCHED == 2 ? 5 * F4_IMG : 2 * F4_BUF];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid & 1, wn = wid >> 1;
+
+  // tile: XCD row bands (see the header), else row-major
+  const int ntm = M / F4_BM, ntn = (N + F4_BN - 1) / F4_BN;
+  const int bid = blockIdx.x;
+  int tm, tn;
+  if ((ntm & 7) == 0 && !(flags & 2)) {
+    const int R = ntm >> 3, x = bid & 7, j = bid >> 3;
+    tm = x * R + j % R;
+    tn = j / R;
+  } else {
+    tm = bid / ntn;
+    tn = bid - tm * ntn;
+  }
+  const int m0 = tm * F4_BM, n0 = tn * F4_BN;
+
+  // DMA piece j (0..7) of wave w: rows 64 w + 8 j + i / 8 of an operand image, lane i ->
+  // physical chunk i % 8 = logical chunk (i % 8) ^ (i / 8).  B rows past N re-read row
+  // N - 1 (their columns are not stored).
+  const int lr = lane >> 3, lc = (lane & 7) ^ lr;
+  uint32_t aoff[8], boff[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int row = 64 * wid + 8 * j + lr;
+    aoff[j] = (uint32_t)(row * lda + lc * 8) * 2u;
+    boff[j] = (uint32_t)((min(n0 + row, N - 1) - n0) * ldb + lc * 8) * 2u;
+  }
+  const bf16_t* Ab = A + (size_t)m0 * lda;
+  const bf16_t* Bb = B + (size_t)n0 * ldb;
+  const uint32_t lbase = (uint32_t)(uintptr_t)lds;
+  // LDS byte offsets of stage s's A and B images: SCHED 0 / 1 two 64 KiB stage buffers;
+  // SCHED 2 a ring of five 32 KiB image slots, A of stage s in slot 2s % 5, B in (2s + 1) % 5
+  auto slot_a = [&](int s) -> uint32_t {
+    if constexpr (SCHED == 2) return (uint32_t)(((2 * s) % 5) * F4_IMG);
+    else return (uint32_t)((s & 1) * F4_BUF);
+  };
+  auto slot_b = [&](int s) -> uint32_t {
+    if constexpr (SCHED == 2) return (uint32_t)(((2 * s + 1) % 5) * F4_IMG);
+    else return (uint32_t)((s & 1) * F4_BUF + F4_IMG);
+  };
+  // piece p of stage s: A pieces 0..7, B pieces 8..15
+  auto piece = [&](int s, int p) {
+    if (p < 8)
+      f4_dma(Ab + s * F4_BK, aoff[p], __builtin_amdgcn_readfirstlane(lbase + slot_a(s) + (64 * wid + 8 * p) * 128));
+    else
+      f4_dma(Bb + s * F4_BK, boff[p - 8],
+             __builtin_amdgcn_readfirstlane(lbase + slot_b(s) + (64 * wid + 8 * (p - 8)) * 128));
+  };
+
+  floatx4_t acc[8][8];  // [n-tile u][m-tile t]: D = B_tile . A_tile^T
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[u][t] = floatx4_t{0.f, 0.f, 0.f, 0.f};
+
+  // fragment of 16 rows x 32 k (half h of a stage): lane l reads row base + (l & 15),
+  // logical chunk 4 h + (l >> 4) at physical chunk (4 h + (l >> 4)) ^ (l & 7)
+  const uint32_t loff = (uint32_t)((lane & 15) * 128 + (((lane >> 4) ^ (lane & 7)) << 4));
+  const uint32_t fa_base = lbase + (uint32_t)(wm * 128 * 128);
+  const uint32_t fb_base = lbase + (uint32_t)(wn * 128 * 128);
+  // read slot r (0..15) of half h of stage s: slots 0..7 the n-tiles, 8..15 the m-tiles
+  auto read_slot = [&](auto r_c, int s, int h, F4Frags& f) {
+    constexpr int r = decltype(r_c)::value;
+    const uint32_t o = loff ^ (uint32_t)(64 * h);
+    if constexpr (r < 8) f4_read<r * 2048>(f.b[r], fb_base + slot_b(s) + o);
+    else f4_read<(r - 8) * 2048>(f.a[r - 8], fa_base + slot_a(s) + o);
+  };
+  auto mfma_group = [&](auto g_c, F4Frags& f) {
+    constexpr int g = decltype(g_c)::value;
+    f4_sfor<8>([&](auto u_c) {
+      constexpr int u = decltype(u_c)::value;
+      f4_mfma<HK>(acc[u][g], f.b[u], f.a[g]);
+    });
+  };
+
+  // one stage (64 deep): half 0 = 64 MFMAs on f0 (its k 0..31) with half 1's 16 fragment
+  // reads interleaved; then (NEXT) wait for stage s + 1 (this wave's only DMAs in flight)
+  // and for this wave's reads, barrier (every wave is done with stage s's buffer), half 1
+  // = 64 MFMAs on f1 with (DMA) stage s + 2's 16 pieces into stage s's buffer and (NEXT)
+  // stage s + 1's half-0 reads interleaved, two of each per 8-MFMA group
+  F4Frags f0, f1;
+  // 64 MFMAs of one half on f with hook(i) after MFMA i (i = 8 t + u)
+  auto half = [&](F4Frags& f, auto&& hook) {
+    f4_sfor<64>([&](auto i_c) {
+      constexpr int i = decltype(i_c)::value;
+      f4_mfma<HK>(acc[i & 7][i >> 3], f.b[i & 7], f.a[i >> 3]);
+      hook(i_c);
+    });
+  };
+  // one stage (64 deep), SCHED 0: half 0 = 64 MFMAs on f0 (its k 0..31) with half 1's 16
+  // fragment reads interleaved; then (NEXT) wait for stage s + 1 (this wave's only DMAs in
+  // flight) and this wave's reads, barrier (every wave is done with stage s's buffer);
+  // half 1 = 64 MFMAs on f1 with (DMA) stage s + 2's 16 pieces into stage s's buffer and
+  // (NEXT) stage s + 1's half-0 reads interleaved, two of each per 8-MFMA group.
+  // SCHED 1 (the 3-phase form): half 0 reads f1 over its first 48 MFMAs; barrier; half 1
+  // issues stage s + 2's pieces over its first 48 MFMAs, then waits for stage s + 1 only
+  // (vmcnt(16): the new pieces may fly), barrier, and reads stage s + 1's half-0 fragments
+  // one per MFMA over its last 16 -- stage s + 1 has a whole stage of DMA latency cover.
+  // SCHED 2 (five 32 KiB image slots): as SCHED 1, but stage s + 2's A image goes into the
+  // slot stage s - 1's B image freed, so its 8 pieces spread over half 0 (one per 8 MFMAs)
+  // and only the B pieces (into stage s's A slot) wait for the mid barrier: the 16 DMA
+  // issues per stage no longer crowd one half.
+  auto stage = [&](int s, auto next_c, auto dma_c) {
+    constexpr bool NEXT = decltype(next_c)::value, DMA = decltype(dma_c)::value;
+    if constexpr (SCHED == 0) {
+      f4_sfor<8>([&](auto g_c) {
+        constexpr int g = decltype(g_c)::value;
+        mfma_group(g_c, f0);
+        read_slot(std::integral_constant<int, 2 * g>{}, s, 1, f1);
+        read_slot(std::integral_constant<int, 2 * g + 1>{}, s, 1, f1);
+      });
+      if constexpr (NEXT) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      f4_sfor<8>([&](auto g_c) {
+        constexpr int g = decltype(g_c)::value;
+        mfma_group(g_c, f1);
+        if constexpr (DMA) {
+          piece(s + 2, 2 * g);
+          piece(s + 2, 2 * g + 1);
+        }
+        if constexpr (NEXT) {
+          read_slot(std::integral_constant<int, 2 * g>{}, s + 1, 0, f0);
+          read_slot(std::integral_constant<int, 2 * g + 1>{}, s + 1, 0, f0);
+        }
+      });
+    } else if constexpr (SCHED == 2) {
+      half(f0, [&](auto i_c) {
+        constexpr int i = decltype(i_c)::value;
+        if constexpr (DMA && i % 8 == 7) piece(s + 2, i / 8);
+        if constexpr (i % 3 == 2 && i / 3 < 16) read_slot(std::integral_constant<int, i / 3>{}, s, 1, f1);
+      });
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      half(f1, [&](auto i_c) {
+        constexpr int i = decltype(i_c)::value;
+        if constexpr (DMA && i % 6 == 0 && i / 6 < 8) piece(s + 2, 8 + i / 6);
+        if constexpr (NEXT && i == 47) {
+          if constexpr (DMA) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+        if constexpr (NEXT && i >= 48) read_slot(std::integral_constant<int, i - 48>{}, s + 1, 0, f0);
+      });
+    } else {
+      half(f0, [&](auto i_c) {
+        constexpr int i = decltype(i_c)::value;
+        if constexpr (i % 3 == 2 && i / 3 < 16) read_slot(std::integral_constant<int, i / 3>{}, s, 1, f1);
+      });
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      half(f1, [&](auto i_c) {
+        constexpr int i = decltype(i_c)::value;
+        if constexpr (DMA && i % 3 == 0 && i / 3 < 16) piece(s + 2, i / 3);
+        if constexpr (NEXT && i == 47) {
+          if constexpr (DMA) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+        if constexpr (NEXT && i >= 48) read_slot(std::integral_constant<int, i - 48>{}, s + 1, 0, f0);
+      });
+    }
+    // the next stage's first MFMAs read f0: this wave's half-0 reads must have landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+
+  const int ns = K / F4_BK;  // >= 2 (launcher-checked)
+  // prologue: stages 0 and 1 in flight, stage 0 landed, its half-0 fragments read
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int p = 0; p < 16; ++p) piece(s, p);
+  asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+  f4_sfor<16>([&](auto r_c) { read_slot(r_c, 0, 0, f0); });
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (stamp) { st_r[1] = __builtin_amdgcn_s_memrealtime(); st_c[1] = __builtin_amdgcn_s_memtime(); }
+
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  int s = 0;
+#pragma unroll 1
+  for (; s + 2 < ns; ++s) stage(s, T_{}, T_{});
+  stage(s, T_{}, F_{});
+  stage(s + 1, F_{}, F_{});
+  if (stamp) { st_r[2] = __builtin_amdgcn_s_memrealtime(); st_c[2] = __builtin_amdgcn_s_memtime(); }
+
+  // epilogue: 16 wait states for the last MFMAs' accumulators, every wave done with the ring;
+  // wave w stages its 128 x 128 block in bytes [32 KiB w, 32 KiB (w + 1)): row r (256 bytes),
+  // 16-byte chunk c at c ^ (r & 15)
+  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+  asm volatile("s_barrier" ::: "memory");
+  char* const stg = lds + wid * 32768;
+  const int l16 = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = 16 * t + l16, c = 2 * u + (q >> 1);
+      *reinterpret_cast<uint2*>(stg + r * 256 + ((c ^ (r & 15)) << 4) + (q & 1) * 8) = f4_pack<HK>(acc[u][t]);
+    }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's own block only
+  const int ch = lane & 15, r0 = lane >> 4;
+  const int col = n0 + wn * 128 + ch * 8;
+  const bool col_ok = col < N;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(C + (size_t)(m0 + wm * 128) * ldc, 0, 128 * ldc * 2, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const int r = 4 * i + r0;
+    const f4_u32x4_t v = *reinterpret_cast<const f4_u32x4_t*>(stg + r * 256 + ((ch ^ (r & 15)) << 4));
+    const int off = (r * ldc + col) * 2;
+    if (col_ok) {
+      if (flags & 1) __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 16);  // sc1 write-through
+      else __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
+    }
+  }
+  if (stamp) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st_r[3] = __builtin_amdgcn_s_memrealtime();
+    st_c[3] = __builtin_amdgcn_s_memtime();
+    unsigned long long* o = stamps + 16 * (size_t)blockIdx.x;
+    if (lane < 4) {
+      o[lane] = lane == 0 ? st_r[0] : lane == 1 ? st_r[1] : lane == 2 ? st_r[2] : st_r[3];
+      o[4 + lane] = lane == 0 ? st_c[0] : lane == 1 ? st_c[1] : lane == 2 ? st_c[2] : st_c[3];
+    }
+    if (lane == 0) {
+      unsigned hw, xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      o[8] = hw;
+      o[9] = xcc;
+      o[10] = (unsigned long long)((tm << 16) | tn);
+    }
+  }
+}
+
+// flags: 1 = write-through C stores, 2 = row-major tile order (A/B knob), 16 = SCHED 1, 64 = SCHED 2
+DLT_API int dlt_gemm_fw4(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K, int lda, int ldb, int ldc,
+                         int flags, int hk, unsigned long long* stamps, hipStream_t st) {
+  if (M <= 0 || N <= 0 || K <= 0 || M % F4_BM || N % 128 || K % F4_BK || K < 2 * F4_BK || lda % 8 || ldb % 8 ||
+      ldc % 8 || lda < K || ldb < K || ldc < N)
+    return -1;
+  const long tiles = (long)(M / F4_BM) * ((N + F4_BN - 1) / F4_BN);
+  if (tiles > 0x7fffffff || 128L * ldc * 2 > 0x7fffffffL || 256L * lda * 2 > 0xffffffffL ||
+      256L * ldb * 2 > 0xffffffffL)
+    return -1;
+  if (flags & 64)
+    DLT_HK_DISPATCH(hk, k_gemm_fw4<HKC, 2><<<(int)tiles, 256, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, stamps));
+  else if (flags & 16)
+    DLT_HK_DISPATCH(hk, k_gemm_fw4<HKC, 1><<<(int)tiles, 256, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, stamps));
+  else
+    DLT_HK_DISPATCH(hk, k_gemm_fw4<HKC, 0><<<(int)tiles, 256, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, stamps));
+  DLT_CHECK_LAUNCH();
+}

@@ -66,6 +66,8 @@ _SIGS = {
                          c_void_p],
     "dlt_gemm_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                      c_void_p],
+    "dlt_gemm_fw4": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                     c_void_p],
     "dlt_gemm_bf16_qkv_rope": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                                c_void_p],
     "dlt_gemm_bf16_gu_swiglu": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
@@ -915,6 +917,38 @@ def gemm_fwd(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = Non
     c = torch.empty(M, N, dtype=a.dtype, device=a.device) if out is None else out
     _req(c, a.dtype, "gemm_fwd.c", M * N)
     _chk(lib().dlt_gemm_fwd(_p(a), _p(b), _p(c), M, N, K, K, K, N, _FWD_FLAGS, _FWD_BN, hk, _stream()), "gemm_fwd")
+    return c
+
+
+def gemm_fw4_fits(M: int, N: int, K: int) -> bool:
+    """Shapes the 4-wave 256 x 256 forward GEMM (csrc/gemm_fw4.hip) tiles."""
+    return M > 0 and N > 0 and K > 0 and M % 256 == 0 and N % 128 == 0 and K % 64 == 0 and K >= 128
+
+
+# launch flags of k_gemm_fw4: 1 = write-through (sc1) C stores, 2 = row-major tile order
+_FW4_FLAGS = int(os.environ.get("DLT_GEMM_FW4_FLAGS", "1"))
+
+
+def gemm_fw4(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
+             flags: Optional[int] = None, stamps: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """C[M,N] = A[M,K] @ B[N,K]^T (bf16 or fp16 in/out, fp32 accumulate) with the 4-wave
+    256 x 256 one-tile-per-workgroup MFMA kernel (128 x 128 per wave, AGPR accumulators).
+    Returns None (nothing launched) when the shape does not tile (M % 256, N % 128, K % 64,
+    K < 128)."""
+    M, K = a.shape
+    N = b.shape[0]
+    if not gemm_fw4_fits(M, N, K) or b.shape[1] != K:
+        return None
+    hk = _req_act(a, a.dtype, "gemm_fw4.a")
+    _req(b, a.dtype, "gemm_fw4.b")
+    c = torch.empty(M, N, dtype=a.dtype, device=a.device) if out is None else out
+    _req(c, a.dtype, "gemm_fw4.c", M * N)
+    fl = _FW4_FLAGS if flags is None else flags
+    if stamps is not None:  # diagnostic: int64 [tiles, 16] per-workgroup timestamps (csrc/gemm_fw4.hip)
+        if stamps.dtype != torch.int64 or stamps.numel() < 16 * (M // 256) * ((N + 255) // 256) or not stamps.is_cuda:
+            raise ValueError("gemm_fw4: stamps must be a CUDA int64 tensor of 16 * tiles entries")
+    _chk(lib().dlt_gemm_fw4(_p(a), _p(b), _p(c), M, N, K, K, K, N, fl, hk,
+                            _p(stamps) if stamps is not None else None, _stream()), "gemm_fw4")
     return c
 
 

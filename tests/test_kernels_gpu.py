@@ -605,6 +605,40 @@ def test_gemm_fwd(M, N, K, dtype, monkeypatch):
     assert hip.gemm_fwd(a, b[:N - 8].contiguous()) is None  # N % 128
 
 
+# K = 128 (two stages: no steady-state loop iteration), 192 (three) and 768 / 3072 (the
+# projections); ragged last column tile (N % 256 = 128); tile-row counts that are and are
+# not multiples of 8
+@pytest.mark.parametrize("M,N,K", [(16384, 2304, 768), (16384, 768, 3072), (4096, 6144, 768), (2048, 50304, 768),
+                                   (768, 1280, 512), (256, 256, 128), (1280, 640, 192), (2048, 384, 256)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_gemm_fw4(M, N, K, dtype):
+    """4-wave 256 x 256 MFMA GEMM C = A B^T (csrc/gemm_fw4.hip, AGPR accumulators, every
+    schedule) vs fp32 torch, bf16 and fp16 operands: every element within 16-bit output
+    rounding, every tile written exactly once (a poisoned output is fully overwritten),
+    plain and write-through stores, XCD-band and row-major tile orders; the diagnostic
+    stamps leave the result unchanged."""
+    torch.manual_seed(M + N + K)
+    a = (torch.rand(M, K, device=DEV) * 2 - 1).to(dtype)
+    b = (torch.rand(N, K, device=DEV) * 2 - 1).to(dtype)
+    want = a.float() @ b.float().t()
+    first = None
+    for flags in (1, 0, 2, 17, 16, 65, 64, 66):
+        c = torch.full((M, N), float("nan"), device=DEV, dtype=dtype)
+        assert hip.gemm_fw4(a, b, out=c, flags=flags) is not None
+        assert not torch.isnan(c).any(), f"unwritten output (flags {flags})"
+        assert _relerr(c, want) < 8e-3
+        _close(c, want, 8e-3 * want.abs().max().item(), 8e-3, f"gemm_fw4 flags {flags}")
+        if first is None:
+            first = c
+        assert torch.equal(c, first), f"schedules / store flavours must agree bitwise (flags {flags})"
+    st = torch.zeros((M // 256) * ((N + 255) // 256), 16, dtype=torch.int64, device=DEV)
+    c = torch.empty(M, N, device=DEV, dtype=dtype)
+    hip.gemm_fw4(a, b, out=c, flags=64, stamps=st)
+    assert torch.equal(c, first) and bool((st[:, 3] >= st[:, 0]).all())
+    assert hip.gemm_fw4(a[:, :K - 32].contiguous(), b[:, :K - 32].contiguous()) is None  # K % 64
+    assert hip.gemm_fw4(a, b[:N - 8].contiguous()) is None  # N % 128
+
+
 @pytest.fixture(params=[0, 4096], ids=["stage-in-loop", "epilogue-first"])
 def gemm_late_flag(request, monkeypatch):
     """Runs a test with and without flags bit 4096 (epilogue-first staging of the next

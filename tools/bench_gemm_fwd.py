@@ -1,6 +1,6 @@
 """Isolated timing of the forward projection GEMMs at the headline chain shape (M = 16384):
 hipBLASLt (the planner's library path) vs the persistent hand kernel (k_gemm_bf16) vs the
-one-tile-per-workgroup 256 x 128 kernel (k_gemm_fwd).  Mean of --iters launches after
+one-tile-per-workgroup kernels (k_gemm_fwd 8-wave, k_gemm_fw4 4-wave 128 x 128 per wave).  Mean of --iters launches after
 warmup, CUDA events.  usage: python tools/bench_gemm_fwd.py [--iters 50]"""
 import argparse
 import os
@@ -31,9 +31,18 @@ def timed(fn, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--shapes", default=",".join(SHAPES), help="comma list of SHAPES keys")
+    ap.add_argument("--impls", default="lib,bf16,fwd,fw4", help="comma list of lib / bf16 / fwd / fw4")
+    ap.add_argument("--stamp_flags", type=int, default=16, help="k_gemm_fw4 flags of the --stamps runs")
+    ap.add_argument("--stamps", action="store_true",
+                    help="diagnostic: per-workgroup timestamps of k_gemm_fw4 (SCHED 1) on each shape")
     args = ap.parse_args()
+    impls = args.impls.split(",")
+    if args.stamps:
+        return stamps(args)
     g = gemm.HipGemm()
-    for name, (M, N, K) in SHAPES.items():
+    for name in args.shapes.split(","):
+        M, N, K = SHAPES[name]
         a = torch.randn(M, K, device="cuda").bfloat16()
         b = torch.randn(N, K, device="cuda").bfloat16()
         y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
@@ -41,16 +50,66 @@ def main():
         row = [f"{name:8s} {M}x{N}x{K}:"]
         for label, fn in (("lib", lambda: g._lib_linear(a, b, y)),
                           ("bf16", (lambda: hip.gemm_bf16(a, b, out=y)) if hip.gemm_bf16_fits(M, N, K) else None),
-                          ("fwd", lambda: hip.gemm_fwd(a, b, out=y))):
+                          ("fwd", lambda: hip.gemm_fwd(a, b, out=y)),
+                          ("fw4", lambda: hip.gemm_fw4(a, b, out=y)),
+                          ("fw4s1", lambda: hip.gemm_fw4(a, b, out=y, flags=hip._FW4_FLAGS | 16)),
+                          ("fw4s2", lambda: hip.gemm_fw4(a, b, out=y, flags=hip._FW4_FLAGS | 64)),
+                          ("fw4s2w", lambda: hip.gemm_fw4(a, b, out=y, flags=64))):
+            if label not in impls:
+                continue
             if fn is None:
                 row.append(f"{label} -")
                 continue
             us = timed(fn, args.iters)
             row.append(f"{label} {us:7.1f} us {flops / us / 1e6:6.0f} TF")
         ref = (a.float() @ b.float().t())
-        hip.gemm_fwd(a, b, out=y)
-        err = ((y.float() - ref).norm() / ref.norm()).item()
-        print(" | ".join(row) + f" | fwd relerr {err:.1e}", flush=True)
+        errs = []
+        for label, fn in (("fwd", hip.gemm_fwd), ("fw4", hip.gemm_fw4),
+                          ("fw4s1", lambda a, b, out: hip.gemm_fw4(a, b, out=out, flags=hip._FW4_FLAGS | 16)),
+                          ("fw4s2", lambda a, b, out: hip.gemm_fw4(a, b, out=out, flags=hip._FW4_FLAGS | 64))):
+            if label not in impls:
+                continue
+            y.fill_(float("nan"))
+            fn(a, b, out=y)
+            errs.append(f"{label} relerr {((y.float() - ref).norm() / ref.norm()).item():.1e}")
+        print(" | ".join(row + errs), flush=True)
+
+
+def stamps(args):
+    """Per-workgroup phase times of k_gemm_fw4 from its diagnostic stamps: prologue (start ->
+    first fragments in registers), main loop, epilogue (-> stores landed), in us of
+    s_memrealtime (100 MHz) and loop shader-clock cycles; plus the idle gap between a
+    workgroup's end and the next start on the same CU (hardware id)."""
+    import statistics as stt
+    for name in args.shapes.split(","):
+        M, N, K = SHAPES[name]
+        a = torch.randn(M, K, device="cuda").bfloat16()
+        b = torch.randn(N, K, device="cuda").bfloat16()
+        y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        tiles = (M // 256) * ((N + 255) // 256)
+        st = torch.zeros(tiles, 16, dtype=torch.int64, device="cuda")
+        for _ in range(3):
+            hip.gemm_fw4(a, b, out=y, flags=hip._FW4_FLAGS | args.stamp_flags, stamps=st)
+        torch.cuda.synchronize()
+        s = st.cpu().tolist()
+        t0 = min(r[0] for r in s)
+        pro = [(r[1] - r[0]) / 100 for r in s]
+        loop = [(r[2] - r[1]) / 100 for r in s]
+        epi = [(r[3] - r[2]) / 100 for r in s]
+        cyc = [r[6] - r[5] for r in s]
+        span = (max(r[3] for r in s) - t0) / 100
+        clk = stt.median([(r[6] - r[5]) / max(1, r[2] - r[1]) * 100 / 1000 for r in s])  # GHz
+        by_cu = {}
+        for r in s:
+            by_cu.setdefault((r[9], r[8] & 0xFFFF), []).append((r[0], r[3]))
+        gaps = []
+        for v in by_cu.values():
+            v.sort()
+            gaps += [(v[i + 1][0] - v[i][1]) / 100 for i in range(len(v) - 1)]
+        q = lambda x: f"med {stt.median(x):6.2f} p10 {sorted(x)[len(x) // 10]:6.2f} p90 {sorted(x)[9 * len(x) // 10]:6.2f}"  # noqa: E731
+        print(f"{name} {M}x{N}x{K}: {tiles} tiles, span {span:.1f} us, CUs seen {len(by_cu)}, loop clock {clk:.2f} GHz")
+        print(f"   prologue us {q(pro)} | loop us {q(loop)} | epilogue us {q(epi)}")
+        print(f"   loop kcycles {q([c / 1000 for c in cyc])} | CU idle gap us {q(gaps) if gaps else '-'}", flush=True)
 
 
 if __name__ == "__main__":
