@@ -47,6 +47,11 @@ namespace {
 constexpr int F4_BM = 256, F4_BN = 256, F4_BK = 64;
 constexpr int F4_IMG = 256 * F4_BK * 2;  // bytes of one operand image (32 KiB)
 constexpr int F4_BUF = 2 * F4_IMG;       // A image then B image (64 KiB)
+// SCHED 4's B image: 32 pieces of 8 rows x 128 B, each padded to 1040 B (see the header)
+constexpr int F4_PIECE_BP = 1040;
+constexpr int F4_IMG_BP = 32 * F4_PIECE_BP;
+// SCHED 4's B swizzle: logical chunk c of a row of piece v (mod 16) sits at c ^ f4_fb(v)
+__device__ __forceinline__ int f4_fb(int v) { return ((v + 4) >> 3) & 1; }
 
 template <typename F, int... Is>
 __device__ __forceinline__ void f4_sfor_impl(F&& f, std::integer_sequence<int, Is...>) {
@@ -103,7 +108,11 @@ __global__ __launch_bounds__(256, 1) void k_gemm_fw4(const bf16_t* __restrict__ 
   unsigned long long st_r[4], st_c[4];
   const bool stamp = stamps != nullptr && threadIdx.x < 64;
   if (stamp) { st_r[0] = __builtin_amdgcn_s_memrealtime(); st_c[0] = __builtin_amdgcn_s_memtime(); }
-  __shared__ __attribute__((aligned(16))) char lds[SCHED == 2 ? 5 * F4_IMG : 2 * F4_BUF];
+  // EPI: interleaved B n-tiles + direct epilogue (SCHED 4: padded B pieces, conflict-free;
+  // SCHED 5: the five-slot ring, unpadded B with two-way bank conflicts on its reads)
+  constexpr bool EPI = SCHED == 4 || SCHED == 5, PAD = SCHED == 4, RING = SCHED == 3 || SCHED == 5;
+  constexpr int STG = PAD ? F4_IMG + F4_IMG_BP : F4_BUF;  // bytes of one stage buffer (2-buffer schedules)
+  __shared__ __attribute__((aligned(16))) char lds[RING ? 5 * F4_IMG : 2 * STG];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wid & 1, wn = wid >> 1;
@@ -131,7 +140,10 @@ __global__ __launch_bounds__(256, 1) void k_gemm_fw4(const bf16_t* __restrict__ 
   for (int j = 0; j < 8; ++j) {
     const int row = 64 * wid + 8 * j + lr;
     aoff[j] = (uint32_t)(row * lda + lc * 8) * 2u;
-    boff[j] = (uint32_t)((min(n0 + row, N - 1) - n0) * ldb + lc * 8) * 2u;
+    // SCHED 4: piece 8 w + j of the B image holds rows 8 v + u (v = piece % 16) of n-tile u
+    // (SCHED 5: logical chunk c of B-image row 8 v + u at c ^ (v & 7))
+    const int blc = PAD ? (lane & 7) ^ f4_fb((8 * wid + j) & 15) : EPI ? (lane & 7) ^ ((8 * wid + j) & 7) : lc;
+    boff[j] = (uint32_t)((min(n0 + row, N - 1) - n0) * ldb + blc * 8) * 2u;
   }
   const bf16_t* Ab = A + (size_t)m0 * lda;
   const bf16_t* Bb = B + (size_t)n0 * ldb;
@@ -139,12 +151,12 @@ __global__ __launch_bounds__(256, 1) void k_gemm_fw4(const bf16_t* __restrict__ 
   // LDS byte offsets of stage s's A and B images: SCHED 0 / 1 two 64 KiB stage buffers;
   // SCHED 2 a ring of five 32 KiB image slots, A of stage s in slot 2s % 5, B in (2s + 1) % 5
   auto slot_a = [&](int s) -> uint32_t {
-    if constexpr (SCHED == 2) return (uint32_t)(((2 * s) % 5) * F4_IMG);
-    else return (uint32_t)((s & 1) * F4_BUF);
+    if constexpr (RING) return (uint32_t)(((2 * s) % 5) * F4_IMG);
+    else return (uint32_t)((s & 1) * STG);
   };
   auto slot_b = [&](int s) -> uint32_t {
-    if constexpr (SCHED == 2) return (uint32_t)(((2 * s + 1) % 5) * F4_IMG);
-    else return (uint32_t)((s & 1) * F4_BUF + F4_IMG);
+    if constexpr (RING) return (uint32_t)(((2 * s + 1) % 5) * F4_IMG);
+    else return (uint32_t)((s & 1) * STG + F4_IMG);
   };
   // piece p of stage s: A pieces 0..7, B pieces 8..15
   auto piece = [&](int s, int p) {
@@ -152,7 +164,8 @@ __global__ __launch_bounds__(256, 1) void k_gemm_fw4(const bf16_t* __restrict__ 
       f4_dma(Ab + s * F4_BK, aoff[p], __builtin_amdgcn_readfirstlane(lbase + slot_a(s) + (64 * wid + 8 * p) * 128));
     else
       f4_dma(Bb + s * F4_BK, boff[p - 8],
-             __builtin_amdgcn_readfirstlane(lbase + slot_b(s) + (64 * wid + 8 * (p - 8)) * 128));
+             __builtin_amdgcn_readfirstlane(lbase + slot_b(s) +
+                                            (PAD ? (8 * wid + p - 8) * F4_PIECE_BP : (64 * wid + 8 * (p - 8)) * 128)));
   };
 
   floatx4_t acc[8][8];  // [n-tile u][m-tile t]: D = B_tile . A_tile^T
@@ -165,19 +178,29 @@ __global__ __launch_bounds__(256, 1) void k_gemm_fw4(const bf16_t* __restrict__ 
   // logical chunk 4 h + (l >> 4) at physical chunk (4 h + (l >> 4)) ^ (l & 7)
   const uint32_t loff = (uint32_t)((lane & 15) * 128 + (((lane >> 4) ^ (lane & 7)) << 4));
   const uint32_t fa_base = lbase + (uint32_t)(wm * 128 * 128);
-  const uint32_t fb_base = lbase + (uint32_t)(wn * 128 * 128);
+  // SCHED 4 n-tile u: rows 8 v + u of pieces wn * 16 + v (v = l & 15), chunk (4 h + q) ^ fb(v)
+  const uint32_t fb_base =
+      PAD   ? lbase + (uint32_t)((wn * 16 + (lane & 15)) * F4_PIECE_BP + (((lane >> 4) ^ f4_fb(lane & 15)) << 4))
+      : EPI ? (uint32_t)((wn * 128 + 8 * (lane & 15)) * 128 + (((lane >> 4) ^ (lane & 7)) << 4))  // + lbase at use
+            : lbase + (uint32_t)(wn * 128 * 128);
   // read slot r (0..15) of half h of stage s: slots 0..7 the n-tiles, 8..15 the m-tiles
   auto read_slot = [&](auto r_c, int s, int h, F4Frags& f) {
     constexpr int r = decltype(r_c)::value;
     const uint32_t o = loff ^ (uint32_t)(64 * h);
-    if constexpr (r < 8) f4_read<r * 2048>(f.b[r], fb_base + slot_b(s) + o);
-    else f4_read<(r - 8) * 2048>(f.a[r - 8], fa_base + slot_a(s) + o);
+    if constexpr (r < 8) {
+      if constexpr (PAD) f4_read<r * 128>(f.b[r], fb_base + slot_b(s) + (uint32_t)(64 * h));
+      else if constexpr (EPI) f4_read<r * 128>(f.b[r], lbase + (fb_base ^ (uint32_t)(64 * h)) + slot_b(s));
+      else f4_read<r * 2048>(f.b[r], fb_base + slot_b(s) + o);
+    } else {
+      f4_read<(r - 8) * 2048>(f.a[r - 8], fa_base + slot_a(s) + o);
+    }
   };
   auto mfma_group = [&](auto g_c, F4Frags& f) {
     constexpr int g = decltype(g_c)::value;
     f4_sfor<8>([&](auto u_c) {
       constexpr int u = decltype(u_c)::value;
-      f4_mfma<HK>(acc[u][g], f.b[u], f.a[g]);
+      if constexpr (EPI) f4_mfma<HK>(acc[u][g], f.a[g], f.b[u]);
+      else f4_mfma<HK>(acc[u][g], f.b[u], f.a[g]);
     });
   };
 
@@ -191,7 +214,8 @@ __global__ __launch_bounds__(256, 1) void k_gemm_fw4(const bf16_t* __restrict__ 
   auto half = [&](F4Frags& f, auto&& hook) {
     f4_sfor<64>([&](auto i_c) {
       constexpr int i = decltype(i_c)::value;
-      f4_mfma<HK>(acc[i & 7][i >> 3], f.b[i & 7], f.a[i >> 3]);
+      if constexpr (EPI) f4_mfma<HK>(acc[i & 7][i >> 3], f.a[i >> 3], f.b[i & 7]);
+      else f4_mfma<HK>(acc[i & 7][i >> 3], f.b[i & 7], f.a[i >> 3]);
       hook(i_c);
     });
   };
@@ -210,43 +234,39 @@ __global__ __launch_bounds__(256, 1) void k_gemm_fw4(const bf16_t* __restrict__ 
   // issues per stage no longer crowd one half.
   auto stage = [&](int s, auto next_c, auto dma_c) {
     constexpr bool NEXT = decltype(next_c)::value, DMA = decltype(dma_c)::value;
-    if constexpr (SCHED == 0) {
-      f4_sfor<8>([&](auto g_c) {
-        constexpr int g = decltype(g_c)::value;
-        mfma_group(g_c, f0);
-        read_slot(std::integral_constant<int, 2 * g>{}, s, 1, f1);
-        read_slot(std::integral_constant<int, 2 * g + 1>{}, s, 1, f1);
-      });
-      if constexpr (NEXT) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      f4_sfor<8>([&](auto g_c) {
-        constexpr int g = decltype(g_c)::value;
-        mfma_group(g_c, f1);
-        if constexpr (DMA) {
-          piece(s + 2, 2 * g);
-          piece(s + 2, 2 * g + 1);
-        }
-        if constexpr (NEXT) {
-          read_slot(std::integral_constant<int, 2 * g>{}, s + 1, 0, f0);
-          read_slot(std::integral_constant<int, 2 * g + 1>{}, s + 1, 0, f0);
-        }
-      });
-    } else if constexpr (SCHED == 2) {
+    if constexpr (RING) {
+      // SCHED 3: the barrier at MFMA 39 of half 1 and stage s + 1's reads over MFMAs 40..55
+      // (8 MFMAs of cover before the stage ends); the next half 0 waits per 8-MFMA group
+      // for exactly the fragments it uses (n-tiles first, then m-tile t before group t)
+      constexpr int BAR = 39;
       half(f0, [&](auto i_c) {
         constexpr int i = decltype(i_c)::value;
+        if constexpr (i % 8 == 7 && i < 63) {
+          // before group t = (i + 1) / 8: reads 0 .. 8 + t of f0 done; younger: the rest of
+          // f0's (7 - t) and the f1 reads issued so far (one per 3 MFMAs, i % 3 == 2)
+          constexpr int t = (i + 1) / 8;
+          constexpr int nf1 = (i + 1) / 3 < 16 ? (i + 1) / 3 : 16;
+          constexpr int X = (7 - t) + nf1 > 15 ? 15 : (7 - t) + nf1;
+          asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(X) : "memory");
+        }
         if constexpr (DMA && i % 8 == 7) piece(s + 2, i / 8);
         if constexpr (i % 3 == 2 && i / 3 < 16) read_slot(std::integral_constant<int, i / 3>{}, s, 1, f1);
       });
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       half(f1, [&](auto i_c) {
         constexpr int i = decltype(i_c)::value;
-        if constexpr (DMA && i % 6 == 0 && i / 6 < 8) piece(s + 2, 8 + i / 6);
-        if constexpr (NEXT && i == 47) {
+        if constexpr (DMA && i % 5 == 0 && i / 5 < 8) piece(s + 2, 8 + i / 5);
+        if constexpr (NEXT && i == BAR) {
           if constexpr (DMA) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
           else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
         }
-        if constexpr (NEXT && i >= 48) read_slot(std::integral_constant<int, i - 48>{}, s + 1, 0, f0);
+        if constexpr (NEXT && i > BAR && i <= BAR + 16) read_slot(std::integral_constant<int, i - BAR - 1>{}, s + 1, 0, f0);
       });
+      if constexpr (NEXT) {
+        // the next half 0's group 0 needs reads 0..8 (8 n-tiles + m-tile 0)
+        asm volatile("s_waitcnt lgkmcnt(7)" ::: "memory");
+        return;
+      }
     } else {
       half(f0, [&](auto i_c) {
         constexpr int i = decltype(i_c)::value;
@@ -287,33 +307,61 @@ __global__ __launch_bounds__(256, 1) void k_gemm_fw4(const bf16_t* __restrict__ 
   stage(s + 1, F_{}, F_{});
   if (stamp) { st_r[2] = __builtin_amdgcn_s_memrealtime(); st_c[2] = __builtin_amdgcn_s_memtime(); }
 
-  // epilogue: 16 wait states for the last MFMAs' accumulators, every wave done with the ring;
-  // wave w stages its 128 x 128 block in bytes [32 KiB w, 32 KiB (w + 1)): row r (256 bytes),
-  // 16-byte chunk c at c ^ (r & 15)
+  // epilogue: 16 wait states for the last MFMAs' accumulators
   asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
-  asm volatile("s_barrier" ::: "memory");
-  char* const stg = lds + wid * 32768;
   const int l16 = lane & 15, q = lane >> 4;
-#pragma unroll
-  for (int t = 0; t < 8; ++t)
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int r = 16 * t + l16, c = 2 * u + (q >> 1);
-      *reinterpret_cast<uint2*>(stg + r * 256 + ((c ^ (r & 15)) << 4) + (q & 1) * 8) = f4_pack<HK>(acc[u][t]);
-    }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's own block only
-  const int ch = lane & 15, r0 = lane >> 4;
-  const int col = n0 + wn * 128 + ch * 8;
-  const bool col_ok = col < N;
-  const auto rs = __builtin_amdgcn_make_buffer_rsrc(C + (size_t)(m0 + wm * 128) * ldc, 0, 128 * ldc * 2, 0x00020000);
-#pragma unroll
-  for (int i = 0; i < 32; ++i) {
-    const int r = 4 * i + r0;
-    const f4_u32x4_t v = *reinterpret_cast<const f4_u32x4_t*>(stg + r * 256 + ((ch ^ (r & 15)) << 4));
-    const int off = (r * ldc + col) * 2;
+  if constexpr (EPI) {
+    // SCHED 4 (product D = A_tile . B_tile^T): lane l, register r of tile (u, t) is output
+    // row 16 t + 4 (l >> 4) + r, column wn*128 + 8 (l & 15) + u (n-tile u holds columns
+    // 8 v + u), so the eight n-tiles give 8 consecutive columns and the 16 lanes of a row
+    // 256 contiguous bytes: one 16-byte store per (m-tile, r), 4 rows per instruction, no LDS
+    const int col = n0 + wn * 128 + 8 * l16;
+    const bool col_ok = n0 + wn * 128 < N;
+    const auto rs =
+        __builtin_amdgcn_make_buffer_rsrc(C + (size_t)(m0 + wm * 128) * ldc, 0, 128 * ldc * 2, 0x00020000);
     if (col_ok) {
-      if (flags & 1) __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 16);  // sc1 write-through
-      else __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          floatx4_t lo{acc[0][t][r], acc[1][t][r], acc[2][t][r], acc[3][t][r]};
+          floatx4_t hi{acc[4][t][r], acc[5][t][r], acc[6][t][r], acc[7][t][r]};
+          const uint2 a = f4_pack<HK>(lo), b = f4_pack<HK>(hi);
+          const f4_u32x4_t v{a.x, a.y, b.x, b.y};
+          const int off = ((16 * t + 4 * q + r) * ldc + col) * 2;
+          if (flags & 1) __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 16);  // sc1 write-through
+          else if (flags & 4) __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 2);  // nt
+          else __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
+        }
+    }
+  } else {
+    // wave w stages its 128 x 128 block in bytes [32 KiB w, 32 KiB (w + 1)) once every wave
+    // is done with the ring: row r (256 bytes), 16-byte chunk c at c ^ (r & 15)
+    asm volatile("s_barrier" ::: "memory");
+    char* const stg = lds + wid * 32768;
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int r = 16 * t + l16, c = 2 * u + (q >> 1);
+        *reinterpret_cast<uint2*>(stg + r * 256 + ((c ^ (r & 15)) << 4) + (q & 1) * 8) = f4_pack<HK>(acc[u][t]);
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's own block only
+    const int ch = lane & 15, r0 = lane >> 4;
+    const int col = n0 + wn * 128 + ch * 8;
+    const bool col_ok = col < N;
+    const auto rs =
+        __builtin_amdgcn_make_buffer_rsrc(C + (size_t)(m0 + wm * 128) * ldc, 0, 128 * ldc * 2, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const int r = 4 * i + r0;
+      const f4_u32x4_t v = *reinterpret_cast<const f4_u32x4_t*>(stg + r * 256 + ((ch ^ (r & 15)) << 4));
+      const int off = (r * ldc + col) * 2;
+      if (col_ok) {
+        if (flags & 1) __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 16);  // sc1 write-through
+        else if (flags & 4) __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 2);  // nt
+        else __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
+      }
     }
   }
   if (stamp) {
@@ -336,7 +384,8 @@ __global__ __launch_bounds__(256, 1) void k_gemm_fw4(const bf16_t* __restrict__ 
   }
 }
 
-// flags: 1 = write-through C stores, 2 = row-major tile order (A/B knob), 16 = SCHED 1, 64 = SCHED 2
+// flags: 1 = write-through (sc1) C stores, 4 = nt C stores, 2 = row-major tile order (A/B knob);
+// schedule: 16 = SCHED 1, 128 = SCHED 3, 144 = SCHED 5, else SCHED 4
 DLT_API int dlt_gemm_fw4(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K, int lda, int ldb, int ldc,
                          int flags, int hk, unsigned long long* stamps, hipStream_t st) {
   if (M <= 0 || N <= 0 || K <= 0 || M % F4_BM || N % 128 || K % F4_BK || K < 2 * F4_BK || lda % 8 || ldb % 8 ||
@@ -346,11 +395,13 @@ DLT_API int dlt_gemm_fw4(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int
   if (tiles > 0x7fffffff || 128L * ldc * 2 > 0x7fffffffL || 256L * lda * 2 > 0xffffffffL ||
       256L * ldb * 2 > 0xffffffffL)
     return -1;
-  if (flags & 64)
-    DLT_HK_DISPATCH(hk, k_gemm_fw4<HKC, 2><<<(int)tiles, 256, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, stamps));
+  if ((flags & 128) && (flags & 16))
+    DLT_HK_DISPATCH(hk, k_gemm_fw4<HKC, 5><<<(int)tiles, 256, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, stamps));
+  else if (flags & 128)
+    DLT_HK_DISPATCH(hk, k_gemm_fw4<HKC, 3><<<(int)tiles, 256, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, stamps));
   else if (flags & 16)
     DLT_HK_DISPATCH(hk, k_gemm_fw4<HKC, 1><<<(int)tiles, 256, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, stamps));
   else
-    DLT_HK_DISPATCH(hk, k_gemm_fw4<HKC, 0><<<(int)tiles, 256, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, stamps));
+    DLT_HK_DISPATCH(hk, k_gemm_fw4<HKC, 4><<<(int)tiles, 256, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, stamps));
   DLT_CHECK_LAUNCH();
 }

@@ -120,10 +120,12 @@ def load_plan(path: str, shipped: bool = False) -> None:
                 raise RuntimeError(f"dlt_gemm_pin failed ({rc})")
             _PINNED["hipblaslt"][tuple(v[:-1])] = line
     # "tn": forward-projection race ("bf16" = the persistent hand-written kernel, "fwd" =
-    # the one-tile-per-workgroup hand-written kernel, null = hipBLASLt; the
+    # the one-tile-per-workgroup hand-written kernel, "fw4" = the 4-wave 256 x 256 one with
+    # AGPR accumulators (csrc/gemm_fw4.hip; "fw4:<flags>" with its own launch flags), null =
+    # hipBLASLt; the
     # round-2 integer tile configs of the retired gemm_tn kernels read as "library");
     # "fused": "kind:MxNxK" -> fused epilogue picked (older keys without a kind are ignored)
-    _PINNED["tn"] = {tuple(int(x) for x in k.split("x")): (c if c in ("bf16", "fwd") else None)
+    _PINNED["tn"] = {tuple(int(x) for x in k.split("x")): (c if c in ("bf16", "fwd", "fw4") or str(c).startswith("fw4:") else None)
                      for k, c in plan.get("tn", {}).items()}
     for k, c in plan.get("fused", {}).items():
         if ":" in k:
@@ -334,7 +336,7 @@ class HipGemm:
 
     def _pick(self, x, w, y):
         """Forward projection race, once per shape: hipBLASLt (None), the persistent
-        hand-written kernel ("bf16") or the one-tile-per-workgroup one ("fwd"); a hand-written pick
+        hand-written kernel ("bf16") or the one-tile-per-workgroup ones ("fwd", "fw4"); a hand-written pick
         must beat the library by RACE_MARGIN.  The shipped plan pins the in-step winners."""
         from . import hip
         key = (x.shape[0], w.shape[0], x.shape[1])
@@ -350,6 +352,8 @@ class HipGemm:
             cands.append(("bf16", lambda: hip.gemm_bf16(x, w, out=y)))
         if hip.gemm_fwd_fits(*key) and os.environ.get("DLT_GEMM_FWD2", "1") != "0":
             cands.append(("fwd", lambda: hip.gemm_fwd(x, w, out=y)))
+        if hip.gemm_fw4_fits(*key):
+            cands.append(("fw4", lambda: hip.gemm_fw4(x, w, out=y)))
         for name, fn in cands:
             t = _time_of(fn)
             if t < best:
@@ -369,6 +373,10 @@ class HipGemm:
             return y
         if pick == "fwd" and hip.gemm_fwd(x, w, out=y) is not None:
             return y
+        if pick == "fw4" and hip.gemm_fw4(x, w, out=y) is not None:
+            return y
+        if isinstance(pick, str) and pick.startswith("fw4:") and hip.gemm_fw4(x, w, out=y, flags=int(pick[4:])) is not None:
+            return y  # "fw4:<flags>": the kernel with its own launch flags (schedule / store flavour)
         self._lib_linear(x, w, y)
         return y
 

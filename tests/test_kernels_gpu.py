@@ -622,7 +622,7 @@ def test_gemm_fw4(M, N, K, dtype):
     b = (torch.rand(N, K, device=DEV) * 2 - 1).to(dtype)
     want = a.float() @ b.float().t()
     first = None
-    for flags in (1, 0, 2, 17, 16, 65, 64, 66):
+    for flags in (1, 0, 4, 2, 17, 16, 18, 129, 128, 130, 144, 145, 148, 146):
         c = torch.full((M, N), float("nan"), device=DEV, dtype=dtype)
         assert hip.gemm_fw4(a, b, out=c, flags=flags) is not None
         assert not torch.isnan(c).any(), f"unwritten output (flags {flags})"
@@ -633,7 +633,7 @@ def test_gemm_fw4(M, N, K, dtype):
         assert torch.equal(c, first), f"schedules / store flavours must agree bitwise (flags {flags})"
     st = torch.zeros((M // 256) * ((N + 255) // 256), 16, dtype=torch.int64, device=DEV)
     c = torch.empty(M, N, device=DEV, dtype=dtype)
-    hip.gemm_fw4(a, b, out=c, flags=64, stamps=st)
+    hip.gemm_fw4(a, b, out=c, flags=0, stamps=st)
     assert torch.equal(c, first) and bool((st[:, 3] >= st[:, 0]).all())
     assert hip.gemm_fw4(a[:, :K - 32].contiguous(), b[:, :K - 32].contiguous()) is None  # K % 64
     assert hip.gemm_fw4(a, b[:N - 8].contiguous()) is None  # N % 128

@@ -52,9 +52,15 @@ def main():
                           ("bf16", (lambda: hip.gemm_bf16(a, b, out=y)) if hip.gemm_bf16_fits(M, N, K) else None),
                           ("fwd", lambda: hip.gemm_fwd(a, b, out=y)),
                           ("fw4", lambda: hip.gemm_fw4(a, b, out=y)),
+                          ("fw4p", lambda: hip.gemm_fw4(a, b, out=y, flags=0)),
+                          ("fw4nt", lambda: hip.gemm_fw4(a, b, out=y, flags=4)),
                           ("fw4s1", lambda: hip.gemm_fw4(a, b, out=y, flags=hip._FW4_FLAGS | 16)),
-                          ("fw4s2", lambda: hip.gemm_fw4(a, b, out=y, flags=hip._FW4_FLAGS | 64)),
-                          ("fw4s2w", lambda: hip.gemm_fw4(a, b, out=y, flags=64))):
+                          ("fw4s3", lambda: hip.gemm_fw4(a, b, out=y, flags=hip._FW4_FLAGS | 128)),
+                          ("fw4s5", lambda: hip.gemm_fw4(a, b, out=y, flags=144)),
+                          ("fw4s5nt", lambda: hip.gemm_fw4(a, b, out=y, flags=148)),
+                          ("fw4s5w", lambda: hip.gemm_fw4(a, b, out=y, flags=145)),
+                          ("fw4ntrm", lambda: hip.gemm_fw4(a, b, out=y, flags=6)),
+                          ("fw4s5ntrm", lambda: hip.gemm_fw4(a, b, out=y, flags=150))):
             if label not in impls:
                 continue
             if fn is None:
@@ -66,7 +72,7 @@ def main():
         errs = []
         for label, fn in (("fwd", hip.gemm_fwd), ("fw4", hip.gemm_fw4),
                           ("fw4s1", lambda a, b, out: hip.gemm_fw4(a, b, out=out, flags=hip._FW4_FLAGS | 16)),
-                          ("fw4s2", lambda a, b, out: hip.gemm_fw4(a, b, out=out, flags=hip._FW4_FLAGS | 64))):
+                          ("fw4s3", lambda a, b, out: hip.gemm_fw4(a, b, out=out, flags=hip._FW4_FLAGS | 128))):
             if label not in impls:
                 continue
             y.fill_(float("nan"))
