@@ -6,33 +6,42 @@
 // Why this shape (round 6).  In the two-chain training window a forward GEMM runs beside
 // the other chain's memory-bound kernels; a persistent grid starves them (profiles/
 // r6_gemm_fwd.md), so this kernel computes ONE tile per workgroup and hands its CU back
-// to the dispatcher after every tile.  Its main loop is built for the matrix pipe:
+// to the dispatcher after every tile, like hipBLASLt's MT256x256x64 kernel it replaces.
 //   * 256 threads = 4 waves (one per SIMD), each owning a 128 x 128 block of the tile:
 //     8 x 8 accumulators of v_mfma_f32_16x16x32_bf16 = all 256 AGPRs (the MFMAs are
 //     issued from inline asm with "+a" accumulators: the compiler's own MFMA selection
 //     splits 256 loop-carried accumulators over both register halves and copies them
 //     through v_accvgpr_read/write every iteration); 0.25 ds_read_b128 per MFMA;
-//   * BK = 32 stages in a ring of 4 x 32 KiB (A image, then B image): stage s + 4 is
-//     DMA'd into stage s's buffer while stage s computes, so three stages (96 KiB per CU)
-//     are in flight behind the one being consumed -- ~3 x 1000 cycles of L2 / MALL
-//     latency cover;
-//   * one barrier per stage: wait (counted vmcnt) for stage s + 1 and for this wave's
-//     fragment reads of stage s, barrier (every wave's reads of stage s's buffer are done,
-//     stage s + 1 visible), then 64 MFMAs on stage s's fragments with the 16 fragment
-//     reads of stage s + 1 and the 8 LDS-DMA pieces of stage s + 4 interleaved (two reads
-//     and one piece per 8-MFMA group); fragment registers alternate between two sets (the
-//     loop runs stages in pairs, the last four are peeled for the counted waits), so
-//     every instruction of the loop is inline asm in a fixed order;
-//   * LDS images with 64-byte rows (32 k): 16-byte chunk c of row r is stored at
-//     c ^ (2 * ((r >> 3) & 1)) -- a 16-lane group of ds_read_b128 (16 rows) covers all 64
-//     banks; the DMA is lane-linear on the LDS side, so the swizzle lives in the per-lane
-//     source offsets;
-//   * swapped product D = B_tile . A_tile^T, so a lane holds 4 consecutive columns of one
-//     output row; the epilogue stages each wave's 128 x 128 block in its own quarter of
-//     the ring (chunk-swizzled 256-byte rows) and stores whole row runs, 16 bytes a lane;
-//   * XCD row bands: block b runs on the XCD of b % 8 (round-robin dispatch; speed only):
-//     that XCD owns a band of tile rows and walks it column by column, so its A panels
-//     stay in its L2 and each B panel is fetched once per XCD.
+//   * BK = 64 stages (128-byte operand rows: every LDS-DMA piece moves 8 whole 128-byte
+//     lines), fragments of a stage read in two 32-deep halves; every instruction of the
+//     loop is inline asm in a fixed order (MFMAs, fragment reads, DMA pieces, counted
+//     vmcnt / lgkmcnt waits, barriers);
+//   * schedules (launch flags): SCHED 1 (16) two 64 KiB stage buffers, the 3-phase form:
+//     half 0 reads half 1's fragments; barrier; half 1 issues stage s + 2's DMA, waits
+//     (vmcnt(16)) for stage s + 1, barrier, reads its half-0 fragments.  SCHED 3 (128) /
+//     SCHED 5 (144): a ring of five 32 KiB image slots (A of stage s in slot 2s % 5, B in
+//     2s + 1): stage s + 2's A image goes into the slot stage s - 1's B freed, so its DMA
+//     spreads over half 0 and only the B image waits for the mid barrier; per-group
+//     counted lgkmcnt waits.  SCHED 4 (default) / 5 use the INTERLEAVED epilogue below;
+//     SCHED 1 / 3 stage the tile through LDS (swapped product, chunk-swizzled rows);
+//   * interleaved epilogue (SCHED 4 / 5): n-tile u of a wave holds the B rows (output
+//     columns) 8 v + u, v = 0..15, so register r of the 8 n-tiles is 8 consecutive columns
+//     of row 16 t + 4 (l >> 4) + r: one 16-byte store per (m-tile, r) straight from the
+//     accumulators, the 16 lanes of a row writing 256 contiguous bytes -- no LDS, no
+//     barrier.  SCHED 4 pads the B pieces to 1040 bytes (conflict-free reads), SCHED 5
+//     keeps the ring's 32 KiB slots (two-way bank conflicts on the B reads);
+//   * SwiGLU epilogue (flags 1024, SCHED 4 / 5): the gate/up projection with
+//     s = silu(gate) * up computed from the accumulators -- each wave's 128 B rows are 64
+//     gate rows and the 64 up rows of the same intermediate indices, a row_ror:8 DPP move
+//     pairs them in one lane, k_swiglu_fwd's arithmetic (same bits); gu keeps [gate | up];
+//   * LDS images: A rows of 128 bytes, 16-byte chunk c of row r at c ^ (r & 7) (a 16-lane
+//     group of ds_read_b128 covers all 64 banks); the DMA is lane-linear on the LDS side,
+//     so every swizzle lives in the per-lane source offsets;
+//   * tile order: XCD row bands (block b runs on the XCD of b % 8 under round-robin
+//     dispatch; speed only): that XCD owns a band of tile rows and walks it column by
+//     column (A panels stay in its L2); 2048: half-height bands, two per XCD; 2: row-major
+//     (with N / 256 % 8 == 0 each XCD keeps a fixed set of B panels).  C stores: plain,
+//     1 = write-through (sc1), 4 = nt.
 //
 // Requirements (launcher-checked): M % 256 == 0, N % 128 == 0, K % 64 == 0, K >= 128, rows
 // 16-byte aligned; a ragged last column tile (N % 256 == 128, the lm_head) clamps its B
@@ -101,7 +110,8 @@ struct F4Frags {
 template <int HK, int SCHED>
 __global__ __launch_bounds__(256, 1) void k_gemm_fw4(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                      bf16_t* __restrict__ C, int M, int N, int K, int lda, int ldb,
-                                                     int ldc, int flags, unsigned long long* __restrict__ stamps) {
+                                                     int ldc, int flags, bf16_t* __restrict__ S, int ldS,
+                                                     unsigned long long* __restrict__ stamps) {
   // diagnostic (stamps != nullptr, tools/bench_gemm_fwd.py --stamps): wave 0 records
   // s_memrealtime (100 MHz) / s_memtime at start, after the prologue, after the main loop
   // and after its stores landed, plus the hardware ids, into stamps[16 * blockIdx.x ..]
@@ -121,7 +131,13 @@ __global__ __launch_bounds__(256, 1) void k_gemm_fw4(const bf16_t* __restrict__ 
   const int ntm = M / F4_BM, ntn = (N + F4_BN - 1) / F4_BN;
   const int bid = blockIdx.x;
   int tm, tn;
-  if ((ntm & 7) == 0 && !(flags & 2)) {
+  if ((ntm & 15) == 0 && (flags & 2048)) {
+    // 2048: half-height bands, two per XCD (band x, then band x + 8): R = ntm / 16 rows
+    const int R = ntm >> 4, x = bid & 7, j = bid >> 3, per = R * ntn;
+    const int band = j < per ? x : x + 8, jj = j < per ? j : j - per;
+    tm = band * R + jj % R;
+    tn = jj / R;
+  } else if ((ntm & 7) == 0 && !(flags & 2)) {
     const int R = ntm >> 3, x = bid & 7, j = bid >> 3;
     tm = x * R + j % R;
     tn = j / R;
@@ -143,10 +159,15 @@ __global__ __launch_bounds__(256, 1) void k_gemm_fw4(const bf16_t* __restrict__ 
     // SCHED 4: piece 8 w + j of the B image holds rows 8 v + u (v = piece % 16) of n-tile u
     // (SCHED 5: logical chunk c of B-image row 8 v + u at c ^ (v & 7))
     const int blc = PAD ? (lane & 7) ^ f4_fb((8 * wid + j) & 15) : EPI ? (lane & 7) ^ ((8 * wid + j) & 7) : lc;
-    boff[j] = (uint32_t)((min(n0 + row, N - 1) - n0) * ldb + blc * 8) * 2u;
+    // SWIGLU (flags & 1024, EPI schedules): the tile covers intermediate indices
+    // [128 tn, 128 tn + 128); wave-half wn of its B rows = 64 gate rows then the 64 up rows
+    // of indices 128 tn + 64 wn + 0..63 (Wgu rows j and I + j)
+    const int brow = (flags & 1024) ? ((row & 127) >> 6) * (N >> 1) + 64 * (row >> 7) + (row & 63)
+                                    : min(n0 + row, N - 1) - n0;
+    boff[j] = (uint32_t)(brow * ldb + blc * 8) * 2u;
   }
   const bf16_t* Ab = A + (size_t)m0 * lda;
-  const bf16_t* Bb = B + (size_t)n0 * ldb;
+  const bf16_t* Bb = B + (size_t)((flags & 1024) ? 128 * tn : n0) * ldb;
   const uint32_t lbase = (uint32_t)(uintptr_t)lds;
   // LDS byte offsets of stage s's A and B images: SCHED 0 / 1 two 64 KiB stage buffers;
   // SCHED 2 a ring of five 32 KiB image slots, A of stage s in slot 2s % 5, B in (2s + 1) % 5
@@ -319,7 +340,50 @@ __global__ __launch_bounds__(256, 1) void k_gemm_fw4(const bf16_t* __restrict__ 
     const bool col_ok = n0 + wn * 128 < N;
     const auto rs =
         __builtin_amdgcn_make_buffer_rsrc(C + (size_t)(m0 + wm * 128) * ldc, 0, 128 * ldc * 2, 0x00020000);
-    if (col_ok) {
+    if (flags & 1024) {
+      // SWIGLU: lanes v = l & 15 < 8 hold gate indices jb + 8 v + u, lanes v + 8 the up values
+      // of the same indices; after a row_ror:8 exchange each lane of the pair has both and
+      // computes s = silu(g) * u -- k_swiglu_fwd's arithmetic on the bf16-rounded g and u,
+      // same bits -- for 4 of the 8 indices.  gu keeps its [M, 2I] layout (gate | up).
+      const int I = N >> 1, jb = 128 * tn + 64 * wn, v = l16;
+      const int gcol = (v < 8 ? jb : I + jb) + 8 * (v & 7), e0 = v < 8 ? 0 : 4;
+      const auto rss =
+          __builtin_amdgcn_make_buffer_rsrc(S + (size_t)(m0 + wm * 128) * ldS, 0, 128 * ldS * 2, 0x00020000);
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          floatx4_t lo{acc[0][t][r], acc[1][t][r], acc[2][t][r], acc[3][t][r]};
+          floatx4_t hi{acc[4][t][r], acc[5][t][r], acc[6][t][r], acc[7][t][r]};
+          const uint2 a = f4_pack<HK>(lo), b = f4_pack<HK>(hi);
+          const f4_u32x4_t P{a.x, a.y, b.x, b.y};
+          f4_u32x4_t Q;
+#pragma unroll
+          for (int d = 0; d < 4; ++d) Q[d] = (uint32_t)__builtin_amdgcn_mov_dpp((int)P[d], 0x128, 0xf, 0xf, false);
+          const int row = 16 * t + 4 * q + r;
+          const int off = (row * ldc + gcol) * 2;
+          if (flags & 1) __builtin_amdgcn_raw_buffer_store_b128(P, rs, off, 0, 16);
+          else if (flags & 4) __builtin_amdgcn_raw_buffer_store_b128(P, rs, off, 0, 2);
+          else __builtin_amdgcn_raw_buffer_store_b128(P, rs, off, 0, 0);
+          const f4_u32x4_t G = v < 8 ? P : Q, U = v < 8 ? Q : P;
+          uint32_t o2[2];
+#pragma unroll
+          for (int e = 0; e < 4; e += 2) {
+            const int w0 = (e0 + e) >> 1;  // dword holding elements e0 + e, e0 + e + 1
+            float sv[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const float gv = h2f<HK>((uint16_t)(G[w0] >> (16 * h)));
+              const float uv = h2f<HK>((uint16_t)(U[w0] >> (16 * h)));
+              sv[h] = gv * dlt_sigmoid(gv) * uv;
+            }
+            o2[e >> 1] = (uint32_t)f2h<HK>(sv[0]) | ((uint32_t)f2h<HK>(sv[1]) << 16);
+          }
+          const int soff = (row * ldS + jb + 8 * (v & 7) + e0) * 2;
+          typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+          __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{o2[0], o2[1]}, rss, soff, 0, 0);
+        }
+    } else if (col_ok) {
 #pragma unroll
       for (int t = 0; t < 8; ++t)
 #pragma unroll
@@ -385,23 +449,28 @@ __global__ __launch_bounds__(256, 1) void k_gemm_fw4(const bf16_t* __restrict__ 
 }
 
 // flags: 1 = write-through (sc1) C stores, 4 = nt C stores, 2 = row-major tile order (A/B knob);
-// schedule: 16 = SCHED 1, 128 = SCHED 3, 144 = SCHED 5, else SCHED 4
+// schedule: 16 = SCHED 1, 128 = SCHED 3, 144 = SCHED 5, else SCHED 4; 1024 = SwiGLU epilogue (SCHED 4 / 5)
 DLT_API int dlt_gemm_fw4(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K, int lda, int ldb, int ldc,
-                         int flags, int hk, unsigned long long* stamps, hipStream_t st) {
+                         int flags, int hk, bf16_t* S, int ldS, unsigned long long* stamps, hipStream_t st) {
   if (M <= 0 || N <= 0 || K <= 0 || M % F4_BM || N % 128 || K % F4_BK || K < 2 * F4_BK || lda % 8 || ldb % 8 ||
       ldc % 8 || lda < K || ldb < K || ldc < N)
+    return -1;
+  // SWIGLU epilogue (flags & 1024): N = 2I with I % 128 == 0, s [M, ldS >= I], EPI schedules
+  const int sched_bits = flags & (16 | 128);  // 0: SCHED 4, 16 | 128: SCHED 5
+  if ((flags & 1024) && (S == nullptr || N % 256 || ldS < N / 2 || ldS % 8 || sched_bits == 16 || sched_bits == 128 ||
+                         128L * ldS * 2 > 0x7fffffffL || (long)(N / 2 + 127) * ldb * 2 > 0xffffffffL))
     return -1;
   const long tiles = (long)(M / F4_BM) * ((N + F4_BN - 1) / F4_BN);
   if (tiles > 0x7fffffff || 128L * ldc * 2 > 0x7fffffffL || 256L * lda * 2 > 0xffffffffL ||
       256L * ldb * 2 > 0xffffffffL)
     return -1;
   if ((flags & 128) && (flags & 16))
-    DLT_HK_DISPATCH(hk, k_gemm_fw4<HKC, 5><<<(int)tiles, 256, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, stamps));
+    DLT_HK_DISPATCH(hk, k_gemm_fw4<HKC, 5><<<(int)tiles, 256, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, S, ldS, stamps));
   else if (flags & 128)
-    DLT_HK_DISPATCH(hk, k_gemm_fw4<HKC, 3><<<(int)tiles, 256, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, stamps));
+    DLT_HK_DISPATCH(hk, k_gemm_fw4<HKC, 3><<<(int)tiles, 256, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, S, ldS, stamps));
   else if (flags & 16)
-    DLT_HK_DISPATCH(hk, k_gemm_fw4<HKC, 1><<<(int)tiles, 256, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, stamps));
+    DLT_HK_DISPATCH(hk, k_gemm_fw4<HKC, 1><<<(int)tiles, 256, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, S, ldS, stamps));
   else
-    DLT_HK_DISPATCH(hk, k_gemm_fw4<HKC, 4><<<(int)tiles, 256, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, stamps));
+    DLT_HK_DISPATCH(hk, k_gemm_fw4<HKC, 4><<<(int)tiles, 256, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, S, ldS, stamps));
   DLT_CHECK_LAUNCH();
 }

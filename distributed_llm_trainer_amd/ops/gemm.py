@@ -130,7 +130,10 @@ def load_plan(path: str, shipped: bool = False) -> None:
     for k, c in plan.get("fused", {}).items():
         if ":" in k:
             kind, dims = k.split(":", 1)
-            _PINNED["tn"][(kind, *(int(x) for x in dims.split("x")))] = bool(c)
+            # "swiglu4": the 4-wave k_gemm_fw4 with the SwiGLU epilogue, value = its launch flags
+            # (an int; false / null = not used); every other kind is a bool
+            _PINNED["tn"][(kind, *(int(x) for x in dims.split("x")))] = (
+                (int(c) if c is not None and c is not False else None) if kind == "swiglu4" else bool(c))
     _PINNED["splitk"] = {_splitk_key(k): int(c) for k, c in plan.get("splitk", {}).items()}
     if _RACES:
         _RACES["tn"].update(_PINNED["tn"])
@@ -167,7 +170,8 @@ def export_plan() -> dict:
     return {"hipblaslt_version": int(lib().dlt_gemm_lib_version()),
             "hipblaslt": [hl[k] for k in sorted(hl)],
             "tn": {"x".join(map(str, k)): c for k, c in tn.items() if len(k) == 3},
-            "fused": {f"{k[0]}:" + "x".join(map(str, k[1:])): bool(c) for k, c in tn.items() if len(k) == 4},
+            "fused": {f"{k[0]}:" + "x".join(map(str, k[1:])): (c if k[0] == "swiglu4" else bool(c))
+                      for k, c in tn.items() if len(k) == 4},
             "splitk": {"x".join(map(str, k)): c for k, c in sk.items()}}
 
 
@@ -436,6 +440,12 @@ class HipGemm:
 
         def fused():
             hip.gemm_gu_swiglu(x, w, gu_out=gu, s_out=s)
+        # the 4-wave k_gemm_fw4 with the SwiGLU epilogue: plan kind "swiglu4" (its launch flags)
+        # or DLT_GEMM_FW4_SWIGLU=<flags> (A/B knob)
+        fw4 = os.environ.get("DLT_GEMM_FW4_SWIGLU") or self._choice.get(("swiglu4", M, I2, x.shape[1]))
+        if fw4 is not None and self._hand16_ok(x, w) and s.is_contiguous() and \
+                hip.gemm_fw4_swiglu(x, w, gu_out=gu, s_out=s, flags=int(fw4)) is not None:
+            return gu, s
         ok = I2 % 192 == 0 and hip.gemm_bf16_fits192(M, I2, x.shape[1]) and s.is_contiguous()
         if ok and self._fused_pick("swiglu", x, w, fused, unfused):
             fused()
@@ -444,10 +454,13 @@ class HipGemm:
         return gu, s
 
     def report_choices(self) -> dict:
-        out = {f"M{k[0]}xN{k[1]}xK{k[2]}": ("hipBLASLt" if c is None else "hand-written gemm_bf16")
+        names = {"bf16": "hand-written gemm_bf16 (persistent)", "fwd": "hand-written gemm_fwd", "fw4": "hand-written gemm_fw4"}
+        out = {f"M{k[0]}xN{k[1]}xK{k[2]}": ("hipBLASLt" if c is None else names.get(c, f"hand-written gemm_{c}"))
                for k, c in self._choice.items() if len(k) == 3}
         out.update({f"{k[0]} M{k[1]}xN{k[2]}xK{k[3]}": (("hand-written gemm_dgrad" if c else "hipBLASLt")
                                                        if k[0].startswith("dgrad") else
+                                                       (f"fused gemm_fw4 (flags {c})" if c is not None else "not used")
+                                                       if k[0] == "swiglu4" else
                                                        ("fused gemm_bf16" if c else "unfused (linear + kernel)"))
                     for k, c in self._choice.items() if len(k) == 4})
         out.update({f"wgrad{f' ({key[3]} out)' if len(key) == 4 else ''} M{key[0]}xN{key[1]}xK{key[2]}":

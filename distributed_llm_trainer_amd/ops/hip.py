@@ -67,7 +67,7 @@ _SIGS = {
     "dlt_gemm_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                      c_void_p],
     "dlt_gemm_fw4": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
-                     c_void_p],
+                     c_int, c_void_p, c_void_p],
     "dlt_gemm_bf16_qkv_rope": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                                c_void_p],
     "dlt_gemm_bf16_gu_swiglu": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
@@ -926,7 +926,7 @@ def gemm_fw4_fits(M: int, N: int, K: int) -> bool:
 
 
 # launch flags of k_gemm_fw4: 1 = write-through (sc1) C stores, 2 = row-major tile order
-_FW4_FLAGS = int(os.environ.get("DLT_GEMM_FW4_FLAGS", "1"))
+_FW4_FLAGS = int(os.environ.get("DLT_GEMM_FW4_FLAGS", "148"))
 
 
 def gemm_fw4(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
@@ -947,9 +947,38 @@ def gemm_fw4(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = Non
     if stamps is not None:  # diagnostic: int64 [tiles, 16] per-workgroup timestamps (csrc/gemm_fw4.hip)
         if stamps.dtype != torch.int64 or stamps.numel() < 16 * (M // 256) * ((N + 255) // 256) or not stamps.is_cuda:
             raise ValueError("gemm_fw4: stamps must be a CUDA int64 tensor of 16 * tiles entries")
-    _chk(lib().dlt_gemm_fw4(_p(a), _p(b), _p(c), M, N, K, K, K, N, fl, hk,
+    _chk(lib().dlt_gemm_fw4(_p(a), _p(b), _p(c), M, N, K, K, K, N, fl & ~1024, hk, None, 0,
                             _p(stamps) if stamps is not None else None, _stream()), "gemm_fw4")
     return c
+
+
+def gemm_fw4_swiglu_fits(M: int, I2: int, K: int) -> bool:
+    return gemm_fw4_fits(M, I2, K) and I2 % 256 == 0
+
+
+def gemm_fw4_swiglu(x: torch.Tensor, wgu: torch.Tensor, gu_out: Optional[torch.Tensor] = None,
+                    s_out: Optional[torch.Tensor] = None, flags: Optional[int] = None):
+    """(gu[M, 2I], s[M, I]): gu = x @ Wgu^T (gate rows [0, I), up rows [I, 2I)) by the 4-wave
+    k_gemm_fw4 with s = silu(gate) * up in its epilogue (csrc/gemm_fw4.hip, flags 1024;
+    k_swiglu_fwd's arithmetic, same bits).  None if the shape does not tile (I % 128,
+    M % 256, K % 64)."""
+    M, K = x.shape
+    I2 = wgu.shape[0]
+    I = I2 // 2
+    if not gemm_fw4_swiglu_fits(M, I2, K) or wgu.shape[1] != K:
+        return None
+    hk = _req_act(x, x.dtype, "gemm_fw4_swiglu.x")
+    _req(wgu, x.dtype, "gemm_fw4_swiglu.w")
+    gu = torch.empty(M, I2, dtype=x.dtype, device=x.device) if gu_out is None else gu_out
+    s = torch.empty(M, I, dtype=x.dtype, device=x.device) if s_out is None else s_out
+    _req(gu, x.dtype, "gemm_fw4_swiglu.gu", M * I2)
+    _req(s, x.dtype, "gemm_fw4_swiglu.s", M * I)
+    fl = (_FW4_FLAGS if flags is None else flags) & ~(16 | 128)
+    if flags is not None and (flags & (16 | 128)) == (16 | 128):
+        fl |= 16 | 128  # SCHED 5
+    _chk(lib().dlt_gemm_fw4(_p(x), _p(wgu), _p(gu), M, I2, K, K, K, I2, fl | 1024, hk, _p(s), I, None, _stream()),
+         "gemm_fw4_swiglu")
+    return gu, s
 
 
 def gemm_qkv_rope(x: torch.Tensor, wqkv: torch.Tensor, S: int, cos: torch.Tensor, sin: torch.Tensor,

@@ -639,6 +639,22 @@ def test_gemm_fw4(M, N, K, dtype):
     assert hip.gemm_fw4(a, b[:N - 8].contiguous()) is None  # N % 128
 
 
+@pytest.mark.parametrize("M,I,K", [(16384, 3072, 768), (512, 256, 128), (1024, 384, 192)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_gemm_fw4_swiglu(M, I, K, dtype):
+    """k_gemm_fw4 with the SwiGLU epilogue (csrc/gemm_fw4.hip flags 1024): gu bitwise equal to
+    the plain k_gemm_fw4 GEMM of the same schedule, s bitwise equal to swiglu_fwd(gu)."""
+    torch.manual_seed(M + I + K)
+    x = (torch.rand(M, K, device=DEV) * 2 - 1).to(dtype)
+    w = (torch.rand(2 * I, K, device=DEV) * 2 - 1).to(dtype)
+    for flags in (0, 4, 1, 144, 150):
+        gu, s = hip.gemm_fw4_swiglu(x, w, flags=flags)
+        plain = hip.gemm_fw4(x, w, flags=flags)
+        assert torch.equal(gu, plain), f"gu differs from the plain GEMM (flags {flags})"
+        assert torch.equal(s, hip.swiglu_fwd(gu)), f"s differs from swiglu_fwd (flags {flags})"
+    assert hip.gemm_fw4_swiglu(x, w[:2 * I - 128].contiguous()) is None or I % 128 == 64
+
+
 @pytest.fixture(params=[0, 4096], ids=["stage-in-loop", "epilogue-first"])
 def gemm_late_flag(request, monkeypatch):
     """Runs a test with and without flags bit 4096 (epilogue-first staging of the next

@@ -267,3 +267,34 @@ def test_gemm_planner_routes_fp16_dgrad_to_the_hand_kernel(monkeypatch):
     calls.clear()
     g.linear_dgrad(torch.zeros(256, 128, dtype=torch.float16), torch.zeros(128, 192, dtype=torch.float16))
     assert calls == [("hand", torch.float16)]
+
+
+def test_gemm_planner_routes_fw4_picks(monkeypatch):
+    """Plan values of the forward race: "fw4:<flags>" runs the 4-wave k_gemm_fw4 with its own
+    launch flags (schedule / store flavour), the fused kind "swiglu4" (an int) runs its
+    SwiGLU-epilogue form; the shipped plan pins both for the headline forward roles, so
+    the bf16 step has no library forward GEMM."""
+    import json
+    import os
+    import torch
+    from distributed_llm_trainer_amd.ops import gemm, hip
+    g = object.__new__(gemm.HipGemm)
+    g._choice, g._splitk = {(256, 384, 128): "fw4:148", ("swiglu4", 256, 512, 128): 4}, {}
+    g._race = g._fuse = g._dgrad_on = g._hand_wgrad = g._splitk_on = True
+    g._fp16_hand = False
+    calls = []
+    monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: False)
+    monkeypatch.setattr(hip, "gemm_fw4", lambda a, b, out=None, flags=None: calls.append(("fw4", flags)) or out)
+    monkeypatch.setattr(hip, "gemm_fw4_swiglu",
+                        lambda x, w, gu_out=None, s_out=None, flags=None: calls.append(("fw4sw", flags)) or (gu_out, s_out))
+    monkeypatch.setattr(gemm.HipGemm, "_lib_linear", lambda self, x, w, y: calls.append(("lib", None)))
+    x = torch.zeros(256, 128, dtype=torch.bfloat16)
+    g.linear(x, torch.zeros(384, 128, dtype=torch.bfloat16))
+    assert calls == [("fw4", 148)]
+    calls.clear()
+    g.linear_swiglu(x, torch.zeros(512, 128, dtype=torch.bfloat16), ops=None)
+    assert calls == [("fw4sw", 4)]
+    plan = json.load(open(os.path.join(os.path.dirname(__file__), "..", "configs", "gemm_plan_mi355x.json")))
+    fwd = {k: v for k, v in plan["tn"].items() if k.startswith("16384x")}
+    assert all(v is not None for v in fwd.values()), fwd  # no library forward GEMM at the headline shapes
+    assert isinstance(plan["fused"]["swiglu4:16384x6144x768"], int)

@@ -60,7 +60,9 @@ def main():
                           ("fw4s5nt", lambda: hip.gemm_fw4(a, b, out=y, flags=148)),
                           ("fw4s5w", lambda: hip.gemm_fw4(a, b, out=y, flags=145)),
                           ("fw4ntrm", lambda: hip.gemm_fw4(a, b, out=y, flags=6)),
-                          ("fw4s5ntrm", lambda: hip.gemm_fw4(a, b, out=y, flags=150))):
+                          ("fw4s5ntrm", lambda: hip.gemm_fw4(a, b, out=y, flags=150)),
+                          ("fw4nth", lambda: hip.gemm_fw4(a, b, out=y, flags=4 | 2048)),
+                          ("fw4s5nth", lambda: hip.gemm_fw4(a, b, out=y, flags=148 | 2048))):
             if label not in impls:
                 continue
             if fn is None:
