@@ -119,13 +119,13 @@ def load_plan(path: str, shipped: bool = False) -> None:
             if rc != 0:
                 raise RuntimeError(f"dlt_gemm_pin failed ({rc})")
             _PINNED["hipblaslt"][tuple(v[:-1])] = line
-    # "tn": forward-projection race ("bf16" = the persistent hand-written kernel, "fwd" =
-    # the one-tile-per-workgroup hand-written kernel, "fw4" = the 4-wave 256 x 256 one with
+    # "tn": forward-projection race ("bf16" = the persistent hand-written kernel, "fw4" = the
+    # one-tile-per-workgroup 4-wave 256 x 256 one with
     # AGPR accumulators (csrc/gemm_fw4.hip; "fw4:<flags>" with its own launch flags), null =
     # hipBLASLt; the
     # round-2 integer tile configs of the retired gemm_tn kernels read as "library");
     # "fused": "kind:MxNxK" -> fused epilogue picked (older keys without a kind are ignored)
-    _PINNED["tn"] = {tuple(int(x) for x in k.split("x")): (c if c in ("bf16", "fwd", "fw4") or str(c).startswith("fw4:") else None)
+    _PINNED["tn"] = {tuple(int(x) for x in k.split("x")): (c if c in ("bf16", "fw4") or str(c).startswith("fw4:") else None)
                      for k, c in plan.get("tn", {}).items()}
     for k, c in plan.get("fused", {}).items():
         if ":" in k:
@@ -340,7 +340,7 @@ class HipGemm:
 
     def _pick(self, x, w, y):
         """Forward projection race, once per shape: hipBLASLt (None), the persistent
-        hand-written kernel ("bf16") or the one-tile-per-workgroup ones ("fwd", "fw4"); a hand-written pick
+        hand-written kernel ("bf16") or the one-tile-per-workgroup one ("fw4"); a hand-written pick
         must beat the library by RACE_MARGIN.  The shipped plan pins the in-step winners."""
         from . import hip
         key = (x.shape[0], w.shape[0], x.shape[1])
@@ -354,8 +354,6 @@ class HipGemm:
         cands = []
         if hip.gemm_bf16_fits(*key):
             cands.append(("bf16", lambda: hip.gemm_bf16(x, w, out=y)))
-        if hip.gemm_fwd_fits(*key) and os.environ.get("DLT_GEMM_FWD2", "1") != "0":
-            cands.append(("fwd", lambda: hip.gemm_fwd(x, w, out=y)))
         if hip.gemm_fw4_fits(*key):
             cands.append(("fw4", lambda: hip.gemm_fw4(x, w, out=y)))
         for name, fn in cands:
@@ -374,8 +372,6 @@ class HipGemm:
         pick = self._pick(x, w, y) if self._race and self._hand16_ok(x, w) else None
         from . import hip
         if pick == "bf16" and (x.dtype == torch.bfloat16 or self._fp16_hand) and hip.gemm_bf16(x, w, out=y) is not None:
-            return y
-        if pick == "fwd" and hip.gemm_fwd(x, w, out=y) is not None:
             return y
         if pick == "fw4" and hip.gemm_fw4(x, w, out=y) is not None:
             return y
@@ -454,7 +450,7 @@ class HipGemm:
         return gu, s
 
     def report_choices(self) -> dict:
-        names = {"bf16": "hand-written gemm_bf16 (persistent)", "fwd": "hand-written gemm_fwd", "fw4": "hand-written gemm_fw4"}
+        names = {"bf16": "hand-written gemm_bf16 (persistent)", "fw4": "hand-written gemm_fw4"}
         out = {f"M{k[0]}xN{k[1]}xK{k[2]}": ("hipBLASLt" if c is None else names.get(c, f"hand-written gemm_{c}"))
                for k, c in self._choice.items() if len(k) == 3}
         out.update({f"{k[0]} M{k[1]}xN{k[2]}xK{k[3]}": (("hand-written gemm_dgrad" if c else "hipBLASLt")

@@ -64,8 +64,6 @@ _SIGS = {
     "dlt_scale_bf16": [c_void_p, c_void_p, ctypes.c_long, c_void_p, c_float, c_int, c_void_p],
     "dlt_gemm_bf16_tn": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                          c_void_p],
-    "dlt_gemm_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
-                     c_void_p],
     "dlt_gemm_fw4": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
                      c_int, c_void_p, c_void_p],
     "dlt_gemm_bf16_qkv_rope": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
@@ -889,34 +887,6 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = No
     _req(c, dt, "gemm_bf16.c", M * N)
     _chk(lib().dlt_gemm_bf16_tn(_p(a), _p(b), _p(c), M, N, K, K, K, N, _fwd_flags(), _WG_HK[dt], _stream()),
          "gemm_bf16")
-    return c
-
-
-def gemm_fwd_fits(M: int, N: int, K: int) -> bool:
-    """Shapes the one-tile-per-workgroup forward GEMM (csrc/gemm_fwd.hip) tiles."""
-    return M > 0 and N > 0 and K > 0 and M % 256 == 0 and N % 128 == 0 and K % 32 == 0
-
-
-# launch flags of k_gemm_fwd: 1 = write-through (sc1) C stores, 2 = row-major tile order
-# (A/B knob; default: XCD row bands); DLT_GEMM_FWD2_BN = 128 / 256 pins its tile width
-# (default 0: 256 when the 256-wide tiles fill two rounds of the CUs, else 128)
-_FWD_FLAGS = int(os.environ.get("DLT_GEMM_FWD2_FLAGS", "1"))
-_FWD_BN = int(os.environ.get("DLT_GEMM_FWD2_BN", "0"))
-
-
-def gemm_fwd(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
-    """C[M,N] = A[M,K] @ B[N,K]^T (bf16 or fp16 in/out, fp32 accumulate) with the
-    one-tile-per-workgroup MFMA kernel (256 x 256 tiles, or 256 x 128 two per CU).  Returns None
-    (nothing launched) when the shape does not tile (M % 256, N % 128, K % 32)."""
-    M, K = a.shape
-    N = b.shape[0]
-    if not gemm_fwd_fits(M, N, K) or b.shape[1] != K:
-        return None
-    hk = _req_act(a, a.dtype, "gemm_fwd.a")
-    _req(b, a.dtype, "gemm_fwd.b")
-    c = torch.empty(M, N, dtype=a.dtype, device=a.device) if out is None else out
-    _req(c, a.dtype, "gemm_fwd.c", M * N)
-    _chk(lib().dlt_gemm_fwd(_p(a), _p(b), _p(c), M, N, K, K, K, N, _FWD_FLAGS, _FWD_BN, hk, _stream()), "gemm_fwd")
     return c
 
 

@@ -1,6 +1,6 @@
 """Isolated timing of the forward projection GEMMs at the headline chain shape (M = 16384):
 hipBLASLt (the planner's library path) vs the persistent hand kernel (k_gemm_bf16) vs the
-one-tile-per-workgroup kernels (k_gemm_fwd 8-wave, k_gemm_fw4 4-wave 128 x 128 per wave).  Mean of --iters launches after
+one-tile-per-workgroup k_gemm_fw4 (4-wave, 128 x 128 per wave) in its launch variants.  Mean of --iters launches after
 warmup, CUDA events.  usage: python tools/bench_gemm_fwd.py [--iters 50]"""
 import argparse
 import os
@@ -32,14 +32,19 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--shapes", default=",".join(SHAPES), help="comma list of SHAPES keys")
-    ap.add_argument("--impls", default="lib,bf16,fwd,fw4", help="comma list of lib / bf16 / fwd / fw4")
+    ap.add_argument("--impls", default="lib,bf16,fw4", help="comma list of lib / bf16 / fw4 / fw4<variant>")
     ap.add_argument("--stamp_flags", type=int, default=16, help="k_gemm_fw4 flags of the --stamps runs")
+    ap.add_argument("--dgrad", action="store_true",
+                    help="data-gradient shapes dX = dY @ W: the persistent reduction-major kernel (hip.gemm_dgrad), "
+                         "hipBLASLt, and k_gemm_fw4 on a transposed weight copy (TN form)")
     ap.add_argument("--stamps", action="store_true",
                     help="diagnostic: per-workgroup timestamps of k_gemm_fw4 (SCHED 1) on each shape")
     args = ap.parse_args()
     impls = args.impls.split(",")
     if args.stamps:
         return stamps(args)
+    if args.dgrad:
+        return dgrad(args)
     g = gemm.HipGemm()
     for name in args.shapes.split(","):
         M, N, K = SHAPES[name]
@@ -50,7 +55,6 @@ def main():
         row = [f"{name:8s} {M}x{N}x{K}:"]
         for label, fn in (("lib", lambda: g._lib_linear(a, b, y)),
                           ("bf16", (lambda: hip.gemm_bf16(a, b, out=y)) if hip.gemm_bf16_fits(M, N, K) else None),
-                          ("fwd", lambda: hip.gemm_fwd(a, b, out=y)),
                           ("fw4", lambda: hip.gemm_fw4(a, b, out=y)),
                           ("fw4p", lambda: hip.gemm_fw4(a, b, out=y, flags=0)),
                           ("fw4nt", lambda: hip.gemm_fw4(a, b, out=y, flags=4)),
@@ -72,7 +76,7 @@ def main():
             row.append(f"{label} {us:7.1f} us {flops / us / 1e6:6.0f} TF")
         ref = (a.float() @ b.float().t())
         errs = []
-        for label, fn in (("fwd", hip.gemm_fwd), ("fw4", hip.gemm_fw4),
+        for label, fn in (("fw4", hip.gemm_fw4),
                           ("fw4s1", lambda a, b, out: hip.gemm_fw4(a, b, out=out, flags=hip._FW4_FLAGS | 16)),
                           ("fw4s3", lambda a, b, out: hip.gemm_fw4(a, b, out=out, flags=hip._FW4_FLAGS | 128))):
             if label not in impls:
@@ -81,6 +85,33 @@ def main():
             fn(a, b, out=y)
             errs.append(f"{label} relerr {((y.float() - ref).norm() / ref.norm()).item():.1e}")
         print(" | ".join(row + errs), flush=True)
+
+
+DGRAD = {"dqkv": (16384, 768, 2304), "do": (16384, 768, 768), "dgu": (16384, 768, 6144),
+         "dlm": (8192, 768, 50304), "ddown": (16384, 3072, 768)}
+
+
+def dgrad(args):
+    """dX[M, N] = dY[M, K] @ W[K, N]: hand persistent NN kernel vs library vs fw4 on W^T."""
+    g = gemm.HipGemm()
+    for name, (M, N, K) in DGRAD.items():
+        dy = torch.randn(M, K, device="cuda").bfloat16()
+        w = torch.randn(K, N, device="cuda").bfloat16()
+        wt = w.t().contiguous()
+        y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        flops = 2.0 * M * N * K
+        row = [f"{name:6s} {M}x{N}x{K}:"]
+        for label, fn in (("hand", lambda: hip.gemm_dgrad(dy, w, out=y)),
+                          ("lib", lambda: g._lib_dgrad(dy, w, y)),
+                          ("fw4", lambda: hip.gemm_fw4(dy, wt, out=y, flags=148)),
+                          ("fw4b", lambda: hip.gemm_fw4(dy, wt, out=y, flags=4)),
+                          ("fw4h", lambda: hip.gemm_fw4(dy, wt, out=y, flags=148 | 2048))):
+            us = timed(fn, args.iters)
+            row.append(f"{label} {us:7.1f} us {flops / us / 1e6:5.0f} TF")
+        ref = dy.float() @ w.float()
+        hip.gemm_fw4(dy, wt, out=y, flags=148)
+        row.append(f"fw4 relerr {((y.float() - ref).norm() / ref.norm()).item():.1e}")
+        print(" | ".join(row), flush=True)
 
 
 def stamps(args):
