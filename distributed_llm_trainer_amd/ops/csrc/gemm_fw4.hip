@@ -107,248 +107,237 @@ struct F4Frags {
 
 }  // namespace
 
-template <int HK, int SCHED>
+template <int HK, int SCHED, int TT, bool SW>
 __global__ __launch_bounds__(256, 1) void k_gemm_fw4(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                      bf16_t* __restrict__ C, int M, int N, int K, int lda, int ldb,
-                                                     int ldc, int flags, bf16_t* __restrict__ S, int ldS,
-                                                     unsigned long long* __restrict__ stamps) {
-  // diagnostic (stamps != nullptr, tools/bench_gemm_fwd.py --stamps): wave 0 records
-  // s_memrealtime (100 MHz) / s_memtime at start, after the prologue, after the main loop
-  // and after its stores landed, plus the hardware ids, into stamps[16 * blockIdx.x ..]
-  unsigned long long st_r[4], st_c[4];
-  const bool stamp = stamps != nullptr && threadIdx.x < 64;
-  if (stamp) { st_r[0] = __builtin_amdgcn_s_memrealtime(); st_c[0] = __builtin_amdgcn_s_memtime(); }
-  // EPI: interleaved B n-tiles + direct epilogue (SCHED 4: padded B pieces, conflict-free;
-  // SCHED 5: the five-slot ring, unpadded B with two-way bank conflicts on its reads)
-  constexpr bool EPI = SCHED == 4 || SCHED == 5, PAD = SCHED == 4, RING = SCHED == 3 || SCHED == 5;
-  constexpr int STG = PAD ? F4_IMG + F4_IMG_BP : F4_BUF;  // bytes of one stage buffer (2-buffer schedules)
+                                                     int ldc, int flags, bf16_t* __restrict__ S, int ldS) {
+  static_assert(SCHED == 4 || SCHED == 5, "k_gemm_fw4: schedules 4 and 5");
+  // SCHED 4: two stage buffers, B pieces padded (conflict-free reads); SCHED 5: the
+  // five-slot ring, unpadded B (two-way bank conflicts on its reads)
+  constexpr bool PAD = SCHED == 4, RING = SCHED == 5;
+  constexpr int STG = F4_IMG + F4_IMG_BP;  // bytes of one SCHED 4 stage buffer
   __shared__ __attribute__((aligned(16))) char lds[RING ? 5 * F4_IMG : 2 * STG];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wid & 1, wn = wid >> 1;
+  const int l16 = lane & 15, q = lane >> 4;
+  constexpr bool swiglu = SW;  // flags 1024: the gate/up projection with the SwiGLU epilogue
+  constexpr int T = TT;  // tiles per workgroup (flags 4096: two, the second's first stages prefetched)
 
-  // tile: XCD row bands (see the header), else row-major
+  // tile j of this workgroup -> (tm, tn): block b runs on the XCD of b % 8 (round-robin
+  // dispatch; speed only) and that XCD takes its tiles in the order jj = (b >> 3) * T + j:
+  // XCD row bands (default), half-height bands (2048) or row-major (2)
   const int ntm = M / F4_BM, ntn = (N + F4_BN - 1) / F4_BN;
-  const int bid = blockIdx.x;
-  int tm, tn;
-  if ((ntm & 15) == 0 && (flags & 2048)) {
-    // 2048: half-height bands, two per XCD (band x, then band x + 8): R = ntm / 16 rows
-    const int R = ntm >> 4, x = bid & 7, j = bid >> 3, per = R * ntn;
-    const int band = j < per ? x : x + 8, jj = j < per ? j : j - per;
-    tm = band * R + jj % R;
-    tn = jj / R;
-  } else if ((ntm & 7) == 0 && !(flags & 2)) {
-    const int R = ntm >> 3, x = bid & 7, j = bid >> 3;
-    tm = x * R + j % R;
-    tn = j / R;
-  } else {
-    tm = bid / ntn;
-    tn = bid - tm * ntn;
-  }
-  const int m0 = tm * F4_BM, n0 = tn * F4_BN;
+  auto tile_of = [&](int j, int& tm, int& tn) {
+    const int b = blockIdx.x, x = b & 7, jj = (b >> 3) * T + j;
+    if ((ntm & 15) == 0 && (flags & 2048)) {
+      const int R = ntm >> 4, per = R * ntn;
+      const int band = jj < per ? x : x + 8, k = jj < per ? jj : jj - per;
+      tm = band * R + k % R;
+      tn = k / R;
+    } else if ((ntm & 7) == 0 && !(flags & 2)) {
+      const int R = ntm >> 3;
+      tm = x * R + jj % R;
+      tn = jj / R;
+    } else {
+      const int t = b * T + j;
+      tm = t / ntn;
+      tn = t - tm * ntn;
+    }
+  };
 
   // DMA piece j (0..7) of wave w: rows 64 w + 8 j + i / 8 of an operand image, lane i ->
-  // physical chunk i % 8 = logical chunk (i % 8) ^ (i / 8).  B rows past N re-read row
-  // N - 1 (their columns are not stored).
+  // physical chunk i % 8.  A: logical chunk (i % 8) ^ (i / 8).  B (interleaved n-tiles: piece
+  // p = 8 w + j holds rows 8 v + u of n-tile u, v = p % 16): SCHED 4 chunk (i % 8) ^ fb(v),
+  // SCHED 5 (i % 8) ^ (v & 7).  B rows past N re-read row N - 1 (their columns are not stored).
   const int lr = lane >> 3, lc = (lane & 7) ^ lr;
-  uint32_t aoff[8], boff[8];
+  uint32_t aoff[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int row = 64 * wid + 8 * j + lr;
-    aoff[j] = (uint32_t)(row * lda + lc * 8) * 2u;
-    // SCHED 4: piece 8 w + j of the B image holds rows 8 v + u (v = piece % 16) of n-tile u
-    // (SCHED 5: logical chunk c of B-image row 8 v + u at c ^ (v & 7))
-    const int blc = PAD ? (lane & 7) ^ f4_fb((8 * wid + j) & 15) : EPI ? (lane & 7) ^ ((8 * wid + j) & 7) : lc;
-    // SWIGLU (flags & 1024, EPI schedules): the tile covers intermediate indices
-    // [128 tn, 128 tn + 128); wave-half wn of its B rows = 64 gate rows then the 64 up rows
-    // of indices 128 tn + 64 wn + 0..63 (Wgu rows j and I + j)
-    const int brow = (flags & 1024) ? ((row & 127) >> 6) * (N >> 1) + 64 * (row >> 7) + (row & 63)
-                                    : min(n0 + row, N - 1) - n0;
-    boff[j] = (uint32_t)(brow * ldb + blc * 8) * 2u;
-  }
-  const bf16_t* Ab = A + (size_t)m0 * lda;
-  const bf16_t* Bb = B + (size_t)((flags & 1024) ? 128 * tn : n0) * ldb;
+  for (int j = 0; j < 8; ++j) aoff[j] = (uint32_t)((64 * wid + 8 * j + lr) * lda + lc * 8) * 2u;
+  struct Tile {
+    int tm, tn, m0, n0;
+    const bf16_t* Ab;
+    const bf16_t* Bb;
+    uint32_t boff[8];
+  };
+  auto setup = [&](int j, Tile& t) {
+    // j opaque from here: keeps the compiler from hoisting a later tile's setup (its
+    // per-lane offsets) over the previous tile, where it would spill
+    int ln = lane;
+    asm volatile("" : "+s"(j), "+v"(ln));
+    tile_of(j, t.tm, t.tn);
+    t.m0 = t.tm * F4_BM;
+    t.n0 = t.tn * F4_BN;
+    t.Ab = A + (size_t)t.m0 * lda;
+    // SWIGLU (flags 1024): the tile covers intermediate indices [128 tn, 128 tn + 128);
+    // wave-half wn of its B rows = 64 gate rows then the 64 up rows of indices
+    // 128 tn + 64 wn + 0..63 (Wgu rows j and I + j)
+    t.Bb = B + (size_t)(swiglu ? 128 * t.tn : t.n0) * ldb;
+    const int lr2 = ln >> 3;
+#pragma unroll
+    for (int j2 = 0; j2 < 8; ++j2) {
+      const int row = 64 * wid + 8 * j2 + lr2;
+      const int v = (8 * wid + j2) & 15;
+      const int blc = PAD ? (ln & 7) ^ f4_fb(v) : (ln & 7) ^ (v & 7);
+      const int brow = swiglu ? ((row & 127) >> 6) * (N >> 1) + 64 * (row >> 7) + (row & 63)
+                              : min(t.n0 + row, N - 1) - t.n0;
+      t.boff[j2] = (uint32_t)(brow * ldb + blc * 8) * 2u;
+    }
+  };
   const uint32_t lbase = (uint32_t)(uintptr_t)lds;
-  // LDS byte offsets of stage s's A and B images: SCHED 0 / 1 two 64 KiB stage buffers;
-  // SCHED 2 a ring of five 32 KiB image slots, A of stage s in slot 2s % 5, B in (2s + 1) % 5
-  auto slot_a = [&](int s) -> uint32_t {
-    if constexpr (RING) return (uint32_t)(((2 * s) % 5) * F4_IMG);
-    else return (uint32_t)((s & 1) * STG);
+  // LDS byte offsets of global stage g's A and B images (g counts stages over the
+  // workgroup's tiles, so the ring keeps rotating across a tile seam)
+  auto slot_a = [&](int g) -> uint32_t {
+    if constexpr (RING) return (uint32_t)(((2 * g) % 5) * F4_IMG);
+    else return (uint32_t)((g & 1) * STG);
   };
-  auto slot_b = [&](int s) -> uint32_t {
-    if constexpr (RING) return (uint32_t)(((2 * s + 1) % 5) * F4_IMG);
-    else return (uint32_t)((s & 1) * STG + F4_IMG);
+  auto slot_b = [&](int g) -> uint32_t {
+    if constexpr (RING) return (uint32_t)(((2 * g + 1) % 5) * F4_IMG);
+    else return (uint32_t)((g & 1) * STG + F4_IMG);
   };
-  // piece p of stage s: A pieces 0..7, B pieces 8..15
-  auto piece = [&](int s, int p) {
+  // piece p of local stage s (k offset) into global stage g's slots: A pieces 0..7, B 8..15
+  auto piece = [&](const Tile& t, int s, int g, int p) {
     if (p < 8)
-      f4_dma(Ab + s * F4_BK, aoff[p], __builtin_amdgcn_readfirstlane(lbase + slot_a(s) + (64 * wid + 8 * p) * 128));
+      f4_dma(t.Ab + s * F4_BK, aoff[p], __builtin_amdgcn_readfirstlane(lbase + slot_a(g) + (64 * wid + 8 * p) * 128));
     else
-      f4_dma(Bb + s * F4_BK, boff[p - 8],
-             __builtin_amdgcn_readfirstlane(lbase + slot_b(s) +
+      f4_dma(t.Bb + s * F4_BK, t.boff[p - 8],
+             __builtin_amdgcn_readfirstlane(lbase + slot_b(g) +
                                             (PAD ? (8 * wid + p - 8) * F4_PIECE_BP : (64 * wid + 8 * (p - 8)) * 128)));
   };
 
-  floatx4_t acc[8][8];  // [n-tile u][m-tile t]: D = B_tile . A_tile^T
-#pragma unroll
-  for (int u = 0; u < 8; ++u)
-#pragma unroll
-    for (int t = 0; t < 8; ++t) acc[u][t] = floatx4_t{0.f, 0.f, 0.f, 0.f};
+  floatx4_t acc[8][8];  // [n-tile u][m-tile t]: D = A_tile . B_tile^T
 
   // fragment of 16 rows x 32 k (half h of a stage): lane l reads row base + (l & 15),
-  // logical chunk 4 h + (l >> 4) at physical chunk (4 h + (l >> 4)) ^ (l & 7)
+  // logical chunk 4 h + (l >> 4).  A: physical chunk (4 h + (l >> 4)) ^ (l & 7).  B n-tile u:
+  // rows 8 v + u (v = l & 15) -- SCHED 4 of padded pieces wn * 16 + v, chunk (4 h + q) ^ fb(v);
+  // SCHED 5 chunk (4 h + q) ^ (v & 7)
   const uint32_t loff = (uint32_t)((lane & 15) * 128 + (((lane >> 4) ^ (lane & 7)) << 4));
   const uint32_t fa_base = lbase + (uint32_t)(wm * 128 * 128);
-  // SCHED 4 n-tile u: rows 8 v + u of pieces wn * 16 + v (v = l & 15), chunk (4 h + q) ^ fb(v)
-  const uint32_t fb_base =
-      PAD   ? lbase + (uint32_t)((wn * 16 + (lane & 15)) * F4_PIECE_BP + (((lane >> 4) ^ f4_fb(lane & 15)) << 4))
-      : EPI ? (uint32_t)((wn * 128 + 8 * (lane & 15)) * 128 + (((lane >> 4) ^ (lane & 7)) << 4))  // + lbase at use
-            : lbase + (uint32_t)(wn * 128 * 128);
-  // read slot r (0..15) of half h of stage s: slots 0..7 the n-tiles, 8..15 the m-tiles
-  auto read_slot = [&](auto r_c, int s, int h, F4Frags& f) {
+  const uint32_t fb_off =
+      PAD ? (uint32_t)((wn * 16 + l16) * F4_PIECE_BP + ((q ^ f4_fb(l16)) << 4))
+          : (uint32_t)((wn * 128 + 8 * l16) * 128 + ((q ^ (l16 & 7)) << 4));
+  // read slot r (0..15) of half h of global stage g: slots 0..7 the n-tiles, 8..15 the m-tiles
+  auto read_slot = [&](auto r_c, int g, int h, F4Frags& f) {
     constexpr int r = decltype(r_c)::value;
-    const uint32_t o = loff ^ (uint32_t)(64 * h);
     if constexpr (r < 8) {
-      if constexpr (PAD) f4_read<r * 128>(f.b[r], fb_base + slot_b(s) + (uint32_t)(64 * h));
-      else if constexpr (EPI) f4_read<r * 128>(f.b[r], lbase + (fb_base ^ (uint32_t)(64 * h)) + slot_b(s));
-      else f4_read<r * 2048>(f.b[r], fb_base + slot_b(s) + o);
+      if constexpr (PAD) f4_read<r * 128>(f.b[r], lbase + fb_off + slot_b(g) + (uint32_t)(64 * h));
+      else f4_read<r * 128>(f.b[r], lbase + (fb_off ^ (uint32_t)(64 * h)) + slot_b(g));
     } else {
-      f4_read<(r - 8) * 2048>(f.a[r - 8], fa_base + slot_a(s) + o);
+      f4_read<(r - 8) * 2048>(f.a[r - 8], fa_base + slot_a(g) + (loff ^ (uint32_t)(64 * h)));
     }
   };
-  auto mfma_group = [&](auto g_c, F4Frags& f) {
-    constexpr int g = decltype(g_c)::value;
-    f4_sfor<8>([&](auto u_c) {
-      constexpr int u = decltype(u_c)::value;
-      if constexpr (EPI) f4_mfma<HK>(acc[u][g], f.a[g], f.b[u]);
-      else f4_mfma<HK>(acc[u][g], f.b[u], f.a[g]);
-    });
-  };
-
-  // one stage (64 deep): half 0 = 64 MFMAs on f0 (its k 0..31) with half 1's 16 fragment
-  // reads interleaved; then (NEXT) wait for stage s + 1 (this wave's only DMAs in flight)
-  // and for this wave's reads, barrier (every wave is done with stage s's buffer), half 1
-  // = 64 MFMAs on f1 with (DMA) stage s + 2's 16 pieces into stage s's buffer and (NEXT)
-  // stage s + 1's half-0 reads interleaved, two of each per 8-MFMA group
   F4Frags f0, f1;
   // 64 MFMAs of one half on f with hook(i) after MFMA i (i = 8 t + u)
   auto half = [&](F4Frags& f, auto&& hook) {
     f4_sfor<64>([&](auto i_c) {
       constexpr int i = decltype(i_c)::value;
-      if constexpr (EPI) f4_mfma<HK>(acc[i & 7][i >> 3], f.a[i >> 3], f.b[i & 7]);
-      else f4_mfma<HK>(acc[i & 7][i >> 3], f.b[i & 7], f.a[i >> 3]);
+      f4_mfma<HK>(acc[i & 7][i >> 3], f.a[i >> 3], f.b[i & 7]);
       hook(i_c);
     });
   };
-  // one stage (64 deep), SCHED 0: half 0 = 64 MFMAs on f0 (its k 0..31) with half 1's 16
-  // fragment reads interleaved; then (NEXT) wait for stage s + 1 (this wave's only DMAs in
-  // flight) and this wave's reads, barrier (every wave is done with stage s's buffer);
-  // half 1 = 64 MFMAs on f1 with (DMA) stage s + 2's 16 pieces into stage s's buffer and
-  // (NEXT) stage s + 1's half-0 reads interleaved, two of each per 8-MFMA group.
-  // SCHED 1 (the 3-phase form): half 0 reads f1 over its first 48 MFMAs; barrier; half 1
-  // issues stage s + 2's pieces over its first 48 MFMAs, then waits for stage s + 1 only
-  // (vmcnt(16): the new pieces may fly), barrier, and reads stage s + 1's half-0 fragments
-  // one per MFMA over its last 16 -- stage s + 1 has a whole stage of DMA latency cover.
-  // SCHED 2 (five 32 KiB image slots): as SCHED 1, but stage s + 2's A image goes into the
-  // slot stage s - 1's B image freed, so its 8 pieces spread over half 0 (one per 8 MFMAs)
-  // and only the B pieces (into stage s's A slot) wait for the mid barrier: the 16 DMA
-  // issues per stage no longer crowd one half.
-  auto stage = [&](int s, auto next_c, auto dma_c) {
+  // one stage (64 deep) of tile t, local stage s = global stage g:
+  //  SCHED 4 (two stage buffers, the 3-phase form): half 0 reads f1 over its first 48 MFMAs;
+  //   barrier; half 1 issues stage s + 2's 16 pieces over its first 48 MFMAs, waits for
+  //   stage s + 1 only (vmcnt(16): the new pieces may fly), barrier, reads stage s + 1's
+  //   half-0 fragments one per MFMA over its last 16.
+  //  SCHED 5 (five 32 KiB image slots, A of stage g in slot 2g % 5, B in 2g + 1): stage
+  //   s + 2's A image goes into the slot stage g - 1's B freed, so its 8 pieces spread over
+  //   half 0 and only the B pieces (into stage g's A slot) wait for the mid barrier; the
+  //   barrier for stage s + 1 at MFMA 39 of half 1, its reads over MFMAs 40..55, and the
+  //   next half 0 waits per 8-MFMA group for exactly the fragments it uses.
+  // NEXT: stage s + 1 follows in this tile; DMA: stage s + 2 is staged
+  auto stage = [&](const Tile& t, int s, int g, auto next_c, auto dma_c) {
     constexpr bool NEXT = decltype(next_c)::value, DMA = decltype(dma_c)::value;
     if constexpr (RING) {
-      // SCHED 3: the barrier at MFMA 39 of half 1 and stage s + 1's reads over MFMAs 40..55
-      // (8 MFMAs of cover before the stage ends); the next half 0 waits per 8-MFMA group
-      // for exactly the fragments it uses (n-tiles first, then m-tile t before group t)
-      constexpr int BAR = 39;
       half(f0, [&](auto i_c) {
         constexpr int i = decltype(i_c)::value;
         if constexpr (i % 8 == 7 && i < 63) {
-          // before group t = (i + 1) / 8: reads 0 .. 8 + t of f0 done; younger: the rest of
-          // f0's (7 - t) and the f1 reads issued so far (one per 3 MFMAs, i % 3 == 2)
-          constexpr int t = (i + 1) / 8;
+          // before group gi = (i + 1) / 8: reads 0 .. 8 + gi of f0 done; younger: the rest of
+          // f0's (7 - gi) and the f1 reads issued so far (one per 3 MFMAs, i % 3 == 2)
+          constexpr int gi = (i + 1) / 8;
           constexpr int nf1 = (i + 1) / 3 < 16 ? (i + 1) / 3 : 16;
-          constexpr int X = (7 - t) + nf1 > 15 ? 15 : (7 - t) + nf1;
+          constexpr int X = (7 - gi) + nf1 > 15 ? 15 : (7 - gi) + nf1;
           asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(X) : "memory");
         }
-        if constexpr (DMA && i % 8 == 7) piece(s + 2, i / 8);
-        if constexpr (i % 3 == 2 && i / 3 < 16) read_slot(std::integral_constant<int, i / 3>{}, s, 1, f1);
+        if constexpr (DMA && i % 8 == 7) piece(t, s + 2, g + 2, i / 8);
+        if constexpr (i % 3 == 2 && i / 3 < 16) read_slot(std::integral_constant<int, i / 3>{}, g, 1, f1);
       });
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       half(f1, [&](auto i_c) {
         constexpr int i = decltype(i_c)::value;
-        if constexpr (DMA && i % 5 == 0 && i / 5 < 8) piece(s + 2, 8 + i / 5);
-        if constexpr (NEXT && i == BAR) {
+        if constexpr (DMA && i % 5 == 0 && i / 5 < 8) piece(t, s + 2, g + 2, 8 + i / 5);
+        if constexpr (NEXT && i == 39) {
           if constexpr (DMA) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
           else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
         }
-        if constexpr (NEXT && i > BAR && i <= BAR + 16) read_slot(std::integral_constant<int, i - BAR - 1>{}, s + 1, 0, f0);
+        if constexpr (NEXT && i > 39 && i <= 55) read_slot(std::integral_constant<int, i - 40>{}, g + 1, 0, f0);
       });
-      if constexpr (NEXT) {
-        // the next half 0's group 0 needs reads 0..8 (8 n-tiles + m-tile 0)
-        asm volatile("s_waitcnt lgkmcnt(7)" ::: "memory");
-        return;
-      }
+      if constexpr (NEXT) asm volatile("s_waitcnt lgkmcnt(7)" ::: "memory");  // next group 0: reads 0..8
+      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     } else {
       half(f0, [&](auto i_c) {
         constexpr int i = decltype(i_c)::value;
-        if constexpr (i % 3 == 2 && i / 3 < 16) read_slot(std::integral_constant<int, i / 3>{}, s, 1, f1);
+        if constexpr (i % 3 == 2 && i / 3 < 16) read_slot(std::integral_constant<int, i / 3>{}, g, 1, f1);
       });
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       half(f1, [&](auto i_c) {
         constexpr int i = decltype(i_c)::value;
-        if constexpr (DMA && i % 3 == 0 && i / 3 < 16) piece(s + 2, i / 3);
+        if constexpr (DMA && i % 3 == 0 && i / 3 < 16) piece(t, s + 2, g + 2, i / 3);
         if constexpr (NEXT && i == 47) {
           if constexpr (DMA) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
           else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
         }
-        if constexpr (NEXT && i >= 48) read_slot(std::integral_constant<int, i - 48>{}, s + 1, 0, f0);
+        if constexpr (NEXT && i >= 48) read_slot(std::integral_constant<int, i - 48>{}, g + 1, 0, f0);
       });
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
-    // the next stage's first MFMAs read f0: this wave's half-0 reads must have landed
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };
 
   const int ns = K / F4_BK;  // >= 2 (launcher-checked)
-  // prologue: stages 0 and 1 in flight, stage 0 landed, its half-0 fragments read
-#pragma unroll
-  for (int s = 0; s < 2; ++s)
-#pragma unroll
-    for (int p = 0; p < 16; ++p) piece(s, p);
-  asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
-  f4_sfor<16>([&](auto r_c) { read_slot(r_c, 0, 0, f0); });
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  if (stamp) { st_r[1] = __builtin_amdgcn_s_memrealtime(); st_c[1] = __builtin_amdgcn_s_memtime(); }
-
   using T_ = std::true_type;
   using F_ = std::false_type;
-  int s = 0;
+  Tile cur, nxt;
+  setup(0, cur);
+  // prologue of the first tile: stages 0 and 1 in flight
+#pragma unroll
+  for (int st = 0; st < 2; ++st)
+#pragma unroll
+    for (int p = 0; p < 16; ++p) piece(cur, st, st, p);
+  int g0 = 0;  // global stage of the current tile's stage 0
+#pragma unroll
+  for (int j = 0; j < T; ++j) {
+    // stage 0 of this tile landed (its stage 1 may fly), fragments of its half 0 read
+    asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int tt = 0; tt < 8; ++tt) acc[u][tt] = floatx4_t{0.f, 0.f, 0.f, 0.f};
+    f4_sfor<16>([&](auto r_c) { read_slot(r_c, g0, 0, f0); });
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    int s = 0;
 #pragma unroll 1
-  for (; s + 2 < ns; ++s) stage(s, T_{}, T_{});
-  stage(s, T_{}, F_{});
-  stage(s + 1, F_{}, F_{});
-  if (stamp) { st_r[2] = __builtin_amdgcn_s_memrealtime(); st_c[2] = __builtin_amdgcn_s_memtime(); }
+    for (; s + 2 < ns; ++s) stage(cur, s, g0 + s, T_{}, T_{});
+    stage(cur, s, g0 + s, T_{}, F_{});
+    stage(cur, s + 1, g0 + s + 1, F_{}, F_{});
+    // 16 wait states for the last MFMAs' accumulators
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+    const bool more = j + 1 < T;
 
-  // epilogue: 16 wait states for the last MFMAs' accumulators
-  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
-  const int l16 = lane & 15, q = lane >> 4;
-  if constexpr (EPI) {
-    // SCHED 4 (product D = A_tile . B_tile^T): lane l, register r of tile (u, t) is output
+    // epilogue (product D = A_tile . B_tile^T): lane l, register r of tile (u, t) is output
     // row 16 t + 4 (l >> 4) + r, column wn*128 + 8 (l & 15) + u (n-tile u holds columns
     // 8 v + u), so the eight n-tiles give 8 consecutive columns and the 16 lanes of a row
     // 256 contiguous bytes: one 16-byte store per (m-tile, r), 4 rows per instruction, no LDS
-    const int col = n0 + wn * 128 + 8 * l16;
-    const bool col_ok = n0 + wn * 128 < N;
     const auto rs =
-        __builtin_amdgcn_make_buffer_rsrc(C + (size_t)(m0 + wm * 128) * ldc, 0, 128 * ldc * 2, 0x00020000);
-    if (flags & 1024) {
+        __builtin_amdgcn_make_buffer_rsrc(C + (size_t)(cur.m0 + wm * 128) * ldc, 0, 128 * ldc * 2, 0x00020000);
+    if constexpr (swiglu) {
       // SWIGLU: lanes v = l & 15 < 8 hold gate indices jb + 8 v + u, lanes v + 8 the up values
       // of the same indices; after a row_ror:8 exchange each lane of the pair has both and
       // computes s = silu(g) * u -- k_swiglu_fwd's arithmetic on the bf16-rounded g and u,
       // same bits -- for 4 of the 8 indices.  gu keeps its [M, 2I] layout (gate | up).
-      const int I = N >> 1, jb = 128 * tn + 64 * wn, v = l16;
+      const int I = N >> 1, jb = 128 * cur.tn + 64 * wn, v = l16;
       const int gcol = (v < 8 ? jb : I + jb) + 8 * (v & 7), e0 = v < 8 ? 0 : 4;
       const auto rss =
-          __builtin_amdgcn_make_buffer_rsrc(S + (size_t)(m0 + wm * 128) * ldS, 0, 128 * ldS * 2, 0x00020000);
+          __builtin_amdgcn_make_buffer_rsrc(S + (size_t)(cur.m0 + wm * 128) * ldS, 0, 128 * ldS * 2, 0x00020000);
 #pragma unroll
       for (int t = 0; t < 8; ++t)
 #pragma unroll
@@ -383,7 +372,8 @@ __global__ __launch_bounds__(256, 1) void k_gemm_fw4(const bf16_t* __restrict__ 
           typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
           __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{o2[0], o2[1]}, rss, soff, 0, 0);
         }
-    } else if (col_ok) {
+    } else if (cur.n0 + wn * 128 < N) {
+      const int col = cur.n0 + wn * 128 + 8 * l16;
 #pragma unroll
       for (int t = 0; t < 8; ++t)
 #pragma unroll
@@ -398,79 +388,53 @@ __global__ __launch_bounds__(256, 1) void k_gemm_fw4(const bf16_t* __restrict__ 
           else __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
         }
     }
-  } else {
-    // wave w stages its 128 x 128 block in bytes [32 KiB w, 32 KiB (w + 1)) once every wave
-    // is done with the ring: row r (256 bytes), 16-byte chunk c at c ^ (r & 15)
-    asm volatile("s_barrier" ::: "memory");
-    char* const stg = lds + wid * 32768;
+    if (more) {
+      // the next tile's stages 0 and 1 (global stages g0 + ns, + 1), issued right behind this
+      // tile's stores so their latency overlaps the store drain and the next tile's setup
+      // (every wave is done with this tile's slots after the barrier)
+      setup(j + 1, nxt);
+      asm volatile("s_barrier" ::: "memory");
 #pragma unroll
-    for (int t = 0; t < 8; ++t)
+      for (int st = 0; st < 2; ++st)
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int r = 16 * t + l16, c = 2 * u + (q >> 1);
-        *reinterpret_cast<uint2*>(stg + r * 256 + ((c ^ (r & 15)) << 4) + (q & 1) * 8) = f4_pack<HK>(acc[u][t]);
-      }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's own block only
-    const int ch = lane & 15, r0 = lane >> 4;
-    const int col = n0 + wn * 128 + ch * 8;
-    const bool col_ok = col < N;
-    const auto rs =
-        __builtin_amdgcn_make_buffer_rsrc(C + (size_t)(m0 + wm * 128) * ldc, 0, 128 * ldc * 2, 0x00020000);
-#pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      const int r = 4 * i + r0;
-      const f4_u32x4_t v = *reinterpret_cast<const f4_u32x4_t*>(stg + r * 256 + ((ch ^ (r & 15)) << 4));
-      const int off = (r * ldc + col) * 2;
-      if (col_ok) {
-        if (flags & 1) __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 16);  // sc1 write-through
-        else if (flags & 4) __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 2);  // nt
-        else __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
-      }
-    }
-  }
-  if (stamp) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    st_r[3] = __builtin_amdgcn_s_memrealtime();
-    st_c[3] = __builtin_amdgcn_s_memtime();
-    unsigned long long* o = stamps + 16 * (size_t)blockIdx.x;
-    if (lane < 4) {
-      o[lane] = lane == 0 ? st_r[0] : lane == 1 ? st_r[1] : lane == 2 ? st_r[2] : st_r[3];
-      o[4 + lane] = lane == 0 ? st_c[0] : lane == 1 ? st_c[1] : lane == 2 ? st_c[2] : st_c[3];
-    }
-    if (lane == 0) {
-      unsigned hw, xcc;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      o[8] = hw;
-      o[9] = xcc;
-      o[10] = (unsigned long long)((tm << 16) | tn);
+        for (int p = 0; p < 16; ++p) piece(nxt, st, g0 + ns + st, p);
+      cur = nxt;
+      g0 += ns;
     }
   }
 }
 
-// flags: 1 = write-through (sc1) C stores, 4 = nt C stores, 2 = row-major tile order (A/B knob);
-// schedule: 16 = SCHED 1, 128 = SCHED 3, 144 = SCHED 5, else SCHED 4; 1024 = SwiGLU epilogue (SCHED 4 / 5)
+// flags: 1 = write-through (sc1) C stores, 4 = nt C stores; tile order 2 = row-major, 2048 = half-height
+// XCD bands (default XCD row bands); schedule 16 | 128 = SCHED 5 (else SCHED 4); 1024 = SwiGLU epilogue;
+// 4096 = two tiles per workgroup (the second tile's first stages prefetched behind the first's epilogue)
 DLT_API int dlt_gemm_fw4(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K, int lda, int ldb, int ldc,
-                         int flags, int hk, bf16_t* S, int ldS, unsigned long long* stamps, hipStream_t st) {
+                         int flags, int hk, bf16_t* S, int ldS, hipStream_t st) {
   if (M <= 0 || N <= 0 || K <= 0 || M % F4_BM || N % 128 || K % F4_BK || K < 2 * F4_BK || lda % 8 || ldb % 8 ||
       ldc % 8 || lda < K || ldb < K || ldc < N)
     return -1;
-  // SWIGLU epilogue (flags & 1024): N = 2I with I % 128 == 0, s [M, ldS >= I], EPI schedules
   const int sched_bits = flags & (16 | 128);  // 0: SCHED 4, 16 | 128: SCHED 5
-  if ((flags & 1024) && (S == nullptr || N % 256 || ldS < N / 2 || ldS % 8 || sched_bits == 16 || sched_bits == 128 ||
-                         128L * ldS * 2 > 0x7fffffffL || (long)(N / 2 + 127) * ldb * 2 > 0xffffffffL))
+  if (sched_bits == 16 || sched_bits == 128) return -1;
+  // SwiGLU epilogue (flags & 1024): N = 2I with I % 128 == 0, s [M, ldS >= I]
+  if ((flags & 1024) && (S == nullptr || N % 256 || ldS < N / 2 || ldS % 8 || 128L * ldS * 2 > 0x7fffffffL ||
+                         (long)(N / 2 + 127) * ldb * 2 > 0xffffffffL))
     return -1;
   const long tiles = (long)(M / F4_BM) * ((N + F4_BN - 1) / F4_BN);
   if (tiles > 0x7fffffff || 128L * ldc * 2 > 0x7fffffffL || 256L * lda * 2 > 0xffffffffL ||
       256L * ldb * 2 > 0xffffffffL)
     return -1;
-  if ((flags & 128) && (flags & 16))
-    DLT_HK_DISPATCH(hk, k_gemm_fw4<HKC, 5><<<(int)tiles, 256, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, S, ldS, stamps));
-  else if (flags & 128)
-    DLT_HK_DISPATCH(hk, k_gemm_fw4<HKC, 3><<<(int)tiles, 256, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, S, ldS, stamps));
-  else if (flags & 16)
-    DLT_HK_DISPATCH(hk, k_gemm_fw4<HKC, 1><<<(int)tiles, 256, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, S, ldS, stamps));
-  else
-    DLT_HK_DISPATCH(hk, k_gemm_fw4<HKC, 4><<<(int)tiles, 256, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, S, ldS, stamps));
+  // two tiles per workgroup (4096): the XCD orders need tiles % 16 == 0, row-major tiles % 2
+  if ((flags & 4096) && (tiles % 16 || (flags & 1024))) return -1;
+  const int grid = (int)((flags & 4096) ? tiles / 2 : tiles);
+  const bool two = flags & 4096, sw = flags & 1024;
+#define F4_LAUNCH(SC, TT_, SW_) \
+  DLT_HK_DISPATCH(hk, k_gemm_fw4<HKC, SC, TT_, SW_><<<grid, 256, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, S, ldS))
+  if (sw) {  // the gate/up projection: one tile per workgroup
+    if (sched_bits) F4_LAUNCH(5, 1, true);
+    else F4_LAUNCH(4, 1, true);
+  } else if (sched_bits && two) F4_LAUNCH(5, 2, false);
+  else if (sched_bits) F4_LAUNCH(5, 1, false);
+  else if (two) F4_LAUNCH(4, 2, false);
+  else F4_LAUNCH(4, 1, false);
+#undef F4_LAUNCH
   DLT_CHECK_LAUNCH();
 }

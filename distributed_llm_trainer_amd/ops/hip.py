@@ -65,7 +65,7 @@ _SIGS = {
     "dlt_gemm_bf16_tn": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                          c_void_p],
     "dlt_gemm_fw4": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
-                     c_int, c_void_p, c_void_p],
+                     c_int, c_void_p],
     "dlt_gemm_bf16_qkv_rope": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                                c_void_p],
     "dlt_gemm_bf16_gu_swiglu": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
@@ -895,12 +895,13 @@ def gemm_fw4_fits(M: int, N: int, K: int) -> bool:
     return M > 0 and N > 0 and K > 0 and M % 256 == 0 and N % 128 == 0 and K % 64 == 0 and K >= 128
 
 
-# launch flags of k_gemm_fw4: 1 = write-through (sc1) C stores, 2 = row-major tile order
+# launch flags of k_gemm_fw4 (csrc/gemm_fw4.hip): 1 = write-through (sc1) / 4 = nt C stores, 2 =
+# row-major / 2048 = half-band tile order, 16 | 128 = SCHED 5, 4096 = two tiles per workgroup
 _FW4_FLAGS = int(os.environ.get("DLT_GEMM_FW4_FLAGS", "148"))
 
 
 def gemm_fw4(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
-             flags: Optional[int] = None, stamps: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+             flags: Optional[int] = None) -> Optional[torch.Tensor]:
     """C[M,N] = A[M,K] @ B[N,K]^T (bf16 or fp16 in/out, fp32 accumulate) with the 4-wave
     256 x 256 one-tile-per-workgroup MFMA kernel (128 x 128 per wave, AGPR accumulators).
     Returns None (nothing launched) when the shape does not tile (M % 256, N % 128, K % 64,
@@ -914,11 +915,10 @@ def gemm_fw4(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = Non
     c = torch.empty(M, N, dtype=a.dtype, device=a.device) if out is None else out
     _req(c, a.dtype, "gemm_fw4.c", M * N)
     fl = _FW4_FLAGS if flags is None else flags
-    if stamps is not None:  # diagnostic: int64 [tiles, 16] per-workgroup timestamps (csrc/gemm_fw4.hip)
-        if stamps.dtype != torch.int64 or stamps.numel() < 16 * (M // 256) * ((N + 255) // 256) or not stamps.is_cuda:
-            raise ValueError("gemm_fw4: stamps must be a CUDA int64 tensor of 16 * tiles entries")
-    _chk(lib().dlt_gemm_fw4(_p(a), _p(b), _p(c), M, N, K, K, K, N, fl & ~1024, hk, None, 0,
-                            _p(stamps) if stamps is not None else None, _stream()), "gemm_fw4")
+    rc = lib().dlt_gemm_fw4(_p(a), _p(b), _p(c), M, N, K, K, K, N, fl & ~1024, hk, None, 0, _stream())
+    if rc == -1:
+        return None  # a launch variant the shape does not take (two tiles per workgroup: tiles % 16)
+    _chk(rc, "gemm_fw4")
     return c
 
 
@@ -946,7 +946,7 @@ def gemm_fw4_swiglu(x: torch.Tensor, wgu: torch.Tensor, gu_out: Optional[torch.T
     fl = (_FW4_FLAGS if flags is None else flags) & ~(16 | 128)
     if flags is not None and (flags & (16 | 128)) == (16 | 128):
         fl |= 16 | 128  # SCHED 5
-    _chk(lib().dlt_gemm_fw4(_p(x), _p(wgu), _p(gu), M, I2, K, K, K, I2, fl | 1024, hk, _p(s), I, None, _stream()),
+    _chk(lib().dlt_gemm_fw4(_p(x), _p(wgu), _p(gu), M, I2, K, K, K, I2, (fl | 1024) & ~4096, hk, _p(s), I, _stream()),
          "gemm_fw4_swiglu")
     return gu, s
 

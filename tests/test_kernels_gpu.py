@@ -583,17 +583,19 @@ def test_gemm_bf16(M, N, K, dtype):
                                    (768, 1280, 512), (256, 256, 128), (1280, 640, 192), (2048, 384, 256)])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 def test_gemm_fw4(M, N, K, dtype):
-    """4-wave 256 x 256 MFMA GEMM C = A B^T (csrc/gemm_fw4.hip, AGPR accumulators, every
-    schedule) vs fp32 torch, bf16 and fp16 operands: every element within 16-bit output
+    """4-wave 256 x 256 MFMA GEMM C = A B^T (csrc/gemm_fw4.hip, AGPR accumulators, both
+    schedules) vs fp32 torch, bf16 and fp16 operands: every element within 16-bit output
     rounding, every tile written exactly once (a poisoned output is fully overwritten),
-    plain and write-through stores, XCD-band and row-major tile orders; the diagnostic
-    stamps leave the result unchanged."""
+    plain / write-through / nt stores, XCD-band / half-band / row-major tile orders, one
+    or two tiles per workgroup -- all bitwise equal."""
     torch.manual_seed(M + N + K)
     a = (torch.rand(M, K, device=DEV) * 2 - 1).to(dtype)
     b = (torch.rand(N, K, device=DEV) * 2 - 1).to(dtype)
     want = a.float() @ b.float().t()
     first = None
-    for flags in (1, 0, 4, 2, 17, 16, 18, 129, 128, 130, 144, 145, 148, 146):
+    tiles = (M // 256) * ((N + 255) // 256)
+    two = (4096, 4100, 4240, 4244, 6148) if tiles % 16 == 0 else ()  # two tiles per workgroup
+    for flags in (1, 0, 4, 2, 2048, 144, 145, 148, 146) + two:
         c = torch.full((M, N), float("nan"), device=DEV, dtype=dtype)
         assert hip.gemm_fw4(a, b, out=c, flags=flags) is not None
         assert not torch.isnan(c).any(), f"unwritten output (flags {flags})"
@@ -602,10 +604,9 @@ def test_gemm_fw4(M, N, K, dtype):
         if first is None:
             first = c
         assert torch.equal(c, first), f"schedules / store flavours must agree bitwise (flags {flags})"
-    st = torch.zeros((M // 256) * ((N + 255) // 256), 16, dtype=torch.int64, device=DEV)
-    c = torch.empty(M, N, device=DEV, dtype=dtype)
-    hip.gemm_fw4(a, b, out=c, flags=0, stamps=st)
-    assert torch.equal(c, first) and bool((st[:, 3] >= st[:, 0]).all())
+    if tiles % 16:
+        assert hip.gemm_fw4(a, b, flags=4096) is None  # two tiles per workgroup need tiles % 16 == 0
+    assert hip.gemm_fw4(a, b, flags=16) is None and hip.gemm_fw4(a, b, flags=128) is None  # retired schedules
     assert hip.gemm_fw4(a[:, :K - 32].contiguous(), b[:, :K - 32].contiguous()) is None  # K % 64
     assert hip.gemm_fw4(a, b[:N - 8].contiguous()) is None  # N % 128
 
@@ -618,7 +619,7 @@ def test_gemm_fw4_swiglu(M, I, K, dtype):
     torch.manual_seed(M + I + K)
     x = (torch.rand(M, K, device=DEV) * 2 - 1).to(dtype)
     w = (torch.rand(2 * I, K, device=DEV) * 2 - 1).to(dtype)
-    for flags in (0, 4, 1, 144, 150):
+    for flags in (0, 4, 1, 144, 150, 2048):
         gu, s = hip.gemm_fw4_swiglu(x, w, flags=flags)
         plain = hip.gemm_fw4(x, w, flags=flags)
         assert torch.equal(gu, plain), f"gu differs from the plain GEMM (flags {flags})"

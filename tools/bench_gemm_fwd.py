@@ -33,7 +33,6 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--shapes", default=",".join(SHAPES), help="comma list of SHAPES keys")
     ap.add_argument("--impls", default="lib,bf16,fw4", help="comma list of lib / bf16 / fw4 / fw4<variant>")
-    ap.add_argument("--stamp_flags", type=int, default=16, help="k_gemm_fw4 flags of the --stamps runs")
     ap.add_argument("--dgrad", action="store_true",
                     help="data-gradient shapes dX = dY @ W: the persistent reduction-major kernel (hip.gemm_dgrad), "
                          "hipBLASLt, and k_gemm_fw4 on a transposed weight copy (TN form)")
@@ -41,8 +40,6 @@ def main():
                     help="diagnostic: per-workgroup timestamps of k_gemm_fw4 (SCHED 1) on each shape")
     args = ap.parse_args()
     impls = args.impls.split(",")
-    if args.stamps:
-        return stamps(args)
     if args.dgrad:
         return dgrad(args)
     g = gemm.HipGemm()
@@ -58,15 +55,12 @@ def main():
                           ("fw4", lambda: hip.gemm_fw4(a, b, out=y)),
                           ("fw4p", lambda: hip.gemm_fw4(a, b, out=y, flags=0)),
                           ("fw4nt", lambda: hip.gemm_fw4(a, b, out=y, flags=4)),
-                          ("fw4s1", lambda: hip.gemm_fw4(a, b, out=y, flags=hip._FW4_FLAGS | 16)),
-                          ("fw4s3", lambda: hip.gemm_fw4(a, b, out=y, flags=hip._FW4_FLAGS | 128)),
-                          ("fw4s5", lambda: hip.gemm_fw4(a, b, out=y, flags=144)),
-                          ("fw4s5nt", lambda: hip.gemm_fw4(a, b, out=y, flags=148)),
-                          ("fw4s5w", lambda: hip.gemm_fw4(a, b, out=y, flags=145)),
-                          ("fw4ntrm", lambda: hip.gemm_fw4(a, b, out=y, flags=6)),
-                          ("fw4s5ntrm", lambda: hip.gemm_fw4(a, b, out=y, flags=150)),
-                          ("fw4nth", lambda: hip.gemm_fw4(a, b, out=y, flags=4 | 2048)),
-                          ("fw4s5nth", lambda: hip.gemm_fw4(a, b, out=y, flags=148 | 2048))):
+                          ("fw4rm", lambda: hip.gemm_fw4(a, b, out=y, flags=150)),
+                          ("fw4h", lambda: hip.gemm_fw4(a, b, out=y, flags=148 | 2048)),
+                          ("fw4x2", lambda: hip.gemm_fw4(a, b, out=y, flags=4 | 4096)),
+                          ("fw4s5x2", lambda: hip.gemm_fw4(a, b, out=y, flags=148 | 4096)),
+                          ("fw4hx2", lambda: hip.gemm_fw4(a, b, out=y, flags=148 | 2048 | 4096)),
+                          ("fw4px2", lambda: hip.gemm_fw4(a, b, out=y, flags=144 | 4096))):
             if label not in impls:
                 continue
             if fn is None:
@@ -77,8 +71,7 @@ def main():
         ref = (a.float() @ b.float().t())
         errs = []
         for label, fn in (("fw4", hip.gemm_fw4),
-                          ("fw4s1", lambda a, b, out: hip.gemm_fw4(a, b, out=out, flags=hip._FW4_FLAGS | 16)),
-                          ("fw4s3", lambda a, b, out: hip.gemm_fw4(a, b, out=out, flags=hip._FW4_FLAGS | 128))):
+                          ("fw4x2", lambda a, b, out: hip.gemm_fw4(a, b, out=out, flags=4 | 4096))):
             if label not in impls:
                 continue
             y.fill_(float("nan"))
@@ -112,43 +105,6 @@ def dgrad(args):
         hip.gemm_fw4(dy, wt, out=y, flags=148)
         row.append(f"fw4 relerr {((y.float() - ref).norm() / ref.norm()).item():.1e}")
         print(" | ".join(row), flush=True)
-
-
-def stamps(args):
-    """Per-workgroup phase times of k_gemm_fw4 from its diagnostic stamps: prologue (start ->
-    first fragments in registers), main loop, epilogue (-> stores landed), in us of
-    s_memrealtime (100 MHz) and loop shader-clock cycles; plus the idle gap between a
-    workgroup's end and the next start on the same CU (hardware id)."""
-    import statistics as stt
-    for name in args.shapes.split(","):
-        M, N, K = SHAPES[name]
-        a = torch.randn(M, K, device="cuda").bfloat16()
-        b = torch.randn(N, K, device="cuda").bfloat16()
-        y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-        tiles = (M // 256) * ((N + 255) // 256)
-        st = torch.zeros(tiles, 16, dtype=torch.int64, device="cuda")
-        for _ in range(3):
-            hip.gemm_fw4(a, b, out=y, flags=hip._FW4_FLAGS | args.stamp_flags, stamps=st)
-        torch.cuda.synchronize()
-        s = st.cpu().tolist()
-        t0 = min(r[0] for r in s)
-        pro = [(r[1] - r[0]) / 100 for r in s]
-        loop = [(r[2] - r[1]) / 100 for r in s]
-        epi = [(r[3] - r[2]) / 100 for r in s]
-        cyc = [r[6] - r[5] for r in s]
-        span = (max(r[3] for r in s) - t0) / 100
-        clk = stt.median([(r[6] - r[5]) / max(1, r[2] - r[1]) * 100 / 1000 for r in s])  # GHz
-        by_cu = {}
-        for r in s:
-            by_cu.setdefault((r[9], r[8] & 0xFFFF), []).append((r[0], r[3]))
-        gaps = []
-        for v in by_cu.values():
-            v.sort()
-            gaps += [(v[i + 1][0] - v[i][1]) / 100 for i in range(len(v) - 1)]
-        q = lambda x: f"med {stt.median(x):6.2f} p10 {sorted(x)[len(x) // 10]:6.2f} p90 {sorted(x)[9 * len(x) // 10]:6.2f}"  # noqa: E731
-        print(f"{name} {M}x{N}x{K}: {tiles} tiles, span {span:.1f} us, CUs seen {len(by_cu)}, loop clock {clk:.2f} GHz")
-        print(f"   prologue us {q(pro)} | loop us {q(loop)} | epilogue us {q(epi)}")
-        print(f"   loop kcycles {q([c / 1000 for c in cyc])} | CU idle gap us {q(gaps) if gaps else '-'}", flush=True)
 
 
 if __name__ == "__main__":
