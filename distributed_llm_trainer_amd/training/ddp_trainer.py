@@ -114,7 +114,8 @@ class DistributedTrainer:
         if self.use_engine:
             act = self.dtype if self.device.type == "cuda" else None
             eng = self.model.enable_engine(seed=self.training_config.seed + 1000003 * self.rank, act_dtype=act)
-            if self.training_config.memory_first:
+            if self.training_config.memory_first and self.training_config.defer_roles == "all":
+                # memory-first defers no weight gradient unless the config names roles
                 self.training_config.defer_roles = LEAN_DEFER_ROLES
                 eng.s_refill = True
             eng.defer_roles = parse_defer_roles(self.training_config.defer_roles)

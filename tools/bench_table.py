@@ -19,6 +19,7 @@ REF = {("ddp", "small", 1): 12500, ("ddp", "small", 2): 24100, ("ddp", "small", 
 CONFIGS = {
     "ddp_small": ["--model_size", "small", "--batch_size", "8", "--grad_accum", "4"],
     "ddp_small_lean": ["--model_size", "small", "--batch_size", "8", "--grad_accum", "4", "--memory_lean"],
+    "ddp_small_memfirst": ["--model_size", "small", "--batch_size", "8", "--grad_accum", "4", "--memory_first"],
     "ddp_small_fp16": ["--model_size", "small", "--batch_size", "8", "--grad_accum", "4", "--precision", "fp16"],
     "ddp_small_fp32": ["--model_size", "small", "--batch_size", "8", "--grad_accum", "4", "--precision", "fp32"],
     # head_dim 128 (6 heads of the small model's 768): the D = 128 MFMA attention kernels
