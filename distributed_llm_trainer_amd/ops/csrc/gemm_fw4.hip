@@ -107,12 +107,10 @@ struct F4Frags {
 
 }  // namespace
 
-template <int HK, int SCHED, int TT, int EK>
+template <int HK, int SCHED, int TT, bool SW>
 __global__ __launch_bounds__(256, 1) void k_gemm_fw4(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                      bf16_t* __restrict__ C, int M, int N, int K, int lda, int ldb,
-                                                     int ldc, int flags, bf16_t* __restrict__ S, int ldS,
-                                                     const float* __restrict__ cosT, const float* __restrict__ sinT,
-                                                     int Sq, int rot) {
+                                                     int ldc, int flags, bf16_t* __restrict__ S, int ldS) {
   static_assert(SCHED == 4 || SCHED == 5, "k_gemm_fw4: schedules 4 and 5");
   // SCHED 4: two stage buffers, B pieces padded (conflict-free reads); SCHED 5: the
   // five-slot ring, unpadded B (two-way bank conflicts on its reads)
@@ -123,9 +121,7 @@ __global__ __launch_bounds__(256, 1) void k_gemm_fw4(const bf16_t* __restrict__ 
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wid & 1, wn = wid >> 1;
   const int l16 = lane & 15, q = lane >> 4;
-  // epilogue kind EK: 0 plain, 1 (flags 1024) the gate/up projection with the SwiGLU, 2 (flags
-  // 8192) the packed QKV projection with NeoX RoPE on its q / k columns (head_dim 64)
-  constexpr bool swiglu = EK == 1, rope = EK == 2;
+  constexpr bool swiglu = SW;  // flags 1024: the gate/up projection with the SwiGLU epilogue
   constexpr int T = TT;  // tiles per workgroup (flags 4096: two, the second's first stages prefetched)
 
   // tile j of this workgroup -> (tm, tn): block b runs on the XCD of b % 8 (round-robin
@@ -376,52 +372,6 @@ __global__ __launch_bounds__(256, 1) void k_gemm_fw4(const bf16_t* __restrict__ 
           typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
           __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{o2[0], o2[1]}, rss, soff, 0, 0);
         }
-    } else if (rope && cur.n0 + wn * 128 < rot) {
-      // ROPE (q / k columns < rot = 2H, head_dim 64): lane v = l & 15 holds dims
-      // 8 (v & 7) .. + 7 of head (cb + 8 v) / 64; lanes with (v & 4) == 0 hold rotation
-      // half x1 (dims j < 32), their partner v ^ 4 the x2 half of the same j: after the
-      // exchange each lane writes its own half -- k_rope_qk_inplace's arithmetic on the
-      // bf16-rounded GEMM outputs, same bits; position = row % Sq
-      const int col = cur.n0 + wn * 128 + 8 * l16, j0 = 8 * (l16 & 3);
-      const bool lo_half = (l16 & 4) == 0;
-#pragma unroll
-      for (int t = 0; t < 8; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          floatx4_t lo{acc[0][t][r], acc[1][t][r], acc[2][t][r], acc[3][t][r]};
-          floatx4_t hi{acc[4][t][r], acc[5][t][r], acc[6][t][r], acc[7][t][r]};
-          const uint2 a = f4_pack<HK>(lo), b = f4_pack<HK>(hi);
-          const f4_u32x4_t P{a.x, a.y, b.x, b.y};
-          f4_u32x4_t Q;
-#pragma unroll
-          for (int d = 0; d < 4; ++d) Q[d] = (uint32_t)__shfl_xor((int)P[d], 4, 16);
-          const int row = 16 * t + 4 * q + r;
-          const int pos = (cur.m0 + wm * 128 + row) % Sq;
-          const float4* cp = reinterpret_cast<const float4*>(cosT + (size_t)pos * 32 + j0);
-          const float4* sp = reinterpret_cast<const float4*>(sinT + (size_t)pos * 32 + j0);
-          const float4 c0 = cp[0], c1 = cp[1], s0 = sp[0], s1 = sp[1];
-          const float cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-          const float ss[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-          f4_u32x4_t O;
-#pragma unroll
-          for (int w2 = 0; w2 < 4; ++w2) {
-            uint32_t packed = 0;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              const int e = 2 * w2 + h;
-              const float own = h2f<HK>((uint16_t)(P[w2] >> (16 * h)));
-              const float oth = h2f<HK>((uint16_t)(Q[w2] >> (16 * h)));
-              const float x1 = lo_half ? own : oth, x2 = lo_half ? oth : own;
-              const float o = lo_half ? x1 * cc[e] - x2 * ss[e] : x2 * cc[e] + x1 * ss[e];
-              packed |= (uint32_t)f2h<HK>(o) << (16 * h);
-            }
-            O[w2] = packed;
-          }
-          const int off = (row * ldc + col) * 2;
-          if (flags & 1) __builtin_amdgcn_raw_buffer_store_b128(O, rs, off, 0, 16);
-          else if (flags & 4) __builtin_amdgcn_raw_buffer_store_b128(O, rs, off, 0, 2);
-          else __builtin_amdgcn_raw_buffer_store_b128(O, rs, off, 0, 0);
-        }
     } else if (cur.n0 + wn * 128 < N) {
       const int col = cur.n0 + wn * 128 + 8 * l16;
 #pragma unroll
@@ -456,11 +406,9 @@ __global__ __launch_bounds__(256, 1) void k_gemm_fw4(const bf16_t* __restrict__ 
 
 // flags: 1 = write-through (sc1) C stores, 4 = nt C stores; tile order 2 = row-major, 2048 = half-height
 // XCD bands (default XCD row bands); schedule 16 | 128 = SCHED 5 (else SCHED 4); 1024 = SwiGLU epilogue;
-// 4096 = two tiles per workgroup (the second tile's first stages prefetched behind the first's epilogue);
-// 8192 = RoPE epilogue (packed QKV, head_dim 64)
+// 4096 = two tiles per workgroup (the second tile's first stages prefetched behind the first's epilogue)
 DLT_API int dlt_gemm_fw4(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K, int lda, int ldb, int ldc,
-                         int flags, int hk, bf16_t* S, int ldS, const float* cosT, const float* sinT, int Sq,
-                         int rot, hipStream_t st) {
+                         int flags, int hk, bf16_t* S, int ldS, hipStream_t st) {
   if (M <= 0 || N <= 0 || K <= 0 || M % F4_BM || N % 128 || K % F4_BK || K < 2 * F4_BK || lda % 8 || ldb % 8 ||
       ldc % 8 || lda < K || ldb < K || ldc < N)
     return -1;
@@ -470,34 +418,23 @@ DLT_API int dlt_gemm_fw4(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int
   if ((flags & 1024) && (S == nullptr || N % 256 || ldS < N / 2 || ldS % 8 || 128L * ldS * 2 > 0x7fffffffL ||
                          (long)(N / 2 + 127) * ldb * 2 > 0xffffffffL))
     return -1;
-  // RoPE epilogue (flags & 8192): head_dim 64 q / k columns [0, rot), rot % 128 == 0, M % Sq == 0,
-  // cos / sin [>= Sq, 32] fp32
-  if ((flags & 8192) && ((flags & 1024) || cosT == nullptr || sinT == nullptr || Sq <= 0 || M % Sq || rot % 128 ||
-                         rot > N))
-    return -1;
   const long tiles = (long)(M / F4_BM) * ((N + F4_BN - 1) / F4_BN);
   if (tiles > 0x7fffffff || 128L * ldc * 2 > 0x7fffffffL || 256L * lda * 2 > 0xffffffffL ||
       256L * ldb * 2 > 0xffffffffL)
     return -1;
   // two tiles per workgroup (4096): the XCD orders need tiles % 16 == 0, row-major tiles % 2
-  if ((flags & 4096) && (tiles % 16 || (flags & (1024 | 8192)))) return -1;
+  if ((flags & 4096) && (tiles % 16 || (flags & 1024))) return -1;
   const int grid = (int)((flags & 4096) ? tiles / 2 : tiles);
-  const bool two = flags & 4096, sw = flags & 1024, rp = flags & 8192;
-#define F4_LAUNCH(SC, TT_, EK_)                                                                                   \
-  DLT_HK_DISPATCH(hk, k_gemm_fw4<HKC, SC, TT_, EK_><<<grid, 256, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, S, \
-                                                                          ldS, cosT, sinT, Sq, rot))
-  if (sw || rp) {  // fused epilogues: one tile per workgroup
-    if (sched_bits) {
-      if (sw) F4_LAUNCH(5, 1, 1);
-      else F4_LAUNCH(5, 1, 2);
-    } else {
-      if (sw) F4_LAUNCH(4, 1, 1);
-      else F4_LAUNCH(4, 1, 2);
-    }
-  } else if (sched_bits && two) F4_LAUNCH(5, 2, 0);
-  else if (sched_bits) F4_LAUNCH(5, 1, 0);
-  else if (two) F4_LAUNCH(4, 2, 0);
-  else F4_LAUNCH(4, 1, 0);
+  const bool two = flags & 4096, sw = flags & 1024;
+#define F4_LAUNCH(SC, TT_, SW_) \
+  DLT_HK_DISPATCH(hk, k_gemm_fw4<HKC, SC, TT_, SW_><<<grid, 256, 0, st>>>(A, B, C, M, N, K, lda, ldb, ldc, flags, S, ldS))
+  if (sw) {  // the gate/up projection: one tile per workgroup
+    if (sched_bits) F4_LAUNCH(5, 1, true);
+    else F4_LAUNCH(4, 1, true);
+  } else if (sched_bits && two) F4_LAUNCH(5, 2, false);
+  else if (sched_bits) F4_LAUNCH(5, 1, false);
+  else if (two) F4_LAUNCH(4, 2, false);
+  else F4_LAUNCH(4, 1, false);
 #undef F4_LAUNCH
   DLT_CHECK_LAUNCH();
 }

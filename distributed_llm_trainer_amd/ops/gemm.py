@@ -130,10 +130,10 @@ def load_plan(path: str, shipped: bool = False) -> None:
     for k, c in plan.get("fused", {}).items():
         if ":" in k:
             kind, dims = k.split(":", 1)
-            # "swiglu4" / "rope4": the 4-wave k_gemm_fw4 with the SwiGLU / RoPE epilogue, value =
-            # its launch flags (an int; false / null = not used); every other kind is a bool
+            # "swiglu4": the 4-wave k_gemm_fw4 with the SwiGLU epilogue, value = its launch flags
+            # (an int; false / null = not used); every other kind is a bool
             _PINNED["tn"][(kind, *(int(x) for x in dims.split("x")))] = (
-                (int(c) if c is not None and c is not False else None) if kind in ("swiglu4", "rope4") else bool(c))
+                (int(c) if c is not None and c is not False else None) if kind == "swiglu4" else bool(c))
     _PINNED["splitk"] = {_splitk_key(k): int(c) for k, c in plan.get("splitk", {}).items()}
     if _RACES:
         _RACES["tn"].update(_PINNED["tn"])
@@ -170,7 +170,7 @@ def export_plan() -> dict:
     return {"hipblaslt_version": int(lib().dlt_gemm_lib_version()),
             "hipblaslt": [hl[k] for k in sorted(hl)],
             "tn": {"x".join(map(str, k)): c for k, c in tn.items() if len(k) == 3},
-            "fused": {f"{k[0]}:" + "x".join(map(str, k[1:])): (c if k[0] in ("swiglu4", "rope4") else bool(c))
+            "fused": {f"{k[0]}:" + "x".join(map(str, k[1:])): (c if k[0] == "swiglu4" else bool(c))
                       for k, c in tn.items() if len(k) == 4},
             "splitk": {"x".join(map(str, k)): c for k, c in sk.items()}}
 
@@ -413,12 +413,6 @@ class HipGemm:
 
         def fused():
             hip.gemm_qkv_rope(x, w, S, cos, sin, out=y)
-        # the 4-wave k_gemm_fw4 with the RoPE epilogue: plan kind "rope4" (its launch flags)
-        # or DLT_GEMM_FW4_ROPE=<flags> (A/B knob)
-        fw4 = os.environ.get("DLT_GEMM_FW4_ROPE") or self._choice.get(("rope4", M, w.shape[0], x.shape[1]))
-        if fw4 is not None and w.shape[0] == 3 * nh * 64 and self._hand16_ok(x, w) and \
-                hip.gemm_fw4_rope(x, w, S, cos, sin, out=y, flags=int(fw4)) is not None:
-            return y
         ok = (w.shape[0] == 3 * nh * 64 and hip.gemm_bf16_fits192(M, w.shape[0], x.shape[1]) and M % S == 0
               and cos.dtype == torch.float32 and cos.is_contiguous() and sin.is_contiguous())
         if ok and self._fused_pick("rope", x, w, fused, unfused):
@@ -462,7 +456,7 @@ class HipGemm:
         out.update({f"{k[0]} M{k[1]}xN{k[2]}xK{k[3]}": (("hand-written gemm_dgrad" if c else "hipBLASLt")
                                                        if k[0].startswith("dgrad") else
                                                        (f"fused gemm_fw4 (flags {c})" if c is not None else "not used")
-                                                       if k[0] in ("swiglu4", "rope4") else
+                                                       if k[0] == "swiglu4" else
                                                        ("fused gemm_bf16" if c else "unfused (linear + kernel)"))
                     for k, c in self._choice.items() if len(k) == 4})
         out.update({f"wgrad{f' ({key[3]} out)' if len(key) == 4 else ''} M{key[0]}xN{key[1]}xK{key[2]}":

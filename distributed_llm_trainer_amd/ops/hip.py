@@ -65,7 +65,7 @@ _SIGS = {
     "dlt_gemm_bf16_tn": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                          c_void_p],
     "dlt_gemm_fw4": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
-                     c_int, c_void_p, c_void_p, c_int, c_int, c_void_p],
+                     c_int, c_void_p],
     "dlt_gemm_bf16_qkv_rope": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                                c_void_p],
     "dlt_gemm_bf16_gu_swiglu": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
@@ -915,8 +915,7 @@ def gemm_fw4(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = Non
     c = torch.empty(M, N, dtype=a.dtype, device=a.device) if out is None else out
     _req(c, a.dtype, "gemm_fw4.c", M * N)
     fl = _FW4_FLAGS if flags is None else flags
-    rc = lib().dlt_gemm_fw4(_p(a), _p(b), _p(c), M, N, K, K, K, N, fl & ~(1024 | 8192), hk, None, 0, None, None, 0, 0,
-                            _stream())
+    rc = lib().dlt_gemm_fw4(_p(a), _p(b), _p(c), M, N, K, K, K, N, fl & ~1024, hk, None, 0, _stream())
     if rc == -1:
         return None  # a launch variant the shape does not take (two tiles per workgroup: tiles % 16)
     _chk(rc, "gemm_fw4")
@@ -947,32 +946,9 @@ def gemm_fw4_swiglu(x: torch.Tensor, wgu: torch.Tensor, gu_out: Optional[torch.T
     fl = (_FW4_FLAGS if flags is None else flags) & ~(16 | 128)
     if flags is not None and (flags & (16 | 128)) == (16 | 128):
         fl |= 16 | 128  # SCHED 5
-    _chk(lib().dlt_gemm_fw4(_p(x), _p(wgu), _p(gu), M, I2, K, K, K, I2, (fl | 1024) & ~(4096 | 8192), hk, _p(s), I,
-                            None, None, 0, 0, _stream()), "gemm_fw4_swiglu")
+    _chk(lib().dlt_gemm_fw4(_p(x), _p(wgu), _p(gu), M, I2, K, K, K, I2, (fl | 1024) & ~4096, hk, _p(s), I, _stream()),
+         "gemm_fw4_swiglu")
     return gu, s
-
-
-def gemm_fw4_rope(x: torch.Tensor, wqkv: torch.Tensor, S: int, cos: torch.Tensor, sin: torch.Tensor,
-                  out: Optional[torch.Tensor] = None, flags: Optional[int] = None) -> Optional[torch.Tensor]:
-    """qkv[M, 3H] = x @ Wqkv^T with NeoX RoPE on the q and k heads (head_dim 64, position of
-    row m = m % S) in the epilogue of the 4-wave k_gemm_fw4 (csrc/gemm_fw4.hip, flags 8192;
-    k_rope_qk_inplace's arithmetic on the bf16-rounded outputs, same bits).  cos / sin:
-    [>= S, 32] fp32.  None if the shape does not tile (2H % 128, M % 256, K % 64, M % S)."""
-    M, K = x.shape
-    N = wqkv.shape[0]
-    H = N // 3
-    if (not gemm_fw4_fits(M, N, K) or N % 3 or H % 64 or (2 * H) % 128 or wqkv.shape[1] != K or M % S
-            or cos.dtype != torch.float32 or sin.dtype != torch.float32 or cos.shape[-1] != 32 or cos.shape[0] < S
-            or not cos.is_contiguous() or not sin.is_contiguous()):
-        return None
-    hk = _req_act(x, x.dtype, "gemm_fw4_rope.x")
-    _req(wqkv, x.dtype, "gemm_fw4_rope.w")
-    c = torch.empty(M, N, dtype=x.dtype, device=x.device) if out is None else out
-    _req(c, x.dtype, "gemm_fw4_rope.out", M * N)
-    fl = (_FW4_FLAGS if flags is None else flags) & ~(1024 | 4096)
-    _chk(lib().dlt_gemm_fw4(_p(x), _p(wqkv), _p(c), M, N, K, K, K, N, fl | 8192, hk, None, 0, _p(cos), _p(sin), S,
-                            2 * H, _stream()), "gemm_fw4_rope")
-    return c
 
 
 def gemm_qkv_rope(x: torch.Tensor, wqkv: torch.Tensor, S: int, cos: torch.Tensor, sin: torch.Tensor,

@@ -627,23 +627,6 @@ def test_gemm_fw4_swiglu(M, I, K, dtype):
     assert hip.gemm_fw4_swiglu(x, w[:2 * I - 128].contiguous()) is None or I % 128 == 64
 
 
-@pytest.mark.parametrize("B,S,nh,K", [(16, 1024, 12, 768), (2, 384, 4, 128), (1, 256, 8, 192)])
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-def test_gemm_fw4_rope(B, S, nh, K, dtype):
-    """k_gemm_fw4 with the RoPE epilogue (csrc/gemm_fw4.hip flags 8192): bitwise equal to
-    the plain k_gemm_fw4 GEMM followed by rope_qk_inplace (q / k heads rotated, v kept)."""
-    torch.manual_seed(B * S + nh)
-    M, N = B * S, 3 * nh * 64
-    x = (torch.rand(M, K, device=DEV) * 2 - 1).to(dtype)
-    w = (torch.rand(N, K, device=DEV) * 2 - 1).to(dtype)
-    cos, sin = hip.rope_tables(64, S, device=DEV)
-    for flags in (0, 4, 144, 148, 2):
-        got = hip.gemm_fw4_rope(x, w, S, cos, sin, flags=flags)
-        want = hip.gemm_fw4(x, w, flags=flags)
-        hip.rope_qk_inplace(want, B, S, nh, cos, sin)
-        assert torch.equal(got, want), f"fused RoPE differs from GEMM + rope_qk_inplace (flags {flags})"
-
-
 @pytest.fixture(params=[0, 4096], ids=["stage-in-loop", "epilogue-first"])
 def gemm_late_flag(request, monkeypatch):
     """Runs a test with and without flags bit 4096 (epilogue-first staging of the next
