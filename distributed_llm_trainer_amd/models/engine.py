@@ -264,13 +264,6 @@ class GPTEngine:
             self.ac_budget = torch.cuda.get_device_properties(torch.cuda.current_device()).total_memory / 3.0
         else:
             self.ac_budget = 48e9
-        # data gradients in "TN" form on the 4-wave k_gemm_fw4 (DLT_GEMM_DGRAD4=<flags>, or the
-        # gemm plan's "dgrad4" picks): dX = dY . W needs W^T [in, out] K-contiguous, so each
-        # projection weight is transposed once per optimizer step, right after its unit's
-        # (lazy) update in the step's first forward; the backward waits on that copy's event
-        self._wt = {}        # (layer | "head", name) -> (epoch, W^T, event)
-        self._wt_epoch = 0   # bumped at every accumulation-window start (weights change only between)
-        self._wt_on = False  # set by the trainer / knob: only for providers with stable weights
         # attention keep-bit masks (1 bit per causal score, two layouts) are kept from the
         # forward for the backward while one micro-step's masks of all layers fit in this
         # budget; beyond it (long context: 3.2 GB per layer at S = 32768, nh 12) the
@@ -300,8 +293,6 @@ class GPTEngine:
         tools/wgrad_m_test.py).  Memory: ~250 MB per layer per micro-step (small).
         """
         self.acc_slot, self.acc_slots = int(slot), int(n_slots)
-        if self.acc_slot == 0:
-            self._wt_epoch += 1
         # A one-micro-step window defers too (DLT_DEFER_GA1=0: inline wgrads): the slot
         # buffers then let the weight-gradient GEMMs run on the side stream, overlapped
         # with the next layer's dgrad chain (attention/norm/SwiGLU backward).
@@ -394,34 +385,6 @@ class GPTEngine:
         self.gemm.wgrad_acc(acc, dl, nfs)
 
     # ---------------------------------------------------------------- helpers
-    def _wt_refresh(self, unit, named) -> None:
-        """Transposed copies W^T of a unit's projection weights for the "TN" data gradients,
-        made once per accumulation window on the stream that runs the unit's first forward
-        (after the provider's pre_forward applied a pending optimizer update)."""
-        for name, w in named:
-            key = (unit, name)
-            ent = self._wt.get(key)
-            if ent is not None and ent[0] == self._wt_epoch:
-                continue
-            buf = ent[1] if ent is not None and tuple(ent[1].shape) == (w.shape[1], w.shape[0]) else \
-                torch.empty(w.shape[1], w.shape[0], dtype=w.dtype, device=w.device)
-            if ent is not None and ent[2] is not None:
-                torch.cuda.current_stream().wait_event(ent[2])  # the previous window's readers are done
-            buf.copy_(w.t())
-            ev = torch.cuda.Event() if buf.is_cuda else None
-            if ev is not None:
-                ev.record()
-            self._wt[key] = (self._wt_epoch, buf, ev)
-
-    def _wt_get(self, unit, name):
-        """W^T for the data gradient (None when the TN form is off or not made this window)."""
-        ent = self._wt.get((unit, name)) if self._wt_on else None
-        if ent is None or ent[0] != self._wt_epoch:
-            return None
-        if ent[2] is not None:
-            torch.cuda.current_stream().wait_event(ent[2])
-        return ent[1]
-
     def rope(self, S: int, device):
         key = (S, str(device))
         if key not in self._rope:
@@ -636,15 +599,10 @@ class GPTEngine:
 
         prov.pre_forward("head")
         hw = prov.head()
-        if need_bwd and self._wt_on:
-            self._wt_refresh("head", (("lm_head", hw.lm_head),))
         r = self.ops.embedding_fwd(ids, hw.embed)
         d, key_d, p_d = None, 0, 0.0
         for i in range(self.cfg.num_layers):
             prov.pre_forward(i)
-            if need_bwd and self._wt_on:
-                w_i = prov.layer(i)
-                self._wt_refresh(i, (("wqkv", w_i.wqkv), ("wo", w_i.wo), ("wgu", w_i.wgu)))
             save = need_bwd and not recompute
             r_new, d_new, c = self._layer_forward(st, i, r, d, key_d, p_d, save)
             if need_bwd:
@@ -893,7 +851,7 @@ class GPTEngine:
             del nfs
         else:
             # lm_head: dnf = dlogits @ E ; dE += dlogits^T @ (nf * dloss)
-            dnf = gm.linear_dgrad(st.dlogits, hw.lm_head, wt=self._wt_get("head", "lm_head"))
+            dnf = gm.linear_dgrad(st.dlogits, hw.lm_head)
             nf_out = self._sb(st, "head", "nf", M, H, dev)
             if prev is None and mine is not None and _TEST_DELAY_FIRST_BWD:
                 # race test hook (DLT_TEST_DELAY_FIRST_BWD=cycles): the first overlapped backward
@@ -1023,12 +981,12 @@ class GPTEngine:
                 ds = gm.linear_dgrad(g_d, w.wdown)
                 dgu = ops.swiglu_bwd(c.gu, ds, out=sb(i, "dgu", 2 * I), **s_kw)
                 del ds
-            dn2 = gm.linear_dgrad(dgu, w.wgu, wt=self._wt_get(i, "wgu"))
+            dn2 = gm.linear_dgrad(dgu, w.wgu)
             dx2, da = ops.rmsnorm_bwd(dn2, c.x2, c.rstd2, w.ln2, g_x2, gr.ln2, ph, k_resid,
                                       ddelta_out=sb(i, "da", H))
             del dn2
             # attention
-            do = gm.linear_dgrad(da, w.wo, wt=self._wt_get(i, "wo"))
+            do = gm.linear_dgrad(da, w.wo)
             if c.k is None:  # packed: dq/dk/dv land in [M, 3H] with the inverse RoPE applied
                 dqkv = ops.attention_bwd_packed(c.q, c.o, do, c.lse, pa, k_attn, B, S, cfg.num_heads, cos, sin,
                                                 out=sb(i, "dqkv", 3 * H))
@@ -1038,7 +996,7 @@ class GPTEngine:
                 del do
                 dqkv = ops.rope_qkv_bwd(dq, dk, dv, cos, sin, out=sb(i, "dqkv", 3 * H))
                 del dq, dk, dv
-            dn1 = gm.linear_dgrad(dqkv, w.wqkv, wt=self._wt_get(i, "wqkv"))
+            dn1 = gm.linear_dgrad(dqkv, w.wqkv)
             key_prev = self._keys(st.micro, i - 1)[2] if i > 0 else 0
             p_prev = ph if i > 0 else 0.0
             g_x2n, g_dn = ops.rmsnorm_bwd(dn1, c.x, c.rstd1, w.ln1, dx2, gr.ln1, p_prev, key_prev,
@@ -1461,7 +1419,7 @@ class _TorchGemm:
         return torch.matmul(x, w.t())
 
     @staticmethod
-    def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None, wt=None) -> torch.Tensor:
+    def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
         if out is not None:
             return torch.matmul(dy, w, out=out)
         return torch.matmul(dy, w)

@@ -130,11 +130,10 @@ def load_plan(path: str, shipped: bool = False) -> None:
     for k, c in plan.get("fused", {}).items():
         if ":" in k:
             kind, dims = k.split(":", 1)
-            # "swiglu4" / "dgrad4": the 4-wave k_gemm_fw4 with the SwiGLU epilogue / on the
-            # transposed weight (data gradients), value = its launch flags (an int; false / null
-            # = not used); every other kind is a bool
+            # "swiglu4": the 4-wave k_gemm_fw4 with the SwiGLU epilogue, value = its launch flags
+            # (an int; false / null = not used); every other kind is a bool
             _PINNED["tn"][(kind, *(int(x) for x in dims.split("x")))] = (
-                (int(c) if c is not None and c is not False else None) if kind in ("swiglu4", "dgrad4") else bool(c))
+                (int(c) if c is not None and c is not False else None) if kind == "swiglu4" else bool(c))
     _PINNED["splitk"] = {_splitk_key(k): int(c) for k, c in plan.get("splitk", {}).items()}
     if _RACES:
         _RACES["tn"].update(_PINNED["tn"])
@@ -171,7 +170,7 @@ def export_plan() -> dict:
     return {"hipblaslt_version": int(lib().dlt_gemm_lib_version()),
             "hipblaslt": [hl[k] for k in sorted(hl)],
             "tn": {"x".join(map(str, k)): c for k, c in tn.items() if len(k) == 3},
-            "fused": {f"{k[0]}:" + "x".join(map(str, k[1:])): (c if k[0] in ("swiglu4", "dgrad4") else bool(c))
+            "fused": {f"{k[0]}:" + "x".join(map(str, k[1:])): (c if k[0] == "swiglu4" else bool(c))
                       for k, c in tn.items() if len(k) == 4},
             "splitk": {"x".join(map(str, k)): c for k, c in sk.items()}}
 
@@ -457,7 +456,7 @@ class HipGemm:
         out.update({f"{k[0]} M{k[1]}xN{k[2]}xK{k[3]}": (("hand-written gemm_dgrad" if c else "hipBLASLt")
                                                        if k[0].startswith("dgrad") else
                                                        (f"fused gemm_fw4 (flags {c})" if c is not None else "not used")
-                                                       if k[0] in ("swiglu4", "dgrad4") else
+                                                       if k[0] == "swiglu4" else
                                                        ("fused gemm_bf16" if c else "unfused (linear + kernel)"))
                     for k, c in self._choice.items() if len(k) == 4})
         out.update({f"wgrad{f' ({key[3]} out)' if len(key) == 4 else ''} M{key[0]}xN{key[1]}xK{key[2]}":
@@ -472,27 +471,14 @@ class HipGemm:
         K = w.shape[1]
         _gemm(0, 0, K, M, N, w, _rowmajor(w), dy, _rowmajor(dy), dx, K)
 
-    def wants_weight_t(self) -> bool:
-        """Whether some data gradient runs in the "TN" form (plan kind "dgrad4" or
-        DLT_GEMM_DGRAD4): the engine then keeps transposed weight copies (GPTEngine._wt)."""
-        return bool(os.environ.get("DLT_GEMM_DGRAD4")) or any(
-            len(k) == 4 and k[0] == "dgrad4" and c is not None for k, c in self._choice.items())
-
-    def linear_dgrad(self, dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None,
-                     wt: torch.Tensor = None) -> torch.Tensor:
+    def linear_dgrad(self, dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
         """dX[M, K] = dY[M, N] @ W[N, K]: the hand-written reduction-major-B kernel
         (``hip.gemm_dgrad``, W read as stored) or hipBLASLt, raced once per shape (kind
-        "dgrad" in the plan's "fused" table; ``DLT_GEMM_DGRAD=0``: library only).  With the
-        engine's transposed copy ``wt`` = W^T [K, N] and a "dgrad4" pick (its k_gemm_fw4
-        launch flags; ``DLT_GEMM_DGRAD4=<flags>``): the "TN" form dY . (W^T)^T on k_gemm_fw4."""
+        "dgrad" in the plan's "fused" table; ``DLT_GEMM_DGRAD=0``: library only)."""
         from . import hip
         M, N = dy.shape
         K = w.shape[1]
         dx = torch.empty(M, K, dtype=dy.dtype, device=dy.device) if out is None else out
-        if wt is not None:
-            fw4 = os.environ.get("DLT_GEMM_DGRAD4") or self._choice.get(("dgrad4", M, K, N))
-            if fw4 is not None and self._hand16_ok(dy, wt, dx) and hip.gemm_fw4(dy, wt, out=dx, flags=int(fw4)) is not None:
-                return dx
         ok = self._dgrad_on and self._race and hip.gemm_bf16_fits(M, K, N) and self._hand16_ok(dy, w, dx)
         # bf16 and fp16 race separately (kind "dgrad" / "dgrad16"): one format's pick must
         # not decide the other's

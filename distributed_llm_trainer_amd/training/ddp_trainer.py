@@ -120,9 +120,6 @@ class DistributedTrainer:
                     self.training_config.defer_roles = LEAN_DEFER_ROLES
                 eng.s_refill = True
             eng.defer_roles = parse_defer_roles(self.training_config.defer_roles)
-            # "TN" data gradients on transposed weight copies (plan kind "dgrad4"): the flat
-            # store's weights change only between accumulation windows, which the trainer marks
-            eng._wt_on = bool(getattr(eng.gemm, "wants_weight_t", lambda: False)())
             if "head" not in eng.defer_roles and not eng.head_chunks_env:
                 eng.head_chunks = 2  # memory-lean: chunked lm_head run in the forwards (GPTEngine)
             self.store = self.model.store
