@@ -322,18 +322,6 @@ __global__ __launch_bounds__(256, 1) void k_gemm_fw4(const bf16_t* __restrict__ 
     // 16 wait states for the last MFMAs' accumulators
     asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
     const bool more = j + 1 < T;
-    // flags 8192 (two tiles): the next tile's stages 0 and 1 issued BEFORE this tile's
-    // epilogue (its loads then fly under the stores instead of behind them)
-    const bool early = more && (flags & 8192);
-    auto prefetch_next = [&]() {
-      setup(j + 1, nxt);
-      asm volatile("s_barrier" ::: "memory");  // every wave is done with this tile's slots
-#pragma unroll
-      for (int st = 0; st < 2; ++st)
-#pragma unroll
-        for (int p = 0; p < 16; ++p) piece(nxt, st, g0 + ns + st, p);
-    };
-    if (early) prefetch_next();
 
     // epilogue (product D = A_tile . B_tile^T): lane l, register r of tile (u, t) is output
     // row 16 t + 4 (l >> 4) + r, column wn*128 + 8 (l & 15) + u (n-tile u holds columns
@@ -404,7 +392,12 @@ __global__ __launch_bounds__(256, 1) void k_gemm_fw4(const bf16_t* __restrict__ 
       // the next tile's stages 0 and 1 (global stages g0 + ns, + 1), issued right behind this
       // tile's stores so their latency overlaps the store drain and the next tile's setup
       // (every wave is done with this tile's slots after the barrier)
-      if (!early) prefetch_next();
+      setup(j + 1, nxt);
+      asm volatile("s_barrier" ::: "memory");
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int p = 0; p < 16; ++p) piece(nxt, st, g0 + ns + st, p);
       cur = nxt;
       g0 += ns;
     }
@@ -413,8 +406,7 @@ __global__ __launch_bounds__(256, 1) void k_gemm_fw4(const bf16_t* __restrict__ 
 
 // flags: 1 = write-through (sc1) C stores, 4 = nt C stores; tile order 2 = row-major, 2048 = half-height
 // XCD bands (default XCD row bands); schedule 16 | 128 = SCHED 5 (else SCHED 4); 1024 = SwiGLU epilogue;
-// 4096 = two tiles per workgroup (the second tile's first stages prefetched behind the first's epilogue;
-// with 8192 ahead of it)
+// 4096 = two tiles per workgroup (the second tile's first stages prefetched behind the first's epilogue)
 DLT_API int dlt_gemm_fw4(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K, int lda, int ldb, int ldc,
                          int flags, int hk, bf16_t* S, int ldS, hipStream_t st) {
   if (M <= 0 || N <= 0 || K <= 0 || M % F4_BM || N % 128 || K % F4_BK || K < 2 * F4_BK || lda % 8 || ldb % 8 ||

@@ -60,9 +60,7 @@ def main():
                           ("fw4x2", lambda: hip.gemm_fw4(a, b, out=y, flags=4 | 4096)),
                           ("fw4s5x2", lambda: hip.gemm_fw4(a, b, out=y, flags=148 | 4096)),
                           ("fw4hx2", lambda: hip.gemm_fw4(a, b, out=y, flags=148 | 2048 | 4096)),
-                          ("fw4px2", lambda: hip.gemm_fw4(a, b, out=y, flags=144 | 4096)),
-                          ("fw4x2e", lambda: hip.gemm_fw4(a, b, out=y, flags=4 | 4096 | 8192)),
-                          ("fw4s5x2e", lambda: hip.gemm_fw4(a, b, out=y, flags=148 | 4096 | 8192))):
+                          ("fw4px2", lambda: hip.gemm_fw4(a, b, out=y, flags=144 | 4096))):
             if label not in impls:
                 continue
             if fn is None:
@@ -73,8 +71,7 @@ def main():
         ref = (a.float() @ b.float().t())
         errs = []
         for label, fn in (("fw4", hip.gemm_fw4),
-                          ("fw4x2", lambda a, b, out: hip.gemm_fw4(a, b, out=out, flags=4 | 4096)),
-                          ("fw4x2e", lambda a, b, out: hip.gemm_fw4(a, b, out=out, flags=4 | 4096 | 8192))):
+                          ("fw4x2", lambda a, b, out: hip.gemm_fw4(a, b, out=out, flags=4 | 4096))):
             if label not in impls:
                 continue
             y.fill_(float("nan"))
