@@ -118,10 +118,13 @@ class DistributedTrainer:
                 if self.training_config.defer_roles == "all":
                     # memory-first defers no weight gradient unless the config names roles
                     self.training_config.defer_roles = LEAN_DEFER_ROLES
-                eng.s_refill = True
+                eng.s_refill = os.environ.get("DLT_S_REFILL", "1") != "0"
             eng.defer_roles = parse_defer_roles(self.training_config.defer_roles)
             if "head" not in eng.defer_roles and not eng.head_chunks_env:
-                eng.head_chunks = 2  # memory-lean: chunked lm_head run in the forwards (GPTEngine)
+                # memory-lean: chunked lm_head run in the forwards (GPTEngine); memory-first
+                # (unfused 8192-row micro-steps) takes each micro-step's rows in one chunk:
+                # +0.4 GB, +3 % (tools/ab/r6/memfirst_ab.sh)
+                eng.head_chunks = 1 if self.training_config.memory_first else 2
             self.store = self.model.store
         else:
             self.store = FlatParamStore(self.model, self.device, compute_dtype=torch.float32)

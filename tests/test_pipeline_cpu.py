@@ -506,6 +506,10 @@ def test_memory_first_matches_memory_lean():
                             defer_roles=LEAN_DEFER_ROLES, micro_step_fusion=1, memory_first=first)
         tr = DistributedTrainer(tiny(), tc)
         assert tr.model.engine.s_refill == first
+        # memory-first takes a micro-step's head rows in one chunk, lean in two: same chunking
+        # here, so the only difference left is the SwiGLU output's refill
+        assert tr.model.engine.head_chunks == (1 if first else 2)
+        tr.model.engine.head_chunks = 1
         losses = [tr.train_step({"input_ids": d})["loss"] for d in data]
         res.append((losses, tr.flat_params().clone()))
     assert res[0][0] == res[1][0]

@@ -81,7 +81,7 @@ def main():
 
 
 DGRAD = {"dqkv": (16384, 768, 2304), "do": (16384, 768, 768), "dgu": (16384, 768, 6144),
-         "dlm": (8192, 768, 50304), "ddown": (16384, 3072, 768)}
+         "dlm": (8192, 768, 50304), "dlm16": (16384, 768, 50304), "ddown": (16384, 3072, 768)}
 
 
 def dgrad(args):
