@@ -782,7 +782,7 @@ def test_planner_fused_races_match_unfused():
     from distributed_llm_trainer_amd.ops import gemm
     torch.manual_seed(4)
     g = gemm.HipGemm()
-    B, S, nh, K, I = 8, 1024, 12, 768, 3072
+    B, S, nh, K, I = 4, 1024, 12, 768, 3072  # M = 4096: no shipped pin (the 8192-row shapes are pinned)
     M = B * S
     x = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
     wqkv = ((torch.rand(3 * nh * 64, K, device=DEV) * 2 - 1) / K ** 0.5).bfloat16()
