@@ -65,7 +65,11 @@ class DDPRuntime:
         # row-sparse embedding reductions in flight: (work, rows, index, a, b, H)
         self.row_handles: List[Tuple[object, torch.Tensor, torch.Tensor, int, int, int]] = []
         self.split_head = os.environ.get("DLT_DDP_SPLIT_HEAD", "1") != "0"
-        self.sparse_rows_max = float(os.environ.get("DLT_DDP_SPARSE_ROWS", "0.5"))  # union share for sparse
+        # row-sparse embedding part (opt-in): reduce only the union of non-zero rows when it
+        # is at most this share of the rows.  Finding the union costs a host sync on its row
+        # count at the end of every backward: -1 % on a forced-RCCL rank with synthetic
+        # tokens (union = every row, dense anyway; tools/ab/r6/rccl_knobs.sh), so 0 = dense.
+        self.sparse_rows_max = float(os.environ.get("DLT_DDP_SPARSE_ROWS", "0"))
         self.last_head = None  # how the last embedding bucket was reduced: "dense" / ("rows", U, Vp)
         lay = store.layout
         elem = store.grad.element_size()
@@ -160,6 +164,10 @@ class DDPRuntime:
         """All-reduce the rows of grad[a:b] (a [rows, H] matrix) that are non-zero on any
         rank; rows zero on every rank stay zero (their sum).  One byte per row is MAX-
         reduced first so every rank gathers the same rows (a host sync on the row count)."""
+        if self.sparse_rows_max <= 0:  # dense (default): no union, no host sync
+            self.last_head = "dense"
+            self._launch(a, b)
+            return
         g = self.store.grad[a:b].view(-1, H)
         touched = (g != 0).any(dim=1).to(torch.uint8)
         dist.all_reduce(touched, op=dist.ReduceOp.MAX, group=self.pg)

@@ -415,10 +415,12 @@ def test_fsdp_limit_all_gathers_bounds_prefetch():
         assert len(issued) == want, (limit, issued)
 
 
-def _count_worker(rank, world, mode, strategy="FULL_SHARD"):
+def _count_worker(rank, world, mode, strategy="FULL_SHARD", sparse_rows=None):
     """One warm step, then the collectives of one optimizer step (GA = 2 micro-steps),
     counted by wrapping torch.distributed: [(name, numel, element size)]."""
     import torch.distributed as dist
+    if sparse_rows is not None:
+        os.environ["DLT_DDP_SPARSE_ROWS"] = str(sparse_rows)
     from distributed_llm_trainer_amd.models.config import GPTConfig
     cfg = GPTConfig(**TINY)
     if mode == "ddp":
@@ -462,15 +464,18 @@ def _count_worker(rank, world, mode, strategy="FULL_SHARD"):
     return log, units, cfg.num_layers
 
 
-def test_ddp_collective_pattern_per_step():
+@pytest.mark.parametrize("sparse", [False, True])
+def test_ddp_collective_pattern_per_step(sparse):
     """SURVEY §2.4 X3/X4 on 2 gloo ranks: one optimizer step (2 micro-steps) issues its
     gradient all-reduces only in the last micro-step (no_sync): one fp32 all-reduce per
     layer bucket, the lm_head part of the tied gradient ([Vp, H], handed over by the engine
-    at the start of the last backward), the embedding part row-sparse (one byte per row
-    MAX-reduced, then only the union of non-zero rows -- or dense when the union exceeds
-    half the rows), the norm weights, plus the logged global loss (one scalar).  No
-    per-step buffer broadcast (X3 is dropped by design)."""
-    for log, d, _ in run_multiprocess(_count_worker, world=2, args=("ddp",)):
+    at the start of the last backward), the embedding part -- dense by default, row-sparse
+    with DLT_DDP_SPARSE_ROWS (one byte per row MAX-reduced, then only the union of non-zero
+    rows, or dense when the union exceeds that share of the rows) -- the norm weights, plus
+    the logged global loss (one scalar).  No per-step buffer broadcast (X3 is dropped by
+    design)."""
+    for log, d, _ in run_multiprocess(_count_worker, world=2,
+                                      args=("ddp", "FULL_SHARD", 0.5 if sparse else None)):
         ar = [x for x in log if x[0] == "all_reduce"]
         assert len(log) == len(ar), log  # no broadcast / gather / reduce-scatter per step
         H, Vp = d["H"], d["Vp"]
@@ -479,8 +484,11 @@ def test_ddp_collective_pattern_per_step():
         # layer buckets first, in backward order, fp32, covering the layer region once
         assert sum(x[1] for x in ar if x[1] in layer and x[2] == 4) >= d["embed"]
         assert Vp * H in sizes  # the lm_head part (or a dense embedding part too)
-        assert [x for x in ar if x[2] == 1] == [("all_reduce", Vp, 1)]  # the union bitmap
+        # the union bitmap (row-sparse mode only)
+        assert [x for x in ar if x[2] == 1] == ([("all_reduce", Vp, 1)] if sparse else [])
         head = d["head"]
+        if not sparse:
+            assert head == "dense"
         assert head == "dense" or (head[0] == "rows" and 0 < head[1] <= Vp // 2 and head[2] == Vp), head
         if head != "dense":
             assert head[1] * H in sizes
