@@ -4,7 +4,7 @@ synthetic token sequences for N steps.  A correct forward/backward/optimizer mem
 it, so the loss must fall far below ln(V) = 10.8; the eager autocast model is trained on
 the same data in the same way for comparison (parity of the loss curve).
 
-usage: python tools/converge.py --steps 150 [--eager] [--precision bf16|fp16|fp32]
+usage: python tools/converge.py --steps 150 [--eager] [--precision bf16|fp16|fp32] [--memory_first]
 
 ``--precision`` trains the engine in another activation precision on the same data and
 init (fp16: dynamic loss scaling; fp32: the fp32 kernels and GEMM-formulated attention),
@@ -28,13 +28,14 @@ def main():
     ap.add_argument("--log", type=int, default=10)
     ap.add_argument("--seed", type=int, default=1234, help="trainer seed (model init + dropout streams)")
     ap.add_argument("--precision", default="bf16", choices=("bf16", "fp16", "fp32"))
+    ap.add_argument("--memory_first", action="store_true", help="TrainingConfig.memory_first (the <= 8.2 GB mode)")
     a = ap.parse_args()
     from distributed_llm_trainer_amd.models.config import GPTConfig
     from distributed_llm_trainer_amd.training.configs import TrainingConfig
     from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
     cfg = GPTConfig.gpt2_small()
     tc = TrainingConfig(batch_size=8, gradient_accumulation_steps=4, max_steps=a.steps, warmup_steps=20,
-                        learning_rate=a.lr, mixed_precision=a.precision, seed=a.seed)
+                        learning_rate=a.lr, mixed_precision=a.precision, seed=a.seed, memory_first=a.memory_first)
     tr = DistributedTrainer(cfg, tc, use_engine=not a.eager)
     if a.eager:  # the reference path: torch modules under bf16 autocast
         tr.autocast_ctx = torch.autocast(device_type="cuda", dtype=torch.bfloat16)
@@ -48,7 +49,8 @@ def main():
         if step % a.log == 0 or step == a.steps - 1:
             out.append({"step": step, "loss": float(loss)})
             print(json.dumps(out[-1]), flush=True)
-    print(json.dumps({"path": "eager" if a.eager else "engine", "precision": a.precision, "seed": a.seed, "seconds": round(time.time() - t0, 1),
+    print(json.dumps({"path": "eager" if a.eager else "engine", "precision": a.precision, "seed": a.seed,
+                      "memory_first": a.memory_first, "seconds": round(time.time() - t0, 1),
                       "first": out[0]["loss"], "last": out[-1]["loss"]}), flush=True)
 
 
