@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build ops/_dlt_kernels_base.so from the kernel sources of git revision $1 (default HEAD)
-# for tools/ab/ab_kernels.sh (extra hipcc flags, e.g. a diagnostic -D, in DLT_BASE_CFLAGS).  Runs on the CPU container (hipcc cross-compiles gfx950).
+# for tools/ab/kernels_ab.sh (extra hipcc flags, e.g. a diagnostic -D, in DLT_BASE_CFLAGS).  Runs on the CPU container (hipcc cross-compiles gfx950).
 set -eu
 rev=${1:-HEAD}
 mkdir -p .scratch && tmp=$(mktemp -d -p "$PWD/.scratch")

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Same-box A/B of a kernel change: bench.py with ops/_dlt_kernels_base.so (built from
 # another revision by tools/ab/build_base_lib.sh) against the current ops/_dlt_kernels.so,
-# alternating.  usage: bash tools/ab/ab_kernels.sh [rounds] [bench args...]
+# alternating.  usage: bash tools/ab/kernels_ab.sh [rounds] [bench args...]
 set -u
 mkdir -p gpurun_out
 R=${1:-2}; shift || true
