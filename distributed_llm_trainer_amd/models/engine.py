@@ -194,6 +194,7 @@ class GPTEngine:
         # which weight gradients a deferred window defers (the others run per micro-step):
         # all by default; the memory-lean mode defers none (per-chain weight gradients)
         self.defer_roles = frozenset(self.ROLES)
+        self.defer_layers = int(os.environ.get("DLT_DEFER_LAYERS", "0"))  # see _deferred
         self._slots = {}
         # dY-operand slot ring (ffbb window, see _window_ffbb): 0 = one slot per layer
         self._ring = 0
@@ -303,15 +304,21 @@ class GPTEngine:
                   "lg": "head", "nf": "head"}
     ROLES = ("qkv", "o", "gu", "down", "head")
 
-    def _deferred(self, st, role: str) -> bool:
+    def _deferred(self, st, role: str, layer=None) -> bool:
         if role == "head" and self.head_chunks > 0:
             return False  # the chunked head computes its weight gradient per micro-step
-        return st.defer and role in self.defer_roles
+        d = st.defer and role in self.defer_roles
+        # defer_layers > 0: only layers below it defer their roles (a memory / speed dial
+        # between "none" and a whole role, e.g. --memory_first --defer_roles o); the
+        # ffbb dY ring assumes whole roles, so it ignores the dial
+        if d and layer is not None and 0 < self.defer_layers <= layer and not self._ring:
+            return False
+        return d
 
     def _sb(self, st, layer, name: str, M: int, N: int, device):
         """The micro-step's slice of a slot buffer when ``name``'s weight gradient is
         deferred, else None (the producing kernel allocates as usual)."""
-        if not self._deferred(st, self._SLOT_ROLE[name]):
+        if not self._deferred(st, self._SLOT_ROLE[name], layer):
             return None
         return self._slot_buf(st, layer, name, M, N, device)[0]
 
@@ -1014,6 +1021,7 @@ class GPTEngine:
             # concurrently with the next layer's dgrad chain (the small-output
             # wgrads leave most CUs idle); the layer's gradient hook (DDP
             # bucket all-reduce) is issued from the same stream.
+            dfl = {r: self._deferred(st, r, i) for r in self.ROLES}  # this layer's deferred roles
             if win:
                 if side is not None and i >= n_main:
                     ev = torch.cuda.Event()
@@ -1021,28 +1029,28 @@ class GPTEngine:
                     side.wait_event(ev)
                     side_ctx = torch.cuda.stream(side)
                     side_ctx.__enter__()
-                if dfr["down"]:
+                if dfl["down"]:
                     _wgrad(gm, gr.wdown, full(i, "dd", H), full(i, "s", I))
-                if dfr["gu"]:
+                if dfl["gu"]:
                     _wgrad(gm, gr.wgu, full(i, "dgu", 2 * I), full(i, "n2", H))
-                if dfr["o"]:
+                if dfl["o"]:
                     _wgrad(gm, gr.wo, full(i, "da", H), full(i, "o", H))
-                if dfr["qkv"]:
+                if dfl["qkv"]:
                     _wgrad(gm, gr.wqkv, full(i, "dqkv", 3 * H), full(i, "n1", H))
                 if self._ring:
                     ev = torch.cuda.Event()
                     ev.record()
                     self._ring_done[i] = ev
-            if not all(dfr.values()):  # the per-micro-step ones, on this backward's stream
+            if not all(dfl.values()):  # the per-micro-step ones, on this backward's stream
                 if side_ctx is not None:
                     side_ctx.__exit__(None, None, None)
-                if not dfr["down"]:
+                if not dfl["down"]:
                     _wgrad(gm, gr.wdown, g_d, c.s if s_new is None else s_new)
-                if not dfr["gu"]:
+                if not dfl["gu"]:
                     _wgrad(gm, gr.wgu, dgu, c.n2)
-                if not dfr["o"]:
+                if not dfl["o"]:
                     _wgrad(gm, gr.wo, da, c.o)
-                if not dfr["qkv"]:
+                if not dfl["qkv"]:
                     _wgrad(gm, gr.wqkv, dqkv, c.n1)
                 if side_ctx is not None:
                     # the gradient hook goes out from the side stream, after both halves

@@ -514,3 +514,25 @@ def test_memory_first_matches_memory_lean():
         res.append((losses, tr.flat_params().clone()))
     assert res[0][0] == res[1][0]
     assert torch.equal(res[0][1], res[1][1])
+
+
+def test_partial_layer_deferral_matches_inline():
+    """GPTEngine.defer_layers (DLT_DEFER_LAYERS): only layers below it defer their roles'
+    weight gradients to the window.  --memory_first --defer_roles o with the o weight
+    gradient deferred for layer 0 only: same losses, and weights within summation-order
+    noise of deferring it for every layer and of deferring nothing."""
+    from distributed_llm_trainer_amd.training.configs import TrainingConfig
+    from distributed_llm_trainer_amd.training.ddp_trainer import DistributedTrainer
+    torch.manual_seed(23)
+    data = [torch.randint(0, 256, (8, 32)) for _ in range(3)]
+    res = {}
+    for name, roles, layers in (("none", "none", 0), ("all", "o", 0), ("part", "o", 1)):
+        tc = TrainingConfig(batch_size=2, gradient_accumulation_steps=4, warmup_steps=2, max_steps=10,
+                            defer_roles=roles, memory_first=True)
+        tr = DistributedTrainer(tiny(), tc)
+        tr.model.engine.defer_layers = layers
+        losses = [tr.train_step({"input_ids": d})["loss"] for d in data]
+        res[name] = (losses, tr.flat_params().clone())
+    for name in ("all", "part"):
+        assert res[name][0][0] == res["none"][0][0]
+        torch.testing.assert_close(res[name][1], res["none"][1], rtol=1e-5, atol=1e-6)
